@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ by running the REFERENCE itself.
+
+Runs only in the build container, where the reference tree is mounted read-only at
+/root/reference (it never travels to the GPU box; only the .npz/.json outputs do).
+
+* Imports the reference's ``model.FastSpeech2`` / ``model.modules.LengthRegulator`` with six
+  text-frontend modules stubbed (unidecode, inflect, quickspacer, g2pk, jamo, jamo.jamo:
+  ordinary ModuleNotFoundErrors) and synthetic side files
+  (stats/speakers/emotions.json) in a temp ``preprocessed_path``.
+* Fills the 240-key state_dict from the counter-based generator
+  ``fs2amd.synth_weights`` (seed 0), runs eval-mode fp32 forwards on CPU and writes
+  inputs + the 10-tuple outputs (+ LR source-index maps captured through the reference's
+  own LengthRegulator on an index-valued input).
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+"""
+import hashlib
+import json
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("FS2_REFERENCE", "/root/reference")
+sys.path.insert(0, os.path.join(REPO, "expressive-fastspeech2-mandarin_amd"))
+
+from fs2amd import config as C  # noqa: E402
+from fs2amd.data import synth_batch  # noqa: E402
+from fs2amd.synth_weights import fill_module  # noqa: E402
+
+
+def _stub(name):
+    mod = types.ModuleType(name)
+
+    def ga(attr):
+        if attr.startswith("__"):
+            raise AttributeError(attr)
+        return lambda *a, **k: None
+
+    mod.__getattr__ = ga
+    mod.__path__ = []
+    return mod
+
+
+def import_reference():
+    for m in ["unidecode", "inflect", "quickspacer", "g2pk", "jamo", "jamo.jamo"]:
+        sys.modules.setdefault(m, _stub(m))
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    from model import FastSpeech2  # noqa
+    from model.modules import LengthRegulator  # noqa
+    return FastSpeech2, LengthRegulator
+
+
+def t2n(v):
+    if v is None:
+        return None
+    if torch.is_tensor(v):
+        return v.detach().cpu().numpy()
+    return np.asarray(v)
+
+
+OUT_NAMES = ["mel", "postnet_mel", "p_pred", "e_pred", "log_d", "d_rounded", "src_masks", "mel_masks",
+             "src_lens_out", "mel_lens_out"]
+
+
+def index_map(LR, duration, max_len):
+    """Reference LengthRegulator applied to x[b,i,0] = i+1 -> source index per frame (-1 = pad)."""
+    B, L = duration.shape
+    idx = (torch.arange(L, dtype=torch.float64) + 1).view(1, L, 1).expand(B, L, 1).contiguous()
+    out, mel_len = LR()(idx, duration, max_len)
+    return (out[..., 0].round().to(torch.int64) - 1).numpy().astype(np.int32), mel_len.numpy()
+
+
+def run_case(model, LR, name, args, controls=(1.0, 1.0, 1.0), save_full=True):
+    p_c, e_c, d_c = controls
+    with torch.no_grad():
+        outs = model(**args, p_control=p_c, e_control=e_c, d_control=d_c)
+    rec = {}
+    for k, v in args.items():
+        if v is None:
+            continue
+        rec["in_" + k] = t2n(v)
+    rec["controls"] = np.array(controls, dtype=np.float64)
+    for k, v in zip(OUT_NAMES, outs):
+        if save_full:
+            rec["out_" + k] = t2n(v)
+    dur = outs[5] if args.get("d_targets") is None else args["d_targets"]
+    max_len = args.get("max_mel_len")
+    rec["lr_index_map"], rec["lr_mel_len"] = index_map(LR, dur, max_len)
+    if not save_full:
+        mel, post = outs[0].double(), outs[1].double()
+        mel_lens = outs[9]
+        valid = (torch.arange(mel.shape[1])[None, :] < mel_lens[:, None]).double()[..., None]
+        rec["ck_mel_valid_sum"] = (mel * valid).sum((1, 2)).numpy()
+        rec["ck_post_valid_sum"] = (post * valid).sum((1, 2)).numpy()
+        rec["ck_post_valid_abs"] = (post.abs() * valid).sum((1, 2)).numpy()
+        rec["ck_post_all_sum"] = post.sum((1, 2)).numpy()
+        rec["ck_post_sq"] = (post * post).sum((1, 2)).numpy()
+        for k in ("p_pred", "e_pred", "log_d", "d_rounded", "mel_lens_out", "src_masks", "mel_masks"):
+            rec["out_" + k] = t2n(outs[OUT_NAMES.index(k)])
+        rec["out_shape_mel"] = np.array(outs[0].shape)
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **rec)
+    print(f"{name}: {os.path.getsize(path) / 1e3:.1f} kB  mel {tuple(outs[0].shape)}")
+
+
+def lr_cases(LR):
+    g = torch.Generator().manual_seed(7)
+    cases = {}
+    x = torch.randn(3, 7, 5, generator=g)
+    cases["int"] = (x, torch.tensor([[2, 0, 3, 1, 0, 0, 0], [1, 1, 1, 1, 1, 1, 1], [0, 4, 0, 0, 2, 0, 0]]), None)
+    cases["float_trunc"] = (x, torch.tensor([[2.7, 0.4, -1.5, 3.0, 1.999, 0.0, 0.0],
+                                             [1.0, -0.0, 5.5, 0.0, 0.0, 0.0, 0.0],
+                                             [0.9, 0.9, 0.9, 0.9, 2.01, 0.0, 1.0]]), None)
+    cases["pad_longer"] = (x, cases["int"][1], 12)
+    cases["crop_shorter"] = (x, cases["int"][1], 4)
+    cases["zero_row"] = (x, torch.tensor([[0, 0, 0, 0, 0, 0, 0], [3, 0, 0, 0, 0, 0, 2], [1, 2, 3, 0, 0, 0, 0]]), None)
+    cases["nonzero_padding_slots"] = (x, torch.tensor([[1, 1, 1, 9, 9, 0, 0], [2, 2, 2, 2, 2, 2, 2], [0, 0, 0, 0, 0, 0, 7]]), 30)
+    rec = {}
+    for name, (xx, d, max_len) in cases.items():
+        out, mel_len = LR()(xx, d, max_len)
+        rec[f"{name}__x"] = xx.numpy()
+        rec[f"{name}__d"] = d.numpy()
+        rec[f"{name}__max_len"] = np.array(-1 if max_len is None else max_len)
+        rec[f"{name}__out"] = out.numpy()
+        rec[f"{name}__mel_len"] = mel_len.numpy()
+    np.savez_compressed(os.path.join(HERE, "lr_cases.npz"), **rec)
+    print("lr_cases:", list(cases))
+
+
+def main():
+    FastSpeech2, LR = import_reference()
+    torch.manual_seed(0)
+    tmp = tempfile.mkdtemp(prefix="fs2_golden_")
+    C.write_side_files(tmp)
+    pc, mc, _ = C.synthetic_configs(tmp)
+    model = FastSpeech2(pc, mc)
+    fill_module(model, seed=0)
+    model.eval()
+    torch.set_num_threads(8)
+
+    sd = model.state_dict()
+    manifest = {"reference": REF, "torch": torch.__version__, "weights_seed": 0, "n_keys": len(sd), "keys": {}}
+    for k, v in sd.items():
+        a = v.detach().double()
+        manifest["keys"][k] = {"shape": list(v.shape), "dtype": str(v.dtype).replace("torch.", ""),
+                               "sum": float(a.sum()), "sumsq": float((a * a).sum()),
+                               "sha256": hashlib.sha256(v.detach().cpu().contiguous().numpy().tobytes()).hexdigest()}
+    with open(os.path.join(HERE, "weights_manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=0, sort_keys=True)
+    print("manifest:", len(sd), "keys")
+
+    lr_cases(LR)
+    run_case(model, LR, "cfg1_teacher", synth_batch(1, 32, seed=1))
+    run_case(model, LR, "cfg1_free", synth_batch(1, 32, seed=1, teacher=False))
+    run_case(model, LR, "mini_teacher", synth_batch(4, 12, 40, seed=2))
+    run_case(model, LR, "mini_targets", synth_batch(4, 10, 36, seed=3, pe_targets=True), controls=(0.8, 1.2, 1.0))
+    run_case(model, LR, "mini_free_ctrl", synth_batch(4, 12, 40, seed=4, teacher=False), controls=(1.2, 0.7, 1.3))
+    run_case(model, LR, "mini_free_ctrl2", synth_batch(4, 12, 40, seed=5, teacher=False), controls=(0.8, 1.0, 0.8))
+    # padding classes: one utterance, alone and beside companions that are 1, 2 and 3 phonemes longer
+    base = synth_batch(3, 20, seed=6)
+    run_case(model, LR, "pad_base", {k: (v[:1] if torch.is_tensor(v) else v) for k, v in base.items()} | {
+        "max_src_len": int(base["src_lens"][0]), "max_mel_len": int(base["mel_lens"][0])})
+    run_case(model, LR, "cfg2_checksums", synth_batch(64, 64, seed=1), save_full=False)
+    # LR stress durations (cfg4 shape): index map only
+    b4 = synth_batch(256, 16, 160, seed=1)
+    im, ml = index_map(LR, b4["d_targets"], b4["max_mel_len"])
+    np.savez_compressed(os.path.join(HERE, "cfg4_lr_index.npz"), d=b4["d_targets"].numpy().astype(np.int16),
+                        index_map=im.astype(np.int16), mel_len=ml, max_mel_len=np.array(b4["max_mel_len"]))
+    print("cfg4 lr index:", im.shape)
+
+
+if __name__ == "__main__":
+    main()

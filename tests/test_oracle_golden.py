@@ -1,0 +1,56 @@
+"""Pin the oracle (oracle/fs2_oracle.py) against golden vectors captured from the reference."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from _common import GOLDEN_CASES, OUT_NAMES, configs, load_case, manifest, oracle_state_dict
+from oracle import fs2_oracle as O
+
+
+def test_weight_generator_matches_manifest():
+    """The counter-based generator regenerates exactly the weights the goldens were made with."""
+    sd = oracle_state_dict()
+    man = manifest()["keys"]
+    assert set(sd) == set(man) and len(sd) == 240
+    for k, meta in man.items():
+        v = sd[k]
+        assert list(v.shape) == meta["shape"], k
+        digest = hashlib.sha256(v.detach().cpu().contiguous().numpy().tobytes()).hexdigest()
+        assert digest == meta["sha256"], k
+
+
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_oracle_bit_exact_vs_reference(case):
+    torch.set_num_threads(8)
+    args, (p_c, e_c, d_c), outs, _ = load_case(case)
+    pc, mc, _ = configs()
+    got = O.forward(oracle_state_dict(), mc, pc, **args, p_control=p_c, e_control=e_c, d_control=d_c)
+    for name, g in zip(OUT_NAMES, got):
+        ref = outs[name]
+        g = g.numpy()
+        assert g.shape == ref.shape, name
+        assert g.dtype == ref.dtype, name
+        np.testing.assert_array_equal(g, ref, err_msg=f"{case}:{name}")
+
+
+@pytest.mark.parametrize("case", GOLDEN_CASES)
+def test_oracle_lr_index_map(case):
+    args, _, outs, z = load_case(case)
+    dur = torch.from_numpy(outs["d_rounded"]) if "d_targets" not in args else args["d_targets"]
+    im, ml = O.length_regulate_index_map(dur, args.get("max_mel_len"))
+    np.testing.assert_array_equal(im.numpy(), z["lr_index_map"])
+    np.testing.assert_array_equal(ml.numpy(), z["lr_mel_len"])
+
+
+def test_oracle_lr_cases(golden_dir):
+    z = np.load(f"{golden_dir}/lr_cases.npz")
+    names = sorted({k.split("__")[0] for k in z.files})
+    assert len(names) >= 6
+    for n in names:
+        ml = int(z[f"{n}__max_len"])
+        out, mel_len = O.length_regulate(torch.from_numpy(z[f"{n}__x"]), torch.from_numpy(z[f"{n}__d"]),
+                                         None if ml < 0 else ml)
+        np.testing.assert_array_equal(out.numpy(), z[f"{n}__out"], err_msg=n)
+        np.testing.assert_array_equal(mel_len.numpy(), z[f"{n}__mel_len"], err_msg=n)
