@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Mel-synthesis throughput bench (BASELINE.json metric: mel-frames/sec/GPU, batch-64 synth).
+
+One step = one FastSpeech2.forward (eval, bf16 perf mode) over one batch of 64 synthetic
+pinyin utterances of 64 phonemes (durations U{2..10} teacher-forced, so
+T_max ~ 430 frames; pitch/energy predicted), inputs resident in HBM, random-init weights of
+the ESD-Chinese-Singing-MFA architecture from the counter-based generator.
+
+Multi-GPU: one process per GPU (torchrun), each rank synthesises its OWN batch of 64
+(weak scaling; utterances are independent, no collective on the data path). The timed
+region is bracketed by a barrier + device sync on both sides; the max over ranks is the
+job time; value = all valid mel frames of all ranks / job time.
+
+Also reported:
+* roofline — the dominant kernel (the FFN Conv1d k=9 implicit GEMM of the decoder, ~76 % of
+  the FLOPs) timed with HIP events on the stream it launches on; achieved = algorithmic FLOPs
+  of one launch (valid frames x 2*256*9*1024) / its mean duration, vs 2.5 PF dense bf16.
+  ``traffic`` comes from the committed rocprofv3 PMC pass (profiles/) when present.
+* cpu_baseline — the oracle (CPU restatement of the reference, fp32 PyTorch) on a bounded
+  sample of the same workload, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "expressive-fastspeech2-mandarin_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HOP, SR = 256, 22050
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+F32_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--phonemes", type=int, default=64)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--graph", type=int, default=1, help="replay the forward as a captured HIP graph")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--kernel-reps", type=int, default=20)
+    return ap.parse_args()
+
+
+def build_model(device, dtype):
+    from fs2amd import config as C
+    from fs2amd.model import FastSpeech2
+    from fs2amd.synth_weights import fill_module
+
+    side = C.write_side_files(tempfile.mkdtemp(prefix="fs2_bench_"))
+    pc, mc, _ = C.synthetic_configs(side)
+    model = FastSpeech2(pc, mc)
+    fill_module(model, seed=0)
+    model = model.to(device).eval().set_precision(dtype)
+    return model, pc, mc
+
+
+def time_dominant_kernel(model, batch, device, reps):
+    """Mean duration of the decoder FFN conv-k9 GEMM (HIP events on its launch stream)."""
+    from fs2amd import _lib as L
+    from fs2amd import ops
+
+    P = model.packed(device)
+    lp = P.dec_layers[0]
+    B, T = batch["d_targets"].shape[0], int(batch["max_mel_len"])
+    g = torch.Generator(device="cpu").manual_seed(5)
+    h = torch.randn(B, T, lp.c1, generator=g).to(device=device, dtype=ops.torch_dtype(P.act_dtype))
+    out = torch.empty(B, T, lp.w1.shape[0], device=device, dtype=h.dtype)
+    run = lambda: ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=P.compute,
+                             epilogue=L.EPI_BIAS_RELU, out=out)
+    for _ in range(3):
+        run()
+    stream = torch.cuda.current_stream(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        run()
+    e1.record(stream)
+    e1.synchronize()
+    mean_s = e0.elapsed_time(e1) / 1e3 / reps
+    valid = int(batch["mel_lens"].sum())
+    flops = 2.0 * valid * lp.c1 * lp.k1 * lp.w1.shape[0]
+    return mean_s, flops
+
+
+def cpu_baseline(batch_cpu, pc, mc, budget_s=20.0):
+    """The oracle (reference restatement, fp32 PyTorch CPU) on a bounded sample."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle import fs2_oracle as O
+    from fs2amd.synth_weights import synth_state_dict
+    from fs2amd import config as C
+    from fs2amd.model import FastSpeech2
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    shapes = {k: tuple(v.shape) for k, v in FastSpeech2(pc, mc).state_dict().items()}
+    sd = O.build_state_dict(mc, pc, C.SYNTH_STATS, synth_state_dict(shapes, seed=0))
+    n = 8  # utterances per sample forward (a slice of the same batch)
+    sub = {k: (v[:n] if torch.is_tensor(v) and v.dim() >= 1 and v.shape[0] == batch_cpu["texts"].shape[0] else v)
+           for k, v in batch_cpu.items()}
+    sub["max_src_len"] = int(sub["src_lens"].max())
+    sub["max_mel_len"] = int(sub["mel_lens"].max())
+    sub["texts"] = sub["texts"][:, :sub["max_src_len"]]
+    sub["d_targets"] = sub["d_targets"][:, :sub["max_src_len"]]
+    frames = int(sub["mel_lens"].sum())
+    with torch.no_grad():
+        O.forward(sd, mc, pc, **sub)  # warm-up
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            O.forward(sd, mc, pc, **sub)
+            reps += 1
+            if time.perf_counter() - t0 > budget_s or reps >= 50:
+                break
+        dt = time.perf_counter() - t0
+    return {"value": round(frames * reps / dt, 1), "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "sample": f"oracle fp32 forward, {n} of the 64 utterances ({frames} frames) x {reps} reps, "
+                      f"{dt:.1f} s, torch.set_num_threads({threads})"}
+
+
+def load_traffic():
+    path = os.path.join(REPO, "profiles", "conv9_traffic.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    device = torch.device(f"cuda:{local}")
+
+    from fs2amd.data import synth_batch, to_device
+
+    model, pc, mc = build_model(device, args.dtype)
+    batch_cpu = synth_batch(args.batch, args.phonemes, seed=1 + rank)
+    batch = to_device(batch_cpu, device)
+    frames = int(batch_cpu["mel_lens"].sum())
+
+    def step():
+        with torch.no_grad():
+            return model(**batch)
+
+    for _ in range(max(1, args.warmup)):
+        out = step()
+    torch.cuda.synchronize(device)
+    graph = None
+    if args.graph:
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                step()
+        torch.cuda.current_stream(device).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = step()
+        graph.replay()
+        torch.cuda.synchronize(device)
+
+    run = graph.replay if graph is not None else step
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    tot_frames = frames
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        f = torch.tensor([frames], device=device, dtype=torch.float64)
+        dist.all_reduce(f, op=dist.ReduceOp.SUM)
+        tot_frames = int(f.item())
+
+    kernel_s, kernel_flops = time_dominant_kernel(model, batch_cpu, device, args.kernel_reps)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = tot_frames * args.steps / elapsed
+    peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
+    achieved = kernel_flops / kernel_s / 1e12
+    rec = {
+        "metric": "mel-frames/sec/GPU (batch-64 synth) at 1/2/4/8 MI355X; RTF",
+        "value": round(value, 1),
+        "unit": "mel-frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (seeded pinyin ids U{64..107}, durations U{2..10} teacher-forced, pitch/energy "
+                "predicted; counter-generated random-init weights)",
+        "config": {"workload": f"cfg2: batch={args.batch} x {args.phonemes} phonemes per GPU, ESD-Chinese-Singing-MFA "
+                               f"model.yaml, FastSpeech2.forward eval {args.dtype}",
+                   "global_batch": args.batch * world, "seq_len": args.phonemes,
+                   "mel_frames_per_gpu_batch": frames, "T_max": int(batch_cpu["max_mel_len"]),
+                   "parallelism": f"dp{world} (independent shards, no collective)",
+                   "hip_graph": bool(args.graph)},
+        "rtf": round((elapsed / args.steps) / (tot_frames / world * HOP / SR), 7),
+        "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel<bf16,2,2> (decoder FFN Conv1d k=9, 256->1024)",
+                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": load_traffic(),
+                     "kernel_ms": round(kernel_s * 1e3, 4), "flops_per_launch": kernel_flops},
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(batch_cpu, pc, mc)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,248 @@
+// Self-attention with a key-padding mask for the FFT blocks, CDNA4 MFMA (bf16 or exact f32).
+//
+// Reference: transformer/Modules.py:14-25 (bmm(q, k^T) / temperature, masked_fill(mask, -inf),
+// softmax(dim=2), bmm(attn, v)) with the head split/merge of transformer/SubLayers.py:36-52.
+// The reference materialises the [H*B, T, T] score tensor (94.7 MB fp32 per decoder layer at
+// B=64, T=430); here one workgroup owns 64 query rows of one (sequence, head), keeps its Q
+// fragments in registers, streams 64-key K/V tiles through LDS only up to the sequence's key
+// length (padded keys beyond it are never touched) and keeps an online softmax in f32.
+//
+// Per 64-key tile, wave w (16 query rows):
+//   S = Q K^T      4 key blocks x (128/32) bf16 MFMAs (or 128/16 x 4 f32 MFMAs)
+//   online max / sum across the 16 lanes that share a row (xor shuffles), O *= exp2(m_old-m_new)
+//   P -> LDS (wave-private rows), read back as A fragments
+//   O += P V       V is staged TRANSPOSED in LDS (Vt[d][key]) so B fragments are 16-byte reads.
+// LDS rows are XOR-swizzled by row so every fragment read is bank-conflict free.
+#include <type_traits>
+
+#include "fs2_common.h"
+
+namespace {
+
+constexpr int DK = 128;
+constexpr int QT = 64;  // query rows per workgroup
+constexpr int KT = 64;  // keys per tile
+
+template <int CT>
+struct ATraits;
+template <>
+struct ATraits<FS2_BF16> {
+  using T = bf16;
+  static constexpr int CEp = 8;  // elements per 16-byte chunk
+};
+template <>
+struct ATraits<FS2_F32> {
+  using T = float;
+  static constexpr int CEp = 4;
+};
+
+template <int CT>
+__global__ __launch_bounds__(256, 2) void attn_kernel(const typename ATraits<CT>::T *__restrict__ qkv, int64_t qs,
+                                                      const int64_t *__restrict__ lens, int T, int H, float scale_log2,
+                                                      typename ATraits<CT>::T *__restrict__ out, int64_t os) {
+  using TE = typename ATraits<CT>::T;
+  constexpr int ES = sizeof(TE);
+  constexpr int CEp = ATraits<CT>::CEp;
+  constexpr int KROW = DK * ES;          // bytes per K row (16 or 32 chunks)
+  constexpr int VROW = KT * ES;          // bytes per Vt / P row (8 or 16 chunks)
+  constexpr int VSW = VROW / 16 - 1;     // swizzle mask for Vt / P rows (7 or 15)
+  __shared__ __attribute__((aligned(16))) char Ks[KT * KROW];
+  __shared__ __attribute__((aligned(16))) char Vts[DK * VROW];
+  __shared__ __attribute__((aligned(16))) char Ps[4 * 16 * VROW];
+
+  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int64_t len64 = lens[b];
+  const int len = (int)(len64 < 0 ? 0 : (len64 > T ? T : len64));
+  const TE *base = qkv + (int64_t)b * T * qs;
+
+  auto koff = [](int row, int chunk) { return row * KROW + ((chunk ^ (row & 15)) << 4); };
+  auto voff = [](int row, int chunk) { return row * VROW + ((chunk ^ (row & VSW)) << 4); };
+
+  // ---- Q fragments (registers, whole head dim) -----------------------------------------------
+  const int qrow = q0 + 16 * w + (lane & 15);
+  const bool q_ok = qrow < T;
+  constexpr int QSTEPS = (CT == FS2_BF16) ? DK / 32 : DK / 16;
+  using QFrag = typename std::conditional<CT == FS2_BF16, bf16x8, f32x4>::type;
+  QFrag qf[QSTEPS];
+#pragma unroll
+  for (int s = 0; s < QSTEPS; ++s) {
+    const int k = (s * 4 + (lane >> 4)) * CEp;
+    if (q_ok)
+      qf[s] = *reinterpret_cast<const QFrag *>(base + (int64_t)qrow * qs + h * DK + k);
+    else
+      qf[s] = QFrag{};
+  }
+
+  f32x4 oacc[DK / 16];
+#pragma unroll
+  for (int i = 0; i < DK / 16; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[4], l_run[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    m_run[j] = -INFINITY;
+    l_run[j] = 0.f;
+  }
+
+  const int ntiles = (len + KT - 1) / KT;
+  char *Pw = Ps + w * 16 * VROW;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int k0 = kt * KT;
+    __syncthreads();  // previous tile's K / Vt reads are done
+    // K tile: KT rows x KROW bytes
+    constexpr int KCH = KT * KROW / 16;
+    for (int e = tid; e < KCH; e += 256) {
+      const int r = e / (KROW / 16), c = e % (KROW / 16);
+      const int key = k0 + r;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (key < T) v = *reinterpret_cast<const uint4 *>(base + (int64_t)key * qs + (H + h) * DK + c * CEp);
+      *reinterpret_cast<uint4 *>(Ks + koff(r, c)) = v;
+    }
+    // V tile transposed: unit = (key pair, 16-byte d chunk)
+    constexpr int VUNITS = (KT / 2) * (DK / CEp);
+    for (int e = tid; e < VUNITS; e += 256) {
+      const int kp = e / (DK / CEp), dc = e % (DK / CEp);
+      const int key = k0 + 2 * kp;
+      TE v0[CEp], v1[CEp];
+      uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
+      const TE *vp = base + (2 * H + h) * DK + dc * CEp;
+      if (key < T) r0 = *reinterpret_cast<const uint4 *>(vp + (int64_t)key * qs);
+      if (key + 1 < T) r1 = *reinterpret_cast<const uint4 *>(vp + (int64_t)(key + 1) * qs);
+      __builtin_memcpy(v0, &r0, 16);
+      __builtin_memcpy(v1, &r1, 16);
+      const int kk = 2 * kp;  // key within tile (even)
+#pragma unroll
+      for (int q = 0; q < CEp; ++q) {
+        const int d = dc * CEp + q;
+        char *dst = Vts + voff(d, kk / CEp) + (kk % CEp) * ES;
+        if constexpr (CT == FS2_BF16) {
+          bf16 pair[2] = {v0[q], v1[q]};
+          uint32_t u;
+          __builtin_memcpy(&u, pair, 4);
+          *reinterpret_cast<uint32_t *>(dst) = u;
+        } else {
+          *reinterpret_cast<float2 *>(dst) = make_float2(v0[q], v1[q]);
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- S = Q K^T --------------------------------------------------------------------------
+    f32x4 sacc[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) sacc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < QSTEPS; ++s) {
+      const int ch = s * 4 + (lane >> 4);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const QFrag kf = *reinterpret_cast<const QFrag *>(Ks + koff(ni * 16 + (lane & 15), ch));
+        if constexpr (CT == FS2_BF16) {
+          sacc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[s], kf, sacc[ni], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sacc[ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(qf[s][j], kf[j], sacc[ni], 0, 0, 0);
+        }
+      }
+    }
+
+    // ---- online softmax (rows 4*(lane>>4)+j of the wave's 16, keys ni*16 + (lane&15)) -------
+    float alpha[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int key = k0 + ni * 16 + (lane & 15);
+        float sv = sacc[ni][j] * scale_log2;
+        sv = key < len ? sv : -INFINITY;
+        sacc[ni][j] = sv;
+        mx = fmaxf(mx, sv);
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+      const float m_new = fmaxf(m_run[j], mx);
+      alpha[j] = exp2f(m_run[j] - m_new);
+      m_run[j] = m_new;
+      float sum = 0.f;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const float p = exp2f(sacc[ni][j] - m_new);
+        sacc[ni][j] = p;
+        sum += p;
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
+      l_run[j] = l_run[j] * alpha[j] + sum;
+    }
+#pragma unroll
+    for (int ni = 0; ni < DK / 16; ++ni)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) oacc[ni][j] *= alpha[j];
+
+    // ---- P -> LDS (wave-private 16 x 64) ---------------------------------------------------
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 4 * (lane >> 4) + j;
+        const int key = ni * 16 + (lane & 15);
+        *reinterpret_cast<TE *>(Pw + voff(row, key / CEp) + (key % CEp) * ES) = (TE)sacc[ni][j];
+      }
+    __syncthreads();
+
+    // ---- O += P V -----------------------------------------------------------------------------
+    constexpr int PSTEPS = (CT == FS2_BF16) ? KT / 32 : KT / 16;
+#pragma unroll
+    for (int s = 0; s < PSTEPS; ++s) {
+      const int ch = s * 4 + (lane >> 4);
+      const QFrag pa = *reinterpret_cast<const QFrag *>(Pw + voff(lane & 15, ch));
+#pragma unroll
+      for (int ni = 0; ni < DK / 16; ++ni) {
+        const QFrag vf = *reinterpret_cast<const QFrag *>(Vts + voff(ni * 16 + (lane & 15), ch));
+        if constexpr (CT == FS2_BF16) {
+          oacc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vf, oacc[ni], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) oacc[ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[j], vf[j], oacc[ni], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- normalise and store ---------------------------------------------------------------------
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = q0 + 16 * w + 4 * (lane >> 4) + j;
+    if (q >= T) continue;
+    const float inv = l_run[j] > 0.f ? 1.0f / l_run[j] : 0.f;
+    TE *orow = out + ((int64_t)b * T + q) * os + h * DK + (lane & 15);
+#pragma unroll
+    for (int ni = 0; ni < DK / 16; ++ni) orow[ni * 16] = (TE)(oacc[ni][j] * inv);
+  }
+}
+
+}  // namespace
+
+extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
+                             int H, int dk, float temperature, void *out, int64_t out_row_stride, fs2_stream_t stream) {
+  if (qkv == nullptr || key_lens == nullptr || out == nullptr) return FS2_EINVAL;
+  if (dk != DK || H <= 0 || B < 0 || T < 0 || !(temperature > 0.f)) return FS2_EINVAL;
+  if (qkv_row_stride < 3LL * H * dk || out_row_stride < (int64_t)H * dk) return FS2_EINVAL;
+  const int ce = dtype == FS2_BF16 ? 8 : 4;
+  if ((qkv_row_stride % ce) != 0) return FS2_EINVAL;
+  if (B == 0 || T == 0) return FS2_OK;
+  const float scale_log2 = 1.4426950408889634f / temperature;
+  dim3 grid((T + QT - 1) / QT, H, B);
+  hipStream_t s = as_stream(stream);
+  if (dtype == FS2_BF16)
+    hipLaunchKernelGGL(attn_kernel<FS2_BF16>, grid, dim3(256), 0, s, reinterpret_cast<const bf16 *>(qkv),
+                       qkv_row_stride, key_lens, T, H, scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride);
+  else if (dtype == FS2_F32)
+    hipLaunchKernelGGL(attn_kernel<FS2_F32>, grid, dim3(256), 0, s, reinterpret_cast<const float *>(qkv),
+                       qkv_row_stride, key_lens, T, H, scale_log2, reinterpret_cast<float *>(out), out_row_stride);
+  else
+    return FS2_EUNSUPPORTED;
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}

@@ -1,0 +1,178 @@
+// LengthRegulator on CDNA4: per-sequence duration scan + per-frame gather (HBM-bound).
+//
+// Reference: model/modules.py:161-194 (LengthRegulator.LR / expand / forward) and the pad()
+// it calls, utils/tools.py:360-378. The reference walks B*L_max phonemes in Python, calls
+// .item() on each duration (one device->host sync each on a GPU), expands with
+// vec.expand(max(int(d), 0)), concatenates and zero-pads/crops to max_len.
+//
+// Here: launch 1 (one workgroup per sequence) turns durations into frame counts
+// max(trunc(d), 0), wavefront-scans them into an inclusive prefix sum `cum` and writes
+// mel_len (the uncropped total). Launch 2 (B x ceil(T_out/32) workgroups) binary-searches
+// each output frame's source phoneme in `cum` (first i with cum[i] > t) and streams the
+// D-wide row with 16-byte vector loads/stores; frames at or past min(mel_len, T_out) are
+// zero. An optional f32 position-encoding row is added on the way out (Decoder input,
+// transformer/Models.py:158-160) so the expanded tensor is written to HBM exactly once.
+#include "fs2_common.h"
+
+namespace {
+
+constexpr int kScanThreads = 256;
+constexpr int kRowsPerBlock = 32;
+
+__device__ __forceinline__ int64_t frames_of(const void *dur, int kind, float d_control, int64_t idx,
+                                             float *d_rounded) {
+  if (kind == FS2_DUR_I64) {
+    int64_t d = reinterpret_cast<const int64_t *>(dur)[idx];
+    return d > 0 ? d : 0;
+  }
+  float v = reinterpret_cast<const float *>(dur)[idx];
+  if (kind == FS2_DUR_LOGPRED) {
+    // torch.clamp(torch.round(torch.exp(log_d) - 1) * d_control, min=0)  (modules.py:132-135)
+    float r = rintf(expf(v) - 1.0f) * d_control;
+    r = r < 0.0f ? 0.0f : r;
+    if (d_rounded) d_rounded[idx] = r;
+    v = r;
+  }
+  // int(expand_size) truncates toward zero; max(., 0)                 (modules.py:186-187)
+  if (!(v > 0.0f)) return 0;
+  if (v >= 9.2e18f) return INT64_MAX / 4;
+  return (int64_t)v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void lr_durations_kernel(const void *dur, int kind, float d_control, int L,
+                                                                    int32_t *cum, int64_t *mel_len, float *d_rounded) {
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int per = (L + kScanThreads - 1) / kScanThreads;
+  const int i0 = min(tid * per, L), i1 = min(i0 + per, L);
+  const int64_t base = (int64_t)b * L;
+
+  int64_t local = 0;
+  for (int i = i0; i < i1; ++i) local += frames_of(dur, kind, d_control, base + i, nullptr);
+
+  // inclusive wave scan, then across the 4 waves through LDS
+  int64_t incl = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  __shared__ int64_t wave_tot[kScanThreads / 64];
+  if (lane == 63) wave_tot[wid] = incl;
+  __syncthreads();
+  int64_t prefix = 0;
+  for (int w = 0; w < wid; ++w) prefix += wave_tot[w];
+  int64_t run = prefix + incl - local;  // exclusive prefix of this thread's span
+
+  for (int i = i0; i < i1; ++i) {
+    run += frames_of(dur, kind, d_control, base + i, d_rounded);
+    cum[base + i] = (int32_t)(run < 0x7fffffff ? run : 0x7fffffff);
+  }
+  if (tid == kScanThreads - 1) {
+    int64_t total = 0;
+    for (int w = 0; w < kScanThreads / 64; ++w) total += wave_tot[w];
+    mel_len[b] = total;
+  }
+}
+
+template <typename TX, typename TO>
+__global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x, const int32_t *__restrict__ cum,
+                                                        const int64_t *__restrict__ mel_len, int L, int D, int T_out,
+                                                        const float *__restrict__ pe, TO *__restrict__ out,
+                                                        int32_t *__restrict__ index_map) {
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * kRowsPerBlock;
+  const int tid = threadIdx.x;
+  __shared__ int src[kRowsPerBlock];
+  const int64_t ml = mel_len[b];
+  const int lim = (int)(ml < (int64_t)T_out ? ml : (int64_t)T_out);
+  const int32_t *c = cum + (int64_t)b * L;
+  if (tid < kRowsPerBlock) {
+    const int t = t0 + tid;
+    int s = -1;
+    if (t < lim) {
+      int lo = 0, hi = L - 1;  // first i with cum[i] > t (exists because t < mel_len)
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (c[mid] > t) hi = mid; else lo = mid + 1;
+      }
+      s = lo;
+    }
+    src[tid] = s;
+    if (index_map != nullptr && t < T_out) index_map[(int64_t)b * T_out + t] = s;
+  }
+  __syncthreads();
+  const int vpr = D >> 3;
+  const int rows = min(kRowsPerBlock, T_out - t0);
+  for (int e = tid; e < rows * vpr; e += 256) {
+    const int r = e / vpr;
+    const int col = (e - r * vpr) << 3;
+    const int t = t0 + r;
+    const int s = src[r];
+    float v[8];
+    if (s >= 0) {
+      load8(x + ((int64_t)b * L + s) * D + col, v);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = 0.0f;
+    }
+    if (pe != nullptr) {
+      float p[8];
+      load8(pe + (int64_t)t * D + col, p);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += p[q];
+    }
+    store8(out + ((int64_t)b * T_out + t) * D + col, v);
+  }
+}
+
+template <typename TX, typename TO>
+void launch_expand(const void *x, const int32_t *cum, const int64_t *mel_len, int B, int L, int D, int T_out,
+                   const float *pe, void *out, int32_t *index_map, hipStream_t s) {
+  dim3 grid((T_out + kRowsPerBlock - 1) / kRowsPerBlock, B);
+  hipLaunchKernelGGL((lr_expand_kernel<TX, TO>), grid, dim3(256), 0, s, reinterpret_cast<const TX *>(x), cum, mel_len,
+                     L, D, T_out, pe, reinterpret_cast<TO *>(out), index_map);
+}
+
+}  // namespace
+
+extern "C" int fs2_lr_durations(const void *dur, int dur_kind, float d_control, int B, int L, int32_t *cum,
+                                int64_t *mel_len, float *d_rounded, fs2_stream_t stream) {
+  if (dur == nullptr || cum == nullptr || mel_len == nullptr || B < 0 || L <= 0) return FS2_EINVAL;
+  if (dur_kind < FS2_DUR_I64 || dur_kind > FS2_DUR_LOGPRED) return FS2_EINVAL;
+  if (B == 0) return FS2_OK;
+  hipLaunchKernelGGL(lr_durations_kernel, dim3(B), dim3(kScanThreads), 0, as_stream(stream), dur, dur_kind, d_control,
+                     L, cum, mel_len, d_rounded);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_lr_expand(const void *x, int x_dtype, const int32_t *cum, const int64_t *mel_len, int B, int L,
+                             int D, int T_out, const float *pe, void *out, int out_dtype, int32_t *index_map,
+                             fs2_stream_t stream) {
+  if (x == nullptr || cum == nullptr || mel_len == nullptr || out == nullptr) return FS2_EINVAL;
+  if (B < 0 || L <= 0 || D <= 0 || (D & 7) != 0 || T_out < 0) return FS2_EINVAL;
+  if (B == 0 || T_out == 0) return FS2_OK;
+  hipStream_t s = as_stream(stream);
+  if (x_dtype == FS2_F32 && out_dtype == FS2_F32)
+    launch_expand<float, float>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, s);
+  else if (x_dtype == FS2_BF16 && out_dtype == FS2_BF16)
+    launch_expand<bf16, bf16>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, s);
+  else if (x_dtype == FS2_F32 && out_dtype == FS2_BF16)
+    launch_expand<float, bf16>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, s);
+  else if (x_dtype == FS2_BF16 && out_dtype == FS2_F32)
+    launch_expand<bf16, float>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, s);
+  else
+    return FS2_EUNSUPPORTED;
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_length_regulate(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control, int B,
+                                   int L, int D, int T_out, const float *pe, void *out, int out_dtype, int32_t *cum,
+                                   int64_t *mel_len, float *d_rounded, int32_t *index_map, fs2_stream_t stream) {
+  int rc = fs2_lr_durations(dur, dur_kind, d_control, B, L, cum, mel_len, d_rounded, stream);
+  if (rc != FS2_OK) return rc;
+  return fs2_lr_expand(x, x_dtype, cum, mel_len, B, L, D, T_out, pe, out, out_dtype, index_map, stream);
+}

@@ -1,0 +1,176 @@
+// Small bandwidth kernels around the GEMMs: encoder embedding + position encoding, the
+// per-utterance speaker/emotion conditioning vectors, and the pitch/energy bucketize +
+// embedding add of the VarianceAdaptor.
+#include "fs2_common.h"
+
+namespace {
+
+// out[b,l,:] = table[tok, :] + pe[l, :]          (transformer/Models.py:82-91)
+template <typename TO>
+__global__ __launch_bounds__(256) void embed_pe_kernel(const int64_t *__restrict__ tokens, const float *__restrict__ table,
+                                                       int vocab, const float *__restrict__ pe, int L, int D,
+                                                       int64_t rows, TO *__restrict__ out) {
+  const int vpr = D >> 3;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= rows * vpr) return;
+  const int64_t row = e / vpr;
+  const int col = (int)(e - row * vpr) << 3;
+  const int l = (int)(row % L);
+  int64_t tok = tokens[row];
+  tok = tok < 0 ? 0 : (tok >= vocab ? vocab - 1 : tok);
+  float v[8], p[8];
+  load8(table + tok * D + col, v);
+  load8(pe + (int64_t)l * D + col, p);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] += p[q];
+  store8(out + row * D + col, v);
+}
+
+__device__ __forceinline__ int64_t clampi(int64_t v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
+
+// One workgroup per utterance, one thread per output channel.   (model/fastspeech2.py:101-110)
+__global__ void cond_kernel(const int64_t *speakers, const float *spk_table, int n_spk, const int64_t *emotions,
+                            const float *emo_table, int n_emo, int d_emo, const int64_t *arousals,
+                            const float *aro_table, int n_aro, int d_aro, const int64_t *valences,
+                            const float *val_table, int n_val, int d_val, const float *lin_w, const float *lin_b,
+                            int D, float *spk_out, float *emo_out) {
+  extern __shared__ float cat[];
+  const int b = blockIdx.x;
+  const int dc = d_emo + d_aro + d_val;
+  if (emo_table != nullptr) {
+    const int64_t e = clampi(emotions[b], n_emo), a = clampi(arousals[b], n_aro), v = clampi(valences[b], n_val);
+    for (int k = threadIdx.x; k < dc; k += blockDim.x) {
+      float x;
+      if (k < d_emo)
+        x = emo_table[e * d_emo + k];
+      else if (k < d_emo + d_aro)
+        x = aro_table[a * d_aro + (k - d_emo)];
+      else
+        x = val_table[v * d_val + (k - d_emo - d_aro)];
+      cat[k] = x;
+    }
+  }
+  __syncthreads();
+  for (int n = threadIdx.x; n < D; n += blockDim.x) {
+    if (spk_table != nullptr) spk_out[(int64_t)b * D + n] = spk_table[clampi(speakers[b], n_spk) * D + n];
+    if (emo_table != nullptr) {
+      float s = 0.f;
+      const float *wr = lin_w + (int64_t)n * dc;
+      for (int k = 0; k < dc; ++k) s = fmaf(wr[k], cat[k], s);
+      s += lin_b[n];
+      emo_out[(int64_t)b * D + n] = fmaxf(s, 0.f);
+    }
+  }
+}
+
+// 32 lanes per row (inside one wave, so the read of pred[m] by every lane precedes lane 0's
+// write-back), 8 channels per lane per step.                   (model/modules.py:80-100)
+template <typename TX>
+__global__ __launch_bounds__(256) void variance_embed_kernel(TX *__restrict__ x, float *__restrict__ pred,
+                                                             const float *__restrict__ target, float control,
+                                                             const float *__restrict__ bins, int nb,
+                                                             const float *__restrict__ table, int M, int D) {
+  const int m = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int sub = threadIdx.x & 31;
+  if (m >= M) return;
+  float v;
+  if (target != nullptr) {
+    v = target[m];
+  } else {
+    v = pred[m] * control;
+  }
+  // torch.bucketize(v, bins, right=False): number of boundaries strictly below v
+  int lo = 0, hi = nb;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (bins[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  if (target == nullptr && sub == 0) pred[m] = v;
+  const float *trow = table + (int64_t)lo * D;
+  TX *xrow = x + (int64_t)m * D;
+  for (int col = sub * 8; col < D; col += 256) {
+    float a[8], t[8];
+    load8(xrow + col, a);
+    load8(trow + col, t);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a[q] += t[q];
+    store8(xrow + col, a);
+  }
+}
+
+}  // namespace
+
+extern "C" int fs2_embed_pe(const int64_t *tokens, const float *table, int vocab, const float *pe, int B, int L, int D,
+                            void *out, int out_dtype, fs2_stream_t stream) {
+  if (tokens == nullptr || table == nullptr || pe == nullptr || out == nullptr) return FS2_EINVAL;
+  if (B < 0 || L < 0 || D <= 0 || (D & 7) || vocab <= 0) return FS2_EINVAL;
+  const int64_t rows = (int64_t)B * L;
+  if (rows == 0) return FS2_OK;
+  const int64_t work = rows * (D >> 3);
+  dim3 grid((unsigned)((work + 255) / 256));
+  hipStream_t s = as_stream(stream);
+  if (out_dtype == FS2_F32)
+    hipLaunchKernelGGL(embed_pe_kernel<float>, grid, dim3(256), 0, s, tokens, table, vocab, pe, L, D, rows,
+                       reinterpret_cast<float *>(out));
+  else if (out_dtype == FS2_BF16)
+    hipLaunchKernelGGL(embed_pe_kernel<bf16>, grid, dim3(256), 0, s, tokens, table, vocab, pe, L, D, rows,
+                       reinterpret_cast<bf16 *>(out));
+  else
+    return FS2_EUNSUPPORTED;
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_cond_vectors(const int64_t *speakers, const float *speaker_table, int n_speaker,
+                                const int64_t *emotions, const float *emo_table, int n_emo, int d_emo,
+                                const int64_t *arousals, const float *aro_table, int n_aro, int d_aro,
+                                const int64_t *valences, const float *val_table, int n_val, int d_val,
+                                const float *lin_w, const float *lin_b, int B, int D, float *spk_out, float *emo_out,
+                                fs2_stream_t stream) {
+  if (B < 0 || D <= 0) return FS2_EINVAL;
+  if (speaker_table != nullptr && (speakers == nullptr || spk_out == nullptr || n_speaker <= 0)) return FS2_EINVAL;
+  if (emo_table != nullptr &&
+      (emotions == nullptr || arousals == nullptr || valences == nullptr || aro_table == nullptr ||
+       val_table == nullptr || lin_w == nullptr || lin_b == nullptr || emo_out == nullptr || n_emo <= 0 ||
+       n_aro <= 0 || n_val <= 0))
+    return FS2_EINVAL;
+  if (B == 0 || (speaker_table == nullptr && emo_table == nullptr)) return FS2_OK;
+  const int dc = emo_table != nullptr ? d_emo + d_aro + d_val : 0;
+  hipLaunchKernelGGL(cond_kernel, dim3(B), dim3(256), (size_t)dc * sizeof(float), as_stream(stream), speakers,
+                     speaker_table, n_speaker, emotions, emo_table, n_emo, d_emo, arousals, aro_table, n_aro, d_aro,
+                     valences, val_table, n_val, d_val, lin_w, lin_b, D, spk_out, emo_out);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_variance_embed(void *x, int x_dtype, float *pred, const float *target, float control,
+                                  const float *bins, int n_bins, const float *table, int M, int D,
+                                  fs2_stream_t stream) {
+  if (x == nullptr || pred == nullptr || bins == nullptr || table == nullptr) return FS2_EINVAL;
+  if (M < 0 || D <= 0 || (D & 7) || n_bins < 2) return FS2_EINVAL;
+  if (M == 0) return FS2_OK;
+  dim3 grid((M + 7) / 8);
+  hipStream_t s = as_stream(stream);
+  if (x_dtype == FS2_F32)
+    hipLaunchKernelGGL(variance_embed_kernel<float>, grid, dim3(256), 0, s, reinterpret_cast<float *>(x), pred, target,
+                       control, bins, n_bins - 1, table, M, D);
+  else if (x_dtype == FS2_BF16)
+    hipLaunchKernelGGL(variance_embed_kernel<bf16>, grid, dim3(256), 0, s, reinterpret_cast<bf16 *>(x), pred, target,
+                       control, bins, n_bins - 1, table, M, D);
+  else
+    return FS2_EUNSUPPORTED;
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" const char *fs2_version(void) { return "fs2hip 0.1.0 (gfx950)"; }
+
+extern "C" const char *fs2_status_string(int status) {
+  switch (status) {
+    case FS2_OK: return "ok";
+    case FS2_EINVAL: return "invalid argument";
+    case FS2_ELAUNCH: return "kernel launch failed";
+    case FS2_EUNSUPPORTED: return "unsupported dtype/configuration";
+    default: return "unknown status";
+  }
+}

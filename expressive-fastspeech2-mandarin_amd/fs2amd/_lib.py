@@ -1,0 +1,99 @@
+"""ctypes binding of libfs2hip.so (the C ABI declared in include/fs2hip.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950)
+into ``fs2amd/_lib/libfs2hip.so``; ``FS2_LIB`` overrides the path. There is no CPU fallback:
+if the library is missing the import of :mod:`fs2amd.ops` raises.
+
+``import torch`` must happen before the library is loaded so that its libamdhip64.so.7
+resolves (by SONAME) to the HIP runtime torch already mapped: one runtime per process.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime first)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DEFAULT_LIB = os.path.join(HERE, "_lib", "libfs2hip.so")
+
+FS2_F32, FS2_BF16 = 0, 1
+FS2_OK, FS2_EINVAL, FS2_ELAUNCH, FS2_EUNSUPPORTED = 0, 1, 2, 3
+(EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_TANH, EPI_BIAS_RES, EPI_RES_LN, EPI_RELU_LN, EPI_RELU_LN_DOT) = range(7)
+DUR_I64, DUR_F32, DUR_LOGPRED = 0, 1, 2
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+
+
+class ConvDesc(ctypes.Structure):
+    """Mirror of ``fs2_conv_desc`` (include/fs2hip.h)."""
+
+    _fields_ = [
+        ("x", _p), ("x_dtype", _i), ("x_row_stride", _i64),
+        ("w", _p), ("bias", _p),
+        ("B", _i), ("T", _i), ("Cin", _i), ("Cin_pad", _i), ("N", _i), ("KS", _i), ("pad", _i),
+        ("compute", _i), ("epilogue", _i),
+        ("residual", _p), ("res_dtype", _i), ("res_row_stride", _i64),
+        ("ln_gamma", _p), ("ln_beta", _p), ("ln_eps", _f),
+        ("lens", _p), ("addvec1", _p), ("addvec2", _p),
+        ("dot_w", _p), ("dot_b", _f),
+        ("out", _p), ("out_dtype", _i), ("out_row_stride", _i64),
+    ]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "fs2_version": (ctypes.c_char_p, []),
+    "fs2_status_string": (ctypes.c_char_p, [_i]),
+    "fs2_conv_cin_pad": (_i, [_i, _i]),
+    "fs2_conv1d": (_i, [ctypes.POINTER(ConvDesc), _p]),
+    "fs2_attention": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p]),
+    "fs2_embed_pe": (_i, [_p, _p, _i, _p, _i, _i, _i, _p, _i, _p]),
+    "fs2_cond_vectors": (_i, [_p, _p, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p,
+                              _p]),
+    "fs2_variance_embed": (_i, [_p, _i, _p, _p, _f, _p, _i, _p, _i, _i, _p]),
+    "fs2_lr_durations": (_i, [_p, _i, _f, _i, _i, _p, _p, _p, _p]),
+    "fs2_lr_expand": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _p, _p, _i, _p, _p]),
+    "fs2_length_regulate": (_i, [_p, _i, _p, _i, _f, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p, _p, _p]),
+}
+
+
+def header_symbols(header_path):
+    """Every ``fs2_*`` function declared in include/fs2hip.h (for the export test)."""
+    import re
+
+    text = open(header_path).read()
+    return sorted(set(re.findall(r"\b(fs2_[a-z0-9_]+)\s*\(", text)) - {"fs2_conv_desc"})
+
+
+_LIB = None
+
+
+def lib_path():
+    return os.environ.get("FS2_LIB", DEFAULT_LIB)
+
+
+def load():
+    """Load (once) and return the ctypes library; raises if it was not built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"fs2amd: HIP library not found at {path}. Build it with `python -c 'import __graft_entry__ as g; "
+            f"g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != FS2_OK:
+        msg = load().fs2_status_string(rc).decode()
+        raise RuntimeError(f"{what} failed: fs2 status {rc} ({msg})")

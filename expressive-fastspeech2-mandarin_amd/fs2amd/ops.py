@@ -1,0 +1,205 @@
+"""Torch-facing wrappers of the fs2hip C ABI: device tensors in, device tensors out.
+
+Each wrapper validates shapes on the host, passes raw device pointers + sizes to
+libfs2hip.so and launches on ``torch.cuda.current_stream()``. PyTorch only provides the
+memory and the stream; every arithmetic op below runs in a hand-written HIP kernel. There
+is no CPU path: CPU tensors raise.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+_lib = L.load()
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _dt(t):
+    if t.dtype == torch.bfloat16:
+        return L.FS2_BF16
+    if t.dtype == torch.float32:
+        return L.FS2_F32
+    raise TypeError(f"fs2amd: unsupported dtype {t.dtype} (float32 / bfloat16 only)")
+
+
+def torch_dtype(code):
+    return torch.bfloat16 if code == L.FS2_BF16 else torch.float32
+
+
+def _gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("fs2amd: the HIP backend needs ROCm device tensors (got a CPU tensor); "
+                               "there is no CPU fallback")
+
+
+def _rows(x, name):
+    """Row stride (elements) of a [B, T, C] tensor whose rows are evenly spaced."""
+    if x.dim() != 3 or x.stride(2) != 1 or x.stride(0) != x.shape[1] * x.stride(1):
+        raise ValueError(f"fs2amd: {name} must be a [B, T, C] tensor with unit channel stride and packed rows")
+    return x.stride(1)
+
+
+def cin_pad(cin, compute):
+    return _lib.fs2_conv_cin_pad(cin, compute)
+
+
+def pack_conv_weight(w, compute, scale=None):
+    """nn.Conv1d weight [N, Cin, KS] (or nn.Linear [N, Cin]) -> packed [N, KS, Cin_pad] in the
+    compute dtype, optionally scaled per output channel (BatchNorm folding)."""
+    if w.dim() == 2:
+        w = w.unsqueeze(-1)
+    w = w.detach().float()
+    if scale is not None:
+        w = w * scale.detach().float().view(-1, 1, 1)
+    N, cin, ks = w.shape
+    cp = cin_pad(cin, compute)
+    out = torch.zeros(N, ks, cp, dtype=torch_dtype(compute), device=w.device)
+    out[:, :, :cin] = w.permute(0, 2, 1).to(out.dtype)
+    return out.contiguous()
+
+
+def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None, out=None, residual=None,
+           ln=None, lens=None, addvec1=None, addvec2=None, dot=None, n=None):
+    """Implicit-GEMM Conv1d / Linear with a fused epilogue (fs2_conv1d)."""
+    _gpu(x, w_packed, bias, residual, lens, addvec1, addvec2)
+    B, T, _ = x.shape
+    N = w_packed.shape[0] if n is None else n
+    d = L.ConvDesc()
+    d.x, d.x_dtype, d.x_row_stride = x.data_ptr(), _dt(x), _rows(x, "x")
+    d.w = w_packed.data_ptr()
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.B, d.T, d.Cin, d.Cin_pad, d.N, d.KS, d.pad = B, T, cin, w_packed.shape[-1], N, ks, pad
+    d.compute, d.epilogue = compute, epilogue
+    if residual is not None:
+        d.residual, d.res_dtype, d.res_row_stride = residual.data_ptr(), _dt(residual), _rows(residual, "residual")
+    if ln is not None:
+        g, b, eps = ln
+        d.ln_gamma, d.ln_beta, d.ln_eps = g.data_ptr(), b.data_ptr(), float(eps)
+    if lens is not None:
+        assert lens.dtype == torch.int64 and lens.numel() == B
+        d.lens = lens.data_ptr()
+    if addvec1 is not None:
+        d.addvec1 = addvec1.data_ptr()
+    if addvec2 is not None:
+        d.addvec2 = addvec2.data_ptr()
+    if epilogue == L.EPI_RELU_LN_DOT:
+        dw, db = dot
+        d.dot_w, d.dot_b = dw.data_ptr(), float(db)
+        if out is None:
+            out = torch.empty(B, T, device=x.device, dtype=torch.float32)
+        d.out, d.out_dtype, d.out_row_stride = out.data_ptr(), L.FS2_F32, 1
+    else:
+        if out is None:
+            out = torch.empty(B, T, N, device=x.device, dtype=torch_dtype(out_dtype))
+        d.out, d.out_dtype, d.out_row_stride = out.data_ptr(), _dt(out), _rows(out, "out")
+    L.check(_lib.fs2_conv1d(ctypes.byref(d), _stream(x)), "fs2_conv1d")
+    return out
+
+
+def attention(qkv, lens, n_head, d_k, temperature, out=None):
+    """Key-padding-masked multi-head self-attention over a fused [B, T, 3*H*dk] projection."""
+    _gpu(qkv, lens)
+    B, T, _ = qkv.shape
+    if out is None:
+        out = torch.empty(B, T, n_head * d_k, device=qkv.device, dtype=qkv.dtype)
+    L.check(_lib.fs2_attention(_ptr(qkv), _dt(qkv), _rows(qkv, "qkv"), _ptr(lens), B, T, n_head, d_k,
+                               float(temperature), _ptr(out), _rows(out, "out"), _stream(qkv)), "fs2_attention")
+    return out
+
+
+def embed_pe(tokens, table, pe, out_dtype):
+    _gpu(tokens, table, pe)
+    B, Lx = tokens.shape
+    D = table.shape[1]
+    out = torch.empty(B, Lx, D, device=tokens.device, dtype=torch_dtype(out_dtype))
+    L.check(_lib.fs2_embed_pe(_ptr(tokens.contiguous()), _ptr(table), table.shape[0], _ptr(pe), B, Lx, D, _ptr(out),
+                              out_dtype, _stream(tokens)), "fs2_embed_pe")
+    return out
+
+
+def cond_vectors(speakers, spk_table, emotions, arousals, valences, emo_table, aro_table, val_table, lin_w, lin_b, D):
+    ref = speakers if speakers is not None else emotions
+    _gpu(ref)
+    B = ref.shape[0]
+    spk_out = torch.empty(B, D, device=ref.device) if spk_table is not None else None
+    emo_out = torch.empty(B, D, device=ref.device) if emo_table is not None else None
+    d_emo = emo_table.shape[1] if emo_table is not None else 0
+    d_aro = aro_table.shape[1] if aro_table is not None else 0
+    d_val = val_table.shape[1] if val_table is not None else 0
+    L.check(_lib.fs2_cond_vectors(
+        _ptr(speakers), _ptr(spk_table), spk_table.shape[0] if spk_table is not None else 0,
+        _ptr(emotions), _ptr(emo_table), emo_table.shape[0] if emo_table is not None else 0, d_emo,
+        _ptr(arousals), _ptr(aro_table), aro_table.shape[0] if aro_table is not None else 0, d_aro,
+        _ptr(valences), _ptr(val_table), val_table.shape[0] if val_table is not None else 0, d_val,
+        _ptr(lin_w), _ptr(lin_b), B, D, _ptr(spk_out), _ptr(emo_out), _stream(ref)), "fs2_cond_vectors")
+    return spk_out, emo_out
+
+
+def variance_embed(x, pred, target, control, bins, table):
+    """In place: pred *= control (no target); x += table[bucketize(target or pred, bins)]."""
+    _gpu(x, pred, target, bins, table)
+    M = pred.numel()
+    D = x.shape[-1]
+    L.check(_lib.fs2_variance_embed(_ptr(x), _dt(x), _ptr(pred), _ptr(target), float(control), _ptr(bins),
+                                    bins.numel() + 1, _ptr(table), M, D, _stream(x)), "fs2_variance_embed")
+
+
+def _dur_kind(dur, logpred):
+    if logpred:
+        return L.DUR_LOGPRED
+    if dur.dtype == torch.int64:
+        return L.DUR_I64
+    if dur.dtype == torch.float32:
+        return L.DUR_F32
+    raise TypeError(f"fs2amd: durations must be int64 or float32, got {dur.dtype}")
+
+
+def lr_durations(dur, logpred=False, d_control=1.0):
+    """Frame counts -> (cum int32 [B, L], mel_len int64 [B], d_rounded f32 [B, L] or None)."""
+    _gpu(dur)
+    dur = dur.contiguous()
+    B, Lx = dur.shape
+    cum = torch.empty(B, Lx, device=dur.device, dtype=torch.int32)
+    mel_len = torch.empty(B, device=dur.device, dtype=torch.int64)
+    d_rounded = torch.empty(B, Lx, device=dur.device, dtype=torch.float32) if logpred else None
+    L.check(_lib.fs2_lr_durations(_ptr(dur), _dur_kind(dur, logpred), float(d_control), B, Lx, _ptr(cum),
+                                  _ptr(mel_len), _ptr(d_rounded), _stream(dur)), "fs2_lr_durations")
+    return cum, mel_len, d_rounded
+
+
+def lr_expand(x, cum, mel_len, T_out, pe=None, out_dtype=None, index_map=False):
+    _gpu(x, cum, mel_len, pe)
+    x = x.contiguous()
+    B, Lx, D = x.shape
+    od = _dt(x) if out_dtype is None else out_dtype
+    out = torch.empty(B, T_out, D, device=x.device, dtype=torch_dtype(od))
+    im = torch.empty(B, T_out, device=x.device, dtype=torch.int32) if index_map else None
+    L.check(_lib.fs2_lr_expand(_ptr(x), _dt(x), _ptr(cum), _ptr(mel_len), B, Lx, D, T_out, _ptr(pe), _ptr(out), od,
+                               _ptr(im), _stream(x)), "fs2_lr_expand")
+    return (out, im) if index_map else out
+
+
+def length_regulate(x, duration, max_len=None, return_index_map=False):
+    """Drop-in for the reference ``LengthRegulator.forward(x, duration, max_len)``
+    (model/modules.py:192-194): returns (output [B, T, D], mel_len int64 [B]).
+
+    T = max_len when given (and non-zero, like utils/tools.py:361), else max(mel_len) — the
+    one device->host read this path needs."""
+    cum, mel_len, _ = lr_durations(duration)
+    if max_len:
+        T_out = int(max_len)
+    else:
+        T_out = int(mel_len.max().item()) if mel_len.numel() else 0
+    res = lr_expand(x, cum, mel_len, T_out, index_map=return_index_map)
+    if return_index_map:
+        return res[0], mel_len, res[1]
+    return res, mel_len

@@ -1,0 +1,40 @@
+"""ScheduledOptim: Adam with the Noam warm-up / inverse-sqrt schedule and step annealing
+(model/optimizer.py:5-51): lr = d_model^-0.5 * min(step^-0.5, warmup^-1.5 * step)
+* anneal_rate^(#anneal_steps passed)."""
+import numpy as np
+import torch
+
+
+class ScheduledOptim:
+    def __init__(self, model, train_config, model_config, current_step):
+        opt = train_config["optimizer"]
+        self._optimizer = torch.optim.Adam(model.parameters(), betas=opt["betas"], eps=opt["eps"],
+                                           weight_decay=opt["weight_decay"])
+        self.n_warmup_steps = opt["warm_up_step"]
+        self.anneal_steps = opt["anneal_steps"]
+        self.anneal_rate = opt["anneal_rate"]
+        self.current_step = current_step
+        self.init_lr = np.power(model_config["transformer"]["encoder_hidden"], -0.5)
+
+    def step_and_update_lr(self):
+        self._update_learning_rate()
+        self._optimizer.step()
+
+    def zero_grad(self):
+        self._optimizer.zero_grad()
+
+    def load_state_dict(self, state):
+        self._optimizer.load_state_dict(state)
+
+    def _get_lr_scale(self):
+        lr = np.min([np.power(self.current_step, -0.5), np.power(self.n_warmup_steps, -1.5) * self.current_step])
+        for s in self.anneal_steps:
+            if self.current_step > s:
+                lr = lr * self.anneal_rate
+        return lr
+
+    def _update_learning_rate(self):
+        self.current_step += 1
+        lr = self.init_lr * self._get_lr_scale()
+        for group in self._optimizer.param_groups:
+            group["lr"] = lr

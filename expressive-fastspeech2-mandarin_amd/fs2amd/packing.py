@@ -1,0 +1,94 @@
+"""Weight packing for the fs2hip kernels (host side, once per parameter version).
+
+* Q|K|V projections concatenated into one [768, 1, Cin_pad] GEMM operand (one launch, one
+  read of x instead of three: SubLayers.py:39-41).
+* Conv1d weights [N, Cin, K] re-laid to [N, K, Cin_pad] (k-steps = (tap, channel block)).
+* PostNet BatchNorm1d (eval: running stats) folded into its conv: w' = w * g/sqrt(rv+eps),
+  b' = (b - rm) * g/sqrt(rv+eps) + beta (transformer/Layers.py:92-135).
+* bf16 precision: FFT blocks, mel_linear, PostNet in bf16; VariancePredictors always f32.
+Everything else (LayerNorm affine, biases, embedding tables, bins, PE tables) stays f32.
+"""
+from types import SimpleNamespace
+
+import torch
+
+from . import _lib as L
+from .ops import pack_conv_weight
+
+
+def _f32(t, device):
+    return t.detach().to(device=device, dtype=torch.float32).contiguous()
+
+
+def _fft_layer(layer, device, compute):
+    a, f = layer.slf_attn, layer.pos_ffn
+    wqkv = torch.cat([a.w_qs.weight, a.w_ks.weight, a.w_vs.weight], 0).to(device)
+    bqkv = torch.cat([a.w_qs.bias, a.w_ks.bias, a.w_vs.bias], 0)
+    return SimpleNamespace(
+        n_head=a.n_head, d_k=a.d_k,
+        wqkv=pack_conv_weight(wqkv, compute), bqkv=_f32(bqkv, device),
+        wfc=pack_conv_weight(a.fc.weight.to(device), compute), bfc=_f32(a.fc.bias, device),
+        ln1=(_f32(a.layer_norm.weight, device), _f32(a.layer_norm.bias, device), a.layer_norm.eps),
+        w1=pack_conv_weight(f.w_1.weight.to(device), compute), b1=_f32(f.w_1.bias, device),
+        k1=f.w_1.kernel_size[0], p1=f.w_1.padding[0], c1=f.w_1.in_channels,
+        w2=pack_conv_weight(f.w_2.weight.to(device), compute), b2=_f32(f.w_2.bias, device),
+        k2=f.w_2.kernel_size[0], p2=f.w_2.padding[0], c2=f.w_2.in_channels,
+        ln2=(_f32(f.layer_norm.weight, device), _f32(f.layer_norm.bias, device), f.layer_norm.eps),
+    )
+
+
+def _vp(vp, device):
+    cl = vp.conv_layer
+    c1, c2 = cl.conv1d_1.conv, cl.conv1d_2.conv
+    return SimpleNamespace(
+        w1=pack_conv_weight(c1.weight.to(device), L.FS2_F32), b1=_f32(c1.bias, device), k1=c1.kernel_size[0],
+        p1=c1.padding[0], c1=c1.in_channels,
+        ln1=(_f32(cl.layer_norm_1.weight, device), _f32(cl.layer_norm_1.bias, device), cl.layer_norm_1.eps),
+        w2=pack_conv_weight(c2.weight.to(device), L.FS2_F32), b2=_f32(c2.bias, device), k2=c2.kernel_size[0],
+        p2=c2.padding[0], c2=c2.in_channels,
+        ln2=(_f32(cl.layer_norm_2.weight, device), _f32(cl.layer_norm_2.bias, device), cl.layer_norm_2.eps),
+        lin_w=_f32(vp.linear_layer.weight.view(-1), device), lin_b=float(vp.linear_layer.bias.detach().cpu()[0]),
+    )
+
+
+def _postnet(pn, device, compute):
+    layers = []
+    for seq in pn.convolutions:
+        conv, bn = seq[0].conv, seq[1]
+        s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
+        b = (conv.bias.detach().float() - bn.running_mean.detach().float()) * s + bn.bias.detach().float()
+        layers.append(SimpleNamespace(w=pack_conv_weight(conv.weight.to(device), compute, scale=s.to(device)),
+                                      b=_f32(b, device), k=conv.kernel_size[0], p=conv.padding[0],
+                                      cin=conv.in_channels, cout=conv.out_channels))
+    return layers
+
+
+def pack_model(model, device, precision):
+    device = torch.device(device)
+    big = L.FS2_BF16 if precision == "bf16" else L.FS2_F32
+    va = model.variance_adaptor
+    P = SimpleNamespace(precision=precision, compute=big, act_dtype=big, device=device)
+    P.enc_emb = _f32(model.encoder.src_word_emb.weight, device)
+    P.enc_pe = _f32(model.encoder.position_enc[0], device)
+    P.dec_pe = _f32(model.decoder.position_enc[0], device)
+    P.enc_layers = [_fft_layer(l, device, big) for l in model.encoder.layer_stack]
+    P.dec_layers = [_fft_layer(l, device, big) for l in model.decoder.layer_stack]
+    P.vp = {k: _vp(getattr(va, f"{k}_predictor"), device) for k in ("duration", "pitch", "energy")}
+    P.bins = {k: _f32(getattr(va, f"{k}_bins"), device) for k in ("pitch", "energy")}
+    P.var_table = {k: _f32(getattr(va, f"{k}_embedding").weight, device) for k in ("pitch", "energy")}
+    P.mel_w = pack_conv_weight(model.mel_linear.weight.to(device), big)
+    P.mel_b = _f32(model.mel_linear.bias, device)
+    P.n_mel = model.mel_linear.out_features
+    P.postnet = _postnet(model.postnet, device, big)
+    P.spk_table = _f32(model.speaker_emb.weight, device) if model.speaker_emb is not None else None
+    if model.emotion_emb is not None:
+        P.emo_table = _f32(model.emotion_emb.weight, device)
+        P.aro_table = _f32(model.arousal_emb.weight, device)
+        P.val_table = _f32(model.valence_emb.weight, device)
+        P.emo_w = _f32(model.emotion_linear[0].weight, device)
+        P.emo_b = _f32(model.emotion_linear[0].bias, device)
+    else:
+        P.emo_table = None
+    P.d_model = model.encoder.d_model
+    P.max_seq_len = model.encoder.max_seq_len
+    return P

@@ -1,0 +1,174 @@
+/*
+ * fs2hip.h — C ABI of libfs2hip.so, the MI355X (gfx950 / CDNA4) kernels of the FastSpeech2
+ * mel-synthesis forward (Napoliee/Expressive-FastSpeech2-Mandarin).
+ *
+ * Plain pointers and sizes only: every pointer is a device pointer the caller allocated
+ * (HBM), every launch goes on the caller's stream, nothing is allocated or synchronised
+ * inside, and there is no global mutable state (reentrant; one call per DataParallel
+ * thread is fine). Return value: 0 (FS2_OK) or an fs2_status code; the Python host layer
+ * (fs2amd/_lib.py) maps non-zero codes to RuntimeError.
+ *
+ * Layouts: activations are row-major [B, T, C] ("rows" = (b, t) pairs, C contiguous; a
+ * row stride in ELEMENTS may exceed C). dtype codes: FS2_F32 / FS2_BF16.
+ * Reference citations are /root/reference paths (the reference is pure PyTorch: these
+ * entry points replace the implicit ATen kernels its modules dispatch).
+ */
+#ifndef FS2HIP_H
+#define FS2HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *fs2_stream_t; /* a hipStream_t (NULL = default stream) */
+
+enum fs2_dtype { FS2_F32 = 0, FS2_BF16 = 1 };
+
+enum fs2_status {
+  FS2_OK = 0,
+  FS2_EINVAL = 1,       /* bad argument / shape the kernels do not cover */
+  FS2_ELAUNCH = 2,      /* hipGetLastError() after the launch was non-zero */
+  FS2_EUNSUPPORTED = 3, /* dtype / tile combination not instantiated */
+};
+
+/* ---- epilogues of fs2_conv1d ------------------------------------------------------------ */
+enum fs2_epilogue {
+  FS2_EPI_BIAS = 0,        /* y = acc + bias                                                */
+  FS2_EPI_BIAS_RELU = 1,   /* y = relu(acc + bias)            (FFN w_1, SubLayers.py:88)    */
+  FS2_EPI_BIAS_TANH = 2,   /* y = tanh(acc + bias)            (PostNet, Layers.py:133)      */
+  FS2_EPI_BIAS_RES = 3,    /* y = acc + bias + residual       (PostNet residual, fastspeech2.py:136) */
+  FS2_EPI_RES_LN = 4,      /* y = LN(acc + bias + residual); rows t >= lens[b] -> 0;
+                              then y += addvec1[b] (+ addvec2[b]).  Requires N == 256.
+                              (MHA fc / FFN w_2 + LayerNorm + masked_fill, SubLayers.py:54-55,
+                              :88-91, Layers.py:25,28; speaker/emotion add fastspeech2.py:101-110) */
+  FS2_EPI_RELU_LN = 5,     /* y = LN(relu(acc + bias))        (VariancePredictor, modules.py:218-233) */
+  FS2_EPI_RELU_LN_DOT = 6, /* out[row] = (t >= lens[b]) ? 0 : dot(LN(relu(acc+bias)), dot_w) + dot_b
+                              -> f32 [B*T]                    (VP linear + masked_fill, modules.py:240-250) */
+};
+
+/*
+ * fs2_conv1d — implicit-GEMM Conv1d / Linear over padded sequences, bf16 or f32 MFMA.
+ *
+ *   y[b,t,n] = epi( sum_{k<KS} sum_{c<Cin} x[b, t+k-pad, c] * w[n][k][c] + bias[n] )
+ *
+ * with x[b, s, :] = 0 outside s in [0, T) (per-sequence zero padding, as nn.Conv1d on the
+ * [B, C, T] transpose; padded frames INSIDE [0, T) are read as they are).
+ * KS = 1, pad = 0 is nn.Linear.  Replaces: nn.Linear in MultiHeadAttention (w_qs/w_ks/w_vs
+ * fused into one N=768 GEMM, fc) transformer/SubLayers.py:18-20,39-41,54; nn.Conv1d in
+ * PositionwiseFeedForward SubLayers.py:68-80; VariancePredictor Conv model/modules.py:253-296;
+ * mel_linear model/fastspeech2.py:23-26,134; PostNet ConvNorm+BatchNorm1d(eval, folded into
+ * w and bias by the host) transformer/Layers.py:33-137.
+ *
+ * w is PACKED: [N][KS][Cin_pad] in the compute dtype, Cin_pad = Cin rounded up to 64 (bf16)
+ * or 32 (f32) with zeros (fs2_conv_cin_pad()). Cin and N must be multiples of 8 and 4.
+ */
+typedef struct fs2_conv_desc {
+  const void *x;            /* [B, T, >=Cin], dtype x_dtype                              */
+  int x_dtype;
+  int64_t x_row_stride;     /* elements between rows of x                                  */
+  const void *w;            /* packed weights (compute dtype)                              */
+  const float *bias;        /* [N] or NULL                                                 */
+  int B, T, Cin, Cin_pad, N, KS, pad;
+  int compute;              /* FS2_BF16 (mfma_f32_16x16x32_bf16) or FS2_F32 (mfma_f32_16x16x4f32) */
+  int epilogue;             /* enum fs2_epilogue                                           */
+  const void *residual;     /* [B, T, N] (BIAS_RES / RES_LN)                               */
+  int res_dtype;
+  int64_t res_row_stride;
+  const float *ln_gamma;    /* [N] (LN epilogues)                                          */
+  const float *ln_beta;
+  float ln_eps;
+  const int64_t *lens;      /* [B] valid rows per sequence (RES_LN / RELU_LN_DOT) or NULL  */
+  const float *addvec1;     /* [B, N] or NULL (RES_LN)                                     */
+  const float *addvec2;     /* [B, N] or NULL (RES_LN)                                     */
+  const float *dot_w;       /* [N] (RELU_LN_DOT)                                           */
+  float dot_b;
+  void *out;                /* [B, T, N] (f32 [B*T] for RELU_LN_DOT)                       */
+  int out_dtype;
+  int64_t out_row_stride;
+} fs2_conv_desc;
+
+int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream);
+int fs2_conv_cin_pad(int Cin, int compute);
+
+/*
+ * fs2_attention — ScaledDotProductAttention with a key-padding mask, all heads.
+ * Replaces transformer/Modules.py:14-25 (bmm, /temperature, masked_fill(-inf), softmax(dim=2),
+ * bmm) and the head split/merge permutes of SubLayers.py:42-52.
+ * qkv: [B, T, 3*H*dk] rows (the fused projection's output): Q at column h*dk, K at
+ * (H+h)*dk, V at (2H+h)*dk.  out: [B, T, H*dk], head h at column h*dk.
+ * Keys t >= key_lens[b] get zero weight; every query row (padded ones included) is computed.
+ * A sequence with key_lens[b] == 0 yields zeros (the reference yields NaN rows that its
+ * masked_fill then zeroes).  dk must be 128.
+ */
+int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
+                  int H, int dk, float temperature, void *out, int64_t out_row_stride, fs2_stream_t stream);
+
+/*
+ * fs2_embed_pe — out[b,l,:] = table[tokens[b,l], :] + pe[l, :]   (f32 math)
+ * Replaces Encoder src_word_emb + position_enc (transformer/Models.py:82-91).
+ * tokens outside [0, vocab) are clamped (the reference raises IndexError on the host).
+ */
+int fs2_embed_pe(const int64_t *tokens, const float *table, int vocab, const float *pe, int B, int L, int D,
+                 void *out, int out_dtype, fs2_stream_t stream);
+
+/*
+ * fs2_cond_vectors — the per-utterance conditioning vectors added to every encoder position:
+ *   spk_out[b] = speaker_table[speakers[b]]                               (fastspeech2.py:101-104)
+ *   emo_out[b] = relu(W @ cat(emo[e_b], aro[a_b], val[v_b]) + bias)      (fastspeech2.py:106-110)
+ * W is [D][d_emo + d_aro + d_val] (nn.Linear layout).  Either table may be NULL (skipped).
+ */
+int fs2_cond_vectors(const int64_t *speakers, const float *speaker_table, int n_speaker, const int64_t *emotions,
+                     const float *emo_table, int n_emo, int d_emo, const int64_t *arousals, const float *aro_table,
+                     int n_aro, int d_aro, const int64_t *valences, const float *val_table, int n_val, int d_val,
+                     const float *lin_w, const float *lin_b, int B, int D, float *spk_out, float *emo_out,
+                     fs2_stream_t stream);
+
+/*
+ * fs2_variance_embed — pitch/energy bucketize + embedding add (model/modules.py:80-100,117-126):
+ *   v = target ? target[m] : (pred[m] *= control);  idx = #{bins[i] < v}  (torch.bucketize, right=False)
+ *   x[m, :] += table[idx, :]
+ * x: [M, D] in place (dtype x_dtype); pred f32 [M] (scaled in place when target == NULL);
+ * bins f32 [n_bins - 1]; table f32 [n_bins, D].
+ */
+int fs2_variance_embed(void *x, int x_dtype, float *pred, const float *target, float control, const float *bins,
+                       int n_bins, const float *table, int M, int D, fs2_stream_t stream);
+
+/*
+ * LengthRegulator (model/modules.py:161-194 + utils/tools.py:360-378), split in two launches
+ * so a caller without max_mel_len can read max(mel_len) in between (one D2H read per batch,
+ * where the reference does B*L_max .item() syncs).
+ *
+ * fs2_lr_durations: per sequence, frames_i = max(trunc(d_i), 0) over ALL L positions,
+ *   cum[b,i] = sum_{j<=i} frames_j (int32, saturating), mel_len[b] = sum (int64, not cropped).
+ *   dur_kind FS2_DUR_I64: d int64 targets; FS2_DUR_F32: f32 durations (truncated like int());
+ *   FS2_DUR_LOGPRED: d = f32 log-duration predictions, rounded like modules.py:132-135:
+ *   d_rounded = clamp(round_half_even(exp(d) - 1) * d_control, min=0), written to d_rounded.
+ * fs2_lr_expand: out[b,t,:] = (t < min(mel_len[b], T_out) ? x[b, src(b,t), :] : 0) (+ pe[t,:]),
+ *   src(b,t) = first i with cum[b,i] > t.  pe (f32 [>=T_out, D]) may be NULL; a non-NULL pe
+ *   fuses the Decoder's position_enc add (transformer/Models.py:158-160).  index_map (int32
+ *   [B, T_out], -1 on padding) is optional.  D must be a multiple of 8.
+ */
+enum fs2_dur_kind { FS2_DUR_I64 = 0, FS2_DUR_F32 = 1, FS2_DUR_LOGPRED = 2 };
+
+int fs2_lr_durations(const void *dur, int dur_kind, float d_control, int B, int L, int32_t *cum, int64_t *mel_len,
+                     float *d_rounded, fs2_stream_t stream);
+int fs2_lr_expand(const void *x, int x_dtype, const int32_t *cum, const int64_t *mel_len, int B, int L, int D,
+                  int T_out, const float *pe, void *out, int out_dtype, int32_t *index_map, fs2_stream_t stream);
+
+/* Convenience: both launches with a caller-known T_out (the teacher-forced / max_mel_len path). */
+int fs2_length_regulate(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control, int B, int L,
+                        int D, int T_out, const float *pe, void *out, int out_dtype, int32_t *cum, int64_t *mel_len,
+                        float *d_rounded, int32_t *index_map, fs2_stream_t stream);
+
+/* Library identification. */
+const char *fs2_version(void);
+const char *fs2_status_string(int status);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FS2HIP_H */

@@ -1,0 +1,151 @@
+"""Host-side logic on CPU: the C-ABI library loads and exports every declared symbol, the
+drop-in module has the reference's constructor / state_dict contract, packing is right."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from _common import configs, manifest, oracle_state_dict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    from fs2amd import _lib
+
+    lib = _lib.load()
+    declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
+    assert len(declared) == len(_lib.SIGNATURES) == 11
+    for name in declared:
+        assert hasattr(lib, name), name
+        assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
+    assert b"gfx950" in lib.fs2_version()
+    assert lib.fs2_status_string(1) == b"invalid argument"
+    assert lib.fs2_conv_cin_pad(80, _lib.FS2_BF16) == 128 and lib.fs2_conv_cin_pad(80, _lib.FS2_F32) == 96
+
+
+def test_conv_desc_layout_matches_header():
+    """ctypes mirror of fs2_conv_desc has the C layout (offsets computed by the compiler)."""
+    import subprocess
+    import tempfile
+
+    from fs2amd import _lib
+
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "fs2hip.h"
+#define P(f) printf("%s %zu\n", #f, offsetof(fs2_conv_desc, f));
+int main(void){ P(x) P(x_row_stride) P(w) P(B) P(compute) P(residual) P(res_row_stride) P(ln_gamma) P(ln_eps)
+ P(lens) P(dot_w) P(dot_b) P(out) P(out_dtype) P(out_row_stride) printf("size %zu\n", sizeof(fs2_conv_desc)); }
+'''
+    d = tempfile.mkdtemp()
+    with open(os.path.join(d, "t.c"), "w") as f:
+        f.write(src)
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), os.path.join(d, "t.c"), "-o", os.path.join(d, "t")],
+                   check=True)
+    out = subprocess.run([os.path.join(d, "t")], capture_output=True, text=True, check=True).stdout.split("\n")
+    for line in out:
+        if not line:
+            continue
+        name, off = line.split()
+        if name == "size":
+            assert int(off) == ctypes.sizeof(_lib.ConvDesc)
+        else:
+            assert getattr(_lib.ConvDesc, name).offset == int(off), name
+
+
+def test_invalid_arguments_are_rejected_without_a_gpu():
+    from fs2amd import _lib
+
+    lib = _lib.load()
+    d = _lib.ConvDesc()  # all-null descriptor
+    assert lib.fs2_conv1d(ctypes.byref(d), None) == _lib.FS2_EINVAL
+    assert lib.fs2_attention(None, 0, 768, None, 1, 1, 2, 128, 11.3, None, 256, None) == _lib.FS2_EINVAL
+    assert lib.fs2_lr_durations(None, 0, 1.0, 1, 1, None, None, None, None) == _lib.FS2_EINVAL
+    assert lib.fs2_lr_expand(None, 0, None, None, 1, 1, 8, 1, None, None, 0, None, None) == _lib.FS2_EINVAL
+
+
+def _model():
+    from fs2amd.model import FastSpeech2
+
+    pc, mc, _ = configs()
+    return FastSpeech2(pc, mc)
+
+
+def test_state_dict_contract_matches_reference():
+    m = _model()
+    sd = m.state_dict()
+    man = manifest()["keys"]
+    assert list(sd.keys()) == list(man.keys()) or set(sd.keys()) == set(man.keys())
+    assert len(sd) == 240
+    for k, v in sd.items():
+        assert list(v.shape) == man[k]["shape"], k
+    # constructor-computed tensors are identical to the reference's (PE tables, bins)
+    for k in ("encoder.position_enc", "decoder.position_enc", "variance_adaptor.pitch_bins",
+              "variance_adaptor.energy_bins"):
+        import hashlib
+        assert hashlib.sha256(sd[k].numpy().tobytes()).hexdigest() == man[k]["sha256"], k
+    n_train = sum(p.numel() for p in m.parameters() if p.requires_grad)
+    assert n_train == 34_659_075
+
+
+def test_load_reference_state_dict_strict():
+    m = _model()
+    m.load_state_dict(oracle_state_dict(), strict=True)
+
+
+def test_packing_batchnorm_fold_and_layouts():
+    """Packed operands reproduce the reference ops in plain torch (CPU)."""
+    from fs2amd import _lib as L
+    from fs2amd.packing import pack_model
+
+    m = _model()
+    m.load_state_dict(oracle_state_dict())
+    m.eval()
+    P = pack_model(m, "cpu", "fp32")
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 31, 512, generator=g)
+    seq = m.postnet.convolutions[1]
+    with torch.no_grad():
+        ref = seq[1](seq[0].conv(x.transpose(1, 2))).transpose(1, 2)
+    lp = P.postnet[1]
+    w = lp.w[:, :, :512].permute(0, 2, 1)
+    got = F.conv1d(x.transpose(1, 2), w, lp.b, padding=2).transpose(1, 2)
+    assert float((got - ref).abs().max()) < 1e-4
+    lay = P.enc_layers[0]
+    a = m.encoder.layer_stack[0].slf_attn
+    assert torch.equal(lay.wqkv[:256, 0, :], a.w_qs.weight) and torch.equal(lay.wqkv[512:, 0, :], a.w_vs.weight)
+    assert lay.w1.shape == (1024, 9, 256) and torch.equal(lay.w1[:, 3, :], m.encoder.layer_stack[0].pos_ffn.w_1.weight[:, :, 3])
+    Pb = pack_model(m, "cpu", "bf16")
+    assert Pb.enc_layers[0].w1.dtype == torch.bfloat16 and Pb.vp["pitch"].w1.dtype == torch.float32
+    assert Pb.postnet[0].w.shape == (512, 5, 128)
+
+
+def test_forward_refuses_cpu_and_training():
+    from fs2amd.data import synth_batch
+
+    m = _model().eval()
+    with pytest.raises(RuntimeError, match="HIP"):
+        with torch.no_grad():
+            m(**synth_batch(1, 8, seed=3))
+    m.train()
+    with pytest.raises(NotImplementedError):
+        m(**synth_batch(1, 8, seed=3))
+
+
+def test_drop_in_import_path():
+    """`from model import FastSpeech2, FastSpeech2Loss, ScheduledOptim` like the reference callers."""
+    import importlib
+    import sys
+
+    pkg_root = os.path.join(REPO, "expressive-fastspeech2-mandarin_amd")
+    sys.path.insert(0, pkg_root)
+    mod = importlib.import_module("model")
+    assert mod.__file__.startswith(pkg_root)
+    from fs2amd.model import FastSpeech2
+    assert mod.FastSpeech2 is FastSpeech2
+    assert hasattr(mod, "FastSpeech2Loss") and hasattr(mod, "ScheduledOptim")
