@@ -26,6 +26,8 @@
 // Epilogue: the f32 accumulator tile goes through LDS (reusing the staging buffers) and is
 // written row-major with 8/16-byte stores; the LayerNorm epilogues run one wave per row
 // (N = 256 = 64 lanes x 4) with shuffle reductions.
+#include <type_traits>
+
 #include "fs2_common.h"
 
 namespace {
@@ -50,40 +52,56 @@ struct CTraits<FS2_F32> {
 };
 
 // One 16-byte LDS chunk (CE compute elements) staged in registers from an input of type TIn.
+// Loads are raw buffer loads: an out-of-range byte offset (kOOB) returns zeros in hardware, so
+// the conv's zero padding / tile edges cost a select on the offset instead of a branch per load
+// (branches around loads make hipcc wait vmcnt(0) per element, serialising the stage).
+constexpr uint32_t kOOB = 0x80000000u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void *p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 bload16(rsrc_t r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ uint2 bload8(rsrc_t r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return make_uint2(v[0], v[1]);
+}
+
 template <int CT, typename TIn>
 struct Stage;
 template <>
 struct Stage<FS2_BF16, bf16> {
   uint4 r;
-  __device__ __forceinline__ void load(const bf16 *p) { r = *reinterpret_cast<const uint4 *>(p); }
-  __device__ __forceinline__ void zero() { r = make_uint4(0u, 0u, 0u, 0u); }
+  __device__ __forceinline__ void load(rsrc_t rs, uint32_t off) { r = bload16(rs, off); }
   __device__ __forceinline__ uint4 chunk() const { return r; }
 };
 template <>
 struct Stage<FS2_BF16, float> {
-  float4 a, b;
-  __device__ __forceinline__ void load(const float *p) {
-    a = reinterpret_cast<const float4 *>(p)[0];
-    b = reinterpret_cast<const float4 *>(p)[1];
+  uint4 a, b;
+  __device__ __forceinline__ void load(rsrc_t rs, uint32_t off) {
+    a = bload16(rs, off);
+    b = bload16(rs, off + 16u);
   }
-  __device__ __forceinline__ void zero() { a = b = make_float4(0.f, 0.f, 0.f, 0.f); }
   __device__ __forceinline__ uint4 chunk() const {
-    bf16x8 v = {(bf16)a.x, (bf16)a.y, (bf16)a.z, (bf16)a.w, (bf16)b.x, (bf16)b.y, (bf16)b.z, (bf16)b.w};
+    bf16x8 v = {(bf16)__uint_as_float(a.x), (bf16)__uint_as_float(a.y), (bf16)__uint_as_float(a.z),
+                (bf16)__uint_as_float(a.w), (bf16)__uint_as_float(b.x), (bf16)__uint_as_float(b.y),
+                (bf16)__uint_as_float(b.z), (bf16)__uint_as_float(b.w)};
     return *reinterpret_cast<uint4 *>(&v);
   }
 };
 template <>
 struct Stage<FS2_F32, float> {
   uint4 r;
-  __device__ __forceinline__ void load(const float *p) { r = *reinterpret_cast<const uint4 *>(p); }
-  __device__ __forceinline__ void zero() { r = make_uint4(0u, 0u, 0u, 0u); }
+  __device__ __forceinline__ void load(rsrc_t rs, uint32_t off) { r = bload16(rs, off); }
   __device__ __forceinline__ uint4 chunk() const { return r; }
 };
 template <>
 struct Stage<FS2_F32, bf16> {
   uint2 r;
-  __device__ __forceinline__ void load(const bf16 *p) { r = *reinterpret_cast<const uint2 *>(p); }
-  __device__ __forceinline__ void zero() { r = make_uint2(0u, 0u); }
+  __device__ __forceinline__ void load(rsrc_t rs, uint32_t off) { r = bload8(rs, off); }
   __device__ __forceinline__ uint4 chunk() const {
     return make_uint4(r.x << 16, r.x & 0xffff0000u, r.y << 16, r.y & 0xffff0000u);
   }
@@ -95,6 +113,8 @@ struct ConvArgs {
   const void *w;
   const float *bias;
   int B, T, Cin, Cin_pad, N, KS, pad, M;
+  int ntn;  // number of N tiles
+  uint32_t x_bytes, w_bytes;
   int epi;
   const void *res;
   int res_dt;
@@ -125,143 +145,265 @@ __device__ __forceinline__ void store_any4(void *p, int dt, int64_t off, const f
     store4(reinterpret_cast<float *>(p) + off, v);
 }
 
-template <int CT, int WGM, int WGN, typename TIn>
+// Tile (WGM x WGN waves, each wave WMI x 4 MFMA 16x16 blocks):  BM = 16*WMI*WGM, BN = 64*WGN.
+// KSMAX bounds the conv taps the LDS halo is sized for.
+template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, bool GL>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
-  constexpr int BM = 64 * WGM, BN = 64 * WGN;
+  constexpr int WROWS = 16 * WMI;
+  constexpr int BM = WROWS * WGM, BN = 64 * WGN;
   constexpr int KE = CTraits<CT>::KE, CE = CTraits<CT>::CE;
   using TW = typename CTraits<CT>::T;
-  constexpr int A_CH = BM * 8 / 256, B_CH = BN * 8 / 256;
-  constexpr int STAGE_BYTES = (BM + BN) * kRowBytes;
+  constexpr int HMAX0 = BM + KSMAX - 1;
+  constexpr int HMAX = GL ? (HMAX0 + 7) / 8 * 8 : HMAX0;  // halo rows of one A stage (whole 1 KiB pieces)
+  constexpr int A_CH = (HMAX * 8 + 255) / 256;         // 16-byte chunks per thread (A halo)
+  constexpr int B_CH = BN * 8 / 256;
+  constexpr int A_BYTES = HMAX * kRowBytes, B_BYTES = BN * kRowBytes;
+  constexpr int STAGE = 2 * (A_BYTES + B_BYTES);
   constexpr int EPI_LD = BN + 4;
-  constexpr int SMEM = (2 * STAGE_BYTES > BM * EPI_LD * 4) ? 2 * STAGE_BYTES : BM * EPI_LD * 4;
+  constexpr int SMEM = (STAGE > BM * EPI_LD * 4) ? STAGE : BM * EPI_LD * 4;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  char *const Abuf = smem;                  // 2 x A_BYTES
+  char *const Bbuf = smem + 2 * A_BYTES;    // 2 x B_BYTES
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform for the compiler
   const int wr = wid / WGN, wc = wid % WGN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+
+  // XCD-aware tile order: the dispatcher deals workgroups round-robin over the 8 XCDs, so
+  // give each XCD a contiguous run of tiles, N-fastest: the N tiles of one row panel run
+  // together on one XCD and share that panel (and its halo) through the XCD's L2.
+  const int nwg = gridDim.x, id = blockIdx.x;
+  const int q = nwg >> 3, rem = nwg & 7, xcd = id & 7, li = id >> 3;
+  const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + li;
+  const int mt = tile / a.ntn, nt = tile - mt * a.ntn;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int KS = a.KS, pad = a.pad;
+  const int H = BM + KS - 1;
   const int nCk = a.Cin_pad / KE;
-  const int nK = a.KS * nCk;
+  const int nK = KS * nCk;
   const int T = a.T, M = a.M;
 
-  const TIn *__restrict__ x = reinterpret_cast<const TIn *>(a.x);
-  const TW *__restrict__ w = reinterpret_cast<const TW *>(a.w);
 
   const int srow = tid >> 3, schunk = tid & 7;
-  int a_t[A_CH];
-  int a_m[A_CH];
-  bool a_ok[A_CH];
-#pragma unroll
-  for (int j = 0; j < A_CH; ++j) {
-    const int m = m0 + srow + 32 * j;
-    a_ok[j] = m < M;
-    a_m[j] = m;
-    const int bb = m / T;
-    a_t[j] = m - bb * T;
-  }
-  const TW *wp[B_CH];
-  bool b_ok[B_CH];
-  const int64_t wrow = (int64_t)a.KS * a.Cin_pad;
+  // B rows this thread stages (byte offsets into the packed weights; kOOB past N)
+  const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
+  uint32_t wofs[B_CH];
+  const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * (uint32_t)sizeof(TW);
 #pragma unroll
   for (int j = 0; j < B_CH; ++j) {
     const int n = n0 + srow + 32 * j;
-    b_ok[j] = n < a.N;
-    wp[j] = w + (int64_t)(b_ok[j] ? n : 0) * wrow + schunk * CE;
+    wofs[j] = n < a.N ? (uint32_t)n * wrow + schunk * 16u : kOOB;
   }
+  // sequence position of this lane's A fragment rows (tap validity)
+  int tpos[WMI];
+#pragma unroll
+  for (int mi = 0; mi < WMI; ++mi) {
+    const int m = m0 + wr * WROWS + mi * 16 + (lane & 15);
+    tpos[mi] = m % T;
+  }
+  // wave-uniform: do this wave's WROWS rows lie inside one sequence? Then a tap shift is valid
+  // for all of them or for none at the tile's own rows, and the per-lane masking is skipped.
+  const int tw = (m0 + wr * WROWS) % T;
+  const bool wave_inside = tw + WROWS <= T && m0 + wr * WROWS + WROWS <= M;
+  // LDS fragment-read bases: a 16-row step keeps (row & 7), so the swizzle is the same for
+  // every mi / ni block and the block offset is an immediate.
+  const int arow0 = wr * WROWS + (lane & 15);
+  const int bread0 = lds_off(wc * 64 + (lane & 15), lane >> 4);
+  const int bread1 = lds_off(wc * 64 + (lane & 15), 4 + (lane >> 4));
 
-  Stage<CT, TIn> sa[A_CH];
-  Stage<CT, TW> sb[B_CH];
+  Stage<CT, TIn> sa[A_CH];        // A halo of the next channel block (issued at its tap 0)
+  Stage<CT, TW> sb0[B_CH], sb1[B_CH];  // 2-deep ring of B (weight) tiles: step k lives in sb[k & 1]
 
-  auto gload = [&](int ks) {
-    const int tap = ks / nCk;
-    const int cb = ks - tap * nCk;
+  auto gload_a = [&](int cb) {
     const int ch = cb * KE + schunk * CE;
-    const int sh = tap - a.pad;
     const bool ch_ok = ch < a.Cin;
 #pragma unroll
     for (int j = 0; j < A_CH; ++j) {
-      const int ts = a_t[j] + sh;
-      if (a_ok[j] && ch_ok && ts >= 0 && ts < T)
-        sa[j].load(x + (int64_t)(a_m[j] + sh) * a.xs + ch);
-      else
-        sa[j].zero();
-    }
-#pragma unroll
-    for (int j = 0; j < B_CH; ++j) {
-      if (b_ok[j])
-        sb[j].load(wp[j] + (int64_t)ks * KE);
-      else
-        sb[j].zero();
+      const int h = srow + 32 * j;
+      const int gm = m0 - pad + h;
+      const bool ok = h < H && ch_ok && gm >= 0 && gm < M;
+      sa[j].load(xr, ok ? ((uint32_t)gm * (uint32_t)a.xs + (uint32_t)ch) * (uint32_t)sizeof(TIn) : kOOB);
     }
   };
-  auto lstore = [&](int buf) {
-    char *As = smem + buf * STAGE_BYTES;
-    char *Bs = As + BM * kRowBytes;
+  auto gload_b = [&](Stage<CT, TW>(&sb)[B_CH], int cb, int tap) {
+    const uint32_t off = ((uint32_t)tap * a.Cin_pad + cb * KE) * (uint32_t)sizeof(TW);
 #pragma unroll
-    for (int j = 0; j < A_CH; ++j) *reinterpret_cast<uint4 *>(As + lds_off(srow + 32 * j, schunk)) = sa[j].chunk();
+    for (int j = 0; j < B_CH; ++j) sb[j].load(wr_, wofs[j] == kOOB ? kOOB : wofs[j] + off);
+  };
+  auto lstore_a = [&](int buf) {
+    char *As = Abuf + buf * A_BYTES;
+#pragma unroll
+    for (int j = 0; j < A_CH; ++j) {
+      const int h = srow + 32 * j;
+      if (h < HMAX) *reinterpret_cast<uint4 *>(As + lds_off(h, schunk)) = sa[j].chunk();
+    }
+  };
+  auto lstore_b = [&](Stage<CT, TW>(&sb)[B_CH], int buf) {
+    char *Bs = Bbuf + buf * B_BYTES;
 #pragma unroll
     for (int j = 0; j < B_CH; ++j) *reinterpret_cast<uint4 *>(Bs + lds_off(srow + 32 * j, schunk)) = sb[j].chunk();
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[WMI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < WMI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int ks = 0; ks < nK; ++ks) {
-    const int cur = ks & 1;
-    if (ks + 1 < nK) gload(ks + 1);
-    const char *As = smem + cur * STAGE_BYTES;
-    const char *Bs = As + BM * kRowBytes;
+  auto compute = [&](int cb, int tap, int ks) {
+    const char *As = Abuf + (cb & 1) * A_BYTES;
+    const char *Bs = Bbuf + (ks & 1) * B_BYTES;
+    const int sh = tap - pad;
+    const bool need_mask = !(wave_inside && tw + sh >= 0 && tw + WROWS - 1 + sh < T);
+    bool vrow[WMI];
+#pragma unroll
+    for (int mi = 0; mi < WMI; ++mi) vrow[mi] = (unsigned)(tpos[mi] + sh) < (unsigned)T;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int ch = s * 4 + (lane >> 4);
+      const char *Ab = As + lds_off(arow0 + tap, s * 4 + (lane >> 4));
+      const char *Bb = Bs + (s ? bread1 : bread0);
       if constexpr (CT == FS2_BF16) {
-        bf16x8 af[4], bfr[4];
+        bf16x8 af[WMI], bfr[4];
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-          af[mi] = *reinterpret_cast<const bf16x8 *>(As + lds_off(wr * 64 + mi * 16 + (lane & 15), ch));
+        for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const bf16x8 *>(Ab + mi * 16 * kRowBytes);
+        if (need_mask) {
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          bfr[ni] = *reinterpret_cast<const bf16x8 *>(Bs + lds_off(wc * 64 + ni * 16 + (lane & 15), ch));
+          for (int mi = 0; mi < WMI; ++mi)
+            if (!vrow[mi]) af[mi] = bf16x8{};
+        }
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+        for (int ni = 0; ni < 4; ++ni) bfr[ni] = *reinterpret_cast<const bf16x8 *>(Bb + ni * 16 * kRowBytes);
+#pragma unroll
+        for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
           for (int ni = 0; ni < 4; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
       } else {
-        f32x4 af[4], bfr[4];
+        f32x4 af[WMI], bfr[4];
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-          af[mi] = *reinterpret_cast<const f32x4 *>(As + lds_off(wr * 64 + mi * 16 + (lane & 15), ch));
+        for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const f32x4 *>(Ab + mi * 16 * kRowBytes);
+        if (need_mask) {
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          bfr[ni] = *reinterpret_cast<const f32x4 *>(Bs + lds_off(wc * 64 + ni * 16 + (lane & 15), ch));
+          for (int mi = 0; mi < WMI; ++mi)
+            if (!vrow[mi]) af[mi] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) bfr[ni] = *reinterpret_cast<const f32x4 *>(Bb + ni * 16 * kRowBytes);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int mi = 0; mi < 4; ++mi)
+          for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni)
               acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi][j], bfr[ni][j], acc[mi][ni], 0, 0, 0);
       }
     }
-    if (ks + 1 < nK) lstore(cur ^ 1);
+  };
+
+  if constexpr (GL) {
+    // ---- LDS-DMA staging: buffer_load_dwordx4 ... lds, one 1 KiB piece (8 rows x 128 B) per
+    // wave-instruction. The LDS image is lane-linear (row 8p + lane/8, physical chunk lane&7);
+    // lane l therefore fetches the LOGICAL chunk (lane&7) ^ (row&7), i.e. the XOR swizzle is
+    // applied on the source address and the reads use the same lds_off(). OOB offsets land zeros.
+    constexpr int AP = HMAX / 8, BP = BN / 8;  // pieces per stage
+    const int prow = lane >> 3, plc = (lane & 7) ^ ((lane >> 3) & 7);
+    auto glds = [&](rsrc_t rs, char *dst, uint32_t off) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)dst, 16, off, 0, 0, 0);
+    };
+    auto dma_a = [&](int cb, int buf) {
+      const int ch = cb * KE + plc * CE;
+      const bool ch_ok = ch < a.Cin;
+      char *As = Abuf + buf * A_BYTES;
+#pragma unroll
+      for (int it = 0; it < (AP + 3) / 4; ++it) {
+        const int p = wid + 4 * it;
+        if (p < AP) {
+          const int h = 8 * p + prow;
+          const int gm = m0 - pad + h;
+          const bool ok = h < H && ch_ok && gm >= 0 && gm < M;
+          glds(xr, As + p * 1024, ok ? ((uint32_t)gm * (uint32_t)a.xs + (uint32_t)ch) * (uint32_t)sizeof(TIn) : kOOB);
+        }
+      }
+    };
+    const uint32_t bcol = (uint32_t)(plc * CE) * (uint32_t)sizeof(TW);
+    auto dma_b = [&](int cb, int tap, int buf) {
+      const uint32_t off = ((uint32_t)tap * a.Cin_pad + cb * KE) * (uint32_t)sizeof(TW) + bcol;
+      char *Bs = Bbuf + buf * B_BYTES;
+#pragma unroll
+      for (int it = 0; it < BP / 4; ++it) {
+        const int p = wid + 4 * it;
+        const int n = n0 + 8 * p + prow;
+        glds(wr_, Bs + p * 1024, n < a.N ? (uint32_t)n * wrow + off : kOOB);
+      }
+    };
+    int cb = 0, tap = 0;
+    dma_a(0, 0);
+    dma_b(0, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int ks = 0; ks < nK; ++ks) {
+      const bool last_tap = tap == KS - 1;
+      const int ncb = last_tap ? cb + 1 : cb, ntap = last_tap ? 0 : tap + 1;
+      if (ks + 1 < nK) {
+        dma_b(ncb, ntap, (ks + 1) & 1);
+        if (last_tap) dma_a(ncb, ncb & 1);
+      }
+      compute(cb, tap, ks);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      cb = ncb;
+      tap = ntap;
+    }
+  } else {
+  // (cb, tap) of step k + 2 tracked incrementally
+    int cb = 0, tap = 0;
+    int cb2 = (KS > 2) ? 0 : (2 / KS), tap2 = 2 % KS;
+    gload_a(0);
+    gload_b(sb0, 0, 0);
+    if (nK > 1) gload_b(sb1, 1 / KS, 1 % KS);
+    lstore_a(0);
+    lstore_b(sb0, 0);
+    __syncthreads();
+
+    // One pipeline step. Step k's B tile sits in LDS buffer k&1; sb_this (its register set) is
+    // free and receives step k+2; sb_next holds step k+1 and is written to LDS after the MFMAs.
+    auto step = [&](int ks, Stage<CT, TW>(&sb_this)[B_CH], Stage<CT, TW>(&sb_next)[B_CH]) {
+      const bool last_tap = tap == KS - 1;
+      if (ks + 2 < nK) gload_b(sb_this, cb2, tap2);
+      if (tap == 0 && cb + 1 < nCk) gload_a(cb + 1);
+      compute(cb, tap, ks);
+      if (ks + 1 < nK) lstore_b(sb_next, (ks + 1) & 1);
+      if (last_tap && cb + 1 < nCk) lstore_a((cb + 1) & 1);
+      __syncthreads();
+      if (last_tap) {
+        ++cb;
+        tap = 0;
+      } else {
+        ++tap;
+      }
+      if (++tap2 == KS) {
+        tap2 = 0;
+        ++cb2;
+      }
+    };
+    for (int ks = 0; ks < nK; ks += 2) {
+      step(ks, sb0, sb1);
+      if (ks + 1 < nK) step(ks + 1, sb1, sb0);
+    }
+
   }
 
   // ---- epilogue: accumulator tile -> LDS (f32, row-major, padded rows) -------------------------
   float *E = reinterpret_cast<float *>(smem);
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+  for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        E[(wr * 64 + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
+        E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
   __syncthreads();
 
   const int epi = a.epi;
@@ -364,11 +506,35 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
   }
 }
 
-template <int CT, int WGM, int WGN, typename TIn>
-void launch(const ConvArgs &a, hipStream_t s) {
-  constexpr int BM = 64 * WGM, BN = 64 * WGN;
-  dim3 grid((a.M + BM - 1) / BM, (a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, TIn>), grid, dim3(256), 0, s, a);
+template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn>
+void launch(ConvArgs a, hipStream_t s) {
+  constexpr int BM = 16 * WMI * WGM, BN = 64 * WGN;
+  constexpr bool GL = std::is_same<TIn, typename CTraits<CT>::T>::value;  // LDS-DMA needs no conversion
+  a.ntn = (a.N + BN - 1) / BN;
+  const int nwg = ((a.M + BM - 1) / BM) * a.ntn;
+  hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, WMI, KSMAX, TIn, GL>), dim3(nwg), dim3(256), 0, s, a);
+}
+
+// Row-tile choice: the largest tile that still gives >= 2 workgroups per CU (256 CUs), so the
+// small-M launches (encoder / variance predictors, M = B*L ~ 4k) fill the chip.
+constexpr int kTargetWGs = 512;
+
+template <int CT, typename TIn>
+void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
+  if (ln) {  // 256-wide rows for the LayerNorm epilogues; WMI <= 2 keeps 2 workgroups / CU in LDS
+    if ((int64_t)((a.M + 31) / 32) >= kTargetWGs)
+      launch<CT, 1, 4, 2, 3, TIn>(a, s);
+    else
+      launch<CT, 1, 4, 1, 3, TIn>(a, s);
+  } else {
+    const int ntn = (a.N + 127) / 128;
+    if ((int64_t)((a.M + 127) / 128) * ntn >= kTargetWGs)
+      launch<CT, 2, 2, 4, 9, TIn>(a, s);
+    else if ((int64_t)((a.M + 63) / 64) * ntn >= kTargetWGs)
+      launch<CT, 2, 2, 2, 9, TIn>(a, s);
+    else
+      launch<CT, 2, 2, 1, 9, TIn>(a, s);
+  }
 }
 
 }  // namespace
@@ -426,21 +592,23 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.out = d->out;
   a.out_dt = d->out_dtype;
   a.os = d->out_row_stride;
+  {
+    const int xes = d->x_dtype == FS2_BF16 ? 2 : 4, wes = d->compute == FS2_BF16 ? 2 : 4;
+    const int64_t xb = M64 * d->x_row_stride * xes;
+    const int64_t wb = (int64_t)d->N * d->KS * d->Cin_pad * wes;
+    if (xb >= (1LL << 31) || wb >= (1LL << 31)) return FS2_EUNSUPPORTED;  // 31-bit buffer offsets
+    a.x_bytes = (uint32_t)xb;
+    a.w_bytes = (uint32_t)wb;
+  }
 
   hipStream_t s = as_stream(stream);
-  const bool xb = d->x_dtype == FS2_BF16;
   if (d->x_dtype != FS2_BF16 && d->x_dtype != FS2_F32) return FS2_EUNSUPPORTED;
-  if (d->compute == FS2_BF16) {
-    if (ln)
-      xb ? launch<FS2_BF16, 1, 4, bf16>(a, s) : launch<FS2_BF16, 1, 4, float>(a, s);
-    else
-      xb ? launch<FS2_BF16, 2, 2, bf16>(a, s) : launch<FS2_BF16, 2, 2, float>(a, s);
-  } else {
-    if (ln)
-      xb ? launch<FS2_F32, 1, 4, bf16>(a, s) : launch<FS2_F32, 1, 4, float>(a, s);
-    else
-      xb ? launch<FS2_F32, 2, 2, bf16>(a, s) : launch<FS2_F32, 2, 2, float>(a, s);
-  }
+  if (d->KS > (ln ? 3 : 9)) return FS2_EUNSUPPORTED;
+  const bool xb = d->x_dtype == FS2_BF16;
+  if (d->compute == FS2_BF16)
+    xb ? dispatch<FS2_BF16, bf16>(a, ln, s) : dispatch<FS2_BF16, float>(a, ln, s);
+  else
+    xb ? dispatch<FS2_F32, bf16>(a, ln, s) : dispatch<FS2_F32, float>(a, ln, s);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Launch ONE hot-path kernel repeatedly at the bench's cfg2 shapes (for rocprofv3 PMC passes).
+
+    python tools/kernel_probe.py conv9 --reps 20
+kernels: conv9 (decoder FFN Conv1d k=9 256->1024), conv1 (FFN k=1 1024->256 + res + LN),
+qkv, attn, lr (LengthRegulator gather + PE), postnet (512->512 k=5 + tanh).
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "expressive-fastspeech2-mandarin_amd"))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("kernel")
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--time", action="store_true", help="print mean duration (HIP events) instead of profiling")
+    a = ap.parse_args()
+    import bench
+    from fs2amd import _lib as L, ops
+    from fs2amd.data import synth_batch, to_device
+
+    dev = torch.device("cuda:0")
+    model, _, _ = bench.build_model(dev, a.dtype)
+    P = model.packed(dev)
+    bc = synth_batch(64, 64, seed=1)
+    b = to_device(bc, dev)
+    B, T = 64, int(bc["max_mel_len"])
+    dt = ops.torch_dtype(P.act_dtype)
+    lp = P.dec_layers[0]
+    g = torch.Generator().manual_seed(0)
+    rnd = lambda *s: torch.randn(*s, generator=g).to(dev, dt)
+    lens = b["mel_lens"]
+    if a.kernel == "conv9":
+        h = rnd(B, T, 256)
+        fn = lambda: ops.conv1d(h, lp.w1, lp.b1, cin=256, ks=9, pad=4, compute=P.compute, epilogue=L.EPI_BIAS_RELU,
+                                out_dtype=P.act_dtype)
+    elif a.kernel == "conv1":
+        f, h = rnd(B, T, 1024), rnd(B, T, 256)
+        fn = lambda: ops.conv1d(f, lp.w2, lp.b2, cin=1024, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_RES_LN,
+                                out_dtype=P.act_dtype, residual=h, ln=lp.ln2, lens=lens)
+    elif a.kernel == "qkv":
+        h = rnd(B, T, 256)
+        fn = lambda: ops.conv1d(h, lp.wqkv, lp.bqkv, cin=256, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
+                                out_dtype=P.act_dtype)
+    elif a.kernel == "attn":
+        qkv = rnd(B, T, 768)
+        fn = lambda: ops.attention(qkv, lens, 2, 128, 128 ** 0.5)
+    elif a.kernel == "lr":
+        x = rnd(B, 64, 256)
+        cum, ml, _ = ops.lr_durations(b["d_targets"])
+        fn = lambda: ops.lr_expand(x, cum, ml, T, pe=P.dec_pe, out_dtype=P.act_dtype)
+    elif a.kernel == "postnet":
+        y = rnd(B, T, 512)
+        pl = P.postnet[1]
+        fn = lambda: ops.conv1d(y, pl.w, pl.b, cin=512, ks=5, pad=2, compute=P.compute, epilogue=L.EPI_BIAS_TANH,
+                                out_dtype=P.act_dtype)
+    elif a.kernel in ("enc_conv9", "enc_ln", "vp"):
+        Be, Le = 64, 64
+        xe = rnd(Be, Le, 256)
+        le = b["src_lens"]
+        el = P.enc_layers[0]
+        if a.kernel == "enc_conv9":
+            fn = lambda: ops.conv1d(xe, el.w1, el.b1, cin=256, ks=9, pad=4, compute=P.compute,
+                                    epilogue=L.EPI_BIAS_RELU, out_dtype=P.act_dtype)
+        elif a.kernel == "enc_ln":
+            fe = rnd(Be, Le, 1024)
+            fn = lambda: ops.conv1d(fe, el.w2, el.b2, cin=1024, ks=1, pad=0, compute=P.compute,
+                                    epilogue=L.EPI_RES_LN, out_dtype=P.act_dtype, residual=xe, ln=el.ln2, lens=le)
+        else:
+            from fs2amd.runtime import variance_predictor
+            fn = lambda: variance_predictor(P.vp["pitch"], xe, le)
+    else:
+        raise SystemExit(f"unknown kernel {a.kernel}")
+    if a.time:
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        print(f"{a.kernel}: {e0.elapsed_time(e1) * 1e3 / a.reps:.2f} us/launch")
+        return
+    for _ in range(a.reps):
+        fn()
+    torch.cuda.synchronize()
+    print("probe done", a.kernel, a.reps)
+
+
+if __name__ == "__main__":
+    main()
