@@ -31,7 +31,6 @@ sys.path.insert(0, os.path.join(REPO, "expressive-fastspeech2-mandarin_amd"))
 sys.path.insert(0, REPO)
 
 import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 HOP, SR = 256, 22050
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
@@ -66,8 +65,23 @@ def build_model(device, dtype):
     return model, pc, mc
 
 
+def time_kernel_in_forward(model, batch, n_fwd=3):
+    """Mean duration of the decoder FFN conv-k9 GEMM launches inside real (eager) forwards:
+    HIP events recorded around each launch on its stream (fs2amd.runtime.TIMERS)."""
+    from fs2amd import runtime
+
+    runtime.TIMERS = []
+    with torch.no_grad():
+        for _ in range(n_fwd):
+            model(**batch)
+    torch.cuda.synchronize()
+    ts = [a.elapsed_time(b) / 1e3 for a, b in runtime.TIMERS]
+    runtime.TIMERS = None
+    return sum(ts) / len(ts), len(ts)
+
+
 def time_dominant_kernel(model, batch, device, reps):
-    """Mean duration of the decoder FFN conv-k9 GEMM (HIP events on its launch stream)."""
+    """Mean duration of the decoder FFN conv-k9 GEMM run standalone on random data."""
     from fs2amd import _lib as L
     from fs2amd import ops
 
@@ -139,13 +153,9 @@ def load_traffic():
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
-    device = torch.device(f"cuda:{local}")
+    from fs2amd import parallel
+
+    rank, local, world, device = parallel.init("nccl")
 
     from fs2amd.data import synth_batch, to_device
 
@@ -176,27 +186,18 @@ def main():
         torch.cuda.synchronize(device)
 
     run = graph.replay if graph is not None else step
-    if world > 1:
-        dist.barrier()
+    parallel.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
     torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
+    parallel.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed, tot_frames = parallel.aggregate(elapsed, frames, device)
 
-    tot_frames = frames
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        f = torch.tensor([frames], device=device, dtype=torch.float64)
-        dist.all_reduce(f, op=dist.ReduceOp.SUM)
-        tot_frames = int(f.item())
-
-    kernel_s, kernel_flops = time_dominant_kernel(model, batch_cpu, device, args.kernel_reps)
+    kernel_s, n_launch = time_kernel_in_forward(model, batch)
+    standalone_s, kernel_flops = time_dominant_kernel(model, batch_cpu, device, args.kernel_reps)
     ms_per_step = elapsed / args.steps * 1e3
     value = tot_frames * args.steps / elapsed
     peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
@@ -225,14 +226,17 @@ def main():
         "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel<bf16,2,2> (decoder FFN Conv1d k=9, 256->1024)",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": load_traffic(),
-                     "kernel_ms": round(kernel_s * 1e3, 4), "flops_per_launch": kernel_flops},
+                     "kernel_ms": round(kernel_s * 1e3, 4), "launches_timed": n_launch,
+                     "timing": "HIP events around each decoder conv-k9 launch in 3 eager forwards",
+                     "kernel_ms_standalone_random": round(standalone_s * 1e3, 4),
+                     "flops_per_launch": kernel_flops,
+                     "traffic_note": "2*FETCH_SIZE + WRITE_SIZE per launch (rocprofv3 PMC, profiles/conv9_traffic.json)"},
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(batch_cpu, pc, mc)
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    parallel.shutdown()
 
 
 if __name__ == "__main__":

@@ -45,7 +45,12 @@ def _pe(P, which, n):
     return getattr(P, key)
 
 
-def fft_block(P, lp, x, lens, addvec1=None, addvec2=None):
+# Optional measurement hook: when a list, the decoder's FFN conv-k9 launches are bracketed by
+# HIP events on the launch stream (bench.py's live roofline timing of the dominant kernel).
+TIMERS = None
+
+
+def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False):
     """One FFT block (transformer/Layers.py:21-30) = 5 launches."""
     c = P.compute
     dt = P.act_dtype
@@ -55,7 +60,13 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None):
     att = ops.attention(qkv, lens, H, dk, float(np.power(dk, 0.5)))
     h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
                    residual=x, ln=lp.ln1, lens=lens)
+    if timed and TIMERS is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
     f = ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=c, epilogue=L.EPI_BIAS_RELU, out_dtype=dt)
+    if timed and TIMERS is not None:
+        e1.record()
+        TIMERS.append((e0, e1))
     return ops.conv1d(f, lp.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
                       residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2)
 
@@ -166,7 +177,7 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
 
     # ---- decoder --------------------------------------------------------------------------------
     for lp in P.dec_layers:
-        x = fft_block(P, lp, x, dec_lens)
+        x = fft_block(P, lp, x, dec_lens, timed=True)
 
     # ---- mel_linear + PostNet (+ residual) -----------------------------------------------------
     mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
