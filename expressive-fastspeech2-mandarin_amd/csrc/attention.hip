@@ -222,6 +222,171 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const typename ATraits<CT>
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// bf16 fast path. Same math, different data flow:
+//   S^T = K Q^T   (A = K rows from LDS, B = Q fragments in registers): the accumulator holds,
+//                 per lane, 16 scores of ONE query (column l&15) -> the softmax row statistics
+//                 are per lane, reduced across the 4 lanes of that query with 2 xor-shuffles.
+//   O^T = V^T P^T (A = V^T from LDS with ds_read_b64_tr_b16 on the row-major V tile, B = P
+//                 straight from the S^T registers): no P round trip through LDS, no transposing
+//                 V writes. The k order inside each 32-key MFMA step is permuted identically on
+//                 both operands (lane group g takes keys 4g..4g+3 and 16+4g..16+4g+3).
+// K and V tiles arrive by LDS-DMA (buffer_load ... lds, OOB rows -> zeros) into a dual-use XOR
+// image (row reads and transposed reads conflict-light), double buffered. Workgroups of one
+// (utterance, head) are placed on one XCD so its K/V stay in that XCD's L2.
+__device__ __forceinline__ int kv_off(int row, int chunk) {
+  return row * 256 + ((chunk ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restrict__ qkv, int64_t qs, uint32_t qkv_bytes,
+                                                           const int64_t *__restrict__ lens, int B, int T, int H,
+                                                           int nqt, float scale_log2, bf16 *__restrict__ out,
+                                                           int64_t os) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * KT * 256];  // K0 V0 K1 V1
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+
+  const int nwg = gridDim.x, id = blockIdx.x;
+  const int q8 = nwg >> 3, rem = nwg & 7, xcd = id & 7;
+  const int t = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (id >> 3);
+  const int qt = t % nqt, bh = t / nqt, h = bh % H, b = bh / H;
+  const int q0 = qt * QT;
+  int64_t len64 = lens[b];
+  const int len = (int)(len64 < 0 ? 0 : (len64 > T ? T : len64));
+
+  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16 *>(qkv), (short)0, (int)qkv_bytes, 0x00020000);
+  const uint32_t row_bytes = (uint32_t)qs * 2u;
+  const uint32_t seq_base = (uint32_t)b * (uint32_t)T;
+
+  // Q^T fragments (B operand): query q0 + 16w + li, head dims 32s + 8g .. +7
+  const int qrow = q0 + 16 * w + li;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const uint32_t off = qrow < T ? (seq_base + qrow) * row_bytes + (uint32_t)(h * DK + 32 * s + 8 * g) * 2u : 0x80000000u;
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    qf[s] = *reinterpret_cast<bf16x8 *>(&v);
+  }
+
+  // LDS-DMA of one 64-key tile: 16 pieces of 4 rows x 256 B for K, 16 for V; 8 per wave.
+  const int prow = lane >> 4, pch = lane & 15;
+  auto dma = [&](int k0, int buf) {
+    char *Kb = smem + buf * 2 * KT * 256;
+    char *Vb = Kb + KT * 256;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int p = w + 4 * it;
+      const int r = 4 * p + prow;
+      const int lc = pch ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      const int key = k0 + r;
+      const uint32_t base = key < T ? (seq_base + key) * row_bytes + (uint32_t)lc * 16u : 0x80000000u;
+      const uint32_t koff = base == 0x80000000u ? base : base + (uint32_t)((H + h) * DK) * 2u;
+      const uint32_t voff = base == 0x80000000u ? base : base + (uint32_t)((2 * H + h) * DK) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(Kb + p * 1024), 16, koff,
+                                               0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(Vb + p * 1024), 16, voff,
+                                               0, 0, 0);
+    }
+  };
+
+  f32x4 oacc[DK / 16];
+#pragma unroll
+  for (int i = 0; i < DK / 16; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int ntiles = (len + KT - 1) / KT;
+  if (ntiles > 0) dma(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // transposed-read lane roles: lane 4q+p of its 16-lane group addresses row q, columns 4p..4p+3
+  const int tq = li >> 2, tp = li & 3;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int k0 = kt * KT;
+    if (kt + 1 < ntiles) dma(k0 + KT, (kt + 1) & 1);
+    const char *Kb = smem + (kt & 1) * 2 * KT * 256;
+    const char *Vb = Kb + KT * 256;
+
+    f32x4 sacc[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      sacc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(Kb + kv_off(ni * 16 + li, 4 * s + g));
+        sacc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], sacc[ni], 0, 0, 0);
+      }
+    }
+    // scores of query li: keys k0 + ni*16 + 4g + j
+    float mx = -INFINITY;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = k0 + ni * 16 + 4 * g + j;
+        const float sv = key < len ? sacc[ni][j] * scale_log2 : -INFINITY;
+        sacc[ni][j] = sv;
+        mx = fmaxf(mx, sv);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float sum = 0.f;
+    bf16x8 pf[2];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = exp2f(sacc[ni][j] - m_new);
+        sum += p;
+        pf[ni >> 1][(ni & 1) * 4 + j] = (bf16)p;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    l_run = l_run * alpha + sum;
+#pragma unroll
+    for (int nd = 0; nd < DK / 16; ++nd) oacc[nd] *= alpha;
+
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r0 = 32 * s2 + 4 * g + tq;  // this lane's address row (block 1), +16 for block 2
+#pragma unroll
+      for (int nd = 0; nd < DK / 16; ++nd) {
+        const int ch = nd * 2 + (tp >> 1), sub = (tp & 1) * 8;
+        auto lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4 *)(Vb + kv_off(r0, ch) + sub));
+        auto hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4 *)(Vb + kv_off(r0 + 16, ch) + sub));
+        bf16x8 vf;
+        __builtin_memcpy(&vf, &lo, 8);
+        __builtin_memcpy(reinterpret_cast<char *>(&vf) + 8, &hi, 8);
+        oacc[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[s2], oacc[nd], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // O^T[d = nd*16 + 4g + j][query li]
+  const int q = q0 + 16 * w + li;
+  if (q < T) {
+    const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
+    bf16 *orow = out + ((int64_t)b * T + q) * os + h * DK + 4 * g;
+#pragma unroll
+    for (int nd = 0; nd < DK / 16; ++nd) {
+      bf16x4 o = {(bf16)(oacc[nd][0] * inv), (bf16)(oacc[nd][1] * inv), (bf16)(oacc[nd][2] * inv),
+                  (bf16)(oacc[nd][3] * inv)};
+      *reinterpret_cast<bf16x4 *>(orow + nd * 16) = o;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
@@ -235,10 +400,14 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
   const float scale_log2 = 1.4426950408889634f / temperature;
   dim3 grid((T + QT - 1) / QT, H, B);
   hipStream_t s = as_stream(stream);
-  if (dtype == FS2_BF16)
-    hipLaunchKernelGGL(attn_kernel<FS2_BF16>, grid, dim3(256), 0, s, reinterpret_cast<const bf16 *>(qkv),
-                       qkv_row_stride, key_lens, T, H, scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride);
-  else if (dtype == FS2_F32)
+  if (dtype == FS2_BF16) {
+    const int64_t bytes = (int64_t)B * T * qkv_row_stride * 2;
+    if (bytes >= (1LL << 31) || (out_row_stride & 3)) return FS2_EUNSUPPORTED;
+    const int nqt = (T + QT - 1) / QT;
+    hipLaunchKernelGGL(attn_bf16_kernel, dim3(nqt * H * B), dim3(256), 0, s, reinterpret_cast<const bf16 *>(qkv),
+                       qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt, scale_log2,
+                       reinterpret_cast<bf16 *>(out), out_row_stride);
+  } else if (dtype == FS2_F32)
     hipLaunchKernelGGL(attn_kernel<FS2_F32>, grid, dim3(256), 0, s, reinterpret_cast<const float *>(qkv),
                        qkv_row_stride, key_lens, T, H, scale_log2, reinterpret_cast<float *>(out), out_row_stride);
   else
