@@ -145,18 +145,126 @@ __device__ __forceinline__ void store_any4(void *p, int dt, int64_t off, const f
     store4(reinterpret_cast<float *>(p) + off, v);
 }
 
+// Epilogue of one BM x BN tile whose f32 accumulators sit in LDS (E, row stride BN + 4).
+template <int BM, int BN, int NWAVES>
+__device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int m0, int n0, int tid) {
+  constexpr int EPI_LD = BN + 4;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int T = a.T, M = a.M;
+  const int epi = a.epi;
+  if (epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN || epi == FS2_EPI_RELU_LN_DOT) {
+    // one wave per row; N == BN == 256 (checked on the host), lane owns columns 4*lane..4*lane+3
+    const int n = lane * 4;
+    float bias4[4], g4[4], be4[4];
+    load4(a.gamma + n, g4);
+    load4(a.beta + n, be4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bias4[q] = a.bias[n + q];
+    const float inv_n = 1.0f / (float)a.N;
+    for (int r = wid; r < BM; r += NWAVES) {
+      const int m = m0 + r;
+      if (m >= M) break;
+      float v[4];
+      load4(E + r * EPI_LD + n, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += bias4[q];
+      if (epi == FS2_EPI_RES_LN) {
+        float rv[4];
+        load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n, rv);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += rv[q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.0f);
+      }
+      const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * inv_n;
+      float d[4], ss = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        d[q] = v[q] - mean;
+        ss += d[q] * d[q];
+      }
+      const float var = wave_sum(ss) * inv_n;
+      const float rstd = 1.0f / sqrtf(var + a.eps);
+      float y[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y[q] = d[q] * rstd * g4[q] + be4[q];
+      const int bb = m / T;
+      const int t = m - bb * T;
+      const bool masked = (a.lens != nullptr) && ((int64_t)t >= a.lens[bb]);
+      if (epi == FS2_EPI_RELU_LN_DOT) {
+        float dw4[4];
+        load4(a.dw + n, dw4);
+        const float s = wave_sum(y[0] * dw4[0] + y[1] * dw4[1] + y[2] * dw4[2] + y[3] * dw4[3]) + a.db;
+        if (lane == 0) reinterpret_cast<float *>(a.out)[m] = masked ? 0.0f : s;
+        continue;
+      }
+      if (epi == FS2_EPI_RES_LN) {
+        if (masked) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) y[q] = 0.0f;
+        }
+        if (a.av1 != nullptr) {
+          float av[4];
+          load4(a.av1 + (int64_t)bb * a.N + n, av);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) y[q] += av[q];
+        }
+        if (a.av2 != nullptr) {
+          float av[4];
+          load4(a.av2 + (int64_t)bb * a.N + n, av);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) y[q] += av[q];
+        }
+      }
+      store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, y);
+    }
+    return;
+  }
+
+  constexpr int G = BN / 4;
+  for (int e = tid; e < BM * G; e += 64 * NWAVES) {
+    const int r = e / G;
+    const int cg = e - r * G;
+    const int m = m0 + r;
+    const int n = n0 + cg * 4;
+    if (m >= M || n >= a.N) continue;
+    float v[4];
+    load4(E + r * EPI_LD + cg * 4, v);
+    if (a.bias != nullptr) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += a.bias[n + q];
+    }
+    if (epi == FS2_EPI_BIAS_RELU) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.0f);
+    } else if (epi == FS2_EPI_BIAS_TANH) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
+    } else if (epi == FS2_EPI_BIAS_RES) {
+      float rv[4];
+      load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n, rv);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += rv[q];
+    }
+    store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, v);
+  }
+}
+
 // Tile (WGM x WGN waves, each wave WMI x 4 MFMA 16x16 blocks):  BM = 16*WMI*WGM, BN = 64*WGN.
 // KSMAX bounds the conv taps the LDS halo is sized for.
 template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, bool GL>
-__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
+__global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv_gemm_kernel(ConvArgs a) {
+  constexpr int NW = WGM * WGN, NT = 64 * NW;  // waves / threads per workgroup (4 or 8)
   constexpr int WROWS = 16 * WMI;
   constexpr int BM = WROWS * WGM, BN = 64 * WGN;
   constexpr int KE = CTraits<CT>::KE, CE = CTraits<CT>::CE;
   using TW = typename CTraits<CT>::T;
   constexpr int HMAX0 = BM + KSMAX - 1;
   constexpr int HMAX = GL ? (HMAX0 + 7) / 8 * 8 : HMAX0;  // halo rows of one A stage (whole 1 KiB pieces)
-  constexpr int A_CH = (HMAX * 8 + 255) / 256;         // 16-byte chunks per thread (A halo)
-  constexpr int B_CH = BN * 8 / 256;
+  constexpr int A_CH = (HMAX * 8 + NT - 1) / NT;       // 16-byte chunks per thread (A halo)
+  constexpr int B_CH = BN * 8 / NT;
+  constexpr int RPP = NT / 8;                           // staged rows per pass
   constexpr int A_BYTES = HMAX * kRowBytes, B_BYTES = BN * kRowBytes;
   constexpr int STAGE = 2 * (A_BYTES + B_BYTES);
   constexpr int EPI_LD = BN + 4;
@@ -193,7 +301,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
   const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * (uint32_t)sizeof(TW);
 #pragma unroll
   for (int j = 0; j < B_CH; ++j) {
-    const int n = n0 + srow + 32 * j;
+    const int n = n0 + srow + RPP * j;
     wofs[j] = n < a.N ? (uint32_t)n * wrow + schunk * 16u : kOOB;
   }
   // sequence position of this lane's A fragment rows (tap validity)
@@ -221,7 +329,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
     const bool ch_ok = ch < a.Cin;
 #pragma unroll
     for (int j = 0; j < A_CH; ++j) {
-      const int h = srow + 32 * j;
+      const int h = srow + RPP * j;
       const int gm = m0 - pad + h;
       const bool ok = h < H && ch_ok && gm >= 0 && gm < M;
       sa[j].load(xr, ok ? ((uint32_t)gm * (uint32_t)a.xs + (uint32_t)ch) * (uint32_t)sizeof(TIn) : kOOB);
@@ -236,14 +344,14 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
     char *As = Abuf + buf * A_BYTES;
 #pragma unroll
     for (int j = 0; j < A_CH; ++j) {
-      const int h = srow + 32 * j;
+      const int h = srow + RPP * j;
       if (h < HMAX) *reinterpret_cast<uint4 *>(As + lds_off(h, schunk)) = sa[j].chunk();
     }
   };
   auto lstore_b = [&](Stage<CT, TW>(&sb)[B_CH], int buf) {
     char *Bs = Bbuf + buf * B_BYTES;
 #pragma unroll
-    for (int j = 0; j < B_CH; ++j) *reinterpret_cast<uint4 *>(Bs + lds_off(srow + 32 * j, schunk)) = sb[j].chunk();
+    for (int j = 0; j < B_CH; ++j) *reinterpret_cast<uint4 *>(Bs + lds_off(srow + RPP * j, schunk)) = sb[j].chunk();
   };
 
   f32x4 acc[WMI][4];
@@ -252,9 +360,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int cb, int tap, int ks) {
-    const char *As = Abuf + (cb & 1) * A_BYTES;
-    const char *Bs = Bbuf + (ks & 1) * B_BYTES;
+  auto compute = [&](int aslot, int tap, const char *Bs) {
+    const char *As = Abuf + aslot * A_BYTES;
     const int sh = tap - pad;
     const bool need_mask = !(wave_inside && tw + sh >= 0 && tw + WROWS - 1 + sh < T);
     bool vrow[WMI];
@@ -317,8 +424,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
       const bool ch_ok = ch < a.Cin;
       char *As = Abuf + buf * A_BYTES;
 #pragma unroll
-      for (int it = 0; it < (AP + 3) / 4; ++it) {
-        const int p = wid + 4 * it;
+      for (int it = 0; it < (AP + NW - 1) / NW; ++it) {
+        const int p = wid + NW * it;
         if (p < AP) {
           const int h = 8 * p + prow;
           const int gm = m0 - pad + h;
@@ -332,8 +439,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
       const uint32_t off = ((uint32_t)tap * a.Cin_pad + cb * KE) * (uint32_t)sizeof(TW) + bcol;
       char *Bs = Bbuf + buf * B_BYTES;
 #pragma unroll
-      for (int it = 0; it < BP / 4; ++it) {
-        const int p = wid + 4 * it;
+      for (int it = 0; it < BP / NW; ++it) {
+        const int p = wid + NW * it;
         const int n = n0 + 8 * p + prow;
         glds(wr_, Bs + p * 1024, n < a.N ? (uint32_t)n * wrow + off : kOOB);
       }
@@ -350,7 +457,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         dma_b(ncb, ntap, (ks + 1) & 1);
         if (last_tap) dma_a(ncb, ncb & 1);
       }
-      compute(cb, tap, ks);
+      compute(cb & 1, tap, Bbuf + (ks & 1) * B_BYTES);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       cb = ncb;
@@ -373,7 +480,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
       const bool last_tap = tap == KS - 1;
       if (ks + 2 < nK) gload_b(sb_this, cb2, tap2);
       if (tap == 0 && cb + 1 < nCk) gload_a(cb + 1);
-      compute(cb, tap, ks);
+      compute(cb & 1, tap, Bbuf + (ks & 1) * B_BYTES);
       if (ks + 1 < nK) lstore_b(sb_next, (ks + 1) & 1);
       if (last_tap && cb + 1 < nCk) lstore_a((cb + 1) & 1);
       __syncthreads();
@@ -406,104 +513,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvArgs a) {
         E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
   __syncthreads();
 
-  const int epi = a.epi;
-  if (epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN || epi == FS2_EPI_RELU_LN_DOT) {
-    // one wave per row; N == BN == 256 (checked on the host), lane owns columns 4*lane..4*lane+3
-    const int n = lane * 4;
-    float bias4[4], g4[4], be4[4];
-    load4(a.gamma + n, g4);
-    load4(a.beta + n, be4);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bias4[q] = a.bias[n + q];
-    const float inv_n = 1.0f / (float)a.N;
-    for (int r = wid; r < BM; r += 4) {
-      const int m = m0 + r;
-      if (m >= M) break;
-      float v[4];
-      load4(E + r * EPI_LD + n, v);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] += bias4[q];
-      if (epi == FS2_EPI_RES_LN) {
-        float rv[4];
-        load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n, rv);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] += rv[q];
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.0f);
-      }
-      const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * inv_n;
-      float d[4], ss = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        d[q] = v[q] - mean;
-        ss += d[q] * d[q];
-      }
-      const float var = wave_sum(ss) * inv_n;
-      const float rstd = 1.0f / sqrtf(var + a.eps);
-      float y[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) y[q] = d[q] * rstd * g4[q] + be4[q];
-      const int bb = m / T;
-      const int t = m - bb * T;
-      const bool masked = (a.lens != nullptr) && ((int64_t)t >= a.lens[bb]);
-      if (epi == FS2_EPI_RELU_LN_DOT) {
-        float dw4[4];
-        load4(a.dw + n, dw4);
-        const float s = wave_sum(y[0] * dw4[0] + y[1] * dw4[1] + y[2] * dw4[2] + y[3] * dw4[3]) + a.db;
-        if (lane == 0) reinterpret_cast<float *>(a.out)[m] = masked ? 0.0f : s;
-        continue;
-      }
-      if (epi == FS2_EPI_RES_LN) {
-        if (masked) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) y[q] = 0.0f;
-        }
-        if (a.av1 != nullptr) {
-          float av[4];
-          load4(a.av1 + (int64_t)bb * a.N + n, av);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) y[q] += av[q];
-        }
-        if (a.av2 != nullptr) {
-          float av[4];
-          load4(a.av2 + (int64_t)bb * a.N + n, av);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) y[q] += av[q];
-        }
-      }
-      store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, y);
-    }
-    return;
-  }
-
-  constexpr int G = BN / 4;
-  for (int e = tid; e < BM * G; e += 256) {
-    const int r = e / G;
-    const int cg = e - r * G;
-    const int m = m0 + r;
-    const int n = n0 + cg * 4;
-    if (m >= M || n >= a.N) continue;
-    float v[4];
-    load4(E + r * EPI_LD + cg * 4, v);
-    if (a.bias != nullptr) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] += a.bias[n + q];
-    }
-    if (epi == FS2_EPI_BIAS_RELU) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.0f);
-    } else if (epi == FS2_EPI_BIAS_TANH) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
-    } else if (epi == FS2_EPI_BIAS_RES) {
-      float rv[4];
-      load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n, rv);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] += rv[q];
-    }
-    store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, v);
-  }
+  epilogue<BM, BN, NW>(a, E, m0, n0, tid);
 }
 
 template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn>
@@ -512,7 +522,7 @@ void launch(ConvArgs a, hipStream_t s) {
   constexpr bool GL = std::is_same<TIn, typename CTraits<CT>::T>::value;  // LDS-DMA needs no conversion
   a.ntn = (a.N + BN - 1) / BN;
   const int nwg = ((a.M + BM - 1) / BM) * a.ntn;
-  hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, WMI, KSMAX, TIn, GL>), dim3(nwg), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, WMI, KSMAX, TIn, GL>), dim3(nwg), dim3(64 * WGM * WGN), 0, s, a);
 }
 
 // Row-tile choice: the largest tile that still gives >= 2 workgroups per CU (256 CUs), so the
@@ -522,7 +532,9 @@ constexpr int kTargetWGs = 512;
 template <int CT, typename TIn>
 void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
   if (ln) {  // 256-wide rows for the LayerNorm epilogues; WMI <= 2 keeps 2 workgroups / CU in LDS
-    if ((int64_t)((a.M + 31) / 32) >= kTargetWGs)
+    if (a.M >= 192 * 128)  // large M (decoder): 128 x 256 tile, 8 waves of 64 x 64, 1 workgroup / CU
+      launch<CT, 2, 4, 4, 3, TIn>(a, s);
+    else if ((int64_t)((a.M + 31) / 32) >= kTargetWGs)
       launch<CT, 1, 4, 2, 3, TIn>(a, s);
     else
       launch<CT, 1, 4, 1, 3, TIn>(a, s);

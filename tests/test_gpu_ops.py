@@ -46,7 +46,9 @@ def _rel_err(got, ref):
 
 @pytest.mark.parametrize("compute", [0, 1])
 @pytest.mark.parametrize("B,T,Cin,N,KS", [(2, 37, 256, 768, 1), (3, 50, 256, 1024, 9), (2, 29, 1024, 256, 1),
-                                          (1, 130, 80, 512, 5), (2, 70, 512, 80, 5), (4, 9, 256, 256, 3)])
+                                          (1, 130, 80, 512, 5), (2, 70, 512, 80, 5), (4, 9, 256, 256, 3),
+                                          # >= 256 tiles of 256x128: the 512-thread deep-pipeline kernel (bf16)
+                                          (16, 513, 256, 1024, 9), (32, 510, 512, 512, 5)])
 def test_conv1d_bias_relu_tanh(ops, compute, B, T, Cin, N, KS):
     L = _L()
     g = torch.Generator().manual_seed(B * 1000 + T + N)
@@ -98,24 +100,25 @@ def test_conv1d_f32_input_bf16_compute_and_residual(ops, compute):
 
 
 @pytest.mark.parametrize("compute", [0, 1])
-def test_conv1d_res_ln_mask_addvec(ops, compute):
+@pytest.mark.parametrize("B,T,Cin", [(5, 41, 256), (64, 401, 1024)])  # the 2nd routes to the 8-wave 128x256 tile
+def test_conv1d_res_ln_mask_addvec(ops, compute, B, T, Cin):
     L = _L()
     g = torch.Generator().manual_seed(5)
-    B, T, C = 5, 41, 256
-    x = torch.randn(B, T, C, generator=g)
+    C = 256
+    x = torch.randn(B, T, Cin, generator=g)
     res = torch.randn(B, T, C, generator=g)
-    w = torch.randn(C, C, 1, generator=g) / 16
+    w = torch.randn(C, Cin, 1, generator=g) / np.sqrt(Cin)
     b = torch.randn(C, generator=g) * 0.1
     gam, bet = 1 + 0.1 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
-    lens = torch.tensor([41, 1, 0, 17, 40])
+    lens = torch.tensor([41, 1, 0, 17, 40]) if B == 5 else torch.randint(0, T + 1, (B,), generator=g)
     av1, av2 = torch.randn(B, C, generator=g), torch.randn(B, C, generator=g)
     dt = torch.float32 if compute == 0 else torch.bfloat16
     wp = ops.pack_conv_weight(w.to(DEV), compute)
     xd, rd = x.to(DEV, dt), res.to(DEV, dt)
-    out = ops.conv1d(xd, wp, b.to(DEV), cin=C, ks=1, pad=0, compute=compute, epilogue=L.EPI_RES_LN,
+    out = ops.conv1d(xd, wp, b.to(DEV), cin=Cin, ks=1, pad=0, compute=compute, epilogue=L.EPI_RES_LN,
                      out_dtype=L.FS2_F32, residual=rd, ln=(gam.to(DEV), bet.to(DEV), 1e-5), lens=lens.to(DEV),
                      addvec1=av1.to(DEV), addvec2=av2.to(DEV))
-    pre = _ref_conv(xd.float().cpu(), wp.float().cpu().permute(0, 2, 1), b, 0) + rd.float().cpu()
+    pre = _ref_conv(xd.float().cpu(), wp.float().cpu()[:, :, :Cin].permute(0, 2, 1), b, 0) + rd.float().cpu()
     y = F.layer_norm(pre, (C,), gam, bet)
     mask = torch.arange(T)[None, :] >= lens[:, None]
     y = y.masked_fill(mask.unsqueeze(-1), 0) + av1[:, None, :] + av2[:, None, :]
