@@ -7,7 +7,7 @@
 //
 // Here: launch 1 (one workgroup per sequence) turns durations into frame counts
 // max(trunc(d), 0), wavefront-scans them into an inclusive prefix sum `cum` and writes
-// mel_len (the uncropped total). Launch 2 (B x ceil(T_out/32) workgroups) binary-searches
+// mel_len (the uncropped total). Launch 2 (B x ceil(T_out/64) workgroups) binary-searches
 // each output frame's source phoneme in `cum` (first i with cum[i] > t) and streams the
 // D-wide row with 16-byte vector loads/stores; frames at or past min(mel_len, T_out) are
 // zero. An optional f32 position-encoding row is added on the way out (Decoder input,
@@ -17,7 +17,7 @@
 namespace {
 
 constexpr int kScanThreads = 256;
-constexpr int kRowsPerBlock = 32;
+constexpr int kRowsPerBlock = 64;
 
 __device__ __forceinline__ int64_t frames_of(const void *dur, int kind, float d_control, int64_t idx,
                                              float *d_rounded) {
@@ -76,11 +76,15 @@ __global__ __launch_bounds__(kScanThreads) void lr_durations_kernel(const void *
   }
 }
 
-template <typename TX, typename TO>
+// 64 output frames per workgroup; each thread keeps UNR independent 16-byte row pieces in
+// flight (all loads issued before the stores) so a workgroup streams 32 KiB (bf16, D = 256)
+// with one round trip of latency.
+template <typename TX, typename TO, bool HAS_PE>
 __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x, const int32_t *__restrict__ cum,
                                                         const int64_t *__restrict__ mel_len, int L, int D, int T_out,
                                                         const float *__restrict__ pe, TO *__restrict__ out,
                                                         int32_t *__restrict__ index_map) {
+  constexpr int UNR = 8;
   const int b = blockIdx.y;
   const int t0 = blockIdx.x * kRowsPerBlock;
   const int tid = threadIdx.x;
@@ -94,7 +98,7 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x
     if (t < lim) {
       int lo = 0, hi = L - 1;  // first i with cum[i] > t (exists because t < mel_len)
       while (lo < hi) {
-        int mid = (lo + hi) >> 1;
+        const int mid = (lo + hi) >> 1;
         if (c[mid] > t) hi = mid; else lo = mid + 1;
       }
       s = lo;
@@ -105,25 +109,37 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x
   __syncthreads();
   const int vpr = D >> 3;
   const int rows = min(kRowsPerBlock, T_out - t0);
-  for (int e = tid; e < rows * vpr; e += 256) {
-    const int r = e / vpr;
-    const int col = (e - r * vpr) << 3;
-    const int t = t0 + r;
-    const int s = src[r];
-    float v[8];
-    if (s >= 0) {
-      load8(x + ((int64_t)b * L + s) * D + col, v);
-    } else {
+  const int total = rows * vpr;
+  const TX *xb = x + (int64_t)b * L * D;
+  TO *ob = out + ((int64_t)b * T_out + t0) * D;
+  for (int base = tid; base < total; base += 256 * UNR) {
+    float v[UNR][8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = 0.0f;
-    }
-    if (pe != nullptr) {
-      float p[8];
-      load8(pe + (int64_t)t * D + col, p);
+    for (int u = 0; u < UNR; ++u) {
+      const int e = base + u * 256;
+      const int r = e / vpr;
+      const int col = (e - r * vpr) << 3;
+      const int s = e < total ? src[r] : -1;
+      if (s >= 0) {
+        load8(xb + (int64_t)s * D + col, v[u]);
+      } else {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] += p[q];
+        for (int q = 0; q < 8; ++q) v[u][q] = 0.0f;
+      }
+      if constexpr (HAS_PE) {
+        if (e < total) {
+          float p[8];
+          load8(pe + (int64_t)(t0 + r) * D + col, p);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[u][q] += p[q];
+        }
+      }
     }
-    store8(out + ((int64_t)b * T_out + t) * D + col, v);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int e = base + u * 256;
+      if (e < total) store8(ob + (int64_t)e * 8, v[u]);
+    }
   }
 }
 
@@ -131,11 +147,34 @@ template <typename TX, typename TO>
 void launch_expand(const void *x, const int32_t *cum, const int64_t *mel_len, int B, int L, int D, int T_out,
                    const float *pe, void *out, int32_t *index_map, hipStream_t s) {
   dim3 grid((T_out + kRowsPerBlock - 1) / kRowsPerBlock, B);
-  hipLaunchKernelGGL((lr_expand_kernel<TX, TO>), grid, dim3(256), 0, s, reinterpret_cast<const TX *>(x), cum, mel_len,
-                     L, D, T_out, pe, reinterpret_cast<TO *>(out), index_map);
+  if (pe != nullptr)
+    hipLaunchKernelGGL((lr_expand_kernel<TX, TO, true>), grid, dim3(256), 0, s, reinterpret_cast<const TX *>(x), cum,
+                       mel_len, L, D, T_out, pe, reinterpret_cast<TO *>(out), index_map);
+  else
+    hipLaunchKernelGGL((lr_expand_kernel<TX, TO, false>), grid, dim3(256), 0, s, reinterpret_cast<const TX *>(x), cum,
+                       mel_len, L, D, T_out, pe, reinterpret_cast<TO *>(out), index_map);
+}
+
+// get_mask_from_lengths (utils/tools.py:152-160): mask[b, t] = t >= lens[b]  (True = padding)
+__global__ __launch_bounds__(256) void length_mask_kernel(const int64_t *__restrict__ lens, int width, int64_t n,
+                                                          bool *__restrict__ mask) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t b = i / width;
+  mask[i] = (int64_t)(i - b * width) >= lens[b];
 }
 
 }  // namespace
+
+extern "C" int fs2_length_masks(const int64_t *lens, int B, int width, bool *mask, fs2_stream_t stream) {
+  if (lens == nullptr || mask == nullptr || B < 0 || width < 0) return FS2_EINVAL;
+  const int64_t n = (int64_t)B * width;
+  if (n == 0) return FS2_OK;
+  hipLaunchKernelGGL(length_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), lens, width,
+                     n, mask);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
 
 extern "C" int fs2_lr_durations(const void *dur, int dur_kind, float d_control, int B, int L, int32_t *cum,
                                 int64_t *mel_len, float *d_rounded, fs2_stream_t stream) {

@@ -55,6 +55,7 @@ SIGNATURES = {
     "fs2_variance_embed": (_i, [_p, _i, _p, _p, _f, _p, _i, _p, _i, _i, _p]),
     "fs2_lr_durations": (_i, [_p, _i, _f, _i, _i, _p, _p, _p, _p]),
     "fs2_lr_expand": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _p, _p, _i, _p, _p]),
+    "fs2_length_masks": (_i, [_p, _i, _i, _p, _p]),
     "fs2_length_regulate": (_i, [_p, _i, _p, _i, _f, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p, _p, _p]),
 }
 

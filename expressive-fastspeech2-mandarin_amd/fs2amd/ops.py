@@ -153,6 +153,16 @@ def variance_embed(x, pred, target, control, bins, table):
                                     bins.numel() + 1, _ptr(table), M, D, _stream(x)), "fs2_variance_embed")
 
 
+def length_mask(lens, width):
+    """get_mask_from_lengths (utils/tools.py:152-160) in one launch: bool [B, width], True = pad."""
+    _gpu(lens)
+    lens = lens.to(torch.int64).contiguous()
+    B = lens.shape[0]
+    mask = torch.empty(B, int(width), device=lens.device, dtype=torch.bool)
+    L.check(_lib.fs2_length_masks(_ptr(lens), B, int(width), _ptr(mask), _stream(lens)), "fs2_length_masks")
+    return mask
+
+
 def _dur_kind(dur, logpred):
     if logpred:
         return L.DUR_LOGPRED

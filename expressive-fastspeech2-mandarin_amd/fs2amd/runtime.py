@@ -28,7 +28,9 @@ from .model import sinusoid_table
 
 
 def _mask(lengths, width):
-    """get_mask_from_lengths (utils/tools.py:152-160): True = padding."""
+    """get_mask_from_lengths (utils/tools.py:152-160): True = padding (one fs2_length_masks launch)."""
+    if lengths.is_cuda:
+        return ops.length_mask(lengths, width)
     ids = torch.arange(0, width, device=lengths.device).unsqueeze(0).expand(lengths.shape[0], -1)
     return ids >= lengths.unsqueeze(1).expand(-1, width)
 

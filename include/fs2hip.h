@@ -16,6 +16,7 @@
 #ifndef FS2HIP_H
 #define FS2HIP_H
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -162,6 +163,12 @@ int fs2_lr_expand(const void *x, int x_dtype, const int32_t *cum, const int64_t 
 int fs2_length_regulate(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control, int B, int L,
                         int D, int T_out, const float *pe, void *out, int out_dtype, int32_t *cum, int64_t *mel_len,
                         float *d_rounded, int32_t *index_map, fs2_stream_t stream);
+
+/*
+ * fs2_length_masks — get_mask_from_lengths (utils/tools.py:152-160): mask[b, t] = (t >= lens[b]),
+ * bool [B, width], True = padding. The forward returns src_masks / mel_masks built this way.
+ */
+int fs2_length_masks(const int64_t *lens, int B, int width, bool *mask, fs2_stream_t stream);
 
 /* Library identification. */
 const char *fs2_version(void);

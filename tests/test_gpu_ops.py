@@ -283,3 +283,10 @@ def test_single_hip_runtime_loaded(ops):
     hip = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
     assert len(hip) == 1, hip
     assert any("libfs2hip.so" in line for line in maps.splitlines())
+
+
+def test_length_masks(ops):
+    lens = torch.tensor([0, 3, 7, 9, 2])
+    m = ops.length_mask(lens.to(DEV), 7)
+    torch.cuda.synchronize()
+    assert torch.equal(m.cpu(), torch.arange(7)[None, :] >= lens[:, None])

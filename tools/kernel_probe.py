@@ -56,6 +56,11 @@ def main():
         x = rnd(B, 64, 256)
         cum, ml, _ = ops.lr_durations(b["d_targets"])
         fn = lambda: ops.lr_expand(x, cum, ml, T, pe=P.dec_pe, out_dtype=P.act_dtype)
+    elif a.kernel == "lr4":  # LR stress shape (cfg4: B=256, L 16..160, T ~1000), bf16 + PE
+        b4 = to_device(synth_batch(256, 16, 160, seed=1), dev)
+        x4 = torch.randn(256, b4["texts"].shape[1], 256, generator=g).to(dev, dt)
+        cum4, ml4, _ = ops.lr_durations(b4["d_targets"])
+        fn = lambda: ops.lr_expand(x4, cum4, ml4, int(b4["max_mel_len"]), pe=P.dec_pe, out_dtype=P.act_dtype)
     elif a.kernel == "postnet":
         y = rnd(B, T, 512)
         pl = P.postnet[1]
