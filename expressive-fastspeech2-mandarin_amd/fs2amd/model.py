@@ -199,14 +199,19 @@ class FastSpeech2(nn.Module):
             self.emotion_linear = nn.Sequential(nn.Linear(d, d), nn.ReLU())
         hip = model_config.get("hip", {}) if isinstance(model_config, dict) else {}
         self._precision = hip.get("dtype", os.environ.get("FS2_HIP_DTYPE", "fp32"))
+        self._vp_precision = hip.get("vp_dtype", os.environ.get("FS2_HIP_VP_DTYPE", "fp32"))
         self._packs = {}
         self.register_load_state_dict_post_hook(lambda mod, keys: mod.invalidate_packed())
 
     # ---- precision / packed weights --------------------------------------------------------------
-    def set_precision(self, dtype):
-        if dtype not in ("fp32", "bf16"):
+    def set_precision(self, dtype, vp_dtype=None):
+        """dtype of the FFT blocks / attention / mel_linear / PostNet ('fp32' | 'bf16'); vp_dtype of
+        the three VariancePredictors ('fp32' | 'bf16', bf16 only takes effect in bf16 mode)."""
+        if dtype not in ("fp32", "bf16") or vp_dtype not in (None, "fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
         self._precision = dtype
+        if vp_dtype is not None:
+            self._vp_precision = vp_dtype
         return self
 
     @property
@@ -222,11 +227,11 @@ class FastSpeech2(nn.Module):
     def packed(self, device):
         from .packing import pack_model
 
-        key = (self._precision, str(device))
+        key = (self._precision, self._vp_precision, str(device))
         fp = self._fingerprint()
         ent = self._packs.get(key)
         if ent is None or ent[0] != fp:
-            ent = (fp, pack_model(self, device, self._precision))
+            ent = (fp, pack_model(self, device, self._precision, self._vp_precision))
             self._packs[key] = ent
         return ent[1]
 

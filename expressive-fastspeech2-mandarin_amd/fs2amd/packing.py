@@ -5,7 +5,8 @@
 * Conv1d weights [N, Cin, K] re-laid to [N, K, Cin_pad] (k-steps = (tap, channel block)).
 * PostNet BatchNorm1d (eval: running stats) folded into its conv: w' = w * g/sqrt(rv+eps),
   b' = (b - rm) * g/sqrt(rv+eps) + beta (transformer/Layers.py:92-135).
-* bf16 precision: FFT blocks, mel_linear, PostNet in bf16; VariancePredictors always f32.
+* bf16 precision: FFT blocks, mel_linear, PostNet in bf16; VariancePredictors f32 unless
+  vp_precision == "bf16".
 Everything else (LayerNorm affine, biases, embedding tables, bins, PE tables) stays f32.
 """
 from types import SimpleNamespace
@@ -37,14 +38,15 @@ def _fft_layer(layer, device, compute):
     )
 
 
-def _vp(vp, device):
+def _vp(vp, device, compute):
     cl = vp.conv_layer
     c1, c2 = cl.conv1d_1.conv, cl.conv1d_2.conv
     return SimpleNamespace(
-        w1=pack_conv_weight(c1.weight.to(device), L.FS2_F32), b1=_f32(c1.bias, device), k1=c1.kernel_size[0],
+        compute=compute,
+        w1=pack_conv_weight(c1.weight.to(device), compute), b1=_f32(c1.bias, device), k1=c1.kernel_size[0],
         p1=c1.padding[0], c1=c1.in_channels,
         ln1=(_f32(cl.layer_norm_1.weight, device), _f32(cl.layer_norm_1.bias, device), cl.layer_norm_1.eps),
-        w2=pack_conv_weight(c2.weight.to(device), L.FS2_F32), b2=_f32(c2.bias, device), k2=c2.kernel_size[0],
+        w2=pack_conv_weight(c2.weight.to(device), compute), b2=_f32(c2.bias, device), k2=c2.kernel_size[0],
         p2=c2.padding[0], c2=c2.in_channels,
         ln2=(_f32(cl.layer_norm_2.weight, device), _f32(cl.layer_norm_2.bias, device), cl.layer_norm_2.eps),
         lin_w=_f32(vp.linear_layer.weight.view(-1), device), lin_b=float(vp.linear_layer.bias.detach().cpu()[0]),
@@ -63,9 +65,10 @@ def _postnet(pn, device, compute):
     return layers
 
 
-def pack_model(model, device, precision):
+def pack_model(model, device, precision, vp_precision="fp32"):
     device = torch.device(device)
     big = L.FS2_BF16 if precision == "bf16" else L.FS2_F32
+    vpc = L.FS2_BF16 if (precision == "bf16" and vp_precision == "bf16") else L.FS2_F32
     va = model.variance_adaptor
     P = SimpleNamespace(precision=precision, compute=big, act_dtype=big, device=device)
     P.enc_emb = _f32(model.encoder.src_word_emb.weight, device)
@@ -73,7 +76,7 @@ def pack_model(model, device, precision):
     P.dec_pe = _f32(model.decoder.position_enc[0], device)
     P.enc_layers = [_fft_layer(l, device, big) for l in model.encoder.layer_stack]
     P.dec_layers = [_fft_layer(l, device, big) for l in model.decoder.layer_stack]
-    P.vp = {k: _vp(getattr(va, f"{k}_predictor"), device) for k in ("duration", "pitch", "energy")}
+    P.vp = {k: _vp(getattr(va, f"{k}_predictor"), device, vpc) for k in ("duration", "pitch", "energy")}
     P.bins = {k: _f32(getattr(va, f"{k}_bins"), device) for k in ("pitch", "energy")}
     P.var_table = {k: _f32(getattr(va, f"{k}_embedding").weight, device) for k in ("pitch", "energy")}
     P.mel_w = pack_conv_weight(model.mel_linear.weight.to(device), big)

@@ -74,10 +74,10 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False):
 
 
 def variance_predictor(vp, x, lens):
-    """VariancePredictor (model/modules.py:209-250) in f32: 2 launches -> f32 [B, T]."""
-    h = ops.conv1d(x, vp.w1, vp.b1, cin=vp.c1, ks=vp.k1, pad=vp.p1, compute=L.FS2_F32, epilogue=L.EPI_RELU_LN,
-                   out_dtype=L.FS2_F32, ln=vp.ln1)
-    return ops.conv1d(h, vp.w2, vp.b2, cin=vp.c2, ks=vp.k2, pad=vp.p2, compute=L.FS2_F32,
+    """VariancePredictor (model/modules.py:209-250): 2 launches -> f32 [B, T] (f32 or bf16 MFMA)."""
+    h = ops.conv1d(x, vp.w1, vp.b1, cin=vp.c1, ks=vp.k1, pad=vp.p1, compute=vp.compute, epilogue=L.EPI_RELU_LN,
+                   out_dtype=vp.compute, ln=vp.ln1)
+    return ops.conv1d(h, vp.w2, vp.b2, cin=vp.c2, ks=vp.k2, pad=vp.p2, compute=vp.compute,
                       epilogue=L.EPI_RELU_LN_DOT, ln=vp.ln2, lens=lens, dot=(vp.lin_w, vp.lin_b))
 
 
