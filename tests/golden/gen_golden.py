@@ -135,7 +135,7 @@ def lr_cases(LR):
     print("lr_cases:", list(cases))
 
 
-def main():
+def main(only=None):
     FastSpeech2, LR = import_reference()
     torch.manual_seed(0)
     tmp = tempfile.mkdtemp(prefix="fs2_golden_")
@@ -169,6 +169,7 @@ def main():
     run_case(model, LR, "pad_base", {k: (v[:1] if torch.is_tensor(v) else v) for k, v in base.items()} | {
         "max_src_len": int(base["src_lens"][0]), "max_mel_len": int(base["mel_lens"][0])})
     run_case(model, LR, "cfg2_checksums", synth_batch(64, 64, seed=1), save_full=False)
+    run_case(model, LR, "cfg4_checksums", synth_batch(256, 16, 160, seed=1), save_full=False)
     # LR stress durations (cfg4 shape): index map only
     b4 = synth_batch(256, 16, 160, seed=1)
     im, ml = index_map(LR, b4["d_targets"], b4["max_mel_len"])

@@ -119,3 +119,24 @@ def test_cpu_tensors_fail_loudly(model):
     with pytest.raises(RuntimeError, match="HIP"):
         with torch.no_grad():
             m(**synth_batch(1, 8, seed=3))
+
+
+def test_cfg4_variable_length_fp32_checksums(model, golden_dir):
+    """cfg4 (B=256, 16-160 phonemes, T_max 971): LR-stress shape, ragged padding everywhere."""
+    from fs2amd.data import synth_batch
+
+    z = np.load(f"{golden_dir}/cfg4_checksums.npz")
+    args = synth_batch(256, 16, 160, seed=1)
+    got = _run(model, args, (1.0, 1.0, 1.0), "fp32")
+    post = got[1].double().cpu()
+    ml = got[9].cpu()
+    assert tuple(got[0].shape) == tuple(z["out_shape_mel"])
+    valid = (torch.arange(post.shape[1])[None, :] < ml[:, None]).double()[..., None]
+    np.testing.assert_allclose((post * valid).sum((1, 2)).numpy(), z["ck_post_valid_sum"], rtol=0, atol=1.0)
+    np.testing.assert_allclose((post.abs() * valid).sum((1, 2)).numpy(), z["ck_post_valid_abs"], rtol=2e-5)
+    np.testing.assert_allclose(post.sum((1, 2)).numpy(), z["ck_post_all_sum"], rtol=0, atol=2.0)
+    np.testing.assert_allclose(_np(got[2]), z["out_p_pred"], atol=5e-4)
+    np.testing.assert_allclose(_np(got[4]), z["out_log_d"], atol=5e-4)
+    np.testing.assert_array_equal(ml.numpy(), z["out_mel_lens_out"])
+    np.testing.assert_array_equal(_np(got[6]), z["out_src_masks"])
+    np.testing.assert_array_equal(_np(got[7]), z["out_mel_masks"])
