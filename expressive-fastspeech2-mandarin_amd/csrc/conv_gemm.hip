@@ -26,6 +26,7 @@
 // Epilogue: the f32 accumulator tile goes through LDS (reusing the staging buffers) and is
 // written row-major with 8/16-byte stores; the LayerNorm epilogues run one wave per row
 // (N = 256 = 64 lanes x 4) with shuffle reductions.
+#include <cstdlib>
 #include <type_traits>
 
 #include "fs2_common.h"
@@ -516,6 +517,214 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
   epilogue<BM, BN, NW>(a, E, m0, n0, tid);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Phased 256 x 256 kernel for the large bf16 convolutions (decoder FFN Conv1d k=9, PostNet k=5).
+// 8 waves = 2 (M halves) x 4 (N quarters), each wave a 128 x 64 output (8 x 4 MFMA blocks,
+// 128 accumulator VGPRs). Every k-tile (one tap x 64 channels) runs as 4 phases; a phase is
+//   [ds_read the quadrant's fragments + issue part of the NEXT k-tile's LDS-DMA] s_barrier
+//   [16 x mfma_f32_16x16x32_bf16 on one C quadrant]                              s_barrier
+// and the two M halves run one barrier apart (waves w and w+4 share a SIMD), so on every SIMD
+// one wave's MFMA segment overlaps its partner's read/DMA segment. The A rows of each tap are
+// DMA'd separately (row m0+r+tap-pad), with the sequence-boundary test applied to the source
+// offset (out-of-range -> zeros), so no fragment masking is needed. LDS: 2 k-tile buffers of
+// A (256 x 128 B) and B (256 x 128 B), XOR-swizzled as elsewhere = 128 KiB; the epilogue
+// reuses it one M half at a time.
+__global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
+  constexpr int BM = 256, BN = 256, KE = 64;
+  constexpr int TILE = 256 * kRowBytes;  // 32 KiB: one operand of one k-tile
+  constexpr int EPI_LD = BN + 4;
+  constexpr int SMEM = (4 * TILE > 128 * EPI_LD * 4) ? 4 * TILE : 128 * EPI_LD * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];  // A0 A1 B0 B1
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;  // M half (stagger group), N quarter
+
+  const int nwg = gridDim.x, id = blockIdx.x;
+  const int q = nwg >> 3, rem = nwg & 7, xcd = id & 7, li = id >> 3;
+  const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + li;
+  const int mt = tile / a.ntn, nt = tile - mt * a.ntn;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int KS = a.KS, pad = a.pad, T = a.T, M = a.M;
+  const int nCk = a.Cin_pad / KE;
+  const int nK = KS * nCk;
+  const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
+  const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * 2u;
+
+  // ---- DMA roles. A k-tile is moved in 4 parts, each 16 x 1 KiB pieces (2 per wave), matched to
+  // the phase that first reads it: A0 = rows wr*128 + 0..63 of both M halves (phase 1), A1 = rows
+  // wr*128 + 64..127 (phase 3), B0 = cols wc*64 + 0..31 (phase 1), B1 = cols wc*64 + 32..63 (phase 2).
+  // A piece p covers rows 8p..8p+7: part Px owns p = 8*h + 4*x + (0..3) for h in {0,1} plus +16...
+  //   A part x, wave w: pieces 16*(w>>2) + 8*x ... see apiece(); B part x, wave w: wc*8 + 4x + 2*(w>>2) + {0,1}.
+  const int prow = lane >> 3, plc = (lane & 7) ^ ((lane >> 3) & 7);
+  auto apiece = [&](int x, int i) { return 16 * (w >> 2) + 8 * x + 2 * (w & 3) + i; };  // rows of M half w>>2
+  auto bpiece = [&](int x, int i) { return (w & 3) * 8 + 4 * x + 2 * (w >> 2) + i; };
+  int arow[2][2], apos[2][2];
+  uint32_t boff[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = 8 * apiece(x, i) + prow;
+      arow[x][i] = m0 + r;
+      apos[x][i] = arow[x][i] < M ? arow[x][i] % T : -(1 << 30);
+      const int n = n0 + 8 * bpiece(x, i) + prow;
+      boff[x][i] = n < a.N ? (uint32_t)n * wrow + (uint32_t)(plc * 8) * 2u : kOOB;
+    }
+  auto glds = [&](rsrc_t rs, char *dst, uint32_t off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)dst, 16, off, 0, 0, 0);
+  };
+  auto dma_a = [&](int kt, int buf, int x) {
+    const int tap = kt / nCk, cb = kt - tap * nCk;
+    const int sh = tap - pad;
+    const int ch = cb * KE + plc * 8;
+    const bool ch_ok = ch < a.Cin;
+    char *As = smem + buf * TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ts = apos[x][i] + sh;
+      const bool ok = ch_ok && ts >= 0 && ts < T;
+      glds(xr, As + apiece(x, i) * 1024,
+           ok ? ((uint32_t)(arow[x][i] + sh) * (uint32_t)a.xs + (uint32_t)ch) * 2u : kOOB);
+    }
+  };
+  auto dma_b = [&](int kt, int buf, int x) {
+    const int tap = kt / nCk, cb = kt - tap * nCk;
+    const uint32_t off = ((uint32_t)tap * a.Cin_pad + cb * KE) * 2u;
+    char *Bs = smem + 2 * TILE + buf * TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds(wr_, Bs + bpiece(x, i) * 1024, boff[x][i] == kOOB ? kOOB : boff[x][i] + off);
+  };
+
+  // ---- fragment reads: A rows wr*128 + mi*16 + (lane&15), B rows wc*64 + ni*16 + (lane&15)
+  const int aread[2] = {lds_off(wr * 128 + (lane & 15), lane >> 4), lds_off(wr * 128 + (lane & 15), 4 + (lane >> 4))};
+  const int bread[2] = {lds_off(wc * 64 + (lane & 15), lane >> 4), lds_off(wc * 64 + (lane & 15), 4 + (lane >> 4))};
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bfr[4][2];
+
+  auto read_a = [&](const char *As, int mh) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        af[i][s] = *reinterpret_cast<const bf16x8 *>(As + aread[s] + (mh * 4 + i) * 16 * kRowBytes);
+  };
+  auto read_b = [&](const char *Bs, int nh) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        bfr[nh * 2 + i][s] = *reinterpret_cast<const bf16x8 *>(Bs + bread[s] + (nh * 2 + i) * 16 * kRowBytes);
+  };
+  auto mma = [&](int mh, int nh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh * 4 + i][nh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[nh * 2 + j][s], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = []() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: k-tile 0 complete in buffer 0 for everyone, then stagger the two M halves
+  dma_a(0, 0, 0);
+  dma_b(0, 0, 0);
+  dma_b(0, 0, 1);
+  dma_a(0, 0, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wr == 1) bar();
+
+  // Per k-tile t (buffer cur) the DMAs for t+1 go to the other buffer: A0+B0 in phase 1, B1 in
+  // phase 3, A1 in phase 4. A part is waited for (this wave's pieces, counted vmcnt) in the
+  // segment before the barrier that precedes its first read, which for the trailing M half is
+  // the barrier that ends the leading half's previous segment.
+  for (int kt = 0; kt < nK; ++kt) {
+    const int cur = kt & 1, nxt = cur ^ 1;
+    const bool more = kt + 1 < nK;
+    const char *As = smem + cur * TILE;
+    const char *Bs = smem + 2 * TILE + cur * TILE;
+    // phase 1: quadrant (0, 0); B1(t) must have landed (only A1(t) may still be in flight)
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    read_a(As, 0);
+    read_b(Bs, 0);
+    if (more) {
+      dma_a(kt + 1, nxt, 0);
+      dma_b(kt + 1, nxt, 0);
+    }
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mma(0, 0);
+    bar();
+    // phase 2: quadrant (0, 1); A1(t) must have landed (A0+B0(t+1) may be in flight)
+    if (more)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    read_b(Bs, 1);
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mma(0, 1);
+    bar();
+    // phase 3: quadrant (1, 1)
+    read_a(As, 1);
+    if (more) dma_b(kt + 1, nxt, 1);
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mma(1, 1);
+    bar();
+    // phase 4: quadrant (1, 0); A0+B0(t+1) must have landed (B1(t+1) may be in flight)
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      dma_a(kt + 1, nxt, 1);
+    }
+    bar();
+    mma(1, 0);
+    bar();
+  }
+  if (wr == 0) bar();
+  __syncthreads();
+
+  // ---- epilogue, one M half at a time through LDS
+  float *E = reinterpret_cast<float *>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wr == h) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            E[(mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
+    }
+    __syncthreads();
+    epilogue<128, BN, 8>(a, E, m0 + h * 128, n0, tid);
+    __syncthreads();
+  }
+}
+
+void launch_8p(ConvArgs a, hipStream_t s) {
+  a.ntn = (a.N + 255) / 256;
+  const int nwg = ((a.M + 255) / 256) * a.ntn;
+  hipLaunchKernelGGL(conv_gemm_8p_kernel, dim3(nwg), dim3(512), 0, s, a);
+}
+
 template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn>
 void launch(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM, BN = 64 * WGN;
@@ -531,6 +740,18 @@ constexpr int kTargetWGs = 512;
 
 template <int CT, typename TIn>
 void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
+  if constexpr (CT == FS2_BF16 && std::is_same<TIn, bf16>::value) {
+    // The phased 256x256 kernel is correct (parity-tested) but in round 1 measured slower than
+    // the 4-wave 128x128 kernel on the decoder shapes (barrier-bound: MFMA busy 34 %); opt-in.
+    static const bool phased = [] {
+      const char *e = getenv("FS2_CONV_PHASED");
+      return e != nullptr && e[0] == '1';
+    }();
+    if (phased && !ln && a.KS >= 4 && a.N >= 256 && (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 192) {
+      launch_8p(a, s);
+      return;
+    }
+  }
   if (ln) {  // 256-wide rows for the LayerNorm epilogues; WMI <= 2 keeps 2 workgroups / CU in LDS
     if (a.M >= 192 * 128)  // large M (decoder): 128 x 256 tile, 8 waves of 64 x 64, 1 workgroup / CU
       launch<CT, 2, 4, 4, 3, TIn>(a, s);

@@ -47,8 +47,8 @@ def _rel_err(got, ref):
 @pytest.mark.parametrize("compute", [0, 1])
 @pytest.mark.parametrize("B,T,Cin,N,KS", [(2, 37, 256, 768, 1), (3, 50, 256, 1024, 9), (2, 29, 1024, 256, 1),
                                           (1, 130, 80, 512, 5), (2, 70, 512, 80, 5), (4, 9, 256, 256, 3),
-                                          # >= 256 tiles of 256x128: the 512-thread deep-pipeline kernel (bf16)
-                                          (16, 513, 256, 1024, 9), (32, 510, 512, 512, 5)])
+                                          # large shapes (bf16: the phased 256x256 kernel when FS2_CONV_PHASED=1)
+                                          (24, 513, 256, 1024, 9), (48, 510, 512, 512, 5)])
 def test_conv1d_bias_relu_tanh(ops, compute, B, T, Cin, N, KS):
     L = _L()
     g = torch.Generator().manual_seed(B * 1000 + T + N)
@@ -290,3 +290,33 @@ def test_length_masks(ops):
     m = ops.length_mask(lens.to(DEV), 7)
     torch.cuda.synchronize()
     assert torch.equal(m.cpu(), torch.arange(7)[None, :] >= lens[:, None])
+
+
+def test_phased_conv_kernel_parity():
+    """The opt-in phased 256x256 conv kernel (FS2_CONV_PHASED=1) against F.conv1d, in a child
+    process (the switch is read once per process)."""
+    import subprocess
+    import sys
+
+    code = r"""
+import sys, torch, numpy as np, torch.nn.functional as F
+sys.path.insert(0, 'expressive-fastspeech2-mandarin_amd')
+from fs2amd import ops, _lib as L
+g = torch.Generator().manual_seed(1)
+for (B, T, Cin, N, KS) in [(24, 513, 256, 1024, 9), (48, 510, 512, 512, 5)]:
+    x = torch.randn(B, T, Cin, generator=g).to('cuda', torch.bfloat16)
+    w = (torch.randn(N, Cin, KS, generator=g) / np.sqrt(Cin * KS)).to('cuda')
+    b = (torch.randn(N, generator=g) * 0.1).to('cuda')
+    wp = ops.pack_conv_weight(w, L.FS2_BF16)
+    out = ops.conv1d(x, wp, b, cin=Cin, ks=KS, pad=(KS - 1) // 2, compute=L.FS2_BF16, epilogue=L.EPI_BIAS_RELU,
+                     out_dtype=L.FS2_F32)
+    ref = torch.relu(F.conv1d(x.float().cpu().transpose(1, 2), wp.float().cpu()[:, :, :Cin].permute(0, 2, 1),
+                              b.cpu(), padding=(KS - 1) // 2).transpose(1, 2))
+    err = float((out.cpu() - ref).abs().max() / ref.abs().max())
+    assert err < 2.5e-2, err
+print('ok')
+"""
+    env = dict(os.environ, FS2_CONV_PHASED="1")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=repo, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
