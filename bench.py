@@ -85,14 +85,19 @@ def time_dominant_kernel(model, batch, device, reps):
     from fs2amd import _lib as L
     from fs2amd import ops
 
+    from fs2amd import runtime
+
     P = model.packed(device)
     lp = P.dec_layers[0]
     B, T = batch["d_targets"].shape[0], int(batch["max_mel_len"])
     g = torch.Generator(device="cpu").manual_seed(5)
-    h = torch.randn(B, T, lp.c1, generator=g).to(device=device, dtype=ops.torch_dtype(P.act_dtype))
-    out = torch.empty(B, T, lp.w1.shape[0], device=device, dtype=h.dtype)
+    # the launch the forward makes: packed valid frames (runtime.packed_decoder_ok) or padded rows
+    lay = ops.SeqLayout(batch["mel_lens"].to(device), T) if runtime.packed_decoder_ok(P) else None
+    shape = (B * T,) if lay is not None else (B, T)
+    h = torch.randn(*shape, lp.c1, generator=g).to(device=device, dtype=ops.torch_dtype(P.act_dtype))
+    out = torch.empty(*shape, lp.w1.shape[0], device=device, dtype=h.dtype)
     run = lambda: ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=P.compute,
-                             epilogue=L.EPI_BIAS_RELU, out=out)
+                             epilogue=L.EPI_BIAS_RELU, out=out, layout=lay)
     for _ in range(3):
         run()
     stream = torch.cuda.current_stream(device)

@@ -39,7 +39,8 @@ struct ATraits<FS2_F32> {
 template <int CT>
 __global__ __launch_bounds__(256, 2) void attn_kernel(const typename ATraits<CT>::T *__restrict__ qkv, int64_t qs,
                                                       const int64_t *__restrict__ lens, int T, int H, float scale_log2,
-                                                      typename ATraits<CT>::T *__restrict__ out, int64_t os) {
+                                                      typename ATraits<CT>::T *__restrict__ out, int64_t os,
+                                                      const int32_t *__restrict__ cu) {
   using TE = typename ATraits<CT>::T;
   constexpr int ES = sizeof(TE);
   constexpr int CEp = ATraits<CT>::CEp;
@@ -52,9 +53,21 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const typename ATraits<CT>
 
   const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * QT;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int64_t len64 = lens[b];
-  const int len = (int)(len64 < 0 ? 0 : (len64 > T ? T : len64));
-  const TE *base = qkv + (int64_t)b * T * qs;
+  // padded rows: sequence b is rows b*T.., all T query rows computed, keys >= lens[b] masked;
+  // packed rows (cu): sequence b is rows cu[b] .. cu[b+1]-1 and only those exist
+  int len;
+  int64_t row0;
+  if (cu != nullptr) {
+    row0 = cu[b];
+    len = cu[b + 1] - cu[b];
+    T = len;
+  } else {
+    const int64_t len64 = lens[b];
+    len = (int)(len64 < 0 ? 0 : (len64 > T ? T : len64));
+    row0 = (int64_t)b * T;
+  }
+  if (q0 >= T) return;
+  const TE *base = qkv + row0 * qs;
 
   auto koff = [](int row, int chunk) { return row * KROW + ((chunk ^ (row & 15)) << 4); };
   auto voff = [](int row, int chunk) { return row * VROW + ((chunk ^ (row & VSW)) << 4); };
@@ -216,7 +229,7 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const typename ATraits<CT>
     const int q = q0 + 16 * w + 4 * (lane >> 4) + j;
     if (q >= T) continue;
     const float inv = l_run[j] > 0.f ? 1.0f / l_run[j] : 0.f;
-    TE *orow = out + ((int64_t)b * T + q) * os + h * DK + (lane & 15);
+    TE *orow = out + (row0 + q) * os + h * DK + (lane & 15);
 #pragma unroll
     for (int ni = 0; ni < DK / 16; ++ni) orow[ni * 16] = (TE)(oacc[ni][j] * inv);
   }
@@ -245,7 +258,7 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restrict__ qkv, int64_t qs, uint32_t qkv_bytes,
                                                            const int64_t *__restrict__ lens, int B, int T, int H,
                                                            int nqt, float scale_log2, bf16 *__restrict__ out,
-                                                           int64_t os) {
+                                                           int64_t os, const int32_t *__restrict__ cu) {
   __shared__ __attribute__((aligned(16))) char smem[4 * KT * 256];  // K0 V0 K1 V1
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -256,12 +269,21 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
   const int t = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (id >> 3);
   const int qt = t % nqt, bh = t / nqt, h = bh % H, b = bh / H;
   const int q0 = qt * QT;
-  int64_t len64 = lens[b];
-  const int len = (int)(len64 < 0 ? 0 : (len64 > T ? T : len64));
+  int len;
+  uint32_t seq_base;
+  if (cu != nullptr) {  // packed rows: only the sequence's own rows exist
+    seq_base = (uint32_t)cu[b];
+    len = cu[b + 1] - cu[b];
+    T = len;
+  } else {
+    const int64_t len64 = lens[b];
+    len = (int)(len64 < 0 ? 0 : (len64 > T ? T : len64));
+    seq_base = (uint32_t)b * (uint32_t)T;
+  }
+  if (q0 >= T) return;
 
   const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16 *>(qkv), (short)0, (int)qkv_bytes, 0x00020000);
   const uint32_t row_bytes = (uint32_t)qs * 2u;
-  const uint32_t seq_base = (uint32_t)b * (uint32_t)T;
 
   // Q^T fragments (B operand): query q0 + 16w + li, head dims 32s + 8g .. +7
   const int qrow = q0 + 16 * w + li;
@@ -377,7 +399,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
   const int q = q0 + 16 * w + li;
   if (q < T) {
     const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
-    bf16 *orow = out + ((int64_t)b * T + q) * os + h * DK + 4 * g;
+    bf16 *orow = out + ((int64_t)seq_base + q) * os + h * DK + 4 * g;
 #pragma unroll
     for (int nd = 0; nd < DK / 16; ++nd) {
       bf16x4 o = {(bf16)(oacc[nd][0] * inv), (bf16)(oacc[nd][1] * inv), (bf16)(oacc[nd][2] * inv),
@@ -390,8 +412,9 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
 }  // namespace
 
 extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
-                             int H, int dk, float temperature, void *out, int64_t out_row_stride, fs2_stream_t stream) {
-  if (qkv == nullptr || key_lens == nullptr || out == nullptr) return FS2_EINVAL;
+                             int H, int dk, float temperature, void *out, int64_t out_row_stride,
+                             const int32_t *seq_cu, fs2_stream_t stream) {
+  if (qkv == nullptr || (key_lens == nullptr && seq_cu == nullptr) || out == nullptr) return FS2_EINVAL;
   if (dk != DK || H <= 0 || B < 0 || T < 0 || !(temperature > 0.f)) return FS2_EINVAL;
   if (qkv_row_stride < 3LL * H * dk || out_row_stride < (int64_t)H * dk) return FS2_EINVAL;
   const int ce = dtype == FS2_BF16 ? 8 : 4;
@@ -406,10 +429,11 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
     const int nqt = (T + QT - 1) / QT;
     hipLaunchKernelGGL(attn_bf16_kernel, dim3(nqt * H * B), dim3(256), 0, s, reinterpret_cast<const bf16 *>(qkv),
                        qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt, scale_log2,
-                       reinterpret_cast<bf16 *>(out), out_row_stride);
+                       reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
   } else if (dtype == FS2_F32)
     hipLaunchKernelGGL(attn_kernel<FS2_F32>, grid, dim3(256), 0, s, reinterpret_cast<const float *>(qkv),
-                       qkv_row_stride, key_lens, T, H, scale_log2, reinterpret_cast<float *>(out), out_row_stride);
+                       qkv_row_stride, key_lens, T, H, scale_log2, reinterpret_cast<float *>(out), out_row_stride,
+                       seq_cu);
   else
     return FS2_EUNSUPPORTED;
   FS2_CHECK_LAUNCH();

@@ -131,7 +131,30 @@ struct ConvArgs {
   void *out;
   int out_dt;
   int64_t os;
+  // packed rows (NULL = padded [B, T] rows): active row count = *rows_dev, row r is frame
+  // row_pos[2r] of a sequence of length row_pos[2r+1]
+  const int32_t *rows_dev;
+  const int2 *row_pos;
+  const int32_t *a_rowmap;  // KS == 1 only: A row of output row m (-1 = zero row)
 };
+
+// Active rows and the XCD-aware tile of this workgroup. The dispatcher deals workgroup ids
+// round-robin over the 8 XCDs; each XCD gets a contiguous run of tiles, N-fastest, so the N tiles
+// of one row panel share it through one L2. With packed rows the active tile count is known only
+// here, so the remap is over the active count (ids past it exit) and every XCD stays busy.
+template <int BM>
+__device__ __forceinline__ bool conv_tile(const ConvArgs &a, int &M, int &m0, int &n0, int BN) {
+  M = a.rows_dev != nullptr ? *a.rows_dev : a.M;
+  const int nwg = a.rows_dev != nullptr ? ((M + BM - 1) / BM) * a.ntn : (int)gridDim.x;
+  const int id = blockIdx.x;
+  if (id >= nwg) return false;
+  const int q = nwg >> 3, rem = nwg & 7, xcd = id & 7, li = id >> 3;
+  const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + li;  // bijective
+  const int mt = tile / a.ntn, nt = tile - mt * a.ntn;
+  m0 = mt * BM;
+  n0 = nt * BN;
+  return true;
+}
 
 __device__ __forceinline__ void load_any4(const void *p, int dt, int64_t off, float v[4]) {
   if (dt == FS2_BF16)
@@ -148,10 +171,10 @@ __device__ __forceinline__ void store_any4(void *p, int dt, int64_t off, const f
 
 // Epilogue of one BM x BN tile whose f32 accumulators sit in LDS (E, row stride BN + 4).
 template <int BM, int BN, int NWAVES>
-__device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int m0, int n0, int tid) {
+__device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int m0, int n0, int tid, int M) {
   constexpr int EPI_LD = BN + 4;
   const int lane = tid & 63, wid = tid >> 6;
-  const int T = a.T, M = a.M;
+  const int T = a.T;
   const int epi = a.epi;
   if (epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN || epi == FS2_EPI_RELU_LN_DOT) {
     // one wave per row; N == BN == 256 (checked on the host), lane owns columns 4*lane..4*lane+3
@@ -278,20 +301,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform for the compiler
   const int wr = wid / WGN, wc = wid % WGN;
 
-  // XCD-aware tile order: the dispatcher deals workgroups round-robin over the 8 XCDs, so
-  // give each XCD a contiguous run of tiles, N-fastest: the N tiles of one row panel run
-  // together on one XCD and share that panel (and its halo) through the XCD's L2.
-  const int nwg = gridDim.x, id = blockIdx.x;
-  const int q = nwg >> 3, rem = nwg & 7, xcd = id & 7, li = id >> 3;
-  const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + li;
-  const int mt = tile / a.ntn, nt = tile - mt * a.ntn;
-  const int m0 = mt * BM, n0 = nt * BN;
+  int M, m0, n0;
+  if (!conv_tile<BM>(a, M, m0, n0, BN)) return;
 
   const int KS = a.KS, pad = a.pad;
   const int H = BM + KS - 1;
   const int nCk = a.Cin_pad / KE;
   const int nK = KS * nCk;
-  const int T = a.T, M = a.M;
+  const int T = a.T;
 
 
   const int srow = tid >> 3, schunk = tid & 7;
@@ -305,17 +322,30 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
     const int n = n0 + srow + RPP * j;
     wofs[j] = n < a.N ? (uint32_t)n * wrow + schunk * 16u : kOOB;
   }
-  // sequence position of this lane's A fragment rows (tap validity)
-  int tpos[WMI];
+  // sequence position / length of this lane's A fragment rows (tap validity)
+  int tpos[WMI], tlen[WMI];
 #pragma unroll
   for (int mi = 0; mi < WMI; ++mi) {
     const int m = m0 + wr * WROWS + mi * 16 + (lane & 15);
-    tpos[mi] = m % T;
+    if (a.row_pos != nullptr) {
+      const int2 p = m < M ? a.row_pos[m] : make_int2(0, 0);
+      tpos[mi] = p.x;
+      tlen[mi] = p.y;
+    } else {
+      tpos[mi] = m % T;
+      tlen[mi] = T;
+    }
   }
   // wave-uniform: do this wave's WROWS rows lie inside one sequence? Then a tap shift is valid
   // for all of them or for none at the tile's own rows, and the per-lane masking is skipped.
-  const int tw = (m0 + wr * WROWS) % T;
-  const bool wave_inside = tw + WROWS <= T && m0 + wr * WROWS + WROWS <= M;
+  const int mw = m0 + wr * WROWS;
+  int tw = mw % T, lw = T;
+  if (a.row_pos != nullptr) {
+    const int2 p = mw < M ? a.row_pos[mw] : make_int2(0, 0);
+    tw = p.x;
+    lw = p.y;
+  }
+  const bool wave_inside = tw + WROWS <= lw && mw + WROWS <= M;
   // LDS fragment-read bases: a 16-row step keeps (row & 7), so the swizzle is the same for
   // every mi / ni block and the block offset is an immediate.
   const int arow0 = wr * WROWS + (lane & 15);
@@ -331,8 +361,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
 #pragma unroll
     for (int j = 0; j < A_CH; ++j) {
       const int h = srow + RPP * j;
-      const int gm = m0 - pad + h;
-      const bool ok = h < H && ch_ok && gm >= 0 && gm < M;
+      int gm = m0 - pad + h;
+      bool ok = h < H && ch_ok && gm >= 0 && gm < M;
+      if (ok && a.a_rowmap != nullptr) {
+        gm = a.a_rowmap[gm];
+        ok = gm >= 0;
+      }
       sa[j].load(xr, ok ? ((uint32_t)gm * (uint32_t)a.xs + (uint32_t)ch) * (uint32_t)sizeof(TIn) : kOOB);
     }
   };
@@ -364,10 +398,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
   auto compute = [&](int aslot, int tap, const char *Bs) {
     const char *As = Abuf + aslot * A_BYTES;
     const int sh = tap - pad;
-    const bool need_mask = !(wave_inside && tw + sh >= 0 && tw + WROWS - 1 + sh < T);
+    const bool need_mask = !(wave_inside && tw + sh >= 0 && tw + WROWS - 1 + sh < lw);
     bool vrow[WMI];
 #pragma unroll
-    for (int mi = 0; mi < WMI; ++mi) vrow[mi] = (unsigned)(tpos[mi] + sh) < (unsigned)T;
+    for (int mi = 0; mi < WMI; ++mi) vrow[mi] = (unsigned)(tpos[mi] + sh) < (unsigned)tlen[mi];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const char *Ab = As + lds_off(arow0 + tap, s * 4 + (lane >> 4));
@@ -420,18 +454,25 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
     auto glds = [&](rsrc_t rs, char *dst, uint32_t off) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)dst, 16, off, 0, 0, 0);
     };
+    constexpr int AIT = (AP + NW - 1) / NW;
+    int asrc[AIT];  // source row of each halo row this lane moves (-1: zeros)
+#pragma unroll
+    for (int it = 0; it < AIT; ++it) {
+      const int h = 8 * (wid + NW * it) + prow;
+      const int gm = m0 - pad + h;
+      asrc[it] = (h < H && gm >= 0 && gm < M) ? (a.a_rowmap != nullptr ? a.a_rowmap[gm] : gm) : -1;
+    }
     auto dma_a = [&](int cb, int buf) {
       const int ch = cb * KE + plc * CE;
       const bool ch_ok = ch < a.Cin;
       char *As = Abuf + buf * A_BYTES;
 #pragma unroll
-      for (int it = 0; it < (AP + NW - 1) / NW; ++it) {
+      for (int it = 0; it < AIT; ++it) {
         const int p = wid + NW * it;
         if (p < AP) {
-          const int h = 8 * p + prow;
-          const int gm = m0 - pad + h;
-          const bool ok = h < H && ch_ok && gm >= 0 && gm < M;
-          glds(xr, As + p * 1024, ok ? ((uint32_t)gm * (uint32_t)a.xs + (uint32_t)ch) * (uint32_t)sizeof(TIn) : kOOB);
+          const bool ok = ch_ok && asrc[it] >= 0;
+          glds(xr, As + p * 1024,
+               ok ? ((uint32_t)asrc[it] * (uint32_t)a.xs + (uint32_t)ch) * (uint32_t)sizeof(TIn) : kOOB);
         }
       }
     };
@@ -514,7 +555,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
         E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
   __syncthreads();
 
-  epilogue<BM, BN, NW>(a, E, m0, n0, tid);
+  epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -714,7 +755,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
             E[(mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
     }
     __syncthreads();
-    epilogue<128, BN, 8>(a, E, m0 + h * 128, n0, tid);
+    epilogue<128, BN, 8>(a, E, m0 + h * 128, n0, tid, M);
     __syncthreads();
   }
 }
@@ -747,7 +788,7 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       const char *e = getenv("FS2_CONV_PHASED");
       return e != nullptr && e[0] == '1';
     }();
-    if (phased && !ln && a.KS >= 4 && a.N >= 256 && (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 192) {
+    if (phased && !ln && a.row_pos == nullptr && a.KS >= 4 && a.N >= 256 && (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 192) {
       launch_8p(a, s);
       return;
     }
@@ -795,6 +836,11 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
     return FS2_EINVAL;
   const int64_t M64 = (int64_t)d->B * d->T;
   if (M64 > 0x7fffff00LL) return FS2_EINVAL;
+  if ((d->rows_dev == nullptr) != (d->row_pos == nullptr)) return FS2_EINVAL;
+  if (d->rows_dev != nullptr && (d->lens != nullptr || d->addvec1 != nullptr || d->addvec2 != nullptr ||
+                                 d->a_rowmap != nullptr))
+    return FS2_EINVAL;
+  if (d->a_rowmap != nullptr && (d->KS != 1 || d->pad != 0)) return FS2_EINVAL;
   if (M64 == 0) return FS2_OK;
 
   ConvArgs a;
@@ -825,6 +871,9 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.out = d->out;
   a.out_dt = d->out_dtype;
   a.os = d->out_row_stride;
+  a.rows_dev = d->rows_dev;
+  a.row_pos = reinterpret_cast<const int2 *>(d->row_pos);
+  a.a_rowmap = d->a_rowmap;
   {
     const int xes = d->x_dtype == FS2_BF16 ? 2 : 4, wes = d->compute == FS2_BF16 ? 2 : 4;
     const int64_t xb = M64 * d->x_row_stride * xes;

@@ -83,11 +83,15 @@ template <typename TX, typename TO, bool HAS_PE>
 __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x, const int32_t *__restrict__ cum,
                                                         const int64_t *__restrict__ mel_len, int L, int D, int T_out,
                                                         const float *__restrict__ pe, TO *__restrict__ out,
-                                                        int32_t *__restrict__ index_map) {
+                                                        int32_t *__restrict__ index_map,
+                                                        const int32_t *__restrict__ out_cu) {
   constexpr int UNR = 8;
   const int b = blockIdx.y;
   const int t0 = blockIdx.x * kRowsPerBlock;
   const int tid = threadIdx.x;
+  // packed output (out_cu != NULL): only frames t < out_cu[b+1] - out_cu[b] exist, at row out_cu[b] + t
+  const int t_end = out_cu != nullptr ? min(T_out, out_cu[b + 1] - out_cu[b]) : T_out;
+  if (t0 >= t_end && index_map == nullptr) return;
   __shared__ int src[kRowsPerBlock];
   const int64_t ml = mel_len[b];
   const int lim = (int)(ml < (int64_t)T_out ? ml : (int64_t)T_out);
@@ -108,10 +112,11 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x
   }
   __syncthreads();
   const int vpr = D >> 3;
-  const int rows = min(kRowsPerBlock, T_out - t0);
+  const int rows = min(kRowsPerBlock, t_end - t0);
+  if (rows <= 0) return;
   const int total = rows * vpr;
   const TX *xb = x + (int64_t)b * L * D;
-  TO *ob = out + ((int64_t)b * T_out + t0) * D;
+  TO *ob = out + ((out_cu != nullptr ? (int64_t)out_cu[b] : (int64_t)b * T_out) + t0) * D;
   for (int base = tid; base < total; base += 256 * UNR) {
     float v[UNR][8];
 #pragma unroll
@@ -145,14 +150,14 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x
 
 template <typename TX, typename TO>
 void launch_expand(const void *x, const int32_t *cum, const int64_t *mel_len, int B, int L, int D, int T_out,
-                   const float *pe, void *out, int32_t *index_map, hipStream_t s) {
+                   const float *pe, void *out, int32_t *index_map, const int32_t *out_cu, hipStream_t s) {
   dim3 grid((T_out + kRowsPerBlock - 1) / kRowsPerBlock, B);
   if (pe != nullptr)
     hipLaunchKernelGGL((lr_expand_kernel<TX, TO, true>), grid, dim3(256), 0, s, reinterpret_cast<const TX *>(x), cum,
-                       mel_len, L, D, T_out, pe, reinterpret_cast<TO *>(out), index_map);
+                       mel_len, L, D, T_out, pe, reinterpret_cast<TO *>(out), index_map, out_cu);
   else
     hipLaunchKernelGGL((lr_expand_kernel<TX, TO, false>), grid, dim3(256), 0, s, reinterpret_cast<const TX *>(x), cum,
-                       mel_len, L, D, T_out, pe, reinterpret_cast<TO *>(out), index_map);
+                       mel_len, L, D, T_out, pe, reinterpret_cast<TO *>(out), index_map, out_cu);
 }
 
 // get_mask_from_lengths (utils/tools.py:152-160): mask[b, t] = t >= lens[b]  (True = padding)
@@ -164,7 +169,61 @@ __global__ __launch_bounds__(256) void length_mask_kernel(const int64_t *__restr
   mask[i] = (int64_t)(i - b * width) >= lens[b];
 }
 
+// Packed-sequence layout: cu[b] = sum_{j<b} clamp(lens[j], 0, T), cu[B] = total rows; one workgroup.
+__global__ __launch_bounds__(256) void seq_cu_kernel(const int64_t *__restrict__ lens, int B, int T,
+                                                     int32_t *__restrict__ cu) {
+  __shared__ int32_t part[257];
+  const int tid = threadIdx.x;
+  const int per = (B + 255) / 256;
+  const int i0 = min(tid * per, B), i1 = min(i0 + per, B);
+  int32_t local = 0;
+  for (int i = i0; i < i1; ++i) {
+    const int64_t l = lens[i];
+    local += (int32_t)(l < 0 ? 0 : (l > T ? T : l));
+  }
+  part[tid + 1] = local;
+  if (tid == 0) part[0] = 0;
+  __syncthreads();
+  if (tid == 0)
+    for (int i = 1; i <= 256; ++i) part[i] += part[i - 1];
+  __syncthreads();
+  int32_t run = part[tid];
+  for (int i = i0; i < i1; ++i) {
+    cu[i] = run;
+    const int64_t l = lens[i];
+    run += (int32_t)(l < 0 ? 0 : (l > T ? T : l));
+  }
+  if (tid == 255) cu[B] = part[256];
+}
+
+// Over the padded frame index i = b*T + t, with len = cu[b+1] - cu[b]:
+//   rowmap[i] = t < len ? cu[b] + t : -1          (padded row -> packed row)
+//   row_pos[cu[b] + t] = {t, len}  for t < len    (packed row -> position in its sequence)
+__global__ __launch_bounds__(256) void seq_rows_kernel(const int32_t *__restrict__ cu, int B, int T,
+                                                       int2 *__restrict__ row_pos, int32_t *__restrict__ rowmap) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)B * T) return;
+  const int b = (int)(i / T), t = (int)(i - (int64_t)b * T);
+  const int c = cu[b], len = cu[b + 1] - c;
+  if (rowmap != nullptr) rowmap[i] = t < len ? c + t : -1;
+  if (row_pos != nullptr && t < len) row_pos[c + t] = make_int2(t, len);
+}
+
 }  // namespace
+
+extern "C" int fs2_seq_layout(const int64_t *lens, int B, int T, int32_t *cu, int32_t *row_pos, int32_t *rowmap,
+                              fs2_stream_t stream) {
+  if (lens == nullptr || cu == nullptr || B < 0 || T < 0 || (int64_t)B * T > 0x7fffff00LL) return FS2_EINVAL;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(seq_cu_kernel, dim3(1), dim3(256), 0, s, lens, B, T, cu);
+  FS2_CHECK_LAUNCH();
+  if ((rowmap != nullptr || row_pos != nullptr) && (int64_t)B * T > 0) {
+    hipLaunchKernelGGL(seq_rows_kernel, dim3((unsigned)(((int64_t)B * T + 255) / 256)), dim3(256), 0, s, cu, B, T,
+                       reinterpret_cast<int2 *>(row_pos), rowmap);
+    FS2_CHECK_LAUNCH();
+  }
+  return FS2_OK;
+}
 
 extern "C" int fs2_length_masks(const int64_t *lens, int B, int width, bool *mask, fs2_stream_t stream) {
   if (lens == nullptr || mask == nullptr || B < 0 || width < 0) return FS2_EINVAL;
@@ -189,19 +248,19 @@ extern "C" int fs2_lr_durations(const void *dur, int dur_kind, float d_control, 
 
 extern "C" int fs2_lr_expand(const void *x, int x_dtype, const int32_t *cum, const int64_t *mel_len, int B, int L,
                              int D, int T_out, const float *pe, void *out, int out_dtype, int32_t *index_map,
-                             fs2_stream_t stream) {
+                             const int32_t *out_cu, fs2_stream_t stream) {
   if (x == nullptr || cum == nullptr || mel_len == nullptr || out == nullptr) return FS2_EINVAL;
   if (B < 0 || L <= 0 || D <= 0 || (D & 7) != 0 || T_out < 0) return FS2_EINVAL;
   if (B == 0 || T_out == 0) return FS2_OK;
   hipStream_t s = as_stream(stream);
   if (x_dtype == FS2_F32 && out_dtype == FS2_F32)
-    launch_expand<float, float>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, s);
+    launch_expand<float, float>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
   else if (x_dtype == FS2_BF16 && out_dtype == FS2_BF16)
-    launch_expand<bf16, bf16>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, s);
+    launch_expand<bf16, bf16>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
   else if (x_dtype == FS2_F32 && out_dtype == FS2_BF16)
-    launch_expand<float, bf16>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, s);
+    launch_expand<float, bf16>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
   else if (x_dtype == FS2_BF16 && out_dtype == FS2_F32)
-    launch_expand<bf16, float>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, s);
+    launch_expand<bf16, float>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
   else
     return FS2_EUNSUPPORTED;
   FS2_CHECK_LAUNCH();
@@ -213,5 +272,5 @@ extern "C" int fs2_length_regulate(const void *x, int x_dtype, const void *dur, 
                                    int64_t *mel_len, float *d_rounded, int32_t *index_map, fs2_stream_t stream) {
   int rc = fs2_lr_durations(dur, dur_kind, d_control, B, L, cum, mel_len, d_rounded, stream);
   if (rc != FS2_OK) return rc;
-  return fs2_lr_expand(x, x_dtype, cum, mel_len, B, L, D, T_out, pe, out, out_dtype, index_map, stream);
+  return fs2_lr_expand(x, x_dtype, cum, mel_len, B, L, D, T_out, pe, out, out_dtype, index_map, nullptr, stream);
 }

@@ -39,6 +39,7 @@ class ConvDesc(ctypes.Structure):
         ("lens", _p), ("addvec1", _p), ("addvec2", _p),
         ("dot_w", _p), ("dot_b", _f),
         ("out", _p), ("out_dtype", _i), ("out_row_stride", _i64),
+        ("rows_dev", _p), ("row_pos", _p), ("a_rowmap", _p),
     ]
 
 
@@ -48,13 +49,14 @@ SIGNATURES = {
     "fs2_status_string": (ctypes.c_char_p, [_i]),
     "fs2_conv_cin_pad": (_i, [_i, _i]),
     "fs2_conv1d": (_i, [ctypes.POINTER(ConvDesc), _p]),
-    "fs2_attention": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p]),
+    "fs2_attention": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p]),
     "fs2_embed_pe": (_i, [_p, _p, _i, _p, _i, _i, _i, _p, _i, _p]),
     "fs2_cond_vectors": (_i, [_p, _p, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p,
                               _p]),
     "fs2_variance_embed": (_i, [_p, _i, _p, _p, _f, _p, _i, _p, _i, _i, _p]),
     "fs2_lr_durations": (_i, [_p, _i, _f, _i, _i, _p, _p, _p, _p]),
-    "fs2_lr_expand": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _p, _p, _i, _p, _p]),
+    "fs2_lr_expand": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p]),
+    "fs2_seq_layout": (_i, [_p, _i, _i, _p, _p, _p, _p]),
     "fs2_length_masks": (_i, [_p, _i, _i, _p, _p]),
     "fs2_length_regulate": (_i, [_p, _i, _p, _i, _f, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p, _p, _p]),
 }

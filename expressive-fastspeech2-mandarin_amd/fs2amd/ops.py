@@ -42,9 +42,12 @@ def _gpu(*ts):
 
 
 def _rows(x, name):
-    """Row stride (elements) of a [B, T, C] tensor whose rows are evenly spaced."""
+    """Row stride (elements) of a [B, T, C] (or packed [rows, C]) tensor with evenly spaced rows."""
+    if x.dim() == 2 and x.stride(1) == 1:
+        return x.stride(0)
     if x.dim() != 3 or x.stride(2) != 1 or x.stride(0) != x.shape[1] * x.stride(1):
-        raise ValueError(f"fs2amd: {name} must be a [B, T, C] tensor with unit channel stride and packed rows")
+        raise ValueError(f"fs2amd: {name} must be a [B, T, C] or [rows, C] tensor with unit channel stride and "
+                         f"evenly spaced rows")
     return x.stride(1)
 
 
@@ -67,11 +70,57 @@ def pack_conv_weight(w, compute, scale=None):
     return out.contiguous()
 
 
+class SeqLayout:
+    """Packed-sequence layout (fs2_seq_layout): B sequences of clamp(lens[b], 0, T) frames stored
+    back to back in a [B*T, C] buffer (capacity). ``cu`` int32 [B+1] (cu[B] = active rows, read on
+    the device), ``row_pos`` int32 [B*T, 2] = (frame, length) per packed row, ``rowmap`` int32
+    [B*T] padded row -> packed row (-1 = padding). Built with two launches, no host sync."""
+
+    def __init__(self, lens, T):
+        _gpu(lens)
+        lens = lens.to(torch.int64).contiguous()
+        self.B, self.T = int(lens.shape[0]), int(T)
+        dev = lens.device
+        self.cu = torch.empty(self.B + 1, device=dev, dtype=torch.int32)
+        self.row_pos = torch.empty(self.B * self.T, 2, device=dev, dtype=torch.int32)
+        self.rowmap = torch.empty(self.B * self.T, device=dev, dtype=torch.int32)
+        L.check(_lib.fs2_seq_layout(_ptr(lens), self.B, self.T, _ptr(self.cu), _ptr(self.row_pos),
+                                    _ptr(self.rowmap), _stream(lens)), "fs2_seq_layout")
+
+    @property
+    def capacity(self):
+        return self.B * self.T
+
+    @property
+    def rows_dev(self):
+        return self.cu.data_ptr() + 4 * self.B
+
+    def empty(self, C, dtype):
+        return torch.empty(self.capacity, C, device=self.cu.device, dtype=dtype)
+
+    def unpack(self, packed):
+        """Packed [B*T, C] -> padded [B, T, C] with zeros at padding (test / debug helper)."""
+        C = packed.shape[-1]
+        rm = self.rowmap.long()
+        out = packed.new_zeros(self.capacity, C)
+        ok = rm >= 0
+        out[ok] = packed[rm[ok]]
+        return out.view(self.B, self.T, C)
+
+
 def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None, out=None, residual=None,
-           ln=None, lens=None, addvec1=None, addvec2=None, dot=None, n=None):
-    """Implicit-GEMM Conv1d / Linear with a fused epilogue (fs2_conv1d)."""
+           ln=None, lens=None, addvec1=None, addvec2=None, dot=None, n=None, layout=None, src_layout=None):
+    """Implicit-GEMM Conv1d / Linear with a fused epilogue (fs2_conv1d).
+
+    layout: x / residual / out are packed [B*T, C] in that SeqLayout. src_layout (KS == 1): x is
+    packed in it, out is padded [B, T, N] (zeros in, i.e. bias out, at padding)."""
     _gpu(x, w_packed, bias, residual, lens, addvec1, addvec2)
-    B, T, _ = x.shape
+    if layout is not None or src_layout is not None:
+        lay = layout if layout is not None else src_layout
+        B, T = lay.B, lay.T
+        assert x.dim() == 2 and x.shape[0] == lay.capacity, (tuple(x.shape), lay.capacity)
+    else:
+        B, T, _ = x.shape
     N = w_packed.shape[0] if n is None else n
     d = L.ConvDesc()
     d.x, d.x_dtype, d.x_row_stride = x.data_ptr(), _dt(x), _rows(x, "x")
@@ -91,28 +140,40 @@ def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None
         d.addvec1 = addvec1.data_ptr()
     if addvec2 is not None:
         d.addvec2 = addvec2.data_ptr()
+    if layout is not None:
+        d.rows_dev, d.row_pos = layout.rows_dev, layout.row_pos.data_ptr()
+    if src_layout is not None:
+        d.a_rowmap = src_layout.rowmap.data_ptr()
+    oshape = (B * T,) if layout is not None else (B, T)
     if epilogue == L.EPI_RELU_LN_DOT:
         dw, db = dot
         d.dot_w, d.dot_b = dw.data_ptr(), float(db)
         if out is None:
-            out = torch.empty(B, T, device=x.device, dtype=torch.float32)
+            out = torch.empty(*oshape, device=x.device, dtype=torch.float32)
         d.out, d.out_dtype, d.out_row_stride = out.data_ptr(), L.FS2_F32, 1
     else:
         if out is None:
-            out = torch.empty(B, T, N, device=x.device, dtype=torch_dtype(out_dtype))
+            out = torch.empty(*oshape, N, device=x.device, dtype=torch_dtype(out_dtype))
         d.out, d.out_dtype, d.out_row_stride = out.data_ptr(), _dt(out), _rows(out, "out")
     L.check(_lib.fs2_conv1d(ctypes.byref(d), _stream(x)), "fs2_conv1d")
     return out
 
 
-def attention(qkv, lens, n_head, d_k, temperature, out=None):
-    """Key-padding-masked multi-head self-attention over a fused [B, T, 3*H*dk] projection."""
+def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None):
+    """Key-padding-masked multi-head self-attention over a fused [B, T, 3*H*dk] projection
+    (or packed [B*T, 3*H*dk] rows of a SeqLayout: lens unused)."""
     _gpu(qkv, lens)
-    B, T, _ = qkv.shape
+    if layout is not None:
+        B, T = layout.B, layout.T
+        shape = (layout.capacity, n_head * d_k)
+    else:
+        B, T, _ = qkv.shape
+        shape = (B, T, n_head * d_k)
     if out is None:
-        out = torch.empty(B, T, n_head * d_k, device=qkv.device, dtype=qkv.dtype)
+        out = torch.empty(*shape, device=qkv.device, dtype=qkv.dtype)
     L.check(_lib.fs2_attention(_ptr(qkv), _dt(qkv), _rows(qkv, "qkv"), _ptr(lens), B, T, n_head, d_k,
-                               float(temperature), _ptr(out), _rows(out, "out"), _stream(qkv)), "fs2_attention")
+                               float(temperature), _ptr(out), _rows(out, "out"),
+                               _ptr(layout.cu) if layout is not None else None, _stream(qkv)), "fs2_attention")
     return out
 
 
@@ -186,15 +247,21 @@ def lr_durations(dur, logpred=False, d_control=1.0):
     return cum, mel_len, d_rounded
 
 
-def lr_expand(x, cum, mel_len, T_out, pe=None, out_dtype=None, index_map=False):
+def lr_expand(x, cum, mel_len, T_out, pe=None, out_dtype=None, index_map=False, out_layout=None):
+    """Frame gather (+ PE). out_layout: write only the SeqLayout's frames, packed [B*T_out, D]."""
     _gpu(x, cum, mel_len, pe)
     x = x.contiguous()
     B, Lx, D = x.shape
     od = _dt(x) if out_dtype is None else out_dtype
-    out = torch.empty(B, T_out, D, device=x.device, dtype=torch_dtype(od))
+    if out_layout is not None:
+        assert out_layout.B == B and out_layout.T == T_out
+        out = out_layout.empty(D, torch_dtype(od))
+    else:
+        out = torch.empty(B, T_out, D, device=x.device, dtype=torch_dtype(od))
     im = torch.empty(B, T_out, device=x.device, dtype=torch.int32) if index_map else None
     L.check(_lib.fs2_lr_expand(_ptr(x), _dt(x), _ptr(cum), _ptr(mel_len), B, Lx, D, T_out, _ptr(pe), _ptr(out), od,
-                               _ptr(im), _stream(x)), "fs2_lr_expand")
+                               _ptr(im), _ptr(out_layout.cu) if out_layout is not None else None, _stream(x)),
+            "fs2_lr_expand")
     return (out, im) if index_map else out
 
 

@@ -52,25 +52,42 @@ def _pe(P, which, n):
 TIMERS = None
 
 
-def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False):
-    """One FFT block (transformer/Layers.py:21-30) = 5 launches."""
+def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=None):
+    """One FFT block (transformer/Layers.py:21-30) = 5 launches. With ``layout`` (ops.SeqLayout)
+    x is packed [B*T, d_model]: only valid frames exist and no mask is applied (nothing to mask)."""
     c = P.compute
     dt = P.act_dtype
     H, dk = lp.n_head, lp.d_k
     d_model = H * dk
-    qkv = ops.conv1d(x, lp.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_BIAS, out_dtype=dt)
-    att = ops.attention(qkv, lens, H, dk, float(np.power(dk, 0.5)))
+    if layout is not None:
+        lens = None
+    qkv = ops.conv1d(x, lp.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_BIAS, out_dtype=dt,
+                     layout=layout)
+    att = ops.attention(qkv, lens, H, dk, float(np.power(dk, 0.5)), layout=layout)
     h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
-                   residual=x, ln=lp.ln1, lens=lens)
+                   residual=x, ln=lp.ln1, lens=lens, layout=layout)
     if timed and TIMERS is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-    f = ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=c, epilogue=L.EPI_BIAS_RELU, out_dtype=dt)
+    f = ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=c, epilogue=L.EPI_BIAS_RELU, out_dtype=dt,
+                   layout=layout)
     if timed and TIMERS is not None:
         e1.record()
         TIMERS.append((e0, e1))
     return ops.conv1d(f, lp.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
-                      residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2)
+                      residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2, layout=layout)
+
+
+def packed_decoder_ok(P):
+    """The packed decoder equals the reference's padded one when every padded frame an FFT block
+    reads through a conv tap is zero there: h (input of w_1) is masked after the attention
+    LayerNorm, and f = relu(w_1 h + b) (input of w_2) is not, so w_2 must be kernel-1
+    (model.yaml conv_kernel_size [9, 1]). Attention only sees keys < len either way.
+    FS2_PACKED_DECODER=0 forces the padded path."""
+    import os
+    if os.environ.get("FS2_PACKED_DECODER", "1") == "0":
+        return False
+    return all(lp.k2 == 1 and lp.p2 == 0 for lp in P.dec_layers)
 
 
 def variance_predictor(vp, x, lens):
@@ -90,10 +107,14 @@ def _variance(P, kind, x, lens, target, control):
     return pred
 
 
+def _device_ok(dev):
+    return dev.type == "cuda"
+
+
 def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, max_src_len, mels, mel_lens,
                 max_mel_len, p_targets, e_targets, d_targets, p_control, e_control, d_control):
     dev = texts.device
-    if dev.type != "cuda":
+    if not _device_ok(dev):
         raise RuntimeError("fs2amd: FastSpeech2.forward runs on the HIP kernels only; move the model and the batch "
                            "to a ROCm device (no CPU fallback)")
     P = model.packed(dev)
@@ -159,6 +180,17 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
         T_dec = min(T_out, P.max_seq_len)
     else:
         T_dec = T_out
+    if not frame_level and T_dec == T_out and packed_decoder_ok(P):
+        # packed decoder: only the dec_lens frames of each utterance are computed
+        # (cfg2: 24.9k of 27.5k rows, cfg4: 135k of 249k); mel_linear scatters back to [B, T, n_mel]
+        lay = ops.SeqLayout(dec_lens, T_dec)
+        x = ops.lr_expand(x, cum, mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype, out_layout=lay)
+        for lp in P.dec_layers:
+            x = fft_block(P, lp, x, None, timed=True, layout=lay)
+        mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
+                         out_dtype=L.FS2_F32, src_layout=lay)
+        postnet_mel = _postnet(P, mel)
+        return (mel, postnet_mel, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)
     # LR gather with the decoder's position encoding fused (frame-level variance needs the bare
     # expanded x first, so the PE add moves to a second pass in that configuration)
     if frame_level:
@@ -184,6 +216,13 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     # ---- mel_linear + PostNet (+ residual) -----------------------------------------------------
     mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
                      out_dtype=L.FS2_F32)
+    postnet_mel = _postnet(P, mel)
+    return (mel, postnet_mel, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)
+
+
+def _postnet(P, mel):
+    """PostNet (BN folded, transformer/Layers.py:92-137) + residual (fastspeech2.py:136), padded
+    [B, T, n_mel] like the reference: its padded frames (bias values) feed the k5 taps."""
     y = mel
     n_pn = len(P.postnet)
     for i, lp in enumerate(P.postnet):
@@ -193,8 +232,7 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
         else:
             y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute, epilogue=L.EPI_BIAS_RES,
                            out_dtype=L.FS2_F32, residual=mel)
-    postnet_mel = y
-    return (mel, postnet_mel, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)
+    return y
 
 
 def _add_pe(x, pe):

@@ -65,6 +65,15 @@ enum fs2_epilogue {
  *
  * w is PACKED: [N][KS][Cin_pad] in the compute dtype, Cin_pad = Cin rounded up to 64 (bf16)
  * or 32 (f32) with zeros (fs2_conv_cin_pad()). Cin and N must be multiples of 8 and 4.
+ *
+ * Packed sequences (rows_dev != NULL): x / residual / out hold only the valid frames of each
+ * sequence back to back (fs2_seq_layout); the grid is sized for B*T rows (capacity) and the
+ * active row count *rows_dev is read on the device, so no host sync is needed. Row r is frame
+ * row_pos[2r] of a sequence of row_pos[2r+1] frames; taps outside [0, len) read zeros. The
+ * Decoder runs this way (every masked padded frame of an FFT block is dead work,
+ * transformer/Models.py:170-178). lens / addvec must be NULL with packed rows.
+ * a_rowmap (KS == 1, padded output): A row of output row m is x row a_rowmap[m], or zeros when
+ * -1 — mel_linear reading the packed decoder output into the padded [B, T, n_mel] contract.
  */
 typedef struct fs2_conv_desc {
   const void *x;            /* [B, T, >=Cin], dtype x_dtype                              */
@@ -89,6 +98,9 @@ typedef struct fs2_conv_desc {
   void *out;                /* [B, T, N] (f32 [B*T] for RELU_LN_DOT)                       */
   int out_dtype;
   int64_t out_row_stride;
+  const int32_t *rows_dev;  /* packed rows: device int32 = active row count, or NULL (padded) */
+  const int32_t *row_pos;   /* packed rows: int32 [rows][2] = {frame, sequence length}       */
+  const int32_t *a_rowmap;  /* int32 [B*T] packed source row of each output row, or NULL     */
 } fs2_conv_desc;
 
 int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream);
@@ -103,9 +115,12 @@ int fs2_conv_cin_pad(int Cin, int compute);
  * Keys t >= key_lens[b] get zero weight; every query row (padded ones included) is computed.
  * A sequence with key_lens[b] == 0 yields zeros (the reference yields NaN rows that its
  * masked_fill then zeroes).  dk must be 128.
+ * seq_cu (int32 [B+1], fs2_seq_layout) != NULL: packed rows — sequence b is rows
+ * seq_cu[b] .. seq_cu[b+1]-1 of qkv / out (T = capacity bound on its length; key_lens unused).
  */
 int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
-                  int H, int dk, float temperature, void *out, int64_t out_row_stride, fs2_stream_t stream);
+                  int H, int dk, float temperature, void *out, int64_t out_row_stride, const int32_t *seq_cu,
+                  fs2_stream_t stream);
 
 /*
  * fs2_embed_pe — out[b,l,:] = table[tokens[b,l], :] + pe[l, :]   (f32 math)
@@ -151,13 +166,16 @@ int fs2_variance_embed(void *x, int x_dtype, float *pred, const float *target, f
  *   src(b,t) = first i with cum[b,i] > t.  pe (f32 [>=T_out, D]) may be NULL; a non-NULL pe
  *   fuses the Decoder's position_enc add (transformer/Models.py:158-160).  index_map (int32
  *   [B, T_out], -1 on padding) is optional.  D must be a multiple of 8.
+ *   out_cu (int32 [B+1], fs2_seq_layout) != NULL: packed output — only frames
+ *   t < out_cu[b+1] - out_cu[b] are written, at row out_cu[b] + t.
  */
 enum fs2_dur_kind { FS2_DUR_I64 = 0, FS2_DUR_F32 = 1, FS2_DUR_LOGPRED = 2 };
 
 int fs2_lr_durations(const void *dur, int dur_kind, float d_control, int B, int L, int32_t *cum, int64_t *mel_len,
                      float *d_rounded, fs2_stream_t stream);
 int fs2_lr_expand(const void *x, int x_dtype, const int32_t *cum, const int64_t *mel_len, int B, int L, int D,
-                  int T_out, const float *pe, void *out, int out_dtype, int32_t *index_map, fs2_stream_t stream);
+                  int T_out, const float *pe, void *out, int out_dtype, int32_t *index_map, const int32_t *out_cu,
+                  fs2_stream_t stream);
 
 /* Convenience: both launches with a caller-known T_out (the teacher-forced / max_mel_len path). */
 int fs2_length_regulate(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control, int B, int L,
@@ -169,6 +187,16 @@ int fs2_length_regulate(const void *x, int x_dtype, const void *dur, int dur_kin
  * bool [B, width], True = padding. The forward returns src_masks / mel_masks built this way.
  */
 int fs2_length_masks(const int64_t *lens, int B, int width, bool *mask, fs2_stream_t stream);
+
+/*
+ * fs2_seq_layout — packed-sequence layout of B sequences of clamp(lens[b], 0, T) frames:
+ *   cu[b] = sum_{j<b} len_j (int32 [B+1], cu[B] = total rows),
+ *   row_pos[2r], row_pos[2r+1] = {frame, len} of packed row r (int32 [B*T][2], optional),
+ *   rowmap[b*T + t] = t < len_b ? cu[b] + t : -1 (int32 [B*T], optional).
+ * Two launches, no host sync. The Decoder's mel_masks lengths define its packing.
+ */
+int fs2_seq_layout(const int64_t *lens, int B, int T, int32_t *cu, int32_t *row_pos, int32_t *rowmap,
+                   fs2_stream_t stream);
 
 /* Library identification. */
 const char *fs2_version(void);

@@ -1,0 +1,204 @@
+"""Packed-sequence decoder path (ops.SeqLayout): every packed op against the padded op it
+replaces, on ragged lengths including empty and full-length sequences, and the full forward
+with the packed decoder against the padded decoder (FS2_PACKED_DECODER=0).
+
+Exactness: the packed kernels run the same per-row arithmetic as the padded ones (same tile
+code, same k order), so valid rows must agree BIT-EXACTLY with the padded path (fp32 and bf16);
+attention is compared exactly too (same key tiles, same online-softmax order).
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+LENS = [37, 0, 130, 1, 64, 129, 130, 5]  # T = 130: empty, 1-frame, exact tile multiples, full
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from fs2amd import ops, _lib as L
+
+    return ops, L
+
+
+def _layout(ops, lens, T):
+    lens_t = torch.tensor(lens, dtype=torch.int64, device=DEV)
+    return lens_t, ops.SeqLayout(lens_t, T)
+
+
+def _pack(lay, x):
+    """padded [B, T, C] -> packed [B*T, C] (capacity rows; rows past cu[B] left zero)."""
+    rm = lay.rowmap.long()
+    out = x.new_zeros(lay.capacity, x.shape[-1])
+    ok = rm >= 0
+    out[rm[ok]] = x.reshape(-1, x.shape[-1])[ok]
+    return out
+
+
+def _valid(lens, T):
+    return (torch.arange(T, device=DEV)[None, :] < torch.tensor(lens, device=DEV)[:, None])
+
+
+def test_seq_layout(gpu):
+    ops, _ = gpu
+    T = 130
+    lens = LENS + [-3, 500]  # clamped to [0, T]
+    lens_t, lay = _layout(ops, lens, T)
+    cl = np.clip(np.array(lens), 0, T)
+    cu = np.concatenate([[0], np.cumsum(cl)])
+    np.testing.assert_array_equal(lay.cu.cpu().numpy(), cu)
+    rm = lay.rowmap.cpu().numpy().reshape(len(lens), T)
+    rp = lay.row_pos.cpu().numpy()
+    for b, l in enumerate(cl):
+        np.testing.assert_array_equal(rm[b, :l], cu[b] + np.arange(l))
+        assert (rm[b, l:] == -1).all()
+        np.testing.assert_array_equal(rp[cu[b]:cu[b] + l, 0], np.arange(l))
+        assert (rp[cu[b]:cu[b] + l, 1] == l).all()
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("cin,n,ks,epi", [(256, 1024, 9, "relu"), (1024, 256, 1, "res_ln"), (256, 768, 1, "bias")])
+def test_conv_packed_equals_padded(gpu, prec, cin, n, ks, epi):
+    ops, L = gpu
+    T = 130
+    lens_t, lay = _layout(ops, LENS, T)
+    B = len(LENS)
+    c = L.FS2_BF16 if prec == "bf16" else L.FS2_F32
+    dt = ops.torch_dtype(c)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    valid = _valid(LENS, T)[..., None]
+    x = (torch.randn(B, T, cin, device=DEV, generator=g) * valid).to(dt)
+    w = ops.pack_conv_weight(torch.randn(n, cin, ks, device=DEV, generator=g) / (cin * ks) ** 0.5, c)
+    bias = torch.randn(n, device=DEV, generator=g) * 0.1
+    kw = dict(cin=cin, ks=ks, pad=(ks - 1) // 2, compute=c, out_dtype=c)
+    if epi == "relu":
+        kw["epilogue"] = L.EPI_BIAS_RELU
+    elif epi == "bias":
+        kw["epilogue"] = L.EPI_BIAS
+    else:
+        res = (torch.randn(B, T, n, device=DEV, generator=g) * valid).to(dt)
+        ln = (1 + 0.1 * torch.randn(n, device=DEV, generator=g), 0.1 * torch.randn(n, device=DEV, generator=g), 1e-5)
+        kw.update(epilogue=L.EPI_RES_LN, ln=ln)
+    if epi == "res_ln":
+        ref = ops.conv1d(x, w, bias, residual=res, lens=lens_t, **kw)
+        got = ops.conv1d(_pack(lay, x), w, bias, residual=_pack(lay, res), layout=lay, **kw)
+    else:
+        ref = ops.conv1d(x, w, bias, **kw)
+        got = ops.conv1d(_pack(lay, x), w, bias, layout=lay, **kw)
+    torch.cuda.synchronize()
+    R = int(lay.cu[-1])
+    ref_rows = ref.reshape(-1, n)[valid.reshape(-1)]
+    assert torch.equal(got[:R], ref_rows)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_attention_packed_equals_padded(gpu, prec):
+    ops, L = gpu
+    T, H, dk = 130, 2, 128
+    lens_t, lay = _layout(ops, LENS, T)
+    B = len(LENS)
+    dt = torch.bfloat16 if prec == "bf16" else torch.float32
+    g = torch.Generator(device=DEV).manual_seed(5)
+    qkv = torch.randn(B, T, 3 * H * dk, device=DEV, generator=g).to(dt)
+    ref = ops.attention(qkv, lens_t, H, dk, dk ** 0.5)
+    got = ops.attention(_pack(lay, qkv), None, H, dk, dk ** 0.5, layout=lay)
+    torch.cuda.synchronize()
+    R = int(lay.cu[-1])
+    valid = _valid(LENS, T).reshape(-1)
+    assert torch.equal(got[:R], ref.reshape(-1, H * dk)[valid])
+
+
+def test_lr_expand_packed_equals_padded(gpu):
+    ops, L = gpu
+    g = torch.Generator(device=DEV).manual_seed(9)
+    B, Lx, D = 6, 20, 256
+    d = torch.randint(0, 9, (B, Lx), device=DEV, generator=g)
+    d[1] = 0
+    x = torch.randn(B, Lx, D, device=DEV, generator=g)
+    cum, mel_len, _ = ops.lr_durations(d)
+    T = int(mel_len.max()) + 3
+    # decoder lengths: mel_len, one longer than the LR output, one shorter, one cut at T
+    dec = mel_len.clone()
+    dec[0] += 2
+    dec[2] = max(int(dec[2]) - 4, 0)
+    dec[3] = T
+    lay = ops.SeqLayout(dec, T)
+    pe = torch.randn(T, D, device=DEV, generator=g)
+    ref = ops.lr_expand(x, cum, mel_len, T, pe=pe, out_dtype=L.FS2_BF16)
+    got = ops.lr_expand(x, cum, mel_len, T, pe=pe, out_dtype=L.FS2_BF16, out_layout=lay)
+    torch.cuda.synchronize()
+    R = int(lay.cu[-1])
+    valid = (torch.arange(T, device=DEV)[None, :] < dec[:, None]).reshape(-1)
+    assert torch.equal(got[:R], ref.reshape(-1, D)[valid])
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_mel_linear_from_packed(gpu, prec):
+    """src_layout: packed decoder output -> padded [B, T, 80] with bias at padding."""
+    ops, L = gpu
+    T = 130
+    lens_t, lay = _layout(ops, LENS, T)
+    B = len(LENS)
+    c = L.FS2_BF16 if prec == "bf16" else L.FS2_F32
+    g = torch.Generator(device=DEV).manual_seed(11)
+    valid = _valid(LENS, T)[..., None]
+    x = (torch.randn(B, T, 256, device=DEV, generator=g) * valid).to(ops.torch_dtype(c))
+    w = ops.pack_conv_weight(torch.randn(80, 256, device=DEV, generator=g) / 16, c)
+    bias = torch.randn(80, device=DEV, generator=g)
+    kw = dict(cin=256, ks=1, pad=0, compute=c, epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+    ref = ops.conv1d(x, w, bias, **kw)
+    got = ops.conv1d(_pack(lay, x), w, bias, src_layout=lay, **kw)
+    torch.cuda.synchronize()
+    assert got.shape == (B, T, 80)
+    assert torch.equal(got, ref)
+
+
+def test_forward_packed_decoder_equals_padded_decoder(gpu):
+    """Whole forward, bf16 and fp32, cfg4-like ragged batch: packed decoder vs padded decoder.
+    Runs the padded path in a child process (FS2_PACKED_DECODER is read per forward, but a
+    child keeps this process's cached state untouched)."""
+    code = r"""
+import os, sys, torch
+sys.path.insert(0, os.path.join(os.environ["REPO"], "expressive-fastspeech2-mandarin_amd"))
+from fs2amd.model import FastSpeech2
+from fs2amd.data import synth_batch, to_device
+from fs2amd.synth_weights import fill_module
+from fs2amd import config as C
+import tempfile
+d = tempfile.mkdtemp(); C.write_side_files(d); pc, mc, _ = C.synthetic_configs(d)
+m = FastSpeech2(pc, mc); fill_module(m, seed=0); m = m.to("cuda:0").eval()
+outs = {}
+for prec in ("fp32", "bf16"):
+    m.set_precision(prec)
+    args = synth_batch(24, 8, 90, seed=4)
+    with torch.no_grad():
+        o = m(**to_device(args, "cuda:0"))
+    outs[prec] = [t.cpu() if torch.is_tensor(t) else t for t in o]
+torch.save(outs, sys.argv[1])
+"""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for flag in ("1", "0"):
+        path = f"/tmp/fs2_packed_{flag}_{os.getpid()}.pt"
+        env = dict(os.environ, FS2_PACKED_DECODER=flag, REPO=repo)
+        r = subprocess.run([sys.executable, "-c", code, path], env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[flag] = torch.load(path, weights_only=True)
+        os.unlink(path)
+    for prec in ("fp32", "bf16"):
+        a, b = res["1"][prec], res["0"][prec]
+        for i, (x, y) in enumerate(zip(a, b)):
+            if torch.is_tensor(x):
+                assert x.shape == y.shape, (prec, i)
+                if x.is_floating_point():
+                    assert torch.equal(x, y), (prec, i, float((x.float() - y.float()).abs().max()))
+                else:
+                    assert torch.equal(x, y), (prec, i)

@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
     lib = _lib.load()
     declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
-    assert len(declared) == len(_lib.SIGNATURES) == 12
+    assert len(declared) == len(_lib.SIGNATURES) == 13
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
@@ -64,9 +64,10 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     lib = _lib.load()
     d = _lib.ConvDesc()  # all-null descriptor
     assert lib.fs2_conv1d(ctypes.byref(d), None) == _lib.FS2_EINVAL
-    assert lib.fs2_attention(None, 0, 768, None, 1, 1, 2, 128, 11.3, None, 256, None) == _lib.FS2_EINVAL
+    assert lib.fs2_attention(None, 0, 768, None, 1, 1, 2, 128, 11.3, None, 256, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_lr_durations(None, 0, 1.0, 1, 1, None, None, None, None) == _lib.FS2_EINVAL
-    assert lib.fs2_lr_expand(None, 0, None, None, 1, 1, 8, 1, None, None, 0, None, None) == _lib.FS2_EINVAL
+    assert lib.fs2_lr_expand(None, 0, None, None, 1, 1, 8, 1, None, None, 0, None, None, None) == _lib.FS2_EINVAL
+    assert lib.fs2_seq_layout(None, 1, 1, None, None, None, None) == _lib.FS2_EINVAL
 
 
 def _model():
@@ -149,3 +150,59 @@ def test_drop_in_import_path():
     from fs2amd.model import FastSpeech2
     assert mod.FastSpeech2 is FastSpeech2
     assert hasattr(mod, "FastSpeech2Loss") and hasattr(mod, "ScheduledOptim")
+
+
+class _RecordingLib:
+    """Stands in for libfs2hip.so: records every launch entry point call, returns FS2_OK.
+    Host-only helpers (cin_pad, version strings) go to the real library."""
+
+    HOST = {"fs2_conv_cin_pad", "fs2_status_string", "fs2_version"}
+
+    def __init__(self, real):
+        self.real, self.calls = real, []
+
+    def __getattr__(self, name):
+        if name in self.HOST:
+            return getattr(self.real, name)
+
+        def call(*args):
+            self.calls.append(name)
+            return 0
+
+        return call
+
+
+@pytest.mark.parametrize("packed", ["1", "0"])
+@pytest.mark.parametrize("teacher", [True, False])
+def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher):
+    """The forward's Python plumbing (shapes, strides, descriptors, layouts) on CPU with the
+    kernels stubbed: no GPU needed, catches argument errors before any GPU time is spent."""
+    from fs2amd import ops, runtime, _lib
+    from fs2amd.data import synth_batch
+
+    rec = _RecordingLib(_lib.load())
+    monkeypatch.setattr(ops, "_lib", rec)
+    monkeypatch.setattr(ops, "_gpu", lambda *a: None)
+    monkeypatch.setattr(ops, "_stream", lambda *a: None)
+    monkeypatch.setattr(runtime, "_device_ok", lambda dev: True)
+    monkeypatch.setenv("FS2_PACKED_DECODER", packed)
+    m = _model().eval()
+    args = synth_batch(3, 6, 11, seed=2, teacher=teacher)
+    if not teacher:
+        # the stubbed duration kernel writes nothing: give mel_len a defined size
+        real_lr = ops.lr_durations
+
+        def lr_durations(dur, logpred=False, d_control=1.0):
+            cum, ml, dr = real_lr(dur, logpred, d_control)
+            ml.fill_(7)
+            return cum, ml, dr
+
+        monkeypatch.setattr(ops, "lr_durations", lr_durations)
+    with torch.no_grad():
+        out = m(**args)
+    assert len(out) == 10 and out[0].shape[-1] == 80 and out[1].shape == out[0].shape
+    n_conv = rec.calls.count("fs2_conv1d")
+    # 10 FFT blocks x 4 GEMMs + 3 VPs x 2 + mel_linear + 5 PostNet convs
+    assert n_conv == 10 * 4 + 6 + 1 + 5, rec.calls
+    assert rec.calls.count("fs2_attention") == 10
+    assert ("fs2_seq_layout" in rec.calls) == (packed == "1")
