@@ -70,6 +70,10 @@ def time_kernel_in_forward(model, batch, n_fwd=3):
     HIP events recorded around each launch on its stream (fs2amd.runtime.TIMERS)."""
     from fs2amd import runtime
 
+    # one utterance group: the timed launches have the chip to themselves (with stream groups,
+    # concurrent launches share the CUs and per-launch durations stop being kernel speed)
+    prev = os.environ.get("FS2_STREAMS")
+    os.environ["FS2_STREAMS"] = "1"
     runtime.TIMERS = []
     with torch.no_grad():
         for _ in range(n_fwd):
@@ -77,6 +81,10 @@ def time_kernel_in_forward(model, batch, n_fwd=3):
     torch.cuda.synchronize()
     ts = [a.elapsed_time(b) / 1e3 for a, b in runtime.TIMERS]
     runtime.TIMERS = None
+    if prev is None:
+        del os.environ["FS2_STREAMS"]
+    else:
+        os.environ["FS2_STREAMS"] = prev
     return sum(ts) / len(ts), len(ts)
 
 

@@ -560,79 +560,89 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
 
 // ------------------------------------------------------------------------------------------------
 // Phased 256 x 256 kernel for the large bf16 convolutions (decoder FFN Conv1d k=9, PostNet k=5).
-// 8 waves = 2 (M halves) x 4 (N quarters), each wave a 128 x 64 output (8 x 4 MFMA blocks,
-// 128 accumulator VGPRs). Every k-tile (one tap x 64 channels) runs as 4 phases; a phase is
-//   [ds_read the quadrant's fragments + issue part of the NEXT k-tile's LDS-DMA] s_barrier
-//   [16 x mfma_f32_16x16x32_bf16 on one C quadrant]                              s_barrier
-// and the two M halves run one barrier apart (waves w and w+4 share a SIMD), so on every SIMD
-// one wave's MFMA segment overlaps its partner's read/DMA segment. The A rows of each tap are
-// DMA'd separately (row m0+r+tap-pad), with the sequence-boundary test applied to the source
-// offset (out-of-range -> zeros), so no fragment masking is needed. LDS: 2 k-tile buffers of
-// A (256 x 128 B) and B (256 x 128 B), XOR-swizzled as elsewhere = 128 KiB; the epilogue
-// reuses it one M half at a time.
+// 8 waves = 2 (M halves) x 4 (N quarters), each wave a 128 x 64 output (8 x 4 MFMA blocks, 128
+// accumulator registers). A k-tile (one tap x 64 channels) runs as 4 phases, one C quadrant
+// (4 x 2 blocks x K 64 = 16 MFMAs) each:  [ds_read + LDS-DMA issue + counted wait] s_barrier
+// [MFMA] s_barrier. The two M halves run one barrier apart (waves w and w+4 share a SIMD), so on
+// every SIMD one wave's MFMA segment overlaps its partner's read segment.
+//
+// Operand parts (2 x 1 KiB pieces per wave each): A0 / A1 = the A rows of M-quadrant 0 / 1 (both
+// halves), B0 / B1 = the B columns of N-quadrant 0 / 1. Last LDS read of each part in k-tile t:
+// A0, B0 phase 1; B1 phase 2; A1 phase 3 (fragments then stay in registers). Each part of k-tile
+// t+2 (same buffer of the 2-deep ring) is issued two phases after that read (WAR-safe with the
+// stagger), so it has ~6 phases to land:
+//   phase 1: read A0 B0(t), issue A1(t+1), wait B1(t)        phase 2: read B1(t), wait A1(t)
+//   phase 3: read A1(t), issue A0 B0(t+2)                    phase 4: issue B1(t+2), wait A0 B0(t+1)
+// Every wait sits one phase before the read it guards (RAW across the staggered barrier) and is
+// a counted vmcnt (8 or 10 loads may stay in flight); vmcnt(0) only in the last two k-tiles.
+// A rows of each tap are DMA'd separately (row m0+r+tap-pad) with the sequence-boundary test on
+// the source offset (out of range -> zeros), so fragments need no masking. LDS: 2 x (A 32 KiB +
+// B 32 KiB) = 128 KiB, one __shared__ array; the epilogue reuses it one M half at a time.
 __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   constexpr int BM = 256, BN = 256, KE = 64;
   constexpr int TILE = 256 * kRowBytes;  // 32 KiB: one operand of one k-tile
   constexpr int EPI_LD = BN + 4;
   constexpr int SMEM = (4 * TILE > 128 * EPI_LD * 4) ? 4 * TILE : 128 * EPI_LD * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];  // A0 A1 B0 B1
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];  // A0 A1 B0 B1 (buffers)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 2, wc = w & 3;  // M half (stagger group), N quarter
 
-  const int nwg = gridDim.x, id = blockIdx.x;
-  const int q = nwg >> 3, rem = nwg & 7, xcd = id & 7, li = id >> 3;
-  const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + li;
-  const int mt = tile / a.ntn, nt = tile - mt * a.ntn;
-  const int m0 = mt * BM, n0 = nt * BN;
+  int M, m0, n0;
+  if (!conv_tile<BM>(a, M, m0, n0, BN)) return;
 
-  const int KS = a.KS, pad = a.pad, T = a.T, M = a.M;
+  const int KS = a.KS, pad = a.pad, T = a.T;
   const int nCk = a.Cin_pad / KE;
   const int nK = KS * nCk;
   const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
   const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * 2u;
+  const uint32_t xrow = (uint32_t)a.xs * 2u;
 
-  // ---- DMA roles. A k-tile is moved in 4 parts, each 16 x 1 KiB pieces (2 per wave), matched to
-  // the phase that first reads it: A0 = rows wr*128 + 0..63 of both M halves (phase 1), A1 = rows
-  // wr*128 + 64..127 (phase 3), B0 = cols wc*64 + 0..31 (phase 1), B1 = cols wc*64 + 32..63 (phase 2).
-  // A piece p covers rows 8p..8p+7: part Px owns p = 8*h + 4*x + (0..3) for h in {0,1} plus +16...
-  //   A part x, wave w: pieces 16*(w>>2) + 8*x ... see apiece(); B part x, wave w: wc*8 + 4x + 2*(w>>2) + {0,1}.
+  // DMA roles: piece p = rows (or columns) 8p..8p+7 of the 256-row operand image.
+  //   A part x, wave w: pieces 16*(w>>2) + 8x + 2*(w&3) + i  (M half w>>2, quadrant rows 64x..64x+63)
+  //   B part x, wave w: pieces 8*(w&3) + 4x + 2*(w>>2) + i   (N quarter w&3, columns 32x..32x+31)
   const int prow = lane >> 3, plc = (lane & 7) ^ ((lane >> 3) & 7);
-  auto apiece = [&](int x, int i) { return 16 * (w >> 2) + 8 * x + 2 * (w & 3) + i; };  // rows of M half w>>2
+  auto apiece = [&](int x, int i) { return 16 * (w >> 2) + 8 * x + 2 * (w & 3) + i; };
   auto bpiece = [&](int x, int i) { return (w & 3) * 8 + 4 * x + 2 * (w >> 2) + i; };
-  int arow[2][2], apos[2][2];
+  int arow[2][2], apos[2][2], alen[2][2];
   uint32_t boff[2][2];
 #pragma unroll
   for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int r = 8 * apiece(x, i) + prow;
-      arow[x][i] = m0 + r;
-      apos[x][i] = arow[x][i] < M ? arow[x][i] % T : -(1 << 30);
+      const int m = m0 + 8 * apiece(x, i) + prow;
+      arow[x][i] = m;
+      if (m >= M) {
+        apos[x][i] = 0;
+        alen[x][i] = 0;  // every tap out of range -> zeros
+      } else if (a.row_pos != nullptr) {
+        const int2 p = a.row_pos[m];
+        apos[x][i] = p.x;
+        alen[x][i] = p.y;
+      } else {
+        apos[x][i] = m % T;
+        alen[x][i] = T;
+      }
       const int n = n0 + 8 * bpiece(x, i) + prow;
       boff[x][i] = n < a.N ? (uint32_t)n * wrow + (uint32_t)(plc * 8) * 2u : kOOB;
     }
   auto glds = [&](rsrc_t rs, char *dst, uint32_t off) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)dst, 16, off, 0, 0, 0);
   };
-  auto dma_a = [&](int kt, int buf, int x) {
-    const int tap = kt / nCk, cb = kt - tap * nCk;
+  auto dma_a = [&](int tap, int cb, int buf, int x) {
     const int sh = tap - pad;
     const int ch = cb * KE + plc * 8;
     const bool ch_ok = ch < a.Cin;
     char *As = smem + buf * TILE;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int ts = apos[x][i] + sh;
-      const bool ok = ch_ok && ts >= 0 && ts < T;
-      glds(xr, As + apiece(x, i) * 1024,
-           ok ? ((uint32_t)(arow[x][i] + sh) * (uint32_t)a.xs + (uint32_t)ch) * 2u : kOOB);
+      const bool ok = ch_ok && (unsigned)(apos[x][i] + sh) < (unsigned)alen[x][i];
+      glds(xr, As + apiece(x, i) * 1024, ok ? (uint32_t)(arow[x][i] + sh) * xrow + (uint32_t)ch * 2u : kOOB);
     }
   };
-  auto dma_b = [&](int kt, int buf, int x) {
-    const int tap = kt / nCk, cb = kt - tap * nCk;
+  auto dma_b = [&](int tap, int cb, int buf, int x) {
     const uint32_t off = ((uint32_t)tap * a.Cin_pad + cb * KE) * 2u;
     char *Bs = smem + 2 * TILE + buf * TILE;
 #pragma unroll
@@ -681,62 +691,85 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
+  auto lgkm0 = []() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
 
-  // prologue: k-tile 0 complete in buffer 0 for everyone, then stagger the two M halves
-  dma_a(0, 0, 0);
-  dma_b(0, 0, 0);
-  dma_b(0, 0, 1);
-  dma_a(0, 0, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // k-tile t = tap * nCk + cb; (tap1, cb1) tracks t+1 and (tap2, cb2) t+2 (no divisions in the loop)
+  int tap1 = nCk > 1 ? 0 : 1, cb1 = nCk > 1 ? 1 : 0;
+  int tap2 = tap1, cb2 = cb1;
+  if (++cb2 == nCk) {
+    cb2 = 0;
+    ++tap2;
+  }
+
+  // prologue: issue order A0 B0 B1 A1 (t=0), A0 B0 B1 (t=1); k-tile 0 landed for everyone
+  dma_a(0, 0, 0, 0);
+  dma_b(0, 0, 0, 0);
+  dma_b(0, 0, 0, 1);
+  dma_a(0, 0, 0, 1);
+  if (nK > 1) {
+    dma_a(tap1, cb1, 1, 0);
+    dma_b(tap1, cb1, 1, 0);
+    dma_b(tap1, cb1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
   if (wr == 1) bar();
 
-  // Per k-tile t (buffer cur) the DMAs for t+1 go to the other buffer: A0+B0 in phase 1, B1 in
-  // phase 3, A1 in phase 4. A part is waited for (this wave's pieces, counted vmcnt) in the
-  // segment before the barrier that precedes its first read, which for the trailing M half is
-  // the barrier that ends the leading half's previous segment.
-  for (int kt = 0; kt < nK; ++kt) {
-    const int cur = kt & 1, nxt = cur ^ 1;
-    const bool more = kt + 1 < nK;
+  for (int t = 0; t < nK; ++t) {
+    const int cur = t & 1, nxt = cur ^ 1;
+    const bool has1 = t + 1 < nK, has2 = t + 2 < nK;
     const char *As = smem + cur * TILE;
     const char *Bs = smem + 2 * TILE + cur * TILE;
-    // phase 1: quadrant (0, 0); B1(t) must have landed (only A1(t) may still be in flight)
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    // phase 1: quadrant (0, 0)
     read_a(As, 0);
     read_b(Bs, 0);
-    if (more) {
-      dma_a(kt + 1, nxt, 0);
-      dma_b(kt + 1, nxt, 0);
-    }
-    bar();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    mma(0, 0);
-    bar();
-    // phase 2: quadrant (0, 1); A1(t) must have landed (A0+B0(t+1) may be in flight)
-    if (more)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (has1) dma_a(tap1, cb1, nxt, 1);  // A1(t+1)
+    if (has2)
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // B1(t) (A1(t) .. A1(t+1) may fly)
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    read_b(Bs, 1);
     bar();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lgkm0();
+    mma(0, 0);
+    bar();
+    // phase 2: quadrant (0, 1)
+    read_b(Bs, 1);
+    if (has2)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A1(t)
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    lgkm0();
     mma(0, 1);
     bar();
     // phase 3: quadrant (1, 1)
     read_a(As, 1);
-    if (more) dma_b(kt + 1, nxt, 1);
+    if (has2) {
+      dma_a(tap2, cb2, cur, 0);  // A0(t+2)
+      dma_b(tap2, cb2, cur, 0);  // B0(t+2)
+    }
     bar();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lgkm0();
     mma(1, 1);
     bar();
-    // phase 4: quadrant (1, 0); A0+B0(t+1) must have landed (B1(t+1) may be in flight)
-    if (more) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      dma_a(kt + 1, nxt, 1);
+    // phase 4: quadrant (1, 0) from registers
+    if (has2) {
+      dma_b(tap2, cb2, cur, 1);  // B1(t+2)
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0 B0(t+1)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     bar();
     mma(1, 0);
     bar();
+    tap1 = tap2;
+    cb1 = cb2;
+    if (++cb2 == nCk) {
+      cb2 = 0;
+      ++tap2;
+    }
   }
   if (wr == 0) bar();
   __syncthreads();
@@ -766,6 +799,195 @@ void launch_8p(ConvArgs a, hipStream_t s) {
   hipLaunchKernelGGL(conv_gemm_8p_kernel, dim3(nwg), dim3(512), 0, s, a);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Deep-ring kernel for the LayerNorm-epilogue GEMMs (N = 256 = one tile row): fc / FFN-w_2 + LN,
+// VariancePredictor convs + LN (+ dot). At small M (encoder / variance predictor, M = B*L ~ 4k)
+// these run one 16-row tile per CU and stream the whole weight matrix per tile, so a 2-deep
+// stage ring pays one L2/MALL round trip per k-step; here NS stages are in flight.
+//
+// A stage is one k-step (tap, 64-channel block): the tile's BM A rows already shifted by
+// tap - pad, with the sequence test applied to the DMA source offset (out of range -> zeros,
+// no fragment masking), plus the 256 B rows of that k-step. Every wave issues the same number
+// of 1 KiB LDS-DMA pieces per stage (A pieces are duplicated across waves when BM/8 < waves:
+// identical bytes to the same place), so one counted vmcnt per k-step retires stage k while
+// NS-2 later stages stay in flight. One raw s_barrier per k-step (after the wait) both
+// publishes stage k and frees the buffer stage k+NS-1 refills (read in step k-1).
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int CT, int WGM, int WMI, int NS>
+__global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a) {
+  constexpr int WGN = 4, NW = WGM * WGN;
+  constexpr int WROWS = 16 * WMI, BM = WROWS * WGM, BN = 64 * WGN;
+  constexpr int KE = CTraits<CT>::KE, CE = CTraits<CT>::CE;
+  using TW = typename CTraits<CT>::T;
+  constexpr int AP = BM / 8, BP = BN / 8;               // 1 KiB pieces per stage
+  constexpr int AQ = (AP + NW - 1) / NW, BQ = BP / NW;  // pieces per wave
+  constexpr int LPS = AQ + BQ;                          // LDS-DMA loads per wave per stage
+  static_assert(LPS * (NS - 2) <= 63, "vmcnt range");
+  constexpr int STAGE = (AP + BP) * 1024;
+  constexpr int EPI_LD = BN + 4;
+  constexpr int SMEM = (NS * STAGE > BM * EPI_LD * 4) ? NS * STAGE : BM * EPI_LD * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / WGN, wc = wid % WGN;
+  int M, m0, n0;
+  if (!conv_tile<BM>(a, M, m0, n0, BN)) return;
+
+  const int KS = a.KS, pad = a.pad, T = a.T;
+  const int nCk = a.Cin_pad / KE;
+  const int nK = KS * nCk;
+  const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
+  const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * (uint32_t)sizeof(TW);
+  const uint32_t xrow = (uint32_t)a.xs * (uint32_t)sizeof(TW);
+
+  const int prow = lane >> 3, plc = (lane & 7) ^ prow;
+  int arow[AQ], apos[AQ], alen[AQ];
+#pragma unroll
+  for (int i = 0; i < AQ; ++i) {
+    const int m = m0 + 8 * ((wid + NW * i) % AP) + prow;
+    arow[i] = m;
+    if (m >= M) {
+      apos[i] = 0;
+      alen[i] = 0;
+    } else if (a.row_pos != nullptr) {
+      const int2 p = a.row_pos[m];
+      apos[i] = p.x;
+      alen[i] = p.y;
+    } else {
+      apos[i] = m % T;
+      alen[i] = T;
+    }
+  }
+  uint32_t boff[BQ];
+#pragma unroll
+  for (int i = 0; i < BQ; ++i) {
+    const int n = n0 + 8 * (wid + NW * i) + prow;
+    boff[i] = n < a.N ? (uint32_t)n * wrow + (uint32_t)(plc * 16) : kOOB;
+  }
+  auto glds = [&](rsrc_t rs, char *dst, uint32_t off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)dst, 16, off, 0, 0, 0);
+  };
+  auto issue = [&](int tap, int cb, int buf) {
+    char *As = smem + buf * STAGE;
+    char *Bs = As + AP * 1024;
+    const int sh = tap - pad;
+    const int ch = cb * KE + plc * CE;
+    const bool ch_ok = ch < a.Cin;
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      const bool ok = ch_ok && (unsigned)(apos[i] + sh) < (unsigned)alen[i];
+      glds(xr, As + ((wid + NW * i) % AP) * 1024,
+           ok ? (uint32_t)(arow[i] + sh) * xrow + (uint32_t)ch * (uint32_t)sizeof(TW) : kOOB);
+    }
+    const uint32_t off = ((uint32_t)tap * a.Cin_pad + cb * KE) * (uint32_t)sizeof(TW);
+#pragma unroll
+    for (int i = 0; i < BQ; ++i) glds(wr_, Bs + (wid + NW * i) * 1024, boff[i] == kOOB ? kOOB : boff[i] + off);
+  };
+
+  f32x4 acc[WMI][4];
+#pragma unroll
+  for (int i = 0; i < WMI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int aread0 = lds_off(wr * WROWS + (lane & 15), lane >> 4);
+  const int aread1 = lds_off(wr * WROWS + (lane & 15), 4 + (lane >> 4));
+  const int bread0 = lds_off(wc * 64 + (lane & 15), lane >> 4);
+  const int bread1 = lds_off(wc * 64 + (lane & 15), 4 + (lane >> 4));
+  auto compute = [&](const char *S) {
+    const char *As = S;
+    const char *Bs = S + AP * 1024;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const char *Ab = As + (s ? aread1 : aread0);
+      const char *Bb = Bs + (s ? bread1 : bread0);
+      if constexpr (CT == FS2_BF16) {
+        bf16x8 af[WMI], bfr[4];
+#pragma unroll
+        for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const bf16x8 *>(Ab + mi * 16 * kRowBytes);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) bfr[ni] = *reinterpret_cast<const bf16x8 *>(Bb + ni * 16 * kRowBytes);
+#pragma unroll
+        for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+      } else {
+        f32x4 af[WMI], bfr[4];
+#pragma unroll
+        for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const f32x4 *>(Ab + mi * 16 * kRowBytes);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) bfr[ni] = *reinterpret_cast<const f32x4 *>(Bb + ni * 16 * kRowBytes);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi][j], bfr[ni][j], acc[mi][ni], 0, 0, 0);
+      }
+    }
+  };
+
+  // k-step k = cb * KS + tap (tap fastest); (itap, icb) = next stage to issue
+  int itap = 0, icb = 0;
+  auto advance = [&]() {
+    if (++itap == KS) {
+      itap = 0;
+      ++icb;
+    }
+  };
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st) {
+    if (st < nK) {
+      issue(itap, icb, st);
+      advance();
+    }
+  }
+  for (int k = 0; k < nK; ++k) {
+    // stage k landed (this wave's pieces): later issued stages may stay in flight
+    const int ahead = nK - 1 - k;
+    if (ahead >= NS - 2)
+      vm_wait<LPS * (NS - 2)>();
+    else if (NS > 3 && ahead == 1)
+      vm_wait<LPS>();
+    else
+      vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (k + NS - 1 < nK) {
+      issue(itap, icb, (k + NS - 1) % NS);
+      advance();
+    }
+    compute(smem + (k % NS) * STAGE);
+  }
+  __syncthreads();
+
+  float *E = reinterpret_cast<float *>(smem);
+#pragma unroll
+  for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
+  __syncthreads();
+  epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
+}
+
+template <int CT, int WGM, int WMI, int NS>
+void launch_ring(ConvArgs a, hipStream_t s) {
+  constexpr int BM = 16 * WMI * WGM;
+  a.ntn = 1;
+  const int nwg = (a.M + BM - 1) / BM;
+  hipLaunchKernelGGL((conv_gemm_ring_kernel<CT, WGM, WMI, NS>), dim3(nwg), dim3(256 * WGM), 0, s, a);
+}
+
 template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn>
 void launch(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM, BN = 64 * WGN;
@@ -788,8 +1010,23 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       const char *e = getenv("FS2_CONV_PHASED");
       return e != nullptr && e[0] == '1';
     }();
-    if (phased && !ln && a.row_pos == nullptr && a.KS >= 4 && a.N >= 256 && (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 192) {
+    if (phased && !ln && a.KS >= 4 && a.N >= 256 && (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 192) {
       launch_8p(a, s);
+      return;
+    }
+  }
+  if constexpr (std::is_same<TIn, typename CTraits<CT>::T>::value) {
+    static const bool ring = [] {
+      const char *e = getenv("FS2_CONV_RING");
+      return e == nullptr || e[0] != '0';
+    }();
+    if (ln && ring) {  // LDS-DMA deep ring (LN epilogues, N == 256)
+      if (a.M >= 192 * 128)
+        launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages (144 KiB)
+      else if (a.M >= 8192)
+        launch_ring<CT, 1, 2, 4>(a, s);  // 32 x 256, 4 waves, 4 stages
+      else
+        launch_ring<CT, 1, 1, 4>(a, s);  // 16 x 256, 4 waves, 4 stages
       return;
     }
   }

@@ -19,6 +19,8 @@ allocates buffers and builds the two boolean mask tensors the 10-tuple returns. 
 without it, one device->host read of max(mel_len) sizes the decoder (the reference does
 B*L_max .item() syncs in LengthRegulator.expand).
 """
+from types import SimpleNamespace
+
 import numpy as np
 import torch
 
@@ -111,6 +113,126 @@ def _device_ok(dev):
     return dev.type == "cuda"
 
 
+def _streams_for(B):
+    """Utterance groups run as parallel HIP streams (parallel branches of a captured graph): one
+    group's partial last wave of workgroups and its launch ramps overlap the other group's work.
+    FS2_STREAMS groups (default 1: measured no gain under graph replay in round 1), each at least 8
+    utterances."""
+    import os
+    n = int(os.environ.get("FS2_STREAMS", "1"))
+    return max(1, min(n, B // 8))
+
+
+class _ForkJoin:
+    """n utterance groups on n side streams forked from / joined to the caller's stream (graph
+    capture turns them into parallel branches). n == 1 runs inline and touches no stream API."""
+
+    _cache = {}
+
+    def __init__(self, dev, n):
+        import contextlib
+
+        self.n = n
+        if n == 1:
+            self.ctx = lambda i: contextlib.nullcontext()
+            return
+        key = (str(dev), n)
+        if key not in self._cache:
+            self._cache[key] = [torch.cuda.Stream(device=dev) for _ in range(n)]
+        self.streams = self._cache[key]
+        self.main = torch.cuda.current_stream(dev)
+        self.ctx = lambda i: torch.cuda.stream(self.streams[i])
+
+    def fork(self):
+        if self.n > 1:
+            for s in self.streams:
+                s.wait_stream(self.main)
+
+    def join(self, *tensors):
+        """Main stream waits for every group; tensors made on side streams are marked as used by it."""
+        if self.n > 1:
+            for s in self.streams:
+                self.main.wait_stream(s)
+            for t in tensors:
+                if t is not None:
+                    t.record_stream(self.main)
+
+
+def _stage1(P, va, g, p_control, d_control):
+    """Encoder (+ conditioning), variance predictors, duration scan for one utterance group."""
+    x = ops.embed_pe(g.texts, P.enc_emb, _pe(P, "enc", g.Lx), P.act_dtype)
+    spk_vec = emo_vec = None
+    if P.spk_table is not None or P.emo_table is not None:
+        spk_vec, emo_vec = ops.cond_vectors(
+            g.speakers if P.spk_table is not None else None, P.spk_table,
+            g.emotions if P.emo_table is not None else None, g.arousals, g.valences, P.emo_table,
+            getattr(P, "aro_table", None), getattr(P, "val_table", None), getattr(P, "emo_w", None),
+            getattr(P, "emo_b", None), P.d_model)
+    n_enc = len(P.enc_layers)
+    for i, lp in enumerate(P.enc_layers):
+        last = i == n_enc - 1
+        x = fft_block(P, lp, x, g.lens_src, spk_vec if last else None, emo_vec if last else None)
+    if n_enc == 0 and (spk_vec is not None or emo_vec is not None):
+        raise NotImplementedError("encoder_layer = 0")
+
+    st = SimpleNamespace(x=x, p_pred=None, e_pred=None)
+    st.phoneme_p = va.pitch_feature_level == "phoneme_level"
+    st.phoneme_e = va.energy_feature_level == "phoneme_level"
+    st.log_d = variance_predictor(P.vp["duration"], x, g.lens_src)
+    if st.phoneme_p:
+        st.p_pred = _variance(P, "pitch", x, g.lens_src, g.p_targets, p_control)
+    if st.phoneme_e:
+        st.e_pred = _variance(P, "energy", x, g.lens_src, g.e_targets, p_control)  # p_control: modules.py:124-125
+    if g.d_targets is not None:
+        dur = g.d_targets
+        if dur.dtype not in (torch.int64, torch.float32):
+            dur = dur.to(torch.int64)
+        st.cum, st.mel_len, _ = ops.lr_durations(dur)
+        st.d_rounded = None
+    else:
+        st.cum, st.mel_len, st.d_rounded = ops.lr_durations(st.log_d, logpred=True, d_control=d_control)
+    return st
+
+
+def _stage2(P, g, st, T_out, T_dec, p_control):
+    """LengthRegulator gather, decoder, mel_linear, PostNet for one utterance group."""
+    dec_lens = st.mel_len if g.d_targets is None else g.mel_lens
+    frame_level = not (st.phoneme_p and st.phoneme_e)
+    x = st.x
+    if not frame_level and T_dec == T_out and packed_decoder_ok(P):
+        # packed decoder: only the dec_lens frames of each utterance are computed
+        # (cfg2: 24.9k of 27.5k rows, cfg4: 135k of 249k); mel_linear scatters back to [B, T, n_mel]
+        lay = ops.SeqLayout(dec_lens, T_dec)
+        x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype,
+                          out_layout=lay)
+        for lp in P.dec_layers:
+            x = fft_block(P, lp, x, None, timed=True, layout=lay)
+        mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
+                         out_dtype=L.FS2_F32, src_layout=lay)
+        return mel, _postnet(P, mel), st
+    # LR gather with the decoder's position encoding fused (frame-level variance needs the bare
+    # expanded x first, so the PE add moves to a second pass in that configuration)
+    if frame_level:
+        x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=None, out_dtype=P.act_dtype)
+        if not st.phoneme_p:
+            st.p_pred = _variance(P, "pitch", x, dec_lens, g.p_targets, p_control)
+        if not st.phoneme_e:
+            st.e_pred = _variance(P, "energy", x, dec_lens, g.e_targets, p_control)
+        x = x[:, :T_dec].contiguous()
+        x = _add_pe(x, _pe(P, "dec", T_dec))
+    else:
+        x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype)
+        if T_dec != T_out:
+            x = x[:, :T_dec].contiguous()
+    if T_dec != T_out:
+        dec_lens = torch.clamp(dec_lens, max=T_dec)
+    for lp in P.dec_layers:
+        x = fft_block(P, lp, x, dec_lens, timed=True)
+    mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
+                     out_dtype=L.FS2_F32)
+    return mel, _postnet(P, mel), st
+
+
 def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, max_src_len, mels, mel_lens,
                 max_mel_len, p_targets, e_targets, d_targets, p_control, e_control, d_control):
     dev = texts.device
@@ -120,7 +242,7 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     P = model.packed(dev)
     va = model.variance_adaptor
     ids = lambda t: None if t is None else torch.as_tensor(t).to(device=dev, dtype=torch.int64).contiguous()
-    speakers, emotions, arousals, valences = ids(speakers), ids(emotions), ids(arousals), ids(valences)
+    f32 = lambda t: None if t is None else t.to(device=dev, dtype=torch.float32).contiguous()
     B = texts.shape[0]
     Lx = int(max_src_len)
     if texts.shape[1] != Lx:
@@ -129,94 +251,67 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     src_masks = _mask(src_lens, Lx)
     mel_masks = _mask(mel_lens, max_mel_len if max_mel_len is not None else int(mel_lens.max().item())) \
         if mel_lens is not None else None
-    lens_src = src_lens.to(torch.int64).contiguous()
+    full = SimpleNamespace(
+        speakers=ids(speakers), emotions=ids(emotions), arousals=ids(arousals), valences=ids(valences),
+        texts=ids(texts), lens_src=src_lens.to(torch.int64).contiguous(), Lx=Lx,
+        p_targets=f32(p_targets), e_targets=f32(e_targets),
+        d_targets=None if d_targets is None else d_targets.to(dev),
+        mel_lens=None if mel_lens is None else mel_lens.to(dev).to(torch.int64).contiguous())
 
-    # ---- encoder (+ speaker / emotion conditioning fused into the last block's epilogue) -------
-    x = ops.embed_pe(ids(texts), P.enc_emb, _pe(P, "enc", Lx), P.act_dtype)
-    spk_vec = emo_vec = None
-    if P.spk_table is not None or P.emo_table is not None:
-        spk_vec, emo_vec = ops.cond_vectors(
-            speakers if P.spk_table is not None else None, P.spk_table,
-            emotions if P.emo_table is not None else None, arousals, valences, P.emo_table,
-            getattr(P, "aro_table", None), getattr(P, "val_table", None), getattr(P, "emo_w", None),
-            getattr(P, "emo_b", None), P.d_model)
-    n_enc = len(P.enc_layers)
-    for i, lp in enumerate(P.enc_layers):
-        last = i == n_enc - 1
-        x = fft_block(P, lp, x, lens_src, spk_vec if last else None, emo_vec if last else None)
-    if n_enc == 0 and (spk_vec is not None or emo_vec is not None):
-        raise NotImplementedError("encoder_layer = 0")
+    # utterance groups (contiguous ranges of b; same padded L / T as the whole batch, so every
+    # group's outputs are bit-identical to the one-group run)
+    n = _streams_for(B)
+    bounds = [(B * i // n, B * (i + 1) // n) for i in range(n)]
 
-    # ---- variance adaptor --------------------------------------------------------------------
-    phoneme_p = va.pitch_feature_level == "phoneme_level"
-    phoneme_e = va.energy_feature_level == "phoneme_level"
-    log_d = variance_predictor(P.vp["duration"], x, lens_src)
-    p_pred = e_pred = None
-    if phoneme_p:
-        p_pred = _variance(P, "pitch", x, lens_src, p_targets, p_control)
-    if phoneme_e:
-        e_pred = _variance(P, "energy", x, lens_src, e_targets, p_control)  # p_control: modules.py:124-125
+    def part(b0, b1):
+        sl = lambda t: None if t is None else t[b0:b1]
+        return SimpleNamespace(**{k: (sl(v) if torch.is_tensor(v) else v) for k, v in vars(full).items()})
 
-    if d_targets is not None:
-        dur = d_targets.to(dev)
-        if dur.dtype not in (torch.int64, torch.float32):
-            dur = dur.to(torch.int64)
-        cum, mel_len, _ = ops.lr_durations(dur)
-        d_rounded = d_targets
-    else:
-        cum, mel_len, d_rounded = ops.lr_durations(log_d, logpred=True, d_control=d_control)
+    groups = [part(b0, b1) for b0, b1 in bounds] if n > 1 else [full]
+    fj = _ForkJoin(dev, n)
+    fj.fork()
+    sts = []
+    for i, g in enumerate(groups):
+        with fj.ctx(i):
+            sts.append(_stage1(P, va, g, p_control, d_control))
+
+    mel_len = sts[0].mel_len if n == 1 else None
+    if not max_mel_len or d_targets is None:
+        # free-running: the decoder length is max(mel_len) over ALL groups (one host read)
+        if n > 1:
+            fj.join(*[st.mel_len for st in sts])
+            mel_len = torch.cat([st.mel_len for st in sts])
+            fj.fork()
     if max_mel_len:
         T_out = int(max_mel_len)
     else:
         T_out = int(mel_len.max().item()) if B else 0
     if d_targets is None:
         mel_masks = _mask(mel_len, int(mel_len.max().item()) if B else 0)
-    dec_lens = mel_len if d_targets is None else mel_lens.to(dev).to(torch.int64)
     if mel_masks is None or mel_masks.shape[1] != T_out:
         raise RuntimeError(f"decoder mask width {None if mel_masks is None else mel_masks.shape[1]} != length-"
                            f"regulated length {T_out} (the reference fails here too: Models.py:157)")
-    frame_level = not (phoneme_p and phoneme_e)
-    if model.training:
-        T_dec = min(T_out, P.max_seq_len)
-    else:
-        T_dec = T_out
-    if not frame_level and T_dec == T_out and packed_decoder_ok(P):
-        # packed decoder: only the dec_lens frames of each utterance are computed
-        # (cfg2: 24.9k of 27.5k rows, cfg4: 135k of 249k); mel_linear scatters back to [B, T, n_mel]
-        lay = ops.SeqLayout(dec_lens, T_dec)
-        x = ops.lr_expand(x, cum, mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype, out_layout=lay)
-        for lp in P.dec_layers:
-            x = fft_block(P, lp, x, None, timed=True, layout=lay)
-        mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
-                         out_dtype=L.FS2_F32, src_layout=lay)
-        postnet_mel = _postnet(P, mel)
-        return (mel, postnet_mel, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)
-    # LR gather with the decoder's position encoding fused (frame-level variance needs the bare
-    # expanded x first, so the PE add moves to a second pass in that configuration)
-    if frame_level:
-        x = ops.lr_expand(x, cum, mel_len, T_out, pe=None, out_dtype=P.act_dtype)
-        if not phoneme_p:
-            p_pred = _variance(P, "pitch", x, dec_lens, p_targets, p_control)
-        if not phoneme_e:
-            e_pred = _variance(P, "energy", x, dec_lens, e_targets, p_control)
-        x = x[:, :T_dec].contiguous()
-        x = _add_pe(x, _pe(P, "dec", T_dec))
-    else:
-        x = ops.lr_expand(x, cum, mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype)
-        if T_dec != T_out:
-            x = x[:, :T_dec].contiguous()
+    T_dec = min(T_out, P.max_seq_len) if model.training else T_out
     if T_dec != T_out:
         mel_masks = mel_masks[:, :T_dec]
-        dec_lens = torch.clamp(dec_lens, max=T_dec)
 
-    # ---- decoder --------------------------------------------------------------------------------
-    for lp in P.dec_layers:
-        x = fft_block(P, lp, x, dec_lens, timed=True)
-
-    # ---- mel_linear + PostNet (+ residual) -----------------------------------------------------
-    mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
-                     out_dtype=L.FS2_F32)
-    postnet_mel = _postnet(P, mel)
+    res = []
+    for i, (g, st) in enumerate(zip(groups, sts)):
+        with fj.ctx(i):
+            res.append(_stage2(P, g, st, T_out, T_dec, p_control))
+    if n == 1:
+        mel, postnet_mel, st = res[0]
+        out = (mel, postnet_mel, st.p_pred, st.e_pred, st.log_d, st.d_rounded, st.mel_len)
+    else:
+        fj.join(*[t for r in res for t in (r[0], r[1], r[2].p_pred, r[2].e_pred, r[2].log_d, r[2].d_rounded,
+                                           r[2].mel_len)])
+        cat = lambda ts: None if ts[0] is None else torch.cat(ts)
+        out = (cat([r[0] for r in res]), cat([r[1] for r in res]), cat([r[2].p_pred for r in res]),
+               cat([r[2].e_pred for r in res]), cat([r[2].log_d for r in res]),
+               cat([r[2].d_rounded for r in res]), cat([r[2].mel_len for r in res]))
+    mel, postnet_mel, p_pred, e_pred, log_d, d_rounded, mel_len = out
+    if d_targets is not None:
+        d_rounded = d_targets
     return (mel, postnet_mel, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)
 
 

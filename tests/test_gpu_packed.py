@@ -162,7 +162,8 @@ def test_mel_linear_from_packed(gpu, prec):
 
 
 def test_forward_packed_decoder_equals_padded_decoder(gpu):
-    """Whole forward, bf16 and fp32, cfg4-like ragged batch: packed decoder vs padded decoder.
+    """Whole forward, bf16 and fp32, cfg4-like ragged batch: packed decoder + 2 stream groups vs
+    padded decoder and vs one stream (all bit-identical).
     Runs the padded path in a child process (FS2_PACKED_DECODER is read per forward, but a
     child keeps this process's cached state untouched)."""
     code = r"""
@@ -178,27 +179,29 @@ m = FastSpeech2(pc, mc); fill_module(m, seed=0); m = m.to("cuda:0").eval()
 outs = {}
 for prec in ("fp32", "bf16"):
     m.set_precision(prec)
-    args = synth_batch(24, 8, 90, seed=4)
-    with torch.no_grad():
-        o = m(**to_device(args, "cuda:0"))
-    outs[prec] = [t.cpu() if torch.is_tensor(t) else t for t in o]
+    for teacher in (True, False):
+        args = synth_batch(24, 8, 90, seed=4, teacher=teacher)
+        with torch.no_grad():
+            o = m(**to_device(args, "cuda:0"))
+        outs[prec + ("" if teacher else "_free")] = [t.cpu() if torch.is_tensor(t) else t for t in o]
 torch.save(outs, sys.argv[1])
 """
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = {}
-    for flag in ("1", "0"):
-        path = f"/tmp/fs2_packed_{flag}_{os.getpid()}.pt"
-        env = dict(os.environ, FS2_PACKED_DECODER=flag, REPO=repo)
+    # default (packed decoder, 2 utterance-group streams) vs padded decoder vs one stream
+    for tag, packed, streams in (("default", "1", "2"), ("padded", "0", "2"), ("one_stream", "1", "1")):
+        path = f"/tmp/fs2_packed_{tag}_{os.getpid()}.pt"
+        env = dict(os.environ, FS2_PACKED_DECODER=packed, FS2_STREAMS=streams, REPO=repo)
         r = subprocess.run([sys.executable, "-c", code, path], env=env, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-3000:]
-        res[flag] = torch.load(path, weights_only=True)
+        res[tag] = torch.load(path, weights_only=True)
         os.unlink(path)
-    for prec in ("fp32", "bf16"):
-        a, b = res["1"][prec], res["0"][prec]
+    for prec, other in [(p, o) for p in ("fp32", "bf16", "fp32_free", "bf16_free") for o in ("padded", "one_stream")]:
+        a, b = res["default"][prec], res[other][prec]
         for i, (x, y) in enumerate(zip(a, b)):
             if torch.is_tensor(x):
                 assert x.shape == y.shape, (prec, i)
                 if x.is_floating_point():
-                    assert torch.equal(x, y), (prec, i, float((x.float() - y.float()).abs().max()))
+                    assert torch.equal(x, y), (prec, other, i, float((x.float() - y.float()).abs().max()))
                 else:
-                    assert torch.equal(x, y), (prec, i)
+                    assert torch.equal(x, y), (prec, other, i)

@@ -172,9 +172,24 @@ class _RecordingLib:
         return call
 
 
+class _FakeForkJoin:
+    def __init__(self, dev, n):
+        import contextlib
+
+        self.n = n
+        self.ctx = lambda i: contextlib.nullcontext()
+
+    def fork(self):
+        pass
+
+    def join(self, *t):
+        pass
+
+
 @pytest.mark.parametrize("packed", ["1", "0"])
 @pytest.mark.parametrize("teacher", [True, False])
-def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher):
+@pytest.mark.parametrize("streams", ["1", "2"])
+def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher, streams):
     """The forward's Python plumbing (shapes, strides, descriptors, layouts) on CPU with the
     kernels stubbed: no GPU needed, catches argument errors before any GPU time is spent."""
     from fs2amd import ops, runtime, _lib
@@ -186,8 +201,10 @@ def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher):
     monkeypatch.setattr(ops, "_stream", lambda *a: None)
     monkeypatch.setattr(runtime, "_device_ok", lambda dev: True)
     monkeypatch.setenv("FS2_PACKED_DECODER", packed)
+    monkeypatch.setenv("FS2_STREAMS", streams)
+    monkeypatch.setattr(runtime, "_ForkJoin", _FakeForkJoin)
     m = _model().eval()
-    args = synth_batch(3, 6, 11, seed=2, teacher=teacher)
+    args = synth_batch(17, 6, 11, seed=2, teacher=teacher)
     if not teacher:
         # the stubbed duration kernel writes nothing: give mel_len a defined size
         real_lr = ops.lr_durations
@@ -201,8 +218,10 @@ def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher):
     with torch.no_grad():
         out = m(**args)
     assert len(out) == 10 and out[0].shape[-1] == 80 and out[1].shape == out[0].shape
+    assert out[0].shape[0] == 17 and out[9].shape == (17,)
     n_conv = rec.calls.count("fs2_conv1d")
-    # 10 FFT blocks x 4 GEMMs + 3 VPs x 2 + mel_linear + 5 PostNet convs
-    assert n_conv == 10 * 4 + 6 + 1 + 5, rec.calls
-    assert rec.calls.count("fs2_attention") == 10
+    k = int(streams)
+    # per group: 10 FFT blocks x 4 GEMMs + 3 VPs x 2 + mel_linear + 5 PostNet convs
+    assert n_conv == k * (10 * 4 + 6 + 1 + 5), rec.calls
+    assert rec.calls.count("fs2_attention") == k * 10
     assert ("fs2_seq_layout" in rec.calls) == (packed == "1")

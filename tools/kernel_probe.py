@@ -37,25 +37,27 @@ def main():
     g = torch.Generator().manual_seed(0)
     rnd = lambda *s: torch.randn(*s, generator=g).to(dev, dt)
     lens = b["mel_lens"]
+    # decoder kernels run on packed valid frames, as in the forward (runtime._stage2)
+    lay = ops.SeqLayout(lens, T)
     if a.kernel == "conv9":
-        h = rnd(B, T, 256)
+        h = rnd(B * T, 256)
         fn = lambda: ops.conv1d(h, lp.w1, lp.b1, cin=256, ks=9, pad=4, compute=P.compute, epilogue=L.EPI_BIAS_RELU,
-                                out_dtype=P.act_dtype)
+                                out_dtype=P.act_dtype, layout=lay)
     elif a.kernel == "conv1":
-        f, h = rnd(B, T, 1024), rnd(B, T, 256)
+        f, h = rnd(B * T, 1024), rnd(B * T, 256)
         fn = lambda: ops.conv1d(f, lp.w2, lp.b2, cin=1024, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_RES_LN,
-                                out_dtype=P.act_dtype, residual=h, ln=lp.ln2, lens=lens)
+                                out_dtype=P.act_dtype, residual=h, ln=lp.ln2, layout=lay)
     elif a.kernel == "qkv":
-        h = rnd(B, T, 256)
+        h = rnd(B * T, 256)
         fn = lambda: ops.conv1d(h, lp.wqkv, lp.bqkv, cin=256, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
-                                out_dtype=P.act_dtype)
+                                out_dtype=P.act_dtype, layout=lay)
     elif a.kernel == "attn":
-        qkv = rnd(B, T, 768)
-        fn = lambda: ops.attention(qkv, lens, 2, 128, 128 ** 0.5)
+        qkv = rnd(B * T, 768)
+        fn = lambda: ops.attention(qkv, None, 2, 128, 128 ** 0.5, layout=lay)
     elif a.kernel == "lr":
         x = rnd(B, 64, 256)
         cum, ml, _ = ops.lr_durations(b["d_targets"])
-        fn = lambda: ops.lr_expand(x, cum, ml, T, pe=P.dec_pe, out_dtype=P.act_dtype)
+        fn = lambda: ops.lr_expand(x, cum, ml, T, pe=P.dec_pe, out_dtype=P.act_dtype, out_layout=lay)
     elif a.kernel == "lr4":  # LR stress shape (cfg4: B=256, L 16..160, T ~1000), bf16 + PE
         b4 = to_device(synth_batch(256, 16, 160, seed=1), dev)
         x4 = torch.randn(256, b4["texts"].shape[1], 256, generator=g).to(dev, dt)
