@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="replay the forward as a captured HIP graph")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--kernel-reps", type=int, default=20)
+    ap.add_argument("--mode", default="infer", choices=["infer", "train"],
+                    help="infer: the headline cfg2 forward; train: the cfg3 train.py step (B=16/GPU, DDP)")
     return ap.parse_args()
 
 
@@ -164,11 +166,57 @@ def load_traffic():
     return None
 
 
+def main_train(args, rank, world, device):
+    """cfg3: one train.py step per iteration (forward, FastSpeech2Loss, backward, RCCL gradient
+    all-reduce, clip, ScheduledOptim) on B=16 utterances per GPU, lengths U{16..64}, mel / pitch
+    / energy targets N(0,1). value = mel frames of all ranks per second."""
+    from fs2amd import config as C
+    from fs2amd import parallel
+    from fs2amd.data import synth_batch, to_device
+    from fs2amd.trainer import TrainStep
+
+    model, pc, mc = build_model(device, args.dtype)
+    _, _, tc = C.synthetic_configs(tempfile.mkdtemp(prefix="fs2_bench_tc_"))
+    B = 16
+    batch_cpu = synth_batch(B, 16, 64, seed=1 + rank, with_mels=True, pe_targets=True)
+    batch = to_device(batch_cpu, device)
+    frames = int(batch_cpu["mel_lens"].sum())
+    step = TrainStep(model, pc, mc, tc, device=device, world_size=world)
+    for _ in range(max(1, args.warmup)):
+        step(batch)
+    torch.cuda.synchronize(device)
+    parallel.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses = step(batch)
+    torch.cuda.synchronize(device)
+    parallel.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed, tot_frames = parallel.aggregate(elapsed, frames, device)
+    rec = {
+        "metric": "train mel-frames/sec (cfg3 train.py step, batch 16/GPU, DDP over RCCL)",
+        "value": round(tot_frames * args.steps / elapsed, 1), "unit": "mel-frames/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (pinyin ids U{64..107}, lengths U{16..64}, durations U{2..10}, mel/pitch/energy "
+                "targets N(0,1); counter-generated random-init weights)",
+        "config": {"workload": "cfg3: FastSpeech2 train step, ESD-Chinese-Singing-MFA model.yaml",
+                   "global_batch": B * world, "parallelism": f"dp{world} (DDP, 32 MB buckets)"},
+        "loss": round(float(losses[0]), 5),
+    }
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    parallel.shutdown()
+
+
 def main():
     args = parse()
     from fs2amd import parallel
 
     rank, local, world, device = parallel.init("nccl")
+    if args.mode == "train":
+        return main_train(args, rank, world, device)
 
     from fs2amd.data import synth_batch, to_device
 

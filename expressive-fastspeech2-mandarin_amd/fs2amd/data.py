@@ -42,6 +42,13 @@ def synth_batch(B, L_min, L_max=None, seed=1, d_range=(2, 10), teacher=True, pe_
     return args
 
 
+def loss_inputs(args):
+    """The reference batch tuple as FastSpeech2Loss indexes it (``inputs[9:]`` = mels, mel_lens,
+    max_mel_len, pitches, energies, durations; dataset_chinese.py collate order)."""
+    return (None,) * 9 + (args["mels"], args["mel_lens"], args["max_mel_len"], args["p_targets"],
+                          args["e_targets"], args["d_targets"])
+
+
 def to_device(args, device):
     return {k: (v.to(device) if torch.is_tensor(v) else v) for k, v in args.items()}
 

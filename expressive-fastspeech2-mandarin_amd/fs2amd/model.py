@@ -201,6 +201,7 @@ class FastSpeech2(nn.Module):
         self._precision = hip.get("dtype", os.environ.get("FS2_HIP_DTYPE", "fp32"))
         self._vp_precision = hip.get("vp_dtype", os.environ.get("FS2_HIP_VP_DTYPE", "fp32"))
         self._packs = {}
+        self.train_dropout = True  # False: train-mode semantics without dropout (parity tests)
         self.register_load_state_dict_post_hook(lambda mod, keys: mod.invalidate_packed())
 
     # ---- precision / packed weights --------------------------------------------------------------
@@ -239,10 +240,13 @@ class FastSpeech2(nn.Module):
     def forward(self, speakers, emotions, arousals, valences, texts, src_lens, max_src_len, mels=None, mel_lens=None,
                 max_mel_len=None, p_targets=None, e_targets=None, d_targets=None, p_control=1.0, e_control=1.0,
                 d_control=1.0):
-        if self.training and torch.is_grad_enabled():
-            raise NotImplementedError(
-                "fs2amd: the HIP forward is inference-only in this build (model.eval() / torch.no_grad()); "
-                "training (dropout, batch-stat BatchNorm, backward) is not implemented yet")
+        if self.training:
+            # train.py step: dropout, batch-statistic BatchNorm, autograd (fs2amd/training.py)
+            from .training import train_forward
+
+            return train_forward(self, speakers, emotions, arousals, valences, texts, src_lens, max_src_len, mels,
+                                 mel_lens, max_mel_len, p_targets, e_targets, d_targets, p_control, e_control,
+                                 d_control)
         from .runtime import run_forward
 
         return run_forward(self, speakers, emotions, arousals, valences, texts, src_lens, max_src_len, mels, mel_lens,

@@ -87,13 +87,13 @@ def fft_block(sd, pre, x, mask, slf_mask, n_head, kernel_size):
     return out.masked_fill(mask.unsqueeze(-1), 0)
 
 
-def encoder(sd, cfg, src_seq, mask):
-    """ref transformer/Models.py:73-100 (eval)."""
+def encoder(sd, cfg, src_seq, mask, training=False):
+    """ref transformer/Models.py:73-100 (dropout identity; training only changes the PE rule :82)."""
     tr = cfg["transformer"]
     batch_size, max_len = src_seq.shape
     slf_mask = mask.unsqueeze(1).expand(-1, max_len, -1)
     emb = F.embedding(src_seq, sd["encoder.src_word_emb.weight"], padding_idx=0)
-    if max_len > cfg["max_seq_len"]:
+    if not training and max_len > cfg["max_seq_len"]:
         pe = sinusoid_table(max_len, tr["encoder_hidden"])[:max_len, :].unsqueeze(0).expand(batch_size, -1, -1)
     else:
         pe = sd["encoder.position_enc"][:, :max_len, :].expand(batch_size, -1, -1)
@@ -103,11 +103,11 @@ def encoder(sd, cfg, src_seq, mask):
     return out
 
 
-def decoder(sd, cfg, enc_seq, mask):
-    """ref transformer/Models.py:139-171 (eval)."""
+def decoder(sd, cfg, enc_seq, mask, training=False):
+    """ref transformer/Models.py:139-171 (dropout identity; training crops to max_seq_len, :145-162)."""
     tr = cfg["transformer"]
     batch_size, max_len = enc_seq.shape[0], enc_seq.shape[1]
-    if max_len > cfg["max_seq_len"]:
+    if not training and max_len > cfg["max_seq_len"]:
         slf_mask = mask.unsqueeze(1).expand(-1, max_len, -1)
         out = enc_seq + sinusoid_table(max_len, tr["decoder_hidden"])[:max_len, :].unsqueeze(0).expand(batch_size, -1, -1)
     else:
@@ -121,15 +121,16 @@ def decoder(sd, cfg, enc_seq, mask):
     return out, mask
 
 
-def postnet(sd, x):
-    """ref transformer/Layers.py:129-137 (+ ConvNorm :33-64; BatchNorm1d eval; dropout identity)."""
+def postnet(sd, x, training=False):
+    """ref transformer/Layers.py:129-137 (+ ConvNorm :33-64; dropout identity). training: BatchNorm1d
+    uses batch statistics over (B, T) and updates the running buffers in ``sd`` in place."""
     x = x.contiguous().transpose(1, 2)
     n = 5
     for i in range(n):
         pre = f"postnet.convolutions.{i}."
         y = F.conv1d(x, sd[pre + "0.conv.weight"], sd[pre + "0.conv.bias"], padding=2)
         y = F.batch_norm(y, sd[pre + "1.running_mean"], sd[pre + "1.running_var"], sd[pre + "1.weight"],
-                         sd[pre + "1.bias"], False, 0.1, 1e-5)
+                         sd[pre + "1.bias"], training, 0.1, 1e-5)
         x = torch.tanh(y) if i < n - 1 else y
     return x.contiguous().transpose(1, 2)
 
@@ -220,12 +221,13 @@ def variance_adaptor(sd, cfg, pcfg, x, src_mask, mel_mask, max_len, p_t, e_t, d_
 # ---------------------------------------------------------------- top level
 def forward(sd, model_config, preprocess_config, speakers, emotions, arousals, valences, texts, src_lens,
             max_src_len, mels=None, mel_lens=None, max_mel_len=None, p_targets=None, e_targets=None,
-            d_targets=None, p_control=1.0, e_control=1.0, d_control=1.0):
-    """ref model/fastspeech2.py:73-148 (eval). Returns the reference's 10-tuple."""
+            d_targets=None, p_control=1.0, e_control=1.0, d_control=1.0, training=False):
+    """ref model/fastspeech2.py:73-148. Returns the reference's 10-tuple. ``training``: train-mode
+    semantics with every dropout disabled (BN batch statistics, decoder crop), differentiable."""
     cfg = model_config
     src_masks = mask_from_lengths(src_lens, max_src_len)
     mel_masks = mask_from_lengths(mel_lens, max_mel_len) if mel_lens is not None else None
-    output = encoder(sd, cfg, texts, src_masks)
+    output = encoder(sd, cfg, texts, src_masks, training)
     if cfg["multi_speaker"]:
         output = output + F.embedding(speakers, sd["speaker_emb.weight"]).unsqueeze(1).expand(-1, max_src_len, -1)
     if cfg["multi_emotion"]:
@@ -236,10 +238,29 @@ def forward(sd, model_config, preprocess_config, speakers, emotions, arousals, v
     (output, p_pred, e_pred, log_d, d_rounded, mel_lens, mel_masks) = variance_adaptor(
         sd, cfg, preprocess_config, output, src_masks, mel_masks, max_mel_len, p_targets, e_targets, d_targets,
         p_control, e_control, d_control)
-    output, mel_masks = decoder(sd, cfg, output, mel_masks)
+    output, mel_masks = decoder(sd, cfg, output, mel_masks, training)
     output = F.linear(output, sd["mel_linear.weight"], sd["mel_linear.bias"])
-    postnet_output = postnet(sd, output) + output
+    postnet_output = postnet(sd, output, training) + output
     return (output, postnet_output, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_lens)
+
+
+def loss(preprocess_config, mels, pitches, energies, durations, predictions):
+    """ref model/loss.py:19-92: (total, mel L1, postnet L1, pitch MSE, energy MSE, log-duration MSE)
+    over un-padded positions; mel targets cropped to the prediction's frames (:41-42)."""
+    mel_pred, post_pred, p_pred, e_pred, log_d, _, src_masks, mel_masks, _, _ = predictions
+    src_valid, mel_valid = ~src_masks, ~mel_masks
+    log_d_t = torch.log(durations.float() + 1)
+    mels = mels[:, : mel_valid.shape[1], :]
+    sel = lambda lvl: src_valid if lvl == "phoneme_level" else mel_valid
+    pp = preprocess_config["preprocessing"]
+    p_m, e_m = sel(pp["pitch"]["feature"]), sel(pp["energy"]["feature"])
+    mv = mel_valid.unsqueeze(-1)
+    mel_l = F.l1_loss(mel_pred.masked_select(mv), mels.masked_select(mv))
+    post_l = F.l1_loss(post_pred.masked_select(mv), mels.masked_select(mv))
+    p_l = F.mse_loss(p_pred.masked_select(p_m), pitches.masked_select(p_m))
+    e_l = F.mse_loss(e_pred.masked_select(e_m), energies.masked_select(e_m))
+    d_l = F.mse_loss(log_d.masked_select(src_valid), log_d_t.masked_select(src_valid))
+    return mel_l + post_l + d_l + p_l + e_l, mel_l, post_l, p_l, e_l, d_l
 
 
 def build_state_dict(model_config, preprocess_config, stats, generated):

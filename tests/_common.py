@@ -54,3 +54,41 @@ def load_case(name):
             outs[k[4:]] = z[k]
     controls = tuple(float(c) for c in z["controls"])
     return args, controls, outs, z
+
+
+def load_train_case():
+    """tests/golden/train_grads.npz: inputs, reference losses, per-parameter gradient sums /
+    sums of squares / 16 sampled elements, BN running stats after the step."""
+    z = np.load(os.path.join(GOLDEN, "train_grads.npz"))
+    args = {}
+    for k in z.files:
+        if k.startswith("in_"):
+            v = z[k]
+            args[k[3:]] = int(v) if v.ndim == 0 else torch.from_numpy(v)
+    return z, args
+
+
+def check_train_grads(z, named_grads, rtol, sample_atol_frac):
+    """Compare {name: grad} with the reference fixture: per-key sum of squares (relative),
+    sum (relative to sqrt(numel)*rms) and sampled elements (to a fraction of the key's rms)."""
+    keys = [str(k) for k in z["grad_keys"]]
+    assert set(keys) == set(named_grads.keys()), set(keys) ^ set(named_grads.keys())
+    # gradients that are analytically zero (attention key biases: softmax ignores a per-row
+    # shift) are roundoff noise on both sides: bounded absolutely against the model-wide scale
+    rms_all = [(float(z["grad_sumsq"][j]) / named_grads[k].numel()) ** 0.5 for j, k in enumerate(keys)]
+    scale = max(rms_all)
+    worst = {}
+    for j, k in enumerate(keys):
+        g = named_grads[k].detach().double().cpu().reshape(-1)
+        ss_ref, s_ref = float(z["grad_sumsq"][j]), float(z["grad_sum"][j])
+        rms = (ss_ref / g.numel()) ** 0.5
+        if rms < 1e-5 * scale:
+            assert float(g.abs().max()) <= 1e-4 * scale, (k, float(g.abs().max()), scale)
+            continue
+        e_ss = abs(float((g * g).sum()) - ss_ref) / ss_ref
+        e_s = abs(float(g.sum()) - s_ref) / (rms * g.numel() ** 0.5)
+        idx = torch.from_numpy(z[f"gidx_{j}"])
+        e_v = float((g[idx] - torch.from_numpy(z[f"gval_{j}"]).double()).abs().max()) / rms
+        worst[k] = (e_ss, e_s, e_v)
+        assert e_ss <= rtol and e_s <= rtol and e_v <= sample_atol_frac, (k, e_ss, e_s, e_v)
+    return worst

@@ -135,6 +135,52 @@ def lr_cases(LR):
     print("lr_cases:", list(cases))
 
 
+def train_case(FastSpeech2, pc, mc, sd):
+    """One reference training step's gradients (train mode: BatchNorm batch statistics, decoder
+    crop to max_seq_len), with every dropout disabled so the step is deterministic: nn.Dropout
+    modules get p = 0 and the PostNet's hard-coded F.dropout(0.5) (transformer/Layers.py:133-134)
+    is replaced by identity for the duration of this case only."""
+    import torch.nn.functional as F
+    from model.loss import FastSpeech2Loss
+    from fs2amd.data import loss_inputs
+
+    m = FastSpeech2(pc, mc)
+    m.load_state_dict(sd)
+    m.train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    args = synth_batch(4, 10, 24, seed=11, with_mels=True, pe_targets=True)
+    orig = F.dropout
+    F.dropout = lambda x, p=0.5, training=False, inplace=False: x
+    try:
+        out = m(**args)
+        losses = FastSpeech2Loss(pc, mc)(loss_inputs(args), out)
+        losses[0].backward()
+    finally:
+        F.dropout = orig
+    rec = {"in_" + k: t2n(v) for k, v in args.items() if v is not None}
+    rec["losses"] = np.array([float(l) for l in losses], dtype=np.float64)
+    keys = [k for k, p in m.named_parameters() if p.grad is not None]
+    rec["grad_keys"] = np.array(keys)
+    rec["grad_sum"] = np.array([float(p.grad.double().sum()) for k, p in m.named_parameters() if k in keys])
+    rec["grad_sumsq"] = np.array([float((p.grad.double() ** 2).sum()) for k, p in m.named_parameters() if k in keys])
+    g = torch.Generator().manual_seed(3)
+    params = dict(m.named_parameters())
+    for i, k in enumerate(keys):  # samples keyed by position in grad_keys
+        flat = params[k].grad.detach().reshape(-1)
+        idx = torch.randint(0, flat.numel(), (16,), generator=g)
+        rec[f"gidx_{i}"] = idx.numpy()
+        rec[f"gval_{i}"] = flat[idx].numpy()
+    for name, buf in m.named_buffers():
+        if "running_" in name:
+            rec["bn_" + name] = t2n(buf)
+    rec["out_mel_lens"] = t2n(out[9])
+    path = os.path.join(HERE, "train_grads.npz")
+    np.savez_compressed(path, **rec)
+    print(f"train_grads: {os.path.getsize(path) / 1e3:.1f} kB, {len(keys)} grads, losses {rec['losses']}")
+
+
 def main(only=None):
     FastSpeech2, LR = import_reference()
     torch.manual_seed(0)
@@ -147,6 +193,9 @@ def main(only=None):
     torch.set_num_threads(8)
 
     sd = model.state_dict()
+    if only == "train":
+        train_case(FastSpeech2, pc, mc, sd)
+        return
     manifest = {"reference": REF, "torch": torch.__version__, "weights_seed": 0, "n_keys": len(sd), "keys": {}}
     for k, v in sd.items():
         a = v.detach().double()
@@ -176,7 +225,8 @@ def main(only=None):
     np.savez_compressed(os.path.join(HERE, "cfg4_lr_index.npz"), d=b4["d_targets"].numpy().astype(np.int16),
                         index_map=im.astype(np.int16), mel_len=ml, max_mel_len=np.array(b4["max_mel_len"]))
     print("cfg4 lr index:", im.shape)
+    train_case(FastSpeech2, pc, mc, sd)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

@@ -63,3 +63,81 @@ def test_gloo_world2_aggregation():
     assert total == full
     for r, e, f, _ in res:
         assert e == 1.5 and f == full
+
+
+def _ddp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.manual_seed(0)
+    from _stubs import install_training_stubs
+    from _common import configs
+    from fs2amd import parallel
+    from fs2amd.model import FastSpeech2
+    from fs2amd.synth_weights import fill_module
+    from fs2amd.trainer import TrainStep
+
+    install_training_stubs(setattr)
+    r, _, w, dev = parallel.init("gloo")
+    pc, mc, tc = configs()
+    m = FastSpeech2(pc, mc)
+    fill_module(m, seed=0)
+    m.train_dropout = False
+    step = TrainStep(m, pc, mc, tc, device=None, world_size=w, bucket_mb=4)
+    b = shard(synth_batch(4, 6, 10, seed=9, with_mels=True, pe_targets=True), r, w)
+    losses = step(b)
+    q.put((r, float(losses[0]), {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()}))
+    parallel.shutdown()
+
+
+def test_ddp_train_step_gloo_world2(monkeypatch):
+    """TrainStep over gloo, world 2 (kernels stubbed on CPU, torch ops real): after one step both
+    ranks hold identical parameters, equal to one process applying the mean of the two ranks'
+    gradients (DDP's all-reduce semantics) with the same ScheduledOptim step."""
+    from _common import configs
+    from _stubs import install_training_stubs
+    from fs2amd.data import loss_inputs
+    from fs2amd.loss import FastSpeech2Loss
+    from fs2amd.model import FastSpeech2
+    from fs2amd.optimizer import ScheduledOptim
+    from fs2amd.synth_weights import fill_module
+
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sd0 = {k: torch.from_numpy(v) for k, v in res[0][2].items()}
+    sd1 = {k: torch.from_numpy(v) for k, v in res[1][2].items()}
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
+
+    # single-process reference: mean of the per-shard gradients, same optimizer step
+    install_training_stubs(monkeypatch.setattr)
+    pc, mc, tc = configs()
+    m = FastSpeech2(pc, mc)
+    fill_module(m, seed=0)
+    m.train().train_dropout = False
+    full = synth_batch(4, 6, 10, seed=9, with_mels=True, pe_targets=True)
+    grads = {}
+    for r in range(world):
+        b = shard(full, r, world)
+        m.zero_grad()
+        out = m(**b)
+        FastSpeech2Loss(pc, mc)(loss_inputs(b), out)[0].backward()
+        for k, p in m.named_parameters():
+            if p.grad is not None:
+                grads[k] = grads.get(k, 0) + p.grad / world
+    for k, p in m.named_parameters():
+        p.grad = grads.get(k)
+    torch.nn.utils.clip_grad_norm_(m.parameters(), tc["optimizer"]["grad_clip_thresh"])
+    opt = ScheduledOptim(m, tc, mc, 0)
+    opt.step_and_update_lr()
+    for k, v in m.state_dict().items():
+        if "running_" in k or "num_batches" in k:
+            continue  # BN buffers: rank 0's batch statistics (broadcast_buffers)
+        torch.testing.assert_close(sd0[k], v, rtol=1e-5, atol=1e-7, msg=k)

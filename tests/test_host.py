@@ -126,7 +126,7 @@ def test_packing_batchnorm_fold_and_layouts():
     assert Pb.postnet[0].w.shape == (512, 5, 128)
 
 
-def test_forward_refuses_cpu_and_training():
+def test_forward_refuses_cpu_tensors_eval_and_train():
     from fs2amd.data import synth_batch
 
     m = _model().eval()
@@ -134,8 +134,8 @@ def test_forward_refuses_cpu_and_training():
         with torch.no_grad():
             m(**synth_batch(1, 8, seed=3))
     m.train()
-    with pytest.raises(NotImplementedError):
-        m(**synth_batch(1, 8, seed=3))
+    with pytest.raises(RuntimeError, match="HIP"):
+        m(**synth_batch(1, 8, seed=3, with_mels=True, pe_targets=True))
 
 
 def test_drop_in_import_path():
@@ -152,24 +152,7 @@ def test_drop_in_import_path():
     assert hasattr(mod, "FastSpeech2Loss") and hasattr(mod, "ScheduledOptim")
 
 
-class _RecordingLib:
-    """Stands in for libfs2hip.so: records every launch entry point call, returns FS2_OK.
-    Host-only helpers (cin_pad, version strings) go to the real library."""
-
-    HOST = {"fs2_conv_cin_pad", "fs2_status_string", "fs2_version"}
-
-    def __init__(self, real):
-        self.real, self.calls = real, []
-
-    def __getattr__(self, name):
-        if name in self.HOST:
-            return getattr(self.real, name)
-
-        def call(*args):
-            self.calls.append(name)
-            return 0
-
-        return call
+from _stubs import RecordingLib as _RecordingLib  # noqa: E402
 
 
 class _FakeForkJoin:
@@ -225,3 +208,27 @@ def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher, streams):
     assert n_conv == k * (10 * 4 + 6 + 1 + 5), rec.calls
     assert rec.calls.count("fs2_attention") == k * 10
     assert ("fs2_seq_layout" in rec.calls) == (packed == "1")
+
+
+def test_training_step_dry_run(monkeypatch):
+    """train.py's step (forward, FastSpeech2Loss, backward) through fs2amd.training on CPU with the
+    kernels stubbed (zeros) and the LR scan / masks done by the test: checks the autograd graph
+    reaches exactly the parameters the reference's own step gives gradients to."""
+    import numpy as np
+    from fs2amd.data import loss_inputs, synth_batch
+    from fs2amd.loss import FastSpeech2Loss
+    from _common import GOLDEN
+    from _stubs import install_training_stubs
+
+    lib = install_training_stubs(monkeypatch.setattr)
+    pc, mc, _ = configs()
+    m = _model().train()
+    args = synth_batch(3, 5, 9, seed=4, with_mels=True, pe_targets=True)
+    out = m(**args)
+    assert out[0].shape == (3, int(args["max_mel_len"]), 80)
+    losses = FastSpeech2Loss(pc, mc)(loss_inputs(args), out)
+    losses[0].backward()
+    got = {k for k, p in m.named_parameters() if p.grad is not None}
+    ref = {str(k) for k in np.load(f"{GOLDEN}/train_grads.npz")["grad_keys"]}
+    assert got == ref, got ^ ref
+    assert "fs2_conv1d" in lib.calls and "fs2_attention" in lib.calls

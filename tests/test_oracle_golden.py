@@ -54,3 +54,27 @@ def test_oracle_lr_cases(golden_dir):
                                          None if ml < 0 else ml)
         np.testing.assert_array_equal(out.numpy(), z[f"{n}__out"], err_msg=n)
         np.testing.assert_array_equal(mel_len.numpy(), z[f"{n}__mel_len"], err_msg=n)
+
+
+def test_oracle_training_step_matches_reference_gradients():
+    """Train-mode forward (dropout disabled, BN batch statistics) + FastSpeech2Loss + backward of
+    the oracle against the reference's own gradients (tests/golden/train_grads.npz)."""
+    from _common import check_train_grads, load_train_case, oracle_state_dict
+    from oracle import fs2_oracle as O
+
+    z, args = load_train_case()
+    pc, mc, _ = configs()
+    sd = oracle_state_dict()
+    keys = [str(k) for k in z["grad_keys"]]
+    for k in keys:
+        sd[k] = sd[k].clone().requires_grad_(True)
+    out = O.forward(sd, mc, pc, **args, training=True)
+    losses = O.loss(pc, args["mels"], args["p_targets"], args["e_targets"], args["d_targets"], out)
+    np.testing.assert_allclose([float(l) for l in losses], z["losses"], rtol=1e-6)
+    losses[0].backward()
+    named = {k: sd[k].grad for k in keys}
+    check_train_grads(z, named, rtol=1e-5, sample_atol_frac=1e-4)
+    for k in z.files:
+        if k.startswith("bn_"):
+            np.testing.assert_allclose(sd[k[3:]].detach().numpy(), z[k], rtol=1e-5, atol=1e-6)
+
