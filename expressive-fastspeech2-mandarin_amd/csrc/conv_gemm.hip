@@ -115,6 +115,7 @@ struct ConvArgs {
   const float *bias;
   int B, T, Cin, Cin_pad, N, KS, pad, M;
   int ntn;  // number of N tiles
+  int ngr;  // N tiles per group in the tile order (== ntn: N-fastest over the whole row)
   uint32_t x_bytes, w_bytes;
   int epi;
   const void *res;
@@ -150,7 +151,13 @@ __device__ __forceinline__ bool conv_tile(const ConvArgs &a, int &M, int &m0, in
   if (id >= nwg) return false;
   const int q = nwg >> 3, rem = nwg & 7, xcd = id & 7, li = id >> 3;
   const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + li;  // bijective
-  const int mt = tile / a.ntn, nt = tile - mt * a.ntn;
+  // tile order: N groups of ngr tiles outermost, then M panels, then the group's N tiles, so the
+  // tiles an XCD runs at once share ngr/ntn of the weights (large weight matrices: the whole
+  // matrix would not fit one XCD's 4 MiB L2) and each A panel across the group
+  const int mtc = nwg / a.ntn;  // M panels
+  const int per_group = mtc * a.ngr;
+  const int grp = tile / per_group, r = tile - grp * per_group;
+  const int mt = r / a.ngr, nt = grp * a.ngr + (r - (r / a.ngr) * a.ngr);
   m0 = mt * BM;
   n0 = nt * BN;
   return true;
@@ -795,6 +802,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
 
 void launch_8p(ConvArgs a, hipStream_t s) {
   a.ntn = (a.N + 255) / 256;
+  a.ngr = a.ntn;
   const int nwg = ((a.M + 255) / 256) * a.ntn;
   hipLaunchKernelGGL(conv_gemm_8p_kernel, dim3(nwg), dim3(512), 0, s, a);
 }
@@ -984,6 +992,7 @@ template <int CT, int WGM, int WMI, int NS>
 void launch_ring(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM;
   a.ntn = 1;
+  a.ngr = 1;
   const int nwg = (a.M + BM - 1) / BM;
   hipLaunchKernelGGL((conv_gemm_ring_kernel<CT, WGM, WMI, NS>), dim3(nwg), dim3(256 * WGM), 0, s, a);
 }
@@ -993,6 +1002,17 @@ void launch(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM, BN = 64 * WGN;
   constexpr bool GL = std::is_same<TIn, typename CTraits<CT>::T>::value;  // LDS-DMA needs no conversion
   a.ntn = (a.N + BN - 1) / BN;
+  a.ngr = a.ntn;
+  static const bool grouped = [] {
+    const char *e = getenv("FS2_CONV_NGROUP");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (grouped && a.w_bytes > (2u << 20) && a.ntn > 4)  // weights > 2 MiB: groups of <= 4 N tiles
+    for (int g = 4; g >= 1; --g)
+      if (a.ntn % g == 0) {
+        a.ngr = g;
+        break;
+      }
   const int nwg = ((a.M + BM - 1) / BM) * a.ntn;
   hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, WMI, KSMAX, TIn, GL>), dim3(nwg), dim3(64 * WGM * WGN), 0, s, a);
 }
