@@ -177,13 +177,15 @@ __device__ __forceinline__ void store_any4(void *p, int dt, int64_t off, const f
 }
 
 // Epilogue of one BM x BN tile whose f32 accumulators sit in LDS (E, row stride BN + 4).
-template <int BM, int BN, int NWAVES>
+// (Prefetching every row's residual before the LN row loop was measured 3-5 % slower on the
+// LN GEMMs in round 1: more registers, and the row loop is not latency-bound.)
+template <int BM, int BN, int NWAVES, bool LN = true>
 __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int m0, int n0, int tid, int M) {
   constexpr int EPI_LD = BN + 4;
   const int lane = tid & 63, wid = tid >> 6;
   const int T = a.T;
   const int epi = a.epi;
-  if (epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN || epi == FS2_EPI_RELU_LN_DOT) {
+  if constexpr (LN) if (epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN || epi == FS2_EPI_RELU_LN_DOT) {
     // one wave per row; N == BN == 256 (checked on the host), lane owns columns 4*lane..4*lane+3
     const int n = lane * 4;
     float bias4[4], g4[4], be4[4];
@@ -253,19 +255,23 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
     return;
   }
 
+  // elementwise epilogues: each thread keeps one 4-column group (threads % (BN/4) == 0), so its
+  // bias is loaded once; rows step by threads / (BN/4)
   constexpr int G = BN / 4;
-  for (int e = tid; e < BM * G; e += 64 * NWAVES) {
-    const int r = e / G;
-    const int cg = e - r * G;
+  constexpr int NT = 64 * NWAVES;
+  static_assert(NT % G == 0, "column group per thread");
+  const int cg = tid % G;
+  const int n = n0 + cg * 4;
+  if (n >= a.N) return;
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (a.bias != nullptr) load4(a.bias + n, bias4);
+  for (int r = tid / G; r < BM; r += NT / G) {
     const int m = m0 + r;
-    const int n = n0 + cg * 4;
-    if (m >= M || n >= a.N) continue;
+    if (m >= M) break;
     float v[4];
     load4(E + r * EPI_LD + cg * 4, v);
-    if (a.bias != nullptr) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] += a.bias[n + q];
-    }
+    for (int q = 0; q < 4; ++q) v[q] += bias4[q];
     if (epi == FS2_EPI_BIAS_RELU) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.0f);
@@ -795,7 +801,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
             E[(mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
     }
     __syncthreads();
-    epilogue<128, BN, 8>(a, E, m0 + h * 128, n0, tid, M);
+    epilogue<128, BN, 8, false>(a, E, m0 + h * 128, n0, tid, M);  // never an LN epilogue
     __syncthreads();
   }
 }
