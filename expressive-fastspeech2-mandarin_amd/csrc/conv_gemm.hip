@@ -137,6 +137,7 @@ struct ConvArgs {
   const int32_t *rows_dev;
   const int2 *row_pos;
   const int32_t *a_rowmap;  // KS == 1 only: A row of output row m (-1 = zero row)
+  int dbg;                  // analysis only (FS2_CONV_DEBUG): bit 0 skips the K loop, bit 1 the epilogue
 };
 
 // Active rows and the XCD-aware tile of this workgroup. The dispatcher deals workgroup ids
@@ -194,7 +195,36 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
 #pragma unroll
     for (int q = 0; q < 4; ++q) bias4[q] = a.bias[n + q];
     const float inv_n = 1.0f / (float)a.N;
-    for (int r = wid; r < BM; r += NWAVES) {
+    // Residual rows of ALL this wave's rows are loaded before the first row is reduced, and the
+    // empty asm consuming them pins the loads there (otherwise they are scheduled next to their
+    // use: one dependent memory latency per row, 16 per tile on the decoder shapes).
+    static_assert(BM % NWAVES == 0, "rows per wave");
+    constexpr int RPW = BM / NWAVES;
+    uint4 rraw[RPW];
+    const bool res_bf16 = a.res_dt == FS2_BF16;
+    if (epi == FS2_EPI_RES_LN) {
+      if (res_bf16) {
+        const bf16 *rp = reinterpret_cast<const bf16 *>(a.res);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+          const int m = min(m0 + wid + i * NWAVES, M - 1);
+          const uint2 u = *reinterpret_cast<const uint2 *>(rp + (int64_t)m * a.rs + n);
+          rraw[i] = make_uint4(u.x, u.y, 0u, 0u);
+        }
+      } else {
+        const float *rp = reinterpret_cast<const float *>(a.res);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+          const int m = min(m0 + wid + i * NWAVES, M - 1);
+          rraw[i] = *reinterpret_cast<const uint4 *>(rp + (int64_t)m * a.rs + n);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) asm volatile("" ::"v"(rraw[i].x), "v"(rraw[i].y), "v"(rraw[i].z), "v"(rraw[i].w));
+    }
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int r = wid + i * NWAVES;
       const int m = m0 + r;
       if (m >= M) break;
       float v[4];
@@ -203,7 +233,17 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
       for (int q = 0; q < 4; ++q) v[q] += bias4[q];
       if (epi == FS2_EPI_RES_LN) {
         float rv[4];
-        load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n, rv);
+        if (res_bf16) {
+          rv[0] = __uint_as_float(rraw[i].x << 16);
+          rv[1] = __uint_as_float(rraw[i].x & 0xffff0000u);
+          rv[2] = __uint_as_float(rraw[i].y << 16);
+          rv[3] = __uint_as_float(rraw[i].y & 0xffff0000u);
+        } else {
+          rv[0] = __uint_as_float(rraw[i].x);
+          rv[1] = __uint_as_float(rraw[i].y);
+          rv[2] = __uint_as_float(rraw[i].z);
+          rv[3] = __uint_as_float(rraw[i].w);
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] += rv[q];
       } else {
@@ -963,7 +1003,7 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
       advance();
     }
   }
-  for (int k = 0; k < nK; ++k) {
+  for (int k = 0; k < ((a.dbg & 1) ? 0 : nK); ++k) {
     // stage k landed (this wave's pieces): later issued stages may stay in flight
     const int ahead = nK - 1 - k;
     if (ahead >= NS - 2)
@@ -991,7 +1031,203 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
       for (int j = 0; j < 4; ++j)
         E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
   __syncthreads();
+  if (a.dbg & 2) return;
   epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Register-B variant of the ring kernel for the streamed-A LayerNorm GEMMs (decoder fc / FFN w_2,
+// M ~ 25k rows, K = 256 / 1024). There the A rows come from HBM exactly once while the weights
+// are L2-resident, and with B staged through LDS (32 KiB per k-step) only two 16 KiB A stages
+// fit in flight per CU: ~6 MB chip-wide, i.e. ~2 TB/s at a loaded HBM latency of ~3 us. Here each
+// wave loads its own B fragments straight into registers (buffer_load_dwordx4, PB k-steps ahead,
+// 8 x 16 B per lane per k-step) and LDS holds only an NA-deep A ring (A rows shifted by the tap,
+// sequence test on the DMA source). Per k-step a wave issues B(k+PB) first, then A(k+NA-1), so
+// waiting for B(k) (counted vmcnt) never waits for the deeper A stages; one raw s_barrier per
+// k-step publishes A(k) and frees the A buffer the next issue refills.
+template <int CT, int WGM, int WMI, int NA, int PB>
+__global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_rb_kernel(ConvArgs a) {
+  constexpr int WGN = 4, NW = WGM * WGN;
+  constexpr int WROWS = 16 * WMI, BM = WROWS * WGM, BN = 64 * WGN;
+  constexpr int KE = CTraits<CT>::KE, CE = CTraits<CT>::CE;
+  using TW = typename CTraits<CT>::T;
+  constexpr int AP = BM / 8;                            // 1 KiB A pieces per stage
+  constexpr int AQ = (AP + NW - 1) / NW;                // A pieces per wave per stage
+  constexpr int BL = 8;                                 // B fragment loads per lane per k-step
+  constexpr int LPS = AQ + BL;                          // vector-memory ops per wave per k-step
+  static_assert(AQ + LPS * (PB - 1) <= 63, "vmcnt range");
+  constexpr int STAGE = AP * 1024;
+  constexpr int EPI_LD = BN + 4;
+  constexpr int SMEM = (NA * STAGE > BM * EPI_LD * 4) ? NA * STAGE : BM * EPI_LD * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  using Frag = typename std::conditional<CT == FS2_BF16, bf16x8, f32x4>::type;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / WGN, wc = wid % WGN;
+  int M, m0, n0;
+  if (!conv_tile<BM>(a, M, m0, n0, BN)) return;
+
+  const int KS = a.KS, pad = a.pad, T = a.T;
+  const int nCk = a.Cin_pad / KE;
+  const int nK = KS * nCk;
+  const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
+  const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * (uint32_t)sizeof(TW);
+  const uint32_t xrow = (uint32_t)a.xs * (uint32_t)sizeof(TW);
+
+  // A DMA roles (as the ring kernel)
+  const int prow = lane >> 3, plc = (lane & 7) ^ prow;
+  int arow[AQ], apos[AQ], alen[AQ];
+#pragma unroll
+  for (int i = 0; i < AQ; ++i) {
+    const int m = m0 + 8 * ((wid + NW * i) % AP) + prow;
+    arow[i] = m;
+    if (m >= M) {
+      apos[i] = 0;
+      alen[i] = 0;
+    } else if (a.row_pos != nullptr) {
+      const int2 p = a.row_pos[m];
+      apos[i] = p.x;
+      alen[i] = p.y;
+    } else {
+      apos[i] = m % T;
+      alen[i] = T;
+    }
+  }
+  // B fragment of this lane: column n0 + wc*64 + ni*16 + (lane&15), 16-byte chunk s*4 + (lane>>4)
+  uint32_t bofs[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int n = n0 + wc * 64 + ni * 16 + (lane & 15);
+    bofs[ni] = n < a.N ? (uint32_t)n * wrow + (uint32_t)((lane >> 4) * 16) : kOOB;
+  }
+  auto glds = [&](char *dst, uint32_t off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)dst, 16, off, 0, 0, 0);
+  };
+  auto issue_a = [&](int tap, int cb, int buf) {
+    char *As = smem + buf * STAGE;
+    const int sh = tap - pad;
+    const int ch = cb * KE + plc * CE;
+    const bool ch_ok = ch < a.Cin;
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      const bool ok = ch_ok && (unsigned)(apos[i] + sh) < (unsigned)alen[i];
+      glds(As + ((wid + NW * i) % AP) * 1024,
+           ok ? (uint32_t)(arow[i] + sh) * xrow + (uint32_t)ch * (uint32_t)sizeof(TW) : kOOB);
+    }
+  };
+  auto load_b = [&](Frag (&b)[4][2], int tap, int cb) {
+    const uint32_t off = ((uint32_t)tap * a.Cin_pad + cb * KE) * (uint32_t)sizeof(TW);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        auto v = __builtin_amdgcn_raw_buffer_load_b128(wr_, bofs[ni] == kOOB ? kOOB : bofs[ni] + off + s * 64u, 0, 0);
+        b[ni][s] = *reinterpret_cast<Frag *>(&v);
+      }
+  };
+
+  f32x4 acc[WMI][4];
+#pragma unroll
+  for (int i = 0; i < WMI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int aread0 = lds_off(wr * WROWS + (lane & 15), lane >> 4);
+  const int aread1 = lds_off(wr * WROWS + (lane & 15), 4 + (lane >> 4));
+  auto compute = [&](const char *As, const Frag (&b)[4][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const char *Ab = As + (s ? aread1 : aread0);
+      Frag af[WMI];
+#pragma unroll
+      for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const Frag *>(Ab + mi * 16 * kRowBytes);
+      if constexpr (CT == FS2_BF16) {
+#pragma unroll
+        for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], b[ni][s], acc[mi][ni], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi][j], b[ni][s][j], acc[mi][ni], 0, 0, 0);
+      }
+    }
+  };
+
+  // k-step k = cb * KS + tap. (ta, ca): next A stage to issue; (tb, cbb): next B k-step to load
+  int ta = 0, ca = 0, tb = 0, cbb = 0;
+  auto adv = [&](int &t, int &c) {
+    if (++t == KS) {
+      t = 0;
+      ++c;
+    }
+  };
+  Frag bq[PB + 1][4][2];  // B ring in registers: k-step k lives in bq[k % (PB+1)]
+  // prologue: A stages 0..NA-2, then B k-steps 0..PB-1 (B issued last: the first waits see them)
+#pragma unroll
+  for (int st = 0; st < NA - 1; ++st)
+    if (st < nK) {
+      issue_a(ta, ca, st);
+      adv(ta, ca);
+    }
+#pragma unroll
+  for (int j = 0; j < PB; ++j)
+    if (j < nK) {
+      load_b(bq[j], tb, cbb);
+      adv(tb, cbb);
+    }
+  // main loop, unrolled by PB+1 so the B ring index is static
+  for (int k0 = 0; k0 < nK; k0 += PB + 1) {
+#pragma unroll
+    for (int u = 0; u <= PB; ++u) {
+      const int k = k0 + u;
+      if (k < nK) {
+        // B(k) (and, issued before it, A(k)) landed; later issues may stay in flight
+        if (k + PB <= nK - 1 + 0 && k >= 1)
+          vm_wait<AQ + LPS * (PB - 1)>();
+        else
+          vm_wait<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (k + PB < nK) {
+          load_b(bq[(u + PB) % (PB + 1)], tb, cbb);
+          adv(tb, cbb);
+        }
+        if (k + NA - 1 < nK) {
+          issue_a(ta, ca, (k + NA - 1) % NA);
+          adv(ta, ca);
+        }
+        compute(smem + (k % NA) * STAGE, bq[u]);
+      }
+    }
+  }
+  __syncthreads();
+
+  float *E = reinterpret_cast<float *>(smem);
+#pragma unroll
+  for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
+  __syncthreads();
+  epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
+}
+
+template <int CT, int WGM, int WMI, int NA, int PB>
+void launch_rb(ConvArgs a, hipStream_t s) {
+  constexpr int BM = 16 * WMI * WGM;
+  a.ntn = 1;
+  a.ngr = 1;
+  const int nwg = (a.M + BM - 1) / BM;
+  hipLaunchKernelGGL((conv_gemm_rb_kernel<CT, WGM, WMI, NA, PB>), dim3(nwg), dim3(256 * WGM), 0, s, a);
 }
 
 template <int CT, int WGM, int WMI, int NS>
@@ -1047,7 +1283,15 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       return e == nullptr || e[0] != '0';
     }();
     if (ln && ring) {  // LDS-DMA deep ring (LN epilogues, N == 256)
-      if (a.M >= 192 * 128)
+      // register-B variant: correct but measured 1.5x slower on the decoder conv1 in round 1
+      // (per-lane 16 B weight loads from L2, two waves per column group); opt-in
+      static const bool rb = [] {
+        const char *e = getenv("FS2_CONV_RB");
+        return e != nullptr && e[0] == '1';
+      }();
+      if (a.M >= 192 * 128 && rb)
+        launch_rb<CT, 2, 4, 8, 2>(a, s);  // 128 x 256, 8 waves, B in registers, 8 A stages
+      else if (a.M >= 192 * 128)
         launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages (144 KiB)
       else if (a.M >= 8192)
         launch_ring<CT, 1, 2, 4>(a, s);  // 32 x 256, 4 waves, 4 stages
@@ -1134,6 +1378,11 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.out = d->out;
   a.out_dt = d->out_dtype;
   a.os = d->out_row_stride;
+  static const int dbg = [] {
+    const char *e = getenv("FS2_CONV_DEBUG");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  a.dbg = dbg;
   a.rows_dev = d->rows_dev;
   a.row_pos = reinterpret_cast<const int2 *>(d->row_pos);
   a.a_rowmap = d->a_rowmap;

@@ -70,10 +70,24 @@ __device__ __forceinline__ void load4(const bf16 *p, float v[4]) {
   v[3] = __uint_as_float(r.y & 0xffff0000u);
 }
 
+// Full-wave sum, result in every lane. Within each 16-lane row: DPP quad_perm [1,0,3,2],
+// [2,3,0,1], row_half_mirror, row_mirror (VALU ops, no LDS round trip); the four row sums are
+// then combined with v_readlane into a wave-uniform value. (A __shfl_xor butterfly is six
+// dependent ds_bpermute LDS round trips: the LN epilogues' per-row critical path.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  const int b = __builtin_bit_cast(int, v);
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
 }
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
