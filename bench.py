@@ -34,6 +34,7 @@ import torch  # noqa: E402
 
 HOP, SR = 256, 22050
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+FP8_PEAK_TFLOPS = 5000.0   # dense e4m3 (block-scaled 16x16x128 form)
 F32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 
@@ -45,7 +46,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--phonemes", type=int, default=64)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                    help="fp8 = cfg5: FFN Conv1d pair of every FFT block on e4m3 MFMA, the rest bf16")
     ap.add_argument("--graph", type=int, default=1, help="replay the forward as a captured HIP graph")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--kernel-reps", type=int, default=20)
@@ -104,10 +106,17 @@ def time_dominant_kernel(model, batch, device, reps):
     # the launch the forward makes: packed valid frames (runtime.packed_decoder_ok) or padded rows
     lay = ops.SeqLayout(batch["mel_lens"].to(device), T) if runtime.packed_decoder_ok(P) else None
     shape = (B * T,) if lay is not None else (B, T)
-    h = torch.randn(*shape, lp.c1, generator=g).to(device=device, dtype=ops.torch_dtype(P.act_dtype))
-    out = torch.empty(*shape, lp.w1.shape[0], device=device, dtype=h.dtype)
-    run = lambda: ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=P.compute,
-                             epilogue=L.EPI_BIAS_RELU, out=out, layout=lay)
+    if lp.fp8 is not None:  # cfg5: the e4m3 launch the forward makes
+        h = (torch.randn(*shape, lp.c1, generator=g) * 0.5).to(device=device, dtype=torch.float8_e4m3fn)
+        out = torch.empty(*shape, lp.w1.shape[0], device=device, dtype=torch.float8_e4m3fn)
+        run = lambda: ops.conv1d(h, lp.fp8.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=L.FS2_FP8,
+                                 epilogue=L.EPI_BIAS_RELU, out=out, out_dtype=L.FS2_FP8, out_scale=1.0 / lp.fp8.s_f,
+                                 col_scale=lp.fp8.cs1, layout=lay)
+    else:
+        h = torch.randn(*shape, lp.c1, generator=g).to(device=device, dtype=ops.torch_dtype(P.act_dtype))
+        out = torch.empty(*shape, lp.w1.shape[0], device=device, dtype=h.dtype)
+        run = lambda: ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=P.compute,
+                                 epilogue=L.EPI_BIAS_RELU, out=out, layout=lay)
     for _ in range(3):
         run()
     stream = torch.cuda.current_stream(device)
@@ -158,8 +167,8 @@ def cpu_baseline(batch_cpu, pc, mc, budget_s=20.0):
                       f"{dt:.1f} s, torch.set_num_threads({threads})"}
 
 
-def load_traffic():
-    path = os.path.join(REPO, "profiles", "conv9_traffic.json")
+def load_traffic(dtype="bf16"):
+    path = os.path.join(REPO, "profiles", "conv9_traffic.json" if dtype == "bf16" else f"conv9_{dtype}_traffic.json")
     if os.path.exists(path):
         with open(path) as f:
             return json.load(f).get("hbm_bytes_per_launch")
@@ -225,6 +234,10 @@ def main():
     batch = to_device(batch_cpu, device)
     frames = int(batch_cpu["mel_lens"].sum())
 
+    if args.dtype == "fp8":
+        # static activation scales from a calibration batch of the same shape (different seed)
+        model.calibrate_fp8(**to_device(synth_batch(args.batch, args.phonemes, seed=1000 + rank), device))
+
     def step():
         with torch.no_grad():
             return model(**batch)
@@ -261,7 +274,7 @@ def main():
     standalone_s, kernel_flops = time_dominant_kernel(model, batch_cpu, device, args.kernel_reps)
     ms_per_step = elapsed / args.steps * 1e3
     value = tot_frames * args.steps / elapsed
-    peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
+    peak = {"bf16": BF16_PEAK_TFLOPS, "fp8": FP8_PEAK_TFLOPS}.get(args.dtype, F32_PEAK_TFLOPS)
     achieved = kernel_flops / kernel_s / 1e12
     rec = {
         "metric": "mel-frames/sec/GPU (batch-64 synth) at 1/2/4/8 MI355X; RTF",
@@ -284,9 +297,9 @@ def main():
                    "parallelism": f"dp{world} (independent shards, no collective)",
                    "hip_graph": bool(args.graph)},
         "rtf": round((elapsed / args.steps) / (tot_frames / world * HOP / SR), 7),
-        "roofline": {"bound": "mfma", "kernel": "conv_gemm_kernel<bf16,2,2> (decoder FFN Conv1d k=9, 256->1024)",
+        "roofline": {"bound": "mfma", "kernel": f"conv_gemm_kernel<{args.dtype}> (decoder FFN Conv1d k=9, 256->1024)",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": load_traffic(),
+                     "frac": round(achieved / peak, 4), "traffic": load_traffic(args.dtype),
                      "kernel_ms": round(kernel_s * 1e3, 4), "launches_timed": n_launch,
                      "timing": "HIP events around each decoder conv-k9 launch in 3 eager forwards",
                      "kernel_ms_standalone_random": round(standalone_s * 1e3, 4),

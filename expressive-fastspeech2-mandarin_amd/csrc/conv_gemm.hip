@@ -37,6 +37,16 @@ constexpr int kRowBytes = 128;  // one k-step of one tile row
 
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * kRowBytes + ((chunk ^ (row & 7)) << 4); }
 
+// fp8 fragment of mfma_scale_f32_16x16x128_f8f6f4: lane group g = lane>>4 holds k = 32g .. 32g+31
+// of its row (16-byte chunks 2g and 2g+1 of the 128-byte k-step row); A and B use the same map.
+__device__ __forceinline__ i32x8 frag_fp8(const char *p0, const char *p1) {
+  const uint4 lo = *reinterpret_cast<const uint4 *>(p0), hi = *reinterpret_cast<const uint4 *>(p1);
+  return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+__device__ __forceinline__ f32x4 mfma_fp8(i32x8 a, i32x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);  // e4m3 x e4m3, scale 1
+}
+
 template <int CT>
 struct CTraits;
 template <>
@@ -50,6 +60,12 @@ struct CTraits<FS2_F32> {
   static constexpr int KE = 32;
   static constexpr int CE = 4;
   using T = float;
+};
+template <>
+struct CTraits<FS2_FP8> {
+  static constexpr int KE = 128;  // one mfma_scale_f32_16x16x128_f8f6f4 per k-step
+  static constexpr int CE = 16;
+  using T = fp8;
 };
 
 // One 16-byte LDS chunk (CE compute elements) staged in registers from an input of type TIn.
@@ -108,6 +124,13 @@ struct Stage<FS2_F32, bf16> {
   }
 };
 
+template <>
+struct Stage<FS2_FP8, fp8> {
+  uint4 r;
+  __device__ __forceinline__ void load(rsrc_t rs, uint32_t off) { r = bload16(rs, off); }
+  __device__ __forceinline__ uint4 chunk() const { return r; }
+};
+
 struct ConvArgs {
   const void *x;
   int64_t xs;
@@ -138,6 +161,10 @@ struct ConvArgs {
   const int2 *row_pos;
   const int32_t *a_rowmap;  // KS == 1 only: A row of output row m (-1 = zero row)
   int dbg;                  // analysis only (FS2_CONV_DEBUG): bit 0 skips the K loop, bit 1 the epilogue
+  const float *colscale;    // fp8: per-column dequantisation scale of the accumulator (or NULL)
+  float out_scale;          // out_dt == FS2_FP8: e4m3(y * out_scale)
+  void *out2;               // LN epilogues: optional fp8 copy e4m3(y * out2_scale), rows of N bytes
+  float out2_scale;
 };
 
 // Active rows and the XCD-aware tile of this workgroup. The dispatcher deals workgroup ids
@@ -170,9 +197,11 @@ __device__ __forceinline__ void load_any4(const void *p, int dt, int64_t off, fl
   else
     load4(reinterpret_cast<const float *>(p) + off, v);
 }
-__device__ __forceinline__ void store_any4(void *p, int dt, int64_t off, const float v[4]) {
+__device__ __forceinline__ void store_any4(void *p, int dt, int64_t off, const float v[4], float scale = 1.0f) {
   if (dt == FS2_BF16)
     store4(reinterpret_cast<bf16 *>(p) + off, v);
+  else if (dt == FS2_FP8)
+    *reinterpret_cast<unsigned *>(reinterpret_cast<fp8 *>(p) + off) = pack4_fp8(v, scale);
   else
     store4(reinterpret_cast<float *>(p) + off, v);
 }
@@ -189,11 +218,12 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
   if constexpr (LN) if (epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN || epi == FS2_EPI_RELU_LN_DOT) {
     // one wave per row; N == BN == 256 (checked on the host), lane owns columns 4*lane..4*lane+3
     const int n = lane * 4;
-    float bias4[4], g4[4], be4[4];
+    float bias4[4], g4[4], be4[4], cs4[4] = {1.f, 1.f, 1.f, 1.f};
     load4(a.gamma + n, g4);
     load4(a.beta + n, be4);
 #pragma unroll
     for (int q = 0; q < 4; ++q) bias4[q] = a.bias[n + q];
+    if (a.colscale != nullptr) load4(a.colscale + n, cs4);
     const float inv_n = 1.0f / (float)a.N;
     // Residual rows of ALL this wave's rows are loaded before the first row is reduced, and the
     // empty asm consuming them pins the loads there (otherwise they are scheduled next to their
@@ -230,7 +260,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
       float v[4];
       load4(E + r * EPI_LD + n, v);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] += bias4[q];
+      for (int q = 0; q < 4; ++q) v[q] = v[q] * cs4[q] + bias4[q];
       if (epi == FS2_EPI_RES_LN) {
         float rv[4];
         if (res_bf16) {
@@ -290,7 +320,9 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
           for (int q = 0; q < 4; ++q) y[q] += av[q];
         }
       }
-      store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, y);
+      store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, y, a.out_scale);
+      if (a.out2 != nullptr)
+        *reinterpret_cast<unsigned *>(reinterpret_cast<fp8 *>(a.out2) + (int64_t)m * a.N + n) = pack4_fp8(y, a.out2_scale);
     }
     return;
   }
@@ -303,15 +335,16 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
   const int cg = tid % G;
   const int n = n0 + cg * 4;
   if (n >= a.N) return;
-  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f}, cs4[4] = {1.f, 1.f, 1.f, 1.f};
   if (a.bias != nullptr) load4(a.bias + n, bias4);
+  if (a.colscale != nullptr) load4(a.colscale + n, cs4);
   for (int r = tid / G; r < BM; r += NT / G) {
     const int m = m0 + r;
     if (m >= M) break;
     float v[4];
     load4(E + r * EPI_LD + cg * 4, v);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] += bias4[q];
+    for (int q = 0; q < 4; ++q) v[q] = v[q] * cs4[q] + bias4[q];
     if (epi == FS2_EPI_BIAS_RELU) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.0f);
@@ -324,7 +357,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] += rv[q];
     }
-    store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, v);
+    store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, v, a.out_scale);
   }
 }
 
@@ -448,6 +481,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  const int bf8_0 = lds_off(wc * 64 + (lane & 15), 2 * (lane >> 4));
+  const int bf8_1 = lds_off(wc * 64 + (lane & 15), 2 * (lane >> 4) + 1);
   auto compute = [&](int aslot, int tap, const char *Bs) {
     const char *As = Abuf + aslot * A_BYTES;
     const int sh = tap - pad;
@@ -455,6 +490,25 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
     bool vrow[WMI];
 #pragma unroll
     for (int mi = 0; mi < WMI; ++mi) vrow[mi] = (unsigned)(tpos[mi] + sh) < (unsigned)tlen[mi];
+    if constexpr (CT == FS2_FP8) {
+      const char *A0 = As + lds_off(arow0 + tap, 2 * (lane >> 4));
+      const char *A1 = As + lds_off(arow0 + tap, 2 * (lane >> 4) + 1);
+      i32x8 af[WMI], bfr[4];
+#pragma unroll
+      for (int mi = 0; mi < WMI; ++mi) af[mi] = frag_fp8(A0 + mi * 16 * kRowBytes, A1 + mi * 16 * kRowBytes);
+      if (need_mask) {
+#pragma unroll
+        for (int mi = 0; mi < WMI; ++mi)
+          if (!vrow[mi]) af[mi] = i32x8{};
+      }
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bfr[ni] = frag_fp8(Bs + bf8_0 + ni * 16 * kRowBytes, Bs + bf8_1 + ni * 16 * kRowBytes);
+#pragma unroll
+      for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma_fp8(af[mi], bfr[ni], acc[mi][ni]);
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const char *Ab = As + lds_off(arow0 + tap, s * 4 + (lane >> 4));
@@ -956,6 +1010,21 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
   auto compute = [&](const char *S) {
     const char *As = S;
     const char *Bs = S + AP * 1024;
+    if constexpr (CT == FS2_FP8) {
+      const int g2 = 2 * (lane >> 4);
+      const char *A0 = As + lds_off(wr * WROWS + (lane & 15), g2), *A1 = As + lds_off(wr * WROWS + (lane & 15), g2 + 1);
+      const char *B0 = Bs + lds_off(wc * 64 + (lane & 15), g2), *B1 = Bs + lds_off(wc * 64 + (lane & 15), g2 + 1);
+      i32x8 af[WMI], bfr[4];
+#pragma unroll
+      for (int mi = 0; mi < WMI; ++mi) af[mi] = frag_fp8(A0 + mi * 16 * kRowBytes, A1 + mi * 16 * kRowBytes);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bfr[ni] = frag_fp8(B0 + ni * 16 * kRowBytes, B1 + ni * 16 * kRowBytes);
+#pragma unroll
+      for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma_fp8(af[mi], bfr[ni], acc[mi][ni]);
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const char *Ab = As + (s ? aread1 : aread0);
@@ -1289,9 +1358,13 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         const char *e = getenv("FS2_CONV_RB");
         return e != nullptr && e[0] == '1';
       }();
-      if (a.M >= 192 * 128 && rb)
-        launch_rb<CT, 2, 4, 8, 2>(a, s);  // 128 x 256, 8 waves, B in registers, 8 A stages
-      else if (a.M >= 192 * 128)
+      if constexpr (CT != FS2_FP8) {
+        if (a.M >= 192 * 128 && rb) {
+          launch_rb<CT, 2, 4, 8, 2>(a, s);  // 128 x 256, 8 waves, B in registers, 8 A stages
+          return;
+        }
+      }
+      if (a.M >= 192 * 128)
         launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages (144 KiB)
       else if (a.M >= 8192)
         launch_ring<CT, 1, 2, 4>(a, s);  // 32 x 256, 4 waves, 4 stages
@@ -1321,14 +1394,17 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
 }  // namespace
 
 extern "C" int fs2_conv_cin_pad(int Cin, int compute) {
-  const int ke = compute == FS2_BF16 ? CTraits<FS2_BF16>::KE : CTraits<FS2_F32>::KE;
+  const int ke = compute == FS2_BF16  ? CTraits<FS2_BF16>::KE
+                 : compute == FS2_FP8 ? CTraits<FS2_FP8>::KE
+                                      : CTraits<FS2_F32>::KE;
   return (Cin + ke - 1) / ke * ke;
 }
 
 extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   if (d == nullptr || d->x == nullptr || d->w == nullptr || d->out == nullptr) return FS2_EINVAL;
-  if (d->compute != FS2_BF16 && d->compute != FS2_F32) return FS2_EUNSUPPORTED;
-  const int ce = d->compute == FS2_BF16 ? 8 : 4;
+  if (d->compute != FS2_BF16 && d->compute != FS2_F32 && d->compute != FS2_FP8) return FS2_EUNSUPPORTED;
+  const int ce = d->compute == FS2_BF16 ? 8 : (d->compute == FS2_FP8 ? 16 : 4);
+  if (d->compute == FS2_FP8 && d->x_dtype != FS2_FP8) return FS2_EUNSUPPORTED;  // fp8 GEMMs read fp8 copies
   if (d->B < 0 || d->T < 0 || d->Cin <= 0 || d->N <= 0 || d->KS <= 0 || d->pad < 0) return FS2_EINVAL;
   if (d->Cin % ce != 0 || d->N % 4 != 0 || d->Cin_pad != fs2_conv_cin_pad(d->Cin, d->compute)) return FS2_EINVAL;
   if (d->x_row_stride < d->Cin || (d->x_row_stride % ce) != 0) return FS2_EINVAL;
@@ -1386,8 +1462,13 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.rows_dev = d->rows_dev;
   a.row_pos = reinterpret_cast<const int2 *>(d->row_pos);
   a.a_rowmap = d->a_rowmap;
+  a.colscale = d->col_scale;
+  a.out_scale = d->out_scale;
+  a.out2 = d->out2;
+  a.out2_scale = d->out2_scale;
   {
-    const int xes = d->x_dtype == FS2_BF16 ? 2 : 4, wes = d->compute == FS2_BF16 ? 2 : 4;
+    const int xes = d->x_dtype == FS2_BF16 ? 2 : (d->x_dtype == FS2_FP8 ? 1 : 4);
+    const int wes = d->compute == FS2_BF16 ? 2 : (d->compute == FS2_FP8 ? 1 : 4);
     const int64_t xb = M64 * d->x_row_stride * xes;
     const int64_t wb = (int64_t)d->N * d->KS * d->Cin_pad * wes;
     if (xb >= (1LL << 31) || wb >= (1LL << 31)) return FS2_EUNSUPPORTED;  // 31-bit buffer offsets
@@ -1396,10 +1477,13 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   }
 
   hipStream_t s = as_stream(stream);
-  if (d->x_dtype != FS2_BF16 && d->x_dtype != FS2_F32) return FS2_EUNSUPPORTED;
+  if (d->x_dtype != FS2_BF16 && d->x_dtype != FS2_F32 && d->x_dtype != FS2_FP8) return FS2_EUNSUPPORTED;
+  if (d->out2 != nullptr && (!ln || epi == FS2_EPI_RELU_LN_DOT)) return FS2_EINVAL;
   if (d->KS > (ln ? 3 : 9)) return FS2_EUNSUPPORTED;
   const bool xb = d->x_dtype == FS2_BF16;
-  if (d->compute == FS2_BF16)
+  if (d->compute == FS2_FP8)
+    dispatch<FS2_FP8, fp8>(a, ln, s);
+  else if (d->compute == FS2_BF16)
     xb ? dispatch<FS2_BF16, bf16>(a, ln, s) : dispatch<FS2_BF16, float>(a, ln, s);
   else
     xb ? dispatch<FS2_F32, bf16>(a, ln, s) : dispatch<FS2_F32, float>(a, ln, s);

@@ -70,6 +70,19 @@ __device__ __forceinline__ void load4(const bf16 *p, float v[4]) {
   v[3] = __uint_as_float(r.y & 0xffff0000u);
 }
 
+// fp8 e4m3fn (OCP, the gfx950 MFMA format) as raw bytes. Conversion saturates to +-448 first
+// (the hardware conversion does not clamp); 4 values -> one 32-bit word, element 0 in byte 0.
+typedef unsigned char fp8;
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ unsigned pack4_fp8(const float v[4], float scale) {
+  float c[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) c[q] = fminf(fmaxf(v[q] * scale, -448.0f), 448.0f);
+  int r = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+  r = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], r, true);
+  return (unsigned)r;
+}
+
 // Full-wave sum, result in every lane. Within each 16-lane row: DPP quad_perm [1,0,3,2],
 // [2,3,0,1], row_half_mirror, row_mirror (VALU ops, no LDS round trip); the four row sums are
 // then combined with v_readlane into a wave-uniform value. (A __shfl_xor butterfly is six

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first)
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(HERE, "_lib", "libfs2hip.so")
 
-FS2_F32, FS2_BF16 = 0, 1
+FS2_F32, FS2_BF16, FS2_FP8 = 0, 1, 2
 FS2_OK, FS2_EINVAL, FS2_ELAUNCH, FS2_EUNSUPPORTED = 0, 1, 2, 3
 (EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_TANH, EPI_BIAS_RES, EPI_RES_LN, EPI_RELU_LN, EPI_RELU_LN_DOT) = range(7)
 DUR_I64, DUR_F32, DUR_LOGPRED = 0, 1, 2
@@ -40,6 +40,7 @@ class ConvDesc(ctypes.Structure):
         ("dot_w", _p), ("dot_b", _f),
         ("out", _p), ("out_dtype", _i), ("out_row_stride", _i64),
         ("rows_dev", _p), ("row_pos", _p), ("a_rowmap", _p),
+        ("col_scale", _p), ("out_scale", _f), ("out2", _p), ("out2_scale", _f),
     ]
 
 

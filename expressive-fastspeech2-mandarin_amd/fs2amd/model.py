@@ -202,14 +202,15 @@ class FastSpeech2(nn.Module):
         self._vp_precision = hip.get("vp_dtype", os.environ.get("FS2_HIP_VP_DTYPE", "fp32"))
         self._packs = {}
         self.train_dropout = True  # False: train-mode semantics without dropout (parity tests)
+        self._fp8_scales = None    # {("enc"|"dec", layer): (amax of FFN input h, amax of w_1 output f)}
         self.register_load_state_dict_post_hook(lambda mod, keys: mod.invalidate_packed())
 
     # ---- precision / packed weights --------------------------------------------------------------
     def set_precision(self, dtype, vp_dtype=None):
         """dtype of the FFT blocks / attention / mel_linear / PostNet ('fp32' | 'bf16'); vp_dtype of
         the three VariancePredictors ('fp32' | 'bf16', bf16 only takes effect in bf16 mode)."""
-        if dtype not in ("fp32", "bf16") or vp_dtype not in (None, "fp32", "bf16"):
-            raise ValueError("precision must be 'fp32' or 'bf16'")
+        if dtype not in ("fp32", "bf16", "fp8") or vp_dtype not in (None, "fp32", "bf16"):
+            raise ValueError("precision must be 'fp32', 'bf16' or 'fp8' (vp_dtype 'fp32' / 'bf16')")
         self._precision = dtype
         if vp_dtype is not None:
             self._vp_precision = vp_dtype
@@ -218,6 +219,24 @@ class FastSpeech2(nn.Module):
     @property
     def precision(self):
         return self._precision
+
+    def calibrate_fp8(self, **batch):
+        """Static fp8 activation scales (cfg5): one bf16 forward on ``batch`` records, per FFT
+        block, max|h| (input of the FFN Conv1d k=9) and max|relu(w_1 h)| (input of w_2) over the
+        valid frames; fp8 packing derives s = amax / 448 from them. Returns the scales."""
+        from . import runtime
+
+        prev = self._precision
+        self._precision = "bf16"
+        runtime.CALIB = {}
+        try:
+            with torch.no_grad():
+                self.forward(**batch)
+            self._fp8_scales = {k: (float(h), float(f)) for k, (h, f) in runtime.CALIB.items()}
+        finally:
+            runtime.CALIB = None
+            self._precision = prev
+        return self._fp8_scales
 
     def invalidate_packed(self):
         self._packs = {}
@@ -229,10 +248,10 @@ class FastSpeech2(nn.Module):
         from .packing import pack_model
 
         key = (self._precision, self._vp_precision, str(device))
-        fp = self._fingerprint()
+        fp = (self._fingerprint(), id(self._fp8_scales))
         ent = self._packs.get(key)
         if ent is None or ent[0] != fp:
-            ent = (fp, pack_model(self, device, self._precision, self._vp_precision))
+            ent = (fp, pack_model(self, device, self._precision, self._vp_precision, self._fp8_scales))
             self._packs[key] = ent
         return ent[1]
 

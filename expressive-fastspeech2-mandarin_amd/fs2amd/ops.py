@@ -27,10 +27,17 @@ def _dt(t):
         return L.FS2_BF16
     if t.dtype == torch.float32:
         return L.FS2_F32
-    raise TypeError(f"fs2amd: unsupported dtype {t.dtype} (float32 / bfloat16 only)")
+    if t.dtype == torch.float8_e4m3fn:
+        return L.FS2_FP8
+    raise TypeError(f"fs2amd: unsupported dtype {t.dtype} (float32 / bfloat16 / float8_e4m3fn only)")
+
+
+FP8_MAX = 448.0  # e4m3fn
 
 
 def torch_dtype(code):
+    if code == L.FS2_FP8:
+        return torch.float8_e4m3fn
     return torch.bfloat16 if code == L.FS2_BF16 else torch.float32
 
 
@@ -57,7 +64,8 @@ def cin_pad(cin, compute):
 
 def pack_conv_weight(w, compute, scale=None):
     """nn.Conv1d weight [N, Cin, KS] (or nn.Linear [N, Cin]) -> packed [N, KS, Cin_pad] in the
-    compute dtype, optionally scaled per output channel (BatchNorm folding)."""
+    compute dtype, optionally scaled per output channel (BatchNorm folding). fp8: use
+    :func:`pack_conv_weight_fp8` (it also returns the per-channel scales)."""
     if w.dim() == 2:
         w = w.unsqueeze(-1)
     w = w.detach().float()
@@ -108,8 +116,24 @@ class SeqLayout:
         return out.view(self.B, self.T, C)
 
 
+def pack_conv_weight_fp8(w):
+    """Per-output-channel e4m3fn quantisation: w[n] ~= q[n] * s[n], s[n] = max|w[n]| / 448.
+    Returns (packed [N, KS, Cin_pad] float8_e4m3fn, s f32 [N])."""
+    if w.dim() == 2:
+        w = w.unsqueeze(-1)
+    w = w.detach().float()
+    N, cin, ks = w.shape
+    s = (w.abs().amax(dim=(1, 2)) / FP8_MAX).clamp_min(1e-12)
+    q = (w / s.view(-1, 1, 1)).clamp(-FP8_MAX, FP8_MAX)
+    cp = cin_pad(cin, L.FS2_FP8)
+    out = torch.zeros(N, ks, cp, dtype=torch.float8_e4m3fn, device=w.device)
+    out[:, :, :cin] = q.permute(0, 2, 1).to(torch.float8_e4m3fn)
+    return out.contiguous(), s.contiguous()
+
+
 def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None, out=None, residual=None,
-           ln=None, lens=None, addvec1=None, addvec2=None, dot=None, n=None, layout=None, src_layout=None):
+           ln=None, lens=None, addvec1=None, addvec2=None, dot=None, n=None, layout=None, src_layout=None,
+           col_scale=None, out_scale=1.0, out2=None, out2_scale=1.0):
     """Implicit-GEMM Conv1d / Linear with a fused epilogue (fs2_conv1d).
 
     layout: x / residual / out are packed [B*T, C] in that SeqLayout. src_layout (KS == 1): x is
@@ -140,6 +164,11 @@ def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None
         d.addvec1 = addvec1.data_ptr()
     if addvec2 is not None:
         d.addvec2 = addvec2.data_ptr()
+    if col_scale is not None:
+        d.col_scale = col_scale.data_ptr()
+    d.out_scale = float(out_scale)
+    if out2 is not None:
+        d.out2, d.out2_scale = out2.data_ptr(), float(out2_scale)
     if layout is not None:
         d.rows_dev, d.row_pos = layout.rows_dev, layout.row_pos.data_ptr()
     if src_layout is not None:

@@ -7,6 +7,9 @@
   b' = (b - rm) * g/sqrt(rv+eps) + beta (transformer/Layers.py:92-135).
 * bf16 precision: FFT blocks, mel_linear, PostNet in bf16; VariancePredictors f32 unless
   vp_precision == "bf16".
+* fp8 precision (cfg5): as bf16, plus the FFN Conv1d pair of every FFT block in e4m3fn with
+  per-output-channel weight scales; the dequantisation vector col_scale = s_in * s_w[n] uses the
+  layer's static input-activation scale from FastSpeech2.calibrate_fp8 (s = amax / 448).
 Everything else (LayerNorm affine, biases, embedding tables, bins, PE tables) stays f32.
 """
 from types import SimpleNamespace
@@ -14,18 +17,27 @@ from types import SimpleNamespace
 import torch
 
 from . import _lib as L
-from .ops import pack_conv_weight
+from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8
 
 
 def _f32(t, device):
     return t.detach().to(device=device, dtype=torch.float32).contiguous()
 
 
-def _fft_layer(layer, device, compute):
+def _fft_layer(layer, device, compute, key=None, fp8_scales=None):
     a, f = layer.slf_attn, layer.pos_ffn
     wqkv = torch.cat([a.w_qs.weight, a.w_ks.weight, a.w_vs.weight], 0).to(device)
     bqkv = torch.cat([a.w_qs.bias, a.w_ks.bias, a.w_vs.bias], 0)
+    fp8 = None
+    if fp8_scales is not None:
+        amax_h, amax_f = fp8_scales[key]
+        s_h, s_f = max(amax_h, 1e-6) / FP8_MAX, max(amax_f, 1e-6) / FP8_MAX
+        w1, sw1 = pack_conv_weight_fp8(f.w_1.weight.to(device))
+        w2, sw2 = pack_conv_weight_fp8(f.w_2.weight.to(device))
+        fp8 = SimpleNamespace(s_h=s_h, s_f=s_f, w1=w1, w2=w2, cs1=(sw1 * s_h).contiguous(),
+                              cs2=(sw2 * s_f).contiguous())
     return SimpleNamespace(
+        key=key, fp8=fp8,
         n_head=a.n_head, d_k=a.d_k,
         wqkv=pack_conv_weight(wqkv, compute), bqkv=_f32(bqkv, device),
         wfc=pack_conv_weight(a.fc.weight.to(device), compute), bfc=_f32(a.fc.bias, device),
@@ -65,17 +77,20 @@ def _postnet(pn, device, compute):
     return layers
 
 
-def pack_model(model, device, precision, vp_precision="fp32"):
+def pack_model(model, device, precision, vp_precision="fp32", fp8_scales=None):
     device = torch.device(device)
-    big = L.FS2_BF16 if precision == "bf16" else L.FS2_F32
-    vpc = L.FS2_BF16 if (precision == "bf16" and vp_precision == "bf16") else L.FS2_F32
+    big = L.FS2_BF16 if precision in ("bf16", "fp8") else L.FS2_F32
+    vpc = L.FS2_BF16 if (precision in ("bf16", "fp8") and vp_precision == "bf16") else L.FS2_F32
+    if precision == "fp8" and fp8_scales is None:
+        raise RuntimeError("fs2amd: fp8 precision needs activation scales: call model.calibrate_fp8(**batch) first")
+    sc = fp8_scales if precision == "fp8" else None
     va = model.variance_adaptor
     P = SimpleNamespace(precision=precision, compute=big, act_dtype=big, device=device)
     P.enc_emb = _f32(model.encoder.src_word_emb.weight, device)
     P.enc_pe = _f32(model.encoder.position_enc[0], device)
     P.dec_pe = _f32(model.decoder.position_enc[0], device)
-    P.enc_layers = [_fft_layer(l, device, big) for l in model.encoder.layer_stack]
-    P.dec_layers = [_fft_layer(l, device, big) for l in model.decoder.layer_stack]
+    P.enc_layers = [_fft_layer(l, device, big, ("enc", i), sc) for i, l in enumerate(model.encoder.layer_stack)]
+    P.dec_layers = [_fft_layer(l, device, big, ("dec", i), sc) for i, l in enumerate(model.decoder.layer_stack)]
     P.vp = {k: _vp(getattr(va, f"{k}_predictor"), device, vpc) for k in ("duration", "pitch", "energy")}
     P.bins = {k: _f32(getattr(va, f"{k}_bins"), device) for k in ("pitch", "energy")}
     P.var_table = {k: _f32(getattr(va, f"{k}_embedding").weight, device) for k in ("pitch", "energy")}

@@ -52,6 +52,9 @@ def _pe(P, which, n):
 # Optional measurement hook: when a list, the decoder's FFN conv-k9 launches are bracketed by
 # HIP events on the launch stream (bench.py's live roofline timing of the dominant kernel).
 TIMERS = None
+# fp8 calibration hook (FastSpeech2.calibrate_fp8): when a dict, every FFT block records
+# (max|h|, max|f|) of its FFN inputs over the valid rows, keyed by the layer's key.
+CALIB = None
 
 
 def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=None):
@@ -68,6 +71,27 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
     att = ops.attention(qkv, lens, H, dk, float(np.power(dk, 0.5)), layout=layout)
     h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
                    residual=x, ln=lp.ln1, lens=lens, layout=layout)
+    q = lp.fp8
+    if q is not None:
+        # cfg5: the FFN pair on e4m3 MFMA. The fc+LN epilogue also writes the fp8 copy of h the
+        # k=9 conv reads; the k=9 epilogue writes relu(.) directly as fp8 for w_2.
+        h8 = (layout.empty(d_model, torch.float8_e4m3fn) if layout is not None
+              else torch.empty(*x.shape[:-1], d_model, device=x.device, dtype=torch.float8_e4m3fn))
+        h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN,
+                       out_dtype=dt, residual=x, ln=lp.ln1, lens=lens, layout=layout, out2=h8,
+                       out2_scale=1.0 / q.s_h)
+        if timed and TIMERS is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        f8 = ops.conv1d(h8, q.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=L.FS2_FP8,
+                        epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_FP8, out_scale=1.0 / q.s_f, col_scale=q.cs1,
+                        layout=layout)
+        if timed and TIMERS is not None:
+            e1.record()
+            TIMERS.append((e0, e1))
+        return ops.conv1d(f8, q.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=L.FS2_FP8,
+                          epilogue=L.EPI_RES_LN, out_dtype=dt, residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1,
+                          addvec2=addvec2, layout=layout, col_scale=q.cs2)
     if timed and TIMERS is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -76,6 +100,11 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
     if timed and TIMERS is not None:
         e1.record()
         TIMERS.append((e0, e1))
+    if CALIB is not None and lp.key is not None:
+        rows = int(layout.cu[-1]) if layout is not None else None
+        hv, fv = (h[:rows], f[:rows]) if rows is not None else (h, f)
+        CALIB[lp.key] = (float(hv.float().abs().max()) if hv.numel() else 0.0,
+                         float(fv.float().abs().max()) if fv.numel() else 0.0)
     return ops.conv1d(f, lp.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
                       residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2, layout=layout)
 

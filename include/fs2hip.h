@@ -26,7 +26,7 @@ extern "C" {
 
 typedef void *fs2_stream_t; /* a hipStream_t (NULL = default stream) */
 
-enum fs2_dtype { FS2_F32 = 0, FS2_BF16 = 1 };
+enum fs2_dtype { FS2_F32 = 0, FS2_BF16 = 1, FS2_FP8 = 2 /* OCP e4m3fn bytes (gfx950 MFMA format) */ };
 
 enum fs2_status {
   FS2_OK = 0,
@@ -101,6 +101,13 @@ typedef struct fs2_conv_desc {
   const int32_t *rows_dev;  /* packed rows: device int32 = active row count, or NULL (padded) */
   const int32_t *row_pos;   /* packed rows: int32 [rows][2] = {frame, sequence length}       */
   const int32_t *a_rowmap;  /* int32 [B*T] packed source row of each output row, or NULL     */
+  /* fp8 (compute == FS2_FP8: x and w are e4m3fn bytes, mfma_scale_f32_16x16x128_f8f6f4):        */
+  const float *col_scale;   /* [N] dequantisation scale applied to the accumulator before the
+                               bias (x scale * per-channel w scale), or NULL                    */
+  float out_scale;          /* out_dtype == FS2_FP8: stored value = e4m3(y * out_scale)         */
+  void *out2;               /* LN epilogues: optional second output, e4m3(y * out2_scale),
+                               rows of N bytes (the fp8 copy the next fp8 GEMM reads)           */
+  float out2_scale;
 } fs2_conv_desc;
 
 int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream);

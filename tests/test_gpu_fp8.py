@@ -1,0 +1,129 @@
+"""fp8 (e4m3fn, mfma_scale_f32_16x16x128_f8f6f4) conv GEMMs: cfg5 kernels.
+
+Kernel parity is against a float64 conv of the SAME quantised operands (x_q * s_x, w_q * s_w):
+fp8 x fp8 products are exact in f32, so only the f32 summation order differs — tolerance 1e-4
+of the output's max (this pins the MFMA lane map and the dequantisation scales). Quantisation
+error itself (fp8 vs bf16) is a reported number, not a parity bound (test_fp8_model_*).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from fs2amd import _lib as L, ops
+
+    return ops, L
+
+
+def _quant(x):
+    s = float(x.abs().max()) / 448.0
+    return (x / s).clamp(-448, 448).to(torch.float8_e4m3fn), s
+
+
+def _deq_w(wq, sw, cin):
+    return (wq.float()[:, :, :cin].permute(0, 2, 1) * sw.view(-1, 1, 1)).double()
+
+
+@pytest.mark.parametrize("B,T,cin,n,ks,packed", [(8, 130, 256, 1024, 9, False), (5, 77, 256, 512, 5, False),
+                                                 (8, 130, 256, 1024, 9, True), (3, 40, 1024, 256, 1, False)])
+def test_fp8_conv_relu_matches_dequantized_reference(gpu, B, T, cin, n, ks, packed):
+    ops, L = gpu
+    g = torch.Generator().manual_seed(2)
+    lens = torch.randint(1, T + 1, (B,), generator=g)
+    lens[0] = T
+    valid = (torch.arange(T)[None, :] < lens[:, None])[..., None]
+    x = torch.randn(B, T, cin, generator=g) * (valid if packed else 1)
+    w = torch.randn(n, cin, ks, generator=g) / (cin * ks) ** 0.5
+    b = torch.randn(n, generator=g) * 0.1
+    xq, sx = _quant(x)
+    wq, sw = ops.pack_conv_weight_fp8(w.to(DEV))
+    kw = dict(cin=cin, ks=ks, pad=(ks - 1) // 2, compute=L.FS2_FP8, epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_F32,
+              col_scale=(sw * sx).contiguous())
+    xd = xq.double() * sx
+    ref = torch.relu(F.conv1d(xd.transpose(1, 2), _deq_w(wq, sw, cin).cpu(), b.double(), padding=(ks - 1) // 2)
+                     .transpose(1, 2))
+    if packed:
+        lay = ops.SeqLayout(lens.to(DEV), T)
+        rm = lay.rowmap.long().cpu()
+        xp = torch.zeros(B * T, cin, dtype=torch.float8_e4m3fn)
+        ok = rm >= 0
+        xp[rm[ok]] = xq.reshape(-1, cin)[ok]
+        out = ops.conv1d(xp.to(DEV), wq, b.to(DEV), layout=lay, **kw)
+        R = int(lay.cu[-1])
+        got, ref = out[:R].double().cpu(), ref.reshape(-1, n)[valid.reshape(-1)]
+    else:
+        got = ops.conv1d(xq.to(DEV), wq, b.to(DEV), **kw).double().cpu()
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 1e-4, err
+
+
+def test_fp8_output_and_ln_fp8_copy(gpu):
+    """fp8 output of the ReLU epilogue (e4m3(y * out_scale)) and the LN epilogue's fp8 copy
+    (out2) round-trip within e4m3 rounding (2^-4 relative) of the f32 results."""
+    ops, L = gpu
+    g = torch.Generator().manual_seed(3)
+    B, T, cin, n = 4, 64, 1024, 256
+    x = torch.randn(B, T, cin, generator=g)
+    xq, sx = _quant(x)
+    wq, sw = ops.pack_conv_weight_fp8((torch.randn(n, cin, 1, generator=g) / 32).to(DEV))
+    b = (torch.randn(n, generator=g) * 0.1).to(DEV)
+    res = torch.randn(B, T, n, generator=g).to(DEV, torch.bfloat16)
+    ln = (torch.ones(n, device=DEV), torch.zeros(n, device=DEV), 1e-5)
+    kw = dict(cin=cin, ks=1, pad=0, compute=L.FS2_FP8, col_scale=(sw * sx).contiguous())
+    y = ops.conv1d(xq.to(DEV), wq, b, epilogue=L.EPI_RES_LN, out_dtype=L.FS2_F32, residual=res, ln=ln, **kw)
+    y8 = torch.empty(B, T, n, device=DEV, dtype=torch.float8_e4m3fn)
+    s2 = 448.0 / 6.0
+    y_again = ops.conv1d(xq.to(DEV), wq, b, epilogue=L.EPI_RES_LN, out_dtype=L.FS2_F32, residual=res, ln=ln,
+                         out2=y8, out2_scale=s2, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_again)
+    back = y8.float() / s2
+    ref = y.clamp(-6.0, 6.0)
+    assert float(((back - ref).abs() / ref.abs().clamp_min(2 ** -6)).max()) <= 2 ** -4 + 1e-6
+    # ReLU epilogue with an fp8 output
+    f8 = ops.conv1d(xq.to(DEV), wq, b, epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_FP8, out_scale=20.0, **kw)
+    f32 = ops.conv1d(xq.to(DEV), wq, b, epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_F32, **kw)
+    back = f8.float() / 20.0
+    ref = f32.clamp(max=448.0 / 20.0)
+    assert float(((back - ref).abs() / ref.abs().clamp_min(2 ** -6 / 20)).max()) <= 2 ** -4 + 1e-6
+
+
+def test_fp8_model_vs_bf16_reported(gpu):
+    """cfg5 at the bench shape: fp8 FFN GEMMs vs the bf16 path, teacher-forced durations and
+    pitch/energy pinned to the bf16 predictions (no bucket flips). Reported numbers (printed);
+    the bound asserted is a sanity bound, not a parity claim: mean |d postnet| <= 0.1,
+    max <= 1.0 (postnet values are O(1); e4m3 keeps 3 mantissa bits, 2^-4 relative per element;
+    round 1 measured mean 0.050, max 0.33)."""
+    from _common import configs
+    from fs2amd.data import synth_batch, to_device
+    from fs2amd.model import FastSpeech2
+    from fs2amd.synth_weights import fill_module
+
+    pc, mc, _ = configs()
+    m = FastSpeech2(pc, mc)
+    fill_module(m, seed=0)
+    m = m.to(DEV).eval().set_precision("bf16")
+    args = to_device(synth_batch(64, 64, seed=1), DEV)
+    with torch.no_grad():
+        ref = m(**args)
+        pinned = dict(args, p_targets=ref[2], e_targets=ref[3])
+        ref = m(**pinned)
+        m.calibrate_fp8(**to_device(synth_batch(64, 64, seed=1000), DEV))
+        m.set_precision("fp8")
+        got = m(**pinned)
+    ml = ref[9]
+    valid = (torch.arange(ref[1].shape[1], device=DEV)[None, :] < ml[:, None])[..., None]
+    err = (got[1] - ref[1]).abs().masked_select(valid)
+    mel_err = (got[0] - ref[0]).abs().masked_select(valid)
+    print(f"\nfp8 vs bf16 (cfg2, pinned): postnet max {float(err.max()):.4f} mean {float(err.mean()):.5f}; "
+          f"mel max {float(mel_err.max()):.4f} mean {float(mel_err.mean()):.5f}")
+    assert float(err.mean()) <= 0.1 and float(err.max()) <= 1.0
+    assert torch.equal(got[9], ref[9])
