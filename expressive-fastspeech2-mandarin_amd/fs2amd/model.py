@@ -202,7 +202,7 @@ class FastSpeech2(nn.Module):
         self._vp_precision = hip.get("vp_dtype", os.environ.get("FS2_HIP_VP_DTYPE", "fp32"))
         self._packs = {}
         self.train_dropout = True  # False: train-mode semantics without dropout (parity tests)
-        self._fp8_scales = None    # {("enc"|"dec", layer): (amax of FFN input h, amax of w_1 output f)}
+        self._fp8_scales = None    # {("enc"|"dec", layer): {"x": amax block input, "h": FFN input, "f": w_1 out}}
         self.register_load_state_dict_post_hook(lambda mod, keys: mod.invalidate_packed())
 
     # ---- precision / packed weights --------------------------------------------------------------
@@ -222,8 +222,9 @@ class FastSpeech2(nn.Module):
 
     def calibrate_fp8(self, **batch):
         """Static fp8 activation scales (cfg5): one bf16 forward on ``batch`` records, per FFT
-        block, max|h| (input of the FFN Conv1d k=9) and max|relu(w_1 h)| (input of w_2) over the
-        valid frames; fp8 packing derives s = amax / 448 from them. Returns the scales."""
+        block, max|x| (block input, the Q|K|V GEMM's), max|h| (input of the FFN Conv1d k=9) and
+        max|relu(w_1 h)| (input of w_2) over the valid frames; fp8 packing derives s = amax / 448
+        from them. Returns the scales."""
         from . import runtime
 
         prev = self._precision
@@ -232,7 +233,7 @@ class FastSpeech2(nn.Module):
         try:
             with torch.no_grad():
                 self.forward(**batch)
-            self._fp8_scales = {k: (float(h), float(f)) for k, (h, f) in runtime.CALIB.items()}
+            self._fp8_scales = {k: dict(v) for k, v in runtime.CALIB.items()}
         finally:
             runtime.CALIB = None
             self._precision = prev

@@ -7,9 +7,10 @@
   b' = (b - rm) * g/sqrt(rv+eps) + beta (transformer/Layers.py:92-135).
 * bf16 precision: FFT blocks, mel_linear, PostNet in bf16; VariancePredictors f32 unless
   vp_precision == "bf16".
-* fp8 precision (cfg5): as bf16, plus the FFN Conv1d pair of every FFT block in e4m3fn with
-  per-output-channel weight scales; the dequantisation vector col_scale = s_in * s_w[n] uses the
-  layer's static input-activation scale from FastSpeech2.calibrate_fp8 (s = amax / 448).
+* fp8 precision (cfg5): as bf16, plus the FFN Conv1d pair of every FFT block, and the Q|K|V
+  projection of every block after the first of its stack, in e4m3fn with per-output-channel
+  weight scales; the dequantisation vector col_scale = s_in * s_w[n] uses the layer's static
+  input-activation scale from FastSpeech2.calibrate_fp8 (s = amax / 448).
 Everything else (LayerNorm affine, biases, embedding tables, bins, PE tables) stays f32.
 """
 from types import SimpleNamespace
@@ -30,12 +31,15 @@ def _fft_layer(layer, device, compute, key=None, fp8_scales=None):
     bqkv = torch.cat([a.w_qs.bias, a.w_ks.bias, a.w_vs.bias], 0)
     fp8 = None
     if fp8_scales is not None:
-        amax_h, amax_f = fp8_scales[key]
-        s_h, s_f = max(amax_h, 1e-6) / FP8_MAX, max(amax_f, 1e-6) / FP8_MAX
+        sc = fp8_scales[key]
+        s_h, s_f, s_x = (max(sc[k], 1e-6) / FP8_MAX for k in ("h", "f", "x"))
         w1, sw1 = pack_conv_weight_fp8(f.w_1.weight.to(device))
         w2, sw2 = pack_conv_weight_fp8(f.w_2.weight.to(device))
-        fp8 = SimpleNamespace(s_h=s_h, s_f=s_f, w1=w1, w2=w2, cs1=(sw1 * s_h).contiguous(),
-                              cs2=(sw2 * s_f).contiguous())
+        fp8 = SimpleNamespace(s_h=s_h, s_f=s_f, s_x=s_x, w1=w1, w2=w2, cs1=(sw1 * s_h).contiguous(),
+                              cs2=(sw2 * s_f).contiguous(), wqkv=None, cs_qkv=None)
+        if key[1] > 0:  # input produced by the previous block's LN epilogue, which writes the fp8 copy
+            wq, swq = pack_conv_weight_fp8(wqkv)
+            fp8.wqkv, fp8.cs_qkv = wq, (swq * s_x).contiguous()
     return SimpleNamespace(
         key=key, fp8=fp8,
         n_head=a.n_head, d_k=a.d_k,

@@ -57,21 +57,37 @@ TIMERS = None
 CALIB = None
 
 
-def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=None):
+def _fp8_like(x, layout, width):
+    if layout is not None:
+        return layout.empty(width, torch.float8_e4m3fn)
+    return torch.empty(*x.shape[:-1], width, device=x.device, dtype=torch.float8_e4m3fn)
+
+
+def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=None, x8=None, next_s=None):
     """One FFT block (transformer/Layers.py:21-30) = 5 launches. With ``layout`` (ops.SeqLayout)
-    x is packed [B*T, d_model]: only valid frames exist and no mask is applied (nothing to mask)."""
+    x is packed [B*T, d_model]: only valid frames exist and no mask is applied (nothing to mask).
+    fp8 (cfg5): ``x8`` is the fp8 copy of x for the Q|K|V GEMM; ``next_s`` asks for an fp8 copy
+    of the block output at that scale (the next block's Q|K|V input). Returns (out, out8|None)."""
     c = P.compute
     dt = P.act_dtype
     H, dk = lp.n_head, lp.d_k
     d_model = H * dk
     if layout is not None:
         lens = None
-    qkv = ops.conv1d(x, lp.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_BIAS, out_dtype=dt,
-                     layout=layout)
+    q = lp.fp8
+    if CALIB is not None and lp.key is not None:
+        rows = int(layout.cu[-1]) if layout is not None else None
+        xv = x[:rows] if rows is not None else x
+        CALIB.setdefault(lp.key, {})["x"] = float(xv.float().abs().max()) if xv.numel() else 0.0
+    if q is not None and q.wqkv is not None and x8 is not None:
+        qkv = ops.conv1d(x8, q.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=L.FS2_FP8, epilogue=L.EPI_BIAS,
+                         out_dtype=dt, col_scale=q.cs_qkv, layout=layout)
+    else:
+        qkv = ops.conv1d(x, lp.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_BIAS,
+                         out_dtype=dt, layout=layout)
     att = ops.attention(qkv, lens, H, dk, float(np.power(dk, 0.5)), layout=layout)
     h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
                    residual=x, ln=lp.ln1, lens=lens, layout=layout)
-    q = lp.fp8
     if q is not None:
         # cfg5: the FFN pair on e4m3 MFMA. The fc+LN epilogue also writes the fp8 copy of h the
         # k=9 conv reads; the k=9 epilogue writes relu(.) directly as fp8 for w_2.
@@ -89,9 +105,12 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
         if timed and TIMERS is not None:
             e1.record()
             TIMERS.append((e0, e1))
-        return ops.conv1d(f8, q.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=L.FS2_FP8,
-                          epilogue=L.EPI_RES_LN, out_dtype=dt, residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1,
-                          addvec2=addvec2, layout=layout, col_scale=q.cs2)
+        y8 = _fp8_like(x, layout, d_model) if next_s is not None else None
+        y = ops.conv1d(f8, q.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=L.FS2_FP8,
+                       epilogue=L.EPI_RES_LN, out_dtype=dt, residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1,
+                       addvec2=addvec2, layout=layout, col_scale=q.cs2, out2=y8,
+                       out2_scale=1.0 / next_s if next_s is not None else 1.0)
+        return y, y8
     if timed and TIMERS is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -103,10 +122,23 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
     if CALIB is not None and lp.key is not None:
         rows = int(layout.cu[-1]) if layout is not None else None
         hv, fv = (h[:rows], f[:rows]) if rows is not None else (h, f)
-        CALIB[lp.key] = (float(hv.float().abs().max()) if hv.numel() else 0.0,
-                         float(fv.float().abs().max()) if fv.numel() else 0.0)
+        CALIB[lp.key]["h"] = float(hv.float().abs().max()) if hv.numel() else 0.0
+        CALIB[lp.key]["f"] = float(fv.float().abs().max()) if fv.numel() else 0.0
     return ops.conv1d(f, lp.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
-                      residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2, layout=layout)
+                      residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2, layout=layout), None
+
+
+def _stack(P, layers, x, lens, layout=None, timed=False, addvecs=(None, None)):
+    """FFT-block stack; in fp8 mode each block hands the next one an fp8 copy of its output."""
+    x8 = None
+    n = len(layers)
+    for i, lp in enumerate(layers):
+        nxt = layers[i + 1] if i + 1 < n else None
+        next_s = nxt.fp8.s_x if (nxt is not None and nxt.fp8 is not None and nxt.fp8.wqkv is not None) else None
+        last = i == n - 1
+        x, x8 = fft_block(P, lp, x, lens, addvecs[0] if last else None, addvecs[1] if last else None, timed=timed,
+                          layout=layout, x8=x8, next_s=next_s)
+    return x
 
 
 def packed_decoder_ok(P):
@@ -198,9 +230,7 @@ def _stage1(P, va, g, p_control, d_control):
             getattr(P, "aro_table", None), getattr(P, "val_table", None), getattr(P, "emo_w", None),
             getattr(P, "emo_b", None), P.d_model)
     n_enc = len(P.enc_layers)
-    for i, lp in enumerate(P.enc_layers):
-        last = i == n_enc - 1
-        x = fft_block(P, lp, x, g.lens_src, spk_vec if last else None, emo_vec if last else None)
+    x = _stack(P, P.enc_layers, x, g.lens_src, addvecs=(spk_vec, emo_vec))
     if n_enc == 0 and (spk_vec is not None or emo_vec is not None):
         raise NotImplementedError("encoder_layer = 0")
 
@@ -234,8 +264,7 @@ def _stage2(P, g, st, T_out, T_dec, p_control):
         lay = ops.SeqLayout(dec_lens, T_dec)
         x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype,
                           out_layout=lay)
-        for lp in P.dec_layers:
-            x = fft_block(P, lp, x, None, timed=True, layout=lay)
+        x = _stack(P, P.dec_layers, x, None, layout=lay, timed=True)
         mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
                          out_dtype=L.FS2_F32, src_layout=lay)
         return mel, _postnet(P, mel), st
@@ -255,8 +284,7 @@ def _stage2(P, g, st, T_out, T_dec, p_control):
             x = x[:, :T_dec].contiguous()
     if T_dec != T_out:
         dec_lens = torch.clamp(dec_lens, max=T_dec)
-    for lp in P.dec_layers:
-        x = fft_block(P, lp, x, dec_lens, timed=True)
+    x = _stack(P, P.dec_layers, x, dec_lens, timed=True)
     mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
                      out_dtype=L.FS2_F32)
     return mel, _postnet(P, mel), st
