@@ -12,8 +12,6 @@ class FastSpeech2Loss(nn.Module):
         super().__init__()
         self.pitch_feature_level = preprocess_config["preprocessing"]["pitch"]["feature"]
         self.energy_feature_level = preprocess_config["preprocessing"]["energy"]["feature"]
-        self.mse_loss = nn.MSELoss()
-        self.mae_loss = nn.L1Loss()
 
     def forward(self, inputs, predictions):
         mel_targets, _, _, pitch_targets, energy_targets, duration_targets = inputs[9:]
@@ -24,23 +22,19 @@ class FastSpeech2Loss(nn.Module):
         mel_targets = mel_targets[:, : mel_valid.shape[1], :].detach()
         pitch_targets, energy_targets = pitch_targets.detach(), energy_targets.detach()
 
-        def sel(level, pred, tgt):
-            m = src_valid if level == "phoneme_level" else mel_valid
-            return pred.masked_select(m), tgt.masked_select(m)
+        # masked means as sum(err * mask) / count: the same quantity as masked_select(...).mean()
+        # (NaN for an empty selection, like the reference) without a data-dependent shape, so the
+        # step has no host sync here
+        def mmean(err, m):
+            mf = m.to(err.dtype).expand_as(err)
+            return (err * mf).sum() / mf.sum()
 
-        pitch_pred, pitch_targets = sel(self.pitch_feature_level, pitch_pred, pitch_targets)
-        energy_pred, energy_targets = sel(self.energy_feature_level, energy_pred, energy_targets)
-        log_d_pred = log_d_pred.masked_select(src_valid)
-        log_d_targets = log_d_targets.masked_select(src_valid)
+        sel = lambda level: src_valid if level == "phoneme_level" else mel_valid
         mv = mel_valid.unsqueeze(-1)
-        mel_pred = mel_pred.masked_select(mv)
-        postnet_pred = postnet_pred.masked_select(mv)
-        mel_targets = mel_targets.masked_select(mv)
-
-        mel_loss = self.mae_loss(mel_pred, mel_targets)
-        postnet_mel_loss = self.mae_loss(postnet_pred, mel_targets)
-        pitch_loss = self.mse_loss(pitch_pred, pitch_targets)
-        energy_loss = self.mse_loss(energy_pred, energy_targets)
-        duration_loss = self.mse_loss(log_d_pred, log_d_targets)
+        mel_loss = mmean((mel_pred - mel_targets).abs(), mv)
+        postnet_mel_loss = mmean((postnet_pred - mel_targets).abs(), mv)
+        pitch_loss = mmean((pitch_pred - pitch_targets) ** 2, sel(self.pitch_feature_level))
+        energy_loss = mmean((energy_pred - energy_targets) ** 2, sel(self.energy_feature_level))
+        duration_loss = mmean((log_d_pred - log_d_targets) ** 2, src_valid)
         total = mel_loss + postnet_mel_loss + duration_loss + pitch_loss + energy_loss
         return total, mel_loss, postnet_mel_loss, pitch_loss, energy_loss, duration_loss

@@ -73,6 +73,8 @@ def pack_conv_weight(w, compute, scale=None):
         w = w * scale.detach().float().view(-1, 1, 1)
     N, cin, ks = w.shape
     cp = cin_pad(cin, compute)
+    if cp == cin:  # one fused permute + cast copy
+        return torch.empty(N, ks, cin, dtype=torch_dtype(compute), device=w.device).copy_(w.permute(0, 2, 1))
     out = torch.zeros(N, ks, cp, dtype=torch_dtype(compute), device=w.device)
     out[:, :, :cin] = w.permute(0, 2, 1).to(out.dtype)
     return out.contiguous()

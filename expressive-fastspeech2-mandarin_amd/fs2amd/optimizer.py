@@ -8,8 +8,10 @@ import torch
 class ScheduledOptim:
     def __init__(self, model, train_config, model_config, current_step):
         opt = train_config["optimizer"]
-        self._optimizer = torch.optim.Adam(model.parameters(), betas=opt["betas"], eps=opt["eps"],
-                                           weight_decay=opt["weight_decay"])
+        params = [p for p in model.parameters()]
+        fused = bool(params) and all(p.is_cuda for p in params)  # one multi-tensor kernel per step on the GPU
+        self._optimizer = torch.optim.Adam(params, betas=opt["betas"], eps=opt["eps"],
+                                           weight_decay=opt["weight_decay"], fused=fused)
         self.n_warmup_steps = opt["warm_up_step"]
         self.anneal_steps = opt["anneal_steps"]
         self.anneal_rate = opt["anneal_rate"]

@@ -55,8 +55,12 @@ class Conv1dFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             # dx[s] = sum_k W_k^T dy[s + pad - k]: a conv of dy with taps flipped, W transposed
-            wt = w3.flip(-1).transpose(0, 1).contiguous()  # [Cin, N, KS]
-            dx = ops.conv1d(dyc, ops.pack_conv_weight(wt, compute), None, cin=N, ks=KS, pad=KS - 1 - pad,
+            if N == ops.cin_pad(N, compute):  # packed [Cin][KS][N] = w[n, c, KS-1-k]: one copy
+                wtp = torch.empty(Cin, KS, N, dtype=ops.torch_dtype(compute), device=w3.device).copy_(
+                    w3.flip(-1).permute(1, 2, 0))
+            else:
+                wtp = ops.pack_conv_weight(w3.flip(-1).transpose(0, 1), compute)
+            dx = ops.conv1d(dyc, wtp, None, cin=N, ks=KS, pad=KS - 1 - pad,
                             compute=compute, epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
         if ctx.needs_input_grad[1]:
             B, T, _ = xc.shape

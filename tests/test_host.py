@@ -232,3 +232,45 @@ def test_training_step_dry_run(monkeypatch):
     ref = {str(k) for k in np.load(f"{GOLDEN}/train_grads.npz")["grad_keys"]}
     assert got == ref, got ^ ref
     assert "fs2_conv1d" in lib.calls and "fs2_attention" in lib.calls
+
+
+def test_loss_matches_oracle_masked_select_form():
+    """fs2amd.loss (mask-weighted sums, no host sync) vs the oracle's restatement of
+    model/loss.py (masked_select + mean), with gradients."""
+    from oracle import fs2_oracle as O
+    from fs2amd.loss import FastSpeech2Loss
+
+    pc, mc, _ = configs()
+    g = torch.Generator().manual_seed(0)
+    B, L, T = 3, 9, 31
+    src_lens, mel_lens = torch.tensor([9, 5, 1]), torch.tensor([31, 17, 4])
+    src_masks = torch.arange(L)[None, :] >= src_lens[:, None]
+    mel_masks = torch.arange(T)[None, :] >= mel_lens[:, None]
+    preds = [torch.randn(B, T, 80, generator=g, requires_grad=True), torch.randn(B, T, 80, generator=g, requires_grad=True),
+             torch.randn(B, L, generator=g, requires_grad=True), torch.randn(B, L, generator=g, requires_grad=True),
+             torch.randn(B, L, generator=g, requires_grad=True)]
+    out = (*preds, None, src_masks, mel_masks, src_lens, mel_lens)
+    mels, pt, et = torch.randn(B, T + 2, 80, generator=g), torch.randn(B, L, generator=g), torch.randn(B, L, generator=g)
+    dur = torch.randint(0, 7, (B, L), generator=g)
+    ours = FastSpeech2Loss(pc, mc)((None,) * 9 + (mels, mel_lens, T, pt, et, dur), out)
+    ref = O.loss(pc, mels, pt, et, dur, out)
+    for a, b in zip(ours, ref):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+    ga = torch.autograd.grad(ours[0], preds)
+    gb = torch.autograd.grad(ref[0], preds)
+    for a, b in zip(ga, gb):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.parametrize("compute", [0, 1])
+@pytest.mark.parametrize("cin", [80, 256])
+def test_pack_conv_weight_layout(compute, cin):
+    """packed[n, k, c] == w[n, c, k] (zero channel padding), contiguous, compute dtype."""
+    from fs2amd import ops
+
+    w = torch.randn(12, cin, 5)
+    p = ops.pack_conv_weight(w, compute)
+    assert p.is_contiguous() and p.dtype == ops.torch_dtype(compute)
+    assert p.shape == (12, 5, ops.cin_pad(cin, compute))
+    torch.testing.assert_close(p[:, :, :cin].float(), w.permute(0, 2, 1).to(p.dtype).float())
+    assert not p[:, :, cin:].float().abs().sum()
