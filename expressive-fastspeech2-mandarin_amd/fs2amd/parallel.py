@@ -22,19 +22,25 @@ def init(backend=None):
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":
-        torch.cuda.set_device(local)
-        device = torch.device(f"cuda:{local}")
+        ndev = torch.cuda.device_count()
+        dev_index = local if local < ndev else local % max(ndev, 1)
+        torch.cuda.set_device(dev_index)
+        device = torch.device(f"cuda:{dev_index}")
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world)
+        kw = {"device_id": device} if backend == "nccl" else {}
+        dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world, **kw)
     return rank, local, world, device
 
 
 def barrier():
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.barrier()
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
 
 
 def aggregate(elapsed_s, frames, device):

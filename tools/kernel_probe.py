@@ -28,9 +28,11 @@ def main():
 
     dev = torch.device("cuda:0")
     model, _, _ = bench.build_model(dev, a.dtype)
-    P = model.packed(dev)
     bc = synth_batch(64, 64, seed=1)
     b = to_device(bc, dev)
+    if a.dtype == "fp8":
+        model.calibrate_fp8(**to_device(synth_batch(64, 64, seed=1000), dev))
+    P = model.packed(dev)
     B, T = 64, int(bc["max_mel_len"])
     dt = ops.torch_dtype(P.act_dtype)
     lp = P.dec_layers[0]
@@ -39,7 +41,12 @@ def main():
     lens = b["mel_lens"]
     # decoder kernels run on packed valid frames, as in the forward (runtime._stage2)
     lay = ops.SeqLayout(lens, T)
-    if a.kernel == "conv9":
+    if a.kernel == "conv9" and lp.fp8 is not None:
+        h = rnd(B * T, 256).to(torch.float8_e4m3fn)
+        fn = lambda: ops.conv1d(h, lp.fp8.w1, lp.b1, cin=256, ks=9, pad=4, compute=L.FS2_FP8,
+                                epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_FP8, out_scale=1.0 / lp.fp8.s_f,
+                                col_scale=lp.fp8.cs1, layout=lay)
+    elif a.kernel == "conv9":
         h = rnd(B * T, 256)
         fn = lambda: ops.conv1d(h, lp.w1, lp.b1, cin=256, ks=9, pad=4, compute=P.compute, epilogue=L.EPI_BIAS_RELU,
                                 out_dtype=P.act_dtype, layout=lay)
