@@ -30,8 +30,7 @@ def init(backend=None):
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        kw = {"device_id": device} if backend == "nccl" else {}
-        dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world, **kw)
+        dist.init_process_group(backend, init_method="env://", rank=rank, world_size=world)
     return rank, local, world, device
 
 
