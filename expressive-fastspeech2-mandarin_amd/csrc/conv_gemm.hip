@@ -160,7 +160,8 @@ struct ConvArgs {
   const int32_t *rows_dev;
   const int2 *row_pos;
   const int32_t *a_rowmap;  // KS == 1 only: A row of output row m (-1 = zero row)
-  int dbg;                  // analysis only (FS2_CONV_DEBUG): bit 0 skips the K loop, bit 1 the epilogue
+  int dbg;  // analysis only (FS2_CONV_DEBUG): bit 0 skips the K loop, bit 1 the epilogue; LN epilogue
+            // ablations: bit 2 no stores, bit 3 no residual loads, bit 4 no row reductions
   const float *colscale;    // fp8: per-column dequantisation scale of the accumulator (or NULL)
   float out_scale;          // out_dt == FS2_FP8: e4m3(y * out_scale)
   void *out2;               // LN epilogues: optional fp8 copy e4m3(y * out2_scale), rows of N bytes
@@ -232,7 +233,10 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
     constexpr int RPW = BM / NWAVES;
     uint4 rraw[RPW];
     const bool res_bf16 = a.res_dt == FS2_BF16;
-    if (epi == FS2_EPI_RES_LN) {
+    if (epi == FS2_EPI_RES_LN && (a.dbg & 8)) {
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) rraw[i] = make_uint4(0u, 0u, 0u, 0u);
+    } else if (epi == FS2_EPI_RES_LN) {
       if (res_bf16) {
         const bf16 *rp = reinterpret_cast<const bf16 *>(a.res);
 #pragma unroll
@@ -255,8 +259,10 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
       const int r = wid + i * NWAVES;
-      const int m = m0 + r;
-      if (m >= M) break;
+      // rows past M are computed on clamped data and not stored: no control dependency between
+      // rows, so the compiler can interleave their (latency-bound) reduction chains
+      const bool row_ok = m0 + r < M;
+      const int m = min(m0 + r, M - 1);
       float v[4];
       load4(E + r * EPI_LD + n, v);
 #pragma unroll
@@ -280,14 +286,15 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.0f);
       }
-      const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * inv_n;
+      const bool nored = (a.dbg & 16) != 0;
+      const float mean = (nored ? (v[0] + v[1] + v[2] + v[3]) : wave_sum(v[0] + v[1] + v[2] + v[3])) * inv_n;
       float d[4], ss = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         d[q] = v[q] - mean;
         ss += d[q] * d[q];
       }
-      const float var = wave_sum(ss) * inv_n;
+      const float var = (nored ? ss : wave_sum(ss)) * inv_n;
       const float rstd = 1.0f / sqrtf(var + a.eps);
       float y[4];
 #pragma unroll
@@ -299,7 +306,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
         float dw4[4];
         load4(a.dw + n, dw4);
         const float s = wave_sum(y[0] * dw4[0] + y[1] * dw4[1] + y[2] * dw4[2] + y[3] * dw4[3]) + a.db;
-        if (lane == 0) reinterpret_cast<float *>(a.out)[m] = masked ? 0.0f : s;
+        if (lane == 0 && row_ok) reinterpret_cast<float *>(a.out)[m] = masked ? 0.0f : s;
         continue;
       }
       if (epi == FS2_EPI_RES_LN) {
@@ -320,6 +327,11 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
           for (int q = 0; q < 4; ++q) y[q] += av[q];
         }
       }
+      if (a.dbg & 4) {
+        asm volatile("" ::"v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]));
+        continue;
+      }
+      if (!row_ok) continue;
       store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, y, a.out_scale);
       if (a.out2 != nullptr)
         *reinterpret_cast<unsigned *>(reinterpret_cast<fp8 *>(a.out2) + (int64_t)m * a.N + n) = pack4_fp8(y, a.out2_scale);
