@@ -319,14 +319,20 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
   f32x4 oacc[DK / 16];
 #pragma unroll
   for (int i = 0; i < DK / 16; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // running max kept in RAW score units (scale > 0 commutes with max): p = exp2(fma(s, c, -m*c))
   float m_run = -INFINITY, l_run = 0.f;
 
   const int ntiles = (len + KT - 1) / KT;
   if (ntiles > 0) dma(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // transposed-read lane roles: lane 4q+p of its 16-lane group addresses row q, columns 4p..4p+3
+  // transposed-read lane roles: lane 4q+p of its 16-lane group addresses row q, columns 4p..4p+3.
+  // kv_off's swizzle depends on (row & 3, (row >> 2) & 3), so rows +16 / +32 are +4 / +8 KiB:
+  // only the 8 column-block offsets of row r0 are lane-specific (hoisted out of the key loop).
   const int tq = li >> 2, tp = li & 3;
+  int voff[DK / 16];
+#pragma unroll
+  for (int nd = 0; nd < DK / 16; ++nd) voff[nd] = kv_off(4 * g + tq, nd * 2 + (tp >> 1)) + (tp & 1) * 8;
   for (int kt = 0; kt < ntiles; ++kt) {
     const int k0 = kt * KT;
     if (kt + 1 < ntiles) dma(k0 + KT, (kt + 1) & 1);
@@ -343,29 +349,31 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
         sacc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], sacc[ni], 0, 0, 0);
       }
     }
-    // scores of query li: keys k0 + ni*16 + 4g + j
+    // scores of query li: keys k0 + ni*16 + 4g + j; only the last tile can hold padded keys
+    if (k0 + KT > len) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (k0 + ni * 16 + 4 * g + j >= len) sacc[ni][j] = -INFINITY;
+    }
     float mx = -INFINITY;
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int key = k0 + ni * 16 + 4 * g + j;
-        const float sv = key < len ? sacc[ni][j] * scale_log2 : -INFINITY;
-        sacc[ni][j] = sv;
-        mx = fmaxf(mx, sv);
-      }
+    for (int ni = 0; ni < 4; ++ni) mx = fmaxf(mx, fmaxf(fmaxf(sacc[ni][0], sacc[ni][1]), fmaxf(sacc[ni][2], sacc[ni][3])));
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
+    // raw v_exp_f32 (exp2; underflow -> 0, -inf -> 0): libm exp2f's range reduction is dead work here
+    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2);
     m_run = m_new;
+    const float mc = -m_new * scale_log2;
     float sum = 0.f;
     bf16x8 pf[2];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float p = exp2f(sacc[ni][j] - m_new);
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[ni][j], scale_log2, mc));
         sum += p;
         pf[ni >> 1][(ni & 1) * 4 + j] = (bf16)p;
       }
@@ -377,14 +385,12 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
 
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const int r0 = 32 * s2 + 4 * g + tq;  // this lane's address row (block 1), +16 for block 2
+      // this lane's address row r0 = 32*s2 + 4g + tq (block 1), r0 + 16 for block 2
 #pragma unroll
       for (int nd = 0; nd < DK / 16; ++nd) {
-        const int ch = nd * 2 + (tp >> 1), sub = (tp & 1) * 8;
-        auto lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4 *)(Vb + kv_off(r0, ch) + sub));
-        auto hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4 *)(Vb + kv_off(r0 + 16, ch) + sub));
+        const char *vp = Vb + voff[nd] + s2 * 32 * 256;
+        auto lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)vp);
+        auto hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)(vp + 16 * 256));
         bf16x8 vf;
         __builtin_memcpy(&vf, &lo, 8);
         __builtin_memcpy(reinterpret_cast<char *>(&vf) + 8, &hi, 8);
