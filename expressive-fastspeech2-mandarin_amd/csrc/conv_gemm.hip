@@ -166,7 +166,17 @@ struct ConvArgs {
   float out_scale;          // out_dt == FS2_FP8: e4m3(y * out_scale)
   void *out2;               // LN epilogues: optional fp8 copy e4m3(y * out2_scale), rows of N bytes
   float out2_scale;
+  int cin_block;            // split-precision input: logical channel blocks of cin_block (0 = off)
+  int cin_src[4];           // ... block i is source channel cin_src[i] of x
+  int out_split;            // LN epilogue: bf16 hi plane at column n, lo plane at column N + n
 };
+
+// Source channel of logical input channel c (split-precision layouts map channel blocks).
+__device__ __forceinline__ int src_channel(const ConvArgs &a, int c) {
+  if (a.cin_block == 0) return c;
+  const int blk = c / a.cin_block;
+  return a.cin_src[blk] + (c - blk * a.cin_block);
+}
 
 // Active rows and the XCD-aware tile of this workgroup. The dispatcher deals workgroup ids
 // round-robin over the 8 XCDs; each XCD gets a contiguous run of tiles, N-fastest, so the N tiles
@@ -332,6 +342,18 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
         continue;
       }
       if (!row_ok) continue;
+      if (a.out_split) {  // two bf16 planes: hi, lo = bf16(y - hi)
+        float hi[4], lo[4];
+        bf16 *op = reinterpret_cast<bf16 *>(a.out) + (int64_t)m * a.os;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          hi[q] = (float)(bf16)y[q];
+          lo[q] = y[q] - hi[q];
+        }
+        store4(op + n, hi);
+        store4(op + a.N + n, lo);
+        continue;
+      }
       store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, y, a.out_scale);
       if (a.out2 != nullptr)
         *reinterpret_cast<unsigned *>(reinterpret_cast<fp8 *>(a.out2) + (int64_t)m * a.N + n) = pack4_fp8(y, a.out2_scale);
@@ -999,11 +1021,12 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
     const int sh = tap - pad;
     const int ch = cb * KE + plc * CE;
     const bool ch_ok = ch < a.Cin;
+    const int sch = src_channel(a, ch);
 #pragma unroll
     for (int i = 0; i < AQ; ++i) {
       const bool ok = ch_ok && (unsigned)(apos[i] + sh) < (unsigned)alen[i];
       glds(xr, As + ((wid + NW * i) % AP) * 1024,
-           ok ? (uint32_t)(arow[i] + sh) * xrow + (uint32_t)ch * (uint32_t)sizeof(TW) : kOOB);
+           ok ? (uint32_t)(arow[i] + sh) * xrow + (uint32_t)sch * (uint32_t)sizeof(TW) : kOOB);
     }
     const uint32_t off = ((uint32_t)tap * a.Cin_pad + cb * KE) * (uint32_t)sizeof(TW);
 #pragma unroll
@@ -1363,7 +1386,7 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       const char *e = getenv("FS2_CONV_RING");
       return e == nullptr || e[0] != '0';
     }();
-    if (ln && ring) {  // LDS-DMA deep ring (LN epilogues, N == 256)
+    if (ln && (ring || a.cin_block != 0)) {  // LDS-DMA deep ring (LN epilogues, N == 256)
       // register-B variant: correct but measured 1.5x slower on the decoder conv1 in round 1
       // (per-lane 16 B weight loads from L2, two waves per column group); opt-in
       static const bool rb = [] {
@@ -1371,7 +1394,7 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         return e != nullptr && e[0] == '1';
       }();
       if constexpr (CT != FS2_FP8) {
-        if (a.M >= 192 * 128 && rb) {
+        if (a.M >= 192 * 128 && rb && a.cin_block == 0) {
           launch_rb<CT, 2, 4, 8, 2>(a, s);  // 128 x 256, 8 waves, B in registers, 8 A stages
           return;
         }
@@ -1419,7 +1442,18 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   if (d->compute == FS2_FP8 && d->x_dtype != FS2_FP8) return FS2_EUNSUPPORTED;  // fp8 GEMMs read fp8 copies
   if (d->B < 0 || d->T < 0 || d->Cin <= 0 || d->N <= 0 || d->KS <= 0 || d->pad < 0) return FS2_EINVAL;
   if (d->Cin % ce != 0 || d->N % 4 != 0 || d->Cin_pad != fs2_conv_cin_pad(d->Cin, d->compute)) return FS2_EINVAL;
-  if (d->x_row_stride < d->Cin || (d->x_row_stride % ce) != 0) return FS2_EINVAL;
+  if (d->cin_block != 0) {  // split-precision layout: blocks map into x's row; ring kernel path only
+    if (d->cin_block % 64 != 0 || d->Cin % d->cin_block != 0 || d->Cin / d->cin_block > 4) return FS2_EINVAL;
+    for (int i = 0; i < d->Cin / d->cin_block; ++i)
+      if (d->cin_src[i] < 0 || d->cin_src[i] + d->cin_block > d->x_row_stride) return FS2_EINVAL;
+    const bool ln_epi = d->epilogue == FS2_EPI_RES_LN || d->epilogue == FS2_EPI_RELU_LN ||
+                        d->epilogue == FS2_EPI_RELU_LN_DOT;
+    if (d->compute != FS2_BF16 || d->x_dtype != FS2_BF16 || !ln_epi) return FS2_EUNSUPPORTED;
+  } else if (d->x_row_stride < d->Cin) {
+    return FS2_EINVAL;
+  }
+  if ((d->x_row_stride % ce) != 0) return FS2_EINVAL;
+  if (d->out_split && (d->out_dtype != FS2_BF16 || d->out_row_stride < 2 * (int64_t)d->N)) return FS2_EINVAL;
   const int epi = d->epilogue;
   if (epi < FS2_EPI_BIAS || epi > FS2_EPI_RELU_LN_DOT) return FS2_EINVAL;
   const bool ln = epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN || epi == FS2_EPI_RELU_LN_DOT;
@@ -1478,6 +1512,9 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.out_scale = d->out_scale;
   a.out2 = d->out2;
   a.out2_scale = d->out2_scale;
+  a.cin_block = d->cin_block;
+  for (int i = 0; i < 4; ++i) a.cin_src[i] = d->cin_src[i];
+  a.out_split = d->out_split;
   {
     const int xes = d->x_dtype == FS2_BF16 ? 2 : (d->x_dtype == FS2_FP8 ? 1 : 4);
     const int wes = d->compute == FS2_BF16 ? 2 : (d->compute == FS2_FP8 ? 1 : 4);

@@ -41,6 +41,7 @@ class ConvDesc(ctypes.Structure):
         ("out", _p), ("out_dtype", _i), ("out_row_stride", _i64),
         ("rows_dev", _p), ("row_pos", _p), ("a_rowmap", _p),
         ("col_scale", _p), ("out_scale", _f), ("out2", _p), ("out2_scale", _f),
+        ("cin_block", _i), ("cin_src", _i * 4), ("out_split", _i),
     ]
 
 

@@ -199,7 +199,9 @@ class FastSpeech2(nn.Module):
             self.emotion_linear = nn.Sequential(nn.Linear(d, d), nn.ReLU())
         hip = model_config.get("hip", {}) if isinstance(model_config, dict) else {}
         self._precision = hip.get("dtype", os.environ.get("FS2_HIP_DTYPE", "fp32"))
-        self._vp_precision = hip.get("vp_dtype", os.environ.get("FS2_HIP_VP_DTYPE", "fp32"))
+        # VariancePredictors in bf16 / fp8 mode: split-precision bf16x3 (same discrete decisions as
+        # exact f32 on the cfg2 flip-rate sample, tools/flip_rate.py); "fp32" / "bf16" selectable
+        self._vp_precision = hip.get("vp_dtype", os.environ.get("FS2_HIP_VP_DTYPE", "bf16x3"))
         self._packs = {}
         self.train_dropout = True  # False: train-mode semantics without dropout (parity tests)
         self._fp8_scales = None    # {("enc"|"dec", layer): {"x": amax block input, "h": FFN input, "f": w_1 out}}
@@ -209,8 +211,8 @@ class FastSpeech2(nn.Module):
     def set_precision(self, dtype, vp_dtype=None):
         """dtype of the FFT blocks / attention / mel_linear / PostNet ('fp32' | 'bf16'); vp_dtype of
         the three VariancePredictors ('fp32' | 'bf16', bf16 only takes effect in bf16 mode)."""
-        if dtype not in ("fp32", "bf16", "fp8") or vp_dtype not in (None, "fp32", "bf16"):
-            raise ValueError("precision must be 'fp32', 'bf16' or 'fp8' (vp_dtype 'fp32' / 'bf16')")
+        if dtype not in ("fp32", "bf16", "fp8") or vp_dtype not in (None, "fp32", "bf16", "bf16x3"):
+            raise ValueError("precision must be 'fp32', 'bf16' or 'fp8' (vp_dtype 'fp32' / 'bf16' / 'bf16x3')")
         self._precision = dtype
         if vp_dtype is not None:
             self._vp_precision = vp_dtype

@@ -118,6 +118,20 @@ class SeqLayout:
         return out.view(self.B, self.T, C)
 
 
+def pack_conv_weight_split(w, blocks):
+    """bf16x3 split-precision weights: w = hi + lo (bf16 parts); the packed [N, KS, len(blocks)*Cin]
+    bf16 weight holds the part named by each block ('hi' / 'lo'), matching an input whose channel
+    blocks hold x_hi / x_lo (y = x_hi w_hi + x_hi w_lo + x_lo w_hi, the x_lo w_lo term dropped)."""
+    if w.dim() == 2:
+        w = w.unsqueeze(-1)
+    w = w.detach().float()
+    hi = w.to(torch.bfloat16)
+    lo = (w - hi.float()).to(torch.bfloat16)
+    parts = {"hi": hi, "lo": lo}
+    cat = torch.cat([parts[b] for b in blocks], dim=1)  # [N, len*Cin, KS]
+    return pack_conv_weight(cat.float(), L.FS2_BF16)
+
+
 def pack_conv_weight_fp8(w):
     """Per-output-channel e4m3fn quantisation: w[n] ~= q[n] * s[n], s[n] = max|w[n]| / 448.
     Returns (packed [N, KS, Cin_pad] float8_e4m3fn, s f32 [N])."""
@@ -135,7 +149,7 @@ def pack_conv_weight_fp8(w):
 
 def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None, out=None, residual=None,
            ln=None, lens=None, addvec1=None, addvec2=None, dot=None, n=None, layout=None, src_layout=None,
-           col_scale=None, out_scale=1.0, out2=None, out2_scale=1.0):
+           col_scale=None, out_scale=1.0, out2=None, out2_scale=1.0, cin_block=0, cin_src=(), out_split=False):
     """Implicit-GEMM Conv1d / Linear with a fused epilogue (fs2_conv1d).
 
     layout: x / residual / out are packed [B*T, C] in that SeqLayout. src_layout (KS == 1): x is
@@ -166,6 +180,11 @@ def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None
         d.addvec1 = addvec1.data_ptr()
     if addvec2 is not None:
         d.addvec2 = addvec2.data_ptr()
+    if cin_block:
+        d.cin_block = int(cin_block)
+        for i, c in enumerate(cin_src):
+            d.cin_src[i] = int(c)
+    d.out_split = 1 if out_split else 0
     if col_scale is not None:
         d.col_scale = col_scale.data_ptr()
     d.out_scale = float(out_scale)
@@ -184,7 +203,7 @@ def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None
         d.out, d.out_dtype, d.out_row_stride = out.data_ptr(), L.FS2_F32, 1
     else:
         if out is None:
-            out = torch.empty(*oshape, N, device=x.device, dtype=torch_dtype(out_dtype))
+            out = torch.empty(*oshape, 2 * N if out_split else N, device=x.device, dtype=torch_dtype(out_dtype))
         d.out, d.out_dtype, d.out_row_stride = out.data_ptr(), _dt(out), _rows(out, "out")
     L.check(_lib.fs2_conv1d(ctypes.byref(d), _stream(x)), "fs2_conv1d")
     return out

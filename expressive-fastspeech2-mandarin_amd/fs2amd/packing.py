@@ -5,8 +5,9 @@
 * Conv1d weights [N, Cin, K] re-laid to [N, K, Cin_pad] (k-steps = (tap, channel block)).
 * PostNet BatchNorm1d (eval: running stats) folded into its conv: w' = w * g/sqrt(rv+eps),
   b' = (b - rm) * g/sqrt(rv+eps) + beta (transformer/Layers.py:92-135).
-* bf16 precision: FFT blocks, mel_linear, PostNet in bf16; VariancePredictors f32 unless
-  vp_precision == "bf16".
+* bf16 precision: FFT blocks, mel_linear, PostNet in bf16; VariancePredictors exact f32
+  (vp_precision "fp32"), bf16 ("bf16") or split-precision bf16x3 ("bf16x3": w = w_hi + w_lo,
+  the hidden activation as two bf16 planes, three bf16 MFMA products per term).
 * fp8 precision (cfg5): as bf16, plus the FFN Conv1d pair of every FFT block, and the Q|K|V
   projection of every block after the first of its stack, in e4m3fn with per-output-channel
   weight scales; the dequantisation vector col_scale = s_in * s_w[n] uses the layer's static
@@ -18,7 +19,7 @@ from types import SimpleNamespace
 import torch
 
 from . import _lib as L
-from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8
+from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split
 
 
 def _f32(t, device):
@@ -54,11 +55,22 @@ def _fft_layer(layer, device, compute, key=None, fp8_scales=None):
     )
 
 
-def _vp(vp, device, compute):
+def _vp(vp, device, compute, split=False):
     cl = vp.conv_layer
     c1, c2 = cl.conv1d_1.conv, cl.conv1d_2.conv
+    if split:  # bf16x3: [x_hi | x_hi] x [w_hi | w_lo], then [h_hi | h_hi | h_lo] x [w_hi | w_lo | w_hi]
+        return SimpleNamespace(
+            compute=L.FS2_BF16, split=True,
+            w1=pack_conv_weight_split(c1.weight.to(device), ("hi", "lo")), b1=_f32(c1.bias, device),
+            k1=c1.kernel_size[0], p1=c1.padding[0], c1=c1.in_channels,
+            ln1=(_f32(cl.layer_norm_1.weight, device), _f32(cl.layer_norm_1.bias, device), cl.layer_norm_1.eps),
+            w2=pack_conv_weight_split(c2.weight.to(device), ("hi", "lo", "hi")), b2=_f32(c2.bias, device),
+            k2=c2.kernel_size[0], p2=c2.padding[0], c2=c2.in_channels,
+            ln2=(_f32(cl.layer_norm_2.weight, device), _f32(cl.layer_norm_2.bias, device), cl.layer_norm_2.eps),
+            lin_w=_f32(vp.linear_layer.weight.view(-1), device), lin_b=float(vp.linear_layer.bias.detach().cpu()[0]),
+        )
     return SimpleNamespace(
-        compute=compute,
+        compute=compute, split=False,
         w1=pack_conv_weight(c1.weight.to(device), compute), b1=_f32(c1.bias, device), k1=c1.kernel_size[0],
         p1=c1.padding[0], c1=c1.in_channels,
         ln1=(_f32(cl.layer_norm_1.weight, device), _f32(cl.layer_norm_1.bias, device), cl.layer_norm_1.eps),
@@ -84,7 +96,9 @@ def _postnet(pn, device, compute):
 def pack_model(model, device, precision, vp_precision="fp32", fp8_scales=None):
     device = torch.device(device)
     big = L.FS2_BF16 if precision in ("bf16", "fp8") else L.FS2_F32
-    vpc = L.FS2_BF16 if (precision in ("bf16", "fp8") and vp_precision == "bf16") else L.FS2_F32
+    low = precision in ("bf16", "fp8")
+    vpc = L.FS2_BF16 if (low and vp_precision == "bf16") else L.FS2_F32
+    vsplit = low and vp_precision == "bf16x3"
     if precision == "fp8" and fp8_scales is None:
         raise RuntimeError("fs2amd: fp8 precision needs activation scales: call model.calibrate_fp8(**batch) first")
     sc = fp8_scales if precision == "fp8" else None
@@ -95,7 +109,7 @@ def pack_model(model, device, precision, vp_precision="fp32", fp8_scales=None):
     P.dec_pe = _f32(model.decoder.position_enc[0], device)
     P.enc_layers = [_fft_layer(l, device, big, ("enc", i), sc) for i, l in enumerate(model.encoder.layer_stack)]
     P.dec_layers = [_fft_layer(l, device, big, ("dec", i), sc) for i, l in enumerate(model.decoder.layer_stack)]
-    P.vp = {k: _vp(getattr(va, f"{k}_predictor"), device, vpc) for k in ("duration", "pitch", "energy")}
+    P.vp = {k: _vp(getattr(va, f"{k}_predictor"), device, vpc, vsplit) for k in ("duration", "pitch", "energy")}
     P.bins = {k: _f32(getattr(va, f"{k}_bins"), device) for k in ("pitch", "energy")}
     P.var_table = {k: _f32(getattr(va, f"{k}_embedding").weight, device) for k in ("pitch", "energy")}
     P.mel_w = pack_conv_weight(model.mel_linear.weight.to(device), big)

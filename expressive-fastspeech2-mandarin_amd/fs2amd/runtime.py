@@ -154,7 +154,16 @@ def packed_decoder_ok(P):
 
 
 def variance_predictor(vp, x, lens):
-    """VariancePredictor (model/modules.py:209-250): 2 launches -> f32 [B, T] (f32 or bf16 MFMA)."""
+    """VariancePredictor (model/modules.py:209-250): 2 launches -> f32 [B, T] (f32, bf16 or bf16x3 MFMA)."""
+    if vp.split:
+        # bf16x3: logical inputs [x_hi | x_hi] (x is bf16: x_lo = 0) and [h_hi | h_hi | h_lo] read
+        # through the channel-block map; conv1's LN epilogue writes h as two bf16 planes
+        h2 = ops.conv1d(x, vp.w1, vp.b1, cin=2 * vp.c1, ks=vp.k1, pad=vp.p1, compute=L.FS2_BF16,
+                        epilogue=L.EPI_RELU_LN, out_dtype=L.FS2_BF16, ln=vp.ln1, cin_block=vp.c1, cin_src=(0, 0),
+                        out_split=True)
+        return ops.conv1d(h2, vp.w2, vp.b2, cin=3 * vp.c2, ks=vp.k2, pad=vp.p2, compute=L.FS2_BF16,
+                          epilogue=L.EPI_RELU_LN_DOT, ln=vp.ln2, lens=lens, dot=(vp.lin_w, vp.lin_b),
+                          cin_block=vp.c2, cin_src=(0, 0, vp.c2))
     h = ops.conv1d(x, vp.w1, vp.b1, cin=vp.c1, ks=vp.k1, pad=vp.p1, compute=vp.compute, epilogue=L.EPI_RELU_LN,
                    out_dtype=vp.compute, ln=vp.ln1)
     return ops.conv1d(h, vp.w2, vp.b2, cin=vp.c2, ks=vp.k2, pad=vp.p2, compute=vp.compute,

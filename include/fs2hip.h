@@ -108,6 +108,13 @@ typedef struct fs2_conv_desc {
   void *out2;               /* LN epilogues: optional second output, e4m3(y * out2_scale),
                                rows of N bytes (the fp8 copy the next fp8 GEMM reads)           */
   float out2_scale;
+  /* split-precision (bf16x3) GEMM: the logical input channels are blocks of cin_block channels,
+     block i read from source channel cin_src[i] of x (e.g. [x_hi | x_hi | x_lo] against packed
+     weights [w_hi | w_lo | w_hi]); 0 = off. LN epilogue: out_split = 1 stores y as two bf16
+     planes per row, hi at column n and lo = bf16(y - hi) at column N + n.                    */
+  int cin_block;
+  int cin_src[4];
+  int out_split;
 } fs2_conv_desc;
 
 int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream);

@@ -346,3 +346,30 @@ print('ok')
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], cwd=repo, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_split_precision_variance_predictor_matches_f32():
+    """VariancePredictor in bf16x3 split precision (bf16 MFMA, channel-block map, two-plane LN
+    output) vs exact-f32 MFMA on the same bf16 input: |d| <= 2e-4 + 2e-4 |y| (the split keeps
+    ~16 mantissa bits of weights and hidden activations)."""
+    from fs2amd.runtime import variance_predictor
+    from fs2amd.model import FastSpeech2
+    from fs2amd.synth_weights import fill_module
+    from _common import configs
+
+    pc, mc, _ = configs()
+    m = FastSpeech2(pc, mc)
+    fill_module(m, seed=0)
+    m = m.to("cuda").eval()
+    P32 = m.set_precision("bf16", "fp32").packed("cuda")
+    P3 = m.set_precision("bf16", "bf16x3").packed("cuda")
+    g = torch.Generator().manual_seed(4)
+    B, L = 16, 57
+    x = torch.randn(B, L, 256, generator=g).to("cuda", torch.bfloat16)
+    lens = torch.randint(1, L + 1, (B,), generator=g).to("cuda")
+    for k in ("duration", "pitch", "energy"):
+        a = variance_predictor(P32.vp[k], x, lens)
+        b = variance_predictor(P3.vp[k], x, lens)
+        torch.cuda.synchronize()
+        err = (a - b).abs()
+        assert bool((err <= 2e-4 + 2e-4 * a.abs()).all()), (k, float(err.max()))

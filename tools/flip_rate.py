@@ -19,13 +19,13 @@ def main():
     args = to_device(synth_batch(64, 64, seed=1, teacher=False), dev)
     va = model.variance_adaptor
     res = {}
-    for prec, vp in (("fp32", "fp32"), ("bf16", "fp32"), ("bf16vp", "bf16")):
+    for prec, vp in (("fp32", "fp32"), ("bf16", "fp32"), ("bf16vp", "bf16"), ("bf16x3vp", "bf16x3")):
         model.set_precision(prec[:4], vp)
         with torch.no_grad():
             out = model(**args)
         torch.cuda.synchronize()
         res[prec] = out
-    for tag in ("bf16", "bf16vp"):
+    for tag in ("bf16", "bf16vp", "bf16x3vp"):
         report(res["fp32"], res[tag], va, tag)
 
 
