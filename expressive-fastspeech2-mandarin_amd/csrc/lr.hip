@@ -7,7 +7,7 @@
 //
 // Here: launch 1 (one workgroup per sequence) turns durations into frame counts
 // max(trunc(d), 0), wavefront-scans them into an inclusive prefix sum `cum` and writes
-// mel_len (the uncropped total). Launch 2 (B x ceil(T_out/64) workgroups) binary-searches
+// mel_len (the uncropped total). Launch 2 (B x ceil(T_out/32) workgroups) binary-searches
 // each output frame's source phoneme in `cum` (first i with cum[i] > t) and streams the
 // D-wide row with 16-byte vector loads/stores; frames at or past min(mel_len, T_out) are
 // zero. An optional f32 position-encoding row is added on the way out (Decoder input,
@@ -17,7 +17,8 @@
 namespace {
 
 constexpr int kScanThreads = 256;
-constexpr int kRowsPerBlock = 64;
+constexpr int kRowsPerBlock = 32;
+constexpr int kLdsCum = 2048;  // cum rows up to this many phonemes are searched in LDS
 
 __device__ __forceinline__ int64_t frames_of(const void *dur, int kind, float d_control, int64_t idx,
                                              float *d_rounded) {
@@ -76,16 +77,18 @@ __global__ __launch_bounds__(kScanThreads) void lr_durations_kernel(const void *
   }
 }
 
-// 64 output frames per workgroup; each thread keeps UNR independent 16-byte row pieces in
-// flight (all loads issued before the stores) so a workgroup streams 32 KiB (bf16, D = 256)
-// with one round trip of latency.
+// kRowsPerBlock output frames per workgroup. The utterance's `cum` row is staged in LDS with one
+// coalesced load (rows longer than kLdsCum search global memory), so each frame's binary search
+// (first i with cum[i] > t) costs LDS latency, not log2(L) dependent global round trips; then
+// each thread keeps UNR independent 16-byte row pieces in flight (all loads issued before the
+// stores).
 template <typename TX, typename TO, bool HAS_PE>
 __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x, const int32_t *__restrict__ cum,
                                                         const int64_t *__restrict__ mel_len, int L, int D, int T_out,
                                                         const float *__restrict__ pe, TO *__restrict__ out,
                                                         int32_t *__restrict__ index_map,
                                                         const int32_t *__restrict__ out_cu) {
-  constexpr int UNR = 8;
+  constexpr int UNR = 4;
   const int b = blockIdx.y;
   const int t0 = blockIdx.x * kRowsPerBlock;
   const int tid = threadIdx.x;
@@ -93,9 +96,15 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x
   const int t_end = out_cu != nullptr ? min(T_out, out_cu[b + 1] - out_cu[b]) : T_out;
   if (t0 >= t_end && index_map == nullptr) return;
   __shared__ int src[kRowsPerBlock];
+  __shared__ int32_t scum[kLdsCum];
   const int64_t ml = mel_len[b];
   const int lim = (int)(ml < (int64_t)T_out ? ml : (int64_t)T_out);
   const int32_t *c = cum + (int64_t)b * L;
+  const bool in_lds = L <= kLdsCum;
+  if (in_lds)
+    for (int i = tid; i < L; i += 256) scum[i] = c[i];
+  __syncthreads();
+  const int32_t *sc = in_lds ? scum : c;
   if (tid < kRowsPerBlock) {
     const int t = t0 + tid;
     int s = -1;
@@ -103,7 +112,7 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x
       int lo = 0, hi = L - 1;  // first i with cum[i] > t (exists because t < mel_len)
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (c[mid] > t) hi = mid; else lo = mid + 1;
+        if (sc[mid] > t) hi = mid; else lo = mid + 1;
       }
       s = lo;
     }
