@@ -297,7 +297,9 @@ def main():
                    "parallelism": f"dp{world} (independent shards, no collective)",
                    "hip_graph": bool(args.graph)},
         "rtf": round((elapsed / args.steps) / (tot_frames / world * HOP / SR), 7),
-        "roofline": {"bound": "mfma", "kernel": f"conv_gemm_kernel<{args.dtype}> (decoder FFN Conv1d k=9, 256->1024)",
+        "roofline": {"bound": "mfma", "kernel": f"decoder FFN Conv1d k=9, 256->1024 ({args.dtype}): "
+                               + ("conv_gemm_8p_kernel whole rounds + conv_gemm_kernel rows left"
+                                  if args.dtype == "bf16" else "conv_gemm_kernel"),
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": load_traffic(args.dtype),
                      "kernel_ms": round(kernel_s * 1e3, 4), "launches_timed": n_launch,

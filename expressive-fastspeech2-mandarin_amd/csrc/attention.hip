@@ -13,6 +13,7 @@
 //   P -> LDS (wave-private rows), read back as A fragments
 //   O += P V       V is staged TRANSPOSED in LDS (Vt[d][key]) so B fragments are 16-byte reads.
 // LDS rows are XOR-swizzled by row so every fragment read is bank-conflict free.
+#include <cstdlib>
 #include <type_traits>
 
 #include "fs2_common.h"
@@ -28,7 +29,6 @@ struct ATraits;
 template <>
 struct ATraits<FS2_BF16> {
   using T = bf16;
-  static constexpr int CEp = 8;  // elements per 16-byte chunk
 };
 template <>
 struct ATraits<FS2_F32> {
@@ -255,11 +255,25 @@ __device__ __forceinline__ int kv_off(int row, int chunk) {
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
-__global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restrict__ qkv, int64_t qs, uint32_t qkv_bytes,
-                                                           const int64_t *__restrict__ lens, int B, int T, int H,
-                                                           int nqt, float scale_log2, bf16 *__restrict__ out,
-                                                           int64_t os, const int32_t *__restrict__ cu) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * KT * 256];  // K0 V0 K1 V1
+template <int N>
+__device__ __forceinline__ void attn_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// NWV waves (16 queries each) per workgroup, an NST-deep K/V ring: the DMA of key tile kt+NST-1
+// is issued right after the barrier that retires tile kt-1, so each tile has NST-1 tiles of
+// compute to land; one counted vmcnt + one barrier per tile.
+template <int NWV, int NST>
+__global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__restrict__ qkv, int64_t qs,
+                                                                uint32_t qkv_bytes, const int64_t *__restrict__ lens,
+                                                                int B, int T, int H, int nqt, float scale_log2,
+                                                                bf16 *__restrict__ out, int64_t os,
+                                                                const int32_t *__restrict__ cu) {
+  constexpr int QTW = 16 * NWV;          // queries per workgroup
+  constexpr int PPW = 16 / NWV;          // K (and V) 1 KiB pieces per wave per tile
+  constexpr int LPS = 2 * PPW;           // LDS-DMA loads per wave per tile
+  constexpr int STG = 2 * KT * 256;      // K + V bytes of one tile
+  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
@@ -268,7 +282,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
   const int q8 = nwg >> 3, rem = nwg & 7, xcd = id & 7;
   const int t = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (id >> 3);
   const int qt = t % nqt, bh = t / nqt, h = bh % H, b = bh / H;
-  const int q0 = qt * QT;
+  const int q0 = qt * QTW;
   int len;
   uint32_t seq_base;
   if (cu != nullptr) {  // packed rows: only the sequence's own rows exist
@@ -281,6 +295,7 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
     seq_base = (uint32_t)b * (uint32_t)T;
   }
   if (q0 >= T) return;
+  const bool active = q0 + 16 * w < T;  // wave-uniform: this wave has queries (else DMA + barriers only)
 
   const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16 *>(qkv), (short)0, (int)qkv_bytes, 0x00020000);
   const uint32_t row_bytes = (uint32_t)qs * 2u;
@@ -295,14 +310,14 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
     qf[s] = *reinterpret_cast<bf16x8 *>(&v);
   }
 
-  // LDS-DMA of one 64-key tile: 16 pieces of 4 rows x 256 B for K, 16 for V; 8 per wave.
+  // LDS-DMA of one 64-key tile: 16 pieces of 4 rows x 256 B for K, 16 for V; PPW of each per wave.
   const int prow = lane >> 4, pch = lane & 15;
   auto dma = [&](int k0, int buf) {
-    char *Kb = smem + buf * 2 * KT * 256;
+    char *Kb = smem + buf * STG;
     char *Vb = Kb + KT * 256;
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int p = w + 4 * it;
+    for (int it = 0; it < PPW; ++it) {
+      const int p = w + NWV * it;
       const int r = 4 * p + prow;
       const int lc = pch ^ (((r & 3) << 2) | ((r >> 2) & 3));
       const int key = k0 + r;
@@ -323,9 +338,10 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
   float m_run = -INFINITY, l_run = 0.f;
 
   const int ntiles = (len + KT - 1) / KT;
-  if (ntiles > 0) dma(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // the Q loads are waited for with the first tile (they were issued first)
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st)
+    if (st < ntiles) dma(st * KT, st);
   // transposed-read lane roles: lane 4q+p of its 16-lane group addresses row q, columns 4p..4p+3.
   // kv_off's swizzle depends on (row & 3, (row >> 2) & 3), so rows +16 / +32 are +4 / +8 KiB:
   // only the 8 column-block offsets of row r0 are lane-specific (hoisted out of the key loop).
@@ -335,8 +351,21 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
   for (int nd = 0; nd < DK / 16; ++nd) voff[nd] = kv_off(4 * g + tq, nd * 2 + (tp >> 1)) + (tp & 1) * 8;
   for (int kt = 0; kt < ntiles; ++kt) {
     const int k0 = kt * KT;
-    if (kt + 1 < ntiles) dma(k0 + KT, (kt + 1) & 1);
-    const char *Kb = smem + (kt & 1) * 2 * KT * 256;
+    // tile kt landed (this wave's pieces); tiles issued after it may stay in flight
+    const int ahead = ntiles - 1 - kt;
+    if (NST >= 3 && ahead >= NST - 2)
+      attn_vm_wait<LPS * (NST - 2)>();
+    else if (NST >= 4 && ahead == 1)
+      attn_vm_wait<LPS>();
+    else
+      attn_vm_wait<0>();
+    // tile kt visible to all waves; the buffer of tile kt-1 is free. Raw barrier: __syncthreads()
+    // would drain vmcnt to 0 and with it the tiles still in flight.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST - 1 < ntiles) dma(k0 + (NST - 1) * KT, (kt + NST - 1) % NST);
+    if (!active) continue;
+    const char *Kb = smem + (kt % NST) * STG;
     const char *Vb = Kb + KT * 256;
 
     f32x4 sacc[4];
@@ -397,8 +426,6 @@ __global__ __launch_bounds__(256, 2) void attn_bf16_kernel(const bf16 *__restric
         oacc[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[s2], oacc[nd], 0, 0, 0);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
   // O^T[d = nd*16 + 4g + j][query li]
@@ -432,10 +459,38 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
   if (dtype == FS2_BF16) {
     const int64_t bytes = (int64_t)B * T * qkv_row_stride * 2;
     if (bytes >= (1LL << 31) || (out_row_stride & 3)) return FS2_EUNSUPPORTED;
-    const int nqt = (T + QT - 1) / QT;
-    hipLaunchKernelGGL(attn_bf16_kernel, dim3(nqt * H * B), dim3(256), 0, s, reinterpret_cast<const bf16 *>(qkv),
-                       qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt, scale_log2,
-                       reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
+    // FS2_ATTN_VARIANT (A/B switch): 0 = 4 waves / 2 stages, 1 = 8 waves / 3 stages, 2 = 8 waves /
+    // 2 stages, 3 = 4 waves / 3 stages. Measured at the cfg2 decoder shape (packed, ~390 frames):
+    // 34.5 / 35.0 / 29.9 / 49.9 us: occupancy (16 waves per CU with 2 workgroups) hides the
+    // MFMA -> softmax -> MFMA chain better than a deeper K/V ring at 8 waves per CU. Default: 2
+    // for sequences longer than 64 (8 waves share each K/V tile), 0 otherwise (encoder, L <= 64:
+    // a 128-query workgroup would idle half its waves).
+    static const int forced = [] {
+      const char *e = getenv("FS2_ATTN_VARIANT");
+      return e != nullptr ? atoi(e) : -1;
+    }();
+    const int variant = forced >= 0 ? forced : (T > 64 ? 2 : 0);
+    if (variant == 0) {
+      const int nqt = (T + 63) / 64;
+      hipLaunchKernelGGL((attn_bf16_kernel<4, 2>), dim3(nqt * H * B), dim3(256), 0, s,
+                         reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
+                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
+    } else if (variant == 2) {
+      const int nqt = (T + 127) / 128;
+      hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), dim3(nqt * H * B), dim3(512), 0, s,
+                         reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
+                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
+    } else if (variant == 3) {
+      const int nqt = (T + 63) / 64;
+      hipLaunchKernelGGL((attn_bf16_kernel<4, 3>), dim3(nqt * H * B), dim3(256), 0, s,
+                         reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
+                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
+    } else {  // 8 waves (128 queries) share each K/V tile, 3-deep ring
+      const int nqt = (T + 127) / 128;
+      hipLaunchKernelGGL((attn_bf16_kernel<8, 3>), dim3(nqt * H * B), dim3(512), 0, s,
+                         reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
+                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
+    }
   } else if (dtype == FS2_F32)
     hipLaunchKernelGGL(attn_kernel<FS2_F32>, grid, dim3(256), 0, s, reinterpret_cast<const float *>(qkv),
                        qkv_row_stride, key_lens, T, H, scale_log2, reinterpret_cast<float *>(out), out_row_stride,

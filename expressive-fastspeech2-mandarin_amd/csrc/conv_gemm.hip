@@ -169,13 +169,36 @@ struct ConvArgs {
   int cin_block;            // split-precision input: logical channel blocks of cin_block (0 = off)
   int cin_src[4];           // ... block i is source channel cin_src[i] of x
   int out_split;            // LN epilogue: bf16 hi plane at column n, lo plane at column N + n
+  // split-K tail (conv_gemm_kernel, LDS-DMA path): see conv_tile_sk. sk_slots = 0 disables it.
+  int sk_slots;             // workgroups resident at once (CUs x workgroups per CU)
+  int sk_max;               // most segments one tail tile may be split into
+  int *sk_cnt;              // [sk_slots] arrival counters (zero between launches; self-resetting)
+  float *sk_part;           // [sk_slots][BM*BN] f32 partial tiles
+  uint32_t sk_part_bytes;
+  int64_t sk_ws_bytes;      // host side only: workspace size
+  // Row split between the phased 256x256 kernel and the 128x128 kernel (split_rows): 0 = off,
+  // 1 = this launch runs the 256-row panels [0, P1), 2 = it runs the rows from P1 * 256 on.
+  int row_split;
+  int split_slots;          // workgroups the phased kernel runs at once (one per CU)
 };
+
+constexpr int64_t kSkCntBytes = 4096;  // counter block at the start of the split-K workspace
 
 // Source channel of logical input channel c (split-precision layouts map channel blocks).
 __device__ __forceinline__ int src_channel(const ConvArgs &a, int c) {
   if (a.cin_block == 0) return c;
   const int blk = c / a.cin_block;
   return a.cin_src[blk] + (c - blk * a.cin_block);
+}
+
+// The phased kernel takes the 256-row panels that fill whole rounds of its grid (P1 panels:
+// floor(tiles / S) * S of its tiles); the 128 x 128 kernel takes the rows left over, where its
+// smaller tiles and split-K tail cut the partial last round. Both launches compute P1 from the
+// same device-side row count, so the split needs no host sync (packed rows).
+__device__ __forceinline__ int split_panels(const ConvArgs &a, int M) {
+  const int ntn = (a.N + 255) / 256;
+  const int tiles = ((M + 255) / 256) * ntn;
+  return (tiles / a.split_slots) * a.split_slots / ntn;
 }
 
 // Active rows and the XCD-aware tile of this workgroup. The dispatcher deals workgroup ids
@@ -185,7 +208,9 @@ __device__ __forceinline__ int src_channel(const ConvArgs &a, int c) {
 template <int BM>
 __device__ __forceinline__ bool conv_tile(const ConvArgs &a, int &M, int &m0, int &n0, int BN) {
   M = a.rows_dev != nullptr ? *a.rows_dev : a.M;
-  const int nwg = a.rows_dev != nullptr ? ((M + BM - 1) / BM) * a.ntn : (int)gridDim.x;
+  const int nwg = a.row_split == 1         ? split_panels(a, M) * a.ntn
+                  : a.rows_dev != nullptr ? ((M + BM - 1) / BM) * a.ntn
+                                          : (int)gridDim.x;
   const int id = blockIdx.x;
   if (id >= nwg) return false;
   const int q = nwg >> 3, rem = nwg & 7, xcd = id & 7, li = id >> 3;
@@ -199,6 +224,65 @@ __device__ __forceinline__ bool conv_tile(const ConvArgs &a, int &M, int &m0, in
   const int mt = r / a.ngr, nt = grp * a.ngr + (r - (r / a.ngr) * a.ngr);
   m0 = mt * BM;
   n0 = nt * BN;
+  return true;
+}
+
+// Tile order of tile index `tile` among `nt` tiles (see conv_tile).
+__device__ __forceinline__ void tile_coords(const ConvArgs &a, int tile, int nt, int BM, int BN, int &m0, int &n0) {
+  const int mtc = nt / a.ntn;
+  const int per_group = mtc * a.ngr;
+  const int grp = tile / per_group, r = tile - grp * per_group;
+  const int mt = r / a.ngr, ntl = grp * a.ngr + (r - (r / a.ngr) * a.ngr);
+  m0 = mt * BM;
+  n0 = ntl * BN;
+}
+
+// XCD-contiguous remap of workgroup id `id` over `n` ids (n a multiple of 8 or not).
+__device__ __forceinline__ int xcd_remap(int id, int n) {
+  const int q = n >> 3, rem = n & 7, xcd = id & 7, li = id >> 3;
+  return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + li;
+}
+
+// Split-K tail. With S workgroups resident at once, T tiles run as floor(T/S) full rounds plus a
+// tail of T mod S tiles; when that tail is small the last round leaves most of the chip idle
+// (cfg2 decoder conv-k9: 1560 tiles of 128 x 128 on 512 slots = 3 rounds + 24 tiles). Here the
+// tail tiles are cut into s = min(S / tail, sk_max) K segments, so the last round is ~1/s of a
+// round: workgroup ids [0, R*S) run whole tiles (XCD remap as conv_tile), ids R*S + j run
+// segment j % s of tail tile j / s (the grid has S spare ids; the rest exit). Each segment
+// stores its f32 partial tile (sc1) and adds to the tile's counter; the workgroup whose add
+// comes last sums the partials in segment order (deterministic) and runs the epilogue.
+template <int BM>
+__device__ __forceinline__ bool conv_tile_sk(const ConvArgs &a, int BN, int &M, int &m0, int &n0, int &seg,
+                                             int &nseg, int &tl) {
+  M = a.rows_dev != nullptr ? *a.rows_dev : a.M;
+  const int r0 = a.row_split == 2 ? split_panels(a, M) * 256 : 0;  // rows before r0: phased launch
+  const int T = ((M - r0 + BM - 1) / BM) * a.ntn;
+  const int id = blockIdx.x;
+  seg = 0;
+  nseg = 1;
+  tl = -1;
+  int tile;
+  const int S = a.sk_slots;
+  const int R = S > 0 ? T / S : 0, tail = S > 0 ? T - R * S : 0;
+  const int s = tail > 0 ? min(S / tail, a.sk_max) : 1;
+  if (s >= 2) {
+    const int dp = R * S;
+    if (id < dp) {
+      tile = xcd_remap(id, dp);
+    } else {
+      const int j = id - dp;
+      if (j >= tail * s) return false;
+      tl = j / s;
+      seg = j - tl * s;
+      nseg = s;
+      tile = dp + tl;
+    }
+  } else {
+    if (id >= T) return false;
+    tile = xcd_remap(id, T);
+  }
+  tile_coords(a, tile, T, BM, BN, m0, n0);
+  m0 += r0;
   return true;
 }
 
@@ -397,7 +481,33 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
 
 // Tile (WGM x WGN waves, each wave WMI x 4 MFMA 16x16 blocks):  BM = 16*WMI*WGM, BN = 64*WGN.
 // KSMAX bounds the conv taps the LDS halo is sized for.
-template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, bool GL>
+// Wait until at most n of this wave's vector-memory loads are outstanding (n wave-uniform, < 16).
+__device__ __forceinline__ void vm_wait_n(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+}
+
+// NSB: depth of the B (weight) stage ring on the LDS-DMA path. NSB == 2: one k-step in flight,
+// vmcnt(0) per step. NSB > 2 (tall tiles, KS >= NSB): B of step k+NSB-1 is issued right after
+// the barrier that retires step k-1, the next channel block's A halo at tap 0 of the current one
+// (KS-1 steps ahead), and each step waits with a counted vmcnt for its own B only.
+template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, bool GL, int NSB = 2>
 __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv_gemm_kernel(ConvArgs a) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;  // waves / threads per workgroup (4 or 8)
   constexpr int WROWS = 16 * WMI;
@@ -410,25 +520,30 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
   constexpr int B_CH = BN * 8 / NT;
   constexpr int RPP = NT / 8;                           // staged rows per pass
   constexpr int A_BYTES = HMAX * kRowBytes, B_BYTES = BN * kRowBytes;
-  constexpr int STAGE = 2 * (A_BYTES + B_BYTES);
+  static_assert(NSB == 2 || GL, "deep B ring needs the LDS-DMA path");
+  constexpr int STAGE = 2 * A_BYTES + NSB * B_BYTES;
   constexpr int EPI_LD = BN + 4;
   constexpr int SMEM = (STAGE > BM * EPI_LD * 4) ? STAGE : BM * EPI_LD * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  // + 16 B: the split-K "last arriver" word lives in the same array (a second __shared__ object
+  // next to an LDS-DMA staging array can make hipcc drain vmcnt before every k-step's reads)
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + 16];
   char *const Abuf = smem;                  // 2 x A_BYTES
-  char *const Bbuf = smem + 2 * A_BYTES;    // 2 x B_BYTES
+  char *const Bbuf = smem + 2 * A_BYTES;    // NSB x B_BYTES
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform for the compiler
   const int wr = wid / WGN, wc = wid % WGN;
 
-  int M, m0, n0;
-  if (!conv_tile<BM>(a, M, m0, n0, BN)) return;
+  int M, m0, n0, seg, nseg, tl;
+  if (!conv_tile_sk<BM>(a, BN, M, m0, n0, seg, nseg, tl)) return;
 
   const int KS = a.KS, pad = a.pad;
   const int H = BM + KS - 1;
   const int nCk = a.Cin_pad / KE;
   const int nK = KS * nCk;
   const int T = a.T;
+  // k-steps [k0, k1) of this workgroup (the whole K unless it is a split-K tail segment)
+  const int k0 = seg * nK / nseg, k1 = (seg + 1) * nK / nseg;
 
 
   const int srow = tid >> 3, schunk = tid & 7;
@@ -628,15 +743,76 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
         glds(wr_, Bs + p * 1024, n < a.N ? (uint32_t)n * wrow + off : kOOB);
       }
     };
-    int cb = 0, tap = 0;
-    dma_a(0, 0);
-    dma_b(0, 0, 0);
+    if constexpr (NSB > 2) {
+      // this wave's A-halo DMA count (pieces p = wid + NW*it < AP)
+      const int a_w = (AP - wid + NW - 1) / NW;
+      constexpr int BPW = BP / NW;
+      int cb = k0 / KS, tap = k0 - cb * KS;
+      const int cb_last = (k1 - 1) / KS;
+      dma_a(cb, cb & 1);
+      if (cb + 1 <= cb_last) dma_a(cb + 1, (cb + 1) & 1);  // both halo buffers are free at the start
+      {
+        int c = cb, t = tap;
+#pragma unroll
+        for (int j = 0; j < NSB - 1; ++j) {
+          if (k0 + j < k1) dma_b(c, t, (k0 + j) % NSB);
+          if (++t == KS) {
+            t = 0;
+            ++c;
+          }
+        }
+      }
+      // (cbi, tapi) = coordinates of the next B step to issue (k0 + NSB - 1)
+      int cbi = (k0 + NSB - 1) / KS, tapi = (k0 + NSB - 1) - ((k0 + NSB - 1) / KS) * KS;
+      for (int ks = k0; ks < k1; ++ks) {
+        // loads issued after B(ks): B(ks+1 .. ks+NSB-2) and any A halo issued since
+        int after = 0;
+#pragma unroll
+        for (int j = 1; j <= NSB - 2; ++j) after += (ks + j < k1) ? BPW : 0;
+#pragma unroll
+        for (int j = 1; j <= NSB - 2; ++j) {  // steps s = ks - NSB + 1 + j issued an A halo iff tap(s) == 0
+          const int st = ks - NSB + 1 + j;
+          if (st > k0 && st < ks) {
+            const int tp = st - (st / KS) * KS;
+            if (tp == 0 && st / KS + 1 <= cb_last) after += a_w;
+          }
+        }
+        {  // the step that issued B(ks) itself issued its A after it
+          const int st = ks - NSB + 1;
+          if (st > k0) {
+            const int tp = st - (st / KS) * KS;
+            if (tp == 0 && st / KS + 1 <= cb_last) after += a_w;
+          }
+        }
+        vm_wait_n(after);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // raw: __syncthreads() would drain vmcnt (the whole ring) to 0
+        if (ks + NSB - 1 < k1) {
+          dma_b(cbi, tapi, (ks + NSB - 1) % NSB);
+          if (++tapi == KS) {
+            tapi = 0;
+            ++cbi;
+          }
+        }
+        if (tap == 0 && ks > k0 && cb + 1 <= cb_last) dma_a(cb + 1, (cb + 1) & 1);
+        compute(cb & 1, tap, Bbuf + (ks % NSB) * B_BYTES);
+        if (++tap == KS) {
+          tap = 0;
+          ++cb;
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    } else {
+    int cb = k0 / KS, tap = k0 - (k0 / KS) * KS;
+    dma_a(cb, cb & 1);
+    dma_b(cb, tap, k0 & 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int ks = 0; ks < nK; ++ks) {
+    for (int ks = k0; ks < k1; ++ks) {
       const bool last_tap = tap == KS - 1;
       const int ncb = last_tap ? cb + 1 : cb, ntap = last_tap ? 0 : tap + 1;
-      if (ks + 1 < nK) {
+      if (ks + 1 < k1) {
         dma_b(ncb, ntap, (ks + 1) & 1);
         if (last_tap) dma_a(ncb, ncb & 1);
       }
@@ -645,6 +821,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
       __syncthreads();
       cb = ncb;
       tap = ntap;
+    }
     }
   } else {
   // (cb, tap) of step k + 2 tracked incrementally
@@ -683,6 +860,59 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
       if (ks + 1 < nK) step(ks + 1, sb1, sb0);
     }
 
+  }
+
+  if constexpr (GL) {
+    if (nseg > 1) {  // split-K tail segment: hand the partial tile over (conv_tile_sk)
+      static_assert(BM * BN * 4 == NT * WMI * 4 * 16, "partial tile layout");
+      const rsrc_t pr = make_rsrc(a.sk_part, a.sk_part_bytes);
+      const uint32_t tile_bytes = (uint32_t)(BM * BN * 4);
+      auto pofs = [&](int sg, int mi, int ni) {
+        return (uint32_t)(tl * nseg + sg) * tile_bytes + (uint32_t)(((mi * 4 + ni) * NT + tid) * 16);
+      };
+#pragma unroll
+      for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)  // sc1 stores (agent-coherent hand-off, no L2 writeback needed)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc[mi][ni]), pr, pofs(seg, mi, ni),
+              0, 16);
+      int &sk_last = *reinterpret_cast<int *>(smem + SMEM);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(a.sk_cnt + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == nseg - 1;
+        if (last) {
+          __hip_atomic_store(a.sk_cnt + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset for the next launch
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        sk_last = last;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (!sk_last) return;
+      // the last arriver: sum the partials in segment order (its own from registers), sc1 loads
+      f32x4 tot[WMI][4];
+#pragma unroll
+      for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) tot[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int sg = 0; sg < nseg; ++sg) {
+#pragma unroll
+        for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            f32x4 p = acc[mi][ni];
+            if (sg != seg) p = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, pofs(sg, mi, ni), 0, 16));
+            tot[mi][ni] += p;
+          }
+      }
+#pragma unroll
+      for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = tot[mi][ni];
+    }
   }
 
   // ---- epilogue: accumulator tile -> LDS (f32, row-major, padded rows) -------------------------
@@ -937,8 +1167,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
 void launch_8p(ConvArgs a, hipStream_t s) {
   a.ntn = (a.N + 255) / 256;
   a.ngr = a.ntn;
-  const int nwg = ((a.M + 255) / 256) * a.ntn;
-  hipLaunchKernelGGL(conv_gemm_8p_kernel, dim3(nwg), dim3(512), 0, s, a);
+  int nwg = ((a.M + 255) / 256) * a.ntn;
+  if (a.row_split == 1) nwg = nwg / a.split_slots * a.split_slots;  // whole rounds (device M <= a.M)
+  if (nwg > 0) hipLaunchKernelGGL(conv_gemm_8p_kernel, dim3(nwg), dim3(512), 0, s, a);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1325,6 +1556,19 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_rb_kernel(ConvArgs a) 
   epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
 }
 
+// Compute units of the current device (cached per device id).
+int num_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 template <int CT, int WGM, int WMI, int NA, int PB>
 void launch_rb(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM;
@@ -1337,13 +1581,14 @@ void launch_rb(ConvArgs a, hipStream_t s) {
 template <int CT, int WGM, int WMI, int NS>
 void launch_ring(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM;
-  a.ntn = 1;
-  a.ngr = 1;
-  const int nwg = (a.M + BM - 1) / BM;
+  a.ntn = (a.N + 255) / 256;
+  a.ngr = a.ntn;
+  if (a.w_bytes > (2u << 20) && a.ntn > 2 && a.ntn % 2 == 0) a.ngr = 2;  // see launch(): L2-sized N groups
+  const int nwg = (a.M + BM - 1) / BM * a.ntn;
   hipLaunchKernelGGL((conv_gemm_ring_kernel<CT, WGM, WMI, NS>), dim3(nwg), dim3(256 * WGM), 0, s, a);
 }
 
-template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn>
+template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, int NSB = 2>
 void launch(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM, BN = 64 * WGN;
   constexpr bool GL = std::is_same<TIn, typename CTraits<CT>::T>::value;  // LDS-DMA needs no conversion
@@ -1359,8 +1604,32 @@ void launch(ConvArgs a, hipStream_t s) {
         a.ngr = g;
         break;
       }
-  const int nwg = ((a.M + BM - 1) / BM) * a.ntn;
-  hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, WMI, KSMAX, TIn, GL>), dim3(nwg), dim3(64 * WGM * WGN), 0, s, a);
+  int nwg = ((a.M + BM - 1) / BM) * a.ntn;
+  if (a.row_split == 2) {  // rows left after the phased panels: < (S / ntn256 + 1) panels of 256
+    const int left = (a.split_slots / ((a.N + 255) / 256) + 2) * 256;
+    const int bound = ((left + BM - 1) / BM) * a.ntn;
+    if (bound < nwg) nwg = bound;
+  }
+  a.sk_slots = 0;
+  if constexpr (GL) {
+    static const bool splitk = [] {
+      const char *e = getenv("FS2_CONV_SPLITK");
+      return e == nullptr || e[0] != '0';
+    }();
+    const int slots = num_cus() * ((WGM * WGN == 4 && NSB == 2) ? 2 : 1);
+    const int nK = a.KS * (a.Cin_pad / CTraits<CT>::KE);
+    const int64_t need = kSkCntBytes + (int64_t)slots * BM * BN * 4;
+    if (splitk && a.sk_cnt != nullptr && a.sk_ws_bytes >= need && nK >= 16 && slots > 0 && slots * 4 <= kSkCntBytes) {
+      a.sk_slots = slots;
+      // segments of >= 8 k-steps, at most 4 per tile: the last arriver reads the other
+      // segments' partials back (64 KiB each), which costs more than it saves past ~4
+      a.sk_max = nK / 8 < 4 ? nK / 8 : 4;
+      a.sk_part_bytes = (uint32_t)(need - kSkCntBytes);
+      nwg += slots;  // spare ids for the tail segments (exit when unused)
+    }
+  }
+  hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, WMI, KSMAX, TIn, GL, GL ? NSB : 2>), dim3(nwg), dim3(64 * WGM * WGN),
+                     0, s, a);
 }
 
 // Row-tile choice: the largest tile that still gives >= 2 workgroups per CU (256 CUs), so the
@@ -1370,18 +1639,48 @@ constexpr int kTargetWGs = 512;
 template <int CT, typename TIn>
 void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
   if constexpr (CT == FS2_BF16 && std::is_same<TIn, bf16>::value) {
-    // The phased 256x256 kernel is correct (parity-tested) but in round 1 measured slower than
-    // the 4-wave 128x128 kernel on the decoder shapes (barrier-bound: MFMA busy 34 %); opt-in.
+    // Large bf16 convs (decoder FFN conv-k9, PostNet k=5): the phased 256x256 kernel runs the
+    // whole rounds of its tiles (44 % of dense peak on full rounds vs 36 % for 128x128), the
+    // 128x128 kernel (split-K tail) the rows left over (split_panels). FS2_CONV_PHASED=0: off.
     static const bool phased = [] {
       const char *e = getenv("FS2_CONV_PHASED");
+      return e == nullptr || e[0] != '0';
+    }();
+    const int64_t tiles256 = (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256);
+    const int S = num_cus();
+    static const bool tall = [] {
+      const char *e = getenv("FS2_CONV_TALL");
       return e != nullptr && e[0] == '1';
     }();
-    if (phased && !ln && a.KS >= 4 && a.N >= 256 && (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256) >= 192) {
-      launch_8p(a, s);
+    if (tall && !ln && a.KS >= 4 && a.N % 128 == 0 && (int64_t)((a.M + 255) / 256) * (a.N / 128) >= S) {
+      launch<CT, 4, 2, 4, 9, TIn, 4>(a, s);  // 256 x 128, 8 waves, A halo + 4-deep B ring, 1 WG / CU
+      return;
+    }
+    if (phased && !ln && a.KS >= 4 && a.N >= 256 && tiles256 >= 192 && S > 0) {
+      if (tiles256 <= S) {  // at most one round: the phased kernel alone
+        launch_8p(a, s);
+        return;
+      }
+      ConvArgs a1 = a, a2 = a;  // whole rounds of 256 x 256 tiles, then the rows left over
+      a1.row_split = 1;
+      a1.split_slots = S;
+      a2.row_split = 2;
+      a2.split_slots = S;
+      launch_8p(a1, s);
+      launch<CT, 2, 2, 4, 9, TIn>(a2, s);
       return;
     }
   }
   if constexpr (std::is_same<TIn, typename CTraits<CT>::T>::value) {
+    // experiment: deep-ring kernel for the large plain-epilogue convs (FS2_CONV_RING9=1)
+    static const bool ring9 = [] {
+      const char *e = getenv("FS2_CONV_RING9");
+      return e != nullptr && e[0] == '1';
+    }();
+    if (ring9 && !ln && a.KS > 1 && a.N % 256 == 0 && a.M >= 8192 && a.cin_block == 0) {
+      launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages
+      return;
+    }
     static const bool ring = [] {
       const char *e = getenv("FS2_CONV_RING");
       return e == nullptr || e[0] != '0';
@@ -1515,6 +1814,19 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.cin_block = d->cin_block;
   for (int i = 0; i < 4; ++i) a.cin_src[i] = d->cin_src[i];
   a.out_split = d->out_split;
+  a.sk_slots = 0;
+  a.sk_max = 1;
+  a.sk_cnt = nullptr;
+  a.sk_part = nullptr;
+  a.sk_part_bytes = 0;
+  a.sk_ws_bytes = 0;
+  a.row_split = 0;
+  a.split_slots = 1;
+  if (d->splitk_ws != nullptr && d->splitk_ws_bytes > kSkCntBytes && d->splitk_ws_bytes < (1LL << 31) + kSkCntBytes) {
+    a.sk_cnt = reinterpret_cast<int *>(d->splitk_ws);
+    a.sk_part = reinterpret_cast<float *>(reinterpret_cast<char *>(d->splitk_ws) + kSkCntBytes);
+    a.sk_ws_bytes = d->splitk_ws_bytes;
+  }
   {
     const int xes = d->x_dtype == FS2_BF16 ? 2 : (d->x_dtype == FS2_FP8 ? 1 : 4);
     const int wes = d->compute == FS2_BF16 ? 2 : (d->compute == FS2_FP8 ? 1 : 4);

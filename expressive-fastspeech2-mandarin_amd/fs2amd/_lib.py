@@ -42,6 +42,7 @@ class ConvDesc(ctypes.Structure):
         ("rows_dev", _p), ("row_pos", _p), ("a_rowmap", _p),
         ("col_scale", _p), ("out_scale", _f), ("out2", _p), ("out2_scale", _f),
         ("cin_block", _i), ("cin_src", _i * 4), ("out_split", _i),
+        ("splitk_ws", _p), ("splitk_ws_bytes", _i64),
     ]
 
 

@@ -6,6 +6,7 @@ memory and the stream; every arithmetic op below runs in a hand-written HIP kern
 is no CPU path: CPU tensors raise.
 """
 import ctypes
+import os
 
 import torch
 
@@ -147,6 +148,56 @@ def pack_conv_weight_fp8(w):
     return out.contiguous(), s.contiguous()
 
 
+SPLITK_WS_BYTES = 4096 + (32 << 20)  # fs2_conv_desc.splitk_ws: counters + 512 partial 128x128 f32 tiles
+_splitk_ws = {}
+_splitk_slot = [0]
+_splitk_on = [os.environ.get("FS2_CONV_SPLITK", "1") != "0"]
+
+
+class splitk_enabled:
+    """Turn the split-K tail on/off for the launches inside (it changes the f32 summation order,
+    so paths that must agree bit-exactly with an unsplit launch run with it off)."""
+
+    def __init__(self, flag):
+        self.flag = bool(flag)
+
+    def __enter__(self):
+        self.prev = _splitk_on[0]
+        _splitk_on[0] = self.flag
+
+    def __exit__(self, *exc):
+        _splitk_on[0] = self.prev
+
+
+class splitk_slot:
+    """Launches inside use split-K workspace `i` (one per concurrently running stream)."""
+
+    def __init__(self, i):
+        self.i = i
+
+    def __enter__(self):
+        self.prev = _splitk_slot[0]
+        _splitk_slot[0] = self.i
+
+    def __exit__(self, *exc):
+        _splitk_slot[0] = self.prev
+
+
+def splitk_workspace(device):
+    """The split-K tail workspace of (device, current slot): allocated zeroed on first use outside
+    graph capture (its counters must start at zero); None while capturing before it exists."""
+    if device.type != "cuda" or not _splitk_on[0]:
+        return None
+    key = (device.index, _splitk_slot[0])
+    ws = _splitk_ws.get(key)
+    if ws is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        ws = torch.zeros(SPLITK_WS_BYTES, dtype=torch.uint8, device=device)
+        _splitk_ws[key] = ws
+    return ws
+
+
 def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None, out=None, residual=None,
            ln=None, lens=None, addvec1=None, addvec2=None, dot=None, n=None, layout=None, src_layout=None,
            col_scale=None, out_scale=1.0, out2=None, out2_scale=1.0, cin_block=0, cin_src=(), out_split=False):
@@ -194,6 +245,9 @@ def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None
         d.rows_dev, d.row_pos = layout.rows_dev, layout.row_pos.data_ptr()
     if src_layout is not None:
         d.a_rowmap = src_layout.rowmap.data_ptr()
+    ws = splitk_workspace(x.device)
+    if ws is not None:
+        d.splitk_ws, d.splitk_ws_bytes = ws.data_ptr(), ws.numel()
     oshape = (B * T,) if layout is not None else (B, T)
     if epilogue == L.EPI_RELU_LN_DOT:
         dw, db = dot

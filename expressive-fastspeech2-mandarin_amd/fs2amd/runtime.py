@@ -193,6 +193,21 @@ def _streams_for(B):
     return max(1, min(n, B // 8))
 
 
+class _StreamSlot:
+    """Group i: its side stream and its own split-K workspace (ops.splitk_slot)."""
+
+    def __init__(self, stream, i):
+        self.s, self.k = torch.cuda.stream(stream), ops.splitk_slot(i)
+
+    def __enter__(self):
+        self.s.__enter__()
+        self.k.__enter__()
+
+    def __exit__(self, *exc):
+        self.k.__exit__(*exc)
+        return self.s.__exit__(*exc)
+
+
 class _ForkJoin:
     """n utterance groups on n side streams forked from / joined to the caller's stream (graph
     capture turns them into parallel branches). n == 1 runs inline and touches no stream API."""
@@ -211,7 +226,7 @@ class _ForkJoin:
             self._cache[key] = [torch.cuda.Stream(device=dev) for _ in range(n)]
         self.streams = self._cache[key]
         self.main = torch.cuda.current_stream(dev)
-        self.ctx = lambda i: torch.cuda.stream(self.streams[i])
+        self.ctx = lambda i: _StreamSlot(self.streams[i], i)
 
     def fork(self):
         if self.n > 1:

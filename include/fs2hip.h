@@ -115,6 +115,14 @@ typedef struct fs2_conv_desc {
   int cin_block;
   int cin_src[4];
   int out_split;
+  /* split-K tail workspace (optional, NULL = off): when a launch's tiles leave a small last
+     round, its tiles are split along K across the idle workgroups and summed in fixed segment
+     order by the last arriving segment. The first 4 KiB are arrival counters and MUST be zero
+     before first use (they reset themselves); the rest holds f32 partial tiles. 32 MiB + 4 KiB
+     covers 256 CUs. One workspace per stream: concurrent launches must not share it. Results
+     are deterministic but not bitwise equal to the unsplit summation order.                  */
+  void *splitk_ws;
+  int64_t splitk_ws_bytes;
 } fs2_conv_desc;
 
 int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream);

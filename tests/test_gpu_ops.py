@@ -373,3 +373,38 @@ def test_split_precision_variance_predictor_matches_f32():
         torch.cuda.synchronize()
         err = (a - b).abs()
         assert bool((err <= 2e-4 + 2e-4 * a.abs()).all()), (k, float(err.max()))
+
+
+@pytest.mark.parametrize("compute", [0, 1])
+@pytest.mark.parametrize("B,T,packed", [(1, 8576, False),   # 67 x 8 tiles: one full round + a 24-tile tail (256 CUs)
+                                        (3, 50, False),     # all-tail launch (16 tiles)
+                                        (1, 10400, False),  # 3 segments per tail tile: they start mid channel block
+                                        (64, 430, True)])   # cfg2 decoder shape on packed rows
+def test_conv_splitk_tail(ops, compute, B, T, packed):
+    """Split-K tail (ops.splitk_enabled): tail tiles cut along K across idle workgroups, summed
+    in segment order by the last arriver. Against the unsplit launch (same kernel, one K pass):
+    f32 2e-5 / bf16 2.5e-2 of the output scale; and bit-identical across repeated launches
+    (fixed summation order, counters reset themselves)."""
+    L = _L()
+    g = torch.Generator().manual_seed(T)
+    Cin, N, KS = 256, 1024, 9
+    dt = torch.float32 if compute == 0 else torch.bfloat16
+    x = torch.randn(B, T, Cin, generator=g).to(DEV, dt)
+    w = ops.pack_conv_weight((torch.randn(N, Cin, KS, generator=g) / np.sqrt(Cin * KS)).to(DEV), compute)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    kw = dict(cin=Cin, ks=KS, pad=4, compute=compute, epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_F32)
+    if packed:
+        lens = torch.randint(200, T + 1, (B,), generator=g).to(DEV)
+        kw["layout"] = ops.SeqLayout(lens, T)
+        x = x.reshape(B * T, Cin)
+    with ops.splitk_enabled(False):
+        ref = ops.conv1d(x, w, b, **kw)
+    outs = [ops.conv1d(x, w, b, **kw) for _ in range(3)]
+    torch.cuda.synchronize()
+    rows = int(kw["layout"].cu[-1]) if packed else B * T
+    r = ref.reshape(-1, N)[:rows].float()
+    for o in outs:
+        o = o.reshape(-1, N)[:rows].float()
+        err = float((o - r).abs().max() / (r.abs().max() + 1e-6))
+        assert err < _tol(compute), err
+        assert torch.equal(o, outs[0].reshape(-1, N)[:rows].float())

@@ -4,7 +4,7 @@ V=$1; TAG=$2
 mkdir -p gpurun_out/$TAG
 for i in 1 2; do
   for X in 1 0; do
-    env $V=$X timeout -k 10 200 python tools/m_sweep.py --ms 24883,27520 --reps 30 > gpurun_out/$TAG/sweep_${X}_$i.txt 2>&1 || exit $?
+    env $V=$X timeout -k 10 200 python tools/m_sweep.py --ms ${MS:-24883,27520} --reps 30 > gpurun_out/$TAG/sweep_${X}_$i.txt 2>&1 || exit $?
     echo "$V=$X run$i $(grep M= gpurun_out/$TAG/sweep_${X}_$i.txt | tr '\n' ' ')" >> gpurun_out/$TAG/summary.txt
   done
 done
