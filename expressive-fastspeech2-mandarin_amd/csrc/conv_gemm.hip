@@ -481,6 +481,62 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
 
 // Tile (WGM x WGN waves, each wave WMI x 4 MFMA 16x16 blocks):  BM = 16*WMI*WGM, BN = 64*WGN.
 // KSMAX bounds the conv taps the LDS halo is sized for.
+// Split-K hand-off (conv_tile_sk). Every segment stores its f32 partial tile with sc1
+// (write-through) 16-byte stores, drains, and after a workgroup barrier one lane adds to the
+// tile's counter; the workgroup whose add returns nseg-1 is the last arriver: it resets the
+// counter, acquires, and sums the partials in segment order (deterministic; its own segment from
+// registers) with sc1 loads. Returns false for the other segments (they are done). `flag` is a
+// word inside the kernel's one LDS array.
+template <int WMI, int NT>
+__device__ __forceinline__ bool splitk_fixup(const ConvArgs &a, f32x4 (&acc)[WMI][4], int tl, int seg, int nseg,
+                                             int tid, int *flag) {
+  const rsrc_t pr = make_rsrc(a.sk_part, a.sk_part_bytes);
+  constexpr uint32_t tile_bytes = (uint32_t)(NT * WMI * 4 * 16);
+  auto pofs = [&](int sg, int mi, int ni) {
+    return (uint32_t)(tl * nseg + sg) * tile_bytes + (uint32_t)(((mi * 4 + ni) * NT + tid) * 16);
+  };
+#pragma unroll
+  for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc[mi][ni]),
+                                             pr, pofs(seg, mi, ni), 0, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(a.sk_cnt + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == nseg - 1;
+    if (last) {
+      __hip_atomic_store(a.sk_cnt + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset for the next launch
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    *flag = last;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!*flag) return false;
+  f32x4 tot[WMI][4];
+#pragma unroll
+  for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) tot[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int sg = 0; sg < nseg; ++sg) {
+#pragma unroll
+    for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        f32x4 p = acc[mi][ni];
+        if (sg != seg) p = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, pofs(sg, mi, ni), 0, 16));
+        tot[mi][ni] += p;
+      }
+  }
+#pragma unroll
+  for (int mi = 0; mi < WMI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = tot[mi][ni];
+  return true;
+}
+
 // Wait until at most n of this wave's vector-memory loads are outstanding (n wave-uniform, < 16).
 __device__ __forceinline__ void vm_wait_n(int n) {
   switch (n) {
@@ -865,53 +921,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
   if constexpr (GL) {
     if (nseg > 1) {  // split-K tail segment: hand the partial tile over (conv_tile_sk)
       static_assert(BM * BN * 4 == NT * WMI * 4 * 16, "partial tile layout");
-      const rsrc_t pr = make_rsrc(a.sk_part, a.sk_part_bytes);
-      const uint32_t tile_bytes = (uint32_t)(BM * BN * 4);
-      auto pofs = [&](int sg, int mi, int ni) {
-        return (uint32_t)(tl * nseg + sg) * tile_bytes + (uint32_t)(((mi * 4 + ni) * NT + tid) * 16);
-      };
-#pragma unroll
-      for (int mi = 0; mi < WMI; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)  // sc1 stores (agent-coherent hand-off, no L2 writeback needed)
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc[mi][ni]), pr, pofs(seg, mi, ni),
-              0, 16);
-      int &sk_last = *reinterpret_cast<int *>(smem + SMEM);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(a.sk_cnt + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == nseg - 1;
-        if (last) {
-          __hip_atomic_store(a.sk_cnt + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset for the next launch
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-        sk_last = last;
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (!sk_last) return;
-      // the last arriver: sum the partials in segment order (its own from registers), sc1 loads
-      f32x4 tot[WMI][4];
-#pragma unroll
-      for (int mi = 0; mi < WMI; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) tot[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int sg = 0; sg < nseg; ++sg) {
-#pragma unroll
-        for (int mi = 0; mi < WMI; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            f32x4 p = acc[mi][ni];
-            if (sg != seg) p = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, pofs(sg, mi, ni), 0, 16));
-            tot[mi][ni] += p;
-          }
-      }
-#pragma unroll
-      for (int mi = 0; mi < WMI; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = tot[mi][ni];
+      if (!splitk_fixup<WMI, NT>(a, acc, tl, seg, nseg, tid, reinterpret_cast<int *>(smem + SMEM))) return;
     }
   }
 
@@ -1203,17 +1213,18 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
   constexpr int STAGE = (AP + BP) * 1024;
   constexpr int EPI_LD = BN + 4;
   constexpr int SMEM = (NS * STAGE > BM * EPI_LD * 4) ? NS * STAGE : BM * EPI_LD * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + 16];  // + the split-K flag word
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / WGN, wc = wid % WGN;
-  int M, m0, n0;
-  if (!conv_tile<BM>(a, M, m0, n0, BN)) return;
+  int M, m0, n0, seg, nseg, tl;
+  if (!conv_tile_sk<BM>(a, BN, M, m0, n0, seg, nseg, tl)) return;
 
   const int KS = a.KS, pad = a.pad, T = a.T;
   const int nCk = a.Cin_pad / KE;
   const int nK = KS * nCk;
+  const int k0 = seg * nK / nseg, k1 = (seg + 1) * nK / nseg;  // split-K segment (whole K unless split)
   const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
   const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * (uint32_t)sizeof(TW);
@@ -1324,7 +1335,7 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
   };
 
   // k-step k = cb * KS + tap (tap fastest); (itap, icb) = next stage to issue
-  int itap = 0, icb = 0;
+  int itap = k0 % KS, icb = k0 / KS;
   auto advance = [&]() {
     if (++itap == KS) {
       itap = 0;
@@ -1333,14 +1344,14 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
   };
 #pragma unroll
   for (int st = 0; st < NS - 1; ++st) {
-    if (st < nK) {
+    if (k0 + st < k1) {
       issue(itap, icb, st);
       advance();
     }
   }
-  for (int k = 0; k < ((a.dbg & 1) ? 0 : nK); ++k) {
+  for (int k = k0; k < ((a.dbg & 1) ? k0 : k1); ++k) {
     // stage k landed (this wave's pieces): later issued stages may stay in flight
-    const int ahead = nK - 1 - k;
+    const int ahead = k1 - 1 - k;
     if (ahead >= NS - 2)
       vm_wait<LPS * (NS - 2)>();
     else if (NS > 3 && ahead == 1)
@@ -1349,13 +1360,17 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
       vm_wait<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (k + NS - 1 < nK) {
-      issue(itap, icb, (k + NS - 1) % NS);
+    if (k + NS - 1 < k1) {
+      issue(itap, icb, (k - k0 + NS - 1) % NS);
       advance();
     }
-    compute(smem + (k % NS) * STAGE);
+    compute(smem + ((k - k0) % NS) * STAGE);
   }
   __syncthreads();
+  if (nseg > 1) {
+    static_assert(BM * BN * 4 == 256 * WGM * WMI * 4 * 16, "partial tile layout");
+    if (!splitk_fixup<WMI, 256 * WGM>(a, acc, tl, seg, nseg, tid, reinterpret_cast<int *>(smem + SMEM))) return;
+  }
 
   float *E = reinterpret_cast<float *>(smem);
 #pragma unroll
@@ -1556,6 +1571,27 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_rb_kernel(ConvArgs a) 
   epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
 }
 
+// FS2_CONV_SPLITK=0 turns the split-K tail off (A/B switch; the Python layer has its own).
+bool splitk_env() {
+  static const bool on = [] {
+    const char *e = getenv("FS2_CONV_SPLITK");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
+// FS2_CONV_SKPREF=1 (opt-in): small-M launches (encoder / variance predictors, M ~ 4k) use big
+// tiles + split-K instead of small tiles. Measured slower (cfg2 probes, us: VP 56 -> 68, encoder
+// conv-k9 31 -> 39, encoder conv-k1+LN 17 -> 32; bench -3.8 %): the partial-tile hand-off costs
+// more than the weight streaming it saves.
+bool skpref_env() {
+  static const bool on = [] {
+    const char *e = getenv("FS2_CONV_SKPREF");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 // Compute units of the current device (cached per device id).
 int num_cus() {
   static int cache[64] = {0};
@@ -1584,7 +1620,20 @@ void launch_ring(ConvArgs a, hipStream_t s) {
   a.ntn = (a.N + 255) / 256;
   a.ngr = a.ntn;
   if (a.w_bytes > (2u << 20) && a.ntn > 2 && a.ntn % 2 == 0) a.ngr = 2;  // see launch(): L2-sized N groups
-  const int nwg = (a.M + BM - 1) / BM * a.ntn;
+  int nwg = (a.M + BM - 1) / BM * a.ntn;
+  a.sk_slots = 0;
+  {  // split-K (conv_tile_sk): one workgroup per CU; segments of >= 4 k-steps, at most 4 per tile
+    const int slots = num_cus();
+    const int nK = a.KS * (a.Cin_pad / CTraits<CT>::KE);
+    const int64_t need = kSkCntBytes + (int64_t)slots * BM * 256 * 4;
+    if (splitk_env() && a.sk_cnt != nullptr && a.sk_ws_bytes >= need && nK >= 8 && slots > 0 &&
+        slots * 4 <= kSkCntBytes) {
+      a.sk_slots = slots;
+      a.sk_max = nK / 4 < 4 ? nK / 4 : 4;
+      a.sk_part_bytes = (uint32_t)(need - kSkCntBytes);
+      nwg += slots;
+    }
+  }
   hipLaunchKernelGGL((conv_gemm_ring_kernel<CT, WGM, WMI, NS>), dim3(nwg), dim3(256 * WGM), 0, s, a);
 }
 
@@ -1612,10 +1661,7 @@ void launch(ConvArgs a, hipStream_t s) {
   }
   a.sk_slots = 0;
   if constexpr (GL) {
-    static const bool splitk = [] {
-      const char *e = getenv("FS2_CONV_SPLITK");
-      return e == nullptr || e[0] != '0';
-    }();
+    const bool splitk = splitk_env();
     const int slots = num_cus() * ((WGM * WGN == 4 && NSB == 2) ? 2 : 1);
     const int nK = a.KS * (a.Cin_pad / CTraits<CT>::KE);
     const int64_t need = kSkCntBytes + (int64_t)slots * BM * BN * 4;
@@ -1698,8 +1744,14 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
           return;
         }
       }
+      const int nKd = a.KS * (a.Cin_pad / CTraits<CT>::KE);
       if (a.M >= 192 * 128)
         launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages (144 KiB)
+      else if (skpref_env() && splitk_env() && a.sk_cnt != nullptr && nKd >= 8)
+        // small M (encoder / variance predictors, M = B*L ~ 4k): 64-row tiles and split-K fill the
+        // chip with a quarter of the weight streaming of the 16-row tiles below (each tile streams
+        // its K range of the whole weight matrix)
+        launch_ring<CT, 1, 4, 3>(a, s);  // 64 x 256, 4 waves, 3 stages (120 KiB)
       else if (a.M >= 8192)
         launch_ring<CT, 1, 2, 4>(a, s);  // 32 x 256, 4 waves, 4 stages
       else
@@ -1716,8 +1768,13 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       launch<CT, 1, 4, 1, 3, TIn>(a, s);
   } else {
     const int ntn = (a.N + 127) / 128;
+    const int nKd = a.KS * (a.Cin_pad / CTraits<CT>::KE);
+    constexpr bool GLd = std::is_same<TIn, typename CTraits<CT>::T>::value;
     if ((int64_t)((a.M + 127) / 128) * ntn >= kTargetWGs)
       launch<CT, 2, 2, 4, 9, TIn>(a, s);
+    else if (GLd && skpref_env() && splitk_env() && a.sk_cnt != nullptr && nKd >= 16 &&
+             (int64_t)((a.M + 127) / 128) * ntn >= 64)
+      launch<CT, 2, 2, 4, 9, TIn>(a, s);  // 128 x 128 tiles + split-K instead of smaller tiles
     else if ((int64_t)((a.M + 63) / 64) * ntn >= kTargetWGs)
       launch<CT, 2, 2, 2, 9, TIn>(a, s);
     else
