@@ -1349,6 +1349,7 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
       advance();
     }
   }
+  int cbuf = 0, ibuf = NS - 1;  // ring slots of stage k and of stage k + NS - 1
   for (int k = k0; k < ((a.dbg & 1) ? k0 : k1); ++k) {
     // stage k landed (this wave's pieces): later issued stages may stay in flight
     const int ahead = k1 - 1 - k;
@@ -1361,10 +1362,12 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (k + NS - 1 < k1) {
-      issue(itap, icb, (k - k0 + NS - 1) % NS);
+      issue(itap, icb, ibuf);
       advance();
     }
-    compute(smem + ((k - k0) % NS) * STAGE);
+    compute(smem + cbuf * STAGE);
+    cbuf = cbuf == NS - 1 ? 0 : cbuf + 1;
+    ibuf = ibuf == NS - 1 ? 0 : ibuf + 1;
   }
   __syncthreads();
   if (nseg > 1) {
@@ -1571,6 +1574,15 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_rb_kernel(ConvArgs a) 
   epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
 }
 
+// Would a launch of T tiles on S slots split its tail (conv_tile_sk's rule)? Decided on the host
+// from the row capacity (padded launches: exact; packed ones: the device count can only be
+// smaller, and the kernel re-decides on it), so launches that never split get no spare ids.
+bool sk_would_split(int64_t T, int S, int sk_max) {
+  if (S <= 0 || T <= 0) return false;
+  const int64_t tail = T % S;
+  return tail > 0 && S / tail >= 2 && sk_max >= 2;
+}
+
 // FS2_CONV_SPLITK=0 turns the split-K tail off (A/B switch; the Python layer has its own).
 bool splitk_env() {
   static const bool on = [] {
@@ -1626,10 +1638,11 @@ void launch_ring(ConvArgs a, hipStream_t s) {
     const int slots = num_cus();
     const int nK = a.KS * (a.Cin_pad / CTraits<CT>::KE);
     const int64_t need = kSkCntBytes + (int64_t)slots * BM * 256 * 4;
-    if (splitk_env() && a.sk_cnt != nullptr && a.sk_ws_bytes >= need && nK >= 8 && slots > 0 &&
-        slots * 4 <= kSkCntBytes) {
+    const int sk_max = nK / 4 < 4 ? nK / 4 : 4;
+    if (splitk_env() && sk_would_split(nwg, slots, sk_max) && a.sk_cnt != nullptr && a.sk_ws_bytes >= need &&
+        nK >= 8 && slots > 0 && slots * 4 <= kSkCntBytes) {
       a.sk_slots = slots;
-      a.sk_max = nK / 4 < 4 ? nK / 4 : 4;
+      a.sk_max = sk_max;
       a.sk_part_bytes = (uint32_t)(need - kSkCntBytes);
       nwg += slots;
     }
@@ -1665,11 +1678,14 @@ void launch(ConvArgs a, hipStream_t s) {
     const int slots = num_cus() * ((WGM * WGN == 4 && NSB == 2) ? 2 : 1);
     const int nK = a.KS * (a.Cin_pad / CTraits<CT>::KE);
     const int64_t need = kSkCntBytes + (int64_t)slots * BM * BN * 4;
-    if (splitk && a.sk_cnt != nullptr && a.sk_ws_bytes >= need && nK >= 16 && slots > 0 && slots * 4 <= kSkCntBytes) {
+    // segments of >= 8 k-steps, at most 4 per tile: the last arriver reads the other segments'
+    // partials back (64 KiB each), which costs more than it saves past ~4
+    const int sk_max = nK / 8 < 4 ? nK / 8 : 4;
+    const bool may_split = a.row_split == 2 || sk_would_split(nwg, slots, sk_max);
+    if (splitk && may_split && a.sk_cnt != nullptr && a.sk_ws_bytes >= need && nK >= 16 && slots > 0 &&
+        slots * 4 <= kSkCntBytes) {
       a.sk_slots = slots;
-      // segments of >= 8 k-steps, at most 4 per tile: the last arriver reads the other
-      // segments' partials back (64 KiB each), which costs more than it saves past ~4
-      a.sk_max = nK / 8 < 4 ? nK / 8 : 4;
+      a.sk_max = sk_max;
       a.sk_part_bytes = (uint32_t)(need - kSkCntBytes);
       nwg += slots;  // spare ids for the tail segments (exit when unused)
     }
