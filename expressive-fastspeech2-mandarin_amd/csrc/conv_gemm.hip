@@ -964,18 +964,56 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   constexpr int TILE = 256 * kRowBytes;  // 32 KiB: one operand of one k-tile
   constexpr int EPI_LD = BN + 4;
   constexpr int SMEM = (4 * TILE > 128 * EPI_LD * 4) ? 4 * TILE : 128 * EPI_LD * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];  // A0 A1 B0 B1 (buffers)
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + 16];  // A0 A1 B0 B1 (buffers) + stream-K flag
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 2, wc = w & 3;  // M half (stagger group), N quarter
 
-  int M, m0, n0;
-  if (!conv_tile<BM>(a, M, m0, n0, BN)) return;
-
+  const int M = a.rows_dev != nullptr ? *a.rows_dev : a.M;
   const int KS = a.KS, pad = a.pad, T = a.T;
   const int nCk = a.Cin_pad / KE;
   const int nK = KS * nCk;
+
+  // Work: Ttot tiles. Without stream-K (sk_slots == 0) one tile per workgroup. With it (S = one
+  // workgroup per CU): R = Ttot / S whole rounds run one tile per workgroup (ids < R*S, XCD
+  // remap); the k-tiles of the tail tiles (flattened tile-major, W = tail * nK) are cut into Sp
+  // equal contiguous ranges, one per workgroup id R*S + j. Sp >= tail, so a range spans at most
+  // two tiles; a tile cut between ranges is summed by its last-arriving range (sc1 partials,
+  // fixed range order) and that workgroup runs its epilogue.
+  const int Ttot = a.row_split == 1 ? split_panels(a, M) * a.ntn : ((M + 255) / 256) * a.ntn;
+  const int S = a.sk_slots;
+  const int R = S > 0 ? Ttot / S : 0, tail = S > 0 ? Ttot - R * S : 0;
+  const int Sp = tail > 0 ? min(S, 4 * tail) : 0;
+  const int dp = S > 0 ? R * S : Ttot;
+  const int64_t W = (int64_t)tail * nK;
+  const int id = blockIdx.x;
+  int it_tile[2], it_kb[2], it_ke[2], nitems = 0;
+  int j = -1;  // stream-K range index
+  int64_t b0 = 0;
+  if (id < dp) {
+    it_tile[0] = xcd_remap(id, dp);
+    it_kb[0] = 0;
+    it_ke[0] = nK;
+    nitems = 1;
+  } else if (id < dp + Sp) {
+    j = id - dp;
+    b0 = (int64_t)j * W / Sp;
+    const int64_t b1 = (int64_t)(j + 1) * W / Sp;
+    for (int64_t k = b0; k < b1 && nitems < 2;) {
+      const int tt = (int)(k / nK);
+      const int64_t te = min(b1, (int64_t)(tt + 1) * nK);
+      it_tile[nitems] = dp + tt;
+      it_kb[nitems] = (int)(k - (int64_t)tt * nK);
+      it_ke[nitems] = (int)(te - (int64_t)tt * nK);
+      ++nitems;
+      k = te;
+    }
+  } else {
+    return;
+  }
+  // range that holds flattened k-tile k:  j(k) = ((k+1) * Sp - 1) / W
+  auto jof = [&](int64_t k) { return (int)(((k + 1) * Sp - 1) / W); };
   const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
   const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * 2u;
@@ -987,6 +1025,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   const int prow = lane >> 3, plc = (lane & 7) ^ ((lane >> 3) & 7);
   auto apiece = [&](int x, int i) { return 16 * (w >> 2) + 8 * x + 2 * (w & 3) + i; };
   auto bpiece = [&](int x, int i) { return (w & 3) * 8 + 4 * x + 2 * (w >> 2) + i; };
+  for (int item = 0; item < nitems; ++item) {
+  const int tile = item == 0 ? it_tile[0] : it_tile[1];
+  const int kb = item == 0 ? it_kb[0] : it_kb[1];
+  const int ke = item == 0 ? it_ke[0] : it_ke[1];
+  int m0, n0;
+  tile_coords(a, tile, Ttot, BM, BN, m0, n0);
   int arow[2][2], apos[2][2], alen[2][2];
   uint32_t boff[2][2];
 #pragma unroll
@@ -1075,19 +1119,24 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   auto lgkm0 = []() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
 
   // k-tile t = tap * nCk + cb; (tap1, cb1) tracks t+1 and (tap2, cb2) t+2 (no divisions in the loop)
-  int tap1 = nCk > 1 ? 0 : 1, cb1 = nCk > 1 ? 1 : 0;
+  const int tap0 = kb / nCk, cb0 = kb - (kb / nCk) * nCk;
+  int tap1 = tap0, cb1 = cb0;
+  if (++cb1 == nCk) {
+    cb1 = 0;
+    ++tap1;
+  }
   int tap2 = tap1, cb2 = cb1;
   if (++cb2 == nCk) {
     cb2 = 0;
     ++tap2;
   }
 
-  // prologue: issue order A0 B0 B1 A1 (t=0), A0 B0 B1 (t=1); k-tile 0 landed for everyone
-  dma_a(0, 0, 0, 0);
-  dma_b(0, 0, 0, 0);
-  dma_b(0, 0, 0, 1);
-  dma_a(0, 0, 0, 1);
-  if (nK > 1) {
+  // prologue: issue order A0 B0 B1 A1 (t=kb), A0 B0 B1 (t=kb+1); k-tile kb landed for everyone
+  dma_a(tap0, cb0, 0, 0);
+  dma_b(tap0, cb0, 0, 0);
+  dma_b(tap0, cb0, 0, 1);
+  dma_a(tap0, cb0, 0, 1);
+  if (kb + 1 < ke) {
     dma_a(tap1, cb1, 1, 0);
     dma_b(tap1, cb1, 1, 0);
     dma_b(tap1, cb1, 1, 1);
@@ -1098,9 +1147,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   __syncthreads();
   if (wr == 1) bar();
 
-  for (int t = 0; t < nK; ++t) {
-    const int cur = t & 1, nxt = cur ^ 1;
-    const bool has1 = t + 1 < nK, has2 = t + 2 < nK;
+  for (int t = kb; t < ke; ++t) {
+    const int cur = (t - kb) & 1, nxt = cur ^ 1;
+    const bool has1 = t + 1 < ke, has2 = t + 2 < ke;
     const char *As = smem + cur * TILE;
     const char *Bs = smem + 2 * TILE + cur * TILE;
     // phase 1: quadrant (0, 0)
@@ -1155,6 +1204,56 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   if (wr == 0) bar();
   __syncthreads();
 
+  if (kb != 0 || ke != nK) {  // a stream-K tile cut between ranges: hand over / sum the partials
+    const int tt = tile - dp;
+    const int64_t ts = (int64_t)tt * nK;
+    const int jf = jof(ts), nseg = jof(ts + nK - 1) - jf + 1;
+    // partial slot of the range jj's piece of this tile: 2*jj (its first piece) or 2*jj + 1
+    auto slot = [&](int jj) { return 2 * jj + (((int64_t)jj * W / Sp) < ts ? 1 : 0); };
+    const rsrc_t pr = make_rsrc(a.sk_part, a.sk_part_bytes);
+    auto pofs = [&](int sl, int mi, int ni) {
+      return (uint32_t)sl * (uint32_t)(BM * BN * 4) + (uint32_t)(((mi * 4 + ni) * 512 + tid) * 16);
+    };
+    const int own = slot(j);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc[mi][ni]), pr, pofs(own, mi, ni), 0, 16);
+    int &flag = *reinterpret_cast<int *>(smem + SMEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(a.sk_cnt + tt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == nseg - 1;
+      if (last) {
+        __hip_atomic_store(a.sk_cnt + tt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      flag = last;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool last = flag != 0;
+    __syncthreads();  // everyone has read the flag before a later item's hand-off rewrites it
+    if (!last) continue;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int sg = 0; sg < nseg; ++sg) {
+          const int jj = jf + sg;
+          f32x4 pv = acc[mi][ni];
+          if (jj != j)
+            pv = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, pofs(slot(jj), mi, ni), 0, 16));
+          tot += pv;
+        }
+        acc[mi][ni] = tot;
+      }
+  }
+
   // ---- epilogue, one M half at a time through LDS
   float *E = reinterpret_cast<float *>(smem);
 #pragma unroll
@@ -1172,13 +1271,67 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
     epilogue<128, BN, 8, false>(a, E, m0 + h * 128, n0, tid, M);  // never an LN epilogue
     __syncthreads();
   }
+  }  // work items
 }
 
-void launch_8p(ConvArgs a, hipStream_t s) {
+// Would a launch of T tiles on S slots split its tail (conv_tile_sk's rule)? Decided on the host
+// from the row capacity (padded launches: exact; packed ones: the device count can only be
+// smaller, and the kernel re-decides on it), so launches that never split get no spare ids.
+bool sk_would_split(int64_t T, int S, int sk_max) {
+  if (S <= 0 || T <= 0) return false;
+  const int64_t tail = T % S;
+  return tail > 0 && S / tail >= 2 && sk_max >= 2;
+}
+
+// FS2_CONV_SPLITK=0 turns the split-K tail off (A/B switch; the Python layer has its own).
+bool splitk_env() {
+  static const bool on = [] {
+    const char *e = getenv("FS2_CONV_SPLITK");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
+// FS2_CONV_SKPREF=1 (opt-in): small-M launches (encoder / variance predictors, M ~ 4k) use big
+// tiles + split-K instead of small tiles. Measured slower (cfg2 probes, us: VP 56 -> 68, encoder
+// conv-k9 31 -> 39, encoder conv-k1+LN 17 -> 32; bench -3.8 %): the partial-tile hand-off costs
+// more than the weight streaming it saves.
+bool skpref_env() {
+  static const bool on = [] {
+    const char *e = getenv("FS2_CONV_SKPREF");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
+// Compute units of the current device (cached per device id).
+int num_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+void launch_8p(ConvArgs a, hipStream_t s, bool stream_k = false) {
   a.ntn = (a.N + 255) / 256;
   a.ngr = a.ntn;
   int nwg = ((a.M + 255) / 256) * a.ntn;
   if (a.row_split == 1) nwg = nwg / a.split_slots * a.split_slots;  // whole rounds (device M <= a.M)
+  a.sk_slots = 0;
+  if (stream_k && a.row_split == 0) {  // conv_gemm_8p_kernel's stream-K tail: 2 partial slots per range
+    const int S = num_cus();
+    const int64_t need = kSkCntBytes + (int64_t)2 * S * 256 * 256 * 4;
+    if (S > 0 && S * 4 <= kSkCntBytes && a.sk_cnt != nullptr && a.sk_ws_bytes >= need) {
+      a.sk_slots = S;
+      a.sk_part_bytes = (uint32_t)(need - kSkCntBytes);
+      nwg += S;  // the tail's ranges (ids past the whole rounds; unused ids exit)
+    }
+  }
   if (nwg > 0) hipLaunchKernelGGL(conv_gemm_8p_kernel, dim3(nwg), dim3(512), 0, s, a);
 }
 
@@ -1574,49 +1727,6 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_rb_kernel(ConvArgs a) 
   epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
 }
 
-// Would a launch of T tiles on S slots split its tail (conv_tile_sk's rule)? Decided on the host
-// from the row capacity (padded launches: exact; packed ones: the device count can only be
-// smaller, and the kernel re-decides on it), so launches that never split get no spare ids.
-bool sk_would_split(int64_t T, int S, int sk_max) {
-  if (S <= 0 || T <= 0) return false;
-  const int64_t tail = T % S;
-  return tail > 0 && S / tail >= 2 && sk_max >= 2;
-}
-
-// FS2_CONV_SPLITK=0 turns the split-K tail off (A/B switch; the Python layer has its own).
-bool splitk_env() {
-  static const bool on = [] {
-    const char *e = getenv("FS2_CONV_SPLITK");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
-
-// FS2_CONV_SKPREF=1 (opt-in): small-M launches (encoder / variance predictors, M ~ 4k) use big
-// tiles + split-K instead of small tiles. Measured slower (cfg2 probes, us: VP 56 -> 68, encoder
-// conv-k9 31 -> 39, encoder conv-k1+LN 17 -> 32; bench -3.8 %): the partial-tile hand-off costs
-// more than the weight streaming it saves.
-bool skpref_env() {
-  static const bool on = [] {
-    const char *e = getenv("FS2_CONV_SKPREF");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on;
-}
-
-// Compute units of the current device (cached per device id).
-int num_cus() {
-  static int cache[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cache[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    cache[dev] = n;
-  }
-  return cache[dev];
-}
-
 template <int CT, int WGM, int WMI, int NA, int PB>
 void launch_rb(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM;
@@ -1721,6 +1831,19 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
     if (phased && !ln && a.KS >= 4 && a.N >= 256 && tiles256 >= 192 && S > 0) {
       if (tiles256 <= S) {  // at most one round: the phased kernel alone
         launch_8p(a, s);
+        return;
+      }
+      // FS2_CONV_8PSK=1 (opt-in): stream-K over the tail tiles in the phased launch itself. Correct
+      // (parity-tested) but measured slower than the 128x128 remainder launch (cfg2 conv-k9 191 vs
+      // 133 us): 256 KiB f32 partials per cut tile, and the last arriver's (tile fragment x range)
+      // read-back is latency-serialised; kept for later rounds.
+      static const bool sk8 = [] {
+        const char *e = getenv("FS2_CONV_8PSK");
+        return e != nullptr && e[0] == '1';
+      }();
+      if (sk8 && splitk_env() && a.sk_cnt != nullptr &&
+          a.sk_ws_bytes >= kSkCntBytes + (int64_t)2 * S * 256 * 256 * 4) {
+        launch_8p(a, s, true);  // whole rounds + stream-K over the tail tiles, one launch
         return;
       }
       ConvArgs a1 = a, a2 = a;  // whole rounds of 256 x 256 tiles, then the rows left over

@@ -148,7 +148,9 @@ def pack_conv_weight_fp8(w):
     return out.contiguous(), s.contiguous()
 
 
-SPLITK_WS_BYTES = 4096 + (32 << 20)  # fs2_conv_desc.splitk_ws: counters + 512 partial 128x128 f32 tiles
+# fs2_conv_desc.splitk_ws: counters + f32 partial tiles (32 MiB covers the 128x128 kernel's tail
+# segments on 256 CUs; FS2_CONV_8PSK=1, the phased kernel's stream-K, needs 128 MiB)
+SPLITK_WS_BYTES = 4096 + ((128 << 20) if os.environ.get("FS2_CONV_8PSK") == "1" else (32 << 20))
 _splitk_ws = {}
 _splitk_slot = [0]
 _splitk_on = [os.environ.get("FS2_CONV_SPLITK", "1") != "0"]

@@ -118,8 +118,8 @@ typedef struct fs2_conv_desc {
   /* split-K tail workspace (optional, NULL = off): when a launch's tiles leave a small last
      round, its tiles are split along K across the idle workgroups and summed in fixed segment
      order by the last arriving segment. The first 4 KiB are arrival counters and MUST be zero
-     before first use (they reset themselves); the rest holds f32 partial tiles. 32 MiB + 4 KiB
-     covers 256 CUs. One workspace per stream: concurrent launches must not share it. Results
+     before first use (they reset themselves); the rest holds f32 partial tiles. 128 MiB + 4 KiB
+     covers 256 CUs (32 MiB + 4 KiB without the phased kernel's stream-K tail). One workspace per stream: concurrent launches must not share it. Results
      are deterministic but not bitwise equal to the unsplit summation order.                  */
   void *splitk_ws;
   int64_t splitk_ws_bytes;

@@ -376,23 +376,28 @@ def test_split_precision_variance_predictor_matches_f32():
 
 
 @pytest.mark.parametrize("compute", [0, 1])
-@pytest.mark.parametrize("B,T,packed", [(1, 8576, False),   # 67 x 8 tiles: one full round + a 24-tile tail (256 CUs)
-                                        (3, 50, False),     # all-tail launch (16 tiles)
-                                        (1, 10400, False),  # 3 segments per tail tile: they start mid channel block
-                                        (64, 430, True)])   # cfg2 decoder shape on packed rows
-def test_conv_splitk_tail(ops, compute, B, T, packed):
+@pytest.mark.parametrize("B,T,packed,shape", [
+    (1, 8576, False, None),    # 67 x 8 tiles: one full round + a 24-tile tail (256 CUs)
+    (3, 50, False, None),      # all-tail launch (16 tiles)
+    (1, 10400, False, None),   # 3 segments per tail tile: they start mid channel block
+    (64, 430, True, None),     # cfg2 decoder shape on packed rows (bf16: phased kernel + 128x128 rows left)
+    (1, 40000, False, None),   # bf16 phased: 2 whole rounds (+ a 116-tile stream-K tail with FS2_CONV_8PSK=1)
+    (1, 16796, False, None),   # bf16 phased: 1 round + an 8-tile tail (32 ranges of 9 k-tiles under FS2_CONV_8PSK=1)
+    (1, 40000, False, (512, 512, 5))])  # PostNet conv shape (40 k-tiles)
+def test_conv_splitk_tail(ops, compute, B, T, packed, shape):
     """Split-K tail (ops.splitk_enabled): tail tiles cut along K across idle workgroups, summed
-    in segment order by the last arriver. Against the unsplit launch (same kernel, one K pass):
-    f32 2e-5 / bf16 2.5e-2 of the output scale; and bit-identical across repeated launches
-    (fixed summation order, counters reset themselves)."""
+    in segment order by the last arriver (128x128 kernel), or (FS2_CONV_8PSK=1) the phased
+    256x256 kernel's stream-K tail. Against the unsplit launches (ops.splitk_enabled(False)): f32 2e-5 /
+    bf16 2.5e-2 of the output scale; and bit-identical across repeated launches (fixed
+    summation order, counters reset themselves)."""
     L = _L()
     g = torch.Generator().manual_seed(T)
-    Cin, N, KS = 256, 1024, 9
+    Cin, N, KS = shape if shape is not None else (256, 1024, 9)
     dt = torch.float32 if compute == 0 else torch.bfloat16
     x = torch.randn(B, T, Cin, generator=g).to(DEV, dt)
     w = ops.pack_conv_weight((torch.randn(N, Cin, KS, generator=g) / np.sqrt(Cin * KS)).to(DEV), compute)
     b = (torch.randn(N, generator=g) * 0.1).to(DEV)
-    kw = dict(cin=Cin, ks=KS, pad=4, compute=compute, epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_F32)
+    kw = dict(cin=Cin, ks=KS, pad=(KS - 1) // 2, compute=compute, epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_F32)
     if packed:
         lens = torch.randint(200, T + 1, (B,), generator=g).to(DEV)
         kw["layout"] = ops.SeqLayout(lens, T)
