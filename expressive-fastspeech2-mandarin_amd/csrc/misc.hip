@@ -28,38 +28,46 @@ __global__ __launch_bounds__(256) void embed_pe_kernel(const int64_t *__restrict
 
 __device__ __forceinline__ int64_t clampi(int64_t v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
 
-// One workgroup per utterance, one thread per output channel.   (model/fastspeech2.py:101-110)
-__global__ void cond_kernel(const int64_t *speakers, const float *spk_table, int n_spk, const int64_t *emotions,
-                            const float *emo_table, int n_emo, int d_emo, const int64_t *arousals,
-                            const float *aro_table, int n_aro, int d_aro, const int64_t *valences,
-                            const float *val_table, int n_val, int d_val, const float *lin_w, const float *lin_b,
-                            int D, float *spk_out, float *emo_out) {
+// One workgroup per utterance.                                    (model/fastspeech2.py:101-110)
+// Speaker row: one thread per channel. Emotion Linear: one wave per output channel at a time,
+// lanes split the dc-long dot product (4 consecutive weights per lane per step: one coalesced
+// read of the weight row), then a wave reduction; the row reads of the 4 waves are independent,
+// so the 256 KiB weight matrix streams instead of 256 dependent per-thread chains.
+__global__ __launch_bounds__(256) void cond_kernel(const int64_t *speakers, const float *spk_table, int n_spk,
+                                                   const int64_t *emotions, const float *emo_table, int n_emo,
+                                                   int d_emo, const int64_t *arousals, const float *aro_table,
+                                                   int n_aro, int d_aro, const int64_t *valences,
+                                                   const float *val_table, int n_val, int d_val,
+                                                   const float *lin_w, const float *lin_b, int D, float *spk_out,
+                                                   float *emo_out) {
   extern __shared__ float cat[];
   const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int dc = d_emo + d_aro + d_val;
-  if (emo_table != nullptr) {
-    const int64_t e = clampi(emotions[b], n_emo), a = clampi(arousals[b], n_aro), v = clampi(valences[b], n_val);
-    for (int k = threadIdx.x; k < dc; k += blockDim.x) {
-      float x;
-      if (k < d_emo)
-        x = emo_table[e * d_emo + k];
-      else if (k < d_emo + d_aro)
-        x = aro_table[a * d_aro + (k - d_emo)];
-      else
-        x = val_table[v * d_val + (k - d_emo - d_aro)];
-      cat[k] = x;
-    }
+  if (spk_table != nullptr) {
+    const int64_t sp = clampi(speakers[b], n_spk);
+    for (int n = threadIdx.x; n < D; n += blockDim.x) spk_out[(int64_t)b * D + n] = spk_table[sp * D + n];
+  }
+  if (emo_table == nullptr) return;
+  const int64_t e = clampi(emotions[b], n_emo), a = clampi(arousals[b], n_aro), v = clampi(valences[b], n_val);
+  for (int k = threadIdx.x; k < dc; k += blockDim.x) {
+    float x;
+    if (k < d_emo)
+      x = emo_table[e * d_emo + k];
+    else if (k < d_emo + d_aro)
+      x = aro_table[a * d_aro + (k - d_emo)];
+    else
+      x = val_table[v * d_val + (k - d_emo - d_aro)];
+    cat[k] = x;
   }
   __syncthreads();
-  for (int n = threadIdx.x; n < D; n += blockDim.x) {
-    if (spk_table != nullptr) spk_out[(int64_t)b * D + n] = spk_table[clampi(speakers[b], n_spk) * D + n];
-    if (emo_table != nullptr) {
-      float s = 0.f;
-      const float *wr = lin_w + (int64_t)n * dc;
-      for (int k = 0; k < dc; ++k) s = fmaf(wr[k], cat[k], s);
-      s += lin_b[n];
-      emo_out[(int64_t)b * D + n] = fmaxf(s, 0.f);
-    }
+  for (int n = wid; n < D; n += nw) {
+    const float *wr = lin_w + (int64_t)n * dc;
+    float s = 0.f;
+    for (int k = lane; k < dc; k += 64) s = fmaf(wr[k], cat[k], s);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) emo_out[(int64_t)b * D + n] = fmaxf(s + lin_b[n], 0.f);
   }
 }
 
