@@ -614,11 +614,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
     wofs[j] = n < a.N ? (uint32_t)n * wrow + schunk * 16u : kOOB;
   }
   // sequence position / length of this lane's A fragment rows (tap validity)
+  // (kernel-1, unpadded convs have no taps to test: no row_pos reads, no dependent load latency)
+  const bool taps = KS != 1 || pad != 0;
   int tpos[WMI], tlen[WMI];
 #pragma unroll
   for (int mi = 0; mi < WMI; ++mi) {
     const int m = m0 + wr * WROWS + mi * 16 + (lane & 15);
-    if (a.row_pos != nullptr) {
+    if (!taps) {
+      tpos[mi] = 0;
+      tlen[mi] = 1;
+    } else if (a.row_pos != nullptr) {
       const int2 p = m < M ? a.row_pos[m] : make_int2(0, 0);
       tpos[mi] = p.x;
       tlen[mi] = p.y;
@@ -630,13 +635,17 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
   // wave-uniform: do this wave's WROWS rows lie inside one sequence? Then a tap shift is valid
   // for all of them or for none at the tile's own rows, and the per-lane masking is skipped.
   const int mw = m0 + wr * WROWS;
-  int tw = mw % T, lw = T;
-  if (a.row_pos != nullptr) {
-    const int2 p = mw < M ? a.row_pos[mw] : make_int2(0, 0);
-    tw = p.x;
-    lw = p.y;
+  int tw = 0, lw = WROWS;
+  if (taps) {
+    tw = mw % T;
+    lw = T;
+    if (a.row_pos != nullptr) {
+      const int2 p = mw < M ? a.row_pos[mw] : make_int2(0, 0);
+      tw = p.x;
+      lw = p.y;
+    }
   }
-  const bool wave_inside = tw + WROWS <= lw && mw + WROWS <= M;
+  const bool wave_inside = !taps || (tw + WROWS <= lw && mw + WROWS <= M);
   // LDS fragment-read bases: a 16-row step keeps (row & 7), so the swizzle is the same for
   // every mi / ni block and the block offset is an immediate.
   const int arow0 = wr * WROWS + (lane & 15);
@@ -1392,6 +1401,9 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
     if (m >= M) {
       apos[i] = 0;
       alen[i] = 0;
+    } else if (KS == 1 && pad == 0) {  // no taps: every row < M is valid, no row_pos read
+      apos[i] = 0;
+      alen[i] = 1;
     } else if (a.row_pos != nullptr) {
       const int2 p = a.row_pos[m];
       apos[i] = p.x;
@@ -1592,6 +1604,9 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_rb_kernel(ConvArgs a) 
     if (m >= M) {
       apos[i] = 0;
       alen[i] = 0;
+    } else if (KS == 1 && pad == 0) {  // no taps: every row < M is valid, no row_pos read
+      apos[i] = 0;
+      alen[i] = 1;
     } else if (a.row_pos != nullptr) {
       const int2 p = a.row_pos[m];
       apos[i] = p.x;

@@ -29,10 +29,9 @@ __global__ __launch_bounds__(256) void embed_pe_kernel(const int64_t *__restrict
 __device__ __forceinline__ int64_t clampi(int64_t v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
 
 // One workgroup per utterance.                                    (model/fastspeech2.py:101-110)
-// Speaker row: one thread per channel. Emotion Linear: one wave per output channel at a time,
-// lanes split the dc-long dot product (4 consecutive weights per lane per step: one coalesced
-// read of the weight row), then a wave reduction; the row reads of the 4 waves are independent,
-// so the 256 KiB weight matrix streams instead of 256 dependent per-thread chains.
+// Speaker row: one thread per channel. Emotion Linear (dc = 256): lanes split the dot product
+// (4 consecutive weights each: one coalesced 1 KiB read per weight row), each wave issues the
+// reads of 16 output channels before using any, then 16 wave reductions.
 __global__ __launch_bounds__(256) void cond_kernel(const int64_t *speakers, const float *spk_table, int n_spk,
                                                    const int64_t *emotions, const float *emo_table, int n_emo,
                                                    int d_emo, const int64_t *arousals, const float *aro_table,
@@ -61,13 +60,39 @@ __global__ __launch_bounds__(256) void cond_kernel(const int64_t *speakers, cons
     cat[k] = x;
   }
   __syncthreads();
-  for (int n = wid; n < D; n += nw) {
-    const float *wr = lin_w + (int64_t)n * dc;
-    float s = 0.f;
-    for (int k = lane; k < dc; k += 64) s = fmaf(wr[k], cat[k], s);
+  if (dc == 256) {
+    // lane l holds k = 4l .. 4l+3; per pass a wave issues the 16-byte weight reads of 16 output
+    // channels at once (coalesced 1 KiB rows, one memory round trip per pass), then reduces
+    const float4 x4 = reinterpret_cast<const float4 *>(cat)[lane];
+    constexpr int CH = 16;
+    for (int n0 = wid * CH; n0 < D; n0 += nw * CH) {
+      float4 wv[CH];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (lane == 0) emo_out[(int64_t)b * D + n] = fmaxf(s + lin_b[n], 0.f);
+      for (int c = 0; c < CH; ++c)
+        wv[c] = n0 + c < D ? reinterpret_cast<const float4 *>(lin_w + (int64_t)(n0 + c) * dc)[lane]
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      float s[CH];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) s[c] = wv[c].x * x4.x + wv[c].y * x4.y + wv[c].z * x4.z + wv[c].w * x4.w;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s[c] += __shfl_xor(s[c], o, 64);
+      }
+      if (lane < CH && n0 + lane < D) {
+        float v = s[0];
+#pragma unroll
+        for (int c = 1; c < CH; ++c) v = lane == c ? s[c] : v;
+        emo_out[(int64_t)b * D + n0 + lane] = fmaxf(v + lin_b[n0 + lane], 0.f);
+      }
+    }
+    return;
+  }
+  for (int n = threadIdx.x; n < D; n += blockDim.x) {  // general dc: one thread per channel
+    const float *wr = lin_w + (int64_t)n * dc;
+    float acc = 0.f;
+    for (int k = 0; k < dc; ++k) acc = fmaf(wr[k], cat[k], acc);
+    emo_out[(int64_t)b * D + n] = fmaxf(acc + lin_b[n], 0.f);
   }
 }
 

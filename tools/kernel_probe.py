@@ -54,6 +54,10 @@ def main():
         f, h = rnd(B * T, 1024), rnd(B * T, 256)
         fn = lambda: ops.conv1d(f, lp.w2, lp.b2, cin=1024, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_RES_LN,
                                 out_dtype=P.act_dtype, residual=h, ln=lp.ln2, layout=lay)
+    elif a.kernel == "fc":  # attention output projection + residual + LN (decoder, packed rows)
+        o, h = rnd(B * T, 256), rnd(B * T, 256)
+        fn = lambda: ops.conv1d(o, lp.wfc, lp.bfc, cin=256, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_RES_LN,
+                                out_dtype=P.act_dtype, residual=h, ln=lp.ln1, layout=lay)
     elif a.kernel == "qkv":
         h = rnd(B * T, 256)
         fn = lambda: ops.conv1d(h, lp.wqkv, lp.bqkv, cin=256, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
