@@ -180,6 +180,7 @@ struct ConvArgs {
   // 1 = this launch runs the 256-row panels [0, P1), 2 = it runs the rows from P1 * 256 on.
   int row_split;
   int split_slots;          // workgroups the phased kernel runs at once (one per CU)
+  int ashift;               // bf16 LDS-DMA conv: derive tap t's A fragments from tap t-1's (row shift)
 };
 
 constexpr int64_t kSkCntBytes = 4096;  // counter block at the start of the split-K workspace
@@ -559,6 +560,23 @@ __device__ __forceinline__ void vm_wait_n(int n) {
   }
 }
 
+// A fragments of the next tap from the current tap's: the A operand of mfma_16x16x32 holds, in
+// lane l, row (l & 15) of a 16-row block (8 consecutive k), and tap t+1 reads every row one row
+// further down the LDS halo. So lane l of the shifted block takes lane l+1 (DPP row_shl:1, rows
+// of 16 lanes = the operand's row groups) and lane 15 takes lane 0 of the next 16-row block
+// (row_shr:15 into the old value). One LDS read of a 16-row block per tap replaces WMI.
+__device__ __forceinline__ bf16x8 shift_rows(bf16x8 cur, bf16x8 nxt) {
+  typedef int i32x4v __attribute__((ext_vector_type(4)));
+  const i32x4v c = __builtin_bit_cast(i32x4v, cur), n = __builtin_bit_cast(i32x4v, nxt);
+  i32x4v r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int t = __builtin_amdgcn_update_dpp(0, n[q], 0x11F, 0xF, 0xF, false);  // row_shr:15: lane 15 <- lane 0
+    r[q] = __builtin_amdgcn_update_dpp(t, c[q], 0x101, 0xF, 0xF, false);       // row_shl:1: lane i <- lane i+1
+  }
+  return __builtin_bit_cast(bf16x8, r);
+}
+
 // NSB: depth of the B (weight) stage ring on the LDS-DMA path. NSB == 2: one k-step in flight,
 // vmcnt(0) per step. NSB > 2 (tall tiles, KS >= NSB): B of step k+NSB-1 is issued right after
 // the barrier that retires step k-1, the next channel block's A halo at tap 0 of the current one
@@ -697,7 +715,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
 
   const int bf8_0 = lds_off(wc * 64 + (lane & 15), 2 * (lane >> 4));
   const int bf8_1 = lds_off(wc * 64 + (lane & 15), 2 * (lane >> 4) + 1);
-  auto compute = [&](int aslot, int tap, const char *Bs) {
+  // persistent A fragments for the tap-to-tap row shift (bf16, LDS-DMA path)
+  constexpr bool ASH = CT == FS2_BF16 && GL && KSMAX > 1;
+  const bool ashift = ASH && a.ashift && KS > 1;
+  bf16x8 Fs[2][WMI];
+  auto compute = [&](int aslot, int tap, const char *Bs, bool fresh) {
     const char *As = Abuf + aslot * A_BYTES;
     const int sh = tap - pad;
     const bool need_mask = !(wave_inside && tw + sh >= 0 && tw + WROWS - 1 + sh < lw);
@@ -729,8 +751,23 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
       const char *Bb = Bs + (s ? bread1 : bread0);
       if constexpr (CT == FS2_BF16) {
         bf16x8 af[WMI], bfr[4];
+        if (ASH && ashift) {
+          if (fresh) {
 #pragma unroll
-        for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const bf16x8 *>(Ab + mi * 16 * kRowBytes);
+            for (int mi = 0; mi < WMI; ++mi) Fs[s][mi] = *reinterpret_cast<const bf16x8 *>(Ab + mi * 16 * kRowBytes);
+          } else {
+            // block WMI at tap-1: only lane (l & 15) == 0 of each group is used (clamped in the halo)
+            const int er = min(arow0 + 16 * WMI + tap - 1, HMAX - 1);
+            const bf16x8 ext = *reinterpret_cast<const bf16x8 *>(As + lds_off(er, s * 4 + (lane >> 4)));
+#pragma unroll
+            for (int mi = 0; mi < WMI; ++mi) Fs[s][mi] = shift_rows(Fs[s][mi], mi + 1 < WMI ? Fs[s][mi + 1] : ext);
+          }
+#pragma unroll
+          for (int mi = 0; mi < WMI; ++mi) af[mi] = Fs[s][mi];
+        } else {
+#pragma unroll
+          for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const bf16x8 *>(Ab + mi * 16 * kRowBytes);
+        }
         if (need_mask) {
 #pragma unroll
           for (int mi = 0; mi < WMI; ++mi)
@@ -860,7 +897,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
           }
         }
         if (tap == 0 && ks > k0 && cb + 1 <= cb_last) dma_a(cb + 1, (cb + 1) & 1);
-        compute(cb & 1, tap, Bbuf + (ks % NSB) * B_BYTES);
+        compute(cb & 1, tap, Bbuf + (ks % NSB) * B_BYTES, tap == 0 || ks == k0);
         if (++tap == KS) {
           tap = 0;
           ++cb;
@@ -881,7 +918,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
         dma_b(ncb, ntap, (ks + 1) & 1);
         if (last_tap) dma_a(ncb, ncb & 1);
       }
-      compute(cb & 1, tap, Bbuf + (ks & 1) * B_BYTES);
+      compute(cb & 1, tap, Bbuf + (ks & 1) * B_BYTES, tap == 0 || ks == k0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       cb = ncb;
@@ -905,7 +942,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
       const bool last_tap = tap == KS - 1;
       if (ks + 2 < nK) gload_b(sb_this, cb2, tap2);
       if (tap == 0 && cb + 1 < nCk) gload_a(cb + 1);
-      compute(cb & 1, tap, Bbuf + (ks & 1) * B_BYTES);
+      compute(cb & 1, tap, Bbuf + (ks & 1) * B_BYTES, true);
       if (ks + 1 < nK) lstore_b(sb_next, (ks + 1) & 1);
       if (last_tap && cb + 1 < nCk) lstore_a((cb + 1) & 1);
       __syncthreads();
@@ -2033,6 +2070,16 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.sk_ws_bytes = 0;
   a.row_split = 0;
   a.split_slots = 1;
+  {
+    // FS2_CONV_ASHIFT=1 (opt-in): tap-to-tap A-fragment row shift (shift_rows). Correct but slower
+    // (cfg2 probes: conv-k9 rows-left launch 59 -> 71 us, encoder conv-k9 33 -> 40 us): the LDS
+    // reads it saves were not the limit, the DPP chain it adds is.
+    static const bool ash = [] {
+      const char *e = getenv("FS2_CONV_ASHIFT");
+      return e != nullptr && e[0] == '1';
+    }();
+    a.ashift = ash ? 1 : 0;
+  }
   if (d->splitk_ws != nullptr && d->splitk_ws_bytes > kSkCntBytes && d->splitk_ws_bytes < (1LL << 31) + kSkCntBytes) {
     a.sk_cnt = reinterpret_cast<int *>(d->splitk_ws);
     a.sk_part = reinterpret_cast<float *>(reinterpret_cast<char *>(d->splitk_ws) + kSkCntBytes);
