@@ -12,12 +12,13 @@
 // D-wide row with 16-byte vector loads/stores; frames at or past min(mel_len, T_out) are
 // zero. An optional f32 position-encoding row is added on the way out (Decoder input,
 // transformer/Models.py:158-160) so the expanded tensor is written to HBM exactly once.
+#include <cstdlib>
+
 #include "fs2_common.h"
 
 namespace {
 
 constexpr int kScanThreads = 256;
-constexpr int kRowsPerBlock = 32;
 constexpr int kLdsCum = 2048;  // cum rows up to this many phonemes are searched in LDS
 
 __device__ __forceinline__ int64_t frames_of(const void *dur, int kind, float d_control, int64_t idx,
@@ -82,20 +83,20 @@ __global__ __launch_bounds__(kScanThreads) void lr_durations_kernel(const void *
 // (first i with cum[i] > t) costs LDS latency, not log2(L) dependent global round trips; then
 // each thread keeps UNR independent 16-byte row pieces in flight (all loads issued before the
 // stores).
-template <typename TX, typename TO, bool HAS_PE>
+template <typename TX, typename TO, bool HAS_PE, int ROWS, bool NT>
 __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x, const int32_t *__restrict__ cum,
                                                         const int64_t *__restrict__ mel_len, int L, int D, int T_out,
                                                         const float *__restrict__ pe, TO *__restrict__ out,
                                                         int32_t *__restrict__ index_map,
                                                         const int32_t *__restrict__ out_cu) {
-  constexpr int UNR = 4;
+  constexpr int UNR = ROWS / 8;  // D = 256 bf16: 32 16-byte pieces per row, 256 threads
   const int b = blockIdx.y;
-  const int t0 = blockIdx.x * kRowsPerBlock;
+  const int t0 = blockIdx.x * ROWS;
   const int tid = threadIdx.x;
   // packed output (out_cu != NULL): only frames t < out_cu[b+1] - out_cu[b] exist, at row out_cu[b] + t
   const int t_end = out_cu != nullptr ? min(T_out, out_cu[b + 1] - out_cu[b]) : T_out;
   if (t0 >= t_end && index_map == nullptr) return;
-  __shared__ int src[kRowsPerBlock];
+  __shared__ int src[ROWS];
   __shared__ int32_t scum[kLdsCum];
   const int64_t ml = mel_len[b];
   const int lim = (int)(ml < (int64_t)T_out ? ml : (int64_t)T_out);
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x
     for (int i = tid; i < L; i += 256) scum[i] = c[i];
   __syncthreads();
   const int32_t *sc = in_lds ? scum : c;
-  if (tid < kRowsPerBlock) {
+  if (tid < ROWS) {
     const int t = t0 + tid;
     int s = -1;
     if (t < lim) {
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x
   }
   __syncthreads();
   const int vpr = D >> 3;
-  const int rows = min(kRowsPerBlock, t_end - t0);
+  const int rows = min(ROWS, t_end - t0);
   if (rows <= 0) return;
   const int total = rows * vpr;
   const TX *xb = x + (int64_t)b * L * D;
@@ -152,21 +153,53 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int e = base + u * 256;
-      if (e < total) store8(ob + (int64_t)e * 8, v[u]);
+      if (e < total) {
+        if constexpr (NT && sizeof(TO) == 2) {  // streaming output: non-temporal 16-byte stores
+          bf16x8 o;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] = (bf16)v[u][q];
+          __builtin_nontemporal_store(o, reinterpret_cast<bf16x8 *>(ob + (int64_t)e * 8));
+        } else {
+          store8(ob + (int64_t)e * 8, v[u]);
+        }
+      }
     }
   }
 }
 
+template <typename TX, typename TO, int ROWS, bool NT>
+void launch_expand_v(const void *x, const int32_t *cum, const int64_t *mel_len, int B, int L, int D, int T_out,
+                     const float *pe, void *out, int32_t *index_map, const int32_t *out_cu, hipStream_t s) {
+  dim3 grid((T_out + ROWS - 1) / ROWS, B);
+  if (pe != nullptr)
+    hipLaunchKernelGGL((lr_expand_kernel<TX, TO, true, ROWS, NT>), grid, dim3(256), 0, s,
+                       reinterpret_cast<const TX *>(x), cum, mel_len, L, D, T_out, pe, reinterpret_cast<TO *>(out),
+                       index_map, out_cu);
+  else
+    hipLaunchKernelGGL((lr_expand_kernel<TX, TO, false, ROWS, NT>), grid, dim3(256), 0, s,
+                       reinterpret_cast<const TX *>(x), cum, mel_len, L, D, T_out, pe, reinterpret_cast<TO *>(out),
+                       index_map, out_cu);
+}
+
+// FS2_LR_VARIANT (A/B): 0 = 32 rows per workgroup, 1 = 64 rows, 2 = 32 rows + non-temporal output
+// stores (default), 3 = 64 rows + non-temporal stores. Measured (same box, us per launch, cfg2 /
+// cfg4 stress): 9.5 / 26.1, 9.4 / 33.4, 9.2 / 24.2, 9.3 / 28.4 -- cfg4 moves 152 MB, so variant 2
+// streams 6.3 TB/s (79 % of the 8 TB/s HBM peak); the bf16 bench is neutral to it.
 template <typename TX, typename TO>
 void launch_expand(const void *x, const int32_t *cum, const int64_t *mel_len, int B, int L, int D, int T_out,
                    const float *pe, void *out, int32_t *index_map, const int32_t *out_cu, hipStream_t s) {
-  dim3 grid((T_out + kRowsPerBlock - 1) / kRowsPerBlock, B);
-  if (pe != nullptr)
-    hipLaunchKernelGGL((lr_expand_kernel<TX, TO, true>), grid, dim3(256), 0, s, reinterpret_cast<const TX *>(x), cum,
-                       mel_len, L, D, T_out, pe, reinterpret_cast<TO *>(out), index_map, out_cu);
+  static const int v = [] {
+    const char *e = getenv("FS2_LR_VARIANT");
+    return e != nullptr ? atoi(e) : 2;
+  }();
+  if (v == 1)
+    launch_expand_v<TX, TO, 64, false>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
+  else if (v == 2)
+    launch_expand_v<TX, TO, 32, true>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
+  else if (v == 3)
+    launch_expand_v<TX, TO, 64, true>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
   else
-    hipLaunchKernelGGL((lr_expand_kernel<TX, TO, false>), grid, dim3(256), 0, s, reinterpret_cast<const TX *>(x), cum,
-                       mel_len, L, D, T_out, pe, reinterpret_cast<TO *>(out), index_map, out_cu);
+    launch_expand_v<TX, TO, 32, false>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
 }
 
 // get_mask_from_lengths (utils/tools.py:152-160): mask[b, t] = t >= lens[b]  (True = padding)
