@@ -1350,6 +1350,16 @@ bool skpref_env() {
   return on;
 }
 
+// FS2_CONV_DEEPB (A/B): 1 = the 64-row small-M conv tiles use a 3-deep B ring (2 workgroups per
+// CU still fit), 2 = also the 128 x 128 rows-left launch of the decoder conv-k9 (1 per CU).
+int deepb_env() {
+  static const int v = [] {
+    const char *e = getenv("FS2_CONV_DEEPB");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // Compute units of the current device (cached per device id).
 int num_cus() {
   static int cache[64] = {0};
@@ -1837,7 +1847,12 @@ void launch(ConvArgs a, hipStream_t s) {
   a.sk_slots = 0;
   if constexpr (GL) {
     const bool splitk = splitk_env();
-    const int slots = num_cus() * ((WGM * WGN == 4 && NSB == 2) ? 2 : 1);
+    // resident workgroups per CU: LDS-limited (the kernel's SMEM + flag), at most 2 (launch bounds)
+    constexpr int HMX = ((BM + KSMAX - 1) + 7) / 8 * 8;
+    constexpr int STG = 2 * HMX * kRowBytes + NSB * BN * kRowBytes;
+    constexpr int SMB = (STG > BM * (BN + 4) * 4 ? STG : BM * (BN + 4) * 4) + 16;
+    constexpr int PER_CU = (WGM * WGN == 4) ? (163840 / SMB >= 2 ? 2 : 1) : 1;
+    const int slots = num_cus() * PER_CU;
     const int nK = a.KS * (a.Cin_pad / CTraits<CT>::KE);
     const int64_t need = kSkCntBytes + (int64_t)slots * BM * BN * 4;
     // segments of >= 8 k-steps, at most 4 per tile: the last arriver reads the other segments'
@@ -1904,7 +1919,10 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       a2.row_split = 2;
       a2.split_slots = S;
       launch_8p(a1, s);
-      launch<CT, 2, 2, 4, 9, TIn>(a2, s);
+      if (deepb_env() >= 2 && a.KS >= 3)
+        launch<CT, 2, 2, 4, 9, TIn, 3>(a2, s);
+      else
+        launch<CT, 2, 2, 4, 9, TIn>(a2, s);
       return;
     }
   }
@@ -1961,13 +1979,22 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
     const int ntn = (a.N + 127) / 128;
     const int nKd = a.KS * (a.Cin_pad / CTraits<CT>::KE);
     constexpr bool GLd = std::is_same<TIn, typename CTraits<CT>::T>::value;
-    if ((int64_t)((a.M + 127) / 128) * ntn >= kTargetWGs)
+    static const int short_k = [] {  // FS2_CONV_SHORTK=1 (A/B): 64-row tiles for K <= 256 GEMMs
+      const char *e = getenv("FS2_CONV_SHORTK");
+      return e != nullptr ? atoi(e) : 0;
+    }();
+    if (short_k && a.KS == 1 && a.Cin <= 256 && (int64_t)((a.M + 63) / 64) * ntn >= kTargetWGs)
+      launch<CT, 2, 2, 2, 9, TIn>(a, s);
+    else if ((int64_t)((a.M + 127) / 128) * ntn >= kTargetWGs)
       launch<CT, 2, 2, 4, 9, TIn>(a, s);
     else if (GLd && skpref_env() && splitk_env() && a.sk_cnt != nullptr && nKd >= 16 &&
              (int64_t)((a.M + 127) / 128) * ntn >= 64)
       launch<CT, 2, 2, 4, 9, TIn>(a, s);  // 128 x 128 tiles + split-K instead of smaller tiles
     else if ((int64_t)((a.M + 63) / 64) * ntn >= kTargetWGs)
-      launch<CT, 2, 2, 2, 9, TIn>(a, s);
+      if (GLd && deepb_env() >= 1 && a.KS >= 3)
+        launch<CT, 2, 2, 2, 9, TIn, 3>(a, s);
+      else
+        launch<CT, 2, 2, 2, 9, TIn>(a, s);
     else
       launch<CT, 2, 2, 1, 9, TIn>(a, s);
   }
