@@ -181,6 +181,7 @@ struct ConvArgs {
   int row_split;
   int split_slots;          // workgroups the phased kernel runs at once (one per CU)
   int ashift;               // bf16 LDS-DMA conv: derive tap t's A fragments from tap t-1's (row shift)
+  int ln_pairs;             // LayerNorm epilogues: two rows per wave-iteration, 16-byte stores
 };
 
 constexpr int64_t kSkCntBytes = 4096;  // counter block at the start of the split-K workspace
@@ -311,6 +312,149 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
   const int lane = tid & 63, wid = tid >> 6;
   const int T = a.T;
   const int epi = a.epi;
+  static_assert(BM % NWAVES == 0, "rows per wave");
+  if constexpr (LN && (BM / NWAVES) % 2 == 0) if (a.ln_pairs && (epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN ||
+                                                                  epi == FS2_EPI_RELU_LN_DOT)) {
+    // Two rows per wave-iteration: half-wave h = lane >> 5 takes row k = 2p + h of the wave's rows,
+    // lane owns columns 8*(lane & 31) .. +7 (N == BN == 256). 16-byte residual loads and output
+    // stores (8-byte ones are issue-bound), half the reduction chains of one row per wave.
+    constexpr int RPW = BM / NWAVES, NP = RPW / 2;
+    const int h = lane >> 5, hl = lane & 31;
+    const int n = hl * 8;
+    float bias8[8], g8[8], be8[8], cs8[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+    load8(a.gamma + n, g8);
+    load8(a.beta + n, be8);
+    load8(a.bias + n, bias8);
+    if (a.colscale != nullptr) load8(a.colscale + n, cs8);
+    const float inv_n = 1.0f / (float)a.N;
+    auto hsum = [](float v) {  // sum over the 32 lanes of a half-wave
+      v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+      v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+      v += dpp_mov<0x141>(v);  // row_half_mirror
+      v += dpp_mov<0x140>(v);  // row_mirror: every lane of a 16-lane row holds the row's sum
+      return v + __shfl_xor(v, 16, 64);
+    };
+    const bool res_bf16 = a.res_dt == FS2_BF16;
+    uint4 rraw[NP][2];
+    if (epi == FS2_EPI_RES_LN) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int m = min(m0 + wid + (2 * p + h) * NWAVES, M - 1);
+        if (res_bf16) {
+          rraw[p][0] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const bf16 *>(a.res) + (int64_t)m * a.rs + n);
+          rraw[p][1] = rraw[p][0];
+        } else {
+          const uint4 *rp = reinterpret_cast<const uint4 *>(reinterpret_cast<const float *>(a.res) + (int64_t)m * a.rs + n);
+          rraw[p][0] = rp[0];
+          rraw[p][1] = rp[1];
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        asm volatile("" ::"v"(rraw[p][0].x), "v"(rraw[p][0].y), "v"(rraw[p][0].z), "v"(rraw[p][0].w), "v"(rraw[p][1].x),
+                     "v"(rraw[p][1].y), "v"(rraw[p][1].z), "v"(rraw[p][1].w));
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int r = wid + (2 * p + h) * NWAVES;
+      const bool row_ok = m0 + r < M;
+      const int m = min(m0 + r, M - 1);
+      float v[8];
+      load8(E + r * EPI_LD + n, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = v[q] * cs8[q] + bias8[q];
+      if (epi == FS2_EPI_RES_LN) {
+        if (res_bf16) {
+          const uint32_t w4[4] = {rraw[p][0].x, rraw[p][0].y, rraw[p][0].z, rraw[p][0].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[2 * q] += __uint_as_float(w4[q] << 16);
+            v[2 * q + 1] += __uint_as_float(w4[q] & 0xffff0000u);
+          }
+        } else {
+          const uint32_t w8[8] = {rraw[p][0].x, rraw[p][0].y, rraw[p][0].z, rraw[p][0].w,
+                                  rraw[p][1].x, rraw[p][1].y, rraw[p][1].z, rraw[p][1].w};
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] += __uint_as_float(w8[q]);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.0f);
+      }
+      float s1 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s1 += v[q];
+      const float mean = hsum(s1) * inv_n;
+      float d[8], ss = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        d[q] = v[q] - mean;
+        ss += d[q] * d[q];
+      }
+      const float var = hsum(ss) * inv_n;
+      const float rstd = 1.0f / sqrtf(var + a.eps);
+      float y[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) y[q] = d[q] * rstd * g8[q] + be8[q];
+      const int bb = m / T;
+      const int t = m - bb * T;
+      const bool masked = (a.lens != nullptr) && ((int64_t)t >= a.lens[bb]);
+      if (epi == FS2_EPI_RELU_LN_DOT) {
+        float dw8[8];
+        load8(a.dw + n, dw8);
+        float sd = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sd += y[q] * dw8[q];
+        const float sdot = hsum(sd) + a.db;
+        if (hl == 0 && row_ok) reinterpret_cast<float *>(a.out)[m] = masked ? 0.0f : sdot;
+        continue;
+      }
+      if (epi == FS2_EPI_RES_LN) {
+        if (masked) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) y[q] = 0.0f;
+        }
+        if (a.av1 != nullptr) {
+          float av[8];
+          load8(a.av1 + (int64_t)bb * a.N + n, av);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) y[q] += av[q];
+        }
+        if (a.av2 != nullptr) {
+          float av[8];
+          load8(a.av2 + (int64_t)bb * a.N + n, av);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) y[q] += av[q];
+        }
+      }
+      if (!row_ok) continue;
+      if (a.out_split) {  // two bf16 planes: hi, lo = bf16(y - hi)
+        float hi[8], lo[8];
+        bf16 *op = reinterpret_cast<bf16 *>(a.out) + (int64_t)m * a.os;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          hi[q] = (float)(bf16)y[q];
+          lo[q] = y[q] - hi[q];
+        }
+        store8(op + n, hi);
+        store8(op + a.N + n, lo);
+        continue;
+      }
+      if (a.out_dt == FS2_BF16)
+        store8(reinterpret_cast<bf16 *>(a.out) + (int64_t)m * a.os + n, y);
+      else if (a.out_dt == FS2_F32)
+        store8(reinterpret_cast<float *>(a.out) + (int64_t)m * a.os + n, y);
+      else {
+        uint2 o = make_uint2(pack4_fp8(y, a.out_scale), pack4_fp8(y + 4, a.out_scale));
+        *reinterpret_cast<uint2 *>(reinterpret_cast<fp8 *>(a.out) + (int64_t)m * a.os + n) = o;
+      }
+      if (a.out2 != nullptr) {
+        uint2 o = make_uint2(pack4_fp8(y, a.out2_scale), pack4_fp8(y + 4, a.out2_scale));
+        *reinterpret_cast<uint2 *>(reinterpret_cast<fp8 *>(a.out2) + (int64_t)m * a.N + n) = o;
+      }
+    }
+    return;
+  }
   if constexpr (LN) if (epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN || epi == FS2_EPI_RELU_LN_DOT) {
     // one wave per row; N == BN == 256 (checked on the host), lane owns columns 4*lane..4*lane+3
     const int n = lane * 4;
@@ -2106,6 +2250,11 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
       return e != nullptr && e[0] == '1';
     }();
     a.ashift = ash ? 1 : 0;
+    static const bool lnp = [] {  // FS2_LN_PAIRS=0: one row per wave-iteration (round-1 epilogue)
+      const char *e = getenv("FS2_LN_PAIRS");
+      return e == nullptr || e[0] != '0';
+    }();
+    a.ln_pairs = lnp ? 1 : 0;
   }
   if (d->splitk_ws != nullptr && d->splitk_ws_bytes > kSkCntBytes && d->splitk_ws_bytes < (1LL << 31) + kSkCntBytes) {
     a.sk_cnt = reinterpret_cast<int *>(d->splitk_ws);
