@@ -590,10 +590,52 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
     return;
   }
 
+  constexpr int NT = 64 * NWAVES;
+  if ((a.N & 7) == 0 && (a.os & 7) == 0 && a.ln_pairs) {
+    // elementwise epilogues, 8 columns per thread: 16-byte stores (8-byte ones are issue-bound
+    // on the store-heavy launches: Q|K|V writes 3x what it reads)
+    constexpr int G8 = BN / 8;
+    static_assert(NT % G8 == 0, "column group per thread");
+    const int cg = tid % G8;
+    const int n = n0 + cg * 8;
+    if (n >= a.N) return;
+    float bias8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, cs8[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+    if (a.bias != nullptr) load8(a.bias + n, bias8);
+    if (a.colscale != nullptr) load8(a.colscale + n, cs8);
+    for (int r = tid / G8; r < BM; r += NT / G8) {
+      const int m = m0 + r;
+      if (m >= M) break;
+      float v[8];
+      load8(E + r * EPI_LD + cg * 8, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = v[q] * cs8[q] + bias8[q];
+      if (epi == FS2_EPI_BIAS_RELU) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.0f);
+      } else if (epi == FS2_EPI_BIAS_TANH) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = tanhf(v[q]);
+      } else if (epi == FS2_EPI_BIAS_RES) {
+        float rv[8];
+        load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n, rv);
+        load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n + 4, rv + 4);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] += rv[q];
+      }
+      const int64_t o = (int64_t)m * a.os + n;
+      if (a.out_dt == FS2_BF16)
+        store8(reinterpret_cast<bf16 *>(a.out) + o, v);
+      else if (a.out_dt == FS2_F32)
+        store8(reinterpret_cast<float *>(a.out) + o, v);
+      else
+        *reinterpret_cast<uint2 *>(reinterpret_cast<fp8 *>(a.out) + o) =
+            make_uint2(pack4_fp8(v, a.out_scale), pack4_fp8(v + 4, a.out_scale));
+    }
+    return;
+  }
   // elementwise epilogues: each thread keeps one 4-column group (threads % (BN/4) == 0), so its
   // bias is loaded once; rows step by threads / (BN/4)
   constexpr int G = BN / 4;
-  constexpr int NT = 64 * NWAVES;
   static_assert(NT % G == 0, "column group per thread");
   const int cg = tid % G;
   const int n = n0 + cg * 4;
