@@ -591,9 +591,10 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
   }
 
   constexpr int NT = 64 * NWAVES;
-  if ((a.N & 7) == 0 && (a.os & 7) == 0 && a.ln_pairs) {
-    // elementwise epilogues, 8 columns per thread: 16-byte stores (8-byte ones are issue-bound
-    // on the store-heavy launches: Q|K|V writes 3x what it reads)
+  if ((a.N & 7) == 0 && (a.os & 7) == 0 && a.ln_pairs && a.out_dt != FS2_F32) {
+    // elementwise epilogues with bf16 / fp8 outputs, 8 columns per thread: 16-byte stores (8-byte
+    // ones are issue-bound on the store-heavy launches: Q|K|V writes 3x what it reads). f32
+    // outputs keep the 4-column path below, whose stores are 16 bytes already.
     constexpr int G8 = BN / 8;
     static_assert(NT % G8 == 0, "column group per thread");
     const int cg = tid % G8;

@@ -10,7 +10,7 @@ timeout -k 10 500 python bench.py --dtype fp8 --cpu-baseline 0 > gpurun_out/$TAG
 timeout -k 10 300 python bench.py --mode train --steps 10 --warmup 3 > gpurun_out/$TAG/bench_train.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $O/trace -o bench --output-format csv -- \
   python3 bench.py --steps 10 --warmup 3 --cpu-baseline 0 > $O/bench_under_rocprof.log 2>&1 || exit $?
-for K in conv9 lr lr4 attn conv1; do
+for K in conv9 lr lr4 attn conv1 fc qkv; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $C -T -d $O/pmc_${K}_$C -o pmc --output-format csv -- \
       python3 tools/kernel_probe.py $K --reps 10 > $O/pmc_${K}_$C.log 2>&1 || exit $?
