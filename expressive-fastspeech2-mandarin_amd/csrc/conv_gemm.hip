@@ -2170,7 +2170,16 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       const char *e = getenv("FS2_CONV_SHORTK");
       return e != nullptr ? atoi(e) : 0;
     }();
-    if (short_k && a.KS == 1 && a.Cin <= 256 && (int64_t)((a.M + 63) / 64) * ntn >= kTargetWGs)
+    static const int narrow = [] {  // FS2_CONV_NARROW=0: off (A/B)
+      const char *e = getenv("FS2_CONV_NARROW");
+      return e != nullptr ? atoi(e) : 1;
+    }();
+    if (narrow && GLd && ntn == 1 && nKd >= 32 && splitk_env() && a.sk_cnt != nullptr &&
+        (int64_t)((a.M + 127) / 128) >= 64)
+      // one N tile and a long K (PostNet's last conv: N = 80, K = 2560): 128-row tiles and the
+      // split-K tail fill the chip, instead of 32-row tiles that each stream the whole K
+      launch<CT, 2, 2, 4, 9, TIn>(a, s);
+    else if (short_k && a.KS == 1 && a.Cin <= 256 && (int64_t)((a.M + 63) / 64) * ntn >= kTargetWGs)
       launch<CT, 2, 2, 2, 9, TIn>(a, s);
     else if ((int64_t)((a.M + 127) / 128) * ntn >= kTargetWGs)
       launch<CT, 2, 2, 4, 9, TIn>(a, s);
