@@ -164,7 +164,7 @@ struct ConvArgs {
             // ablations: bit 2 no stores, bit 3 no residual loads, bit 4 no row reductions
   const float *colscale;    // fp8: per-column dequantisation scale of the accumulator (or NULL)
   float out_scale;          // out_dt == FS2_FP8: e4m3(y * out_scale)
-  void *out2;               // LN epilogues: optional fp8 copy e4m3(y * out2_scale), rows of N bytes
+  void *out2;               // optional copy, rows of N: LN epilogues e4m3(y * out2_scale), others bf16(y)
   float out2_scale;
   int cin_block;            // split-precision input: logical channel blocks of cin_block (0 = off)
   int cin_src[4];           // ... block i is source channel cin_src[i] of x
@@ -631,6 +631,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
       else
         *reinterpret_cast<uint2 *>(reinterpret_cast<fp8 *>(a.out) + o) =
             make_uint2(pack4_fp8(v, a.out_scale), pack4_fp8(v + 4, a.out_scale));
+      if (a.out2 != nullptr) store8(reinterpret_cast<bf16 *>(a.out2) + (int64_t)m * a.N + n, v);
     }
     return;
   }
@@ -664,6 +665,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
       for (int q = 0; q < 4; ++q) v[q] += rv[q];
     }
     store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, v, a.out_scale);
+    if (a.out2 != nullptr) store4(reinterpret_cast<bf16 *>(a.out2) + (int64_t)m * a.N + n, v);
   }
 }
 
@@ -2325,7 +2327,7 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
 
   hipStream_t s = as_stream(stream);
   if (d->x_dtype != FS2_BF16 && d->x_dtype != FS2_F32 && d->x_dtype != FS2_FP8) return FS2_EUNSUPPORTED;
-  if (d->out2 != nullptr && (!ln || epi == FS2_EPI_RELU_LN_DOT)) return FS2_EINVAL;
+  if (d->out2 != nullptr && (epi == FS2_EPI_RELU_LN_DOT || (!ln && d->out_split))) return FS2_EINVAL;
   if (d->KS > (ln ? 3 : 9)) return FS2_EUNSUPPORTED;
   const bool xb = d->x_dtype == FS2_BF16;
   if (d->compute == FS2_FP8)

@@ -19,6 +19,7 @@ allocates buffers and builds the two boolean mask tensors the 10-tuple returns. 
 without it, one device->host read of max(mel_len) sizes the decoder (the reference does
 B*L_max .item() syncs in LengthRegulator.expand).
 """
+import os
 from types import SimpleNamespace
 
 import numpy as np
@@ -289,9 +290,10 @@ def _stage2(P, g, st, T_out, T_dec, p_control):
         x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype,
                           out_layout=lay)
         x = _stack(P, P.dec_layers, x, None, layout=lay, timed=True)
+        mel_bf = _mel_copy(P, x, (lay.B, lay.T))
         mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
-                         out_dtype=L.FS2_F32, src_layout=lay)
-        return mel, _postnet(P, mel), st
+                         out_dtype=L.FS2_F32, src_layout=lay, out2=mel_bf)
+        return mel, _postnet(P, mel, mel_bf), st
     # LR gather with the decoder's position encoding fused (frame-level variance needs the bare
     # expanded x first, so the PE add moves to a second pass in that configuration)
     if frame_level:
@@ -309,9 +311,10 @@ def _stage2(P, g, st, T_out, T_dec, p_control):
     if T_dec != T_out:
         dec_lens = torch.clamp(dec_lens, max=T_dec)
     x = _stack(P, P.dec_layers, x, dec_lens, timed=True)
+    mel_bf = _mel_copy(P, x, x.shape[:2])
     mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
-                     out_dtype=L.FS2_F32)
-    return mel, _postnet(P, mel), st
+                     out_dtype=L.FS2_F32, out2=mel_bf)
+    return mel, _postnet(P, mel, mel_bf), st
 
 
 def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, max_src_len, mels, mel_lens,
@@ -396,10 +399,20 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     return (mel, postnet_mel, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)
 
 
-def _postnet(P, mel):
+def _mel_copy(P, x, bt):
+    """bf16 copy of mel_linear's output, written by the same epilogue (fs2_conv_desc.out2): PostNet's
+    first conv then reads bf16 through LDS-DMA instead of converting f32 in registers. The bf16
+    GEMM rounds its f32 input to bf16 the same way, so the conv's operands are unchanged."""
+    if P.compute != L.FS2_BF16 or os.environ.get("FS2_MEL_BF16", "1") == "0":
+        return None
+    return torch.empty(*bt, P.mel_w.shape[0], device=x.device, dtype=torch.bfloat16)
+
+
+def _postnet(P, mel, mel_bf=None):
     """PostNet (BN folded, transformer/Layers.py:92-137) + residual (fastspeech2.py:136), padded
-    [B, T, n_mel] like the reference: its padded frames (bias values) feed the k5 taps."""
-    y = mel
+    [B, T, n_mel] like the reference: its padded frames (bias values) feed the k5 taps. mel_bf:
+    optional bf16 copy of mel, the first conv's input (the residual stays f32)."""
+    y = mel if mel_bf is None else mel_bf
     n_pn = len(P.postnet)
     for i, lp in enumerate(P.postnet):
         if i < n_pn - 1:

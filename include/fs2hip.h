@@ -105,8 +105,10 @@ typedef struct fs2_conv_desc {
   const float *col_scale;   /* [N] dequantisation scale applied to the accumulator before the
                                bias (x scale * per-channel w scale), or NULL                    */
   float out_scale;          /* out_dtype == FS2_FP8: stored value = e4m3(y * out_scale)         */
-  void *out2;               /* LN epilogues: optional second output, e4m3(y * out2_scale),
-                               rows of N bytes (the fp8 copy the next fp8 GEMM reads)           */
+  void *out2;               /* optional second output, rows of N elements. LN epilogues:
+                               e4m3(y * out2_scale) (the fp8 copy the next fp8 GEMM reads);
+                               elementwise epilogues: bf16(y) (e.g. mel_linear's f32 output
+                               for the residual + its bf16 copy for PostNet's first conv)      */
   float out2_scale;
   /* split-precision (bf16x3) GEMM: the logical input channels are blocks of cin_block channels,
      block i read from source channel cin_src[i] of x (e.g. [x_hi | x_hi | x_lo] against packed

@@ -99,6 +99,34 @@ def test_conv1d_f32_input_bf16_compute_and_residual(ops, compute):
     assert _rel_err(out0, ref0) < _tol(compute)
 
 
+@pytest.mark.parametrize("B,T", [(3, 77), (64, 430)])
+def test_conv1d_bf16_out2_copy(ops, B, T):
+    """Elementwise epilogue with out2: f32 output + its bf16 copy (mel_linear -> PostNet). The copy
+    is bit-equal to bf16(out), and PostNet's first conv on the copy equals the conv on the f32 mel
+    (the bf16 GEMM rounds f32 inputs the same way)."""
+    L = _L()
+    g = torch.Generator().manual_seed(B + T)
+    x = torch.randn(B, T, 256, generator=g).to(DEV, torch.bfloat16)
+    w = torch.randn(80, 256, 1, generator=g) / 16
+    b = torch.randn(80, generator=g) * 0.1
+    wp = ops.pack_conv_weight(w.to(DEV), L.FS2_BF16)
+    cp = torch.empty(B, T, 80, device=DEV, dtype=torch.bfloat16)
+    mel = ops.conv1d(x, wp, b.to(DEV), cin=256, ks=1, pad=0, compute=L.FS2_BF16, epilogue=L.EPI_BIAS,
+                     out_dtype=L.FS2_F32, out2=cp)
+    torch.cuda.synchronize()
+    assert torch.equal(cp, mel.to(torch.bfloat16))
+    w0 = torch.randn(512, 80, 5, generator=g) / np.sqrt(400)
+    wp0 = ops.pack_conv_weight(w0.to(DEV), L.FS2_BF16)
+    b0 = (torch.randn(512, generator=g) * 0.1).to(DEV)
+    with ops.splitk_enabled(False):
+        ya = ops.conv1d(mel, wp0, b0, cin=80, ks=5, pad=2, compute=L.FS2_BF16, epilogue=L.EPI_BIAS_TANH,
+                        out_dtype=L.FS2_BF16)
+        yb = ops.conv1d(cp, wp0, b0, cin=80, ks=5, pad=2, compute=L.FS2_BF16, epilogue=L.EPI_BIAS_TANH,
+                        out_dtype=L.FS2_BF16)
+    torch.cuda.synchronize()
+    assert (ya.float() - yb.float()).abs().max().item() <= 1e-2, (ya.float() - yb.float()).abs().max().item()
+
+
 @pytest.mark.parametrize("compute", [0, 1])
 @pytest.mark.parametrize("B,T,Cin", [(5, 41, 256), (64, 401, 1024)])  # the 2nd routes to the 8-wave 128x256 tile
 def test_conv1d_res_ln_mask_addvec(ops, compute, B, T, Cin):

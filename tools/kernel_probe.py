@@ -79,9 +79,12 @@ def main():
         pl = P.postnet[1]
         fn = lambda: ops.conv1d(y, pl.w, pl.b, cin=512, ks=5, pad=2, compute=P.compute, epilogue=L.EPI_BIAS_TANH,
                                 out_dtype=P.act_dtype)
-    elif a.kernel in ("postnet_first", "postnet_last"):  # PostNet 80->512 (f32 mel in) / 512->80 + residual
+    elif a.kernel in ("postnet_first", "postnet_first_bf", "postnet_last"):
+        # PostNet 80->512 (f32 mel in, or its bf16 copy) / 512->80 + residual
         mel = torch.randn(B, T, 80, generator=g).to(dev)
-        if a.kernel == "postnet_first":
+        if a.kernel == "postnet_first_bf":
+            mel = mel.to(torch.bfloat16)
+        if a.kernel.startswith("postnet_first"):
             pl = P.postnet[0]
             fn = lambda: ops.conv1d(mel, pl.w, pl.b, cin=pl.cin, ks=pl.k, pad=pl.p, compute=P.compute,
                                     epilogue=L.EPI_BIAS_TANH, out_dtype=P.act_dtype)
