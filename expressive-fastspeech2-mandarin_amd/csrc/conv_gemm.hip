@@ -1194,6 +1194,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
 // A rows of each tap are DMA'd separately (row m0+r+tap-pad) with the sequence-boundary test on
 // the source offset (out of range -> zeros), so fragments need no masking. LDS: 2 x (A 32 KiB +
 // B 32 KiB) = 128 KiB, one __shared__ array; the epilogue reuses it one M half at a time.
+// SK = the stream-K tail (FS2_CONV_8PSK, opt-in): a separate instantiation, so the default kernel
+// carries none of its work-item bookkeeping (with it the kernel spilled 3 VGPRs to scratch).
+template <bool SK>
 __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   constexpr int BM = 256, BN = 256, KE = 64;
   constexpr int TILE = 256 * kRowBytes;  // 32 KiB: one operand of one k-tile
@@ -1217,7 +1220,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   // two tiles; a tile cut between ranges is summed by its last-arriving range (sc1 partials,
   // fixed range order) and that workgroup runs its epilogue.
   const int Ttot = a.row_split == 1 ? split_panels(a, M) * a.ntn : ((M + 255) / 256) * a.ntn;
-  const int S = a.sk_slots;
+  const int S = SK ? a.sk_slots : 0;
   const int R = S > 0 ? Ttot / S : 0, tail = S > 0 ? Ttot - R * S : 0;
   const int Sp = tail > 0 ? min(S, 4 * tail) : 0;
   const int dp = S > 0 ? R * S : Ttot;
@@ -1226,7 +1229,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   int it_tile[2], it_kb[2], it_ke[2], nitems = 0;
   int j = -1;  // stream-K range index
   int64_t b0 = 0;
-  if (id < dp) {
+  if (!SK) {
+    if (id >= Ttot) return;
+    it_tile[0] = xcd_remap(id, Ttot);
+    it_kb[0] = 0;
+    it_ke[0] = nK;
+    nitems = 1;
+  } else if (id < dp) {
     it_tile[0] = xcd_remap(id, dp);
     it_kb[0] = 0;
     it_ke[0] = nK;
@@ -1260,10 +1269,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   const int prow = lane >> 3, plc = (lane & 7) ^ ((lane >> 3) & 7);
   auto apiece = [&](int x, int i) { return 16 * (w >> 2) + 8 * x + 2 * (w & 3) + i; };
   auto bpiece = [&](int x, int i) { return (w & 3) * 8 + 4 * x + 2 * (w >> 2) + i; };
-  for (int item = 0; item < nitems; ++item) {
+  for (int item = 0; item < (SK ? nitems : 1); ++item) {
   const int tile = item == 0 ? it_tile[0] : it_tile[1];
-  const int kb = item == 0 ? it_kb[0] : it_kb[1];
-  const int ke = item == 0 ? it_ke[0] : it_ke[1];
+  const int kb = SK ? (item == 0 ? it_kb[0] : it_kb[1]) : 0;
+  const int ke = SK ? (item == 0 ? it_ke[0] : it_ke[1]) : nK;
   int m0, n0;
   tile_coords(a, tile, Ttot, BM, BN, m0, n0);
   int arow[2][2], apos[2][2], alen[2][2];
@@ -1439,7 +1448,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   if (wr == 0) bar();
   __syncthreads();
 
-  if (kb != 0 || ke != nK) {  // a stream-K tile cut between ranges: hand over / sum the partials
+  if (SK && (kb != 0 || ke != nK)) {  // a stream-K tile cut between ranges: hand over / sum the partials
     const int tt = tile - dp;
     const int64_t ts = (int64_t)tt * nK;
     const int jf = jof(ts), nseg = jof(ts + nK - 1) - jf + 1;
@@ -1577,7 +1586,11 @@ void launch_8p(ConvArgs a, hipStream_t s, bool stream_k = false) {
       nwg += S;  // the tail's ranges (ids past the whole rounds; unused ids exit)
     }
   }
-  if (nwg > 0) hipLaunchKernelGGL(conv_gemm_8p_kernel, dim3(nwg), dim3(512), 0, s, a);
+  if (nwg <= 0) return;
+  if (a.sk_slots > 0)
+    hipLaunchKernelGGL(conv_gemm_8p_kernel<true>, dim3(nwg), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL(conv_gemm_8p_kernel<false>, dim3(nwg), dim3(512), 0, s, a);
 }
 
 // ------------------------------------------------------------------------------------------------
