@@ -1196,9 +1196,15 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
 // B 32 KiB) = 128 KiB, one __shared__ array; the epilogue reuses it one M half at a time.
 // SK = the stream-K tail (FS2_CONV_8PSK, opt-in): a separate instantiation, so the default kernel
 // carries none of its work-item bookkeeping (with it the kernel spilled 3 VGPRs to scratch).
-template <bool SK>
+// HB = 16-row blocks per M half: 8 (256-row tiles) or 7 (224-row tiles: a launch whose 256-row
+// tiles leave part of its one round idle fills the round with more, shorter tiles; PostNet k=5 at
+// cfg2: 216 -> 246 tiles on 256 CUs). The LDS image keeps 128-row halves; rows 112..127 of each
+// half are DMA'd as zeros and skip their MFMAs.
+template <bool SK, int HB = 8>
 __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
-  constexpr int BM = 256, BN = 256, KE = 64;
+  static_assert(HB == 8 || HB == 7, "blocks per half");
+  static_assert(!SK || HB == 8, "stream-K uses 256-row tiles");
+  constexpr int BM = 32 * HB, HR = 16 * HB, BN = 256, KE = 64;
   constexpr int TILE = 256 * kRowBytes;  // 32 KiB: one operand of one k-tile
   constexpr int EPI_LD = BN + 4;
   constexpr int SMEM = (4 * TILE > 128 * EPI_LD * 4) ? 4 * TILE : 128 * EPI_LD * 4;
@@ -1219,7 +1225,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   // equal contiguous ranges, one per workgroup id R*S + j. Sp >= tail, so a range spans at most
   // two tiles; a tile cut between ranges is summed by its last-arriving range (sc1 partials,
   // fixed range order) and that workgroup runs its epilogue.
-  const int Ttot = a.row_split == 1 ? split_panels(a, M) * a.ntn : ((M + 255) / 256) * a.ntn;
+  const int Ttot = a.row_split == 1 ? split_panels(a, M) * a.ntn : ((M + BM - 1) / BM) * a.ntn;
   const int S = SK ? a.sk_slots : 0;
   const int R = S > 0 ? Ttot / S : 0, tail = S > 0 ? Ttot - R * S : 0;
   const int Sp = tail > 0 ? min(S, 4 * tail) : 0;
@@ -1257,7 +1263,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
     return;
   }
   // range that holds flattened k-tile k:  j(k) = ((k+1) * Sp - 1) / W
-  auto jof = [&](int64_t k) { return (int)(((k + 1) * Sp - 1) / W); };
+  auto jof = [&](int64_t k) { return (int)(((k + 1) * Sp - 1) / (W > 0 ? W : 1)); };
   const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
   const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * 2u;
@@ -1281,9 +1287,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int m = m0 + 8 * apiece(x, i) + prow;
+      const int hr = 8 * (apiece(x, i) - 16 * (w >> 2)) + prow;  // row within the M half
+      const int m = m0 + HR * (w >> 2) + hr;
       arow[x][i] = m;
-      if (m >= M) {
+      if (m >= M || hr >= HR) {
         apos[x][i] = 0;
         alen[x][i] = 0;  // every tap out of range -> zeros
       } else if (a.row_pos != nullptr) {
@@ -1331,7 +1338,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
 
   auto read_a = [&](const char *As, int mh) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < ((HB == 7 && mh == 1) ? 3 : 4); ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
         af[i][s] = *reinterpret_cast<const bf16x8 *>(As + aread[s] + (mh * 4 + i) * 16 * kRowBytes);
@@ -1348,7 +1355,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < ((HB == 7 && mh == 1) ? 3 : 4); ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[mh * 4 + i][nh * 2 + j] =
@@ -1453,7 +1460,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
     const int64_t ts = (int64_t)tt * nK;
     const int jf = jof(ts), nseg = jof(ts + nK - 1) - jf + 1;
     // partial slot of the range jj's piece of this tile: 2*jj (its first piece) or 2*jj + 1
-    auto slot = [&](int jj) { return 2 * jj + (((int64_t)jj * W / Sp) < ts ? 1 : 0); };
+    auto slot = [&](int jj) { return 2 * jj + (((int64_t)jj * W / max(Sp, 1)) < ts ? 1 : 0); };
     const rsrc_t pr = make_rsrc(a.sk_part, a.sk_part_bytes);
     auto pofs = [&](int sl, int mi, int ni) {
       return (uint32_t)sl * (uint32_t)(BM * BN * 4) + (uint32_t)(((mi * 4 + ni) * 512 + tid) * 16);
@@ -1504,7 +1511,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   for (int h = 0; h < 2; ++h) {
     if (wr == h) {
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
+      for (int mi = 0; mi < HB; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
@@ -1512,7 +1519,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
             E[(mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
     }
     __syncthreads();
-    epilogue<128, BN, 8, false>(a, E, m0 + h * 128, n0, tid, M);  // never an LN epilogue
+    // never an LN epilogue; rows bounded by the half (HB == 7: 112 rows)
+    epilogue<128, BN, 8, false>(a, E, m0 + h * HR, n0, tid, HB == 8 ? M : min(M, m0 + h * HR + HR));
     __syncthreads();
   }
   }  // work items
@@ -1571,9 +1579,14 @@ int num_cus() {
   return cache[dev];
 }
 
-void launch_8p(ConvArgs a, hipStream_t s, bool stream_k = false) {
+void launch_8p(ConvArgs a, hipStream_t s, bool stream_k = false, bool rows224 = false) {
   a.ntn = (a.N + 255) / 256;
   a.ngr = a.ntn;
+  if (rows224 && !stream_k && a.row_split == 0) {
+    const int nwg = ((a.M + 223) / 224) * a.ntn;
+    if (nwg > 0) hipLaunchKernelGGL((conv_gemm_8p_kernel<false, 7>), dim3(nwg), dim3(512), 0, s, a);
+    return;
+  }
   int nwg = ((a.M + 255) / 256) * a.ntn;
   if (a.row_split == 1) nwg = nwg / a.split_slots * a.split_slots;  // whole rounds (device M <= a.M)
   a.sk_slots = 0;
@@ -2099,7 +2112,14 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
     }
     if (phased && !ln && a.KS >= 4 && a.N >= 256 && tiles256 >= 192 && S > 0) {
       if (tiles256 <= S) {  // at most one round: the phased kernel alone
-        launch_8p(a, s);
+        // 224-row tiles when they still fit the one round (shorter tiles, more CUs busy);
+        // FS2_CONV_8P224=0: off
+        static const bool r224 = [] {
+          const char *e = getenv("FS2_CONV_8P224");
+          return e == nullptr || e[0] != '0';
+        }();
+        const int64_t tiles224 = (int64_t)((a.M + 223) / 224) * ((a.N + 255) / 256);
+        launch_8p(a, s, false, r224 && tiles224 <= S);
         return;
       }
       // FS2_CONV_8PSK=1 (opt-in): stream-K over the tail tiles in the phased launch itself. Correct
