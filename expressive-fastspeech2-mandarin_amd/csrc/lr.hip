@@ -251,12 +251,63 @@ __global__ __launch_bounds__(256) void seq_rows_kernel(const int32_t *__restrict
   if (row_pos != nullptr && t < len) row_pos[c + t] = make_int2(t, len);
 }
 
+// The two launches above as one (B <= kSeqMaxB): every workgroup recomputes cu[0..B] in LDS
+// (clamped lengths, wave shuffle scan; B = 64 costs nothing) and writes its 256 padded frames;
+// workgroup 0 also stores cu. One tiny launch less per layout.
+constexpr int kSeqMaxB = 4096;
+__global__ __launch_bounds__(256) void seq_layout_kernel(const int64_t *__restrict__ lens, int B, int T,
+                                                         int32_t *__restrict__ cu, int2 *__restrict__ row_pos,
+                                                         int32_t *__restrict__ rowmap) {
+  __shared__ int32_t scu[kSeqMaxB + 1];
+  __shared__ int32_t wsum[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int per = (B + 255) / 256;
+  const int i0 = min(tid * per, B), i1 = min(i0 + per, B);
+  auto clen = [&](int i) {
+    const int64_t l = lens[i];
+    return (int32_t)(l < 0 ? 0 : (l > T ? T : l));
+  };
+  int32_t local = 0;
+  for (int i = i0; i < i1; ++i) local += clen(i);
+  int32_t v = local;  // inclusive scan over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) wsum[wv] = v;
+  __syncthreads();
+  int32_t run = v - local;
+  for (int w = 0; w < wv; ++w) run += wsum[w];
+  for (int i = i0; i < i1; ++i) {
+    scu[i] = run;
+    run += clen(i);
+  }
+  if (tid == 0) scu[B] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int i = tid; i <= B; i += 256) cu[i] = scu[i];
+  const int64_t i = (int64_t)blockIdx.x * 256 + tid;
+  if (i >= (int64_t)B * T) return;
+  const int b = (int)(i / T), t = (int)(i - (int64_t)b * T);
+  const int c = scu[b], len = scu[b + 1] - c;
+  if (rowmap != nullptr) rowmap[i] = t < len ? c + t : -1;
+  if (row_pos != nullptr && t < len) row_pos[c + t] = make_int2(t, len);
+}
+
 }  // namespace
 
 extern "C" int fs2_seq_layout(const int64_t *lens, int B, int T, int32_t *cu, int32_t *row_pos, int32_t *rowmap,
                               fs2_stream_t stream) {
   if (lens == nullptr || cu == nullptr || B < 0 || T < 0 || (int64_t)B * T > 0x7fffff00LL) return FS2_EINVAL;
   hipStream_t s = as_stream(stream);
+  if (B <= kSeqMaxB) {
+    const int64_t n = (int64_t)B * T;
+    hipLaunchKernelGGL(seq_layout_kernel, dim3((unsigned)(n > 0 ? (n + 255) / 256 : 1)), dim3(256), 0, s, lens, B, T,
+                       cu, reinterpret_cast<int2 *>(row_pos), rowmap);
+    FS2_CHECK_LAUNCH();
+    return FS2_OK;
+  }
   hipLaunchKernelGGL(seq_cu_kernel, dim3(1), dim3(256), 0, s, lens, B, T, cu);
   FS2_CHECK_LAUNCH();
   if ((rowmap != nullptr || row_pos != nullptr) && (int64_t)B * T > 0) {

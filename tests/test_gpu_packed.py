@@ -51,10 +51,20 @@ def _valid(lens, T):
     return (torch.arange(T, device=DEV)[None, :] < torch.tensor(lens, device=DEV)[:, None])
 
 
-def test_seq_layout(gpu):
+@pytest.mark.parametrize("case", ["fixed", "b300", "t1", "b5000"])
+def test_seq_layout(gpu, case):
+    """One-launch layout (B <= 4096; every workgroup rescans the lengths) and the two-launch
+    fallback (B = 5000)."""
     ops, _ = gpu
-    T = 130
-    lens = LENS + [-3, 500]  # clamped to [0, T]
+    rng = np.random.default_rng(len(case))
+    if case == "fixed":
+        T, lens = 130, LENS + [-3, 500]  # clamped to [0, T]
+    elif case == "b300":
+        T, lens = 37, rng.integers(-2, 45, 300).tolist()
+    elif case == "t1":
+        T, lens = 1, rng.integers(0, 3, 700).tolist()
+    else:
+        T, lens = 3, rng.integers(0, 5, 5000).tolist()
     lens_t, lay = _layout(ops, lens, T)
     cl = np.clip(np.array(lens), 0, T)
     cu = np.concatenate([[0], np.cumsum(cl)])

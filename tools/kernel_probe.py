@@ -93,6 +93,11 @@ def main():
             pl = P.postnet[-1]
             fn = lambda: ops.conv1d(y, pl.w, pl.b, cin=pl.cin, ks=pl.k, pad=pl.p, compute=P.compute,
                                     epilogue=L.EPI_BIAS_RES, out_dtype=L.FS2_F32, residual=mel)
+    elif a.kernel == "cond":  # speaker + emotion/arousal/valence conditioning vectors
+        fn = lambda: ops.cond_vectors(b["speakers"], P.spk_table, b["emotions"], b["arousals"], b["valences"],
+                                      P.emo_table, P.aro_table, P.val_table, P.emo_w, P.emo_b, P.d_model)
+    elif a.kernel == "layout":  # packed-sequence layout of the decoder frames
+        fn = lambda: ops.SeqLayout(lens, T)
     elif a.kernel in ("enc_conv9", "enc_ln", "vp"):
         Be, Le = 64, 64
         xe = rnd(Be, Le, 256)
