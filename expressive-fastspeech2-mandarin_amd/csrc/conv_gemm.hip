@@ -2176,7 +2176,13 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         }
       }
       const int nKd = a.KS * (a.Cin_pad / CTraits<CT>::KE);
-      if (a.M >= 192 * 128)
+      static const bool bm112 = [] {
+        const char *e = getenv("FS2_LN_BM112");
+        return e != nullptr && e[0] == '1';
+      }();
+      if (a.M >= 192 * 128 && bm112 && (a.M + 111) / 112 <= num_cus())
+        launch_ring<CT, 1, 7, 3>(a, s);  // 112 x 256, 4 waves, 3 stages: one round of more, shorter tiles
+      else if (a.M >= 192 * 128)
         launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages (144 KiB)
       else if (skpref_env() && splitk_env() && a.sk_cnt != nullptr && nKd >= 8)
         // small M (encoder / variance predictors, M = B*L ~ 4k): 64-row tiles and split-K fill the
