@@ -1624,10 +1624,15 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int CT, int WGM, int WMI, int NS>
-__global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a) {
-  constexpr int WGN = 4, NW = WGM * WGN;
-  constexpr int WROWS = 16 * WMI, BM = WROWS * WGM, BN = 64 * WGN;
+// WGN = waves across the 256 columns: 4 (64 columns each) or 8 (32 each: two waves per SIMD on
+// the 16-row small-M tiles); split-K only with 4. (16 waves of 16 columns: one LN row per wave,
+// i.e. the single-row LN epilogue on 16-row tiles and the paired one on 32-row tiles, which
+// breaks the packed == padded bit-exactness; not offered.)
+template <int CT, int WGM, int WMI, int NS, int WGN = 4>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvArgs a) {
+  static_assert(WGN == 4 || WGN == 8, "column waves");
+  constexpr int NW = WGM * WGN, WCOL = 256 / WGN, NI = WCOL / 16;
+  constexpr int WROWS = 16 * WMI, BM = WROWS * WGM, BN = 256;
   constexpr int KE = CTraits<CT>::KE, CE = CTraits<CT>::CE;
   using TW = typename CTraits<CT>::T;
   constexpr int AP = BM / 8, BP = BN / 8;               // 1 KiB pieces per stage
@@ -1702,31 +1707,31 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
     for (int i = 0; i < BQ; ++i) glds(wr_, Bs + (wid + NW * i) * 1024, boff[i] == kOOB ? kOOB : boff[i] + off);
   };
 
-  f32x4 acc[WMI][4];
+  f32x4 acc[WMI][NI];
 #pragma unroll
   for (int i = 0; i < WMI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int aread0 = lds_off(wr * WROWS + (lane & 15), lane >> 4);
   const int aread1 = lds_off(wr * WROWS + (lane & 15), 4 + (lane >> 4));
-  const int bread0 = lds_off(wc * 64 + (lane & 15), lane >> 4);
-  const int bread1 = lds_off(wc * 64 + (lane & 15), 4 + (lane >> 4));
+  const int bread0 = lds_off(wc * WCOL + (lane & 15), lane >> 4);
+  const int bread1 = lds_off(wc * WCOL + (lane & 15), 4 + (lane >> 4));
   auto compute = [&](const char *S) {
     const char *As = S;
     const char *Bs = S + AP * 1024;
     if constexpr (CT == FS2_FP8) {
       const int g2 = 2 * (lane >> 4);
       const char *A0 = As + lds_off(wr * WROWS + (lane & 15), g2), *A1 = As + lds_off(wr * WROWS + (lane & 15), g2 + 1);
-      const char *B0 = Bs + lds_off(wc * 64 + (lane & 15), g2), *B1 = Bs + lds_off(wc * 64 + (lane & 15), g2 + 1);
-      i32x8 af[WMI], bfr[4];
+      const char *B0 = Bs + lds_off(wc * WCOL + (lane & 15), g2), *B1 = Bs + lds_off(wc * WCOL + (lane & 15), g2 + 1);
+      i32x8 af[WMI], bfr[NI];
 #pragma unroll
       for (int mi = 0; mi < WMI; ++mi) af[mi] = frag_fp8(A0 + mi * 16 * kRowBytes, A1 + mi * 16 * kRowBytes);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) bfr[ni] = frag_fp8(B0 + ni * 16 * kRowBytes, B1 + ni * 16 * kRowBytes);
+      for (int ni = 0; ni < NI; ++ni) bfr[ni] = frag_fp8(B0 + ni * 16 * kRowBytes, B1 + ni * 16 * kRowBytes);
 #pragma unroll
       for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma_fp8(af[mi], bfr[ni], acc[mi][ni]);
+        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = mfma_fp8(af[mi], bfr[ni], acc[mi][ni]);
       return;
     }
 #pragma unroll
@@ -1734,28 +1739,28 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
       const char *Ab = As + (s ? aread1 : aread0);
       const char *Bb = Bs + (s ? bread1 : bread0);
       if constexpr (CT == FS2_BF16) {
-        bf16x8 af[WMI], bfr[4];
+        bf16x8 af[WMI], bfr[NI];
 #pragma unroll
         for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const bf16x8 *>(Ab + mi * 16 * kRowBytes);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) bfr[ni] = *reinterpret_cast<const bf16x8 *>(Bb + ni * 16 * kRowBytes);
+        for (int ni = 0; ni < NI; ++ni) bfr[ni] = *reinterpret_cast<const bf16x8 *>(Bb + ni * 16 * kRowBytes);
 #pragma unroll
         for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
+          for (int ni = 0; ni < NI; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
       } else {
-        f32x4 af[WMI], bfr[4];
+        f32x4 af[WMI], bfr[NI];
 #pragma unroll
         for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const f32x4 *>(Ab + mi * 16 * kRowBytes);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) bfr[ni] = *reinterpret_cast<const f32x4 *>(Bb + ni * 16 * kRowBytes);
+        for (int ni = 0; ni < NI; ++ni) bfr[ni] = *reinterpret_cast<const f32x4 *>(Bb + ni * 16 * kRowBytes);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+            for (int ni = 0; ni < NI; ++ni)
               acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi][j], bfr[ni][j], acc[mi][ni], 0, 0, 0);
       }
     }
@@ -1797,19 +1802,21 @@ __global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_ring_kernel(ConvArgs a
     ibuf = ibuf == NS - 1 ? 0 : ibuf + 1;
   }
   __syncthreads();
-  if (nseg > 1) {
-    static_assert(BM * BN * 4 == 256 * WGM * WMI * 4 * 16, "partial tile layout");
-    if (!splitk_fixup<WMI, 256 * WGM>(a, acc, tl, seg, nseg, tid, reinterpret_cast<int *>(smem + SMEM))) return;
+  if constexpr (WGN == 4) {
+    if (nseg > 1) {
+      static_assert(BM * BN * 4 == 256 * WGM * WMI * 4 * 16, "partial tile layout");
+      if (!splitk_fixup<WMI, 256 * WGM>(a, acc, tl, seg, nseg, tid, reinterpret_cast<int *>(smem + SMEM))) return;
+    }
   }
 
   float *E = reinterpret_cast<float *>(smem);
 #pragma unroll
   for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
+    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
+        E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * WCOL + ni * 16 + (lane & 15)] = acc[mi][ni][j];
   __syncthreads();
   if (a.dbg & 2) return;
   epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
@@ -2013,7 +2020,7 @@ void launch_rb(ConvArgs a, hipStream_t s) {
   hipLaunchKernelGGL((conv_gemm_rb_kernel<CT, WGM, WMI, NA, PB>), dim3(nwg), dim3(256 * WGM), 0, s, a);
 }
 
-template <int CT, int WGM, int WMI, int NS>
+template <int CT, int WGM, int WMI, int NS, int WGN = 4>
 void launch_ring(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM;
   a.ntn = (a.N + 255) / 256;
@@ -2026,7 +2033,7 @@ void launch_ring(ConvArgs a, hipStream_t s) {
     const int nK = a.KS * (a.Cin_pad / CTraits<CT>::KE);
     const int64_t need = kSkCntBytes + (int64_t)slots * BM * 256 * 4;
     const int sk_max = nK / 4 < 4 ? nK / 4 : 4;
-    if (splitk_env() && sk_would_split(nwg, slots, sk_max) && a.sk_cnt != nullptr && a.sk_ws_bytes >= need &&
+    if (WGN == 4 && splitk_env() && sk_would_split(nwg, slots, sk_max) && a.sk_cnt != nullptr && a.sk_ws_bytes >= need &&
         nK >= 8 && slots > 0 && slots * 4 <= kSkCntBytes) {
       a.sk_slots = slots;
       a.sk_max = sk_max;
@@ -2034,7 +2041,7 @@ void launch_ring(ConvArgs a, hipStream_t s) {
       nwg += slots;
     }
   }
-  hipLaunchKernelGGL((conv_gemm_ring_kernel<CT, WGM, WMI, NS>), dim3(nwg), dim3(256 * WGM), 0, s, a);
+  hipLaunchKernelGGL((conv_gemm_ring_kernel<CT, WGM, WMI, NS, WGN>), dim3(nwg), dim3(64 * WGM * WGN), 0, s, a);
 }
 
 template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, int NSB = 2>
@@ -2176,6 +2183,12 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         }
       }
       const int nKd = a.KS * (a.Cin_pad / CTraits<CT>::KE);
+      // 8 column waves on the small-M tiles (FS2_LN_W8=0: 4): the second wave per SIMD overlaps
+      // LDS reads with the partner's MFMAs (encoder LN 14.5 -> 13.2 us, VP 50.8 -> 48.6 us)
+      static const bool w8 = [] {
+        const char *e = getenv("FS2_LN_W8");
+        return e == nullptr || e[0] != '0';
+      }();
       static const bool bm112 = [] {
         const char *e = getenv("FS2_LN_BM112");
         return e != nullptr && e[0] == '1';
@@ -2190,9 +2203,11 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         // its K range of the whole weight matrix)
         launch_ring<CT, 1, 4, 3>(a, s);  // 64 x 256, 4 waves, 3 stages (120 KiB)
       else if (a.M >= 8192)
-        launch_ring<CT, 1, 2, 4>(a, s);  // 32 x 256, 4 waves, 4 stages
+        w8 ? launch_ring<CT, 1, 2, 4, 8>(a, s)  // 32 x 256, 8 waves of 32 x 32, 4 stages
+           : launch_ring<CT, 1, 2, 4>(a, s);    // 32 x 256, 4 waves of 32 x 64
       else
-        launch_ring<CT, 1, 1, 4>(a, s);  // 16 x 256, 4 waves, 4 stages
+        w8 ? launch_ring<CT, 1, 1, 4, 8>(a, s)  // 16 x 256, 8 waves of 16 x 32, 4 stages
+           : launch_ring<CT, 1, 1, 4>(a, s);    // 16 x 256, 4 waves of 16 x 64
       return;
     }
   }
