@@ -2189,12 +2189,20 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         const char *e = getenv("FS2_LN_W8");
         return e == nullptr || e[0] != '0';
       }();
+      // 16 waves (2 x 8 of 64 x 32) on the decoder's 128-row tiles, 4 per SIMD (FS2_LN_W16DEC=0:
+      // 8 waves of 64 x 64): fc + LN 18.4 -> 16.6 us, conv-k1 + LN 31.9 -> 28.5 us
+      static const bool w16d = [] {
+        const char *e = getenv("FS2_LN_W16DEC");
+        return e == nullptr || e[0] != '0';
+      }();
       static const bool bm112 = [] {
         const char *e = getenv("FS2_LN_BM112");
         return e != nullptr && e[0] == '1';
       }();
       if (a.M >= 192 * 128 && bm112 && (a.M + 111) / 112 <= num_cus())
         launch_ring<CT, 1, 7, 3>(a, s);  // 112 x 256, 4 waves, 3 stages: one round of more, shorter tiles
+      else if (a.M >= 192 * 128 && w16d)
+        launch_ring<CT, 2, 4, 3, 8>(a, s);  // 128 x 256, 16 waves of 64 x 32, 3 stages
       else if (a.M >= 192 * 128)
         launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages (144 KiB)
       else if (skpref_env() && splitk_env() && a.sk_cnt != nullptr && nKd >= 8)
