@@ -677,18 +677,18 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
 // counter, acquires, and sums the partials in segment order (deterministic; its own segment from
 // registers) with sc1 loads. Returns false for the other segments (they are done). `flag` is a
 // word inside the kernel's one LDS array.
-template <int WMI, int NT>
-__device__ __forceinline__ bool splitk_fixup(const ConvArgs &a, f32x4 (&acc)[WMI][4], int tl, int seg, int nseg,
+template <int WMI, int NT, int NI = 4>
+__device__ __forceinline__ bool splitk_fixup(const ConvArgs &a, f32x4 (&acc)[WMI][NI], int tl, int seg, int nseg,
                                              int tid, int *flag) {
   const rsrc_t pr = make_rsrc(a.sk_part, a.sk_part_bytes);
-  constexpr uint32_t tile_bytes = (uint32_t)(NT * WMI * 4 * 16);
+  constexpr uint32_t tile_bytes = (uint32_t)(NT * WMI * NI * 16);
   auto pofs = [&](int sg, int mi, int ni) {
-    return (uint32_t)(tl * nseg + sg) * tile_bytes + (uint32_t)(((mi * 4 + ni) * NT + tid) * 16);
+    return (uint32_t)(tl * nseg + sg) * tile_bytes + (uint32_t)(((mi * NI + ni) * NT + tid) * 16);
   };
 #pragma unroll
   for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
+    for (int ni = 0; ni < NI; ++ni)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc[mi][ni]),
                                              pr, pofs(seg, mi, ni), 0, 16);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -705,16 +705,16 @@ __device__ __forceinline__ bool splitk_fixup(const ConvArgs &a, f32x4 (&acc)[WMI
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (!*flag) return false;
-  f32x4 tot[WMI][4];
+  f32x4 tot[WMI][NI];
 #pragma unroll
   for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) tot[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ni = 0; ni < NI; ++ni) tot[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int sg = 0; sg < nseg; ++sg) {
 #pragma unroll
     for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
+      for (int ni = 0; ni < NI; ++ni) {
         f32x4 p = acc[mi][ni];
         if (sg != seg) p = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, pofs(sg, mi, ni), 0, 16));
         tot[mi][ni] += p;
@@ -723,7 +723,7 @@ __device__ __forceinline__ bool splitk_fixup(const ConvArgs &a, f32x4 (&acc)[WMI
 #pragma unroll
   for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = tot[mi][ni];
+    for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = tot[mi][ni];
   return true;
 }
 
@@ -770,11 +770,14 @@ __device__ __forceinline__ bf16x8 shift_rows(bf16x8 cur, bf16x8 nxt) {
 // vmcnt(0) per step. NSB > 2 (tall tiles, KS >= NSB): B of step k+NSB-1 is issued right after
 // the barrier that retires step k-1, the next channel block's A halo at tap 0 of the current one
 // (KS-1 steps ahead), and each step waits with a counted vmcnt for its own B only.
-template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, bool GL, int NSB = 2>
-__global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv_gemm_kernel(ConvArgs a) {
+// WCOL = columns per wave: 64 (4 MFMA blocks) or 32 (2x the waves for the same tile: 8-wave
+// 128 x 128, two workgroups and four waves per SIMD).
+template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, bool GL, int NSB = 2, int WCOL = 64>
+__global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 ? 4 : 1)) void conv_gemm_kernel(ConvArgs a) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;  // waves / threads per workgroup (4 or 8)
   constexpr int WROWS = 16 * WMI;
-  constexpr int BM = WROWS * WGM, BN = 64 * WGN;
+  constexpr int BM = WROWS * WGM, BN = WCOL * WGN, NI = WCOL / 16;
+  static_assert(WCOL == 64 || WCOL == 32, "columns per wave");
   constexpr int KE = CTraits<CT>::KE, CE = CTraits<CT>::CE;
   using TW = typename CTraits<CT>::T;
   constexpr int HMAX0 = BM + KSMAX - 1;
@@ -856,8 +859,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
   // LDS fragment-read bases: a 16-row step keeps (row & 7), so the swizzle is the same for
   // every mi / ni block and the block offset is an immediate.
   const int arow0 = wr * WROWS + (lane & 15);
-  const int bread0 = lds_off(wc * 64 + (lane & 15), lane >> 4);
-  const int bread1 = lds_off(wc * 64 + (lane & 15), 4 + (lane >> 4));
+  const int bread0 = lds_off(wc * WCOL + (lane & 15), lane >> 4);
+  const int bread1 = lds_off(wc * WCOL + (lane & 15), 4 + (lane >> 4));
 
   Stage<CT, TIn> sa[A_CH];        // A halo of the next channel block (issued at its tap 0)
   Stage<CT, TW> sb0[B_CH], sb1[B_CH];  // 2-deep ring of B (weight) tiles: step k lives in sb[k & 1]
@@ -896,16 +899,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
     for (int j = 0; j < B_CH; ++j) *reinterpret_cast<uint4 *>(Bs + lds_off(srow + RPP * j, schunk)) = sb[j].chunk();
   };
 
-  f32x4 acc[WMI][4];
+  f32x4 acc[WMI][NI];
 #pragma unroll
   for (int i = 0; i < WMI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int bf8_0 = lds_off(wc * 64 + (lane & 15), 2 * (lane >> 4));
-  const int bf8_1 = lds_off(wc * 64 + (lane & 15), 2 * (lane >> 4) + 1);
+  const int bf8_0 = lds_off(wc * WCOL + (lane & 15), 2 * (lane >> 4));
+  const int bf8_1 = lds_off(wc * WCOL + (lane & 15), 2 * (lane >> 4) + 1);
   // persistent A fragments for the tap-to-tap row shift (bf16, LDS-DMA path)
-  constexpr bool ASH = CT == FS2_BF16 && GL && KSMAX > 1;
+  constexpr bool ASH = CT == FS2_BF16 && GL && KSMAX > 1 && WCOL == 64;  // (register budget at WCOL 32)
   const bool ashift = ASH && a.ashift && KS > 1;
   bf16x8 Fs[2][WMI];
   auto compute = [&](int aslot, int tap, const char *Bs, bool fresh) {
@@ -918,7 +921,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
     if constexpr (CT == FS2_FP8) {
       const char *A0 = As + lds_off(arow0 + tap, 2 * (lane >> 4));
       const char *A1 = As + lds_off(arow0 + tap, 2 * (lane >> 4) + 1);
-      i32x8 af[WMI], bfr[4];
+      i32x8 af[WMI], bfr[NI];
 #pragma unroll
       for (int mi = 0; mi < WMI; ++mi) af[mi] = frag_fp8(A0 + mi * 16 * kRowBytes, A1 + mi * 16 * kRowBytes);
       if (need_mask) {
@@ -927,11 +930,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
           if (!vrow[mi]) af[mi] = i32x8{};
       }
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) bfr[ni] = frag_fp8(Bs + bf8_0 + ni * 16 * kRowBytes, Bs + bf8_1 + ni * 16 * kRowBytes);
+      for (int ni = 0; ni < NI; ++ni) bfr[ni] = frag_fp8(Bs + bf8_0 + ni * 16 * kRowBytes, Bs + bf8_1 + ni * 16 * kRowBytes);
 #pragma unroll
       for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma_fp8(af[mi], bfr[ni], acc[mi][ni]);
+        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = mfma_fp8(af[mi], bfr[ni], acc[mi][ni]);
       return;
     }
 #pragma unroll
@@ -939,7 +942,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
       const char *Ab = As + lds_off(arow0 + tap, s * 4 + (lane >> 4));
       const char *Bb = Bs + (s ? bread1 : bread0);
       if constexpr (CT == FS2_BF16) {
-        bf16x8 af[WMI], bfr[4];
+        bf16x8 af[WMI], bfr[NI];
         if (ASH && ashift) {
           if (fresh) {
 #pragma unroll
@@ -963,14 +966,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
             if (!vrow[mi]) af[mi] = bf16x8{};
         }
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) bfr[ni] = *reinterpret_cast<const bf16x8 *>(Bb + ni * 16 * kRowBytes);
+        for (int ni = 0; ni < NI; ++ni) bfr[ni] = *reinterpret_cast<const bf16x8 *>(Bb + ni * 16 * kRowBytes);
 #pragma unroll
         for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
+          for (int ni = 0; ni < NI; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
       } else {
-        f32x4 af[WMI], bfr[4];
+        f32x4 af[WMI], bfr[NI];
 #pragma unroll
         for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const f32x4 *>(Ab + mi * 16 * kRowBytes);
         if (need_mask) {
@@ -979,13 +982,13 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
             if (!vrow[mi]) af[mi] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) bfr[ni] = *reinterpret_cast<const f32x4 *>(Bb + ni * 16 * kRowBytes);
+        for (int ni = 0; ni < NI; ++ni) bfr[ni] = *reinterpret_cast<const f32x4 *>(Bb + ni * 16 * kRowBytes);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+            for (int ni = 0; ni < NI; ++ni)
               acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi][j], bfr[ni][j], acc[mi][ni], 0, 0, 0);
       }
     }
@@ -1155,8 +1158,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
 
   if constexpr (GL) {
     if (nseg > 1) {  // split-K tail segment: hand the partial tile over (conv_tile_sk)
-      static_assert(BM * BN * 4 == NT * WMI * 4 * 16, "partial tile layout");
-      if (!splitk_fixup<WMI, NT>(a, acc, tl, seg, nseg, tid, reinterpret_cast<int *>(smem + SMEM))) return;
+      static_assert(BM * BN * 4 == NT * WMI * NI * 16, "partial tile layout");
+      if (!splitk_fixup<WMI, NT, NI>(a, acc, tl, seg, nseg, tid, reinterpret_cast<int *>(smem + SMEM))) return;
     }
   }
 
@@ -1165,13 +1168,13 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : 1) void conv
 #pragma unroll
   for (int mi = 0; mi < WMI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
+    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
+        E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * WCOL + ni * 16 + (lane & 15)] = acc[mi][ni][j];
   __syncthreads();
 
-  epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
+  epilogue<BM, BN, NW, WCOL == 64>(a, E, m0, n0, tid, M);  // WCOL 32: plain epilogues only (launch_128)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2044,9 +2047,9 @@ void launch_ring(ConvArgs a, hipStream_t s) {
   hipLaunchKernelGGL((conv_gemm_ring_kernel<CT, WGM, WMI, NS, WGN>), dim3(nwg), dim3(64 * WGM * WGN), 0, s, a);
 }
 
-template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, int NSB = 2>
+template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, int NSB = 2, int WCOL = 64>
 void launch(ConvArgs a, hipStream_t s) {
-  constexpr int BM = 16 * WMI * WGM, BN = 64 * WGN;
+  constexpr int BM = 16 * WMI * WGM, BN = WCOL * WGN;
   constexpr bool GL = std::is_same<TIn, typename CTraits<CT>::T>::value;  // LDS-DMA needs no conversion
   a.ntn = (a.N + BN - 1) / BN;
   a.ngr = a.ntn;
@@ -2073,7 +2076,7 @@ void launch(ConvArgs a, hipStream_t s) {
     constexpr int HMX = ((BM + KSMAX - 1) + 7) / 8 * 8;
     constexpr int STG = 2 * HMX * kRowBytes + NSB * BN * kRowBytes;
     constexpr int SMB = (STG > BM * (BN + 4) * 4 ? STG : BM * (BN + 4) * 4) + 16;
-    constexpr int PER_CU = (WGM * WGN == 4) ? (163840 / SMB >= 2 ? 2 : 1) : 1;
+    constexpr int PER_CU = (WGM * WGN == 4 || WCOL == 32) ? (163840 / SMB >= 2 ? 2 : 1) : 1;
     const int slots = num_cus() * PER_CU;
     const int nK = a.KS * (a.Cin_pad / CTraits<CT>::KE);
     const int64_t need = kSkCntBytes + (int64_t)slots * BM * BN * 4;
@@ -2089,13 +2092,28 @@ void launch(ConvArgs a, hipStream_t s) {
       nwg += slots;  // spare ids for the tail segments (exit when unused)
     }
   }
-  hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, WMI, KSMAX, TIn, GL, GL ? NSB : 2>), dim3(nwg), dim3(64 * WGM * WGN),
-                     0, s, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, WMI, KSMAX, TIn, GL, GL ? NSB : 2, WCOL>), dim3(nwg),
+                     dim3(64 * WGM * WGN), 0, s, a);
 }
 
 // Row-tile choice: the largest tile that still gives >= 2 workgroups per CU (256 CUs), so the
 // small-M launches (encoder / variance predictors, M = B*L ~ 4k) fill the chip.
 constexpr int kTargetWGs = 512;
+
+// 128 x 128 tiles: 8 waves of 64 x 32 (two workgroups and four waves per SIMD, as the LayerNorm
+// ring kernels gained from: Q|K|V 28.7 -> 24.9 us, PostNet's last conv 41.6 -> 35.9 us, conv-k9
+// rows left -4 %), or with FS2_CONV_W8=0 the round-1 4 waves of 64 x 64
+template <int CT, typename TIn>
+void launch_128(ConvArgs a, hipStream_t s) {
+  static const bool w8 = [] {
+    const char *e = getenv("FS2_CONV_W8");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (w8)
+    launch<CT, 2, 4, 4, 9, TIn, 2, 32>(a, s);
+  else
+    launch<CT, 2, 2, 4, 9, TIn>(a, s);
+}
 
 template <int CT, typename TIn>
 void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
@@ -2151,7 +2169,7 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       if (deepb_env() >= 2 && a.KS >= 3)
         launch<CT, 2, 2, 4, 9, TIn, 3>(a2, s);
       else
-        launch<CT, 2, 2, 4, 9, TIn>(a2, s);
+        launch_128<CT, TIn>(a2, s);
       return;
     }
   }
@@ -2242,14 +2260,14 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         (int64_t)((a.M + 127) / 128) >= 64)
       // one N tile and a long K (PostNet's last conv: N = 80, K = 2560): 128-row tiles and the
       // split-K tail fill the chip, instead of 32-row tiles that each stream the whole K
-      launch<CT, 2, 2, 4, 9, TIn>(a, s);
+      launch_128<CT, TIn>(a, s);
     else if (short_k && a.KS == 1 && a.Cin <= 256 && (int64_t)((a.M + 63) / 64) * ntn >= kTargetWGs)
       launch<CT, 2, 2, 2, 9, TIn>(a, s);
     else if ((int64_t)((a.M + 127) / 128) * ntn >= kTargetWGs)
-      launch<CT, 2, 2, 4, 9, TIn>(a, s);
+      launch_128<CT, TIn>(a, s);
     else if (GLd && skpref_env() && splitk_env() && a.sk_cnt != nullptr && nKd >= 16 &&
              (int64_t)((a.M + 127) / 128) * ntn >= 64)
-      launch<CT, 2, 2, 4, 9, TIn>(a, s);  // 128 x 128 tiles + split-K instead of smaller tiles
+      launch_128<CT, TIn>(a, s);  // 128 x 128 tiles + split-K instead of smaller tiles
     else if ((int64_t)((a.M + 63) / 64) * ntn >= kTargetWGs)
       if (GLd && deepb_env() >= 1 && a.KS >= 3)
         launch<CT, 2, 2, 2, 9, TIn, 3>(a, s);
