@@ -51,9 +51,40 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="replay the forward as a captured HIP graph")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--kernel-reps", type=int, default=20)
-    ap.add_argument("--mode", default="infer", choices=["infer", "train"],
-                    help="infer: the headline cfg2 forward; train: the cfg3 train.py step (B=16/GPU, DDP)")
+    ap.add_argument("--mode", default="infer", choices=["infer", "train", "selftest"],
+                    help="infer: the headline cfg2 forward; train: the cfg3 train.py step (B=16/GPU, DDP); "
+                         "selftest: the launcher / process-group / timing bookkeeping only (gloo, no GPU)")
+    ap.add_argument("--backend", default=None, choices=[None, "nccl", "gloo"],
+                    help="process-group backend (default: nccl = RCCL; selftest: gloo)")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(argv, n):
+    """``bench.py --gpus N`` started as ONE process: start N rank processes of this same script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env, one GPU each through LOCAL_RANK) and
+    exit with the worst exit code. Runs before anything touches the GPU (the parent never
+    initialises HIP; the children are fresh interpreters, not exec'd replacements)."""
+    import subprocess
+
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def build_model(device, dtype):
@@ -219,11 +250,40 @@ def main_train(args, rank, world, device):
     parallel.shutdown()
 
 
-def main():
-    args = parse()
+def main_selftest(args, rank, world, device):
+    """The N-rank bookkeeping of the bench without a model: barrier + timed region + MAX/SUM over
+    ranks, one JSON line from rank 0 (tests/test_distributed.py runs it over gloo on CPU)."""
     from fs2amd import parallel
 
-    rank, local, world, device = parallel.init("nccl")
+    frames = 1000 * (rank + 1)
+    parallel.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    parallel.barrier()
+    elapsed, tot = parallel.aggregate(time.perf_counter() - t0, frames, device)
+    if rank == 0:
+        print(json.dumps({"metric": "bench launcher self-test", "value": round(tot / elapsed, 1), "unit": "frames/s",
+                          "n_gpus": world, "steps": 1, "warmup": 0, "ms_per_step": round(elapsed * 1e3, 3),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "none",
+                          "data": "none", "config": {"workload": "selftest", "frames_total": tot,
+                                                     "backend": device.type}}), flush=True)
+    parallel.shutdown()
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's single-process `bench.py --gpus N`: become the launcher of N ranks
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    from fs2amd import parallel
+
+    backend = args.backend or ("gloo" if args.mode == "selftest" else "nccl")
+    rank, local, world, device = parallel.init(backend)
+    if world != args.gpus and rank == 0:
+        print(f"bench: note: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the {world} ranks that ran",
+              file=sys.stderr, flush=True)
+    if args.mode == "selftest":
+        return main_selftest(args, rank, world, device)
     if args.mode == "train":
         return main_train(args, rank, world, device)
 

@@ -180,7 +180,6 @@ struct ConvArgs {
   // 1 = this launch runs the 256-row panels [0, P1), 2 = it runs the rows from P1 * 256 on.
   int row_split;
   int split_slots;          // workgroups the phased kernel runs at once (one per CU)
-  int ashift;               // bf16 LDS-DMA conv: derive tap t's A fragments from tap t-1's (row shift)
   int ln_pairs;             // LayerNorm epilogues: two rows per wave-iteration, 16-byte stores
 };
 
@@ -749,30 +748,10 @@ __device__ __forceinline__ void vm_wait_n(int n) {
   }
 }
 
-// A fragments of the next tap from the current tap's: the A operand of mfma_16x16x32 holds, in
-// lane l, row (l & 15) of a 16-row block (8 consecutive k), and tap t+1 reads every row one row
-// further down the LDS halo. So lane l of the shifted block takes lane l+1 (DPP row_shl:1, rows
-// of 16 lanes = the operand's row groups) and lane 15 takes lane 0 of the next 16-row block
-// (row_shr:15 into the old value). One LDS read of a 16-row block per tap replaces WMI.
-__device__ __forceinline__ bf16x8 shift_rows(bf16x8 cur, bf16x8 nxt) {
-  typedef int i32x4v __attribute__((ext_vector_type(4)));
-  const i32x4v c = __builtin_bit_cast(i32x4v, cur), n = __builtin_bit_cast(i32x4v, nxt);
-  i32x4v r;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int t = __builtin_amdgcn_update_dpp(0, n[q], 0x11F, 0xF, 0xF, false);  // row_shr:15: lane 15 <- lane 0
-    r[q] = __builtin_amdgcn_update_dpp(t, c[q], 0x101, 0xF, 0xF, false);       // row_shl:1: lane i <- lane i+1
-  }
-  return __builtin_bit_cast(bf16x8, r);
-}
-
-// NSB: depth of the B (weight) stage ring on the LDS-DMA path. NSB == 2: one k-step in flight,
-// vmcnt(0) per step. NSB > 2 (tall tiles, KS >= NSB): B of step k+NSB-1 is issued right after
-// the barrier that retires step k-1, the next channel block's A halo at tap 0 of the current one
-// (KS-1 steps ahead), and each step waits with a counted vmcnt for its own B only.
+// LDS-DMA path: two stages (A halo + one B k-step each), one k-step in flight, vmcnt(0) per step.
 // WCOL = columns per wave: 64 (4 MFMA blocks) or 32 (2x the waves for the same tile: 8-wave
 // 128 x 128, two workgroups and four waves per SIMD).
-template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, bool GL, int NSB = 2, int WCOL = 64>
+template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, bool GL, int WCOL = 64>
 __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 ? 4 : 1)) void conv_gemm_kernel(ConvArgs a) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;  // waves / threads per workgroup (4 or 8)
   constexpr int WROWS = 16 * WMI;
@@ -786,15 +765,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
   constexpr int B_CH = BN * 8 / NT;
   constexpr int RPP = NT / 8;                           // staged rows per pass
   constexpr int A_BYTES = HMAX * kRowBytes, B_BYTES = BN * kRowBytes;
-  static_assert(NSB == 2 || GL, "deep B ring needs the LDS-DMA path");
-  constexpr int STAGE = 2 * A_BYTES + NSB * B_BYTES;
+  constexpr int STAGE = 2 * A_BYTES + 2 * B_BYTES;
   constexpr int EPI_LD = BN + 4;
   constexpr int SMEM = (STAGE > BM * EPI_LD * 4) ? STAGE : BM * EPI_LD * 4;
   // + 16 B: the split-K "last arriver" word lives in the same array (a second __shared__ object
   // next to an LDS-DMA staging array can make hipcc drain vmcnt before every k-step's reads)
   __shared__ __attribute__((aligned(16))) char smem[SMEM + 16];
   char *const Abuf = smem;                  // 2 x A_BYTES
-  char *const Bbuf = smem + 2 * A_BYTES;    // NSB x B_BYTES
+  char *const Bbuf = smem + 2 * A_BYTES;    // 2 x B_BYTES
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform for the compiler
@@ -907,10 +885,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
 
   const int bf8_0 = lds_off(wc * WCOL + (lane & 15), 2 * (lane >> 4));
   const int bf8_1 = lds_off(wc * WCOL + (lane & 15), 2 * (lane >> 4) + 1);
-  // persistent A fragments for the tap-to-tap row shift (bf16, LDS-DMA path)
-  constexpr bool ASH = CT == FS2_BF16 && GL && KSMAX > 1 && WCOL == 64;  // (register budget at WCOL 32)
-  const bool ashift = ASH && a.ashift && KS > 1;
-  bf16x8 Fs[2][WMI];
   auto compute = [&](int aslot, int tap, const char *Bs, bool fresh) {
     const char *As = Abuf + aslot * A_BYTES;
     const int sh = tap - pad;
@@ -943,20 +917,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
       const char *Bb = Bs + (s ? bread1 : bread0);
       if constexpr (CT == FS2_BF16) {
         bf16x8 af[WMI], bfr[NI];
-        if (ASH && ashift) {
-          if (fresh) {
-#pragma unroll
-            for (int mi = 0; mi < WMI; ++mi) Fs[s][mi] = *reinterpret_cast<const bf16x8 *>(Ab + mi * 16 * kRowBytes);
-          } else {
-            // block WMI at tap-1: only lane (l & 15) == 0 of each group is used (clamped in the halo)
-            const int er = min(arow0 + 16 * WMI + tap - 1, HMAX - 1);
-            const bf16x8 ext = *reinterpret_cast<const bf16x8 *>(As + lds_off(er, s * 4 + (lane >> 4)));
-#pragma unroll
-            for (int mi = 0; mi < WMI; ++mi) Fs[s][mi] = shift_rows(Fs[s][mi], mi + 1 < WMI ? Fs[s][mi + 1] : ext);
-          }
-#pragma unroll
-          for (int mi = 0; mi < WMI; ++mi) af[mi] = Fs[s][mi];
-        } else {
+        {
 #pragma unroll
           for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const bf16x8 *>(Ab + mi * 16 * kRowBytes);
         }
@@ -1037,67 +998,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
         glds(wr_, Bs + p * 1024, n < a.N ? (uint32_t)n * wrow + off : kOOB);
       }
     };
-    if constexpr (NSB > 2) {
-      // this wave's A-halo DMA count (pieces p = wid + NW*it < AP)
-      const int a_w = (AP - wid + NW - 1) / NW;
-      constexpr int BPW = BP / NW;
-      int cb = k0 / KS, tap = k0 - cb * KS;
-      const int cb_last = (k1 - 1) / KS;
-      dma_a(cb, cb & 1);
-      if (cb + 1 <= cb_last) dma_a(cb + 1, (cb + 1) & 1);  // both halo buffers are free at the start
-      {
-        int c = cb, t = tap;
-#pragma unroll
-        for (int j = 0; j < NSB - 1; ++j) {
-          if (k0 + j < k1) dma_b(c, t, (k0 + j) % NSB);
-          if (++t == KS) {
-            t = 0;
-            ++c;
-          }
-        }
-      }
-      // (cbi, tapi) = coordinates of the next B step to issue (k0 + NSB - 1)
-      int cbi = (k0 + NSB - 1) / KS, tapi = (k0 + NSB - 1) - ((k0 + NSB - 1) / KS) * KS;
-      for (int ks = k0; ks < k1; ++ks) {
-        // loads issued after B(ks): B(ks+1 .. ks+NSB-2) and any A halo issued since
-        int after = 0;
-#pragma unroll
-        for (int j = 1; j <= NSB - 2; ++j) after += (ks + j < k1) ? BPW : 0;
-#pragma unroll
-        for (int j = 1; j <= NSB - 2; ++j) {  // steps s = ks - NSB + 1 + j issued an A halo iff tap(s) == 0
-          const int st = ks - NSB + 1 + j;
-          if (st > k0 && st < ks) {
-            const int tp = st - (st / KS) * KS;
-            if (tp == 0 && st / KS + 1 <= cb_last) after += a_w;
-          }
-        }
-        {  // the step that issued B(ks) itself issued its A after it
-          const int st = ks - NSB + 1;
-          if (st > k0) {
-            const int tp = st - (st / KS) * KS;
-            if (tp == 0 && st / KS + 1 <= cb_last) after += a_w;
-          }
-        }
-        vm_wait_n(after);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // raw: __syncthreads() would drain vmcnt (the whole ring) to 0
-        if (ks + NSB - 1 < k1) {
-          dma_b(cbi, tapi, (ks + NSB - 1) % NSB);
-          if (++tapi == KS) {
-            tapi = 0;
-            ++cbi;
-          }
-        }
-        if (tap == 0 && ks > k0 && cb + 1 <= cb_last) dma_a(cb + 1, (cb + 1) & 1);
-        compute(cb & 1, tap, Bbuf + (ks % NSB) * B_BYTES, tap == 0 || ks == k0);
-        if (++tap == KS) {
-          tap = 0;
-          ++cb;
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    } else {
+    {
     int cb = k0 / KS, tap = k0 - (k0 / KS) * KS;
     dma_a(cb, cb & 1);
     dma_b(cb, tap, k0 & 1);
@@ -1197,21 +1098,18 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
 // A rows of each tap are DMA'd separately (row m0+r+tap-pad) with the sequence-boundary test on
 // the source offset (out of range -> zeros), so fragments need no masking. LDS: 2 x (A 32 KiB +
 // B 32 KiB) = 128 KiB, one __shared__ array; the epilogue reuses it one M half at a time.
-// SK = the stream-K tail (FS2_CONV_8PSK, opt-in): a separate instantiation, so the default kernel
-// carries none of its work-item bookkeeping (with it the kernel spilled 3 VGPRs to scratch).
 // HB = 16-row blocks per M half: 8 (256-row tiles) or 7 (224-row tiles: a launch whose 256-row
 // tiles leave part of its one round idle fills the round with more, shorter tiles; PostNet k=5 at
 // cfg2: 216 -> 246 tiles on 256 CUs). The LDS image keeps 128-row halves; rows 112..127 of each
 // half are DMA'd as zeros and skip their MFMAs.
-template <bool SK, int HB = 8>
+template <int HB = 8>
 __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   static_assert(HB == 8 || HB == 7, "blocks per half");
-  static_assert(!SK || HB == 8, "stream-K uses 256-row tiles");
   constexpr int BM = 32 * HB, HR = 16 * HB, BN = 256, KE = 64;
   constexpr int TILE = 256 * kRowBytes;  // 32 KiB: one operand of one k-tile
   constexpr int EPI_LD = BN + 4;
   constexpr int SMEM = (4 * TILE > 128 * EPI_LD * 4) ? 4 * TILE : 128 * EPI_LD * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + 16];  // A0 A1 B0 B1 (buffers) + stream-K flag
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];  // A0 A1 B0 B1 (buffers)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1222,51 +1120,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   const int nCk = a.Cin_pad / KE;
   const int nK = KS * nCk;
 
-  // Work: Ttot tiles. Without stream-K (sk_slots == 0) one tile per workgroup. With it (S = one
-  // workgroup per CU): R = Ttot / S whole rounds run one tile per workgroup (ids < R*S, XCD
-  // remap); the k-tiles of the tail tiles (flattened tile-major, W = tail * nK) are cut into Sp
-  // equal contiguous ranges, one per workgroup id R*S + j. Sp >= tail, so a range spans at most
-  // two tiles; a tile cut between ranges is summed by its last-arriving range (sc1 partials,
-  // fixed range order) and that workgroup runs its epilogue.
+  // Work: Ttot tiles, one per workgroup (XCD-aware remap)
   const int Ttot = a.row_split == 1 ? split_panels(a, M) * a.ntn : ((M + BM - 1) / BM) * a.ntn;
-  const int S = SK ? a.sk_slots : 0;
-  const int R = S > 0 ? Ttot / S : 0, tail = S > 0 ? Ttot - R * S : 0;
-  const int Sp = tail > 0 ? min(S, 4 * tail) : 0;
-  const int dp = S > 0 ? R * S : Ttot;
-  const int64_t W = (int64_t)tail * nK;
-  const int id = blockIdx.x;
-  int it_tile[2], it_kb[2], it_ke[2], nitems = 0;
-  int j = -1;  // stream-K range index
-  int64_t b0 = 0;
-  if (!SK) {
-    if (id >= Ttot) return;
-    it_tile[0] = xcd_remap(id, Ttot);
-    it_kb[0] = 0;
-    it_ke[0] = nK;
-    nitems = 1;
-  } else if (id < dp) {
-    it_tile[0] = xcd_remap(id, dp);
-    it_kb[0] = 0;
-    it_ke[0] = nK;
-    nitems = 1;
-  } else if (id < dp + Sp) {
-    j = id - dp;
-    b0 = (int64_t)j * W / Sp;
-    const int64_t b1 = (int64_t)(j + 1) * W / Sp;
-    for (int64_t k = b0; k < b1 && nitems < 2;) {
-      const int tt = (int)(k / nK);
-      const int64_t te = min(b1, (int64_t)(tt + 1) * nK);
-      it_tile[nitems] = dp + tt;
-      it_kb[nitems] = (int)(k - (int64_t)tt * nK);
-      it_ke[nitems] = (int)(te - (int64_t)tt * nK);
-      ++nitems;
-      k = te;
-    }
-  } else {
-    return;
-  }
-  // range that holds flattened k-tile k:  j(k) = ((k+1) * Sp - 1) / W
-  auto jof = [&](int64_t k) { return (int)(((k + 1) * Sp - 1) / (W > 0 ? W : 1)); };
+  if ((int)blockIdx.x >= Ttot) return;
+  const int tile = xcd_remap(blockIdx.x, Ttot);
   const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
   const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * 2u;
@@ -1278,10 +1135,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   const int prow = lane >> 3, plc = (lane & 7) ^ ((lane >> 3) & 7);
   auto apiece = [&](int x, int i) { return 16 * (w >> 2) + 8 * x + 2 * (w & 3) + i; };
   auto bpiece = [&](int x, int i) { return (w & 3) * 8 + 4 * x + 2 * (w >> 2) + i; };
-  for (int item = 0; item < (SK ? nitems : 1); ++item) {
-  const int tile = item == 0 ? it_tile[0] : it_tile[1];
-  const int kb = SK ? (item == 0 ? it_kb[0] : it_kb[1]) : 0;
-  const int ke = SK ? (item == 0 ? it_ke[0] : it_ke[1]) : nK;
+  const int kb = 0, ke = nK;
   int m0, n0;
   tile_coords(a, tile, Ttot, BM, BN, m0, n0);
   int arow[2][2], apos[2][2], alen[2][2];
@@ -1458,56 +1312,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
   if (wr == 0) bar();
   __syncthreads();
 
-  if (SK && (kb != 0 || ke != nK)) {  // a stream-K tile cut between ranges: hand over / sum the partials
-    const int tt = tile - dp;
-    const int64_t ts = (int64_t)tt * nK;
-    const int jf = jof(ts), nseg = jof(ts + nK - 1) - jf + 1;
-    // partial slot of the range jj's piece of this tile: 2*jj (its first piece) or 2*jj + 1
-    auto slot = [&](int jj) { return 2 * jj + (((int64_t)jj * W / max(Sp, 1)) < ts ? 1 : 0); };
-    const rsrc_t pr = make_rsrc(a.sk_part, a.sk_part_bytes);
-    auto pofs = [&](int sl, int mi, int ni) {
-      return (uint32_t)sl * (uint32_t)(BM * BN * 4) + (uint32_t)(((mi * 4 + ni) * 512 + tid) * 16);
-    };
-    const int own = slot(j);
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc[mi][ni]), pr, pofs(own, mi, ni), 0, 16);
-    int &flag = *reinterpret_cast<int *>(smem + SMEM);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(a.sk_cnt + tt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == nseg - 1;
-      if (last) {
-        __hip_atomic_store(a.sk_cnt + tt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      }
-      flag = last;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const bool last = flag != 0;
-    __syncthreads();  // everyone has read the flag before a later item's hand-off rewrites it
-    if (!last) continue;
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        f32x4 tot = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int sg = 0; sg < nseg; ++sg) {
-          const int jj = jf + sg;
-          f32x4 pv = acc[mi][ni];
-          if (jj != j)
-            pv = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, pofs(slot(jj), mi, ni), 0, 16));
-          tot += pv;
-        }
-        acc[mi][ni] = tot;
-      }
-  }
-
   // ---- epilogue, one M half at a time through LDS
   float *E = reinterpret_cast<float *>(smem);
 #pragma unroll
@@ -1526,7 +1330,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p_kernel(ConvArgs a) {
     epilogue<128, BN, 8, false>(a, E, m0 + h * HR, n0, tid, HB == 8 ? M : min(M, m0 + h * HR + HR));
     __syncthreads();
   }
-  }  // work items
 }
 
 // Would a launch of T tiles on S slots split its tail (conv_tile_sk's rule)? Decided on the host
@@ -1547,28 +1350,6 @@ bool splitk_env() {
   return on;
 }
 
-// FS2_CONV_SKPREF=1 (opt-in): small-M launches (encoder / variance predictors, M ~ 4k) use big
-// tiles + split-K instead of small tiles. Measured slower (cfg2 probes, us: VP 56 -> 68, encoder
-// conv-k9 31 -> 39, encoder conv-k1+LN 17 -> 32; bench -3.8 %): the partial-tile hand-off costs
-// more than the weight streaming it saves.
-bool skpref_env() {
-  static const bool on = [] {
-    const char *e = getenv("FS2_CONV_SKPREF");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on;
-}
-
-// FS2_CONV_DEEPB (A/B): 1 = the 64-row small-M conv tiles use a 3-deep B ring (2 workgroups per
-// CU still fit), 2 = also the 128 x 128 rows-left launch of the decoder conv-k9 (1 per CU).
-int deepb_env() {
-  static const int v = [] {
-    const char *e = getenv("FS2_CONV_DEEPB");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 // Compute units of the current device (cached per device id).
 int num_cus() {
   static int cache[64] = {0};
@@ -1582,31 +1363,18 @@ int num_cus() {
   return cache[dev];
 }
 
-void launch_8p(ConvArgs a, hipStream_t s, bool stream_k = false, bool rows224 = false) {
+void launch_8p(ConvArgs a, hipStream_t s, bool rows224 = false) {
   a.ntn = (a.N + 255) / 256;
   a.ngr = a.ntn;
-  if (rows224 && !stream_k && a.row_split == 0) {
+  a.sk_slots = 0;
+  if (rows224 && a.row_split == 0) {
     const int nwg = ((a.M + 223) / 224) * a.ntn;
-    if (nwg > 0) hipLaunchKernelGGL((conv_gemm_8p_kernel<false, 7>), dim3(nwg), dim3(512), 0, s, a);
+    if (nwg > 0) hipLaunchKernelGGL((conv_gemm_8p_kernel<7>), dim3(nwg), dim3(512), 0, s, a);
     return;
   }
   int nwg = ((a.M + 255) / 256) * a.ntn;
   if (a.row_split == 1) nwg = nwg / a.split_slots * a.split_slots;  // whole rounds (device M <= a.M)
-  a.sk_slots = 0;
-  if (stream_k && a.row_split == 0) {  // conv_gemm_8p_kernel's stream-K tail: 2 partial slots per range
-    const int S = num_cus();
-    const int64_t need = kSkCntBytes + (int64_t)2 * S * 256 * 256 * 4;
-    if (S > 0 && S * 4 <= kSkCntBytes && a.sk_cnt != nullptr && a.sk_ws_bytes >= need) {
-      a.sk_slots = S;
-      a.sk_part_bytes = (uint32_t)(need - kSkCntBytes);
-      nwg += S;  // the tail's ranges (ids past the whole rounds; unused ids exit)
-    }
-  }
-  if (nwg <= 0) return;
-  if (a.sk_slots > 0)
-    hipLaunchKernelGGL(conv_gemm_8p_kernel<true>, dim3(nwg), dim3(512), 0, s, a);
-  else
-    hipLaunchKernelGGL(conv_gemm_8p_kernel<false>, dim3(nwg), dim3(512), 0, s, a);
+  if (nwg > 0) hipLaunchKernelGGL((conv_gemm_8p_kernel<8>), dim3(nwg), dim3(512), 0, s, a);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1825,204 +1593,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvA
   epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
 }
 
-// ------------------------------------------------------------------------------------------------
-// Register-B variant of the ring kernel for the streamed-A LayerNorm GEMMs (decoder fc / FFN w_2,
-// M ~ 25k rows, K = 256 / 1024). There the A rows come from HBM exactly once while the weights
-// are L2-resident, and with B staged through LDS (32 KiB per k-step) only two 16 KiB A stages
-// fit in flight per CU: ~6 MB chip-wide, i.e. ~2 TB/s at a loaded HBM latency of ~3 us. Here each
-// wave loads its own B fragments straight into registers (buffer_load_dwordx4, PB k-steps ahead,
-// 8 x 16 B per lane per k-step) and LDS holds only an NA-deep A ring (A rows shifted by the tap,
-// sequence test on the DMA source). Per k-step a wave issues B(k+PB) first, then A(k+NA-1), so
-// waiting for B(k) (counted vmcnt) never waits for the deeper A stages; one raw s_barrier per
-// k-step publishes A(k) and frees the A buffer the next issue refills.
-template <int CT, int WGM, int WMI, int NA, int PB>
-__global__ __launch_bounds__(256 * WGM, 1) void conv_gemm_rb_kernel(ConvArgs a) {
-  constexpr int WGN = 4, NW = WGM * WGN;
-  constexpr int WROWS = 16 * WMI, BM = WROWS * WGM, BN = 64 * WGN;
-  constexpr int KE = CTraits<CT>::KE, CE = CTraits<CT>::CE;
-  using TW = typename CTraits<CT>::T;
-  constexpr int AP = BM / 8;                            // 1 KiB A pieces per stage
-  constexpr int AQ = (AP + NW - 1) / NW;                // A pieces per wave per stage
-  constexpr int BL = 8;                                 // B fragment loads per lane per k-step
-  constexpr int LPS = AQ + BL;                          // vector-memory ops per wave per k-step
-  static_assert(AQ + LPS * (PB - 1) <= 63, "vmcnt range");
-  constexpr int STAGE = AP * 1024;
-  constexpr int EPI_LD = BN + 4;
-  constexpr int SMEM = (NA * STAGE > BM * EPI_LD * 4) ? NA * STAGE : BM * EPI_LD * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  using Frag = typename std::conditional<CT == FS2_BF16, bf16x8, f32x4>::type;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid / WGN, wc = wid % WGN;
-  int M, m0, n0;
-  if (!conv_tile<BM>(a, M, m0, n0, BN)) return;
-
-  const int KS = a.KS, pad = a.pad, T = a.T;
-  const int nCk = a.Cin_pad / KE;
-  const int nK = KS * nCk;
-  const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
-  const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
-  const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * (uint32_t)sizeof(TW);
-  const uint32_t xrow = (uint32_t)a.xs * (uint32_t)sizeof(TW);
-
-  // A DMA roles (as the ring kernel)
-  const int prow = lane >> 3, plc = (lane & 7) ^ prow;
-  int arow[AQ], apos[AQ], alen[AQ];
-#pragma unroll
-  for (int i = 0; i < AQ; ++i) {
-    const int m = m0 + 8 * ((wid + NW * i) % AP) + prow;
-    arow[i] = m;
-    if (m >= M) {
-      apos[i] = 0;
-      alen[i] = 0;
-    } else if (KS == 1 && pad == 0) {  // no taps: every row < M is valid, no row_pos read
-      apos[i] = 0;
-      alen[i] = 1;
-    } else if (a.row_pos != nullptr) {
-      const int2 p = a.row_pos[m];
-      apos[i] = p.x;
-      alen[i] = p.y;
-    } else {
-      apos[i] = m % T;
-      alen[i] = T;
-    }
-  }
-  // B fragment of this lane: column n0 + wc*64 + ni*16 + (lane&15), 16-byte chunk s*4 + (lane>>4)
-  uint32_t bofs[4];
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int n = n0 + wc * 64 + ni * 16 + (lane & 15);
-    bofs[ni] = n < a.N ? (uint32_t)n * wrow + (uint32_t)((lane >> 4) * 16) : kOOB;
-  }
-  auto glds = [&](char *dst, uint32_t off) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)dst, 16, off, 0, 0, 0);
-  };
-  auto issue_a = [&](int tap, int cb, int buf) {
-    char *As = smem + buf * STAGE;
-    const int sh = tap - pad;
-    const int ch = cb * KE + plc * CE;
-    const bool ch_ok = ch < a.Cin;
-#pragma unroll
-    for (int i = 0; i < AQ; ++i) {
-      const bool ok = ch_ok && (unsigned)(apos[i] + sh) < (unsigned)alen[i];
-      glds(As + ((wid + NW * i) % AP) * 1024,
-           ok ? (uint32_t)(arow[i] + sh) * xrow + (uint32_t)ch * (uint32_t)sizeof(TW) : kOOB);
-    }
-  };
-  auto load_b = [&](Frag (&b)[4][2], int tap, int cb) {
-    const uint32_t off = ((uint32_t)tap * a.Cin_pad + cb * KE) * (uint32_t)sizeof(TW);
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        auto v = __builtin_amdgcn_raw_buffer_load_b128(wr_, bofs[ni] == kOOB ? kOOB : bofs[ni] + off + s * 64u, 0, 0);
-        b[ni][s] = *reinterpret_cast<Frag *>(&v);
-      }
-  };
-
-  f32x4 acc[WMI][4];
-#pragma unroll
-  for (int i = 0; i < WMI; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int aread0 = lds_off(wr * WROWS + (lane & 15), lane >> 4);
-  const int aread1 = lds_off(wr * WROWS + (lane & 15), 4 + (lane >> 4));
-  auto compute = [&](const char *As, const Frag (&b)[4][2]) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const char *Ab = As + (s ? aread1 : aread0);
-      Frag af[WMI];
-#pragma unroll
-      for (int mi = 0; mi < WMI; ++mi) af[mi] = *reinterpret_cast<const Frag *>(Ab + mi * 16 * kRowBytes);
-      if constexpr (CT == FS2_BF16) {
-#pragma unroll
-        for (int mi = 0; mi < WMI; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], b[ni][s], acc[mi][ni], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int mi = 0; mi < WMI; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
-              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi][j], b[ni][s][j], acc[mi][ni], 0, 0, 0);
-      }
-    }
-  };
-
-  // k-step k = cb * KS + tap. (ta, ca): next A stage to issue; (tb, cbb): next B k-step to load
-  int ta = 0, ca = 0, tb = 0, cbb = 0;
-  auto adv = [&](int &t, int &c) {
-    if (++t == KS) {
-      t = 0;
-      ++c;
-    }
-  };
-  Frag bq[PB + 1][4][2];  // B ring in registers: k-step k lives in bq[k % (PB+1)]
-  // prologue: A stages 0..NA-2, then B k-steps 0..PB-1 (B issued last: the first waits see them)
-#pragma unroll
-  for (int st = 0; st < NA - 1; ++st)
-    if (st < nK) {
-      issue_a(ta, ca, st);
-      adv(ta, ca);
-    }
-#pragma unroll
-  for (int j = 0; j < PB; ++j)
-    if (j < nK) {
-      load_b(bq[j], tb, cbb);
-      adv(tb, cbb);
-    }
-  // main loop, unrolled by PB+1 so the B ring index is static
-  for (int k0 = 0; k0 < nK; k0 += PB + 1) {
-#pragma unroll
-    for (int u = 0; u <= PB; ++u) {
-      const int k = k0 + u;
-      if (k < nK) {
-        // B(k) (and, issued before it, A(k)) landed; later issues may stay in flight
-        if (k + PB <= nK - 1 + 0 && k >= 1)
-          vm_wait<AQ + LPS * (PB - 1)>();
-        else
-          vm_wait<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (k + PB < nK) {
-          load_b(bq[(u + PB) % (PB + 1)], tb, cbb);
-          adv(tb, cbb);
-        }
-        if (k + NA - 1 < nK) {
-          issue_a(ta, ca, (k + NA - 1) % NA);
-          adv(ta, ca);
-        }
-        compute(smem + (k % NA) * STAGE, bq[u]);
-      }
-    }
-  }
-  __syncthreads();
-
-  float *E = reinterpret_cast<float *>(smem);
-#pragma unroll
-  for (int mi = 0; mi < WMI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
-  __syncthreads();
-  epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
-}
-
-template <int CT, int WGM, int WMI, int NA, int PB>
-void launch_rb(ConvArgs a, hipStream_t s) {
-  constexpr int BM = 16 * WMI * WGM;
-  a.ntn = 1;
-  a.ngr = 1;
-  const int nwg = (a.M + BM - 1) / BM;
-  hipLaunchKernelGGL((conv_gemm_rb_kernel<CT, WGM, WMI, NA, PB>), dim3(nwg), dim3(256 * WGM), 0, s, a);
-}
-
 template <int CT, int WGM, int WMI, int NS, int WGN = 4>
 void launch_ring(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM;
@@ -2047,7 +1617,7 @@ void launch_ring(ConvArgs a, hipStream_t s) {
   hipLaunchKernelGGL((conv_gemm_ring_kernel<CT, WGM, WMI, NS, WGN>), dim3(nwg), dim3(64 * WGM * WGN), 0, s, a);
 }
 
-template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, int NSB = 2, int WCOL = 64>
+template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, int WCOL = 64>
 void launch(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM, BN = WCOL * WGN;
   constexpr bool GL = std::is_same<TIn, typename CTraits<CT>::T>::value;  // LDS-DMA needs no conversion
@@ -2074,7 +1644,7 @@ void launch(ConvArgs a, hipStream_t s) {
     const bool splitk = splitk_env();
     // resident workgroups per CU: LDS-limited (the kernel's SMEM + flag), at most 2 (launch bounds)
     constexpr int HMX = ((BM + KSMAX - 1) + 7) / 8 * 8;
-    constexpr int STG = 2 * HMX * kRowBytes + NSB * BN * kRowBytes;
+    constexpr int STG = 2 * HMX * kRowBytes + 2 * BN * kRowBytes;
     constexpr int SMB = (STG > BM * (BN + 4) * 4 ? STG : BM * (BN + 4) * 4) + 16;
     constexpr int PER_CU = (WGM * WGN == 4 || WCOL == 32) ? (163840 / SMB >= 2 ? 2 : 1) : 1;
     const int slots = num_cus() * PER_CU;
@@ -2092,7 +1662,7 @@ void launch(ConvArgs a, hipStream_t s) {
       nwg += slots;  // spare ids for the tail segments (exit when unused)
     }
   }
-  hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, WMI, KSMAX, TIn, GL, GL ? NSB : 2, WCOL>), dim3(nwg),
+  hipLaunchKernelGGL((conv_gemm_kernel<CT, WGM, WGN, WMI, KSMAX, TIn, GL, WCOL>), dim3(nwg),
                      dim3(64 * WGM * WGN), 0, s, a);
 }
 
@@ -2110,7 +1680,7 @@ void launch_128(ConvArgs a, hipStream_t s) {
     return e == nullptr || e[0] != '0';
   }();
   if (w8)
-    launch<CT, 2, 4, 4, 9, TIn, 2, 32>(a, s);
+    launch<CT, 2, 4, 4, 9, TIn, 32>(a, s);
   else
     launch<CT, 2, 2, 4, 9, TIn>(a, s);
 }
@@ -2127,14 +1697,6 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
     }();
     const int64_t tiles256 = (int64_t)((a.M + 255) / 256) * ((a.N + 255) / 256);
     const int S = num_cus();
-    static const bool tall = [] {
-      const char *e = getenv("FS2_CONV_TALL");
-      return e != nullptr && e[0] == '1';
-    }();
-    if (tall && !ln && a.KS >= 4 && a.N % 128 == 0 && (int64_t)((a.M + 255) / 256) * (a.N / 128) >= S) {
-      launch<CT, 4, 2, 4, 9, TIn, 4>(a, s);  // 256 x 128, 8 waves, A halo + 4-deep B ring, 1 WG / CU
-      return;
-    }
     if (phased && !ln && a.KS >= 4 && a.N >= 256 && tiles256 >= 192 && S > 0) {
       if (tiles256 <= S) {  // at most one round: the phased kernel alone
         // 224-row tiles when they still fit the one round (shorter tiles, more CUs busy);
@@ -2144,20 +1706,7 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
           return e == nullptr || e[0] != '0';
         }();
         const int64_t tiles224 = (int64_t)((a.M + 223) / 224) * ((a.N + 255) / 256);
-        launch_8p(a, s, false, r224 && tiles224 <= S);
-        return;
-      }
-      // FS2_CONV_8PSK=1 (opt-in): stream-K over the tail tiles in the phased launch itself. Correct
-      // (parity-tested) but measured slower than the 128x128 remainder launch (cfg2 conv-k9 191 vs
-      // 133 us): 256 KiB f32 partials per cut tile, and the last arriver's (tile fragment x range)
-      // read-back is latency-serialised; kept for later rounds.
-      static const bool sk8 = [] {
-        const char *e = getenv("FS2_CONV_8PSK");
-        return e != nullptr && e[0] == '1';
-      }();
-      if (sk8 && splitk_env() && a.sk_cnt != nullptr &&
-          a.sk_ws_bytes >= kSkCntBytes + (int64_t)2 * S * 256 * 256 * 4) {
-        launch_8p(a, s, true);  // whole rounds + stream-K over the tail tiles, one launch
+        launch_8p(a, s, r224 && tiles224 <= S);
         return;
       }
       ConvArgs a1 = a, a2 = a;  // whole rounds of 256 x 256 tiles, then the rows left over
@@ -2166,41 +1715,16 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       a2.row_split = 2;
       a2.split_slots = S;
       launch_8p(a1, s);
-      if (deepb_env() >= 2 && a.KS >= 3)
-        launch<CT, 2, 2, 4, 9, TIn, 3>(a2, s);
-      else
-        launch_128<CT, TIn>(a2, s);
+      launch_128<CT, TIn>(a2, s);
       return;
     }
   }
   if constexpr (std::is_same<TIn, typename CTraits<CT>::T>::value) {
-    // experiment: deep-ring kernel for the large plain-epilogue convs (FS2_CONV_RING9=1)
-    static const bool ring9 = [] {
-      const char *e = getenv("FS2_CONV_RING9");
-      return e != nullptr && e[0] == '1';
-    }();
-    if (ring9 && !ln && a.KS > 1 && a.N % 256 == 0 && a.M >= 8192 && a.cin_block == 0) {
-      launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages
-      return;
-    }
     static const bool ring = [] {
       const char *e = getenv("FS2_CONV_RING");
       return e == nullptr || e[0] != '0';
     }();
     if (ln && (ring || a.cin_block != 0)) {  // LDS-DMA deep ring (LN epilogues, N == 256)
-      // register-B variant: correct but measured 1.5x slower on the decoder conv1 in round 1
-      // (per-lane 16 B weight loads from L2, two waves per column group); opt-in
-      static const bool rb = [] {
-        const char *e = getenv("FS2_CONV_RB");
-        return e != nullptr && e[0] == '1';
-      }();
-      if constexpr (CT != FS2_FP8) {
-        if (a.M >= 192 * 128 && rb && a.cin_block == 0) {
-          launch_rb<CT, 2, 4, 8, 2>(a, s);  // 128 x 256, 8 waves, B in registers, 8 A stages
-          return;
-        }
-      }
-      const int nKd = a.KS * (a.Cin_pad / CTraits<CT>::KE);
       // 8 column waves on the small-M tiles (FS2_LN_W8=0: 4): the second wave per SIMD overlaps
       // LDS reads with the partner's MFMAs (encoder LN 14.5 -> 13.2 us, VP 50.8 -> 48.6 us)
       static const bool w8 = [] {
@@ -2213,21 +1737,10 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         const char *e = getenv("FS2_LN_W16DEC");
         return e == nullptr || e[0] != '0';
       }();
-      static const bool bm112 = [] {
-        const char *e = getenv("FS2_LN_BM112");
-        return e != nullptr && e[0] == '1';
-      }();
-      if (a.M >= 192 * 128 && bm112 && (a.M + 111) / 112 <= num_cus())
-        launch_ring<CT, 1, 7, 3>(a, s);  // 112 x 256, 4 waves, 3 stages: one round of more, shorter tiles
-      else if (a.M >= 192 * 128 && w16d)
+      if (a.M >= 192 * 128 && w16d)
         launch_ring<CT, 2, 4, 3, 8>(a, s);  // 128 x 256, 16 waves of 64 x 32, 3 stages
       else if (a.M >= 192 * 128)
         launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages (144 KiB)
-      else if (skpref_env() && splitk_env() && a.sk_cnt != nullptr && nKd >= 8)
-        // small M (encoder / variance predictors, M = B*L ~ 4k): 64-row tiles and split-K fill the
-        // chip with a quarter of the weight streaming of the 16-row tiles below (each tile streams
-        // its K range of the whole weight matrix)
-        launch_ring<CT, 1, 4, 3>(a, s);  // 64 x 256, 4 waves, 3 stages (120 KiB)
       else if (a.M >= 8192)
         w8 ? launch_ring<CT, 1, 2, 4, 8>(a, s)  // 32 x 256, 8 waves of 32 x 32, 4 stages
            : launch_ring<CT, 1, 2, 4>(a, s);    // 32 x 256, 4 waves of 32 x 64
@@ -2248,10 +1761,6 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
     const int ntn = (a.N + 127) / 128;
     const int nKd = a.KS * (a.Cin_pad / CTraits<CT>::KE);
     constexpr bool GLd = std::is_same<TIn, typename CTraits<CT>::T>::value;
-    static const int short_k = [] {  // FS2_CONV_SHORTK=1 (A/B): 64-row tiles for K <= 256 GEMMs
-      const char *e = getenv("FS2_CONV_SHORTK");
-      return e != nullptr ? atoi(e) : 0;
-    }();
     static const bool w8s = [] {  // 8 waves of 32 columns on the 64-row tiles (FS2_CONV_W8S=0: 4
       const char *e = getenv("FS2_CONV_W8S");  // of 64); encoder conv-k9 32.4 -> 31.1 us
       return e == nullptr || e[0] != '0';
@@ -2265,18 +1774,11 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       // one N tile and a long K (PostNet's last conv: N = 80, K = 2560): 128-row tiles and the
       // split-K tail fill the chip, instead of 32-row tiles that each stream the whole K
       launch_128<CT, TIn>(a, s);
-    else if (short_k && a.KS == 1 && a.Cin <= 256 && (int64_t)((a.M + 63) / 64) * ntn >= kTargetWGs)
-      launch<CT, 2, 2, 2, 9, TIn>(a, s);
     else if ((int64_t)((a.M + 127) / 128) * ntn >= kTargetWGs)
       launch_128<CT, TIn>(a, s);
-    else if (GLd && skpref_env() && splitk_env() && a.sk_cnt != nullptr && nKd >= 16 &&
-             (int64_t)((a.M + 127) / 128) * ntn >= 64)
-      launch_128<CT, TIn>(a, s);  // 128 x 128 tiles + split-K instead of smaller tiles
     else if ((int64_t)((a.M + 63) / 64) * ntn >= kTargetWGs)
-      if (GLd && deepb_env() >= 1 && a.KS >= 3)
-        launch<CT, 2, 2, 2, 9, TIn, 3>(a, s);
-      else if (w8s)
-        launch<CT, 2, 4, 2, 9, TIn, 2, 32>(a, s);  // 64 x 128, 8 waves of 32 x 32
+      if (w8s)
+        launch<CT, 2, 4, 2, 9, TIn, 32>(a, s);  // 64 x 128, 8 waves of 32 x 32
       else
         launch<CT, 2, 2, 2, 9, TIn>(a, s);
     else  // 32 x 128, 4 waves of 16 x 64 (8 waves of 16 x 32 measured 9.1 -> 9.7 us on the encoder Q|K|V)
@@ -2382,14 +1884,6 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.row_split = 0;
   a.split_slots = 1;
   {
-    // FS2_CONV_ASHIFT=1 (opt-in): tap-to-tap A-fragment row shift (shift_rows). Correct but slower
-    // (cfg2 probes: conv-k9 rows-left launch 59 -> 71 us, encoder conv-k9 33 -> 40 us): the LDS
-    // reads it saves were not the limit, the DPP chain it adds is.
-    static const bool ash = [] {
-      const char *e = getenv("FS2_CONV_ASHIFT");
-      return e != nullptr && e[0] == '1';
-    }();
-    a.ashift = ash ? 1 : 0;
     static const bool lnp = [] {  // FS2_LN_PAIRS=0: one row per wave-iteration (round-1 epilogue)
       const char *e = getenv("FS2_LN_PAIRS");
       return e == nullptr || e[0] != '0';

@@ -121,6 +121,7 @@ __global__ __launch_bounds__(256) void lr_expand_kernel(const TX *__restrict__ x
     if (index_map != nullptr && t < T_out) index_map[(int64_t)b * T_out + t] = s;
   }
   __syncthreads();
+  if (out == nullptr) return;  // index-map-only call (the training gather reads the map)
   const int vpr = D >> 3;
   const int rows = min(ROWS, t_end - t0);
   if (rows <= 0) return;
@@ -342,7 +343,9 @@ extern "C" int fs2_lr_durations(const void *dur, int dur_kind, float d_control, 
 extern "C" int fs2_lr_expand(const void *x, int x_dtype, const int32_t *cum, const int64_t *mel_len, int B, int L,
                              int D, int T_out, const float *pe, void *out, int out_dtype, int32_t *index_map,
                              const int32_t *out_cu, fs2_stream_t stream) {
-  if (x == nullptr || cum == nullptr || mel_len == nullptr || out == nullptr) return FS2_EINVAL;
+  // out may be NULL when index_map is given: only the source-index map is written
+  if (x == nullptr || cum == nullptr || mel_len == nullptr || (out == nullptr && index_map == nullptr))
+    return FS2_EINVAL;
   if (B < 0 || L <= 0 || D <= 0 || (D & 7) != 0 || T_out < 0) return FS2_EINVAL;
   if (B == 0 || T_out == 0) return FS2_OK;
   hipStream_t s = as_stream(stream);

@@ -6,19 +6,27 @@
 namespace {
 
 // out[b,l,:] = table[tok, :] + pe[l, :]          (transformer/Models.py:82-91)
+// A token outside [0, vocab) (the reference's nn.Embedding raises IndexError / a device assert)
+// makes its row NaN and increments *bad (optional device counter) -- never a silent clamp.
 template <typename TO>
 __global__ __launch_bounds__(256) void embed_pe_kernel(const int64_t *__restrict__ tokens, const float *__restrict__ table,
                                                        int vocab, const float *__restrict__ pe, int L, int D,
-                                                       int64_t rows, TO *__restrict__ out) {
+                                                       int64_t rows, TO *__restrict__ out, int32_t *__restrict__ bad) {
   const int vpr = D >> 3;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= rows * vpr) return;
   const int64_t row = e / vpr;
   const int col = (int)(e - row * vpr) << 3;
   const int l = (int)(row % L);
-  int64_t tok = tokens[row];
-  tok = tok < 0 ? 0 : (tok >= vocab ? vocab - 1 : tok);
+  const int64_t tok = tokens[row];
   float v[8], p[8];
+  if (tok < 0 || tok >= vocab) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = __builtin_nanf("");
+    store8(out + row * D + col, v);
+    if (bad != nullptr && col == 0) atomicAdd(bad, 1);
+    return;
+  }
   load8(table + tok * D + col, v);
   load8(pe + (int64_t)l * D + col, p);
 #pragma unroll
@@ -134,7 +142,7 @@ __global__ __launch_bounds__(256) void variance_embed_kernel(TX *__restrict__ x,
 }  // namespace
 
 extern "C" int fs2_embed_pe(const int64_t *tokens, const float *table, int vocab, const float *pe, int B, int L, int D,
-                            void *out, int out_dtype, fs2_stream_t stream) {
+                            void *out, int out_dtype, int32_t *bad_ids, fs2_stream_t stream) {
   if (tokens == nullptr || table == nullptr || pe == nullptr || out == nullptr) return FS2_EINVAL;
   if (B < 0 || L < 0 || D <= 0 || (D & 7) || vocab <= 0) return FS2_EINVAL;
   const int64_t rows = (int64_t)B * L;
@@ -144,10 +152,10 @@ extern "C" int fs2_embed_pe(const int64_t *tokens, const float *table, int vocab
   hipStream_t s = as_stream(stream);
   if (out_dtype == FS2_F32)
     hipLaunchKernelGGL(embed_pe_kernel<float>, grid, dim3(256), 0, s, tokens, table, vocab, pe, L, D, rows,
-                       reinterpret_cast<float *>(out));
+                       reinterpret_cast<float *>(out), bad_ids);
   else if (out_dtype == FS2_BF16)
     hipLaunchKernelGGL(embed_pe_kernel<bf16>, grid, dim3(256), 0, s, tokens, table, vocab, pe, L, D, rows,
-                       reinterpret_cast<bf16 *>(out));
+                       reinterpret_cast<bf16 *>(out), bad_ids);
   else
     return FS2_EUNSUPPORTED;
   FS2_CHECK_LAUNCH();

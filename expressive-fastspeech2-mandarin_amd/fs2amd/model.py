@@ -12,8 +12,12 @@ Precision: ``model_config["hip"]["dtype"]`` (or env ``FS2_HIP_DTYPE``, or
 * ``"fp32"`` — every GEMM on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32), f32 activations;
   the parity mode (matches the reference CPU path to ~1e-5).
 * ``"bf16"`` — FFT blocks, attention, mel_linear and PostNet on bf16 MFMA with f32
-  accumulation/LayerNorm; the VariancePredictors stay f32 (their outputs feed discrete
-  decisions: duration rounding and pitch/energy buckets, SURVEY.md §0 trap 2).
+  accumulation/LayerNorm. The VariancePredictors default to split-precision ``"bf16x3"``
+  (x_hi·w_hi + x_hi·w_lo + x_lo·w_hi on bf16 MFMA, f32 accumulation: their outputs feed discrete
+  decisions, duration rounding and pitch/energy buckets, SURVEY.md §0 trap 2);
+  ``vp_dtype="fp32"`` selects exact f32, ``"bf16"`` plain bf16.
+* ``"fp8"`` — cfg5: bf16 mode with the FFN Conv1d pair (and Q|K|V of blocks 1..n) on e4m3
+  MFMA; VariancePredictors as in bf16 mode.
 """
 import json
 import os
@@ -209,8 +213,9 @@ class FastSpeech2(nn.Module):
 
     # ---- precision / packed weights --------------------------------------------------------------
     def set_precision(self, dtype, vp_dtype=None):
-        """dtype of the FFT blocks / attention / mel_linear / PostNet ('fp32' | 'bf16'); vp_dtype of
-        the three VariancePredictors ('fp32' | 'bf16', bf16 only takes effect in bf16 mode)."""
+        """dtype of the FFT blocks / attention / mel_linear / PostNet ('fp32' | 'bf16' | 'fp8'); vp_dtype
+        of the three VariancePredictors ('bf16x3' default | 'fp32' exact | 'bf16'; the bf16 forms only
+        take effect in bf16 / fp8 mode, fp32 mode always runs them exact f32)."""
         if dtype not in ("fp32", "bf16", "fp8") or vp_dtype not in (None, "fp32", "bf16", "bf16x3"):
             raise ValueError("precision must be 'fp32', 'bf16' or 'fp8' (vp_dtype 'fp32' / 'bf16' / 'bf16x3')")
         self._precision = dtype
@@ -243,6 +248,14 @@ class FastSpeech2(nn.Module):
 
     def invalidate_packed(self):
         self._packs = {}
+
+    def _replicate_for_data_parallel(self):
+        # nn.DataParallel (reference train.py:42) shallow-copies __dict__ into each replica; a shared
+        # _packs dict would let replicas reuse weights packed before later optimizer steps (their
+        # broadcast parameters all carry the same _version sum). Each replica packs its own.
+        replica = super()._replicate_for_data_parallel()
+        replica._packs = {}
+        return replica
 
     def _fingerprint(self):
         return sum(p._version for p in self.parameters()) + sum(b._version for b in self.buffers())

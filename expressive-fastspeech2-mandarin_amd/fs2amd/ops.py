@@ -149,8 +149,8 @@ def pack_conv_weight_fp8(w):
 
 
 # fs2_conv_desc.splitk_ws: counters + f32 partial tiles (32 MiB covers the 128x128 kernel's tail
-# segments on 256 CUs; FS2_CONV_8PSK=1, the phased kernel's stream-K, needs 128 MiB)
-SPLITK_WS_BYTES = 4096 + ((128 << 20) if os.environ.get("FS2_CONV_8PSK") == "1" else (32 << 20))
+# segments on 256 CUs)
+SPLITK_WS_BYTES = 4096 + (32 << 20)
 _splitk_ws = {}
 _splitk_slot = [0]
 _splitk_on = [os.environ.get("FS2_CONV_SPLITK", "1") != "0"]
@@ -186,16 +186,17 @@ class splitk_slot:
 
 
 def splitk_workspace(device):
-    """The split-K tail workspace of (device, current slot): allocated zeroed on first use outside
-    graph capture (its counters must start at zero); None while capturing before it exists."""
+    """The split-K tail workspace of (device, current slot, current stream): launches on different
+    streams never share one (concurrent users would race on its arrival counters and partial
+    tiles). Allocated on first use; only the 4 KiB of counters are zeroed (they self-reset after
+    every tile), so under graph capture the first use records one small memset node."""
     if device.type != "cuda" or not _splitk_on[0]:
         return None
-    key = (device.index, _splitk_slot[0])
+    key = (device.index, _splitk_slot[0], torch.cuda.current_stream(device).cuda_stream)
     ws = _splitk_ws.get(key)
     if ws is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None
-        ws = torch.zeros(SPLITK_WS_BYTES, dtype=torch.uint8, device=device)
+        ws = torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=device)
+        ws[:4096].zero_()
         _splitk_ws[key] = ws
     return ws
 
@@ -283,13 +284,38 @@ def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None):
     return out
 
 
+_bad_ids = {}
+
+
+def bad_id_counter(device):
+    """Per-device int32 count of out-of-vocabulary token ids seen by fs2_embed_pe (their rows
+    are NaN). Allocated zeroed on first use outside graph capture."""
+    if device.type != "cuda":
+        return None
+    c = _bad_ids.get(device.index)
+    if c is None and not torch.cuda.is_current_stream_capturing():
+        c = _bad_ids[device.index] = torch.zeros(1, dtype=torch.int32, device=device)
+    return c
+
+
+def raise_if_bad_ids(device):
+    """IndexError (the reference's nn.Embedding error) if any forward on ``device`` met an
+    out-of-vocabulary token id since the last check; one device->host read."""
+    c = _bad_ids.get(device.index) if device.type == "cuda" else None
+    if c is not None:
+        n = int(c.item())
+        if n:
+            c.zero_()
+            raise IndexError(f"fs2amd: {n} token id(s) outside the embedding table (their encoder rows are NaN)")
+
+
 def embed_pe(tokens, table, pe, out_dtype):
     _gpu(tokens, table, pe)
     B, Lx = tokens.shape
     D = table.shape[1]
     out = torch.empty(B, Lx, D, device=tokens.device, dtype=torch_dtype(out_dtype))
     L.check(_lib.fs2_embed_pe(_ptr(tokens.contiguous()), _ptr(table), table.shape[0], _ptr(pe), B, Lx, D, _ptr(out),
-                              out_dtype, _stream(tokens)), "fs2_embed_pe")
+                              out_dtype, _ptr(bad_id_counter(tokens.device)), _stream(tokens)), "fs2_embed_pe")
     return out
 
 
@@ -353,12 +379,18 @@ def lr_durations(dur, logpred=False, d_control=1.0):
     return cum, mel_len, d_rounded
 
 
-def lr_expand(x, cum, mel_len, T_out, pe=None, out_dtype=None, index_map=False, out_layout=None):
-    """Frame gather (+ PE). out_layout: write only the SeqLayout's frames, packed [B*T_out, D]."""
+def lr_expand(x, cum, mel_len, T_out, pe=None, out_dtype=None, index_map=False, out_layout=None, map_only=False):
+    """Frame gather (+ PE). out_layout: write only the SeqLayout's frames, packed [B*T_out, D].
+    map_only: return only the int32 [B, T_out] source-index map (no frames are moved)."""
     _gpu(x, cum, mel_len, pe)
     x = x.contiguous()
     B, Lx, D = x.shape
     od = _dt(x) if out_dtype is None else out_dtype
+    if map_only:
+        im = torch.empty(B, T_out, device=x.device, dtype=torch.int32)
+        L.check(_lib.fs2_lr_expand(_ptr(x), _dt(x), _ptr(cum), _ptr(mel_len), B, Lx, D, T_out, None, None, od,
+                                   _ptr(im), None, _stream(x)), "fs2_lr_expand")
+        return im
     if out_layout is not None:
         assert out_layout.B == B and out_layout.T == T_out
         out = out_layout.empty(D, torch_dtype(od))

@@ -87,16 +87,16 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
         qkv = ops.conv1d(x, lp.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_BIAS,
                          out_dtype=dt, layout=layout)
     att = ops.attention(qkv, lens, H, dk, float(np.power(dk, 0.5)), layout=layout)
-    h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
-                   residual=x, ln=lp.ln1, lens=lens, layout=layout)
+    # cfg5: the fc+LN epilogue also writes the fp8 copy of h the e4m3 k=9 conv reads (one launch)
+    h8 = None
     if q is not None:
-        # cfg5: the FFN pair on e4m3 MFMA. The fc+LN epilogue also writes the fp8 copy of h the
-        # k=9 conv reads; the k=9 epilogue writes relu(.) directly as fp8 for w_2.
         h8 = (layout.empty(d_model, torch.float8_e4m3fn) if layout is not None
               else torch.empty(*x.shape[:-1], d_model, device=x.device, dtype=torch.float8_e4m3fn))
-        h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN,
-                       out_dtype=dt, residual=x, ln=lp.ln1, lens=lens, layout=layout, out2=h8,
-                       out2_scale=1.0 / q.s_h)
+    h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
+                   residual=x, ln=lp.ln1, lens=lens, layout=layout, out2=h8,
+                   out2_scale=1.0 / q.s_h if q is not None else 1.0)
+    if q is not None:
+        # cfg5: the FFN pair on e4m3 MFMA; the k=9 epilogue writes relu(.) directly as fp8 for w_2
         if timed and TIMERS is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -369,7 +369,9 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     if max_mel_len:
         T_out = int(max_mel_len)
     else:
+        # the one host read of the free-running path; out-of-vocabulary ids surface here too
         T_out = int(mel_len.max().item()) if B else 0
+        ops.raise_if_bad_ids(dev)
     if d_targets is None:
         mel_masks = _mask(mel_len, int(mel_len.max().item()) if B else 0)
     if mel_masks is None or mel_masks.shape[1] != T_out:

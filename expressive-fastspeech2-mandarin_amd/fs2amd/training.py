@@ -166,7 +166,7 @@ def _length_regulate(x, dur, max_len):
     """LengthRegulator (model/modules.py:161-194): HIP scan + source-index map, torch gather."""
     cum, mel_len, _ = ops.lr_durations(dur if dur.dtype in (torch.int64, torch.float32) else dur.to(torch.int64))
     T = int(max_len) if max_len else int(mel_len.max().item())
-    _, im = ops.lr_expand(x.detach().float().contiguous(), cum, mel_len, T, index_map=True)
+    im = ops.lr_expand(x.detach(), cum, mel_len, T, map_only=True)
     B, Lx, D = x.shape
     xz = torch.cat([x, x.new_zeros(B, 1, D)], 1)
     idx = torch.where(im < 0, torch.full_like(im, Lx), im).long()
@@ -194,7 +194,10 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
     src_lens = src_lens.to(dev)
     B, Lx = texts.shape
     src_masks = _mask(src_lens, max_src_len)
-    mel_masks = _mask(mel_lens, max_mel_len) if mel_lens is not None else None
+    if mel_lens is not None:  # get_mask_from_lengths falls back to max(lengths) (utils/tools.py:153-155)
+        mel_masks = _mask(mel_lens, max_mel_len if max_mel_len is not None else int(mel_lens.max().item()))
+    else:
+        mel_masks = None
     lens_src = src_lens.to(torch.int64).contiguous()
 
     # encoder (transformer/Models.py:73-100; training never recomputes the PE table)

@@ -149,10 +149,12 @@ int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int6
 /*
  * fs2_embed_pe — out[b,l,:] = table[tokens[b,l], :] + pe[l, :]   (f32 math)
  * Replaces Encoder src_word_emb + position_enc (transformer/Models.py:82-91).
- * tokens outside [0, vocab) are clamped (the reference raises IndexError on the host).
+ * A token outside [0, vocab) — the reference's nn.Embedding raises IndexError (CPU) or a
+ * device-side assert (GPU) — makes its output row NaN and adds 1 to *bad_ids (optional int32
+ * device counter; the Python layer raises IndexError when it reads a non-zero count).
  */
 int fs2_embed_pe(const int64_t *tokens, const float *table, int vocab, const float *pe, int B, int L, int D,
-                 void *out, int out_dtype, fs2_stream_t stream);
+                 void *out, int out_dtype, int32_t *bad_ids, fs2_stream_t stream);
 
 /*
  * fs2_cond_vectors — the per-utterance conditioning vectors added to every encoder position:
@@ -189,7 +191,8 @@ int fs2_variance_embed(void *x, int x_dtype, float *pred, const float *target, f
  * fs2_lr_expand: out[b,t,:] = (t < min(mel_len[b], T_out) ? x[b, src(b,t), :] : 0) (+ pe[t,:]),
  *   src(b,t) = first i with cum[b,i] > t.  pe (f32 [>=T_out, D]) may be NULL; a non-NULL pe
  *   fuses the Decoder's position_enc add (transformer/Models.py:158-160).  index_map (int32
- *   [B, T_out], -1 on padding) is optional.  D must be a multiple of 8.
+ *   [B, T_out], -1 on padding) is optional; with index_map given, out may be NULL (only the
+ *   map is written: the training gather's index-map-only call).  D must be a multiple of 8.
  *   out_cu (int32 [B+1], fs2_seq_layout) != NULL: packed output — only frames
  *   t < out_cu[b+1] - out_cu[b] are written, at row out_cu[b] + t.
  */

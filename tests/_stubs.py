@@ -52,10 +52,12 @@ def lr_durations(dur, logpred=False, d_control=1.0):
     return torch.cumsum(f, 1).int(), f.sum(1), None
 
 
-def lr_expand(x, cum, mel_len, T, pe=None, out_dtype=None, index_map=False, out_layout=None):
+def lr_expand(x, cum, mel_len, T, pe=None, out_dtype=None, index_map=False, out_layout=None, map_only=False):
     t = torch.arange(T)[None, :, None]
     src = (cum[:, None, :].long() <= t).sum(-1)
     im = torch.where(t[..., 0] < mel_len[:, None], src, torch.full_like(src, -1)).int()
+    if map_only:
+        return im
     return torch.zeros(x.shape[0], T, x.shape[2]), im
 
 

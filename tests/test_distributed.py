@@ -141,3 +141,24 @@ def test_ddp_train_step_gloo_world2(monkeypatch):
         if "running_" in k or "num_batches" in k:
             continue  # BN buffers: rank 0's batch statistics (broadcast_buffers)
         torch.testing.assert_close(sd0[k], v, rtol=1e-5, atol=1e-7, msg=k)
+
+
+def test_bench_launcher_starts_n_ranks():
+    """`python bench.py --gpus 2` run as ONE process (the driver's invocation) must start two
+    ranks itself and report n_gpus 2 (selftest mode: the same launcher, process group, barrier
+    and MAX/SUM bookkeeping as the GPU bench, over gloo)."""
+    import json
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--mode", "selftest"],
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2
+    assert rec["config"]["frames_total"] == 1000 + 2000  # SUM over both ranks
+    assert rec["ms_per_step"] >= 20.0 - 1e-6  # MAX over ranks (rank 1 sleeps 20 ms)

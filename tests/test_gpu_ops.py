@@ -305,6 +305,23 @@ def test_embed_pe_and_cond(ops):
     assert float((eo.cpu() - ref).abs().max()) < 1e-5
 
 
+def test_embed_pe_out_of_vocab_is_loud(ops):
+    """The reference's nn.Embedding raises on an id outside the table; here the row is NaN and
+    the next check raises IndexError (never a silent clamp to a valid row)."""
+    g = torch.Generator().manual_seed(9)
+    table, pe = torch.randn(139, 256, generator=g), torch.randn(2001, 256, generator=g)
+    tok = torch.randint(0, 139, (2, 7), generator=g)
+    tok[1, 3], tok[0, 0] = 139, -1
+    out = ops.embed_pe(tok.to(DEV), table.to(DEV), pe.to(DEV), 0).cpu()
+    assert torch.isnan(out[1, 3]).all() and torch.isnan(out[0, 0]).all()
+    ok = torch.ones(2, 7, dtype=torch.bool)
+    ok[1, 3] = ok[0, 0] = False
+    assert torch.equal(out[ok], (F.embedding(tok.clamp(0, 138), table) + pe[:7][None])[ok])
+    with pytest.raises(IndexError):
+        ops.raise_if_bad_ids(torch.device(DEV))
+    ops.raise_if_bad_ids(torch.device(DEV))  # the count was consumed
+
+
 def test_single_hip_runtime_loaded(ops):
     """Our library must share torch's HIP runtime (one libamdhip64 in the process)."""
     maps = open("/proc/self/maps").read()
