@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 GOLDEN = os.path.join(HERE, "golden")
 
 GOLDEN_CASES = ["cfg1_teacher", "cfg1_free", "mini_teacher", "mini_targets", "mini_free_ctrl",
-                "mini_free_ctrl2", "pad_base"]
+                "mini_free_ctrl2", "pad_base", "pad_ph1", "pad_ph2", "pad_ph3", "pad_fr9", "pad_fr10", "pad_fr30"]
 OUT_NAMES = ["mel", "postnet_mel", "p_pred", "e_pred", "log_d", "d_rounded", "src_masks", "mel_masks",
              "src_lens_out", "mel_lens_out"]
 
@@ -56,10 +56,11 @@ def load_case(name):
     return args, controls, outs, z
 
 
-def load_train_case():
-    """tests/golden/train_grads.npz: inputs, reference losses, per-parameter gradient sums /
-    sums of squares / 16 sampled elements, BN running stats after the step."""
-    z = np.load(os.path.join(GOLDEN, "train_grads.npz"))
+def load_train_case(name="train_grads"):
+    """tests/golden/<name>.npz (train_grads: B=4, train_b16: the cfg3 shape B=16, lengths
+    U{16..64}): inputs, reference losses, per-parameter gradient sums / sums of squares / 16
+    sampled elements, BN running stats after the step."""
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
     args = {}
     for k in z.files:
         if k.startswith("in_"):

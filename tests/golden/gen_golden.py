@@ -135,7 +135,7 @@ def lr_cases(LR):
     print("lr_cases:", list(cases))
 
 
-def train_case(FastSpeech2, pc, mc, sd):
+def train_case(FastSpeech2, pc, mc, sd, name="train_grads", shape=(4, 10, 24), seed=11):
     """One reference training step's gradients (train mode: BatchNorm batch statistics, decoder
     crop to max_seq_len), with every dropout disabled so the step is deterministic: nn.Dropout
     modules get p = 0 and the PostNet's hard-coded F.dropout(0.5) (transformer/Layers.py:133-134)
@@ -150,7 +150,7 @@ def train_case(FastSpeech2, pc, mc, sd):
     for mod in m.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.p = 0.0
-    args = synth_batch(4, 10, 24, seed=11, with_mels=True, pe_targets=True)
+    args = synth_batch(*shape, seed=seed, with_mels=True, pe_targets=True)
     orig = F.dropout
     F.dropout = lambda x, p=0.5, training=False, inplace=False: x
     try:
@@ -172,16 +172,72 @@ def train_case(FastSpeech2, pc, mc, sd):
         idx = torch.randint(0, flat.numel(), (16,), generator=g)
         rec[f"gidx_{i}"] = idx.numpy()
         rec[f"gval_{i}"] = flat[idx].numpy()
-    for name, buf in m.named_buffers():
-        if "running_" in name:
-            rec["bn_" + name] = t2n(buf)
+    for bname, buf in m.named_buffers():
+        if "running_" in bname:
+            rec["bn_" + bname] = t2n(buf)
     rec["out_mel_lens"] = t2n(out[9])
-    path = os.path.join(HERE, "train_grads.npz")
+    path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **rec)
-    print(f"train_grads: {os.path.getsize(path) / 1e3:.1f} kB, {len(keys)} grads, losses {rec['losses']}")
+    print(f"{name}: {os.path.getsize(path) / 1e3:.1f} kB, {len(keys)} grads, losses {rec['losses']}")
 
 
-def main(only=None):
+def sub_batch(batch, rows, L=None, T=None):
+    """Rows of a synth batch, re-padded to L phonemes / T frames (zero / cropped)."""
+    out = {}
+    for k, v in batch.items():
+        out[k] = v[rows] if torch.is_tensor(v) and v.dim() >= 1 else v
+    L = int(out["src_lens"].max()) if L is None else L
+    out["max_src_len"] = L
+    for k in ("texts", "d_targets", "p_targets", "e_targets"):
+        if out.get(k) is not None:
+            v = out[k]
+            out[k] = torch.nn.functional.pad(v, (0, max(0, L - v.shape[1])))[:, :L]
+    if out.get("mel_lens") is not None:
+        out["mel_lens"] = out["d_targets"].sum(1)
+        out["max_mel_len"] = int(out["mel_lens"].max()) if T is None else T
+    return out
+
+
+def padding_class_cases(model, LR):
+    """SURVEY.md §8a padding classes, each case a 2-utterance batch whose utterance 0 is the same
+    base utterance (20 phonemes, teacher-forced): the output for it depends on the phoneme padding
+    L_max - L_0 in {0, 1, >=2} (VariancePredictor receptive field +-2: it reads the conditioning
+    vectors and pitch embeddings in padded slots) and on the frame padding T_max - T_0 in
+    {0..9, >=10} (PostNet receptive field +-10: it reads mel_linear's bias in padded frames).
+    Companions are 1 / 2 / 3 phonemes longer (same frame count as the base), and the same length
+    with 9 / 10 / 30 frames more."""
+    g = torch.Generator().manual_seed(21)
+    base = synth_batch(1, 20, seed=6)
+    L0, T0 = 20, int(base["mel_lens"][0])
+    for extra in (1, 2, 3):
+        comp = synth_batch(1, L0 + extra, seed=30 + extra)
+        d = torch.zeros(1, L0 + extra, dtype=torch.int64)
+        d[0, :L0 + extra] = 1
+        # same total frames as the base: spread T0 frames over L0 + extra phonemes
+        q, r = divmod(T0, L0 + extra)
+        d[0] = q
+        d[0, :r] += 1
+        comp["d_targets"], comp["mel_lens"], comp["max_mel_len"] = d, d.sum(1), int(d.sum())
+        pair = {k: torch.cat([torch.nn.functional.pad(base[k], (0, extra)) if base[k].dim() == 2 else base[k],
+                              comp[k]]) if torch.is_tensor(base[k]) else base[k] for k in base}
+        pair["max_src_len"], pair["max_mel_len"] = L0 + extra, max(T0, int(d.sum()))
+        run_case(model, LR, f"pad_ph{extra}", pair)
+    for extra in (9, 10, 30):
+        comp = synth_batch(1, L0, seed=40 + extra)
+        d = comp["d_targets"].clone()
+        while int(d.sum()) != T0 + extra:  # adjust to exactly T0 + extra frames, durations >= 1
+            i = int(torch.randint(0, L0, (1,), generator=g))
+            if int(d.sum()) < T0 + extra:
+                d[0, i] += 1
+            elif d[0, i] > 1:
+                d[0, i] -= 1
+        comp["d_targets"], comp["mel_lens"], comp["max_mel_len"] = d, d.sum(1), int(d.sum())
+        pair = {k: torch.cat([base[k], comp[k]]) if torch.is_tensor(base[k]) else base[k] for k in base}
+        pair["max_src_len"], pair["max_mel_len"] = L0, T0 + extra
+        run_case(model, LR, f"pad_fr{extra}", pair)
+
+
+def main(only=None, only2=None):
     FastSpeech2, LR = import_reference()
     torch.manual_seed(0)
     tmp = tempfile.mkdtemp(prefix="fs2_golden_")
@@ -195,6 +251,12 @@ def main(only=None):
     sd = model.state_dict()
     if only == "train":
         train_case(FastSpeech2, pc, mc, sd)
+        return
+    if only == "round2":  # round-2 additions (the round-1 fixtures above stay byte-identical)
+        if only2 != "train16":
+            padding_class_cases(model, LR)
+            run_case(model, LR, "cfg2_free", synth_batch(64, 64, seed=1, teacher=False), save_full=False)
+        train_case(FastSpeech2, pc, mc, sd, name="train_b16", shape=(16, 16, 64), seed=12)
         return
     manifest = {"reference": REF, "torch": torch.__version__, "weights_seed": 0, "n_keys": len(sd), "keys": {}}
     for k, v in sd.items():
@@ -229,4 +291,4 @@ def main(only=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else None)
+    main(*(sys.argv[1:3]))

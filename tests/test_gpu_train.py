@@ -17,12 +17,12 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-def _step(prec):
+def _step(prec, case="train_grads"):
     from fs2amd.data import loss_inputs, to_device
     from fs2amd.loss import FastSpeech2Loss
     from fs2amd.model import FastSpeech2
 
-    z, args = load_train_case()
+    z, args = load_train_case(case)
     pc, mc, _ = configs()
     m = FastSpeech2(pc, mc)
     m.load_state_dict(oracle_state_dict())
@@ -42,8 +42,10 @@ def gpu():
         pytest.skip("no ROCm device")
 
 
-def test_train_step_fp32_matches_reference_gradients(gpu):
-    z, m, losses, out = _step("fp32")
+@pytest.mark.parametrize("case", ["train_grads", "train_b16"])
+def test_train_step_fp32_matches_reference_gradients(gpu, case):
+    """train_grads: B=4; train_b16: the cfg3 per-GPU shape (B=16, lengths U{16..64})."""
+    z, m, losses, out = _step("fp32", case)
     np.testing.assert_allclose([float(l) for l in losses], z["losses"], rtol=1e-4)
     np.testing.assert_array_equal(out[9].cpu().numpy(), z["out_mel_lens"])
     named = {k: p.grad for k, p in m.named_parameters() if p.grad is not None}
@@ -54,11 +56,12 @@ def test_train_step_fp32_matches_reference_gradients(gpu):
             np.testing.assert_allclose(bufs[k[3:]].cpu().numpy(), z[k], rtol=1e-4, atol=1e-6)
 
 
-def test_train_step_bf16_within_tolerance(gpu):
-    z, m, losses, _ = _step("bf16")
+@pytest.mark.parametrize("case", ["train_grads", "train_b16"])
+def test_train_step_bf16_within_tolerance(gpu, case):
+    z, m, losses, _ = _step("bf16", case)
     np.testing.assert_allclose([float(l) for l in losses], z["losses"], rtol=3e-2)
     # reference gradient direction from the fp32 HIP step (itself pinned by the test above)
-    _, m32, _, _ = _step("fp32")
+    _, m32, _, _ = _step("fp32", case)
     g16 = torch.cat([p.grad.reshape(-1) for _, p in sorted(m.named_parameters()) if p.grad is not None])
     g32 = torch.cat([p.grad.reshape(-1) for _, p in sorted(m32.named_parameters()) if p.grad is not None])
     cos = float(torch.nn.functional.cosine_similarity(g16.double(), g32.double(), dim=0))
