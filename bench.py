@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="replay the forward as a captured HIP graph")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--kernel-reps", type=int, default=20)
+    ap.add_argument("--extra", type=int, default=1,
+                    help="also time free-running cfg2, cfg4 (B=256) and cfg5 (fp8) as extra keys of the JSON line")
     ap.add_argument("--mode", default="infer", choices=["infer", "train", "selftest"],
                     help="infer: the headline cfg2 forward; train: the cfg3 train.py step (B=16/GPU, DDP); "
                          "selftest: the launcher / process-group / timing bookkeeping only (gloo, no GPU)")
@@ -164,8 +166,8 @@ def time_dominant_kernel(model, batch, device, reps):
 
 
 def cpu_baseline(batch_cpu, pc, mc, budget_s=20.0):
-    """The oracle (reference restatement, fp32 PyTorch CPU) on a bounded sample."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
+    """The oracle (reference restatement, fp32 PyTorch CPU, bit-exact to the reference's goldens)
+    on the SAME 64-utterance batch the GPU headline runs, repeated for about budget_s seconds."""
     from oracle import fs2_oracle as O
     from fs2amd.synth_weights import synth_state_dict
     from fs2amd import config as C
@@ -175,27 +177,20 @@ def cpu_baseline(batch_cpu, pc, mc, budget_s=20.0):
     torch.set_num_threads(threads)
     shapes = {k: tuple(v.shape) for k, v in FastSpeech2(pc, mc).state_dict().items()}
     sd = O.build_state_dict(mc, pc, C.SYNTH_STATS, synth_state_dict(shapes, seed=0))
-    n = 8  # utterances per sample forward (a slice of the same batch)
-    sub = {k: (v[:n] if torch.is_tensor(v) and v.dim() >= 1 and v.shape[0] == batch_cpu["texts"].shape[0] else v)
-           for k, v in batch_cpu.items()}
-    sub["max_src_len"] = int(sub["src_lens"].max())
-    sub["max_mel_len"] = int(sub["mel_lens"].max())
-    sub["texts"] = sub["texts"][:, :sub["max_src_len"]]
-    sub["d_targets"] = sub["d_targets"][:, :sub["max_src_len"]]
-    frames = int(sub["mel_lens"].sum())
+    frames = int(batch_cpu["mel_lens"].sum())
     with torch.no_grad():
-        O.forward(sd, mc, pc, **sub)  # warm-up
         t0 = time.perf_counter()
-        reps = 0
-        while True:
-            O.forward(sd, mc, pc, **sub)
-            reps += 1
-            if time.perf_counter() - t0 > budget_s or reps >= 50:
-                break
+        O.forward(sd, mc, pc, **batch_cpu)  # warm-up (also sizes the sample)
+        one = time.perf_counter() - t0
+        reps = max(1, min(20, int(budget_s / max(one, 1e-3))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            O.forward(sd, mc, pc, **batch_cpu)
         dt = time.perf_counter() - t0
+    B = int(batch_cpu["texts"].shape[0])
     return {"value": round(frames * reps / dt, 1), "unit": "mel-frames/s", "cores": threads, "kind": "port",
-            "sample": f"oracle fp32 forward, {n} of the 64 utterances ({frames} frames) x {reps} reps, "
-                      f"{dt:.1f} s, torch.set_num_threads({threads})"}
+            "sample": f"oracle fp32 forward on the benched cfg2 batch ({B} utterances, {frames} frames) x {reps} "
+                      f"reps after 1 warm-up, {dt:.1f} s, torch.set_num_threads({threads})"}
 
 
 def load_traffic(dtype="bf16"):
@@ -250,6 +245,84 @@ def main_train(args, rank, world, device):
     parallel.shutdown()
 
 
+def timed_steps(model, batch, device, steps, warmup, graph, frames_out=None):
+    """W untimed warmups, then EXACTLY `steps` forwards bracketed by barrier + device sync on both
+    sides; returns this rank's elapsed seconds. graph: the forward is captured once as a HIP graph
+    and replayed (needs a sync-free forward: teacher-forced / max_mel_len given)."""
+    from fs2amd import parallel
+
+    def step():
+        with torch.no_grad():
+            return model(**batch)
+
+    for _ in range(max(1, warmup)):
+        out = step()
+    torch.cuda.synchronize(device)
+    run = step
+    if graph:
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                step()
+        torch.cuda.current_stream(device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = step()
+        g.replay()
+        torch.cuda.synchronize(device)
+        run = g.replay
+    if frames_out is not None:
+        frames_out.append(int(out[9].sum()))
+    parallel.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize(device)
+    parallel.barrier()
+    return time.perf_counter() - t0
+
+
+def extra_workloads(model, args, rank, device):
+    """The other BASELINE configs as extra keys on the same JSON line (same barrier / MAX-over-
+    ranks bookkeeping, fewer steps):
+    * free_running_cfg2 — the synthesis path of synthesize_chinese_pinyin.py:140-145: durations
+      predicted and rounded, no max_mel_len, so one device->host read of max(mel_len) per
+      forward and no graph capture (eager launches);
+    * cfg4_b256 — B=256, 16..160 phonemes, teacher-forced, graph-replayed (LengthRegulator and
+      ragged-padding stress);
+    * cfg5_fp8 — cfg2 with the FFN pair (and Q|K|V of blocks 1..n) on e4m3 MFMA, graph-replayed
+      (only when the headline runs bf16)."""
+    from fs2amd import parallel
+    from fs2amd.data import synth_batch, to_device
+
+    res = {}
+    steps = max(3, args.steps // 2)
+    prec = model.precision
+
+    def record(name, batch_cpu, graph, note):
+        b = to_device(batch_cpu, device)
+        got = []
+        el = timed_steps(model, b, device, steps, 2, graph, frames_out=got)
+        el, fr = parallel.aggregate(el, got[0], device)
+        res[name] = {"value": round(fr * steps / el, 1), "unit": "mel-frames/s", "ms_per_step": round(el / steps * 1e3, 4),
+                     "steps": steps, "frames_per_step": fr, "hip_graph": graph, "dtype": model.precision, "note": note}
+
+    record("free_running_cfg2", synth_batch(args.batch, args.phonemes, seed=1 + rank, teacher=False), False,
+           "durations predicted + rounded (modules.py:131-137), one D2H read of max(mel_len), eager")
+    record("cfg4_b256", synth_batch(256, 16, 160, seed=1 + rank), True,
+           "B=256 x U{16..160} phonemes, teacher-forced durations U{2..10}")
+    if prec == "bf16":
+        cal = synth_batch(args.batch, args.phonemes, seed=1000 + rank)
+        model.set_precision("fp8")
+        model.calibrate_fp8(**to_device(cal, device))
+        record("cfg5_fp8", synth_batch(args.batch, args.phonemes, seed=1 + rank), True,
+               "cfg2 with e4m3 FFN + Q|K|V GEMMs (static calibrated scales); tolerance vs bf16 in tests/test_gpu_fp8.py")
+        model.set_precision(prec)
+    return res
+
+
 def main_selftest(args, rank, world, device):
     """The N-rank bookkeeping of the bench without a model: barrier + timed region + MAX/SUM over
     ranks, one JSON line from rank 0 (tests/test_distributed.py runs it over gloo on CPU)."""
@@ -298,37 +371,9 @@ def main():
         # static activation scales from a calibration batch of the same shape (different seed)
         model.calibrate_fp8(**to_device(synth_batch(args.batch, args.phonemes, seed=1000 + rank), device))
 
-    def step():
-        with torch.no_grad():
-            return model(**batch)
-
-    for _ in range(max(1, args.warmup)):
-        out = step()
-    torch.cuda.synchronize(device)
-    graph = None
-    if args.graph:
-        s = torch.cuda.Stream(device)
-        s.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                step()
-        torch.cuda.current_stream(device).wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            out = step()
-        graph.replay()
-        torch.cuda.synchronize(device)
-
-    run = graph.replay if graph is not None else step
-    parallel.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize(device)
-    parallel.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_steps(model, batch, device, args.steps, args.warmup, bool(args.graph))
     elapsed, tot_frames = parallel.aggregate(elapsed, frames, device)
+    extra = extra_workloads(model, args, rank, device) if args.extra else {}
 
     kernel_s, n_launch = time_kernel_in_forward(model, batch)
     standalone_s, kernel_flops = time_dominant_kernel(model, batch_cpu, device, args.kernel_reps)
@@ -370,6 +415,8 @@ def main():
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(batch_cpu, pc, mc)
+    if extra:
+        rec["extra"] = extra
     if rank == 0:
         print(json.dumps(rec), flush=True)
     parallel.shutdown()
