@@ -237,6 +237,47 @@ def padding_class_cases(model, LR):
         run_case(model, LR, f"pad_fr{extra}", pair)
 
 
+def pipeline_case(pc, mc):
+    """The reference's own batch assembly (dataset_chinese.py Dataset / TextDataset collate_fn and
+    utils/tools.py to_device on CPU) over the deterministic synthetic corpus
+    fs2amd.pipeline.write_synthetic_corpus(dir, 24, seed=0, long_every=11): every array of every
+    15- / 9-tuple (batch_size 4, sorted and unsorted, drop_last both ways)."""
+    from fs2amd.pipeline import write_synthetic_corpus
+    from fs2amd import config as C
+    sys.path.insert(0, REF)
+    import dataset_chinese as D
+    from utils.tools import to_device
+
+    d = write_synthetic_corpus(tempfile.mkdtemp(prefix="fs2_corpus_"), 24, seed=0, long_every=11, max_seq_len=2000)
+    pc = dict(pc, path={"preprocessed_path": d})
+    tc = C.ESD_TRAIN_CONFIG
+    rec = {}
+    for tag, (fname, sort, drop) in {"train_sorted": ("train.txt", True, False), "train_drop": ("train.txt", True, True),
+                                      "val_plain": ("val.txt", False, False)}.items():
+        ds = D.Dataset(fname, pc, mc, tc, sort=sort, drop_last=drop)
+        batches = ds.collate_fn([ds[i] for i in range(len(ds))])
+        rec[f"{tag}__n"] = np.array(len(batches))
+        for j, b in enumerate(batches):
+            tb = to_device(b, torch.device("cpu"))
+            for k, v in enumerate(tb):
+                key = f"{tag}__{j}__{k}"
+                if torch.is_tensor(v):
+                    rec[key] = v.numpy()
+                    rec[key + "__dtype"] = np.array(str(v.dtype))
+                elif isinstance(v, list):
+                    rec[key] = np.array(v)
+                else:
+                    rec[key] = np.array(v)
+    td = D.TextDataset(os.path.join(d, "val.txt"), pc, mc)
+    tb = to_device(td.collate_fn([td[i] for i in range(len(td))]), torch.device("cpu"))
+    for k, v in enumerate(tb):
+        rec[f"text__{k}"] = v.numpy() if torch.is_tensor(v) else np.array(v)
+        if torch.is_tensor(v):
+            rec[f"text__{k}__dtype"] = np.array(str(v.dtype))
+    np.savez_compressed(os.path.join(HERE, "pipeline_batches.npz"), **rec)
+    print("pipeline_batches:", {k: int(v) for k, v in rec.items() if k.endswith("__n")})
+
+
 def main(only=None, only2=None):
     FastSpeech2, LR = import_reference()
     torch.manual_seed(0)
@@ -251,6 +292,9 @@ def main(only=None, only2=None):
     sd = model.state_dict()
     if only == "train":
         train_case(FastSpeech2, pc, mc, sd)
+        return
+    if only == "pipeline":
+        pipeline_case(pc, mc)
         return
     if only == "round2":  # round-2 additions (the round-1 fixtures above stay byte-identical)
         if only2 != "train16":

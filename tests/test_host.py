@@ -274,3 +274,44 @@ def test_pack_conv_weight_layout(compute, cin):
     assert p.shape == (12, 5, ops.cin_pad(cin, compute))
     torch.testing.assert_close(p[:, :, :cin].float(), w.permute(0, 2, 1).to(p.dtype).float())
     assert not p[:, :, cin:].float().abs().sum()
+
+
+def test_checkpoint_resume_round_trip(tmp_path):
+    """train.py:151-161 save -> utils/model.py:11-34 restore: the 240-key model state, Adam's
+    moments and the Noam step counter (model/optimizer.py:19) come back, and one more step from
+    the restored pair equals one more step of the original (CPU, gradients injected)."""
+    import types
+    from fs2amd import config as C
+    from fs2amd.checkpoint import checkpoint_path, get_model, load_checkpoint, save_checkpoint
+    from fs2amd.optimizer import ScheduledOptim
+
+    pc, mc, _ = configs()
+    tc = dict(C.ESD_TRAIN_CONFIG, path={"ckpt_path": str(tmp_path)})
+    m = _model()
+    opt = ScheduledOptim(m, tc, mc, 0)
+    g = torch.Generator().manual_seed(0)
+    grads = [[torch.randn(p.shape, generator=g) * 1e-2 for p in m.parameters()] for _ in range(3)]
+
+    def step(model, o, gs):
+        for p, gr in zip(model.parameters(), gs):
+            p.grad = gr.clone() if p.requires_grad else None
+        o.step_and_update_lr()
+        o.zero_grad()
+
+    step(m, opt, grads[0])
+    step(m, opt, grads[1])
+    save_checkpoint(checkpoint_path(tc, 2), m, opt)
+    ck = load_checkpoint(checkpoint_path(tc, 2))
+    assert set(ck) == {"model", "optimizer"} and len(ck["model"]) == 240
+    m2, opt2 = get_model(types.SimpleNamespace(restore_step=2), (pc, mc, tc), "cpu", train=True)
+    assert opt2.current_step == 2 and m2.training
+    for (k, a), b in zip(m.state_dict().items(), m2.state_dict().values()):
+        assert torch.equal(a, b), k
+    step(m, opt, grads[2])
+    step(m2, opt2, grads[2])
+    assert opt.current_step == opt2.current_step == 3
+    assert opt._optimizer.param_groups[0]["lr"] == opt2._optimizer.param_groups[0]["lr"]
+    for (k, a), b in zip(m.state_dict().items(), m2.state_dict().values()):
+        assert torch.equal(a, b), k
+    ev = get_model(types.SimpleNamespace(restore_step=2), (pc, mc, tc), "cpu")
+    assert not ev.training
