@@ -181,6 +181,13 @@ struct ConvArgs {
   int row_split;
   int split_slots;          // workgroups the phased kernel runs at once (one per CU)
   int ln_pairs;             // LayerNorm epilogues: two rows per wave-iteration, 16-byte stores
+  // vocoder extensions (fs2_conv_desc): dilated taps, leaky-ReLU epilogue / out2 activation,
+  // two-addend residual sum with a final divisor
+  int dil;
+  float slope, slope2;
+  int out2_act, out2_f32;
+  const void *res2;
+  float out_div;
 };
 
 constexpr int64_t kSkCntBytes = 4096;  // counter block at the start of the split-K workspace
@@ -615,12 +622,27 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
       } else if (epi == FS2_EPI_BIAS_TANH) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = tanhf(v[q]);
-      } else if (epi == FS2_EPI_BIAS_RES) {
+      } else if (epi == FS2_EPI_BIAS_RES || epi == FS2_EPI_RES_SUM) {
         float rv[8];
         load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n, rv);
         load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n + 4, rv + 4);
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] += rv[q];
+        if (epi == FS2_EPI_RES_SUM) {
+          if (a.res2 != nullptr) {
+            load_any4(a.res2, a.out_dt, (int64_t)m * a.os + n, rv);
+            load_any4(a.res2, a.out_dt, (int64_t)m * a.os + n + 4, rv + 4);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] += rv[q];
+          }
+          if (a.out_div != 1.0f) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = v[q] / a.out_div;
+          }
+        }
+      } else if (epi == FS2_EPI_BIAS_LRELU) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.0f ? v[q] : v[q] * a.slope;
       }
       const int64_t o = (int64_t)m * a.os + n;
       if (a.out_dt == FS2_BF16)
@@ -630,7 +652,16 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
       else
         *reinterpret_cast<uint2 *>(reinterpret_cast<fp8 *>(a.out) + o) =
             make_uint2(pack4_fp8(v, a.out_scale), pack4_fp8(v + 4, a.out_scale));
-      if (a.out2 != nullptr) store8(reinterpret_cast<bf16 *>(a.out2) + (int64_t)m * a.N + n, v);
+      if (a.out2 != nullptr) {
+        if (a.out2_act) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.0f ? v[q] : v[q] * a.slope2;
+        }
+        if (a.out2_f32)
+          store8(reinterpret_cast<float *>(a.out2) + (int64_t)m * a.N + n, v);
+        else
+          store8(reinterpret_cast<bf16 *>(a.out2) + (int64_t)m * a.N + n, v);
+      }
     }
     return;
   }
@@ -657,14 +688,37 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
     } else if (epi == FS2_EPI_BIAS_TANH) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
-    } else if (epi == FS2_EPI_BIAS_RES) {
+    } else if (epi == FS2_EPI_BIAS_RES || epi == FS2_EPI_RES_SUM) {
       float rv[4];
       load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n, rv);
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] += rv[q];
+      if (epi == FS2_EPI_RES_SUM) {
+        if (a.res2 != nullptr) {
+          load_any4(a.res2, a.out_dt, (int64_t)m * a.os + n, rv);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += rv[q];
+        }
+        if (a.out_div != 1.0f) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = v[q] / a.out_div;
+        }
+      }
+    } else if (epi == FS2_EPI_BIAS_LRELU) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.0f ? v[q] : v[q] * a.slope;
     }
     store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, v, a.out_scale);
-    if (a.out2 != nullptr) store4(reinterpret_cast<bf16 *>(a.out2) + (int64_t)m * a.N + n, v);
+    if (a.out2 != nullptr) {
+      if (a.out2_act) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.0f ? v[q] : v[q] * a.slope2;
+      }
+      if (a.out2_f32)
+        store4(reinterpret_cast<float *>(a.out2) + (int64_t)m * a.N + n, v);
+      else
+        store4(reinterpret_cast<bf16 *>(a.out2) + (int64_t)m * a.N + n, v);
+    }
   }
 }
 
@@ -781,8 +835,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
   int M, m0, n0, seg, nseg, tl;
   if (!conv_tile_sk<BM>(a, BN, M, m0, n0, seg, nseg, tl)) return;
 
-  const int KS = a.KS, pad = a.pad;
-  const int H = BM + KS - 1;
+  const int KS = a.KS, pad = a.pad, dil = a.dil;
+  const int H = BM + (KS - 1) * dil;  // halo rows: the tile + the taps' span
   const int nCk = a.Cin_pad / KE;
   const int nK = KS * nCk;
   const int T = a.T;
@@ -887,14 +941,15 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
   const int bf8_1 = lds_off(wc * WCOL + (lane & 15), 2 * (lane >> 4) + 1);
   auto compute = [&](int aslot, int tap, const char *Bs, bool fresh) {
     const char *As = Abuf + aslot * A_BYTES;
-    const int sh = tap - pad;
+    const int toff = tap * dil;  // halo row offset of this tap
+    const int sh = toff - pad;
     const bool need_mask = !(wave_inside && tw + sh >= 0 && tw + WROWS - 1 + sh < lw);
     bool vrow[WMI];
 #pragma unroll
     for (int mi = 0; mi < WMI; ++mi) vrow[mi] = (unsigned)(tpos[mi] + sh) < (unsigned)tlen[mi];
     if constexpr (CT == FS2_FP8) {
-      const char *A0 = As + lds_off(arow0 + tap, 2 * (lane >> 4));
-      const char *A1 = As + lds_off(arow0 + tap, 2 * (lane >> 4) + 1);
+      const char *A0 = As + lds_off(arow0 + toff, 2 * (lane >> 4));
+      const char *A1 = As + lds_off(arow0 + toff, 2 * (lane >> 4) + 1);
       i32x8 af[WMI], bfr[NI];
 #pragma unroll
       for (int mi = 0; mi < WMI; ++mi) af[mi] = frag_fp8(A0 + mi * 16 * kRowBytes, A1 + mi * 16 * kRowBytes);
@@ -913,7 +968,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const char *Ab = As + lds_off(arow0 + tap, s * 4 + (lane >> 4));
+      const char *Ab = As + lds_off(arow0 + toff, s * 4 + (lane >> 4));
       const char *Bb = Bs + (s ? bread1 : bread0);
       if constexpr (CT == FS2_BF16) {
         bf16x8 af[WMI], bfr[NI];
@@ -992,10 +1047,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
       const uint32_t off = ((uint32_t)tap * a.Cin_pad + cb * KE) * (uint32_t)sizeof(TW) + bcol;
       char *Bs = Bbuf + buf * B_BYTES;
 #pragma unroll
-      for (int it = 0; it < BP / NW; ++it) {
+      for (int it = 0; it < (BP + NW - 1) / NW; ++it) {  // narrow tiles: fewer B pieces than waves
         const int p = wid + NW * it;
         const int n = n0 + 8 * p + prow;
-        glds(wr_, Bs + p * 1024, n < a.N ? (uint32_t)n * wrow + off : kOOB);
+        if (BP % NW == 0 || p < BP) glds(wr_, Bs + p * 1024, n < a.N ? (uint32_t)n * wrow + off : kOOB);
       }
     };
     {
@@ -1685,8 +1740,28 @@ void launch_128(ConvArgs a, hipStream_t s) {
     launch<CT, 2, 2, 4, 9, TIn>(a, s);
 }
 
+// Dilated / long-span / narrow-N convs (the HiFi-GAN generator: kernels 3-11, dilations 1-5,
+// 512 -> 32 channels): A halo sized for a 51-row tap span, tile width matched to N so the 32- and
+// 64-channel stages do not run 128-wide tiles of zeros. LDS-DMA path only (input already in the
+// compute dtype).
+template <int CT, typename TIn>
+bool dispatch_wide_taps(const ConvArgs &a, hipStream_t s) {
+  if constexpr (std::is_same<TIn, typename CTraits<CT>::T>::value && CT != FS2_FP8) {
+    if (a.N <= 32)
+      launch<CT, 4, 1, 2, 51, TIn, 32>(a, s);  // 128 x 32, 4 waves of 32 x 32
+    else if (a.N <= 64)
+      launch<CT, 2, 2, 4, 51, TIn, 32>(a, s);  // 128 x 64, 4 waves of 64 x 32
+    else
+      launch<CT, 2, 4, 4, 51, TIn, 32>(a, s);  // 128 x 128, 8 waves of 64 x 32
+    return true;
+  }
+  return false;
+}
+
 template <int CT, typename TIn>
 void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
+  if (!ln && (a.dil > 1 || (a.KS - 1) * a.dil + 1 > 9 || a.N <= 64))
+    if (dispatch_wide_taps<CT, TIn>(a, s)) return;
   if constexpr (CT == FS2_BF16 && std::is_same<TIn, bf16>::value) {
     // Large bf16 convs (decoder FFN conv-k9, PostNet k=5): the phased 256x256 kernel runs the
     // whole rounds of its tiles (44 % of dense peak on full rounds vs 36 % for 128x128), the
@@ -1815,13 +1890,15 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   if ((d->x_row_stride % ce) != 0) return FS2_EINVAL;
   if (d->out_split && (d->out_dtype != FS2_BF16 || d->out_row_stride < 2 * (int64_t)d->N)) return FS2_EINVAL;
   const int epi = d->epilogue;
-  if (epi < FS2_EPI_BIAS || epi > FS2_EPI_RELU_LN_DOT) return FS2_EINVAL;
+  if (epi < FS2_EPI_BIAS || epi > FS2_EPI_RES_SUM) return FS2_EINVAL;
   const bool ln = epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN || epi == FS2_EPI_RELU_LN_DOT;
   if (ln && (d->N != 256 || d->ln_gamma == nullptr || d->ln_beta == nullptr || d->bias == nullptr)) return FS2_EINVAL;
-  if ((epi == FS2_EPI_RES_LN || epi == FS2_EPI_BIAS_RES) && d->residual == nullptr) return FS2_EINVAL;
+  if ((epi == FS2_EPI_RES_LN || epi == FS2_EPI_BIAS_RES || epi == FS2_EPI_RES_SUM) && d->residual == nullptr)
+    return FS2_EINVAL;
   if (epi == FS2_EPI_RELU_LN_DOT && (d->dot_w == nullptr || d->out_dtype != FS2_F32)) return FS2_EINVAL;
   if (epi != FS2_EPI_RELU_LN_DOT && (d->out_row_stride < d->N || (d->out_row_stride & 3) != 0)) return FS2_EINVAL;
-  if ((epi == FS2_EPI_RES_LN || epi == FS2_EPI_BIAS_RES) && (d->res_row_stride < d->N || (d->res_row_stride & 3)))
+  if ((epi == FS2_EPI_RES_LN || epi == FS2_EPI_BIAS_RES || epi == FS2_EPI_RES_SUM) &&
+      (d->res_row_stride < d->N || (d->res_row_stride & 3)))
     return FS2_EINVAL;
   const int64_t M64 = (int64_t)d->B * d->T;
   if (M64 > 0x7fffff00LL) return FS2_EINVAL;
@@ -1908,7 +1985,20 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   hipStream_t s = as_stream(stream);
   if (d->x_dtype != FS2_BF16 && d->x_dtype != FS2_F32 && d->x_dtype != FS2_FP8) return FS2_EUNSUPPORTED;
   if (d->out2 != nullptr && (epi == FS2_EPI_RELU_LN_DOT || (!ln && d->out_split))) return FS2_EINVAL;
-  if (d->KS > (ln ? 3 : 9)) return FS2_EUNSUPPORTED;
+  const int dil = d->dilation > 1 ? d->dilation : 1;
+  const int span = (d->KS - 1) * dil + 1;
+  if (ln ? (d->KS > 3 || dil != 1) : (d->KS > 11 || span > 51)) return FS2_EUNSUPPORTED;
+  const bool wide = !ln && (dil > 1 || span > 9 || d->N <= 64);
+  if (wide && (d->x_dtype != d->compute || d->compute == FS2_FP8 || d->a_rowmap != nullptr || d->cin_block != 0))
+    return FS2_EUNSUPPORTED;  // the wide-tap tiles read the compute dtype by LDS-DMA
+  if ((d->out2_act || d->out2_f32) && (ln || d->out2 == nullptr)) return FS2_EINVAL;
+  a.dil = dil;
+  a.slope = d->act_slope;
+  a.slope2 = d->out2_slope;
+  a.out2_act = d->out2_act;
+  a.out2_f32 = d->out2_f32;
+  a.res2 = d->residual2;
+  a.out_div = d->out_div != 0.0f ? d->out_div : 1.0f;
   const bool xb = d->x_dtype == FS2_BF16;
   if (d->compute == FS2_FP8)
     dispatch<FS2_FP8, fp8>(a, ln, s);

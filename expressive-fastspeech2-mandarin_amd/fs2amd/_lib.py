@@ -17,7 +17,8 @@ DEFAULT_LIB = os.path.join(HERE, "_lib", "libfs2hip.so")
 
 FS2_F32, FS2_BF16, FS2_FP8 = 0, 1, 2
 FS2_OK, FS2_EINVAL, FS2_ELAUNCH, FS2_EUNSUPPORTED = 0, 1, 2, 3
-(EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_TANH, EPI_BIAS_RES, EPI_RES_LN, EPI_RELU_LN, EPI_RELU_LN_DOT) = range(7)
+(EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_TANH, EPI_BIAS_RES, EPI_RES_LN, EPI_RELU_LN, EPI_RELU_LN_DOT, EPI_BIAS_LRELU,
+ EPI_RES_SUM) = range(9)
 DUR_I64, DUR_F32, DUR_LOGPRED = 0, 1, 2
 
 _p = ctypes.c_void_p
@@ -43,6 +44,8 @@ class ConvDesc(ctypes.Structure):
         ("col_scale", _p), ("out_scale", _f), ("out2", _p), ("out2_scale", _f),
         ("cin_block", _i), ("cin_src", _i * 4), ("out_split", _i),
         ("splitk_ws", _p), ("splitk_ws_bytes", _i64),
+        ("dilation", _i), ("act_slope", _f), ("out2_act", _i), ("out2_slope", _f), ("out2_f32", _i),
+        ("residual2", _p), ("out_div", _f),
     ]
 
 

@@ -203,12 +203,15 @@ def splitk_workspace(device):
 
 def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None, out=None, residual=None,
            ln=None, lens=None, addvec1=None, addvec2=None, dot=None, n=None, layout=None, src_layout=None,
-           col_scale=None, out_scale=1.0, out2=None, out2_scale=1.0, cin_block=0, cin_src=(), out_split=False):
+           col_scale=None, out_scale=1.0, out2=None, out2_scale=1.0, cin_block=0, cin_src=(), out_split=False,
+           dilation=1, act_slope=0.0, out2_act=False, out2_slope=0.0, residual2=None, out_div=1.0):
     """Implicit-GEMM Conv1d / Linear with a fused epilogue (fs2_conv1d).
 
     layout: x / residual / out are packed [B*T, C] in that SeqLayout. src_layout (KS == 1): x is
-    packed in it, out is padded [B, T, N] (zeros in, i.e. bias out, at padding)."""
-    _gpu(x, w_packed, bias, residual, lens, addvec1, addvec2)
+    packed in it, out is padded [B, T, N] (zeros in, i.e. bias out, at padding).
+    Vocoder extensions: dilation (tap k reads row t + k*dilation - pad), act_slope (EPI_BIAS_LRELU),
+    out2_act / out2_slope (out2 = leaky_relu(y)), out2 may be f32, residual2 / out_div (EPI_RES_SUM)."""
+    _gpu(x, w_packed, bias, residual, lens, addvec1, addvec2, residual2)
     if layout is not None or src_layout is not None:
         lay = layout if layout is not None else src_layout
         B, T = lay.B, lay.T
@@ -244,6 +247,11 @@ def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None
     d.out_scale = float(out_scale)
     if out2 is not None:
         d.out2, d.out2_scale = out2.data_ptr(), float(out2_scale)
+        d.out2_f32 = 1 if out2.dtype == torch.float32 else 0
+        d.out2_act, d.out2_slope = (1 if out2_act else 0), float(out2_slope)
+    d.dilation, d.act_slope, d.out_div = int(dilation), float(act_slope), float(out_div)
+    if residual2 is not None:
+        d.residual2 = residual2.data_ptr()
     if layout is not None:
         d.rows_dev, d.row_pos = layout.rows_dev, layout.row_pos.data_ptr()
     if src_layout is not None:

@@ -96,6 +96,48 @@ def synth_state_dict(shapes, seed=0):
     return out
 
 
+def _vocoder_role(name, shape, ups_meta):
+    """HiFi-GAN generator keys (hifigan/models.py, weight-normed convs): weight_v uniform with
+    variance 1 / (elements per output-channel row), so each row has norm ~1; weight_g (the row
+    norm the effective weight gets) ~1 for Conv1d and sqrt(Cout * stride / Cin) for the
+    ConvTranspose1d upsamplers, so every layer keeps unit activation variance; biases +-0.05."""
+    leaf = name.rsplit(".", 1)[-1]
+    if leaf == "bias":
+        return 0.0, 0.05
+    if leaf == "weight_v" or leaf == "weight":
+        row = int(np.prod(shape[1:]))
+        return 0.0, float(np.sqrt(3.0 / row))
+    if leaf == "weight_g":
+        if name.startswith("ups."):
+            cin, cout, u = ups_meta[int(name.split(".")[1])]
+            return float(np.sqrt(cout * u / cin)), 0.1 * float(np.sqrt(cout * u / cin))
+        return 1.0, 0.1
+    raise KeyError(name)
+
+
+def synth_vocoder_state_dict(shapes, ups_meta, seed=0):
+    """{name: shape} of a HiFi-GAN Generator -> {name: float32 ndarray} (counter-based, as above).
+    ups_meta[i] = (Cin, Cout, stride) of upsampler i."""
+    out = {}
+    for name, shape in shapes.items():
+        n = int(np.prod(shape)) if len(shape) else 1
+        offset, scale = _vocoder_role(name, shape, ups_meta)
+        out[name] = (offset + scale * uniform("vocoder." + name, n, seed)).astype(np.float32).reshape(shape)
+    return out
+
+
+def fill_vocoder(module, h, seed=0):
+    """Overwrite a HiFi-GAN Generator's parameters in place (reference or fs2amd.vocoder)."""
+    import torch
+
+    sd = module.state_dict()
+    c0 = h["upsample_initial_channel"]
+    meta = [(c0 // 2 ** i, c0 // 2 ** (i + 1), u) for i, u in enumerate(h["upsample_rates"])]
+    gen = synth_vocoder_state_dict({k: tuple(v.shape) for k, v in sd.items()}, meta, seed)
+    module.load_state_dict({k: torch.from_numpy(v) for k, v in gen.items()}, strict=True)
+    return module
+
+
 def fill_module(module, seed=0):
     """Overwrite a torch module's generated parameters/buffers in place (CPU copy)."""
     import torch

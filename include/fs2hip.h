@@ -48,6 +48,11 @@ enum fs2_epilogue {
   FS2_EPI_RELU_LN = 5,     /* y = LN(relu(acc + bias))        (VariancePredictor, modules.py:218-233) */
   FS2_EPI_RELU_LN_DOT = 6, /* out[row] = (t >= lens[b]) ? 0 : dot(LN(relu(acc+bias)), dot_w) + dot_b
                               -> f32 [B*T]                    (VP linear + masked_fill, modules.py:240-250) */
+  FS2_EPI_BIAS_LRELU = 7,  /* y = leaky_relu(acc + bias, act_slope)
+                              (HiFi-GAN ResBlock convs1 + the leaky_relu before convs2, hifigan/models.py:101-104) */
+  FS2_EPI_RES_SUM = 8,     /* y = (acc + bias + residual [+ residual2]) / out_div
+                              (ResBlock residual x = xt + x :104; the multi-receptive-field sum
+                              xs += resblock(x), x = xs / num_kernels, hifigan/models.py:152-158) */
 };
 
 /*
@@ -125,6 +130,17 @@ typedef struct fs2_conv_desc {
      are deterministic but not bitwise equal to the unsplit summation order.                  */
   void *splitk_ws;
   int64_t splitk_ws_bytes;
+  /* ---- vocoder extensions (HiFi-GAN generator, hifigan/models.py; zero = off / defaults) ---- */
+  int dilation;             /* tap k reads x[b, t + k*dilation - pad]; 0 or 1 = undilated. Non-LN
+                               epilogues allow KS <= 11 and (KS-1)*dilation + 1 <= 51            */
+  float act_slope;          /* FS2_EPI_BIAS_LRELU negative slope                                 */
+  int out2_act;             /* elementwise epilogues: 0 = out2 is a copy of y, 1 = leaky_relu(y,
+                               out2_slope) (the next layer's leaky_relu fused into this one)     */
+  float out2_slope;
+  int out2_f32;             /* elementwise epilogues: out2 in f32 instead of bf16                 */
+  const void *residual2;    /* FS2_EPI_RES_SUM: optional second addend, out's dtype and row stride
+                               (may alias out: each element is read before it is written)        */
+  float out_div;            /* FS2_EPI_RES_SUM: divisor applied last (0 = 1)                       */
 } fs2_conv_desc;
 
 int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream);

@@ -237,6 +237,35 @@ def padding_class_cases(model, LR):
         run_case(model, LR, f"pad_fr{extra}", pair)
 
 
+def vocoder_case():
+    """The reference HiFi-GAN generator (hifigan/models.py, V1 config.json) with counter-generated
+    weights (fs2amd.synth_weights.fill_vocoder, seed 0), eval, fp32 CPU, on two mel batches: the
+    reference FastSpeech2's own postnet output of cfg1_teacher ([1, 207, 80]) and of the first two
+    mini_teacher utterances (padded batch). Stores inputs [B, 80, T] and wavs [B, 1, T*256]; also
+    the generator's state_dict key list (drop-in key compatibility)."""
+    sys.path.insert(0, REF)
+    import hifigan
+    from fs2amd.synth_weights import fill_vocoder
+
+    with open(os.path.join(REF, "hifigan", "config.json")) as f:
+        h = json.load(f)
+    g = hifigan.Generator(hifigan.AttrDict(h))
+    fill_vocoder(g, h, seed=0)
+    g.eval()
+    rec = {"keys": np.array(list(g.state_dict().keys()))}
+    c1 = np.load(os.path.join(HERE, "cfg1_teacher.npz"))["out_postnet_mel"]
+    mt = np.load(os.path.join(HERE, "mini_teacher.npz"))["out_postnet_mel"][:2]
+    for name, mel in (("cfg1", c1), ("mini2", mt)):
+        x = torch.from_numpy(mel).transpose(1, 2).contiguous()
+        with torch.no_grad():
+            y = g(x)
+        rec[f"{name}__mel"] = x.numpy()
+        rec[f"{name}__wav"] = y.numpy()
+        print(f"vocoder {name}: mel {tuple(x.shape)} -> wav {tuple(y.shape)}, |wav| max {float(y.abs().max()):.3f} "
+              f"std {float(y.std()):.3f}")
+    np.savez_compressed(os.path.join(HERE, "vocoder.npz"), **rec)
+
+
 def pipeline_case(pc, mc):
     """The reference's own batch assembly (dataset_chinese.py Dataset / TextDataset collate_fn and
     utils/tools.py to_device on CPU) over the deterministic synthetic corpus
@@ -295,6 +324,9 @@ def main(only=None, only2=None):
         return
     if only == "pipeline":
         pipeline_case(pc, mc)
+        return
+    if only == "vocoder":
+        vocoder_case()
         return
     if only == "round2":  # round-2 additions (the round-1 fixtures above stay byte-identical)
         if only2 != "train16":

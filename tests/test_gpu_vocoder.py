@@ -1,0 +1,133 @@
+"""HiFi-GAN generator on the HIP conv kernels against the reference generator's outputs
+(tests/golden/vocoder.npz) and the dilated / wide-tap conv tiles against F.conv1d.
+
+Tolerances (stated here): fp32 mode (exact-f32 MFMA, only summation order differs) |wav - ref|
+<= 2e-3 absolute (|wav| <= 0.77); bf16 mode (bf16 operands, f32 accumulation, bf16 activations
+between the 67 convs) max |err| <= 0.08 and SNR >= 25 dB against the reference waveform.
+Conv kernels: f32 2e-5, bf16 2.5e-2 relative to the output scale."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from _common import GOLDEN
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+
+
+@pytest.fixture(scope="module")
+def gen():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from fs2amd.synth_weights import fill_vocoder
+    from fs2amd.vocoder import V1_CONFIG, Generator
+
+    g = Generator(V1_CONFIG)
+    fill_vocoder(g, V1_CONFIG, seed=0)
+    return g.to(DEV).eval()
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return np.load(os.path.join(GOLDEN, "vocoder.npz"))
+
+
+def _snr_db(ref, got):
+    return 10 * np.log10((ref ** 2).sum() / max(((ref - got) ** 2).sum(), 1e-30))
+
+
+@pytest.mark.parametrize("case", ["cfg1", "mini2"])
+def test_vocoder_fp32_matches_reference(gen, golden, case):
+    mel = torch.from_numpy(golden[f"{case}__mel"]).to(DEV)
+    with torch.no_grad():
+        y = gen.set_precision("fp32")(mel)
+    torch.cuda.synchronize()
+    ref = golden[f"{case}__wav"]
+    got = y.cpu().numpy()
+    assert got.shape == ref.shape
+    err = np.abs(got - ref).max()
+    print(f"vocoder fp32 {case}: max|err| {err:.2e}, SNR {_snr_db(ref, got):.1f} dB")
+    assert err <= 2e-3, err
+
+
+@pytest.mark.parametrize("case", ["cfg1", "mini2"])
+def test_vocoder_bf16_within_tolerance(gen, golden, case):
+    mel = torch.from_numpy(golden[f"{case}__mel"]).to(DEV)
+    with torch.no_grad():
+        y = gen.set_precision("bf16")(mel)
+    torch.cuda.synchronize()
+    ref = golden[f"{case}__wav"]
+    got = y.cpu().numpy()
+    err, snr = np.abs(got - ref).max(), _snr_db(ref, got)
+    print(f"vocoder bf16 {case}: max|err| {err:.2e}, SNR {snr:.1f} dB")
+    assert err <= 0.08 and snr >= 25.0, (err, snr)
+    gen.set_precision("fp32")
+
+
+def test_vocoder_infer_int16(gen, golden):
+    """utils/model.py:74-92: int16 waveforms, each cut to its length in samples."""
+    from fs2amd.vocoder import vocoder_infer
+    from fs2amd import config as C
+
+    mel = torch.from_numpy(golden["mini2__mel"]).to(DEV)
+    lengths = [200 * 256, 150 * 256]
+    wavs = vocoder_infer(mel, gen.set_precision("fp32"), C.ESD_MODEL_CONFIG, C.ESD_PREPROCESS_CONFIG, lengths)
+    ref = (golden["mini2__wav"][:, 0] * 32768.0).astype("int16")
+    for w, r, n in zip(wavs, ref, lengths):
+        assert w.dtype == np.int16 and w.shape == (n,)
+        assert np.abs(w.astype(np.int32) - r[:n].astype(np.int32)).max() <= 80  # 2e-3 * 32768 + 1
+
+
+@pytest.mark.parametrize("cin,n,k,d,compute", [(128, 128, 11, 5, 0), (64, 64, 7, 3, 0), (32, 32, 11, 5, 0),
+                                               (32, 32, 3, 1, 1), (64, 64, 11, 5, 1), (256, 256, 7, 3, 1),
+                                               (32, 4, 7, 1, 0)])
+def test_dilated_conv_matches_torch(cin, n, k, d, compute):
+    """The wide-tap tiles (dilation in the LDS halo, N = 4..256) vs F.conv1d, per-sequence zero
+    padding, with the leaky-ReLU epilogue and the out2 activation."""
+    from fs2amd import _lib as L, ops
+
+    g = torch.Generator().manual_seed(k * 100 + d)
+    B, T = 3, 301
+    pad = (k * d - d) // 2
+    x = torch.randn(B, T, cin, generator=g)
+    w = torch.randn(n, cin, k, generator=g) / (cin * k) ** 0.5
+    b = torch.randn(n, generator=g) * 0.1
+    dt = torch.float32 if compute == 0 else torch.bfloat16
+    xd = x.to(DEV, dt)
+    out = torch.empty(B, T, n, device=DEV, dtype=dt)
+    o2 = torch.empty(B, T, n, device=DEV, dtype=torch.float32)
+    ops.conv1d(xd, ops.pack_conv_weight(w.to(DEV), compute), b.to(DEV), cin=cin, ks=k, pad=pad, compute=compute,
+               epilogue=L.EPI_BIAS_LRELU, out=out, dilation=d, act_slope=0.1, out2=o2, out2_act=True, out2_slope=0.3)
+    torch.cuda.synchronize()
+    xr = x if compute == 0 else x.to(torch.bfloat16).float()
+    wr = w if compute == 0 else w.to(torch.bfloat16).float()
+    ref = F.leaky_relu(F.conv1d(xr.transpose(1, 2), wr, b, padding=pad, dilation=d).transpose(1, 2), 0.1)
+    tol = 2e-5 if compute == 0 else 2.5e-2
+    scale = float(ref.abs().max())
+    assert float((out.float().cpu() - ref).abs().max()) <= tol * scale
+    assert float((o2.cpu() - F.leaky_relu(out.float().cpu(), 0.3)).abs().max()) <= 1e-6 * scale + (0 if compute == 0 else 1e-2 * scale)
+
+
+def test_res_sum_epilogue(gen):
+    """EPI_RES_SUM: y = (conv + bias + residual + residual2) / div, residual2 aliasing out."""
+    from fs2amd import _lib as L, ops
+
+    g = torch.Generator().manual_seed(3)
+    B, T, C, k = 2, 97, 64, 7
+    x, r, acc = (torch.randn(B, T, C, generator=g) for _ in range(3))
+    w = torch.randn(C, C, k, generator=g) / (C * k) ** 0.5
+    b = torch.randn(C, generator=g) * 0.1
+    out = acc.to(DEV).contiguous()
+    ops.conv1d(x.to(DEV), ops.pack_conv_weight(w.to(DEV), 0), b.to(DEV), cin=C, ks=k, pad=3, compute=0,
+               epilogue=L.EPI_RES_SUM, out=out, residual=r.to(DEV), residual2=out, out_div=3.0)
+    ref = (F.conv1d(x.transpose(1, 2), w, b, padding=3).transpose(1, 2) + r + acc) / 3.0
+    assert float((out.cpu() - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
