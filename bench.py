@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--graph", type=int, default=1, help="replay the forward as a captured HIP graph")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--kernel-reps", type=int, default=20)
+    ap.add_argument("--vocoder", type=int, default=1, help="also time the HiFi-GAN generator on the cfg2 mel batch")
     ap.add_argument("--extra", type=int, default=1,
                     help="also time free-running cfg2, cfg4 (B=256) and cfg5 (fp8) as extra keys of the JSON line")
     ap.add_argument("--mode", default="infer", choices=["infer", "train", "selftest"],
@@ -320,7 +321,66 @@ def extra_workloads(model, args, rank, device):
         record("cfg5_fp8", synth_batch(args.batch, args.phonemes, seed=1 + rank), True,
                "cfg2 with e4m3 FFN + Q|K|V GEMMs (static calibrated scales); tolerance vs bf16 in tests/test_gpu_fp8.py")
         model.set_precision(prec)
+    if args.vocoder:
+        res["vocoder_cfg2"] = vocoder_workload(model, args, rank, device, steps)
     return res
+
+
+def vocoder_workload(model, args, rank, device, steps):
+    """HiFi-GAN V1 (hifigan/models.py, random-init weights) on the cfg2 batch's postnet mel
+    [64, T_max, 80] (padded, as synth_samples hands it over), graph-replayed, same precision as
+    the headline; plus the end-to-end synthesis rate (acoustic model + vocoder, both replayed)."""
+    from fs2amd import parallel
+    from fs2amd.data import synth_batch, to_device
+    from fs2amd.synth_weights import fill_vocoder
+    from fs2amd.vocoder import V1_CONFIG, Generator, flops_per_frame
+
+    voc = Generator(V1_CONFIG)
+    fill_vocoder(voc, V1_CONFIG, seed=0)
+    voc = voc.to(device).eval()
+    voc.remove_weight_norm()
+    voc.set_precision("bf16" if model.precision in ("bf16", "fp8") else "fp32")
+    b = to_device(synth_batch(args.batch, args.phonemes, seed=1 + rank), device)
+    with torch.no_grad():
+        mel = model(**b)[1]
+    frames_valid = int(b["mel_lens"].sum())
+    B, T, _ = mel.shape
+
+    def step():
+        with torch.no_grad():
+            return voc.forward_btc(mel)
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize(device)
+    s = torch.cuda.Stream(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream(device).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    g.replay()
+    torch.cuda.synchronize(device)
+    parallel.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize(device)
+    parallel.barrier()
+    el, fr = parallel.aggregate(time.perf_counter() - t0, frames_valid, device)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    ms = el / steps * 1e3
+    tflops = flops_per_frame() * B * T / (el / steps) / 1e12
+    return {"value": round(fr * steps / el, 1), "unit": "mel-frames/s (valid frames vocoded)", "ms_per_step": round(ms, 3),
+            "steps": steps, "frames_per_step_padded": B * T, "samples_per_step": B * T * voc.hop,
+            "dtype": voc._precision, "achieved_tflops": round(tflops, 1),
+            "flops_per_frame": flops_per_frame(), "hip_graph": True,
+            "rtf_vocoder": round((el / steps) / (fr / world * HOP / SR), 7),
+            "note": "HiFi-GAN V1 on the padded cfg2 postnet mel (synth_samples / vocoder_infer input); "
+                    "FLOPs counted on the padded frames it computes"}
 
 
 def main_selftest(args, rank, world, device):

@@ -244,6 +244,23 @@ class Generator(nn.Module):
         return wav[..., 0]
 
 
+def flops_per_frame(h=V1_CONFIG):
+    """Algorithmic multiply-add FLOPs (x2) per mel frame of the generator (conv_pre, the
+    transposed convs counted at their true K/u taps per output sample, the 3 x 6 ResBlock convs
+    per stage, conv_post); V1: ~614 MFLOP per frame."""
+    c = h["upsample_initial_channel"]
+    f = 2 * h["num_mels"] * 7 * c
+    spf = 1
+    for i, (u, k) in enumerate(zip(h["upsample_rates"], h["upsample_kernel_sizes"])):
+        cin, cout = c // 2 ** i, c // 2 ** (i + 1)
+        spf *= u
+        f += spf * 2 * cin * cout * (k // u)
+        f += spf * sum(2 * cout * cout * rk * 2 * len(rd) for rk, rd in
+                       zip(h["resblock_kernel_sizes"], h["resblock_dilation_sizes"]))
+    f += spf * 2 * (c // 2 ** len(h["upsample_rates"])) * 7
+    return f
+
+
 def get_vocoder(config, device, ckpt_dir="hifigan"):
     """utils/model.py:42-71, HiFi-GAN branch: Generator from <ckpt_dir>/config.json (V1 if absent),
     weights from <ckpt_dir>/generator_{LJSpeech,universal}.pth.tar["generator"] loaded with
