@@ -217,7 +217,7 @@ def main_train(args, rank, world, device):
     batch_cpu = synth_batch(B, 16, 64, seed=1 + rank, with_mels=True, pe_targets=True)
     batch = to_device(batch_cpu, device)
     frames = int(batch_cpu["mel_lens"].sum())
-    step = TrainStep(model, pc, mc, tc, device=device, world_size=world)
+    step = TrainStep(model, pc, mc, tc, device=device, world_size=world, graph=bool(args.graph))
     for _ in range(max(1, args.warmup)):
         step(batch)
     torch.cuda.synchronize(device)
@@ -238,7 +238,8 @@ def main_train(args, rank, world, device):
         "data": "synthetic (pinyin ids U{64..107}, lengths U{16..64}, durations U{2..10}, mel/pitch/energy "
                 "targets N(0,1); counter-generated random-init weights)",
         "config": {"workload": "cfg3: FastSpeech2 train step, ESD-Chinese-Singing-MFA model.yaml",
-                   "global_batch": B * world, "parallelism": f"dp{world} (DDP, 32 MB buckets)"},
+                   "global_batch": B * world, "parallelism": f"dp{world} (DDP, 32 MB buckets)",
+                   "hip_graph": step.graph_mode},
         "loss": round(float(losses[0]), 5),
     }
     if rank == 0:

@@ -6,12 +6,18 @@ import torch
 
 
 class ScheduledOptim:
-    def __init__(self, model, train_config, model_config, current_step):
+    def __init__(self, model, train_config, model_config, current_step, capturable=False):
+        """capturable=True (GPU only): Adam keeps its step count and the learning rate in device
+        tensors, so a HIP graph that captured optimizer.step() replays with each step's Noam lr
+        (written into the lr tensor before the replay) — fs2amd.trainer.TrainStep(graph=True)."""
         opt = train_config["optimizer"]
         params = [p for p in model.parameters()]
         fused = bool(params) and all(p.is_cuda for p in params)  # one multi-tensor kernel per step on the GPU
+        extra = {}
+        if capturable and fused:
+            extra = dict(capturable=True, lr=torch.tensor(1e-3, device=params[0].device))
         self._optimizer = torch.optim.Adam(params, betas=opt["betas"], eps=opt["eps"],
-                                           weight_decay=opt["weight_decay"], fused=fused)
+                                           weight_decay=opt["weight_decay"], fused=fused, **extra)
         self.n_warmup_steps = opt["warm_up_step"]
         self.anneal_steps = opt["anneal_steps"]
         self.anneal_rate = opt["anneal_rate"]
@@ -39,4 +45,7 @@ class ScheduledOptim:
         self.current_step += 1
         lr = self.init_lr * self._get_lr_scale()
         for group in self._optimizer.param_groups:
-            group["lr"] = lr
+            if torch.is_tensor(group["lr"]):
+                group["lr"].fill_(float(lr))  # capturable: the graph reads the lr from this tensor
+            else:
+                group["lr"] = lr

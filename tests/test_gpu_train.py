@@ -110,3 +110,35 @@ def test_attention_backward_matches_autograd(gpu):
     (rq,) = torch.autograd.grad(ref, (q2,), do.double())
     assert float((out.double() - ref).abs().max()) < 1e-4
     assert float((gq.double() - rq).abs().max() / rq.abs().max()) < 1e-4
+
+
+def test_graphed_train_step_equals_eager(gpu):
+    """TrainStep(graph=True): after the eager warm-up steps the captured whole-step graph (forward,
+    loss, backward, clip, capturable Adam with the Noam lr in a device tensor) gives the same
+    losses and parameters as eager steps (dropout off; fp32 -> identical kernels, tight tolerance)."""
+    from fs2amd import config as C
+    from fs2amd.data import synth_batch, to_device
+    from fs2amd.model import FastSpeech2
+    from fs2amd.trainer import TrainStep
+
+    pc, mc, _ = configs()
+    tc = C.ESD_TRAIN_CONFIG
+    runs = []
+    for graph in (False, True):
+        m = FastSpeech2(pc, mc)
+        m.load_state_dict(oracle_state_dict())
+        m = m.to(DEV).set_precision("fp32")
+        m.train_dropout = False
+        st = TrainStep(m, pc, mc, tc, device=torch.device(DEV), graph=graph, warmup=2)
+        losses = []
+        base = synth_batch(4, 8, 20, seed=40, with_mels=True, pe_targets=True)
+        for i in range(6):  # same shapes, different values every step (the graph's static buffers refill)
+            b = dict(base, mels=base["mels"] * (1 + 0.1 * i), p_targets=base["p_targets"] + 0.05 * i)
+            losses.append(float(st(to_device(b, DEV))[0]))
+        torch.cuda.synchronize()
+        runs.append((losses, {k: p.detach().clone() for k, p in m.named_parameters()}, st))
+    (le, pe, _), (lg, pg, stg) = runs
+    assert stg._graph is not None, "the graph was never captured"
+    np.testing.assert_allclose(lg, le, rtol=1e-5)
+    for k in pe:
+        assert torch.allclose(pg[k], pe[k], rtol=1e-4, atol=1e-6), k
