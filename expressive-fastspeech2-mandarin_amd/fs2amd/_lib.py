@@ -57,6 +57,7 @@ SIGNATURES = {
     "fs2_conv1d": (_i, [ctypes.POINTER(ConvDesc), _p]),
     "fs2_attention": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p]),
     "fs2_embed_pe": (_i, [_p, _p, _i, _p, _i, _i, _i, _p, _i, _p, _p]),
+    "fs2_attention_bwd": (_i, [_p, _i, _i64, _p, _i64, _p, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p, _i64, _p]),
     "fs2_cond_vectors": (_i, [_p, _p, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p,
                               _p]),
     "fs2_variance_embed": (_i, [_p, _i, _p, _p, _f, _p, _i, _p, _i, _i, _p]),

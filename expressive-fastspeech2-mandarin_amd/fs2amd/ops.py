@@ -317,6 +317,25 @@ def raise_if_bad_ids(device):
             raise IndexError(f"fs2amd: {n} token id(s) outside the embedding table (their encoder rows are NaN)")
 
 
+def attention_bwd(qkv, out, dout, lens, n_head, d_k, temperature, layout=None):
+    """Gradient of :func:`attention` (fs2_attention_bwd): dqkv f32 with qkv's shape. qkv / out in
+    the forward's dtype (the MFMA operand type), dout f32."""
+    _gpu(qkv, out, dout, lens)
+    dout = dout.float().contiguous()
+    if layout is not None:
+        B, T = layout.B, layout.T
+    else:
+        B, T, _ = qkv.shape
+    dqkv = torch.empty(qkv.shape, device=qkv.device, dtype=torch.float32)
+    ws = torch.empty(2 * B * T * n_head, device=qkv.device, dtype=torch.float32)
+    L.check(_lib.fs2_attention_bwd(_ptr(qkv), _dt(qkv), _rows(qkv, "qkv"), _ptr(out), _rows(out, "out"), _ptr(dout),
+                                   _rows(dout, "dout"), _ptr(lens) if layout is None else None, B, T, n_head, d_k,
+                                   float(temperature), _ptr(dqkv), _rows(dqkv, "dqkv"),
+                                   _ptr(layout.cu) if layout is not None else None, _ptr(ws), ws.numel() * 4,
+                                   _stream(qkv)), "fs2_attention_bwd")
+    return dqkv
+
+
 def embed_pe(tokens, table, pe, out_dtype):
     _gpu(tokens, table, pe)
     B, Lx = tokens.shape

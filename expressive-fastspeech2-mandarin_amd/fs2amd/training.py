@@ -11,8 +11,8 @@ Where the arithmetic runs:
   * every Conv1d / Linear with >= 4 outputs: :class:`Conv1dFn` — forward and input-gradient on
     ``fs2_conv1d`` (MFMA; the input gradient is the same per-sequence conv with the taps flipped
     and the weight transposed), weight gradient as ONE hipBLASLt GEMM over the tap-unfolded input;
-  * self-attention: :class:`AttentionFn` — forward ``fs2_attention``; backward recomputes the
-    masked softmax from the saved projection (torch bmm on hipBLASLt);
+  * self-attention: :class:`AttentionFn` — forward ``fs2_attention``, backward
+    ``fs2_attention_bwd`` (flash-style dQ and dK/dV kernels, no T x T tensor);
   * LengthRegulator: the duration scan and source-index map on ``fs2_lr_durations`` /
     ``fs2_lr_expand``, the differentiable gather (and its scatter-add gradient) in torch;
   * LayerNorm, dropout, BatchNorm, embeddings, losses: torch on the device.
@@ -93,27 +93,17 @@ class AttentionFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qkv, lens, n_head, d_k, temperature, compute):
-        out = ops.attention(_act(qkv, compute), lens, n_head, d_k, temperature)
-        ctx.save_for_backward(qkv.detach(), lens)
+        qa = _act(qkv, compute)
+        out = ops.attention(qa, lens, n_head, d_k, temperature)
+        ctx.save_for_backward(qa, out, lens)
         ctx.n_head, ctx.d_k, ctx.temperature = n_head, d_k, temperature
         return out.float()
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, lens = ctx.saved_tensors
-        H, dk, tmp = ctx.n_head, ctx.d_k, ctx.temperature
-        B, T, _ = qkv.shape
-        q, k, v = qkv.view(B, T, 3, H, dk).permute(2, 0, 3, 1, 4)  # [B, H, T, dk]
-        s = torch.matmul(q, k.transpose(-1, -2)) / tmp
-        keypad = (torch.arange(T, device=qkv.device)[None, :] >= lens[:, None]).view(B, 1, 1, T)
-        p = torch.softmax(s.masked_fill(keypad, float("-inf")), dim=-1).nan_to_num(0.0)
-        do = dout.view(B, T, H, dk).transpose(1, 2)
-        dv = torch.matmul(p.transpose(-1, -2), do)
-        dp = torch.matmul(do, v.transpose(-1, -2))
-        ds = p * (dp - (dp * p).sum(-1, keepdim=True))
-        dq = torch.matmul(ds, k) / tmp
-        dkk = torch.matmul(ds.transpose(-1, -2), q) / tmp
-        dqkv = torch.stack([dq, dkk, dv], 0).permute(1, 3, 0, 2, 4).reshape(B, T, 3 * H * dk)
+        # flash-style HIP backward (fs2_attention_bwd): no [B, H, T, T] tensor
+        qa, out, lens = ctx.saved_tensors
+        dqkv = ops.attention_bwd(qa, out, dout, lens, ctx.n_head, ctx.d_k, ctx.temperature)
         return dqkv, None, None, None, None, None
 
 

@@ -163,6 +163,22 @@ int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int6
                   fs2_stream_t stream);
 
 /*
+ * fs2_attention_bwd — gradient of fs2_attention (training; autograd of transformer/Modules.py:14-25
+ * and the head split/merge of SubLayers.py:36-52) without any T x T tensor: two flash-style
+ * kernels (dQ per 64-query block with the softmax statistics rebuilt from Q and K; dK / dV per
+ * 64-key block reading those statistics back).
+ * qkv: the forward's input [rows, >= 3*H*dk] (dtype: FS2_BF16 / FS2_F32, also the MFMA operand
+ * type); out: the forward's output [rows, >= H*dk] (same dtype); dout: f32 [rows, >= H*dk].
+ * dqkv: f32 [rows, >= 3*H*dk] (dQ | dK | dV in the Q | K | V columns; fully written for every
+ * row < T of every sequence). Layout as fs2_attention: key_lens (padded [B, T] rows) XOR seq_cu
+ * (packed rows). ws: f32 workspace of >= 2*B*T*H floats (softmax statistics). dk must be 128.
+ */
+int fs2_attention_bwd(const void *qkv, int dtype, int64_t qkv_row_stride, const void *out, int64_t out_row_stride,
+                      const float *dout, int64_t dout_row_stride, const int64_t *key_lens, int B, int T, int H,
+                      int dk, float temperature, float *dqkv, int64_t dqkv_row_stride, const int32_t *seq_cu,
+                      float *ws, int64_t ws_bytes, fs2_stream_t stream);
+
+/*
  * fs2_embed_pe — out[b,l,:] = table[tokens[b,l], :] + pe[l, :]   (f32 math)
  * Replaces Encoder src_word_emb + position_enc (transformer/Models.py:82-91).
  * A token outside [0, vocab) — the reference's nn.Embedding raises IndexError (CPU) or a

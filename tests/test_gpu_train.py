@@ -91,25 +91,35 @@ def test_conv_backward_matches_autograd(gpu):
             assert err < 1e-4, (B, T, cin, n, ks, err)
 
 
-def test_attention_backward_matches_autograd(gpu):
-    from fs2amd import _lib as L
+@pytest.mark.parametrize("compute,T,lens", [(0, 45, [45, 17, 1]), (0, 150, [150, 70, 129, 0]),
+                                            (1, 150, [150, 70, 129, 0])])
+def test_attention_backward_matches_autograd(gpu, compute, T, lens):
+    """fs2_attention_bwd (flash-style dQ + dK/dV kernels) vs float64 autograd of the reference's
+    masked softmax attention, several key tiles, ragged lengths; a zero-length sequence gets zero
+    gradients (the reference's are NaN). f32: 1e-4 relative; bf16 operands: 3e-2 relative."""
     from fs2amd.training import AttentionFn
 
     g = torch.Generator().manual_seed(1)
-    B, T, H, dk = 3, 45, 2, 128
+    B, H, dk = len(lens), 2, 128
     qkv = (torch.randn(B, T, 3 * H * dk, generator=g) * 0.3).to(DEV).requires_grad_(True)
-    lens = torch.tensor([45, 17, 1], device=DEV)
+    lt = torch.tensor(lens, device=DEV)
     do = torch.randn(B, T, H * dk, generator=g).to(DEV)
-    out = AttentionFn.apply(qkv, lens, H, dk, dk ** 0.5, L.FS2_F32)
+    out = AttentionFn.apply(qkv, lt, H, dk, dk ** 0.5, compute)
     (gq,) = torch.autograd.grad(out, (qkv,), do)
-    q2 = qkv.detach().double().requires_grad_(True)
+    src = qkv.detach()
+    if compute == 1:
+        src = src.to(torch.bfloat16).float()
+    q2 = src.double().requires_grad_(True)
     q, k, v = q2.view(B, T, 3, H, dk).permute(2, 0, 3, 1, 4)
     s = (q @ k.transpose(-1, -2)) / dk ** 0.5
-    s = s.masked_fill((torch.arange(T, device=DEV)[None, :] >= lens[:, None]).view(B, 1, 1, T), float("-inf"))
+    s = s.masked_fill((torch.arange(T, device=DEV)[None, :] >= lt[:, None]).view(B, 1, 1, T), float("-inf"))
     ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B, T, H * dk)
     (rq,) = torch.autograd.grad(ref, (q2,), do.double())
-    assert float((out.double() - ref).abs().max()) < 1e-4
-    assert float((gq.double() - rq).abs().max() / rq.abs().max()) < 1e-4
+    tol = 1e-4 if compute == 0 else 3e-2
+    ok = lt > 0
+    assert float((out.double() - ref)[ok].abs().max()) < tol * float(ref[ok].abs().max())
+    assert float((gq.double() - rq)[ok].abs().max()) < tol * float(rq[ok].abs().max())
+    assert float(gq[~ok].abs().max() if (~ok).any() else 0.0) == 0.0
 
 
 def test_graphed_train_step_equals_eager(gpu):
