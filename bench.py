@@ -269,7 +269,9 @@ def timed_steps(model, batch, device, steps, warmup, graph, frames_out=None):
                 step()
         torch.cuda.current_stream(device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # captured on the warm-up stream: its split-K workspace already exists, so the graph holds
+        # no counter-zeroing memset (ops.splitk_workspace is per stream)
+        with torch.cuda.graph(g, stream=s):
             out = step()
         g.replay()
         torch.cuda.synchronize(device)
@@ -360,7 +362,7 @@ def vocoder_workload(model, args, rank, device, steps):
         step()
     torch.cuda.current_stream(device).wait_stream(s)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, stream=s):
         step()
     g.replay()
     torch.cuda.synchronize(device)

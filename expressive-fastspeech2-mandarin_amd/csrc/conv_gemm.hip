@@ -188,6 +188,7 @@ struct ConvArgs {
   int out2_act, out2_f32;
   const void *res2;
   float out_div;
+  int l2pf;  // ring kernel: warm each XCD's L2 with the whole weight matrix before the K loop
 };
 
 constexpr int64_t kSkCntBytes = 4096;  // counter block at the start of the split-K workspace
@@ -1405,6 +1406,16 @@ bool splitk_env() {
   return on;
 }
 
+// FS2_LN_SMALLM_ROWS (A/B): row tile of the small-M LayerNorm GEMMs (encoder / variance
+// predictors, M = B*L ~ 4k): 16 (default), 32 or 64 rows.
+int small_m_rows() {
+  static const int v = [] {
+    const char *e = getenv("FS2_LN_SMALLM_ROWS");
+    return e != nullptr ? atoi(e) : 16;
+  }();
+  return v;
+}
+
 // Compute units of the current device (cached per device id).
 int num_cus() {
   static int cache[64] = {0};
@@ -1484,6 +1495,23 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvA
   const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
   const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * (uint32_t)sizeof(TW);
   const uint32_t xrow = (uint32_t)a.xs * (uint32_t)sizeof(TW);
+
+  if (a.l2pf) {
+    // Small-M launches: every tile streams the WHOLE weight matrix in lockstep, so without this each
+    // k-step's 32 KiB of B misses the XCD's L2 in all of its 32 workgroups at once and the ring
+    // waits a full HBM latency per step. Instead the workgroups of one XCD (dispatched round-robin:
+    // blockIdx % 8) each read a disjoint slice of the weights once, up front: one miss latency,
+    // then the K loop hits in L2.
+    const int xcd = blockIdx.x & 7;
+    const int per = ((int)gridDim.x - xcd + 7) >> 3, idx = blockIdx.x >> 3;
+    constexpr uint32_t NT16 = 64u * NW * 16u;
+    const uint32_t slice = ((a.w_bytes + per - 1) / per + NT16 - 1) / NT16 * NT16;
+    const uint32_t beg = (uint32_t)idx * slice, end = min(beg + slice, a.w_bytes);
+    uint32_t sink = 0;
+    for (uint32_t off = beg + tid * 16u; off < end; off += NT16) sink ^= bload16(wr_, off).x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (sink == 0x9E3779B9u && a.dbg == 0x7fffffff) smem[0] = 1;  // keeps the loads; never taken
+  }
 
   const int prow = lane >> 3, plc = (lane & 7) ^ prow;
   int arow[AQ], apos[AQ], alen[AQ];
@@ -1648,9 +1676,21 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvA
   epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
 }
 
+// FS2_L2PF (A/B): ring kernel L2 weight prefetch: 0 off, 1 on the small-M tiles (<= 32 rows,
+// default), 2 on every ring launch.
+int l2pf_env() {
+  static const int v = [] {
+    const char *e = getenv("FS2_L2PF");
+    return e != nullptr ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 template <int CT, int WGM, int WMI, int NS, int WGN = 4>
 void launch_ring(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM;
+  // L2 prefetch where the tiles are short (each streams all of w per few rows) and w fits an XCD L2
+  a.l2pf = (l2pf_env() >= 2 || (l2pf_env() == 1 && BM <= 32)) && a.w_bytes <= (3u << 20) ? 1 : 0;
   a.ntn = (a.N + 255) / 256;
   a.ngr = a.ntn;
   if (a.w_bytes > (2u << 20) && a.ntn > 2 && a.ntn % 2 == 0) a.ngr = 2;  // see launch(): L2-sized N groups
@@ -1816,9 +1856,11 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         launch_ring<CT, 2, 4, 3, 8>(a, s);  // 128 x 256, 16 waves of 64 x 32, 3 stages
       else if (a.M >= 192 * 128)
         launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages (144 KiB)
-      else if (a.M >= 8192)
+      else if (a.M >= 8192 || small_m_rows() == 32)
         w8 ? launch_ring<CT, 1, 2, 4, 8>(a, s)  // 32 x 256, 8 waves of 32 x 32, 4 stages
            : launch_ring<CT, 1, 2, 4>(a, s);    // 32 x 256, 4 waves of 32 x 64
+      else if (small_m_rows() == 64)
+        launch_ring<CT, 2, 2, 3, 8>(a, s);  // 64 x 256, 16 waves of 32 x 32, 3 stages
       else
         w8 ? launch_ring<CT, 1, 1, 4, 8>(a, s)  // 16 x 256, 8 waves of 16 x 32, 4 stages
            : launch_ring<CT, 1, 1, 4>(a, s);    // 16 x 256, 4 waves of 16 x 64
@@ -1999,6 +2041,7 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.out2_f32 = d->out2_f32;
   a.res2 = d->residual2;
   a.out_div = d->out_div != 0.0f ? d->out_div : 1.0f;
+  a.l2pf = 0;
   const bool xb = d->x_dtype == FS2_BF16;
   if (d->compute == FS2_FP8)
     dispatch<FS2_FP8, fp8>(a, ln, s);

@@ -95,7 +95,12 @@ def load():
             f"fs2amd: HIP library not found at {path}. Build it with `python -c 'import __graft_entry__ as g; "
             f"g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    # FS2_LIB_ALLOW_MISSING=1 (A/B runs against an older library build only): skip entry points
+    # the override library does not export; calling one of them then raises AttributeError.
+    allow_missing = "FS2_LIB" in os.environ and os.environ.get("FS2_LIB_ALLOW_MISSING") == "1"
     for name, (res, args) in SIGNATURES.items():
+        if allow_missing and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
