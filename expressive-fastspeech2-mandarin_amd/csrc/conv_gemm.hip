@@ -189,6 +189,7 @@ struct ConvArgs {
   const void *res2;
   float out_div;
   int l2pf;  // ring kernel: warm each XCD's L2 with the whole weight matrix before the K loop
+  int group_n, group_cin;  // grouped input: columns [g*group_n, ...) read channels + g*group_cin
 };
 
 constexpr int64_t kSkCntBytes = 4096;  // counter block at the start of the split-K workspace
@@ -313,6 +314,27 @@ __device__ __forceinline__ void store_any4(void *p, int dt, int64_t off, const f
 // Epilogue of one BM x BN tile whose f32 accumulators sit in LDS (E, row stride BN + 4).
 // (Prefetching every row's residual before the LN row loop was measured 3-5 % slower on the
 // LN GEMMs in round 1: more registers, and the row loop is not latency-bound.)
+// Residual rows of the paired LayerNorm epilogue (RES_LN): lane (wave wid, half h, column group
+// hl) loads row m0 + wid + (2p + h) * NWAVES, 8 columns (one uint4 of bf16 or two of f32).
+// (Issuing them before the ring kernel's K loop instead -- untracked asm loads, waited after it --
+// measured fc + LN 16.4 -> 16.0 us: not kept.)
+template <int NP, int NWAVES>
+__device__ __forceinline__ void load_res_pairs(const ConvArgs &a, int m0, int M, int tid, uint4 (&rraw)[NP][2]) {
+  const int lane = tid & 63, wid = tid >> 6, h = lane >> 5, n = (lane & 31) * 8;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int m = min(m0 + wid + (2 * p + h) * NWAVES, M - 1);
+    if (a.res_dt == FS2_BF16) {
+      rraw[p][0] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const bf16 *>(a.res) + (int64_t)m * a.rs + n);
+      rraw[p][1] = rraw[p][0];
+    } else {
+      const uint4 *rp = reinterpret_cast<const uint4 *>(reinterpret_cast<const float *>(a.res) + (int64_t)m * a.rs + n);
+      rraw[p][0] = rp[0];
+      rraw[p][1] = rp[1];
+    }
+  }
+}
+
 template <int BM, int BN, int NWAVES, bool LN = true>
 __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int m0, int n0, int tid, int M) {
   constexpr int EPI_LD = BN + 4;
@@ -344,22 +366,11 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
     const bool res_bf16 = a.res_dt == FS2_BF16;
     uint4 rraw[NP][2];
     if (epi == FS2_EPI_RES_LN) {
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const int m = min(m0 + wid + (2 * p + h) * NWAVES, M - 1);
-        if (res_bf16) {
-          rraw[p][0] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const bf16 *>(a.res) + (int64_t)m * a.rs + n);
-          rraw[p][1] = rraw[p][0];
-        } else {
-          const uint4 *rp = reinterpret_cast<const uint4 *>(reinterpret_cast<const float *>(a.res) + (int64_t)m * a.rs + n);
-          rraw[p][0] = rp[0];
-          rraw[p][1] = rp[1];
-        }
-      }
+      load_res_pairs<NP, NWAVES>(a, m0, M, tid, rraw);
 #pragma unroll
       for (int p = 0; p < NP; ++p)
-        asm volatile("" ::"v"(rraw[p][0].x), "v"(rraw[p][0].y), "v"(rraw[p][0].z), "v"(rraw[p][0].w), "v"(rraw[p][1].x),
-                     "v"(rraw[p][1].y), "v"(rraw[p][1].z), "v"(rraw[p][1].w));
+        asm volatile("" ::"v"(rraw[p][0].x), "v"(rraw[p][0].y), "v"(rraw[p][0].z), "v"(rraw[p][0].w),
+                     "v"(rraw[p][1].x), "v"(rraw[p][1].y), "v"(rraw[p][1].z), "v"(rraw[p][1].w));
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -898,9 +909,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
   Stage<CT, TIn> sa[A_CH];        // A halo of the next channel block (issued at its tap 0)
   Stage<CT, TW> sb0[B_CH], sb1[B_CH];  // 2-deep ring of B (weight) tiles: step k lives in sb[k & 1]
 
+  // grouped input (fs2_conv_desc.group_n): this tile's channel offset
+  const int goff = a.group_n > 0 ? (n0 / a.group_n) * a.group_cin : 0;
   auto gload_a = [&](int cb) {
-    const int ch = cb * KE + schunk * CE;
-    const bool ch_ok = ch < a.Cin;
+    const int lch = cb * KE + schunk * CE;
+    const bool ch_ok = lch < a.Cin;
+    const int ch = src_channel(a, lch) + goff;
 #pragma unroll
     for (int j = 0; j < A_CH; ++j) {
       const int h = srow + RPP * j;
@@ -1030,8 +1044,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, (WGM * WGN == 4) ? 2 : (WCOL == 32 
       asrc[it] = (h < H && gm >= 0 && gm < M) ? (a.a_rowmap != nullptr ? a.a_rowmap[gm] : gm) : -1;
     }
     auto dma_a = [&](int cb, int buf) {
-      const int ch = cb * KE + plc * CE;
-      const bool ch_ok = ch < a.Cin;
+      const int lch = cb * KE + plc * CE;
+      const bool ch_ok = lch < a.Cin;
+      const int ch = src_channel(a, lch) + goff;  // split-precision block map + group offset
       char *As = Abuf + buf * A_BYTES;
 #pragma unroll
       for (int it = 0; it < AIT; ++it) {
@@ -1465,11 +1480,15 @@ __device__ __forceinline__ void vm_wait() {
 // the 16-row small-M tiles); split-K only with 4. (16 waves of 16 columns: one LN row per wave,
 // i.e. the single-row LN epilogue on 16-row tiles and the paired one on 32-row tiles, which
 // breaks the packed == padded bit-exactness; not offered.)
-template <int CT, int WGM, int WMI, int NS, int WGN = 4>
+// BN = 128: the column-split tiles of the small-M elementwise-epilogue GEMMs (variance
+// predictor convs: every workgroup streams only its columns' weights, with the ring's depth).
+template <int CT, int WGM, int WMI, int NS, int WGN = 4, int BN = 256>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvArgs a) {
   static_assert(WGN == 4 || WGN == 8, "column waves");
-  constexpr int NW = WGM * WGN, WCOL = 256 / WGN, NI = WCOL / 16;
-  constexpr int WROWS = 16 * WMI, BM = WROWS * WGM, BN = 256;
+  static_assert(BN == 256 || BN == 128, "tile width");
+  constexpr int NW = WGM * WGN, WCOL = BN / WGN, NI = WCOL / 16;
+  constexpr int WROWS = 16 * WMI, BM = WROWS * WGM;
+  static_assert((BN / 8) % NW == 0, "B pieces per wave");
   constexpr int KE = CTraits<CT>::KE, CE = CTraits<CT>::CE;
   using TW = typename CTraits<CT>::T;
   constexpr int AP = BM / 8, BP = BN / 8;               // 1 KiB pieces per stage
@@ -1495,6 +1514,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvA
   const rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
   const uint32_t wrow = (uint32_t)(KS * a.Cin_pad) * (uint32_t)sizeof(TW);
   const uint32_t xrow = (uint32_t)a.xs * (uint32_t)sizeof(TW);
+  const int goff = a.group_n > 0 ? (n0 / a.group_n) * a.group_cin : 0;  // grouped input
 
   if (a.l2pf) {
     // Small-M launches: every tile streams the WHOLE weight matrix in lockstep, so without this each
@@ -1549,7 +1569,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvA
     const int sh = tap - pad;
     const int ch = cb * KE + plc * CE;
     const bool ch_ok = ch < a.Cin;
-    const int sch = src_channel(a, ch);
+    const int sch = src_channel(a, ch) + goff;
 #pragma unroll
     for (int i = 0; i < AQ; ++i) {
       const bool ok = ch_ok && (unsigned)(apos[i] + sh) < (unsigned)alen[i];
@@ -1658,8 +1678,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvA
   __syncthreads();
   if constexpr (WGN == 4) {
     if (nseg > 1) {
-      static_assert(BM * BN * 4 == 256 * WGM * WMI * 4 * 16, "partial tile layout");
-      if (!splitk_fixup<WMI, 256 * WGM>(a, acc, tl, seg, nseg, tid, reinterpret_cast<int *>(smem + SMEM))) return;
+      static_assert(BM * BN * 4 == 64 * NW * WMI * NI * 16, "partial tile layout");
+      if (!splitk_fixup<WMI, 64 * NW, NI>(a, acc, tl, seg, nseg, tid, reinterpret_cast<int *>(smem + SMEM))) return;
     }
   }
 
@@ -1673,7 +1693,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvA
         E[(wr * WROWS + mi * 16 + 4 * (lane >> 4) + j) * EPI_LD + wc * WCOL + ni * 16 + (lane & 15)] = acc[mi][ni][j];
   __syncthreads();
   if (a.dbg & 2) return;
-  epilogue<BM, BN, NW>(a, E, m0, n0, tid, M);
+  epilogue<BM, BN, NW, BN == 256>(a, E, m0, n0, tid, M);
 }
 
 // FS2_L2PF (A/B): ring kernel L2 weight prefetch: 0 off, 1 on the small-M tiles (<= 32 rows,
@@ -1686,12 +1706,12 @@ int l2pf_env() {
   return v;
 }
 
-template <int CT, int WGM, int WMI, int NS, int WGN = 4>
+template <int CT, int WGM, int WMI, int NS, int WGN = 4, int BN = 256>
 void launch_ring(ConvArgs a, hipStream_t s) {
   constexpr int BM = 16 * WMI * WGM;
   // L2 prefetch where the tiles are short (each streams all of w per few rows) and w fits an XCD L2
-  a.l2pf = (l2pf_env() >= 2 || (l2pf_env() == 1 && BM <= 32)) && a.w_bytes <= (3u << 20) ? 1 : 0;
-  a.ntn = (a.N + 255) / 256;
+  a.l2pf = (l2pf_env() >= 2 || (l2pf_env() == 1 && (BM <= 32 || BN == 128))) && a.w_bytes <= (3u << 20) ? 1 : 0;
+  a.ntn = (a.N + BN - 1) / BN;
   a.ngr = a.ntn;
   if (a.w_bytes > (2u << 20) && a.ntn > 2 && a.ntn % 2 == 0) a.ngr = 2;  // see launch(): L2-sized N groups
   int nwg = (a.M + BM - 1) / BM * a.ntn;
@@ -1699,7 +1719,7 @@ void launch_ring(ConvArgs a, hipStream_t s) {
   {  // split-K (conv_tile_sk): one workgroup per CU; segments of >= 4 k-steps, at most 4 per tile
     const int slots = num_cus();
     const int nK = a.KS * (a.Cin_pad / CTraits<CT>::KE);
-    const int64_t need = kSkCntBytes + (int64_t)slots * BM * 256 * 4;
+    const int64_t need = kSkCntBytes + (int64_t)slots * BM * BN * 4;
     const int sk_max = nK / 4 < 4 ? nK / 4 : 4;
     if (WGN == 4 && splitk_env() && sk_would_split(nwg, slots, sk_max) && a.sk_cnt != nullptr && a.sk_ws_bytes >= need &&
         nK >= 8 && slots > 0 && slots * 4 <= kSkCntBytes) {
@@ -1709,7 +1729,7 @@ void launch_ring(ConvArgs a, hipStream_t s) {
       nwg += slots;
     }
   }
-  hipLaunchKernelGGL((conv_gemm_ring_kernel<CT, WGM, WMI, NS, WGN>), dim3(nwg), dim3(64 * WGM * WGN), 0, s, a);
+  hipLaunchKernelGGL((conv_gemm_ring_kernel<CT, WGM, WMI, NS, WGN, BN>), dim3(nwg), dim3(64 * WGM * WGN), 0, s, a);
 }
 
 template <int CT, int WGM, int WGN, int WMI, int KSMAX, typename TIn, int WCOL = 64>
@@ -1834,6 +1854,25 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       return;
     }
   }
+  if constexpr (std::is_same<TIn, typename CTraits<CT>::T>::value && CT != FS2_FP8) {
+    // split-precision / grouped elementwise GEMMs (the column-split variance predictor convs):
+    // 128-column ring tiles, 64 rows when that still gives a workgroup per CU, else 32
+    static const int vpring = [] {
+      const char *e = getenv("FS2_VP_RING");
+      return e != nullptr ? atoi(e) : 2;
+    }();
+    if (!ln && vpring && (a.cin_block != 0 || a.group_n != 0)) {
+      const int ntn = (a.N + 127) / 128;
+      const bool rows64 = (int64_t)((a.M + 63) / 64) * ntn >= num_cus();
+      if (vpring == 1)
+        rows64 ? launch_ring<CT, 2, 2, 4, 4, 128>(a, s)   // 64 x 128, 8 waves of 32 x 32, 4 stages
+               : launch_ring<CT, 2, 1, 4, 4, 128>(a, s);  // 32 x 128, 8 waves of 16 x 32
+      else
+        rows64 ? launch_ring<CT, 2, 2, 6, 4, 128>(a, s)   // 6 stages (5 k-steps in flight)
+               : launch_ring<CT, 2, 1, 6, 4, 128>(a, s);
+      return;
+    }
+  }
   if constexpr (std::is_same<TIn, typename CTraits<CT>::T>::value) {
     static const bool ring = [] {
       const char *e = getenv("FS2_CONV_RING");
@@ -1923,11 +1962,23 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
     if (d->cin_block % 64 != 0 || d->Cin % d->cin_block != 0 || d->Cin / d->cin_block > 4) return FS2_EINVAL;
     for (int i = 0; i < d->Cin / d->cin_block; ++i)
       if (d->cin_src[i] < 0 || d->cin_src[i] + d->cin_block > d->x_row_stride) return FS2_EINVAL;
-    const bool ln_epi = d->epilogue == FS2_EPI_RES_LN || d->epilogue == FS2_EPI_RELU_LN ||
-                        d->epilogue == FS2_EPI_RELU_LN_DOT;
-    if (d->compute != FS2_BF16 || d->x_dtype != FS2_BF16 || !ln_epi) return FS2_EUNSUPPORTED;
+    if (d->compute != FS2_BF16 || d->x_dtype != FS2_BF16) return FS2_EUNSUPPORTED;
   } else if (d->x_row_stride < d->Cin) {
     return FS2_EINVAL;
+  }
+  if (d->group_n != 0 || d->group_cin != 0) {  // grouped input: elementwise epilogues, whole 128-column tiles
+    const bool ln_epi = d->epilogue == FS2_EPI_RES_LN || d->epilogue == FS2_EPI_RELU_LN ||
+                        d->epilogue == FS2_EPI_RELU_LN_DOT;
+    if (d->group_n <= 0 || d->group_n % 128 != 0 || d->N % d->group_n != 0 || d->group_cin < 0 || ln_epi ||
+        d->compute != FS2_BF16 || d->x_dtype != FS2_BF16 || d->KS > 9 || d->dilation > 1)
+      return FS2_EINVAL;
+    int maxsrc = d->Cin;
+    if (d->cin_block != 0) {
+      maxsrc = 0;
+      for (int i = 0; i < d->Cin / d->cin_block; ++i)
+        maxsrc = d->cin_src[i] + d->cin_block > maxsrc ? d->cin_src[i] + d->cin_block : maxsrc;
+    }
+    if ((int64_t)(d->N / d->group_n - 1) * d->group_cin + maxsrc > d->x_row_stride) return FS2_EINVAL;
   }
   if ((d->x_row_stride % ce) != 0) return FS2_EINVAL;
   if (d->out_split && (d->out_dtype != FS2_BF16 || d->out_row_stride < 2 * (int64_t)d->N)) return FS2_EINVAL;
@@ -1994,6 +2045,8 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.cin_block = d->cin_block;
   for (int i = 0; i < 4; ++i) a.cin_src[i] = d->cin_src[i];
   a.out_split = d->out_split;
+  a.group_n = d->group_n;
+  a.group_cin = d->group_cin;
   a.sk_slots = 0;
   a.sk_max = 1;
   a.sk_cnt = nullptr;

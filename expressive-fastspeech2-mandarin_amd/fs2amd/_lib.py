@@ -46,6 +46,7 @@ class ConvDesc(ctypes.Structure):
         ("splitk_ws", _p), ("splitk_ws_bytes", _i64),
         ("dilation", _i), ("act_slope", _f), ("out2_act", _i), ("out2_slope", _f), ("out2_f32", _i),
         ("residual2", _p), ("out_div", _f),
+        ("group_n", _i), ("group_cin", _i),
     ]
 
 
@@ -64,6 +65,9 @@ SIGNATURES = {
     "fs2_lr_durations": (_i, [_p, _i, _f, _i, _i, _p, _p, _p, _p]),
     "fs2_lr_expand": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p]),
     "fs2_seq_layout": (_i, [_p, _i, _i, _p, _p, _p, _p]),
+    "fs2_vp_norm": (_i, [_p, _i64, _i, _i, _i, _p, _p, _f, _p, _i64, _p]),
+    "fs2_vp_head": (_i, [_p, _i64, _i, _i, _i, _i, _p, _p, _f, _p, _p, _p, _p, _i, _p, _i, _i64, _i, _p, _f, _p, _i, _p,
+                         _p]),
     "fs2_length_masks": (_i, [_p, _i, _i, _p, _p]),
     "fs2_length_regulate": (_i, [_p, _i, _p, _i, _f, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p, _p, _p]),
 }

@@ -204,13 +204,14 @@ def splitk_workspace(device):
 def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None, out=None, residual=None,
            ln=None, lens=None, addvec1=None, addvec2=None, dot=None, n=None, layout=None, src_layout=None,
            col_scale=None, out_scale=1.0, out2=None, out2_scale=1.0, cin_block=0, cin_src=(), out_split=False,
-           dilation=1, act_slope=0.0, out2_act=False, out2_slope=0.0, residual2=None, out_div=1.0):
+           dilation=1, act_slope=0.0, out2_act=False, out2_slope=0.0, residual2=None, out_div=1.0, group=None):
     """Implicit-GEMM Conv1d / Linear with a fused epilogue (fs2_conv1d).
 
     layout: x / residual / out are packed [B*T, C] in that SeqLayout. src_layout (KS == 1): x is
     packed in it, out is padded [B, T, N] (zeros in, i.e. bias out, at padding).
     Vocoder extensions: dilation (tap k reads row t + k*dilation - pad), act_slope (EPI_BIAS_LRELU),
-    out2_act / out2_slope (out2 = leaky_relu(y)), out2 may be f32, residual2 / out_div (EPI_RES_SUM)."""
+    out2_act / out2_slope (out2 = leaky_relu(y)), out2 may be f32, residual2 / out_div (EPI_RES_SUM).
+    group = (group_n, group_cin): output columns [g*group_n, ...) read x's channels + g*group_cin."""
     _gpu(x, w_packed, bias, residual, lens, addvec1, addvec2, residual2)
     if layout is not None or src_layout is not None:
         lay = layout if layout is not None else src_layout
@@ -252,6 +253,8 @@ def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None
     d.dilation, d.act_slope, d.out_div = int(dilation), float(act_slope), float(out_div)
     if residual2 is not None:
         d.residual2 = residual2.data_ptr()
+    if group is not None:
+        d.group_n, d.group_cin = int(group[0]), int(group[1])
     if layout is not None:
         d.rows_dev, d.row_pos = layout.rows_dev, layout.row_pos.data_ptr()
     if src_layout is not None:
@@ -371,6 +374,42 @@ def variance_embed(x, pred, target, control, bins, table):
     D = x.shape[-1]
     L.check(_lib.fs2_variance_embed(_ptr(x), _dt(x), _ptr(pred), _ptr(target), float(control), _ptr(bins),
                                     bins.numel() + 1, _ptr(table), M, D, _stream(x)), "fs2_variance_embed")
+
+
+def vp_norm(y, gamma, beta, eps, out=None):
+    """fs2_vp_norm: y f32 [rows, G*256] (relu(conv1) of G variance predictors) -> LayerNorm per
+    group -> bf16 [rows, G*512]: group g's hi plane at g*512, lo plane at g*512 + 256."""
+    _gpu(y, gamma, beta)
+    G = gamma.numel() // 256
+    rows = y.numel() // y.shape[-1]
+    if out is None:
+        out = torch.empty(*y.shape[:-1], G * 512, device=y.device, dtype=torch.bfloat16)
+    L.check(_lib.fs2_vp_norm(_ptr(y), _rows(y, "y"), rows, G, 256, _ptr(gamma), _ptr(beta), float(eps), _ptr(out),
+                             _rows(out, "out"), _stream(y)), "fs2_vp_norm")
+    return out
+
+
+def vp_head(y, gamma, beta, eps, lin_w, lin_b, lens, embed=None):
+    """fs2_vp_head: y f32 [B, T, G*256] (relu(conv2)) -> per group LayerNorm, Linear(256->1), masked
+    -> pred f32 [G, B, T]. embed = (g, x, target, control, bins, table): group g's value also does
+    the pitch / energy embedding add into x in place (fs2_variance_embed semantics)."""
+    _gpu(y, gamma, beta, lin_w, lin_b, lens)
+    B, T, _ = y.shape
+    G = gamma.numel() // 256
+    assert lens.dtype == torch.int64 and lens.numel() == B
+    pred = torch.empty(G, B, T, device=y.device, dtype=torch.float32)
+    eg, x, target, control, bins, table = embed if embed is not None else (-1, None, None, 1.0, None, None)
+    if x is not None:
+        _gpu(x, target, bins, table)
+        assert x.shape[:2] == (B, T) and table.shape[1] == x.shape[-1]
+        if target is not None:
+            assert target.dtype == torch.float32 and target.is_contiguous() and target.numel() == B * T
+    L.check(_lib.fs2_vp_head(_ptr(y), _rows(y, "y"), B, T, G, 256, _ptr(gamma), _ptr(beta), float(eps), _ptr(lin_w),
+                             _ptr(lin_b), _ptr(lens), _ptr(pred), int(eg), _ptr(x), _dt(x) if x is not None else 0,
+                             _rows(x, "x") if x is not None else 0, x.shape[-1] if x is not None else 0,
+                             _ptr(target), float(control), _ptr(bins),
+                             bins.numel() + 1 if bins is not None else 0, _ptr(table), _stream(y)), "fs2_vp_head")
+    return pred
 
 
 def length_mask(lens, width):

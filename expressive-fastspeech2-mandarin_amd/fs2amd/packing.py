@@ -6,8 +6,9 @@
 * PostNet BatchNorm1d (eval: running stats) folded into its conv: w' = w * g/sqrt(rv+eps),
   b' = (b - rm) * g/sqrt(rv+eps) + beta (transformer/Layers.py:92-135).
 * bf16 precision: FFT blocks, mel_linear, PostNet in bf16; VariancePredictors exact f32
-  (vp_precision "fp32"), bf16 ("bf16") or split-precision bf16x3 ("bf16x3": w = w_hi + w_lo,
-  the hidden activation as two bf16 planes, three bf16 MFMA products per term).
+  (vp_precision "fp32"), bf16 ("bf16") or split-precision bf16x3 ("bf16x3", the default: w = w_hi +
+  w_lo, the hidden activation as two bf16 planes, three bf16 MFMA products per term), the latter
+  also stacked in the column-split form (duration + pitch conv weights side by side).
 * fp8 precision (cfg5): as bf16, plus the FFN Conv1d pair of every FFT block, and the Q|K|V
   projection of every block after the first of its stack, in e4m3fn with per-output-channel
   weight scales; the dequantisation vector col_scale = s_in * s_w[n] uses the layer's static
@@ -81,6 +82,35 @@ def _vp(vp, device, compute, split=False):
     )
 
 
+def _vp_columns(vps, device):
+    """Column-split bf16x3 form of G VariancePredictors that read the same input (runtime.
+    variance_predictors): conv1 / conv2 weights of the G predictors stacked along N (one launch
+    each, workgroups own column slices), LayerNorm / Linear parameters stacked per group for
+    fs2_vp_norm / fs2_vp_head. conv1 reads [x_hi | x_hi] (x is bf16: x_lo = 0) against
+    [w_hi | w_lo]; conv2 reads each group's [h_hi | h_hi | h_lo] against [w_hi | w_lo | w_hi]."""
+    cls = [vp.conv_layer for vp in vps]
+    c1s = [cl.conv1d_1.conv for cl in cls]
+    c2s = [cl.conv1d_2.conv for cl in cls]
+    geo = {(c.kernel_size[0], c.padding[0], c.in_channels, c.out_channels) for c in c1s + c2s}
+    eps = {cl.layer_norm_1.eps for cl in cls} | {cl.layer_norm_2.eps for cl in cls}
+    if len(geo) != 1 or len(eps) != 1:
+        return None
+    k, p, cin, cout = geo.pop()
+    if cin != 256 or cout != 256:
+        return None
+    cat = lambda ts: torch.cat([_f32(t, device).reshape(-1) for t in ts]).contiguous()
+    return SimpleNamespace(
+        G=len(vps), c=cin, k=k, p=p, eps=eps.pop(),
+        w1=torch.cat([pack_conv_weight_split(c.weight.to(device), ("hi", "lo")) for c in c1s], 0).contiguous(),
+        b1=cat([c.bias for c in c1s]),
+        g1=cat([cl.layer_norm_1.weight for cl in cls]), be1=cat([cl.layer_norm_1.bias for cl in cls]),
+        w2=torch.cat([pack_conv_weight_split(c.weight.to(device), ("hi", "lo", "hi")) for c in c2s], 0).contiguous(),
+        b2=cat([c.bias for c in c2s]),
+        g2=cat([cl.layer_norm_2.weight for cl in cls]), be2=cat([cl.layer_norm_2.bias for cl in cls]),
+        lin_w=cat([vp.linear_layer.weight for vp in vps]), lin_b=cat([vp.linear_layer.bias for vp in vps]),
+    )
+
+
 def _postnet(pn, device, compute):
     layers = []
     for seq in pn.convolutions:
@@ -110,6 +140,13 @@ def pack_model(model, device, precision, vp_precision="fp32", fp8_scales=None):
     P.enc_layers = [_fft_layer(l, device, big, ("enc", i), sc) for i, l in enumerate(model.encoder.layer_stack)]
     P.dec_layers = [_fft_layer(l, device, big, ("dec", i), sc) for i, l in enumerate(model.decoder.layer_stack)]
     P.vp = {k: _vp(getattr(va, f"{k}_predictor"), device, vpc, vsplit) for k in ("duration", "pitch", "energy")}
+    # bf16x3 VariancePredictors in their column-split form (duration + pitch side by side, energy)
+    P.vpcols = None
+    if vsplit:
+        dp = _vp_columns([va.duration_predictor, va.pitch_predictor], device)
+        en = _vp_columns([va.energy_predictor], device)
+        if dp is not None and en is not None:
+            P.vpcols = SimpleNamespace(dp=dp, energy=en)
     P.bins = {k: _f32(getattr(va, f"{k}_bins"), device) for k in ("pitch", "energy")}
     P.var_table = {k: _f32(getattr(va, f"{k}_embedding").weight, device) for k in ("pitch", "energy")}
     P.mel_w = pack_conv_weight(model.mel_linear.weight.to(device), big)

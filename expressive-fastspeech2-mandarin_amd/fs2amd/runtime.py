@@ -8,7 +8,8 @@ Mirrors model/fastspeech2.py:73-148 step by step (eval semantics, reference quir
      Q|K|V GEMM (N=768)  -> attention -> fc + res + LN + mask -> conv k9 + ReLU -> conv k1 + res + LN + mask
      (the last block's epilogue also adds the speaker and emotion vectors, fastspeech2.py:101-110)
   VarianceAdaptor                              model/modules.py:102-158
-     duration VP (f32), pitch VP -> bucketize/embed add, energy VP (uses p_control, :124-125)
+     duration + pitch VPs (bf16x3 column-split launches; the head adds the pitch embedding),
+     energy VP (uses p_control, :124-125) + its embedding
      -> LengthRegulator scan (+ duration rounding :132-135) -> gather (+ decoder PE add)
   6 x FFT block (decoder)                      transformer/Models.py:139-171
   mel_linear, PostNet (BN folded) + residual   fastspeech2.py:134-136, transformer/Layers.py:129-137
@@ -171,6 +172,26 @@ def variance_predictor(vp, x, lens):
                       epilogue=L.EPI_RELU_LN_DOT, ln=vp.ln2, lens=lens, dot=(vp.lin_w, vp.lin_b))
 
 
+def vp_columns_on():
+    """FS2_VP_COLUMNS=0: the bf16x3 predictors as LayerNorm-epilogue GEMMs (round-1 form, A/B)."""
+    return os.environ.get("FS2_VP_COLUMNS", "1") != "0"
+
+
+def variance_predictors(F, x, lens, embed=None):
+    """G VariancePredictors on the same input x (model/modules.py:209-250), column-split bf16x3:
+    conv1 (+ ReLU) as one launch over the G predictors' stacked columns, fs2_vp_norm (LayerNorm ->
+    bf16 hi / lo planes), conv2 (+ ReLU) as one grouped launch (group g reads its own planes),
+    fs2_vp_head (LayerNorm, Linear(256 -> 1), mask; optionally the pitch / energy embedding add of
+    one group into x). Returns pred f32 [G, B, T]."""
+    y1 = ops.conv1d(x, F.w1, F.b1, cin=2 * F.c, ks=F.k, pad=F.p, compute=L.FS2_BF16, epilogue=L.EPI_BIAS_RELU,
+                    out_dtype=L.FS2_F32, cin_block=F.c, cin_src=(0, 0))
+    h = ops.vp_norm(y1, F.g1, F.be1, F.eps)
+    y2 = ops.conv1d(h, F.w2, F.b2, cin=3 * F.c, ks=F.k, pad=F.p, compute=L.FS2_BF16, epilogue=L.EPI_BIAS_RELU,
+                    out_dtype=L.FS2_F32, cin_block=F.c, cin_src=(0, 0, F.c),
+                    group=(F.c, 2 * F.c) if F.G > 1 else None)
+    return ops.vp_head(y2, F.g2, F.be2, F.eps, F.lin_w, F.lin_b, lens, embed)
+
+
 def _variance(P, kind, x, lens, target, control):
     pred = variance_predictor(P.vp[kind], x, lens)
     tgt = None
@@ -262,10 +283,20 @@ def _stage1(P, va, g, p_control, d_control):
     st = SimpleNamespace(x=x, p_pred=None, e_pred=None)
     st.phoneme_p = va.pitch_feature_level == "phoneme_level"
     st.phoneme_e = va.energy_feature_level == "phoneme_level"
-    st.log_d = variance_predictor(P.vp["duration"], x, g.lens_src)
-    if st.phoneme_p:
+    if P.vpcols is not None and st.phoneme_p and st.phoneme_e and vp_columns_on():
+        # duration + pitch in one set of launches (both read x; the pitch embedding is added to x
+        # by the head), then energy on x + pitch embedding (modules.py:110-126)
+        V = P.vpcols
+        dp = variance_predictors(V.dp, x, g.lens_src,
+                                 embed=(1, x, g.p_targets, p_control, P.bins["pitch"], P.var_table["pitch"]))
+        st.log_d, st.p_pred = dp[0], dp[1]
+        st.e_pred = variance_predictors(V.energy, x, g.lens_src, embed=(
+            0, x, g.e_targets, p_control, P.bins["energy"], P.var_table["energy"]))[0]  # p_control: :124-125
+    else:
+        st.log_d = variance_predictor(P.vp["duration"], x, g.lens_src)
+    if st.phoneme_p and st.p_pred is None:
         st.p_pred = _variance(P, "pitch", x, g.lens_src, g.p_targets, p_control)
-    if st.phoneme_e:
+    if st.phoneme_e and st.e_pred is None:
         st.e_pred = _variance(P, "energy", x, g.lens_src, g.e_targets, p_control)  # p_control: modules.py:124-125
     if g.d_targets is not None:
         dur = g.d_targets

@@ -141,6 +141,12 @@ typedef struct fs2_conv_desc {
   const void *residual2;    /* FS2_EPI_RES_SUM: optional second addend, out's dtype and row stride
                                (may alias out: each element is read before it is written)        */
   float out_div;            /* FS2_EPI_RES_SUM: divisor applied last (0 = 1)                       */
+  /* ---- grouped input (the variance predictors' column-split form; 0 = off) ----
+     Output columns [g*group_n, (g+1)*group_n) read the input channels shifted by g*group_cin
+     (after the cin_block map): two predictors' conv2 in one launch, each on its own hidden
+     planes. Elementwise epilogues only; group_n a multiple of 128.                           */
+  int group_n;
+  int group_cin;
 } fs2_conv_desc;
 
 int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream);
@@ -209,6 +215,30 @@ int fs2_cond_vectors(const int64_t *speakers, const float *speaker_table, int n_
  */
 int fs2_variance_embed(void *x, int x_dtype, float *pred, const float *target, float control, const float *bins,
                        int n_bins, const float *table, int M, int D, fs2_stream_t stream);
+
+/*
+ * VariancePredictor, column-split form (model/modules.py:197-250; VarianceAdaptor.forward
+ * :110-126). The two Conv1d(k=3) of G predictors that read the same input run as fs2_conv1d
+ * launches whose workgroups each own a slice of the output columns (a small-M LayerNorm GEMM
+ * would make every workgroup stream a whole weight matrix); the two LayerNorms move into these
+ * row kernels. Every group is C = 256 columns (filter_size); one half-wave per (row, group).
+ *
+ * fs2_vp_norm: h = LayerNorm(y[m, g*C : (g+1)*C]; gamma[g], beta[g], eps) written as the bf16x3
+ *   input planes of the second conv: out[m, g*2C + c] = bf16(h), out[m, g*2C + C + c] =
+ *   bf16(h - bf16(h)).  (layer_norm_1 + dropout_1 (eval: identity), modules.py:218-222)
+ * fs2_vp_head: per (row m = b*T + t, group g):
+ *   p = (t >= lens[b]) ? 0 : dot(LayerNorm(y[m, g*C:(g+1)*C]; gamma2[g], beta2[g]), lin_w[g]) + lin_b[g]
+ *   pred[g*B*T + m] = p                        (layer_norm_2, linear_layer, masked_fill :233-250)
+ *   and for g == embed_group (>= 0) the pitch/energy embedding of fs2_variance_embed, in the
+ *   same pass: v = target ? target[m] : (pred *= control); x[m, :D] += table[bucketize(v, bins)].
+ */
+int fs2_vp_norm(const float *y, int64_t y_row_stride, int M, int G, int C, const float *gamma, const float *beta,
+                float eps, void *out, int64_t out_row_stride, fs2_stream_t stream);
+int fs2_vp_head(const float *y, int64_t y_row_stride, int B, int T, int G, int C, const float *gamma,
+                const float *beta, float eps, const float *lin_w, const float *lin_b, const int64_t *lens,
+                float *pred, int embed_group, void *x, int x_dtype, int64_t x_row_stride, int D,
+                const float *target, float control, const float *bins, int n_bins, const float *table,
+                fs2_stream_t stream);
 
 /*
  * LengthRegulator (model/modules.py:161-194 + utils/tools.py:360-378), split in two launches

@@ -42,6 +42,9 @@ class ZeroingLib(RecordingLib):
             elif name == "fs2_attention":
                 B, T, out, os_ = args[4], args[5], args[9], args[10]
                 ctypes.memset(out, 0, B * T * os_ * (2 if args[1] == 1 else 4))
+            elif name == "fs2_attention_bwd":  # dqkv f32 [B*T, >= 3*H*dk] (else uninitialised memory)
+                B, T, dqkv, rs = args[8], args[9], args[13], args[14]
+                ctypes.memset(dqkv, 0, B * T * rs * 4)
             return 0
 
         return call

@@ -420,6 +420,53 @@ def test_split_precision_variance_predictor_matches_f32():
         assert bool((err <= 2e-4 + 2e-4 * a.abs()).all()), (k, float(err.max()))
 
 
+@pytest.mark.parametrize("B,L", [(16, 57), (64, 64), (3, 5)])
+def test_vp_columns_match_f32_and_embed(B, L):
+    """Column-split bf16x3 VariancePredictors (runtime.variance_predictors: conv1 over duration +
+    pitch's stacked columns, fs2_vp_norm, grouped conv2, fs2_vp_head) vs each predictor on
+    exact-f32 MFMA: |d| <= 2e-4 + 2e-4 |y| as the split test above. The head's embedding add:
+    x += table[bucketize(v)] with v = pred * control (pred scaled in place) or the target (pred
+    kept), exact against torch on the kernel's own predictions (modules.py:80-100,117-126)."""
+    from fs2amd.runtime import variance_predictor, variance_predictors
+    from fs2amd.model import FastSpeech2
+    from fs2amd.synth_weights import fill_module
+    from _common import configs
+
+    pc, mc, _ = configs()
+    m = FastSpeech2(pc, mc)
+    fill_module(m, seed=0)
+    m = m.to("cuda").eval()
+    P32 = m.set_precision("bf16", "fp32").packed("cuda")
+    P3 = m.set_precision("bf16", "bf16x3").packed("cuda")
+    assert P3.vpcols is not None
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, L, 256, generator=g).to("cuda", torch.bfloat16)
+    lens = torch.randint(1, L + 1, (B,), generator=g).to("cuda")
+    dp = variance_predictors(P3.vpcols.dp, x, lens)
+    en = variance_predictors(P3.vpcols.energy, x, lens)
+    assert dp.shape == (2, B, L) and en.shape == (1, B, L)
+    for got, k in ((dp[0], "duration"), (dp[1], "pitch"), (en[0], "energy")):
+        ref = variance_predictor(P32.vp[k], x, lens)
+        err = (ref - got).abs()
+        assert bool((err <= 2e-4 + 2e-4 * ref.abs()).all()), (k, float(err.max()))
+        pad = torch.arange(L, device="cuda")[None, :] >= lens[:, None]
+        assert bool((got[pad] == 0).all())
+    bins, table = P3.bins["pitch"], P3.var_table["pitch"]
+
+    def embedded(v):
+        idx = torch.bucketize(v, bins)
+        return (x.float() + table[idx]).to(torch.bfloat16)
+
+    x2 = x.clone()
+    p2 = variance_predictors(P3.vpcols.dp, x2, lens, embed=(1, x2, None, 1.3, bins, table))
+    assert torch.equal(p2[0], dp[0]) and torch.equal(p2[1], dp[1] * 1.3)
+    assert torch.equal(x2, embedded(p2[1]))
+    tgt = torch.randn(B, L, generator=g).to("cuda")
+    x3 = x.clone()
+    p3 = variance_predictors(P3.vpcols.dp, x3, lens, embed=(1, x3, tgt, 1.0, bins, table))
+    assert torch.equal(p3[1], dp[1]) and torch.equal(x3, embedded(tgt))
+
+
 @pytest.mark.parametrize("compute", [0, 1])
 @pytest.mark.parametrize("B,T,packed,shape", [
     (1, 8576, False, None),    # 67 x 8 tiles: one full round + a 24-tile tail (256 CUs)

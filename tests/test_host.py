@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
     lib = _lib.load()
     declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
-    assert len(declared) == len(_lib.SIGNATURES) == 13
+    assert len(declared) == len(_lib.SIGNATURES) == 16
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
@@ -40,7 +40,7 @@ def test_conv_desc_layout_matches_header():
 #include "fs2hip.h"
 #define P(f) printf("%s %zu\n", #f, offsetof(fs2_conv_desc, f));
 int main(void){ P(x) P(x_row_stride) P(w) P(B) P(compute) P(residual) P(res_row_stride) P(ln_gamma) P(ln_eps)
- P(lens) P(dot_w) P(dot_b) P(out) P(out_dtype) P(out_row_stride) printf("size %zu\n", sizeof(fs2_conv_desc)); }
+ P(lens) P(dot_w) P(dot_b) P(out) P(out_dtype) P(out_row_stride) P(out_div) P(group_n) P(group_cin) printf("size %zu\n", sizeof(fs2_conv_desc)); }
 '''
     d = tempfile.mkdtemp()
     with open(os.path.join(d, "t.c"), "w") as f:
@@ -67,6 +67,9 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     assert lib.fs2_attention(None, 0, 768, None, 1, 1, 2, 128, 11.3, None, 256, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_lr_durations(None, 0, 1.0, 1, 1, None, None, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_lr_expand(None, 0, None, None, 1, 1, 8, 1, None, None, 0, None, None, None) == _lib.FS2_EINVAL
+    assert lib.fs2_vp_norm(None, 512, 1, 2, 256, None, None, 1e-5, None, 1024, None) == _lib.FS2_EINVAL
+    assert lib.fs2_vp_head(None, 512, 1, 1, 2, 256, None, None, 1e-5, None, None, None, None, -1, None, 0, 256, 256,
+                           None, 1.0, None, 256, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_seq_layout(None, 1, 1, None, None, None, None) == _lib.FS2_EINVAL
 
 

@@ -98,6 +98,22 @@ def main():
                                       P.emo_table, P.aro_table, P.val_table, P.emo_w, P.emo_b, P.d_model)
     elif a.kernel == "layout":  # packed-sequence layout of the decoder frames
         fn = lambda: ops.SeqLayout(lens, T)
+    elif a.kernel in ("vp_c1", "vp_c2", "vpcols"):  # column-split duration + pitch predictors
+        from fs2amd.runtime import variance_predictors
+        F = P.vpcols.dp
+        xe = rnd(64, 64, 256)
+        le = b["src_lens"]
+        y1 = torch.randn(64, 64, 512, generator=g).to(dev)
+        h = rnd(64, 64, 1024)
+        if a.kernel == "vp_c1":
+            fn = lambda: ops.conv1d(xe, F.w1, F.b1, cin=2 * F.c, ks=F.k, pad=F.p, compute=L.FS2_BF16,
+                                    epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_F32, cin_block=F.c, cin_src=(0, 0))
+        elif a.kernel == "vp_c2":
+            fn = lambda: ops.conv1d(h, F.w2, F.b2, cin=3 * F.c, ks=F.k, pad=F.p, compute=L.FS2_BF16,
+                                    epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_F32, cin_block=F.c,
+                                    cin_src=(0, 0, F.c), group=(F.c, 2 * F.c))
+        else:
+            fn = lambda: variance_predictors(F, xe, le)
     elif a.kernel in ("enc_conv9", "enc_ln", "vp"):
         Be, Le = 64, 64
         xe = rnd(Be, Le, 256)
@@ -116,15 +132,27 @@ def main():
     else:
         raise SystemExit(f"unknown kernel {a.kernel}")
     if a.time:
-        for _ in range(3):
-            fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(a.reps):
-            fn()
-        e1.record()
-        e1.synchronize()
-        print(f"{a.kernel}: {e0.elapsed_time(e1) * 1e3 / a.reps:.2f} us/launch")
+        # the reps are captured as one HIP graph and replayed: small launches are host-bound when
+        # issued from Python one by one (~15 us of ctypes / allocator work per call)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize(dev)
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=s):
+                for _ in range(a.reps):
+                    fn()
+            gr.replay()
+            torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(3):
+                gr.replay()
+            e1.record(s)
+            e1.synchronize()
+        print(f"{a.kernel}: {e0.elapsed_time(e1) * 1e3 / (3 * a.reps):.2f} us/launch (graph)")
         return
     for _ in range(a.reps):
         fn()
