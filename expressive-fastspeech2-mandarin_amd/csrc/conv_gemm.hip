@@ -30,6 +30,7 @@
 #include <type_traits>
 
 #include "fs2_common.h"
+#include "gemm_wres.h"
 
 namespace {
 
@@ -2096,6 +2097,35 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.out_div = d->out_div != 0.0f ? d->out_div : 1.0f;
   a.l2pf = 0;
   const bool xb = d->x_dtype == FS2_BF16;
+  {  // short-K, wide-N bf16 projections (Q|K|V): the weight-resident kernel (gemm_wres.hip)
+    static const bool wres = [] {
+      const char *e = getenv("FS2_WRES");
+      return e == nullptr || e[0] != '0';
+    }();
+    if (wres && d->compute == FS2_BF16 && xb && d->out_dtype == FS2_BF16 && d->KS == 1 && d->pad == 0 &&
+        (epi == FS2_EPI_BIAS || epi == FS2_EPI_BIAS_RELU) && d->Cin == d->Cin_pad && d->Cin <= 256 &&
+        d->N % 128 == 0 && d->a_rowmap == nullptr && d->cin_block == 0 && d->group_n == 0 && d->out2 == nullptr &&
+        d->col_scale == nullptr && dil == 1 && a.M >= 2048) {
+      WresArgs w;
+      w.x = d->x;
+      w.xs = d->x_row_stride;
+      w.w = d->w;
+      w.bias = d->bias;
+      w.out = d->out;
+      w.os = d->out_row_stride;
+      w.M = a.M;
+      w.rows_dev = d->rows_dev;
+      w.N = d->N;
+      w.K = d->Cin;
+      w.relu = epi == FS2_EPI_BIAS_RELU ? 1 : 0;
+      w.x_bytes = a.x_bytes;
+      w.w_bytes = a.w_bytes;
+      if (wres_launch(w, num_cus(), s)) {
+        FS2_CHECK_LAUNCH();
+        return FS2_OK;
+      }
+    }
+  }
   if (d->compute == FS2_FP8)
     dispatch<FS2_FP8, fp8>(a, ln, s);
   else if (d->compute == FS2_BF16)

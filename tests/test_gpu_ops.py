@@ -505,3 +505,42 @@ def test_conv_splitk_tail(ops, compute, B, T, packed, shape):
         err = float((o - r).abs().max() / (r.abs().max() + 1e-6))
         assert err < _tol(compute), err
         assert torch.equal(o, outs[0].reshape(-1, N)[:rows].float())
+
+
+@pytest.mark.parametrize("K,N,relu,packed", [(256, 768, False, False), (256, 768, False, True), (128, 256, True, False),
+                                             (64, 384, False, True), (192, 1280, True, False)])
+def test_weight_resident_projection(ops, K, N, relu, packed):
+    """Short-K bf16 projections (Q|K|V shape) take the weight-resident kernel (gemm_wres.hip):
+    vs torch fp32 on the same bf16 operands, |d| <= 1e-2 * max|y| (bf16 output rounding); packed
+    rows: only the valid rows are written."""
+    L = _L()
+    g = torch.Generator().manual_seed(21)
+    B, T = 7, 433  # 3,031 rows: not a multiple of the 64-row tile
+    x = torch.randn(B, T, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / np.sqrt(K))
+    b = torch.randn(N, generator=g) * 0.1
+    wp = ops.pack_conv_weight(w.to(DEV), 1)
+    epi = L.EPI_BIAS_RELU if relu else L.EPI_BIAS
+    ref = x.float().cpu() @ wp.float().cpu()[:, 0, :].T + b
+    if relu:
+        ref = ref.clamp_min(0)
+    if packed:
+        lens = torch.randint(0, T + 1, (B,), generator=g).to(DEV)
+        lay = ops.SeqLayout(lens, T)
+        xp = torch.zeros(B * T, K, device=DEV, dtype=torch.bfloat16)
+        rm = lay.rowmap.long()
+        ok = rm >= 0
+        xp[rm[ok]] = x.view(B * T, K)[ok]
+        out = torch.full((B * T, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+        ops.conv1d(xp, wp, b.to(DEV), cin=K, ks=1, pad=0, compute=1, epilogue=epi, out=out, layout=lay)
+        got = lay.unpack(out).float().cpu()
+        mask = (torch.arange(T)[None, :] < lens.cpu()[:, None]).unsqueeze(-1)
+        ref = ref * mask
+        rows = int(lay.cu[-1])
+        assert bool(torch.isnan(out[rows:].float()).all())  # nothing written past the active rows
+    else:
+        got = ops.conv1d(x, wp, b.to(DEV), cin=K, ks=1, pad=0, compute=1, epilogue=epi,
+                         out_dtype=L.FS2_BF16).float().cpu()
+    torch.cuda.synchronize()
+    err = (got - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err
