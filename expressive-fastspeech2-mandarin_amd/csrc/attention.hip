@@ -263,16 +263,17 @@ __device__ __forceinline__ void attn_vm_wait() {
 // NWV waves (16 queries each) per workgroup, an NST-deep K/V ring: the DMA of key tile kt+NST-1
 // is issued right after the barrier that retires tile kt-1, so each tile has NST-1 tiles of
 // compute to land; one counted vmcnt + one barrier per tile.
-template <int NWV, int NST>
+template <int NWV, int NST, int KTT = KT>
 __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__restrict__ qkv, int64_t qs,
                                                                 uint32_t qkv_bytes, const int64_t *__restrict__ lens,
                                                                 int B, int T, int H, int nqt, float scale_log2,
                                                                 bf16 *__restrict__ out, int64_t os,
                                                                 const int32_t *__restrict__ cu) {
   constexpr int QTW = 16 * NWV;          // queries per workgroup
-  constexpr int PPW = 16 / NWV;          // K (and V) 1 KiB pieces per wave per tile
+  static_assert(KTT == 64 || KTT == 32, "keys per tile");
+  constexpr int PPW = KTT / 4 / NWV;     // K (and V) 1 KiB pieces per wave per tile
   constexpr int LPS = 2 * PPW;           // LDS-DMA loads per wave per tile
-  constexpr int STG = 2 * KT * 256;      // K + V bytes of one tile
+  constexpr int STG = 2 * KTT * 256;     // K + V bytes of one tile
   __shared__ __attribute__((aligned(16))) char smem[NST * STG];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -314,7 +315,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
   const int prow = lane >> 4, pch = lane & 15;
   auto dma = [&](int k0, int buf) {
     char *Kb = smem + buf * STG;
-    char *Vb = Kb + KT * 256;
+    char *Vb = Kb + KTT * 256;
 #pragma unroll
     for (int it = 0; it < PPW; ++it) {
       const int p = w + NWV * it;
@@ -337,11 +338,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
   // running max kept in RAW score units (scale > 0 commutes with max): p = exp2(fma(s, c, -m*c))
   float m_run = -INFINITY, l_run = 0.f;
 
-  const int ntiles = (len + KT - 1) / KT;
+  const int ntiles = (len + KTT - 1) / KTT;
   // the Q loads are waited for with the first tile (they were issued first)
 #pragma unroll
   for (int st = 0; st < NST - 1; ++st)
-    if (st < ntiles) dma(st * KT, st);
+    if (st < ntiles) dma(st * KTT, st);
   // transposed-read lane roles: lane 4q+p of its 16-lane group addresses row q, columns 4p..4p+3.
   // kv_off's swizzle depends on (row & 3, (row >> 2) & 3), so rows +16 / +32 are +4 / +8 KiB:
   // only the 8 column-block offsets of row r0 are lane-specific (hoisted out of the key loop).
@@ -350,7 +351,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
 #pragma unroll
   for (int nd = 0; nd < DK / 16; ++nd) voff[nd] = kv_off(4 * g + tq, nd * 2 + (tp >> 1)) + (tp & 1) * 8;
   for (int kt = 0; kt < ntiles; ++kt) {
-    const int k0 = kt * KT;
+    const int k0 = kt * KTT;
     // tile kt landed (this wave's pieces); tiles issued after it may stay in flight
     const int ahead = ntiles - 1 - kt;
     if (NST >= 3 && ahead >= NST - 2)
@@ -363,14 +364,15 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
     // would drain vmcnt to 0 and with it the tiles still in flight.
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + NST - 1 < ntiles) dma(k0 + (NST - 1) * KT, (kt + NST - 1) % NST);
+    if (kt + NST - 1 < ntiles) dma(k0 + (NST - 1) * KTT, (kt + NST - 1) % NST);
     if (!active) continue;
     const char *Kb = smem + (kt % NST) * STG;
-    const char *Vb = Kb + KT * 256;
+    const char *Vb = Kb + KTT * 256;
 
-    f32x4 sacc[4];
+    constexpr int NB = KTT / 16;  // 16-key blocks per tile
+    f32x4 sacc[NB];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
+    for (int ni = 0; ni < NB; ++ni) {
       sacc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -379,16 +381,16 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
       }
     }
     // scores of query li: keys k0 + ni*16 + 4g + j; only the last tile can hold padded keys
-    if (k0 + KT > len) {
+    if (k0 + KTT > len) {
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
+      for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (k0 + ni * 16 + 4 * g + j >= len) sacc[ni][j] = -INFINITY;
     }
     float mx = -INFINITY;
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) mx = fmaxf(mx, fmaxf(fmaxf(sacc[ni][0], sacc[ni][1]), fmaxf(sacc[ni][2], sacc[ni][3])));
+    for (int ni = 0; ni < NB; ++ni) mx = fmaxf(mx, fmaxf(fmaxf(sacc[ni][0], sacc[ni][1]), fmaxf(sacc[ni][2], sacc[ni][3])));
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
@@ -397,9 +399,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
     m_run = m_new;
     const float mc = -m_new * scale_log2;
     float sum = 0.f;
-    bf16x8 pf[2];
+    bf16x8 pf[NB / 2];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
+    for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[ni][j], scale_log2, mc));
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
     for (int nd = 0; nd < DK / 16; ++nd) oacc[nd] *= alpha;
 
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
+    for (int s2 = 0; s2 < NB / 2; ++s2) {
       // this lane's address row r0 = 32*s2 + 4g + tq (block 1), r0 + 16 for block 2
 #pragma unroll
       for (int nd = 0; nd < DK / 16; ++nd) {
@@ -670,6 +672,16 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
       hipLaunchKernelGGL((attn_bf16_kernel<4, 3>), dim3(nqt * H * B), dim3(256), 0, s,
                          reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
                          scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
+    } else if (variant == 6 || variant == 7) {  // 8 waves, 32-key tiles: 3 / 4-deep ring at 2 workgroups per CU
+      const int nqt = (T + 127) / 128;
+      if (variant == 6)
+        hipLaunchKernelGGL((attn_bf16_kernel<8, 3, 32>), dim3(nqt * H * B), dim3(512), 0, s,
+                           reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H,
+                           nqt, scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
+      else
+        hipLaunchKernelGGL((attn_bf16_kernel<8, 4, 32>), dim3(nqt * H * B), dim3(512), 0, s,
+                           reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H,
+                           nqt, scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
     } else if (variant == 4 || variant == 5) {  // 32 queries per wave: 4 waves (128 q) or 8 waves (256 q)
       const int qtw = variant == 4 ? 128 : 256;
       const int nqt = (T + qtw - 1) / qtw;
