@@ -350,7 +350,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
   int voff[DK / 16];
 #pragma unroll
   for (int nd = 0; nd < DK / 16; ++nd) voff[nd] = kv_off(4 * g + tq, nd * 2 + (tp >> 1)) + (tp & 1) * 8;
-  for (int kt = 0; kt < ntiles; ++kt) {
+  // one key tile; MASKED (the last tile only) sets the scores of keys >= len to -inf
+  auto tile = [&](int kt, auto masked_tag) {
+    constexpr bool MASKED = decltype(masked_tag)::value;
     const int k0 = kt * KTT;
     // tile kt landed (this wave's pieces); tiles issued after it may stay in flight
     const int ahead = ntiles - 1 - kt;
@@ -365,7 +367,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + NST - 1 < ntiles) dma(k0 + (NST - 1) * KTT, (kt + NST - 1) % NST);
-    if (!active) continue;
+    if (!active) return;
     const char *Kb = smem + (kt % NST) * STG;
     const char *Vb = Kb + KTT * 256;
 
@@ -380,13 +382,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
         sacc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], sacc[ni], 0, 0, 0);
       }
     }
-    // scores of query li: keys k0 + ni*16 + 4g + j; only the last tile can hold padded keys
-    if (k0 + KTT > len) {
+    // scores of query li: keys k0 + ni*16 + 4g + j
+    if constexpr (MASKED) {
+      const int lim = len - k0 - 4 * g;
 #pragma unroll
       for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (k0 + ni * 16 + 4 * g + j >= len) sacc[ni][j] = -INFINITY;
+          if (ni * 16 + j >= lim) sacc[ni][j] = -INFINITY;
     }
     float mx = -INFINITY;
 #pragma unroll
@@ -394,8 +397,15 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
-    // raw v_exp_f32 (exp2; underflow -> 0, -inf -> 0): libm exp2f's range reduction is dead work here
-    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2);
+    // rescale only when some query's running max moved (alpha == 1 exactly for the others): after
+    // the first tiles of a sequence the max rarely moves, and the O rescale is 32 VALU per wave
+    if (__builtin_amdgcn_ballot_w64(m_new != m_run) != 0) {
+      // raw v_exp_f32 (exp2; underflow -> 0, -inf -> 0): libm exp2f's range reduction is dead work here
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2);
+      l_run *= alpha;
+#pragma unroll
+      for (int nd = 0; nd < DK / 16; ++nd) oacc[nd] *= alpha;
+    }
     m_run = m_new;
     const float mc = -m_new * scale_log2;
     float sum = 0.f;
@@ -410,9 +420,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
       }
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
-    l_run = l_run * alpha + sum;
-#pragma unroll
-    for (int nd = 0; nd < DK / 16; ++nd) oacc[nd] *= alpha;
+    l_run += sum;
 
 #pragma unroll
     for (int s2 = 0; s2 < NB / 2; ++s2) {
@@ -428,7 +436,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
         oacc[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[s2], oacc[nd], 0, 0, 0);
       }
     }
-  }
+  };
+  // every tile but the last is fully inside the sequence (keys < len): no masking work there
+  for (int kt = 0; kt + 1 < ntiles; ++kt) tile(kt, std::false_type{});
+  if (ntiles > 0) tile(ntiles - 1, std::true_type{});
 
   // O^T[d = nd*16 + 4g + j][query li]
   const int q = q0 + 16 * w + li;
