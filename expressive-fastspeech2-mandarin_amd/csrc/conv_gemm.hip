@@ -2102,7 +2102,8 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
       const char *e = getenv("FS2_WRES");
       return e == nullptr || e[0] != '0';
     }();
-    if (wres && d->compute == FS2_BF16 && xb && d->out_dtype == FS2_BF16 && d->KS == 1 && d->pad == 0 &&
+    if (wres && d->compute == FS2_BF16 && xb && (d->out_dtype == FS2_BF16 || d->out_dtype == FS2_F32) && d->KS == 1 &&
+        d->pad == 0 &&
         (epi == FS2_EPI_BIAS || epi == FS2_EPI_BIAS_RELU) && d->Cin == d->Cin_pad && d->Cin <= 256 &&
         d->N % 128 == 0 && d->a_rowmap == nullptr && d->cin_block == 0 && d->group_n == 0 && d->out2 == nullptr &&
         d->col_scale == nullptr && dil == 1 && a.M >= 2048) {
@@ -2118,6 +2119,7 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
       w.N = d->N;
       w.K = d->Cin;
       w.relu = epi == FS2_EPI_BIAS_RELU ? 1 : 0;
+      w.out_f32 = d->out_dtype == FS2_F32 ? 1 : 0;
       w.x_bytes = a.x_bytes;
       w.w_bytes = a.w_bytes;
       if (wres_launch(w, num_cus(), s)) {

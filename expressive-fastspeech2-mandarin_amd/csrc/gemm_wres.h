@@ -7,12 +7,13 @@ struct WresArgs {
   int64_t xs;             // x row stride (elements)
   const void *w;          // packed bf16 [N][K] (Conv1d k=1 / Linear)
   const float *bias;      // [N] or NULL
-  void *out;              // bf16 [rows][os]
+  void *out;              // bf16 (or f32 with out_f32) [rows][os]
   int64_t os;
   int M;                  // rows (padded layout) ...
   const int32_t *rows_dev;  // ... or the device-side active row count (packed layout), or NULL
   int N, K;               // N % 128 == 0, K in {64, 128, 192, 256}
   int relu;               // 0: y = acc + bias, 1: relu(acc + bias)
+  int out_f32;            // f32 output (16-byte stores) instead of bf16
   uint32_t x_bytes, w_bytes;
 };
 

@@ -186,15 +186,19 @@ __global__ __launch_bounds__(512, 1) void gemm_wres_kernel(WresArgs a, int nslic
       const int m = rbase + mi * 16;
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
-        bf16x4 o;
+        float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float v = acc[ni][mi][j] + bias4[ni][j];
-          if (a.relu) v = fmaxf(v, 0.0f);
-          o[j] = (bf16)v;
+          v[j] = acc[ni][mi][j] + bias4[ni][j];
+          if (a.relu) v[j] = fmaxf(v[j], 0.0f);
         }
-        if (m < M)
-          *reinterpret_cast<bf16x4 *>(out + (int64_t)m * a.os + n0 + wc * 32 + ni * 16 + 4 * (lane >> 4)) = o;
+        const int64_t o = (int64_t)m * a.os + n0 + wc * 32 + ni * 16 + 4 * (lane >> 4);
+        if (m < M) {
+          if (a.out_f32)
+            *reinterpret_cast<float4 *>(reinterpret_cast<float *>(a.out) + o) = make_float4(v[0], v[1], v[2], v[3]);
+          else
+            *reinterpret_cast<bf16x4 *>(out + o) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        }
       }
     }
     buf = buf == NA - 1 ? 0 : buf + 1;
