@@ -68,12 +68,38 @@ class Conv1dFn(torch.autograd.Function):
                 xu = xc.reshape(B * T, Cin)
             else:
                 xu = F.pad(xc, (0, 0, pad, KS - 1 - pad)).unfold(1, KS, 1).reshape(B * T, Cin * KS)
-            dw = torch.matmul(dyc.reshape(B * T, N).t(), xu).float().view(N, Cin, KS)
+            dw = _wgrad(dyc.reshape(B * T, N), xu, B).view(N, Cin, KS)
             if ctx.linear:
                 dw = dw.view(N, Cin)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum((0, 1))
         return dx, dw, db, None, None
+
+
+def _wgrad_chunks(rows, B, N, K):
+    """Row chunks of the weight-gradient GEMM: a small dW (fc 256 x 256, FFN w_2 256 x 1024, VP)
+    reduced over ~7k rows as one GEMM runs on a handful of workgroups; split into C batched GEMMs
+    (C | B, f32 partials of <= 4 MiB in total) summed afterwards. FS2_WGRAD_SPLIT=0: one GEMM."""
+    import os
+    if os.environ.get("FS2_WGRAD_SPLIT", "1") == "0":
+        return 1
+    c = 1
+    while c * 2 <= B and B % (c * 2) == 0 and (c * 2) * N * K * 4 <= (4 << 20) and rows // (c * 2) >= 128:
+        c *= 2
+    return c
+
+
+def _wgrad(dy2, xu, B):
+    """dW [N, K] = dy2^T xu over the rows (dy2 [rows, N], xu [rows, K], same dtype), f32 out."""
+    rows, N = dy2.shape
+    K = xu.shape[1]
+    c = _wgrad_chunks(rows, B, N, K)
+    if c == 1 or not dy2.is_cuda:
+        return torch.matmul(dy2.t(), xu).float()
+    r = rows // c
+    out = torch.bmm(dy2.view(c, r, N).transpose(1, 2), xu.view(c, r, K), out_dtype=torch.float32) \
+        if dy2.dtype != torch.float32 else torch.bmm(dy2.view(c, r, N).transpose(1, 2), xu.view(c, r, K))
+    return out.sum(0)
 
 
 def conv1d(x, conv, pad, compute):
