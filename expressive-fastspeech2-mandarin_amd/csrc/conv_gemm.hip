@@ -366,7 +366,10 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
     };
     const bool res_bf16 = a.res_dt == FS2_BF16;
     uint4 rraw[NP][2];
-    if (epi == FS2_EPI_RES_LN) {
+    if (epi == FS2_EPI_RES_LN && (a.dbg & 8)) {  // analysis: no residual loads
+#pragma unroll
+      for (int p = 0; p < NP; ++p) rraw[p][0] = rraw[p][1] = make_uint4(0u, 0u, 0u, 0u);
+    } else if (epi == FS2_EPI_RES_LN) {
       load_res_pairs<NP, NWAVES>(a, m0, M, tid, rraw);
 #pragma unroll
       for (int p = 0; p < NP; ++p)
@@ -403,14 +406,15 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
       float s1 = 0.f;
 #pragma unroll
       for (int q = 0; q < 8; ++q) s1 += v[q];
-      const float mean = hsum(s1) * inv_n;
+      const bool nored = (a.dbg & 16) != 0;  // analysis: lane-local statistics (no shuffles)
+      const float mean = (nored ? s1 : hsum(s1)) * inv_n;
       float d[8], ss = 0.f;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         d[q] = v[q] - mean;
         ss += d[q] * d[q];
       }
-      const float var = hsum(ss) * inv_n;
+      const float var = (nored ? ss : hsum(ss)) * inv_n;
       const float rstd = 1.0f / sqrtf(var + a.eps);
       float y[8];
 #pragma unroll
@@ -447,6 +451,10 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
         }
       }
       if (!row_ok) continue;
+      if (a.dbg & 4) {  // analysis: no output stores
+        asm volatile("" ::"v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]), "v"(y[4]), "v"(y[5]), "v"(y[6]), "v"(y[7]));
+        continue;
+      }
       if (a.out_split) {  // two bf16 planes: hi, lo = bf16(y - hi)
         float hi[8], lo[8];
         bf16 *op = reinterpret_cast<bf16 *>(a.out) + (int64_t)m * a.os;
@@ -1483,8 +1491,11 @@ __device__ __forceinline__ void vm_wait() {
 // breaks the packed == padded bit-exactness; not offered.)
 // BN = 128: the column-split tiles of the small-M elementwise-epilogue GEMMs (variance
 // predictor convs: every workgroup streams only its columns' weights, with the ring's depth).
+// NS == 2 with <= 64-row tiles: 80 KiB of LDS, two workgroups per CU (one's LayerNorm epilogue and
+// stores overlap the other's K loop).
 template <int CT, int WGM, int WMI, int NS, int WGN = 4, int BN = 256>
-__global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvArgs a) {
+__global__ __launch_bounds__(64 * WGM * WGN, (NS == 2 && 16 * WMI * WGM <= 64) ? 2 : 1) void conv_gemm_ring_kernel(
+    ConvArgs a) {
   static_assert(WGN == 4 || WGN == 8, "column waves");
   static_assert(BN == 256 || BN == 128, "tile width");
   constexpr int NW = WGM * WGN, WCOL = BN / WGN, NI = WCOL / 16;
@@ -1499,7 +1510,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_gemm_ring_kernel(ConvA
   constexpr int STAGE = (AP + BP) * 1024;
   constexpr int EPI_LD = BN + 4;
   constexpr int SMEM = (NS * STAGE > BM * EPI_LD * 4) ? NS * STAGE : BM * EPI_LD * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + 16];  // + the split-K flag word
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + (WGN == 4 ? 16 : 0)];  // + the split-K flag word
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1892,7 +1903,17 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         const char *e = getenv("FS2_LN_W16DEC");
         return e == nullptr || e[0] != '0';
       }();
-      if (a.M >= 192 * 128 && w16d)
+      // short-K decoder LN GEMMs (fc + residual + LN: K = 256, 4 k-steps): 64-row, 2-stage tiles,
+      // two workgroups per CU, so one's LayerNorm epilogue and stores overlap the other's K loop
+      // (fc + LN 17.0 -> 16.2 us; the K = 1024 conv-k1 + LN is neutral and keeps the 128-row tile).
+      // FS2_LN_2WG: 0 off, 1 on for every decoder LN GEMM, default short K only.
+      static const int two = [] {
+        const char *e = getenv("FS2_LN_2WG");
+        return e != nullptr ? atoi(e) : 2;
+      }();
+      if (a.M >= 192 * 128 && (two == 1 || (two == 2 && a.KS * a.Cin_pad <= 256)))
+        launch_ring<CT, 1, 4, 2, 8>(a, s);  // 64 x 256, 8 waves of 64 x 32, 2 stages (80 KiB)
+      else if (a.M >= 192 * 128 && w16d)
         launch_ring<CT, 2, 4, 3, 8>(a, s);  // 128 x 256, 16 waves of 64 x 32, 3 stages
       else if (a.M >= 192 * 128)
         launch_ring<CT, 2, 4, 3>(a, s);  // 128 x 256, 8 waves, 3 stages (144 KiB)
