@@ -546,7 +546,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_q32_kernel(const bf16 *
   int voffs[DK / 16];
 #pragma unroll
   for (int nd = 0; nd < DK / 16; ++nd) voffs[nd] = kv_off(4 * g + tq, nd * 2 + (tp >> 1)) + (tp & 1) * 8;
-  for (int kt = 0; kt < ntiles; ++kt) {
+  // one key tile; MASKED (the last tile only) sets the scores of keys >= len to -inf
+  auto tile = [&](int kt, auto masked_tag) {
+    constexpr bool MASKED = decltype(masked_tag)::value;
     const int k0 = kt * KT;
     const int ahead = ntiles - 1 - kt;
     if (NST >= 3 && ahead >= NST - 2)
@@ -556,7 +558,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_q32_kernel(const bf16 *
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + NST - 1 < ntiles) dma(k0 + (NST - 1) * KT, (kt + NST - 1) % NST);
-    if (!active) continue;
+    if (!active) return;
     const char *Kb = smem + (kt % NST) * STG;
     const char *Vb = Kb + KT * 256;
 
@@ -575,12 +577,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_q32_kernel(const bf16 *
     bf16x8 pf[2][2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
-      if (k0 + KT > len) {
+      if constexpr (MASKED) {
+        const int lim = len - k0 - 4 * g;
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (k0 + ni * 16 + 4 * g + j >= len) sacc[qb][ni][j] = -INFINITY;
+            if (ni * 16 + j >= lim) sacc[qb][ni][j] = -INFINITY;
       }
       float mx = -INFINITY;
 #pragma unroll
@@ -589,7 +592,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_q32_kernel(const bf16 *
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_run[qb], mx);
-      const float alpha = __builtin_amdgcn_exp2f((m_run[qb] - m_new) * scale_log2);
+      if (__builtin_amdgcn_ballot_w64(m_new != m_run[qb]) != 0) {  // exact: alpha == 1 otherwise
+        const float alpha = __builtin_amdgcn_exp2f((m_run[qb] - m_new) * scale_log2);
+        l_run[qb] *= alpha;
+#pragma unroll
+        for (int nd = 0; nd < DK / 16; ++nd) oacc[qb][nd] *= alpha;
+      }
       m_run[qb] = m_new;
       const float mc = -m_new * scale_log2;
       float sum = 0.f;
@@ -603,9 +611,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_q32_kernel(const bf16 *
         }
       sum += __shfl_xor(sum, 16, 64);
       sum += __shfl_xor(sum, 32, 64);
-      l_run[qb] = l_run[qb] * alpha + sum;
-#pragma unroll
-      for (int nd = 0; nd < DK / 16; ++nd) oacc[qb][nd] *= alpha;
+      l_run[qb] += sum;
     }
 
 #pragma unroll
@@ -622,7 +628,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_q32_kernel(const bf16 *
         oacc[1][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1][s2], oacc[1][nd], 0, 0, 0);
       }
     }
-  }
+  };
+  for (int kt = 0; kt + 1 < ntiles; ++kt) tile(kt, std::false_type{});
+  if (ntiles > 0) tile(ntiles - 1, std::true_type{});
 
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
