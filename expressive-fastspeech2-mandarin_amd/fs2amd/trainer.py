@@ -29,13 +29,16 @@ class TrainStep:
     shapes falls back to an eager step."""
 
     def __init__(self, model, preprocess_config, model_config, train_config, device=None, world_size=1,
-                 bucket_mb=32, current_step=0, graph=False, warmup=3):
+                 bucket_mb=32, current_step=0, graph=False, warmup=3, ddp=None):
         self.model = model.train()
         self.net = model
         self.graph_mode = bool(graph) and world_size == 1 and device is not None and device.type == "cuda"
         self.warmup = warmup
         self._graph = None
-        if world_size > 1:
+        if ddp is None:
+            ddp = world_size > 1
+        if ddp:  # ddp=True at world size 1 still runs DDP's bucketed all-reduce (the RCCL path on one GPU)
+            self.graph_mode = False
             ids = [device.index] if device is not None and device.type == "cuda" else None
             self.net = nn.parallel.DistributedDataParallel(model, device_ids=ids, bucket_cap_mb=bucket_mb,
                                                            gradient_as_bucket_view=True, broadcast_buffers=True)

@@ -152,3 +152,52 @@ def test_graphed_train_step_equals_eager(gpu):
     np.testing.assert_allclose(lg, le, rtol=1e-5)
     for k in pe:
         assert torch.allclose(pg[k], pe[k], rtol=1e-4, atol=1e-6), k
+
+
+def test_ddp_step_over_rccl_equals_plain(gpu):
+    """The data-parallel training path (train.py:52-53 DataParallel -> one process per GPU, DDP over
+    RCCL): a single-rank "nccl" process group wraps TrainStep in DistributedDataParallel, so every
+    step runs DDP's gradient buckets through RCCL all-reduce on the MI355X. With one rank the
+    average is the identity: losses and parameters equal the un-wrapped step (fp32, dropout off)."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+
+    from fs2amd import config as C
+    from fs2amd.data import synth_batch, to_device
+    from fs2amd.model import FastSpeech2
+    from fs2amd.trainer import TrainStep
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="env://", rank=0, world_size=1)
+    try:
+        assert dist.get_backend() == "nccl"
+        t = torch.ones(1024, device=DEV)
+        dist.all_reduce(t)
+        assert float(t.sum()) == 1024.0
+        pc, mc, _ = configs()
+        tc = C.ESD_TRAIN_CONFIG
+        runs = []
+        for ddp in (False, True):
+            m = FastSpeech2(pc, mc)
+            m.load_state_dict(oracle_state_dict())
+            m = m.to(DEV).set_precision("fp32")
+            m.train_dropout = False
+            st = TrainStep(m, pc, mc, tc, device=torch.device(DEV), ddp=ddp, bucket_mb=4)
+            assert isinstance(st.net, torch.nn.parallel.DistributedDataParallel) == ddp
+            base = synth_batch(4, 8, 20, seed=41, with_mels=True, pe_targets=True)
+            losses = [float(st(to_device(dict(base, mels=base["mels"] * (1 + 0.1 * i)), DEV))[0]) for i in range(3)]
+            torch.cuda.synchronize()
+            runs.append((losses, {k: p.detach().clone() for k, p in m.named_parameters()}))
+        (lp, pp), (ld, pd) = runs
+        np.testing.assert_allclose(ld, lp, rtol=1e-5)
+        for k in pp:
+            assert torch.allclose(pd[k], pp[k], rtol=1e-4, atol=1e-6), k
+    finally:
+        dist.destroy_process_group()
