@@ -1727,13 +1727,19 @@ void launch_ring(ConvArgs a, hipStream_t s) {
   a.ngr = a.ntn;
   if (a.w_bytes > (2u << 20) && a.ntn > 2 && a.ntn % 2 == 0) a.ngr = 2;  // see launch(): L2-sized N groups
   int nwg = (a.M + BM - 1) / BM * a.ntn;
+  if (a.row_split == 2) {  // rows left after the phased panels (see launch())
+    const int left = (a.split_slots / ((a.N + 255) / 256) + 2) * 256;
+    const int bound = ((left + BM - 1) / BM) * a.ntn;
+    if (bound < nwg) nwg = bound;
+  }
   a.sk_slots = 0;
   {  // split-K (conv_tile_sk): one workgroup per CU; segments of >= 4 k-steps, at most 4 per tile
     const int slots = num_cus();
     const int nK = a.KS * (a.Cin_pad / CTraits<CT>::KE);
     const int64_t need = kSkCntBytes + (int64_t)slots * BM * BN * 4;
     const int sk_max = nK / 4 < 4 ? nK / 4 : 4;
-    if (WGN == 4 && splitk_env() && sk_would_split(nwg, slots, sk_max) && a.sk_cnt != nullptr && a.sk_ws_bytes >= need &&
+    if (WGN == 4 && splitk_env() && (a.row_split == 2 || sk_would_split(nwg, slots, sk_max)) && a.sk_cnt != nullptr &&
+        a.sk_ws_bytes >= need &&
         nK >= 8 && slots > 0 && slots * 4 <= kSkCntBytes) {
       a.sk_slots = slots;
       a.sk_max = sk_max;
@@ -1862,7 +1868,7 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       a2.row_split = 2;
       a2.split_slots = S;
       launch_8p(a1, s);
-      launch_128<CT, TIn>(a2, s);
+      launch_128<CT, TIn>(a2, s);  // (128 x 128 ring tiles here: 132 -> 148 us, no halo reuse)
       return;
     }
   }
@@ -1947,6 +1953,25 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       const char *e = getenv("FS2_CONV_NARROW");
       return e != nullptr ? atoi(e) : 1;
     }();
+    if constexpr (CT == FS2_BF16 && GLd) {
+      // FFN conv-k9 below the phased kernel's size (encoder, M = 4k): 128 x 128 tiles on the
+      // LDS-DMA ring (4 stages, 3 k-steps in flight, one workgroup per CU) instead of the
+      // double-buffered halo-reuse tiles: 36.8 -> 33.2 us. FS2_PLAIN_RING (A/B): 0 off,
+      // 2 (default) this, 1: 64 x 128 / 6 stages (42 us), 3: 64 x 128 / 4 stages (43 us).
+      static const int pring = [] {
+        const char *e = getenv("FS2_PLAIN_RING");
+        return e != nullptr ? atoi(e) : 2;
+      }();
+      if (pring && a.row_split == 0 && a.KS == 9 && a.Cin_pad == 256 && ntn > 1) {
+        if (pring == 1)
+          launch_ring<CT, 2, 2, 6, 4, 128>(a, s);
+        else if (pring == 2)
+          launch_ring<CT, 2, 4, 4, 4, 128>(a, s);
+        else
+          launch_ring<CT, 2, 2, 4, 4, 128>(a, s);
+        return;
+      }
+    }
     if (narrow && GLd && ntn == 1 && nKd >= 32 && splitk_env() && a.sk_cnt != nullptr &&
         (int64_t)((a.M + 127) / 128) >= 64)
       // one N tile and a long K (PostNet's last conv: N = 80, K = 2560): 128-row tiles and the
