@@ -14,8 +14,12 @@ job time; value = all valid mel frames of all ranks / job time.
 Also reported:
 * roofline — the dominant kernel (the FFN Conv1d k=9 implicit GEMM of the decoder, ~76 % of
   the FLOPs) timed with HIP events on the stream it launches on; achieved = algorithmic FLOPs
-  of one launch (valid frames x 2*256*9*1024) / its mean duration, vs 2.5 PF dense bf16.
+  of one op call (valid frames x 2*256*9*1024) / its mean duration over back-to-back calls in
+  one HIP graph (the eager in-forward time, which includes host launch gaps, is reported beside
+  it), vs 2.5 PF dense bf16.
   ``traffic`` comes from the committed rocprofv3 PMC pass (profiles/) when present.
+* decoder_ops — every op of one decoder FFT block (+ the LengthRegulator gather) at the same
+  shape, graph-timed, each with its algorithmic work and roofline fraction (bf16 line).
 * cpu_baseline — the oracle (CPU restatement of the reference, fp32 PyTorch) on a bounded
   sample of the same workload, rank 0 at N=1 only.
 """
@@ -164,6 +168,93 @@ def time_dominant_kernel(model, batch, device, reps):
     valid = int(batch["mel_lens"].sum())
     flops = 2.0 * valid * lp.c1 * lp.k1 * lp.w1.shape[0]
     return mean_s, flops
+
+
+def _graph_mean_s(fn, device, reps):
+    """Mean duration of one fn() when `reps` calls run back to back inside one HIP graph (the way
+    the bench's graph-replayed forward issues them: no host gap between launches); HIP events on
+    the capture stream, which is the stream the kernels launch on."""
+    s = torch.cuda.Stream(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize(device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize(device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(3):
+            g.replay()
+        e1.record(s)
+        e1.synchronize()
+    dt = e0.elapsed_time(e1) / 1e3 / (3 * reps)
+    del g
+    return dt
+
+
+def decoder_op_table(model, batch_cpu, device, reps):
+    """Every decoder op of one FFT block at the benched cfg2 shape (packed valid frames, as the
+    forward runs them), each timed as `reps` back-to-back launches in one HIP graph, with its
+    algorithmic work per call and the roofline that bounds it:
+      conv9  FFN Conv1d k=9 256->1024 + ReLU   2*F*256*9*1024 FLOP        MFMA
+      conv1  FFN Conv1d k=1 1024->256 + res + LN + mask   2*F*1024*256     MFMA
+      fc     attention out proj + res + LN + mask          2*F*256*256     MFMA
+      qkv    fused Q|K|V projection   F*256*2 in + F*768*2 out + W bytes    HBM
+      attn   SDPA, 2 heads of 128     sum_b 4*len_b^2*128*2 FLOP          MFMA
+      lr     LengthRegulator gather + decoder PE   B*L*256*2 + B*L*8 in + F*256*2 out  HBM
+    (F = valid frames). bf16 only (the fp8 / fp32 lines report the conv-k9 roofline alone)."""
+    from fs2amd import _lib as L
+    from fs2amd import ops
+    from fs2amd.data import to_device
+
+    P = model.packed(device)
+    b = to_device(batch_cpu, device)
+    lp = P.dec_layers[0]
+    B, T = b["d_targets"].shape[0], int(batch_cpu["max_mel_len"])
+    lens = batch_cpu["mel_lens"].long()
+    F = int(lens.sum())
+    Lp = int(batch_cpu["texts"].shape[1])
+    dt = ops.torch_dtype(P.act_dtype)
+    g = torch.Generator().manual_seed(0)
+    rnd = lambda *s: torch.randn(*s, generator=g).to(device, dt)
+    lay = ops.SeqLayout(b["mel_lens"], T)
+    h, o, f, qkv = rnd(B * T, 256), rnd(B * T, 256), rnd(B * T, 1024), rnd(B * T, 768)
+    x = rnd(B, Lp, 256)
+    cum, ml, _ = ops.lr_durations(b["d_targets"])
+    ops_ = {
+        "conv9": (lambda: ops.conv1d(h, lp.w1, lp.b1, cin=256, ks=9, pad=4, compute=P.compute,
+                                     epilogue=L.EPI_BIAS_RELU, out_dtype=P.act_dtype, layout=lay),
+                  "mfma", 2.0 * F * 256 * 9 * 1024),
+        "conv1_ln": (lambda: ops.conv1d(f, lp.w2, lp.b2, cin=1024, ks=1, pad=0, compute=P.compute,
+                                        epilogue=L.EPI_RES_LN, out_dtype=P.act_dtype, residual=h, ln=lp.ln2,
+                                        layout=lay),
+                     "mfma", 2.0 * F * 1024 * 256),
+        "fc_ln": (lambda: ops.conv1d(o, lp.wfc, lp.bfc, cin=256, ks=1, pad=0, compute=P.compute,
+                                     epilogue=L.EPI_RES_LN, out_dtype=P.act_dtype, residual=h, ln=lp.ln1, layout=lay),
+                  "mfma", 2.0 * F * 256 * 256),
+        "qkv": (lambda: ops.conv1d(h, lp.wqkv, lp.bqkv, cin=256, ks=1, pad=0, compute=P.compute,
+                                   epilogue=L.EPI_BIAS, out_dtype=P.act_dtype, layout=lay),
+                "hbm", F * 256 * 2.0 + F * 768 * 2.0 + 768 * 256 * 2.0),
+        "attn": (lambda: ops.attention(qkv, None, 2, 128, 128 ** 0.5, layout=lay),
+                 "mfma", float(sum(4.0 * int(n) ** 2 * 128 * 2 for n in lens))),
+        "lr": (lambda: ops.lr_expand(x, cum, ml, T, pe=P.dec_pe, out_dtype=P.act_dtype, out_layout=lay),
+               "hbm", B * Lp * 256 * 2.0 + B * Lp * 8.0 + F * 256 * 2.0),
+    }
+    out = {}
+    for name, (fn, bound, work) in ops_.items():
+        t = _graph_mean_s(fn, device, reps)
+        if bound == "mfma":
+            ach, peak, unit, wk = work / t / 1e12, BF16_PEAK_TFLOPS, "TFLOP/s", {"flops_per_call": work}
+        else:
+            ach, peak, unit, wk = work / t / 1e9, HBM_PEAK_GBS, "GB/s", {"bytes_per_call": work}
+        out[name] = {"us": round(t * 1e6, 2), "bound": bound, "achieved": round(ach, 1), "peak": peak, "unit": unit,
+                     "frac": round(ach / peak, 4), **wk}
+    return out
 
 
 def cpu_baseline(batch_cpu, pc, mc, budget_s=20.0):
@@ -438,8 +529,22 @@ def main():
     elapsed, tot_frames = parallel.aggregate(elapsed, frames, device)
     extra = extra_workloads(model, args, rank, device) if args.extra else {}
 
-    kernel_s, n_launch = time_kernel_in_forward(model, batch)
+    eager_s, n_launch = time_kernel_in_forward(model, batch)
     standalone_s, kernel_flops = time_dominant_kernel(model, batch_cpu, device, args.kernel_reps)
+    table = None
+    if args.dtype == "bf16":
+        try:  # diagnostics only: never lose the headline line to them
+            table = decoder_op_table(model, batch_cpu, device, args.kernel_reps)
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: decoder op table failed: {e!r}", file=sys.stderr, flush=True)
+    if table is not None:
+        # the op as the graph-replayed forward runs it: launches back to back, no host gap
+        kernel_s = table["conv9"]["us"] / 1e6
+        timing = (f"HIP events on the launch stream around {args.kernel_reps} back-to-back calls of the op captured "
+                  "in one HIP graph (as the graph-replayed forward issues it), packed cfg2 frames")
+    else:
+        kernel_s = eager_s
+        timing = "HIP events around each decoder conv-k9 launch in 3 eager forwards"
     ms_per_step = elapsed / args.steps * 1e3
     value = tot_frames * args.steps / elapsed
     peak = {"bf16": BF16_PEAK_TFLOPS, "fp8": FP8_PEAK_TFLOPS}.get(args.dtype, F32_PEAK_TFLOPS)
@@ -470,12 +575,14 @@ def main():
                                   if args.dtype == "bf16" else "conv_gemm_kernel"),
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": load_traffic(args.dtype),
-                     "kernel_ms": round(kernel_s * 1e3, 4), "launches_timed": n_launch,
-                     "timing": "HIP events around each decoder conv-k9 launch in 3 eager forwards",
+                     "kernel_ms": round(kernel_s * 1e3, 4), "timing": timing,
+                     "kernel_ms_in_eager_forward": round(eager_s * 1e3, 4), "launches_timed_eager": n_launch,
                      "kernel_ms_standalone_random": round(standalone_s * 1e3, 4),
                      "flops_per_launch": kernel_flops,
                      "traffic_note": "2*FETCH_SIZE + WRITE_SIZE per launch (rocprofv3 PMC, profiles/conv9_traffic.json)"},
     }
+    if table is not None:
+        rec["decoder_ops"] = table
     if rank == 0 and world == 1 and args.cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(batch_cpu, pc, mc)
     if extra:
