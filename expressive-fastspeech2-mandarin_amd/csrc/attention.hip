@@ -248,9 +248,14 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const typename ATraits<CT>
 // K and V tiles arrive by LDS-DMA (buffer_load ... lds, OOB rows -> zeros) into a dual-use XOR
 // image (row reads and transposed reads conflict-light), double buffered. Workgroups of one
 // (utterance, head) are placed on one XCD so its K/V stay in that XCD's L2.
-__device__ __forceinline__ int kv_off(int row, int chunk) {
-  return row * 256 + ((chunk ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
-}
+// 16-byte chunk swizzle of K / V row `row` (256 B rows = all 64 banks). The K fragment reads take
+// one chunk of 16 consecutive rows: f must be a bijection on rows 16i..16i+15. The transposed V
+// reads (ds_read_b64_tr_b16) take, per 32 lanes, one 32-byte chunk PAIR {2m, 2m+1} of 8 consecutive
+// rows: f >> 1 must be a bijection on rows 8i..8i+7. f = ((row & 7) << 1) | ((row >> 3) & 1) meets
+// both; the round-1 f = ((row & 3) << 2) | ((row >> 2) & 3) gave rows r and r+4 the same pair
+// (2-way conflicts on every V read: 2.7 M conflict cycles per decoder attention call, rocprofv3).
+__device__ __forceinline__ int kv_swz(int row) { return ((row & 7) << 1) | ((row >> 3) & 1); }
+__device__ __forceinline__ int kv_off(int row, int chunk) { return row * 256 + ((chunk ^ kv_swz(row)) << 4); }
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
@@ -320,7 +325,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
     for (int it = 0; it < PPW; ++it) {
       const int p = w + NWV * it;
       const int r = 4 * p + prow;
-      const int lc = pch ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      const int lc = pch ^ kv_swz(r);
       const int key = k0 + r;
       const uint32_t base = key < T ? (seq_base + key) * row_bytes + (uint32_t)lc * 16u : 0x80000000u;
       const uint32_t koff = base == 0x80000000u ? base : base + (uint32_t)((H + h) * DK) * 2u;
@@ -344,7 +349,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
   for (int st = 0; st < NST - 1; ++st)
     if (st < ntiles) dma(st * KTT, st);
   // transposed-read lane roles: lane 4q+p of its 16-lane group addresses row q, columns 4p..4p+3.
-  // kv_off's swizzle depends on (row & 3, (row >> 2) & 3), so rows +16 / +32 are +4 / +8 KiB:
+  // kv_off's swizzle depends on row & 15 only, so rows +16 / +32 are +4 / +8 KiB:
   // only the 8 column-block offsets of row r0 are lane-specific (hoisted out of the key loop).
   const int tq = li >> 2, tp = li & 3;
   int voff[DK / 16];
@@ -515,7 +520,7 @@ __global__ __launch_bounds__(64 * NWV, 4) void attn_bf16_sp_kernel(const bf16 *_
     for (int it = 0; it < PPW; ++it) {
       const int p = w + NWV * it;
       const int r = 4 * p + prow;
-      const int lc = pch ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      const int lc = pch ^ kv_swz(r);
       const int key = k0 + r;
       const uint32_t off = key < T ? (seq_base + key) * row_bytes + (uint32_t)lc * 16u +
                                          (uint32_t)((part * H + h) * DK) * 2u
@@ -713,7 +718,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_q32_kernel(const bf16 *
     for (int it = 0; it < PPW; ++it) {
       const int p = w + NWV * it;
       const int r = 4 * p + prow;
-      const int lc = pch ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      const int lc = pch ^ kv_swz(r);
       const int key = k0 + r;
       const uint32_t base = key < T ? (seq_base + key) * row_bytes + (uint32_t)lc * 16u : 0x80000000u;
       const uint32_t koff = base == 0x80000000u ? base : base + (uint32_t)((H + h) * DK) * 2u;
