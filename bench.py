@@ -539,7 +539,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             print(f"bench: decoder op table failed: {e!r}", file=sys.stderr, flush=True)
     # the op inside real forwards (interleaved with the block's lighter launches, as in the bench);
-    # 20 back-to-back calls (decoder_ops.conv9) run ~10 % slower: sustained MFMA load lowers clocks
+    # 20 back-to-back calls (decoder_ops.conv9) run ~10-13 % slower (likely clocks under sustained MFMA load)
     kernel_s = eager_s
     timing = "HIP events around each decoder conv-k9 op call (both launches) in 3 eager forwards"
     ms_per_step = elapsed / args.steps * 1e3
