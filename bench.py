@@ -12,10 +12,11 @@ region is bracketed by a barrier + device sync on both sides; the max over ranks
 job time; value = all valid mel frames of all ranks / job time.
 
 Also reported:
-* roofline — the dominant kernel (the FFN Conv1d k=9 implicit GEMM of the decoder, ~76 % of
-  the FLOPs) timed with HIP events on the stream it launches on; achieved = algorithmic FLOPs
-  of one op call (valid frames x 2*256*9*1024) / its mean duration inside real forwards, vs
-  2.5 PF dense bf16.
+* roofline — the dominant kernel: the decoder's fused FFN (fs2_ffn: Conv1d k=9 + ReLU + Conv1d
+  k=1 + residual + LayerNorm, ~86 % of the FLOPs; the conv-k9 launch pair when the fused kernel
+  is off or in fp32 / fp8) timed with HIP events on the stream it launches on; achieved =
+  algorithmic FLOPs of one op call (valid frames x (2*256*9*1024 + 2*1024*256), or x 2*256*9*1024
+  for the conv-k9 alone) / its mean duration inside real forwards, vs the dense MFMA peak.
   ``traffic`` comes from the committed rocprofv3 PMC pass (profiles/) when present.
 * decoder_ops — every op of one decoder FFT block (+ the LengthRegulator gather) at the same
   shape, graph-timed, each with its algorithmic work and roofline fraction (bf16 line).
@@ -28,6 +29,7 @@ import os
 import sys
 import tempfile
 import time
+from types import SimpleNamespace
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "expressive-fastspeech2-mandarin_amd"))
@@ -129,8 +131,21 @@ def time_kernel_in_forward(model, batch, n_fwd=3):
     return sum(ts) / len(ts), len(ts)
 
 
+def ffn_fused(model, batch, device):
+    """Does the benched forward run the decoder FFN as the fused fs2_ffn launch?"""
+    from fs2amd import ops, runtime
+
+    P = model.packed(device)
+    lp = P.dec_layers[0]
+    B, T = batch["d_targets"].shape[0], int(batch["max_mel_len"])
+    lay = SimpleNamespace(capacity=B * T) if runtime.packed_decoder_ok(P) else None
+    probe = torch.empty(B, T, 0, dtype=ops.torch_dtype(P.act_dtype))
+    return lp.fp8 is None and runtime.ffn_fused_ok(P, lp, probe, lay)
+
+
 def time_dominant_kernel(model, batch, device, reps):
-    """Mean duration of the decoder FFN conv-k9 GEMM run standalone on random data."""
+    """Mean duration of the decoder's dominant op (fused FFN, or the FFN conv-k9) run standalone on
+    random data; returns (seconds, algorithmic FLOPs per call)."""
     from fs2amd import _lib as L
     from fs2amd import ops
 
@@ -149,6 +164,10 @@ def time_dominant_kernel(model, batch, device, reps):
         run = lambda: ops.conv1d(h, lp.fp8.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=L.FS2_FP8,
                                  epilogue=L.EPI_BIAS_RELU, out=out, out_dtype=L.FS2_FP8, out_scale=1.0 / lp.fp8.s_f,
                                  col_scale=lp.fp8.cs1, layout=lay)
+    elif ffn_fused(model, batch, device):
+        h = torch.randn(*shape, lp.c1, generator=g).to(device=device, dtype=ops.torch_dtype(P.act_dtype))
+        out = torch.empty_like(h)
+        run = lambda: ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, layout=lay, out=out)
     else:
         h = torch.randn(*shape, lp.c1, generator=g).to(device=device, dtype=ops.torch_dtype(P.act_dtype))
         out = torch.empty(*shape, lp.w1.shape[0], device=device, dtype=h.dtype)
@@ -166,6 +185,8 @@ def time_dominant_kernel(model, batch, device, reps):
     mean_s = e0.elapsed_time(e1) / 1e3 / reps
     valid = int(batch["mel_lens"].sum())
     flops = 2.0 * valid * lp.c1 * lp.k1 * lp.w1.shape[0]
+    if lp.fp8 is None and ffn_fused(model, batch, device):
+        flops += 2.0 * valid * lp.c2 * lp.w2.shape[0]
     return mean_s, flops
 
 
@@ -200,6 +221,7 @@ def decoder_op_table(model, batch_cpu, device, reps):
     """Every decoder op of one FFT block at the benched cfg2 shape (packed valid frames, as the
     forward runs them), each timed as `reps` back-to-back launches in one HIP graph, with its
     algorithmic work per call and the roofline that bounds it:
+      ffn    fused FFN (fs2_ffn): conv9 + ReLU + conv1 + res + LN   2*F*(256*9*1024 + 1024*256)  MFMA
       conv9  FFN Conv1d k=9 256->1024 + ReLU   2*F*256*9*1024 FLOP        MFMA
       conv1  FFN Conv1d k=1 1024->256 + res + LN + mask   2*F*1024*256     MFMA
       fc     attention out proj + res + LN + mask          2*F*256*256     MFMA
@@ -228,6 +250,8 @@ def decoder_op_table(model, batch_cpu, device, reps):
     x = rnd(B, Lp, 256)
     cum, ml, _ = ops.lr_durations(b["d_targets"])
     ops_ = {
+        "ffn": (lambda: ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=9, pad=4, ln=lp.ln2, layout=lay),
+                "mfma", 2.0 * F * (256 * 9 * 1024 + 1024 * 256)),
         "conv9": (lambda: ops.conv1d(h, lp.w1, lp.b1, cin=256, ks=9, pad=4, compute=P.compute,
                                      epilogue=L.EPI_BIAS_RELU, out_dtype=P.act_dtype, layout=lay),
                   "mfma", 2.0 * F * 256 * 9 * 1024),
@@ -286,8 +310,9 @@ def cpu_baseline(batch_cpu, pc, mc, budget_s=20.0):
                       f"reps after 1 warm-up, {dt:.1f} s, torch.set_num_threads({threads})"}
 
 
-def load_traffic(dtype="bf16"):
-    path = os.path.join(REPO, "profiles", "conv9_traffic.json" if dtype == "bf16" else f"conv9_{dtype}_traffic.json")
+def load_traffic(dtype="bf16", fused=False):
+    name = "ffn_traffic.json" if fused else ("conv9_traffic.json" if dtype == "bf16" else f"conv9_{dtype}_traffic.json")
+    path = os.path.join(REPO, "profiles", name)
     if os.path.exists(path):
         with open(path) as f:
             return json.load(f).get("hbm_bytes_per_launch")
@@ -539,9 +564,11 @@ def main():
         except Exception as e:  # noqa: BLE001
             print(f"bench: decoder op table failed: {e!r}", file=sys.stderr, flush=True)
     # the op inside real forwards (interleaved with the block's lighter launches, as in the bench);
-    # 20 back-to-back calls (decoder_ops.conv9) run ~10-13 % slower (likely clocks under sustained MFMA load)
+    # back-to-back calls (decoder_ops) run slower (likely clocks under sustained MFMA load)
     kernel_s = eager_s
-    timing = "HIP events around each decoder conv-k9 op call (both launches) in 3 eager forwards"
+    fused = ffn_fused(model, batch_cpu, device)
+    timing = ("HIP events around each decoder fused-FFN launch in 3 eager forwards" if fused else
+              "HIP events around each decoder conv-k9 op call (both launches) in 3 eager forwards")
     ms_per_step = elapsed / args.steps * 1e3
     value = tot_frames * args.steps / elapsed
     peak = {"bf16": BF16_PEAK_TFLOPS, "fp8": FP8_PEAK_TFLOPS}.get(args.dtype, F32_PEAK_TFLOPS)
@@ -567,16 +594,20 @@ def main():
                    "parallelism": f"dp{world} (independent shards, no collective)",
                    "hip_graph": bool(args.graph)},
         "rtf": round((elapsed / args.steps) / (tot_frames / world * HOP / SR), 7),
-        "roofline": {"bound": "mfma", "kernel": f"decoder FFN Conv1d k=9, 256->1024 ({args.dtype}): "
-                               + ("conv_gemm_8p_kernel whole rounds + conv_gemm_kernel rows left"
-                                  if args.dtype == "bf16" else "conv_gemm_kernel"),
+        "roofline": {"bound": "mfma", "kernel": ("decoder FFN fused (bf16): ffn_fused_kernel = Conv1d k=9 256->1024 + "
+                                                 "ReLU + Conv1d k=1 1024->256 + residual + LayerNorm, one launch"
+                                                 if fused else
+                                                 f"decoder FFN Conv1d k=9, 256->1024 ({args.dtype}): "
+                                                 + ("conv_gemm_8p_kernel whole rounds + conv_gemm_kernel rows left"
+                                                    if args.dtype == "bf16" else "conv_gemm_kernel")),
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": load_traffic(args.dtype),
+                     "frac": round(achieved / peak, 4), "traffic": load_traffic(args.dtype, fused),
                      "kernel_ms": round(kernel_s * 1e3, 4), "timing": timing,
                      "op_calls_timed": n_launch,
                      "kernel_ms_standalone_random": round(standalone_s * 1e3, 4),
                      "flops_per_launch": kernel_flops,
-                     "traffic_note": "2*FETCH_SIZE + WRITE_SIZE per launch (rocprofv3 PMC, profiles/conv9_traffic.json)"},
+                     "traffic_note": "2*FETCH_SIZE + WRITE_SIZE per launch (rocprofv3 PMC, profiles/"
+                                     + ("ffn_traffic.json)" if fused else "conv9_traffic.json)")},
     }
     if table is not None:
         rec["decoder_ops"] = table

@@ -50,12 +50,28 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class FfnDesc(ctypes.Structure):
+    """Mirror of ``fs2_ffn_desc`` (include/fs2hip.h)."""
+
+    _fields_ = [
+        ("x", _p), ("x_row_stride", _i64),
+        ("w", _p), ("b1", _p), ("b2", _p),
+        ("B", _i), ("T", _i), ("D", _i), ("F", _i), ("KS", _i), ("pad", _i),
+        ("ln_gamma", _p), ("ln_beta", _p), ("ln_eps", _f),
+        ("lens", _p), ("addvec1", _p), ("addvec2", _p),
+        ("out", _p), ("out_row_stride", _i64),
+        ("rows_dev", _p), ("row_pos", _p),
+    ]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "fs2_version": (ctypes.c_char_p, []),
     "fs2_status_string": (ctypes.c_char_p, [_i]),
     "fs2_conv_cin_pad": (_i, [_i, _i]),
     "fs2_conv1d": (_i, [ctypes.POINTER(ConvDesc), _p]),
+    "fs2_ffn": (_i, [ctypes.POINTER(FfnDesc), _p]),
+    "fs2_ffn_pitch": (_i, [_i, _i]),
     "fs2_attention": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p]),
     "fs2_embed_pe": (_i, [_p, _p, _i, _p, _i, _i, _i, _p, _i, _p, _p]),
     "fs2_attention_bwd": (_i, [_p, _i, _i64, _p, _i64, _p, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p, _i64, _p]),

@@ -277,6 +277,55 @@ def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None
     return out
 
 
+def pack_ffn_weights(w1, w2):
+    """PositionwiseFeedForward weights -> the fs2_ffn buffer: bf16 rows of pitch max(KS*D, F): the F
+    rows of w_1 (nn.Conv1d weight [F, D, KS], each row as [KS][D]) then the D rows of w_2 ([D, F, 1])."""
+    F, D, ks = w1.shape
+    assert w2.shape[:2] == (D, F) and (w2.dim() == 2 or w2.shape[2] == 1), (tuple(w1.shape), tuple(w2.shape))
+    pitch = _lib.fs2_ffn_pitch(ks, F)
+    out = torch.zeros(F + D, pitch, dtype=torch.bfloat16, device=w1.device)
+    out[:F, :ks * D] = w1.detach().float().permute(0, 2, 1).reshape(F, ks * D).to(torch.bfloat16)
+    out[F:, :F] = w2.detach().float().reshape(D, F).to(torch.bfloat16)
+    return out
+
+
+def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=None, layout=None, out=None):
+    """PositionwiseFeedForward + residual + LayerNorm + mask in one launch (fs2_ffn): bf16 rows of
+    256 (padded [B, T, 256] or packed [B*T, 256] in ``layout``); ``w_packed`` from
+    :func:`pack_ffn_weights`. The hidden [rows, F] never reaches HBM."""
+    _gpu(x, w_packed, b1, b2, lens, addvec1, addvec2)
+    if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
+        raise TypeError("fs2amd.ffn: bf16 activations and weights only")
+    if layout is not None:
+        B, T = layout.B, layout.T
+        assert x.dim() == 2 and x.shape[0] == layout.capacity, (tuple(x.shape), layout.capacity)
+    else:
+        B, T, _ = x.shape
+    D = x.shape[-1]
+    F = b1.numel()
+    assert w_packed.is_contiguous() and w_packed.shape == (F + D, _lib.fs2_ffn_pitch(ks, F)), tuple(w_packed.shape)
+    d = L.FfnDesc()
+    d.x, d.x_row_stride = x.data_ptr(), _rows(x, "x")
+    d.w, d.b1, d.b2 = w_packed.data_ptr(), b1.data_ptr(), b2.data_ptr()
+    d.B, d.T, d.D, d.F, d.KS, d.pad = B, T, D, F, ks, pad
+    g, b, eps = ln
+    d.ln_gamma, d.ln_beta, d.ln_eps = g.data_ptr(), b.data_ptr(), float(eps)
+    if lens is not None:
+        assert lens.dtype == torch.int64 and lens.numel() == B
+        d.lens = lens.data_ptr()
+    if addvec1 is not None:
+        d.addvec1 = addvec1.data_ptr()
+    if addvec2 is not None:
+        d.addvec2 = addvec2.data_ptr()
+    if layout is not None:
+        d.rows_dev, d.row_pos = layout.rows_dev, layout.row_pos.data_ptr()
+    if out is None:
+        out = torch.empty_like(x)
+    d.out, d.out_row_stride = out.data_ptr(), _rows(out, "out")
+    L.check(_lib.fs2_ffn(ctypes.byref(d), _stream(x)), "fs2_ffn")
+    return out
+
+
 def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None):
     """Key-padding-masked multi-head self-attention over a fused [B, T, 3*H*dk] projection
     (or packed [B*T, 3*H*dk] rows of a SeqLayout: lens unused)."""

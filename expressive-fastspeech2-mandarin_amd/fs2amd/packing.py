@@ -20,7 +20,7 @@ from types import SimpleNamespace
 import torch
 
 from . import _lib as L
-from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split
+from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split, pack_ffn_weights
 
 
 def _f32(t, device):
@@ -53,7 +53,16 @@ def _fft_layer(layer, device, compute, key=None, fp8_scales=None):
         w2=pack_conv_weight(f.w_2.weight.to(device), compute), b2=_f32(f.w_2.bias, device),
         k2=f.w_2.kernel_size[0], p2=f.w_2.padding[0], c2=f.w_2.in_channels,
         ln2=(_f32(f.layer_norm.weight, device), _f32(f.layer_norm.bias, device), f.layer_norm.eps),
+        w12=_ffn_pair(f, device, compute),
     )
+
+
+def _ffn_pair(f, device, compute):
+    """w_1 | w_2 in the fs2_ffn layout (bf16 FFNs of the shapes the fused kernel covers), else None."""
+    ks, F, D = f.w_1.kernel_size[0], f.w_1.out_channels, f.w_1.in_channels
+    if compute != L.FS2_BF16 or D != 256 or F not in (512, 1024) or ks not in (3, 9) or f.w_2.kernel_size[0] != 1:
+        return None
+    return pack_ffn_weights(f.w_1.weight.to(device), f.w_2.weight.to(device))
 
 
 def _vp(vp, device, compute, split=False):

@@ -116,6 +116,15 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
     if timed and TIMERS is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
+    if ffn_fused_ok(P, lp, h, layout) and CALIB is None:
+        # the whole FFN (conv-k9 + ReLU + conv-k1 + residual + LN + mask) as one launch: the
+        # [rows, 1024] hidden stays on chip
+        y = ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, lens=lens, addvec1=addvec1,
+                    addvec2=addvec2, layout=layout)
+        if timed and TIMERS is not None:
+            e1.record()
+            TIMERS.append((e0, e1))
+        return y, None
     f = ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=c, epilogue=L.EPI_BIAS_RELU, out_dtype=dt,
                    layout=layout)
     if timed and TIMERS is not None:
@@ -128,6 +137,21 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
         CALIB[lp.key]["f"] = float(fv.float().abs().max()) if fv.numel() else 0.0
     return ops.conv1d(f, lp.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
                       residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2, layout=layout), None
+
+
+FFN_FUSED_MIN_ROWS = 16384
+
+
+def ffn_fused_ok(P, lp, h, layout):
+    """fs2_ffn covers bf16 FFNs with d_model 256, kernel-1 w_2 and a hidden width of whole 256-column
+    chunks; it pays where the launch has enough 112-row tiles to fill the chip (the decoder: cfg2
+    24.9k packed rows; the 4k-row encoder keeps the two fs2_conv1d launches). FS2_FFN_FUSED=0: off
+    (A/B), =2: on at every size (tests)."""
+    mode = os.environ.get("FS2_FFN_FUSED", "0")
+    if mode == "0" or P.compute != L.FS2_BF16 or h.dtype != torch.bfloat16 or getattr(lp, "w12", None) is None:
+        return False
+    rows = layout.capacity if layout is not None else h.shape[0] * h.shape[1]
+    return mode == "2" or rows >= FFN_FUSED_MIN_ROWS
 
 
 def _stack(P, layers, x, lens, layout=None, timed=False, addvecs=(None, None)):

@@ -153,6 +153,47 @@ int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream);
 int fs2_conv_cin_pad(int Cin, int compute);
 
 /*
+ * fs2_ffn — PositionwiseFeedForward + residual + LayerNorm + padding mask as ONE launch
+ * (transformer/SubLayers.py:85-93 w_1 -> ReLU -> w_2 -> dropout(eval) -> LayerNorm(out + residual),
+ * then the FFTBlock's masked_fill, transformer/Layers.py:28; speaker/emotion adds as FS2_EPI_RES_LN):
+ *
+ *   f[m, :] = relu( sum_{k<KS} sum_c x[m + k - pad, c] * w1[j][k][c] + b1[j] )   (per-sequence zero taps)
+ *   y[m, :] = LN( f[m, :] . w2^T + b2 + x[m, :] ); rows t >= lens[b] -> 0; y += addvec1[b] (+ addvec2[b])
+ *
+ * The 1024-wide hidden f never reaches HBM: a workgroup keeps a 112-row tile's f in LDS, one
+ * 256-column chunk at a time, and accumulates w_2's product in registers (two fs2_conv1d launches
+ * write and re-read it: 51 MB each way per cfg2 decoder block).
+ * bf16 only. x / out: bf16 rows of D = 256 (out must not alias x). w: the FFN's two weight
+ * matrices in one bf16 buffer, every row fs2_ffn_pitch(KS, F) = max(KS*D, F) elements long: F rows
+ * of w_1 (row j = w_1.weight[j, :, :] transposed to [KS][D]) followed by D rows of w_2 (row n =
+ * w_2.weight[n, :, 0], F elements). Shapes: D = 256, F in {512, 1024}, KS in {3, 9}, pad <= KS - 1
+ * (FS2_EUNSUPPORTED otherwise: the caller runs the two fs2_conv1d launches). Packed rows (rows_dev / row_pos, fs2_seq_layout) or padded [B, T] rows (lens /
+ * addvec allowed) as in fs2_conv1d. Deterministic; each output row depends only on its own input
+ * rows, so packed and padded launches agree bit for bit.
+ */
+typedef struct fs2_ffn_desc {
+  const void *x;            /* bf16 [B*T, >= D]: the FFN input and the LayerNorm residual        */
+  int64_t x_row_stride;
+  const void *w;            /* packed bf16 w_1 | w_2 rows, pitch fs2_ffn_pitch(KS, F) (see above)  */
+  const float *b1;          /* [F]                                                               */
+  const float *b2;          /* [D]                                                               */
+  int B, T, D, F, KS, pad;
+  const float *ln_gamma;    /* [D]                                                               */
+  const float *ln_beta;
+  float ln_eps;
+  const int64_t *lens;      /* [B] or NULL (padded rows only)                                    */
+  const float *addvec1;     /* [B, D] or NULL (padded rows only)                                 */
+  const float *addvec2;
+  void *out;                /* bf16 [B*T, >= D]                                                  */
+  int64_t out_row_stride;
+  const int32_t *rows_dev;  /* packed rows (fs2_seq_layout cu + B) or NULL                       */
+  const int32_t *row_pos;   /* packed rows: int32 [rows][2] = {frame, sequence length}           */
+} fs2_ffn_desc;
+
+int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream);
+int fs2_ffn_pitch(int KS, int F);
+
+/*
  * fs2_attention — ScaledDotProductAttention with a key-padding mask, all heads.
  * Replaces transformer/Modules.py:14-25 (bmm, /temperature, masked_fill(-inf), softmax(dim=2),
  * bmm) and the head split/merge permutes of SubLayers.py:42-52.

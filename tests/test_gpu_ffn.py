@@ -1,0 +1,148 @@
+"""fs2_ffn — the fused PositionwiseFeedForward (conv-k9 + ReLU + conv-k1 + residual + LayerNorm +
+mask in one launch, transformer/SubLayers.py:85-93 + Layers.py:28).
+
+* against a float64 PyTorch statement of the same op on the same bf16 operands (the hidden f is
+  rounded to bf16 exactly where the two-launch path stores it), bf16 tolerance;
+* against the two fs2_conv1d launches it replaces (same bf16 rounding points; only the f32
+  summation order of the k=9 product differs);
+* packed rows (SeqLayout) bit-identical to padded rows: each output row depends only on its own
+  input rows and the per-row k order, not on where the 112-row tile boundaries fall;
+* ragged lengths 0 / 1 / < the 4-row tap reach / exact tile multiples, row counts that are not
+  multiples of 112, a padded launch with speaker / emotion vectors.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from fs2amd import ops, _lib as L
+
+    return ops, L
+
+
+def _weights(ops, L, F=1024, ks=9, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    w1 = torch.randn(F, 256, ks, device=DEV, generator=g) / (256 * ks) ** 0.5
+    w2 = torch.randn(256, F, 1, device=DEV, generator=g) / F ** 0.5
+    b1 = 0.1 * torch.randn(F, device=DEV, generator=g)
+    b2 = 0.1 * torch.randn(256, device=DEV, generator=g)
+    ln = (1 + 0.1 * torch.randn(256, device=DEV, generator=g), 0.1 * torch.randn(256, device=DEV, generator=g), 1e-5)
+    return dict(w1=w1, w2=w2, b1=b1, b2=b2, ln=ln, p1=ops.pack_conv_weight(w1, L.FS2_BF16),
+                p2=ops.pack_conv_weight(w2, L.FS2_BF16), w12=ops.pack_ffn_weights(w1, w2), ks=ks)
+
+
+def _ref(x, lens, W, addvecs=()):
+    """float64 statement: per-sequence conv (zero taps outside [0, T)), f rounded to bf16 like the
+    stored hidden, LN(f w2^T + b2 + x), rows t >= len -> 0, + addvecs."""
+    ks = W["ks"]
+    xd = x.double()
+    w1 = W["w1"].to(torch.bfloat16).double()
+    w2 = W["w2"].to(torch.bfloat16).double()[:, :, 0]
+    f = torch.nn.functional.conv1d(xd.transpose(1, 2), w1, W["b1"].double(), padding=(ks - 1) // 2).transpose(1, 2)
+    f = torch.relu(f).to(torch.bfloat16).double()
+    y = f @ w2.t() + W["b2"].double() + xd
+    g, b, eps = W["ln"]
+    y = torch.nn.functional.layer_norm(y, (256,), g.double(), b.double(), eps)
+    T = x.shape[1]
+    if lens is not None:
+        y = y * (torch.arange(T, device=DEV)[None, :, None] < lens[:, None, None])
+    for v in addvecs:
+        y = y + v.double()[:, None, :]
+    return y
+
+
+def _x(B, T, lens, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    valid = (torch.arange(T, device=DEV)[None, :] < lens[:, None])[..., None]
+    return (torch.randn(B, T, 256, device=DEV, generator=g) * valid).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("B,T,seed", [(8, 130, 1), (3, 37, 2), (40, 300, 3)])
+def test_ffn_matches_float64(gpu, B, T, seed):
+    ops, L = gpu
+    W = _weights(ops, L, seed=seed)
+    rng = np.random.default_rng(seed)
+    lens_l = rng.integers(0, T + 1, B).tolist()
+    lens_l[0] = T
+    if B > 2:
+        lens_l[1], lens_l[2] = 1, 3  # shorter than the taps' reach on both sides
+    lens = torch.tensor(lens_l, dtype=torch.int64, device=DEV)
+    x = _x(B, T, lens, seed)
+    got = ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], lens=lens)
+    ref = _ref(x, lens, W)
+    err = (got.double() - ref).abs()
+    # bf16 output rounding (|y| <~ 4: 1.6e-2) plus rare 1-ulp flips of a bf16 hidden value
+    assert float(err.max()) <= 3e-2, float(err.max())
+    assert float(err.mean()) <= 2e-3, float(err.mean())
+
+
+def test_ffn_matches_two_launch_path(gpu):
+    ops, L = gpu
+    B, T = 64, 430
+    W = _weights(ops, L, seed=7)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    lens = torch.randint(200, T + 1, (B,), generator=g).to(DEV)
+    x = _x(B, T, lens, 7)
+    fused = ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], lens=lens)
+    kw = dict(compute=L.FS2_BF16, out_dtype=L.FS2_BF16)
+    f = ops.conv1d(x, W["p1"], W["b1"], cin=256, ks=9, pad=4, epilogue=L.EPI_BIAS_RELU, **kw)
+    two = ops.conv1d(f, W["p2"], W["b2"], cin=1024, ks=1, pad=0, epilogue=L.EPI_RES_LN, residual=x, ln=W["ln"],
+                     lens=lens, **kw)
+    d = (fused.float() - two.float()).abs()
+    assert float(d.max()) <= 3e-2 and float(d.mean()) <= 1e-3, (float(d.max()), float(d.mean()))
+
+
+@pytest.mark.parametrize("lens_l,T", [([37, 0, 130, 1, 64, 129, 130, 5], 130),
+                                      ([430] * 3 + [2, 3, 4, 111, 112, 113, 224, 225], 430)])
+def test_ffn_packed_equals_padded(gpu, lens_l, T):
+    ops, L = gpu
+    W = _weights(ops, L, seed=11)
+    lens = torch.tensor(lens_l, dtype=torch.int64, device=DEV)
+    B = len(lens_l)
+    x = _x(B, T, lens, 11)
+    lay = ops.SeqLayout(lens, T)
+    rm = lay.rowmap.long()
+    ok = rm >= 0
+    xp = x.new_zeros(lay.capacity, 256)
+    xp[rm[ok]] = x.reshape(-1, 256)[ok]
+    ref = ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], lens=lens)
+    got = ops.ffn(xp, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay)
+    torch.cuda.synchronize()
+    R = int(lay.cu[-1])
+    assert torch.equal(got[:R], ref.reshape(-1, 256)[ok])
+    assert not torch.isnan(got[:R].float()).any()
+
+
+def test_ffn_addvecs_and_narrow_hidden(gpu):
+    """Padded rows with the speaker / emotion adds of the last encoder block, F = 512 (two chunks)
+    and a k=3 first conv."""
+    ops, L = gpu
+    B, T = 5, 61
+    W = _weights(ops, L, F=512, ks=3, seed=13)
+    lens = torch.tensor([61, 17, 0, 2, 40], dtype=torch.int64, device=DEV)
+    x = _x(B, T, lens, 13)
+    g = torch.Generator(device=DEV).manual_seed(14)
+    a1, a2 = torch.randn(B, 256, device=DEV, generator=g), torch.randn(B, 256, device=DEV, generator=g)
+    got = ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=3, pad=1, ln=W["ln"], lens=lens, addvec1=a1, addvec2=a2)
+    ref = _ref(x, lens, W, (a1, a2))
+    err = (got.double() - ref).abs()
+    assert float(err.max()) <= 5e-2 and float(err.mean()) <= 3e-3, (float(err.max()), float(err.mean()))
+
+
+def test_ffn_rejects_bad_shapes(gpu):
+    ops, L = gpu
+    W = _weights(ops, L, seed=1)
+    x = torch.zeros(2, 8, 256, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):  # out aliasing x: other tiles re-read x rows
+        ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], out=x)
+    with pytest.raises(TypeError):
+        ops.ffn(x.float(), W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"])
+    with pytest.raises(AssertionError):  # w_1 | w_2 buffer of another shape
+        ops.ffn(x, W["w12"][:-1], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"])

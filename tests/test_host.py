@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
     lib = _lib.load()
     declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
-    assert len(declared) == len(_lib.SIGNATURES) == 16
+    assert len(declared) == len(_lib.SIGNATURES) == 18
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
@@ -58,12 +58,58 @@ int main(void){ P(x) P(x_row_stride) P(w) P(B) P(compute) P(residual) P(res_row_
             assert getattr(_lib.ConvDesc, name).offset == int(off), name
 
 
+def test_ffn_desc_layout_matches_header():
+    """ctypes mirror of fs2_ffn_desc has the C layout (every field's offset, and the size)."""
+    import subprocess
+    import tempfile
+
+    from fs2amd import _lib
+
+    names = [f[0] for f in _lib.FfnDesc._fields_]
+    src = "#include <stdio.h>\n#include <stddef.h>\n#include \"fs2hip.h\"\nint main(void){" + "".join(
+        f'printf("{n} %zu\\n", offsetof(fs2_ffn_desc, {n}));' for n in names) + \
+        'printf("size %zu\\n", sizeof(fs2_ffn_desc)); }\n'
+    d = tempfile.mkdtemp()
+    with open(os.path.join(d, "t.c"), "w") as f:
+        f.write(src)
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), os.path.join(d, "t.c"), "-o", os.path.join(d, "t")],
+                   check=True)
+    out = subprocess.run([os.path.join(d, "t")], capture_output=True, text=True, check=True).stdout.split("\n")
+    seen = 0
+    for line in out:
+        if not line:
+            continue
+        name, off = line.split()
+        if name == "size":
+            assert int(off) == ctypes.sizeof(_lib.FfnDesc)
+        else:
+            assert getattr(_lib.FfnDesc, name).offset == int(off), name
+            seen += 1
+    assert seen == len(names)
+
+
 def test_invalid_arguments_are_rejected_without_a_gpu():
     from fs2amd import _lib
 
     lib = _lib.load()
     d = _lib.ConvDesc()  # all-null descriptor
     assert lib.fs2_conv1d(ctypes.byref(d), None) == _lib.FS2_EINVAL
+    fd = _lib.FfnDesc()  # all-null descriptor; then shapes the fused FFN does not cover
+    assert lib.fs2_ffn(ctypes.byref(fd), None) == _lib.FS2_EINVAL
+    for k in ("x", "w", "b1", "b2", "ln_gamma", "ln_beta", "out"):
+        setattr(fd, k, 256)
+    fd.x, fd.out = 512, 1024
+    fd.B, fd.T, fd.D, fd.F, fd.KS, fd.pad, fd.x_row_stride, fd.out_row_stride = 2, 8, 256, 1024, 9, 4, 256, 256
+    fd.D = 512
+    assert lib.fs2_ffn(ctypes.byref(fd), None) == _lib.FS2_EUNSUPPORTED
+    fd.D, fd.F = 256, 1000
+    assert lib.fs2_ffn(ctypes.byref(fd), None) == _lib.FS2_EUNSUPPORTED
+    fd.F, fd.KS = 1024, 11
+    assert lib.fs2_ffn(ctypes.byref(fd), None) == _lib.FS2_EUNSUPPORTED
+    fd.KS, fd.out = 9, fd.x  # out aliasing x
+    assert lib.fs2_ffn(ctypes.byref(fd), None) == _lib.FS2_EINVAL
+    assert lib.fs2_ffn_pitch(9, 1024) == 2304 and lib.fs2_ffn_pitch(3, 1024) == 1024
+
     assert lib.fs2_attention(None, 0, 768, None, 1, 1, 2, 128, 11.3, None, 256, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_lr_durations(None, 0, 1.0, 1, 1, None, None, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_lr_expand(None, 0, None, None, 1, 1, 8, 1, None, None, 0, None, None, None) == _lib.FS2_EINVAL
@@ -318,3 +364,18 @@ def test_checkpoint_resume_round_trip(tmp_path):
         assert torch.equal(a, b), k
     ev = get_model(types.SimpleNamespace(restore_step=2), (pc, mc, tc), "cpu")
     assert not ev.training
+
+
+def test_pack_ffn_weights_layout():
+    """fs2_ffn's weight buffer: w_1 rows as [KS][D], then w_2 rows, every row padded to the pitch."""
+    from fs2amd import ops
+
+    g = torch.Generator().manual_seed(0)
+    for F, ks in ((1024, 9), (1024, 3), (512, 3)):
+        w1, w2 = torch.randn(F, 256, ks, generator=g), torch.randn(256, F, 1, generator=g)
+        p = ops.pack_ffn_weights(w1, w2)
+        pitch = max(ks * 256, F)
+        assert p.shape == (F + 256, pitch) and p.dtype == torch.bfloat16
+        assert torch.equal(p[5, 3 * 256 + 7 if ks > 3 else 256 + 7], w1[5, 7, 3 if ks > 3 else 1].to(torch.bfloat16))
+        assert torch.equal(p[F + 9, 100], w2[9, 100, 0].to(torch.bfloat16))
+        assert not p[:F, ks * 256:].any() and not p[F:, F:].any()

@@ -2,7 +2,7 @@
 """Launch ONE hot-path kernel repeatedly at the bench's cfg2 shapes (for rocprofv3 PMC passes).
 
     python tools/kernel_probe.py conv9 --reps 20
-kernels: conv9 (decoder FFN Conv1d k=9 256->1024), conv1 (FFN k=1 1024->256 + res + LN),
+kernels: ffn (decoder fused FFN, fs2_ffn), conv9 (decoder FFN Conv1d k=9 256->1024), conv1 (FFN k=1 1024->256 + res + LN),
 qkv, attn, lr (LengthRegulator gather + PE), postnet (512->512 k=5 + tanh).
 """
 import argparse
@@ -50,6 +50,10 @@ def main():
         h = rnd(B * T, 256)
         fn = lambda: ops.conv1d(h, lp.w1, lp.b1, cin=256, ks=9, pad=4, compute=P.compute, epilogue=L.EPI_BIAS_RELU,
                                 out_dtype=P.act_dtype, layout=lay)
+    elif a.kernel == "ffn":  # fused FFN (fs2_ffn): conv-k9 + ReLU + conv-k1 + res + LN, packed rows
+        h = rnd(B * T, 256)
+        out = torch.empty_like(h)
+        fn = lambda: ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=9, pad=4, ln=lp.ln2, layout=lay, out=out)
     elif a.kernel == "conv1":
         f, h = rnd(B * T, 1024), rnd(B * T, 256)
         fn = lambda: ops.conv1d(f, lp.w2, lp.b2, cin=1024, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_RES_LN,
