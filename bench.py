@@ -304,10 +304,24 @@ def cpu_baseline(batch_cpu, pc, mc, budget_s=20.0):
         for _ in range(reps):
             O.forward(sd, mc, pc, **batch_cpu)
         dt = time.perf_counter() - t0
+    # single-thread figure on the first 8 utterances of the same batch (one forward, ~5-10 s)
+    from fs2amd.data import shard
+
+    sub = shard(batch_cpu, 0, max(1, int(batch_cpu["texts"].shape[0]) // 8))
+    sub_frames = int(sub["mel_lens"].sum())
+    torch.set_num_threads(1)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        O.forward(sd, mc, pc, **sub)
+        dt1 = time.perf_counter() - t0
+    torch.set_num_threads(threads)
     B = int(batch_cpu["texts"].shape[0])
     return {"value": round(frames * reps / dt, 1), "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(), "value_1thread": round(sub_frames / dt1, 1),
             "sample": f"oracle fp32 forward on the benched cfg2 batch ({B} utterances, {frames} frames) x {reps} "
-                      f"reps after 1 warm-up, {dt:.1f} s, torch.set_num_threads({threads})"}
+                      f"reps after 1 warm-up, {dt:.1f} s, torch.set_num_threads({threads}) (the box's CPU share; "
+                      f"os.cpu_count() = {os.cpu_count()} is the whole host); value_1thread: one forward of its "
+                      f"first {int(sub['texts'].shape[0])} utterances ({sub_frames} frames) on 1 thread, {dt1:.1f} s"}
 
 
 def load_traffic(dtype="bf16", fused=False):
@@ -355,7 +369,11 @@ def main_train(args, rank, world, device):
         "data": "synthetic (pinyin ids U{64..107}, lengths U{16..64}, durations U{2..10}, mel/pitch/energy "
                 "targets N(0,1); counter-generated random-init weights)",
         "config": {"workload": "cfg3: FastSpeech2 train step, ESD-Chinese-Singing-MFA model.yaml",
-                   "global_batch": B * world, "parallelism": f"dp{world} (DDP, 32 MB buckets)",
+                   "global_batch": B * world,
+                   "parallelism": (f"dp{world} (flat fp32 gradient buffer all-reduced over RCCL in 32 MB slices "
+                                   "inside the step's HIP graph)" if step.graph_mode and step.reduce else
+                                   f"dp{world} (DDP over RCCL, 32 MB buckets)" if step.reduce else
+                                   "dp1 (one GPU, no collective)"),
                    "hip_graph": step.graph_mode},
         "loss": round(float(losses[0]), 5),
     }
@@ -577,6 +595,7 @@ def main():
         "metric": "mel-frames/sec/GPU (batch-64 synth) at 1/2/4/8 MI355X; RTF",
         "value": round(value, 1),
         "unit": "mel-frames/s",
+        "per_gpu": round(value / world, 1),  # value is the whole-job aggregate (all ranks' frames / max time)
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,

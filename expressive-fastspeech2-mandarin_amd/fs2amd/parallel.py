@@ -23,7 +23,9 @@ def init(backend=None):
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":
         ndev = torch.cuda.device_count()
-        dev_index = local if local < ndev else local % max(ndev, 1)
+        if local >= ndev:  # one process per GPU: never stack two ranks on one device
+            raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} visible GPU(s); launch at most {ndev} ranks")
+        dev_index = local
         torch.cuda.set_device(dev_index)
         device = torch.device(f"cuda:{dev_index}")
     else:

@@ -49,6 +49,65 @@ def phones_to_ids(text):
     return np.array([SYMBOL_TO_ID[p] for p in body.split() if p in SYMBOL_TO_ID])
 
 
+# ------------------------------------------------------------------ synthesis text front-end
+# synthesize_chinese_pinyin.py:24-130. Initials are tried two-letter first (zh ch sh), then one
+# letter, in the reference's order; every initial maps to itself. Finals map to 1-2 phonemes; a
+# final outside the table is spelled character by character, each character through the same
+# table when it is a one-letter final and kept as-is otherwise.
+_INITIALS_2 = ("zh", "ch", "sh")
+_INITIALS_1 = tuple("bpmfdtnlgkhjqxrzcsyw")
+_FINALS = {
+    "v": "y", "ve": "ue", "vn": "y n",
+    "an": "a n", "en": "e n", "in": "i n", "un": "u n",
+    "ang": "a ng", "eng": "e ng", "ing": "i ng", "ong": "o ng",
+    "ian": "ia n", "iang": "ia ng", "iong": "io ng", "uan": "ua n", "uang": "ua ng",
+}
+for _f in ("a", "o", "e", "i", "u", "ai", "ei", "ui", "ao", "ou", "iu", "ie", "ue", "er", "iao", "uai"):
+    _FINALS[_f] = _f
+
+
+def pinyin_to_phonemes(py):
+    """One toneless pinyin syllable -> phoneme list (synthesize_chinese_pinyin.py:34-96)."""
+    initial = next((i for i in _INITIALS_2 if py.startswith(i)), "") or \
+        next((i for i in _INITIALS_1 if py.startswith(i)), "")
+    final = py[len(initial):]
+    out = [initial] if initial else []
+    if final in _FINALS:
+        out += _FINALS[final].split()
+    else:
+        for ch in final:
+            out += _FINALS[ch].split() if ch in _FINALS else [ch]
+    return out
+
+
+def chinese_to_pinyin_phonemes(text, lazy_pinyin=None):
+    """Chinese characters -> phonemes (synthesize_chinese_pinyin.py:24-104). The syllables come from
+    ``pypinyin.lazy_pinyin(text, style=Style.NORMAL)`` (:29); pypinyin is not part of this image,
+    so pass ``lazy_pinyin`` (text -> list of toneless syllables) or install pypinyin. That one call
+    is parity-unpinned here; the syllable -> phoneme rules are tested."""
+    if lazy_pinyin is None:
+        try:
+            import pypinyin
+        except ImportError as e:
+            raise ImportError("chinese_to_pinyin_phonemes needs pypinyin (or a lazy_pinyin callable) "
+                              "for character text; pass phonemes as '{...}' instead") from e
+        syllables = pypinyin.lazy_pinyin(text, style=pypinyin.Style.NORMAL)
+    else:
+        syllables = lazy_pinyin(text)
+    return [p for py in syllables for p in pinyin_to_phonemes(py)]
+
+
+def preprocess_chinese_text(text, preprocess_config=None, lazy_pinyin=None):
+    """synthesize_chinese_pinyin.py:106-130: ``{...}`` is a phoneme string (split on whitespace),
+    anything else goes through the pinyin rules; a phoneme missing from the symbol table becomes
+    the pad id ``'_'`` (0) — unlike ``Dataset``, which drops it (dataset_chinese.py:55)."""
+    if text.startswith("{") and text.endswith("}"):
+        phonemes = text[1:-1].split()
+    else:
+        phonemes = chinese_to_pinyin_phonemes(text, lazy_pinyin)
+    return np.array([SYMBOL_TO_ID.get(p, SYMBOL_TO_ID["_"]) for p in phonemes])
+
+
 # ------------------------------------------------------------------ padding (utils/tools.py:323-357)
 def pad_1D(inputs, PAD=0):
     """Stack 1-D arrays zero-padded (or PAD-padded) to the longest one."""

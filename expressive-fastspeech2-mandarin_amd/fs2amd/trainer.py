@@ -4,16 +4,25 @@ ScheduledOptim.step_and_update_lr.
 
 Data parallel: the reference uses nn.DataParallel in one process; here
 each rank owns one GPU and its shard of the batch, and the only exchange is the mean all-reduce
-of the 34.66 M fp32 gradients (138.6 MB) over RCCL, bucketed and overlapped with the backward by
-DistributedDataParallel. Buckets are sized for xGMI rings: each bucket's all-reduce is a
-bandwidth-bound ring over 7 point-to-point links, so a few large buckets (default 32 MB: five
-for the whole model) keep per-collective latency small against ~153 GB/s per link, while still
-letting the last decoder layers' gradients start reducing while the encoder's backward runs.
-PostNet BatchNorm running stats are broadcast from rank 0 every forward (broadcast_buffers),
-DataParallel's semantics. Gradient clipping needs no extra collective: after the all-reduce every
-rank holds the same gradients.
+of the 34.66 M fp32 gradients (138.6 MB) over RCCL. Two forms:
+
+* eager steps (graph=False): DistributedDataParallel, bucketed and overlapped with the backward.
+  Buckets are sized for xGMI rings: each bucket's all-reduce is a bandwidth-bound ring over 7
+  point-to-point links, so a few large buckets (default 32 MB: five for the whole model) keep
+  per-collective latency small against ~153 GB/s per link;
+* graph=True: the whole step is captured as ONE HIP graph, RCCL collectives included. The
+  gradients live in one flat fp32 buffer (every ``p.grad`` is a view of it, as DDP's
+  gradient_as_bucket_view), zeroed at the start of each step; after the backward the buffer is
+  all-reduced in ``bucket_mb`` slices (``world_size`` > 1 or ``ddp=True``) and scaled by
+  1/world_size, then clip_grad_norm_ and the capturable fused Adam run inside the same graph.
+  DDP's autograd hooks cannot be captured; this explicit form can.
+
+PostNet BatchNorm running stats follow rank 0 (DataParallel's semantics: DDP broadcast_buffers,
+or one coalesced broadcast per step in the graph form). Gradient clipping needs no extra
+collective: after the all-reduce every rank holds the same gradients.
 """
 import torch
+import torch.distributed as dist
 import torch.nn as nn
 
 from .data import loss_inputs
@@ -22,38 +31,64 @@ from .optimizer import ScheduledOptim
 
 
 class TrainStep:
-    """graph=True (one process, fixed batch shapes): after ``warmup`` eager steps the whole step —
-    forward, loss, backward, clip_grad_norm_, Adam — is captured once as a HIP graph and replayed;
-    each call copies the batch into the graph's static input buffers, writes the step's Noam lr
-    into the optimizer's lr tensor and replays (one launch instead of ~1,600). A batch with other
-    shapes falls back to an eager step."""
+    """graph=True (fixed batch shapes): after ``warmup`` eager steps, run on the capture stream,
+    the whole step — forward, loss, backward, gradient all-reduce, clip_grad_norm_, Adam — is
+    captured once as a HIP graph and replayed; each call copies the batch into the graph's static
+    input buffers, writes the step's Noam lr into the optimizer's lr tensor and replays (one launch
+    instead of ~1,600). A batch with other shapes runs the same step body eagerly (same flat
+    gradient buffer, zeroed first: nothing a replay left behind is accumulated into it).
+
+    ``optimizer``: an existing ScheduledOptim (e.g. the one ``get_model(train=True)`` restored from
+    a checkpoint, utils/model.py:15-28) whose Adam state and step count this step continues.
+    Returned losses are fresh tensors on every call (the graph's static outputs are copied)."""
 
     def __init__(self, model, preprocess_config, model_config, train_config, device=None, world_size=1,
-                 bucket_mb=32, current_step=0, graph=False, warmup=3, ddp=None):
+                 bucket_mb=32, current_step=0, graph=False, warmup=3, ddp=None, optimizer=None, flat_grads=None):
         self.model = model.train()
         self.net = model
-        self.graph_mode = bool(graph) and world_size == 1 and device is not None and device.type == "cuda"
+        self.device = device
+        self.world_size = world_size
+        self.bucket_mb = bucket_mb
+        self.graph_mode = bool(graph) and device is not None and device.type == "cuda"
         self.warmup = warmup
         self._graph = None
         if ddp is None:
             ddp = world_size > 1
-        if ddp:  # ddp=True at world size 1 still runs DDP's bucketed all-reduce (the RCCL path on one GPU)
-            self.graph_mode = False
+        self.reduce = bool(ddp) or world_size > 1  # gradient all-reduce in the step
+        # flat gradient buffer + explicit all-reduce: always with graph=True; flat_grads=True runs the
+        # same step body eagerly (the N-rank test of the graph form's reduction on CPU / gloo)
+        self.flat = self.graph_mode if flat_grads is None else (bool(flat_grads) or self.graph_mode)
+        if ddp and not self.flat:  # ddp=True at world size 1 still runs DDP's bucketed all-reduce
             ids = [device.index] if device is not None and device.type == "cuda" else None
             self.net = nn.parallel.DistributedDataParallel(model, device_ids=ids, bucket_cap_mb=bucket_mb,
                                                            gradient_as_bucket_view=True, broadcast_buffers=True)
         self.loss = FastSpeech2Loss(preprocess_config, model_config)
+        if optimizer is not None:
+            current_step = optimizer.current_step
         self.optimizer = ScheduledOptim(model, train_config, model_config, current_step, capturable=self.graph_mode)
+        if optimizer is not None:
+            self.optimizer.load_state_dict(optimizer._optimizer.state_dict())
         opt = train_config["optimizer"]
         self.grad_acc_step = opt["grad_acc_step"]
         self.grad_clip_thresh = opt["grad_clip_thresh"]
         self.step_no = current_step + 1
+        self._flat = None
+        self._stream = None
+        if self.flat:
+            self._setup_flat_grads()
+        if self.graph_mode:
+            self._stream = torch.cuda.Stream(device)
 
     def __call__(self, batch):
         """One step on this rank's shard (a dict of forward kwargs + mels / targets on the device).
         Returns the 6 loss tensors (train.py:85-86)."""
         if self.graph_mode and self.grad_acc_step == 1:
             return self._graphed(batch)
+        if self.flat:
+            self.optimizer._update_learning_rate()
+            losses = [l.detach() for l in self._step_body(batch)]
+            self.step_no += 1
+            return losses
         return self._eager(batch)
 
     def _eager(self, batch):
@@ -67,34 +102,82 @@ class TrainStep:
         self.step_no += 1
         return losses
 
+    # ---- flat gradients + explicit all-reduce (graph form) -------------------------------------
+    def _setup_flat_grads(self):
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        n = sum(p.numel() for p in params)
+        self._flat = torch.zeros(n, dtype=torch.float32, device=params[0].device)
+        off = 0
+        for p in params:
+            p.grad = self._flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        step = max(1, int(self.bucket_mb * (1 << 20) // 4))
+        self._buckets = [self._flat[i:i + step] for i in range(0, n, step)]
+        self._bn_buffers = [b for name, b in self.model.named_buffers()
+                            if b.is_floating_point() and ("running_" in name)]
+
+    def _reduce_grads(self):
+        if not self.reduce:
+            return
+        for b in self._buckets:
+            dist.all_reduce(b)
+        if self.world_size > 1:
+            self._flat.mul_(1.0 / self.world_size)
+
+    def _sync_buffers(self):
+        if self.world_size > 1 and self._bn_buffers:
+            flat = torch.cat([b.reshape(-1) for b in self._bn_buffers])
+            dist.broadcast(flat, 0)
+            torch._foreach_copy_(self._bn_buffers, list(flat.split([b.numel() for b in self._bn_buffers])))
+
+    def _step_body(self, batch):
+        """zero grads, forward, loss, backward, all-reduce, clip, Adam: the captured step."""
+        self._flat.zero_()
+        self._sync_buffers()
+        output = self.net(**batch)
+        losses = self.loss(loss_inputs(batch), output)
+        losses[0].backward()
+        self._reduce_grads()
+        nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip_thresh)
+        self.optimizer._optimizer.step()
+        return losses
+
     # ---- whole-step HIP graph --------------------------------------------------------------------
     @staticmethod
     def _sig(batch):
         return tuple((k, tuple(v.shape), v.dtype) if torch.is_tensor(v) else (k, v) for k, v in sorted(batch.items()))
 
-    def _step_body(self, batch):
-        output = self.net(**batch)
-        losses = self.loss(loss_inputs(batch), output)
-        losses[0].backward()
-        nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip_thresh)
-        self.optimizer._optimizer.step()
-        return losses
+    def _on_stream(self, fn):
+        """Run fn on the capture stream (warm-up and eager fallbacks: the autograd engine then
+        runs every backward on the stream the graph is captured on)."""
+        cur = torch.cuda.current_stream(self.device)
+        self._stream.wait_stream(cur)
+        with torch.cuda.stream(self._stream):
+            out = fn()
+        cur.wait_stream(self._stream)
+        return out
 
     def _graphed(self, batch):
         if self.step_no <= self.warmup or (self._graph is not None and self._sig(batch) != self._graph[0]):
-            return self._eager(batch)
+            # eager step body (same flat buffer, zeroed inside): detached losses, so no autograd
+            # graph of a warm-up step outlives it into the capture
+            self.optimizer._update_learning_rate()
+            losses = self._on_stream(lambda: [l.detach() for l in self._step_body(batch)])
+            self.step_no += 1
+            return losses
         if self._graph is None:
             static = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in batch.items()}
-            self.optimizer.zero_grad()
             self.optimizer._update_learning_rate()
-            dev = next(self.model.parameters()).device
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):  # zero_grad(set_to_none) above: the backward WRITES every grad
-                losses = self._step_body(static)
+            cur = torch.cuda.current_stream(self.device)
+            self._stream.wait_stream(cur)
+            with torch.cuda.graph(g, stream=self._stream):
+                losses = [l.detach() for l in self._step_body(static)]
+            cur.wait_stream(self._stream)
             self._graph = (self._sig(batch), g, static, losses)
             g.replay()  # the captured step has not run yet: this is its execution
             self.step_no += 1
-            return losses
+            return list(torch.stack(losses).unbind())
         _, g, static, losses = self._graph
         for k, v in batch.items():
             if torch.is_tensor(v):
@@ -102,4 +185,4 @@ class TrainStep:
         self.optimizer._update_learning_rate()
         g.replay()
         self.step_no += 1
-        return losses
+        return list(torch.stack(losses).unbind())

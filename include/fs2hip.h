@@ -76,7 +76,8 @@ enum fs2_epilogue {
  * active row count *rows_dev is read on the device, so no host sync is needed. Row r is frame
  * row_pos[2r] of a sequence of row_pos[2r+1] frames; taps outside [0, len) read zeros. The
  * Decoder runs this way (every masked padded frame of an FFT block is dead work,
- * transformer/Models.py:170-178). lens / addvec must be NULL with packed rows.
+ * Decoder.forward, transformer/Models.py:139-171, layer loop :164-167). lens / addvec must be
+ * NULL with packed rows.
  * a_rowmap (KS == 1, padded output): A row of output row m is x row a_rowmap[m], or zeros when
  * -1 — mel_linear reading the packed decoder output into the padded [B, T, n_mel] contract.
  */

@@ -65,7 +65,7 @@ def test_gloo_world2_aggregation():
         assert e == 1.5 and f == full
 
 
-def _ddp_worker(rank, world, port, q):
+def _ddp_worker(rank, world, port, q, flat=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.manual_seed(0)
@@ -82,17 +82,21 @@ def _ddp_worker(rank, world, port, q):
     m = FastSpeech2(pc, mc)
     fill_module(m, seed=0)
     m.train_dropout = False
-    step = TrainStep(m, pc, mc, tc, device=None, world_size=w, bucket_mb=4)
+    step = TrainStep(m, pc, mc, tc, device=None, world_size=w, bucket_mb=4, flat_grads=flat)
+    assert step.flat == flat
     b = shard(synth_batch(4, 6, 10, seed=9, with_mels=True, pe_targets=True), r, w)
     losses = step(b)
     q.put((r, float(losses[0]), {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()}))
     parallel.shutdown()
 
 
-def test_ddp_train_step_gloo_world2(monkeypatch):
+@pytest.mark.parametrize("flat", [False, True])
+def test_ddp_train_step_gloo_world2(monkeypatch, flat):
     """TrainStep over gloo, world 2 (kernels stubbed on CPU, torch ops real): after one step both
     ranks hold identical parameters, equal to one process applying the mean of the two ranks'
-    gradients (DDP's all-reduce semantics) with the same ScheduledOptim step."""
+    gradients (DDP's all-reduce semantics) with the same ScheduledOptim step. flat=True: the graph
+    form's reduction (flat gradient buffer, explicit bucketed all-reduce, 1/world scale, coalesced
+    BatchNorm buffer broadcast) run eagerly."""
     from _common import configs
     from _stubs import install_training_stubs
     from fs2amd.data import loss_inputs
@@ -104,7 +108,7 @@ def test_ddp_train_step_gloo_world2(monkeypatch):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q, flat)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])

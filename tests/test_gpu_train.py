@@ -125,7 +125,10 @@ def test_attention_backward_matches_autograd(gpu, compute, T, lens):
 def test_graphed_train_step_equals_eager(gpu):
     """TrainStep(graph=True): after the eager warm-up steps the captured whole-step graph (forward,
     loss, backward, clip, capturable Adam with the Noam lr in a device tensor) gives the same
-    losses and parameters as eager steps (dropout off; fp32 -> identical kernels, tight tolerance)."""
+    losses and parameters as eager steps (dropout off; fp32 -> identical kernels, tight tolerance).
+    Step 5 has another batch shape: the graph path runs it eagerly between replays, and its
+    gradients must not pick up what the last replay left in the (shared) gradient buffer. The
+    returned losses of every call are distinct tensors (not the graph's overwritten outputs)."""
     from fs2amd import config as C
     from fs2amd.data import synth_batch, to_device
     from fs2amd.model import FastSpeech2
@@ -140,13 +143,15 @@ def test_graphed_train_step_equals_eager(gpu):
         m = m.to(DEV).set_precision("fp32")
         m.train_dropout = False
         st = TrainStep(m, pc, mc, tc, device=torch.device(DEV), graph=graph, warmup=2)
-        losses = []
+        kept = []
         base = synth_batch(4, 8, 20, seed=40, with_mels=True, pe_targets=True)
-        for i in range(6):  # same shapes, different values every step (the graph's static buffers refill)
-            b = dict(base, mels=base["mels"] * (1 + 0.1 * i), p_targets=base["p_targets"] + 0.05 * i)
-            losses.append(float(st(to_device(b, DEV))[0]))
+        other = synth_batch(4, 11, 20, seed=45, with_mels=True, pe_targets=True)
+        for i in range(8):  # same shapes, different values every step (the graph's static buffers refill)
+            src = other if i == 5 else base
+            b = dict(src, mels=src["mels"] * (1 + 0.1 * i), p_targets=src["p_targets"] + 0.05 * i)
+            kept.append(st(to_device(b, DEV))[0])
         torch.cuda.synchronize()
-        runs.append((losses, {k: p.detach().clone() for k, p in m.named_parameters()}, st))
+        runs.append(([float(l) for l in kept], {k: p.detach().clone() for k, p in m.named_parameters()}, st))
     (le, pe, _), (lg, pg, stg) = runs
     assert stg._graph is not None, "the graph was never captured"
     np.testing.assert_allclose(lg, le, rtol=1e-5)
@@ -184,20 +189,25 @@ def test_ddp_step_over_rccl_equals_plain(gpu):
         pc, mc, _ = configs()
         tc = C.ESD_TRAIN_CONFIG
         runs = []
-        for ddp in (False, True):
+        # plain eager; DDP (eager, RCCL bucket all-reduces); graph + explicit RCCL all-reduce of the
+        # flat gradient buffer in 4 MB slices captured inside the step's HIP graph
+        for ddp, graph in ((False, False), (True, False), (True, True)):
             m = FastSpeech2(pc, mc)
             m.load_state_dict(oracle_state_dict())
             m = m.to(DEV).set_precision("fp32")
             m.train_dropout = False
-            st = TrainStep(m, pc, mc, tc, device=torch.device(DEV), ddp=ddp, bucket_mb=4)
-            assert isinstance(st.net, torch.nn.parallel.DistributedDataParallel) == ddp
+            st = TrainStep(m, pc, mc, tc, device=torch.device(DEV), ddp=ddp, bucket_mb=4, graph=graph, warmup=2)
+            assert isinstance(st.net, torch.nn.parallel.DistributedDataParallel) == (ddp and not graph)
             base = synth_batch(4, 8, 20, seed=41, with_mels=True, pe_targets=True)
-            losses = [float(st(to_device(dict(base, mels=base["mels"] * (1 + 0.1 * i)), DEV))[0]) for i in range(3)]
+            losses = [float(st(to_device(dict(base, mels=base["mels"] * (1 + 0.1 * i)), DEV))[0]) for i in range(5)]
             torch.cuda.synchronize()
+            if graph:
+                assert st._graph is not None and st.reduce and len(st._buckets) > 1
             runs.append((losses, {k: p.detach().clone() for k, p in m.named_parameters()}))
-        (lp, pp), (ld, pd) = runs
-        np.testing.assert_allclose(ld, lp, rtol=1e-5)
-        for k in pp:
-            assert torch.allclose(pd[k], pp[k], rtol=1e-4, atol=1e-6), k
+        lp, pp = runs[0]
+        for ld, pd in runs[1:]:
+            np.testing.assert_allclose(ld, lp, rtol=1e-5)
+            for k in pp:
+                assert torch.allclose(pd[k], pp[k], rtol=1e-4, atol=1e-6), k
     finally:
         dist.destroy_process_group()

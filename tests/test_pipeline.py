@@ -89,6 +89,39 @@ def test_symbol_table():
     assert phones_to_ids("{}").shape == (0,)
 
 
+@pytest.mark.parametrize("py,phones", [
+    ("zhang", ["zh", "a", "ng"]), ("shi", ["sh", "i"]), ("xue", ["x", "ue"]), ("lv", ["l", "y"]),
+    ("lve", ["l", "ue"]), ("yuan", ["y", "ua", "n"]), ("er", ["er"]), ("a", ["a"]),
+    ("duo", ["d", "u", "o"]),  # final 'uo' not in the table: spelled per character
+    ("jiong", ["j", "io", "ng"]), ("ng", ["n", "g"]), ("hm", ["h", "m"]), ("chuang", ["ch", "ua", "ng"]),
+    ("wen", ["w", "e", "n"]), ("qvn", ["q", "y", "n"]), ("", [])])
+def test_pinyin_rules(py, phones):
+    """synthesize_chinese_pinyin.py:34-96, expected lists derived by hand from its rule table
+    (the script imports pypinyin at module level, which this image lacks, so it is not run)."""
+    from fs2amd.pipeline import pinyin_to_phonemes
+
+    assert pinyin_to_phonemes(py) == phones
+
+
+def test_preprocess_chinese_text():
+    """synthesize_chinese_pinyin.py:106-130: '{...}' phoneme strings, unknown phonemes -> '_' (0),
+    character text through lazy_pinyin (parity-unpinned: pypinyin absent; a stub stands in)."""
+    from fs2amd.pipeline import SYMBOL_TO_ID as S, preprocess_chinese_text
+
+    np.testing.assert_array_equal(preprocess_chinese_text("{b ie xx z o ng}"), [67, 80, 0, 106, 88, 87])
+    assert preprocess_chinese_text("{}").shape == (0,)
+    # only a string wrapped on both sides is a phoneme string
+    got = preprocess_chinese_text("{b a", lazy_pinyin=lambda t: ["ba"])
+    np.testing.assert_array_equal(got, [S["b"], S["a"]])
+    got = preprocess_chinese_text("你好", lazy_pinyin=lambda t: ["ni", "hao", "xx1"])
+    np.testing.assert_array_equal(got, [S["n"], S["i"], S["h"], S["ao"], S["x"], S["x"], 0])
+    try:
+        import pypinyin  # noqa: F401
+    except ImportError:
+        with pytest.raises(ImportError):
+            preprocess_chinese_text("你好")
+
+
 def test_pad_helpers():
     from fs2amd.pipeline import pad_1D, pad_2D
 
