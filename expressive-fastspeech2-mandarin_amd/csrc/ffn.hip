@@ -6,9 +6,9 @@
 // Why one kernel: as two launches the 1024-wide hidden f is written to HBM by the k=9 conv and
 // read back by the k=1 conv (cfg2 decoder: 51 MB each way per block), and the k=1 conv + LN runs
 // as its own latency-bound launch (18 % of MFMA peak). Here a workgroup owns BM = 112 rows for
-// the whole FFN and walks the hidden dimension in 4 chunks of 256 columns:
+// the whole FFN and walks the hidden dimension in chunks of 256 columns:
 //
-//   for chunk c:  GEMM1  H^T[j, m] = sum_{cb, tap} W1[c*256 + j, tap, cb*64 ...] . X[m + tap - pad, ...]
+//   for chunk c:  GEMM1  H^T[j, m] = sum_{tap, ch} W1[c*256 + j, tap, ch] . X[m + tap - pad, ch]
 //                 H = relu(H^T + b1) -> bf16 -> LDS [112 x 256]            (chunk of f, on chip)
 //                 GEMM2  Y^T[n, m] += sum_j W2[n, c*256 + j] . H[m, j]      (accumulated in registers)
 //   LN epilogue on Y (through LDS, conv_common.h's epilogue).
@@ -18,17 +18,17 @@
 // 64w .. 64w+63 of every k-step and all 112 activation rows, so its two accumulators (H^T and
 // Y^T, 4 x 7 blocks of 16x16 f32 each) sit in the accumulator registers for the whole kernel.
 //
-// Pipeline (a "unit" = one 32-channel k-step: 28 MFMAs per wave). Each wave streams ITS OWN
-// weight rows through its own 6-unit LDS-DMA ring (4 KiB per unit, the unit 5 ahead in flight) and
-// reads the next unit's fragments while the current unit's MFMAs run (two fragment register
-// sets), so the weight stream needs no workgroup barrier at all: the waves run free. Barriers
-// only where data is shared: the x rows of a 64-channel block (the tile + the taps' halo, 120 x
-// 128 B, DMA'd by all four waves once per (chunk, block) and read shifted by the tap) and the
-// hidden slice H. A fragment whose shifted row leaves its sequence reads a zero slot instead.
-// LDS: rings 96 KiB + H 56 KiB (4 column blocks of 64) + b1 4 KiB; the two halo buffers live
-// inside the H region, which is free while GEMM1 runs (the next chunk's first halo goes into H's
-// column blocks 0-1 once GEMM2 has read them). One workgroup per CU; the LN epilogue reuses it.
+// Data movement. A wave's weight rows are its own (no other wave reads them), so they never touch
+// LDS: the packed buffer (ops.pack_ffn_weights) stores each wave k-step ("unit": 64 rows x 32
+// channels, 28 MFMAs) as 4 KiB in fragment order, loaded by 4 fully coalesced 16-byte-per-lane
+// buffer loads straight into A-operand registers, DEPTH units ahead (a register ring). The
+// activations are shared: the x tile with the taps' halo (BM + KS - 1 rows x 512 B) is DMA'd to
+// LDS once, and each unit reads its 7 B fragments (rows shifted by the tap) one unit ahead of its
+// MFMAs. GEMM1 needs no barrier at all; two per chunk hand the hidden slice H over. LDS holds the
+// x tile (60 KiB), H (56 KiB) and b1; the LN epilogue reuses it. A fragment whose shifted row
+// leaves its sequence reads a 16-byte zero slot instead (address select, no branch).
 #include <type_traits>
+#include <utility>
 
 #include "conv_common.h"
 #include "fs2_common.h"
@@ -36,56 +36,60 @@
 namespace {
 
 #ifndef FFN_ABLATE
-#define FFN_ABLATE 0  // analysis builds only: bit 0 no MFMAs, bit 1 no weight DMA, bit 2 no fragment reads
+#define FFN_ABLATE 0  // analysis builds only: bit 0 no MFMAs, bit 1 no weight loads, bit 2 no B-fragment reads
 #endif
 
 constexpr int kD = 256;            // d_model (encoder_hidden / decoder_hidden)
 constexpr int kChunk = 256;        // hidden columns per chunk
-constexpr int kNU = 6;             // units in each wave's weight ring
-constexpr int kUnitW = 64 * 64;    // one wave's unit: 64 weight rows x 32 bf16 channels (4 KiB)
+constexpr int kUnit = 4096;        // bytes of one wave unit: 4 row blocks x 64 lanes x 16 B
+constexpr int kDepth = 4;          // weight units in flight per wave (register ring)
 
 struct FfnArgs {
   ConvArgs e;          // x / rows / LN epilogue fields (conv_common.h); e.w unused
-  const bf16 *w;       // fs2_ffn_desc.w: F rows of W1 ([KS][256]) then 256 rows of W2 ([F]), pitch ffn_pitch
+  const bf16 *w;       // fs2_ffn_desc.w: w_1 | w_2 in fragment order (include/fs2hip.h)
   const float *b1;     // [F]
   uint32_t w_bytes;
 };
 
-// row pitch (elements) of the packed FFN weights: one pitch for both matrices, so a weight row of
-// either GEMM is the same lane offset (only the scalar unit offset differs)
-constexpr int ffn_pitch(int KS, int F) { return KS * 256 > F ? KS * 256 : F; }
+constexpr int64_t ffn_weight_elems(int KS, int F) { return (int64_t)F * KS * kD + (int64_t)kD * F; }
 
-// physical 16-byte chunk of logical chunk c (0..3) in a 64-byte ring row r: rows r and r + 8 swap
-// chunk pairs, which makes the 16-row fragment reads (ds_read_b128 lane groups) conflict-free
-__device__ __forceinline__ int ring_chunk(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
+// physical 16-byte chunk of logical chunk c in a 512-byte LDS row r: conflict-free ds_read_b128
+// for 16 consecutive rows starting anywhere (the tap shift) and for the H writes
+__device__ __forceinline__ int xchunk(int r, int c) { return c ^ ((r & 7) << 1); }
 
-template <int MB>
-struct FragsT {
-  bf16x8 a[4];   // weight rows: 4 blocks of 16
-  bf16x8 b[MB];  // activation rows: MB blocks of 16
-};
+template <int N, typename Fn, int... I>
+__device__ __forceinline__ void static_for_impl(Fn &&f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn &&f) {
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
 
-// lgkmcnt(0) as a real s_waitcnt the compiler's wait-count pass sees (an asm one is opaque to it,
-// so it would keep counting the previous unit's fragment reads as outstanding): gfx9 simm16 =
-// vmcnt 63 (bits 3:0 and 15:14), expcnt 7, lgkmcnt 0
+// lgkmcnt(0) as a real s_waitcnt the compiler's wait-count pass sees: gfx9 simm16 = vmcnt 63
+// (bits 3:0 and 15:14), expcnt 7, lgkmcnt 0
 constexpr int kLgkm0 = 0xC07F;
 
-template <int HB, int KS, int NCH>
+template <int KS, int NCH>
 __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
-  constexpr int BM = 16 * HB, MB = HB;
-  static_assert(HB <= 7, "LDS sized for <= 112 rows");
-  constexpr int HALO_BYTES = 16 * 1024;             // (BM + 8) x 128 B, 16 pieces: 4 per wave
-  static_assert(BM + 8 <= 128, "halo pieces");
-  constexpr int RING_OFF = 0;                       // wave w's ring at w * kNU * kUnitW
-  constexpr int H_OFF = 4 * kNU * kUnitW;           // H: 4 column blocks of [BM rows][128 B]
-  constexpr int H_BLK = BM * 128;
-  constexpr int B1_OFF = H_OFF + 4 * H_BLK;
-  constexpr int ZERO_OFF = B1_OFF + 4096;           // 16 zero bytes: masked halo fragments read here
+  constexpr int MB = 7, BM = 16 * MB;
+  constexpr int XROWS = BM + KS - 1;
+  constexpr int XPIECES = (XROWS + 1) / 2;           // 1 KiB LDS-DMA pieces of 2 rows
+  constexpr int XP_PER_WAVE = (XPIECES + 3) / 4;
+  constexpr int X_OFF = 0;
+  constexpr int H_OFF = X_OFF + 4 * XP_PER_WAVE * 1024;
+  constexpr int F = NCH * kChunk;
+  constexpr int B1_OFF = H_OFF + BM * 512;
+  constexpr int ZERO_OFF = B1_OFF + F * 4;
   constexpr int EPI_LD = 256 + 4;
   constexpr int SMEM0 = ZERO_OFF + 16;
   constexpr int SMEM = SMEM0 > BM * EPI_LD * 4 ? SMEM0 : BM * EPI_LD * 4;
   static_assert(SMEM <= 163840, "LDS");
-  static_assert(2 * HALO_BYTES <= 4 * H_BLK && HALO_BYTES <= 2 * H_BLK, "halo buffers inside H");
+  constexpr int NK1 = KS * (kD / 32);  // GEMM1 units per chunk (tap-major, 8 k-steps per tap)
+  constexpr int NK2 = kChunk / 32;     // GEMM2 units per chunk
+  constexpr int NU = NK1 + NK2;
+  constexpr int DEPTH = kDepth;
+  static_assert(NK1 % DEPTH == 0 && NK2 % DEPTH == 0, "static register-ring slots");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const ConvArgs &a = p.e;
@@ -95,12 +99,6 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   const int m0 = blockIdx.x * BM;
   if (m0 >= M) return;
   const int pad = a.pad, T = a.T;
-  constexpr int F = NCH * kChunk;
-
-  // ---- b1 -> LDS (plain loads before any LDS-DMA is in flight), the zero slot
-  for (int i = tid; i < F / 4; i += 256)
-    *reinterpret_cast<float4 *>(smem + B1_OFF + 16 * i) = reinterpret_cast<const float4 *>(p.b1)[i];
-  if (tid == 0) *reinterpret_cast<float4 *>(smem + ZERO_OFF) = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // ---- tap validity of this lane's activation rows (sequence position / length)
   int tpos[MB], tlen[MB];
@@ -136,93 +134,78 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     const int sh = tap - pad;
     if (!(tile_inside && tw + sh >= 0 && tw + BM - 1 + sh < lw)) need_mask |= 1u << tap;
   }
-  // consume the row_pos loads here: a first use behind the LDS-DMA stream would drain it
+  // b1 -> LDS, the zero slot; consume the row_pos loads before the DMA stream starts
+  for (int i = tid; i < F / 4; i += 256)
+    *reinterpret_cast<float4 *>(smem + B1_OFF + 16 * i) = reinterpret_cast<const float4 *>(p.b1)[i];
+  if (tid == 0) *reinterpret_cast<float4 *>(smem + ZERO_OFF) = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) asm volatile("" ::"v"(tpos[mb]), "v"(tlen[mb]));
 
-  // ---- DMA addressing
-  constexpr int PITCH = ffn_pitch(KS, F);
-  constexpr uint32_t wrow = (uint32_t)PITCH * 2u, w2off = (uint32_t)F * wrow;
+  // ---- x tile (rows m0 - pad .. m0 + BM + KS - 2, all 256 channels) -> LDS, once
   const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const rsrc_t wr = make_rsrc(p.w, p.w_bytes);
   const uint32_t xrow = (uint32_t)a.xs * 2u;
-  auto glds = [&](rsrc_t rs, char *dst, uint32_t off) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)dst, 16, off, 0, 0, 0);
-  };
-  // Weight units: 1 KiB pieces of 16 rows x 64 B, lane-linear image; lane l -> row 16i + l/4 of
-  // the wave's 64, physical chunk l & 3 (the ring_chunk swizzle applied on the source address)
-  const int urow = lane >> 2;
-  const uint32_t ulo = (uint32_t)(64 * w + urow) * wrow + (uint32_t)ring_chunk(urow, lane & 3) * 16u;
-  // Unit schedule: units come in pairs = 64-channel k-steps (+64 B for the second half). Pairs of
-  // a chunk: GEMM1 pr = cb * KS + tap (pr < NP1), then GEMM2 pr = NP1 + qp (64 hidden columns).
-  // Lane pr of ptab_off / ptab_str holds pair pr's byte offset in chunk 0 and the chunk stride:
-  // the producer reads both with v_readlane instead of decoding the unit.
-  constexpr int NP1 = 4 * KS, NPC = NP1 + kChunk / 64;
-  static_assert(NPC <= 64, "one table lane per pair");
-  const int tl = lane < NPC ? lane : NPC - 1;
-  const uint32_t ptab_off = tl < NP1 ? (uint32_t)((tl % KS) * (2 * kD) + (tl / KS) * 128)
-                                     : w2off + (uint32_t)(128 * (tl - NP1));
-  const uint32_t ptab_str = tl < NP1 ? (uint32_t)kChunk * wrow : (uint32_t)(2 * kChunk);
-  char *const ring = smem + RING_OFF + w * (kNU * kUnitW);
-  // unit `half` of pair (c, pr) into ring slot `slot` (4 pieces). Past the last unit (c == NCH) the
-  // offsets run into W2 or past the buffer (zeros): harmless loads that keep every unit's vmcnt
-  // count equal.
-  auto issue_unit = [&](int c, int pr, int half, int slot) {
-    if (FFN_ABLATE & 2) return;
-    const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)ptab_off, pr) +
-                         (uint32_t)c * (uint32_t)__builtin_amdgcn_readlane((int)ptab_str, pr) +
-                         (uint32_t)(half * 64) + ulo;
-    char *dst = ring + slot * kUnitW;
+  {
+    const int prow = lane >> 5, pch = lane & 31;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds(wr, dst + i * 1024, off + (uint32_t)(16 * i) * wrow);
-  };
-  // halo of channel block cb: rows m0 - pad .. m0 + BM + KS - 2, 128 B (64 channels) each, into
-  // halo buffer `buf` (inside the H region); 4 pieces of 8 rows per wave
-  const int prow = lane >> 3, plc = (lane & 7) ^ ((lane >> 3) & 7);
-  auto issue_halo = [&](int cb, int buf) {
-    char *dst = smem + H_OFF + buf * HALO_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < XP_PER_WAVE; ++i) {
       const int pc = w + 4 * i;
-      const int hr = 8 * pc + prow;
-      const int gm = m0 - pad + hr;
-      const bool ok = hr < BM + KS - 1 && gm >= 0 && gm < M;
-      glds(xr, dst + pc * 1024, ok ? (uint32_t)gm * xrow + (uint32_t)(cb * 64 + plc * 8) * 2u : kOOB);
+      const int r = 2 * pc + prow;
+      const int gm = m0 - pad + r;
+      const bool ok = r < XROWS && gm >= 0 && gm < M;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xr, (__attribute__((address_space(3))) void *)(smem + X_OFF + pc * 1024), 16,
+          ok ? (uint32_t)gm * xrow + (uint32_t)xchunk(r, pch) * 16u : kOOB, 0, 0, 0);
     }
-  };
+  }
 
-  // ---- fragment reads
-  const int aoff = (lane & 15) * 64 + ring_chunk(lane & 15, lane >> 4) * 16;  // + 1 KiB per block
-  const int hrow0 = lane & 15;  // activation row (tile-relative) of block 0
-  auto read_a = [&](int slot, FragsT<MB> &f) {
-    const char *st = ring + slot * kUnitW + aoff;
+  // ---- weight units: register ring of DEPTH units. Every load site is static (its unit is known
+  // from its position in the unrolled code), so the stream needs no branch: a branch there splits
+  // the MFMA sequence and hipcc then copies the accumulators between blocks.
+  constexpr uint32_t W2_BASE = (uint32_t)(F * KS * kD * 2);
+  const uint32_t lane_off = (uint32_t)lane * 16u;
+  auto base1 = [&](int c) { return (uint32_t)((c * 4 + w) * NK1) * (uint32_t)kUnit; };
+  auto base2 = [&](int c) { return W2_BASE + (uint32_t)(w * (F / 32) + c * NK2) * (uint32_t)kUnit; };
+  bf16x8 pa[DEPTH][4];
+  auto load_at = [&](auto S, uint32_t so) {
+    constexpr int s = decltype(S)::value;
+    if (FFN_ABLATE & 2) return;
+    // pinned after the MFMAs that read the slot's previous unit: a load hoisted above them keeps
+    // both units live, and the register allocator then rotates the whole ring through copies
+    // (each copy waiting for its load) at the loop back-edge
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb) f.a[jb] = *reinterpret_cast<const bf16x8 *>(st + jb * 1024);
+    for (int jb = 0; jb < 4; ++jb) {
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(wr, lane_off + jb * 1024, so, 0);
+      pa[s][jb] = __builtin_bit_cast(bf16x8, v);
+    }
+    __builtin_amdgcn_sched_barrier(0);
   };
-  // GEMM1 unit (channel block cb, tap, half s): the halo rows shifted by the tap; a 16-row block
-  // step keeps (row & 7), so one swizzled base serves every block (+ 2 KiB each). A lane whose
-  // shifted row leaves its sequence reads the zero slot instead (address select: no wait for the
-  // data, no branch -- a branch here makes hipcc drain every outstanding read at the join).
-  auto read_g1 = [&](int cb, int tap, int s, int slot, FragsT<MB> &f) {
+  static_for<DEPTH>([&](auto S) { load_at(S, base1(0) + (uint32_t)(decltype(S)::value * kUnit)); });
+
+  // ---- B fragments
+  const int hrow0 = lane & 15;  // activation row (tile-relative) of block 0
+  const int hi = lane >> 4;
+  bf16x8 f0[MB], f1[MB];
+  // GEMM1 unit (tap, k-step ks): x rows shifted by the tap; a 16-row block step keeps (row & 7)
+  auto read_x = [&](int tap, int ks, bf16x8 (&f)[MB]) {
     if (FFN_ABLATE & 4) return;
-    read_a(slot, f);
     const bool all_ok = ((need_mask >> tap) & 1u) == 0;
     const int sh = tap - pad;
-    const int hr = hrow0 + tap;
-    const int hb = H_OFF + (cb & 1) * HALO_BYTES + hr * 128 + (((s * 4 + (lane >> 4)) ^ (hr & 7)) << 4);
+    const int r = hrow0 + tap;
+    const int base = X_OFF + r * 512 + (xchunk(r, 4 * ks + hi) << 4);
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       const bool ok = all_ok || (unsigned)(tpos[mb] + sh) < (unsigned)tlen[mb];
-      f.b[mb] = *reinterpret_cast<const bf16x8 *>(smem + (ok ? hb + mb * 2048 : ZERO_OFF));
+      f[mb] = *reinterpret_cast<const bf16x8 *>(smem + (ok ? base + mb * 8192 : ZERO_OFF));
     }
   };
-  // GEMM2 unit q (32 hidden columns of the chunk): H column block q / 2, half q % 2
-  auto read_g2 = [&](int q, int slot, FragsT<MB> &f) {
+  // GEMM2 unit q (32 hidden columns of the chunk)
+  auto read_h = [&](int q, bf16x8 (&f)[MB]) {
     if (FFN_ABLATE & 4) return;
-    read_a(slot, f);
-    const char *hp = smem + H_OFF + (q >> 1) * H_BLK + hrow0 * 128 + ((((q & 1) * 4 + (lane >> 4)) ^ (lane & 7)) << 4);
+    const char *hp = smem + H_OFF + hrow0 * 512 + (xchunk(hrow0, 4 * q + hi) << 4);
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) f.b[mb] = *reinterpret_cast<const bf16x8 *>(hp + mb * 2048);
+    for (int mb = 0; mb < MB; ++mb) f[mb] = *reinterpret_cast<const bf16x8 *>(hp + mb * 8192);
   };
 
   f32x4 acc1[4][MB], acc2[4][MB];
@@ -233,13 +216,13 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  auto mma = [&](f32x4 (&acc)[4][MB], const FragsT<MB> &f) {
+  auto mma = [&](f32x4 (&acc)[4][MB], const bf16x8 (&fa)[4], const bf16x8 (&fb)[MB]) {
     if (FFN_ABLATE & 1) return;
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
-        acc[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[jb], f.b[mb], acc[jb][mb], 0, 0, 0);
+        acc[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[jb], fb[mb], acc[jb][mb], 0, 0, 0);
   };
   auto bar = []() {
     __builtin_amdgcn_sched_barrier(0);
@@ -247,13 +230,14 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  // chunk c's hidden slice: H[m][j] = bf16(relu(acc1 + b1)); lane holds 4 consecutive j of row m,
-  // all inside column block w
+  // chunk c's hidden slice: H[m][j] = bf16(relu(acc1 + b1)); lane holds 4 consecutive j of row m
   auto write_h = [&](int c) {
+    float z;  // an opaque 0: a constant zero here makes the register allocator rotate acc1
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb) {
-      const int jj = jb * 16 + 4 * (lane >> 4);  // column inside block w
-      const float4 bb = *reinterpret_cast<const float4 *>(smem + B1_OFF + 4 * (c * kChunk + w * 64 + jj));
+      const int j = w * 64 + jb * 16 + 4 * hi;  // hidden column inside the chunk
+      const float4 bb = *reinterpret_cast<const float4 *>(smem + B1_OFF + 4 * (c * kChunk + j));
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) {
         const f32x4 v = acc1[jb][mb];
@@ -263,138 +247,80 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
         o[2] = (bf16)fmaxf(v[2] + bb.z, 0.f);
         o[3] = (bf16)fmaxf(v[3] + bb.w, 0.f);
         const int m = hrow0 + mb * 16;
-        *reinterpret_cast<bf16x4 *>(smem + H_OFF + w * H_BLK + m * 128 + (((jj >> 3) ^ (lane & 7)) << 4) +
-                                    (jj & 7) * 2) = o;
-        acc1[jb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<bf16x4 *>(smem + H_OFF + m * 512 + (xchunk(m, j >> 3) << 4) + (j & 7) * 2) = o;
+        acc1[jb][mb] = f32x4{z, z, z, z};
       }
     }
   };
 
-  // ---- prologue: halo 0 + halo 1 (both buffers free), units 0 .. NU-2 of this wave's ring
-  issue_halo(0, 0);
-  issue_halo(1, 1);
-  int pc = 0, pp = 0, ph = 0;  // producer: chunk, pair, half of the unit issued next
-  auto produce = [&](int slot) {
-    issue_unit(pc, pp, ph, slot);
-    if (++ph == 2) {
-      ph = 0;
-      if (++pp == NPC) {
-        pp = 0;
-        ++pc;
-      }
-    }
-  };
-#pragma unroll
-  for (int u = 0; u < kNU - 1; ++u) produce(u);
-  // halos 0 / 1 and unit 0 landed (units 1 .. NU-2 may stay in flight), every wave's pieces
-  // visible; b1 stored
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  // x tile landed (the DEPTH * 4 weight loads behind it may stay in flight), b1 stored; visible
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * DEPTH) : "memory");
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   bar();
-  FragsT<MB> f0, f1;
-  read_g1(0, 0, 0, 0, f0);
-  int sread = 1;           // ring slot of the next unit to read (unit u + 1)
-  int sprod = kNU - 1;     // ring slot the producer fills next (unit u + NU - 1)
+  read_x(0, 0, f0);
 
-  // One iteration = unit u (its fragments fc were read by the previous iteration): wait for this
-  // wave's own unit u + 1 (vmcnt(12): units u + 2 .. u + 4 may stay in flight; a halo issued in
-  // the last three iterations only makes it wait longer), refill the slot of unit u - 1 (its
-  // fragments are in registers) with unit u + 5, read unit u + 1 into fn, then the 28 MFMAs of
-  // unit u: the LDS reads of u + 1 overlap the matrix work of u. No barrier: the ring is private.
-  auto iter = [&](f32x4 (&acc)[4][MB], FragsT<MB> &fc, auto &&pre, auto &&rd) {
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    __builtin_amdgcn_s_waitcnt(kLgkm0);
-    pre();
-    produce(sprod);
-    sprod = sprod == kNU - 1 ? 0 : sprod + 1;
-    rd(sread);
-    sread = sread == kNU - 1 ? 0 : sread + 1;
-    mma(acc, fc);
+  // One GEMM1 unit k = g * DEPTH + s (ring slot s): read the next unit's B fragments (LDS latency
+  // hidden behind this unit's MFMAs), 28 MFMAs, then refill slot s with the unit DEPTH ahead
+  // (GEMM1 unit k + DEPTH, or in the last group GEMM2 unit s). Units alternate f0 / f1 by parity;
+  // NK1 and NK2 are even.
+  auto unit1 = [&](auto S, int c, int g) {
+    constexpr int s = decltype(S)::value;
+    // the next unit's fragments; after the chunk's last GEMM1 unit this reads "tap KS" (rows past the
+    // x tile, still inside LDS; overwritten by H's first unit): one loop body for every group
+    const int kn = g * DEPTH + s + 1;
+    if constexpr (s & 1)
+      read_x(kn >> 3, kn & 7, f0);
+    else
+      read_x(kn >> 3, kn & 7, f1);
+    if constexpr (s & 1)
+      mma(acc1, pa[s], f1);
+    else
+      mma(acc1, pa[s], f0);
+    const bool more = g + 1 < NK1 / DEPTH;  // else: GEMM2 unit s of this chunk (scalar select)
+    load_at(S, more ? base1(c) + (uint32_t)((g + 1) * DEPTH + s) * (uint32_t)kUnit
+                    : base2(c) + (uint32_t)(s * kUnit));
   };
-  // the units of a shared-data hand-off (inside `pre`, after the iteration's waits): every wave's
-  // halo / H writes visible, every wave past its reads of the buffer about to be refilled
-  auto nopre = [] {};
-  // Units alternate f0 / f1 (even units read theirs from f0; a chunk has an even number of units).
-  // Every iter() call site is unconditional: a call inside a branch makes hipcc merge the
-  // accumulators through a phi and copy all 112 of them every unit.
 #pragma nounroll
   for (int c = 0; c < NCH; ++c) {
 #pragma nounroll
-    for (int cb = 0; cb < 4; ++cb) {
-#pragma nounroll
-      for (int tap = 0; tap < KS; ++tap) {
-        iter(acc1, f0, nopre, [&](int sl) { read_g1(cb, tap, 1, sl, f1); });
-        // after the last tap of block cb: the next block's halo becomes visible to every wave (the
-        // barrier), and every wave is past its reads of block cb (its last unit is in registers),
-        // whose buffer takes block cb + 2 (issued by all waves, consumed 2*KS units later)
-        const bool last_tap = tap + 1 == KS;
-        iter(acc1, f1,
-             [&] {
-               if (last_tap && cb + 1 < 4) {
-                 bar();
-                 if (cb + 2 < 4) issue_halo(cb + 2, cb & 1);
-               }
-             },
-             [&](int sl) {
-               if (!last_tap)
-                 read_g1(cb, tap + 1, 0, sl, f0);
-               else if (cb + 1 < 4)
-                 read_g1(cb + 1, 0, 0, sl, f0);
-               // (after the last GEMM1 unit the next unit reads H: below)
-             });
-      }
-    }
-    // every wave is past its halo reads (barrier): H overwrites the halo buffers; then H visible
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    for (int g = 0; g < NK1 / DEPTH; ++g) static_for<DEPTH>([&](auto S) { unit1(S, c, g); });
+    // every wave is past its GEMM2 reads of the previous chunk's H: overwrite it; then H visible
     bar();
     write_h(c);
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     bar();
-    // (the last GEMM1 iteration advanced sread past this unit without reading it)
-    read_g2(0, sread == 0 ? kNU - 1 : sread - 1, f0);
-#pragma nounroll
-    for (int q = 0; q < kChunk / 32; q += 2) {
-      const bool more = c + 1 < NCH, last = q + 2 == kChunk / 32;
-      // at unit 4: every wave is past its reads of H blocks 0-1 (units 0..3): the next chunk's
-      // first halo goes there
-      iter(acc2, f0,
-           [&] {
-             if (q == 4 && more) {
-               bar();
-               issue_halo(0, 0);
-             }
-           },
-           [&](int sl) { read_g2(q + 1, sl, f1); });
-      // at the last unit: every wave is past its H reads: the next chunk's second halo into H
-      // blocks 1-2; its first halo (issued 3 units ago) is visible after the barrier
-      iter(acc2, f1,
-           [&] {
-             if (last && more) {
-               bar();
-               issue_halo(1, 1);
-             }
-           },
-           [&](int sl) {
-             if (!last)
-               read_g2(q + 2, sl, f0);
-             else if (more)
-               read_g1(0, 0, 0, sl, f0);
-           });
-    }
+    read_h(0, f0);
+    const uint32_t next1 = c + 1 < NCH ? base1(c + 1) : 0u;  // past the last unit: harmless reloads
+    static_for<NK2>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      constexpr int s = q % DEPTH;
+      if constexpr (q + 1 == NK2)
+        read_x(0, 0, f0);  // the next chunk's first unit (x is never overwritten)
+      else if constexpr (q & 1)
+        read_h(q + 1, f0);
+      else
+        read_h(q + 1, f1);
+      if constexpr (q & 1)
+        mma(acc2, pa[s], f1);
+      else
+        mma(acc2, pa[s], f0);
+      if constexpr (q + DEPTH < NK2)
+        load_at(std::integral_constant<int, s>{}, base2(c) + (uint32_t)((q + DEPTH) * kUnit));
+      else
+        load_at(std::integral_constant<int, s>{}, next1 + (uint32_t)((q + DEPTH - NK2) * kUnit));
+    });
   }
 
   // ---- LN epilogue: Y^T accumulators -> E[m][n] f32 -> conv_common.h epilogue (RES_LN)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_waitcnt(kLgkm0);
-  bar();  // every wave is past its last LDS read: E may overwrite the rings / H
+  bar();  // every wave is past its last LDS read: E may overwrite the x tile / H
   float *E = reinterpret_cast<float *>(smem);
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
-      *reinterpret_cast<f32x4 *>(E + (hrow0 + mb * 16) * EPI_LD + w * 64 + nb * 16 + 4 * (lane >> 4)) =
-          acc2[nb][mb];
+      *reinterpret_cast<f32x4 *>(E + (hrow0 + mb * 16) * EPI_LD + w * 64 + nb * 16 + 4 * hi) = acc2[nb][mb];
   __syncthreads();
   epilogue<BM, 256, 4, true>(a, E, m0, 0, tid, M);
 }
@@ -419,7 +345,7 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   if (M64 > 0x7fffff00LL) return FS2_EINVAL;
   if (M64 == 0) return FS2_OK;
   const int64_t xb = M64 * d->x_row_stride * 2;
-  const int64_t wb = (int64_t)(d->F + kD) * fs2_ffn_pitch(d->KS, d->F) * 2;
+  const int64_t wb = ffn_weight_elems(d->KS, d->F) * 2;
   if (xb >= (1LL << 31)) return FS2_EUNSUPPORTED;
 
   FfnArgs p;
@@ -465,17 +391,17 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   hipStream_t s = as_stream(stream);
   // instantiated shapes: kernel 9 (model.yaml conv_kernel_size [9, 1]) or 3, F = 1024 or 512
   if (d->KS == 9 && nch == 4)
-    hipLaunchKernelGGL((ffn_fused_kernel<7, 9, 4>), dim3(nwg), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((ffn_fused_kernel<9, 4>), dim3(nwg), dim3(256), 0, s, p);
   else if (d->KS == 9 && nch == 2)
-    hipLaunchKernelGGL((ffn_fused_kernel<7, 9, 2>), dim3(nwg), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((ffn_fused_kernel<9, 2>), dim3(nwg), dim3(256), 0, s, p);
   else if (d->KS == 3 && nch == 4)
-    hipLaunchKernelGGL((ffn_fused_kernel<7, 3, 4>), dim3(nwg), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((ffn_fused_kernel<3, 4>), dim3(nwg), dim3(256), 0, s, p);
   else if (d->KS == 3 && nch == 2)
-    hipLaunchKernelGGL((ffn_fused_kernel<7, 3, 2>), dim3(nwg), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((ffn_fused_kernel<3, 2>), dim3(nwg), dim3(256), 0, s, p);
   else
     return FS2_EUNSUPPORTED;
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
 
-extern "C" int fs2_ffn_pitch(int KS, int F) { return ffn_pitch(KS, F); }
+extern "C" int64_t fs2_ffn_weight_elems(int KS, int F) { return ffn_weight_elems(KS, F); }

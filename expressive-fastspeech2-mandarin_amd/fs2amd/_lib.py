@@ -71,7 +71,7 @@ SIGNATURES = {
     "fs2_conv_cin_pad": (_i, [_i, _i]),
     "fs2_conv1d": (_i, [ctypes.POINTER(ConvDesc), _p]),
     "fs2_ffn": (_i, [ctypes.POINTER(FfnDesc), _p]),
-    "fs2_ffn_pitch": (_i, [_i, _i]),
+    "fs2_ffn_weight_elems": (ctypes.c_int64, [_i, _i]),
     "fs2_attention": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p]),
     "fs2_embed_pe": (_i, [_p, _p, _i, _p, _i, _i, _i, _p, _i, _p, _p]),
     "fs2_attention_bwd": (_i, [_p, _i, _i64, _p, _i64, _p, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p, _i64, _p]),

@@ -278,15 +278,21 @@ def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None
 
 
 def pack_ffn_weights(w1, w2):
-    """PositionwiseFeedForward weights -> the fs2_ffn buffer: bf16 rows of pitch max(KS*D, F): the F
-    rows of w_1 (nn.Conv1d weight [F, D, KS], each row as [KS][D]) then the D rows of w_2 ([D, F, 1])."""
+    """PositionwiseFeedForward weights -> the fs2_ffn buffer (flat bf16, fs2_ffn_weight_elems(KS, F)
+    elements): both matrices in MFMA fragment order, so that one wave's weight k-step ("unit": 64
+    weight rows x 32 channels) is 4 KiB contiguous and each 1 KiB row block is one fully coalesced
+    16-byte-per-lane load straight into the A-operand registers (lane l = 16 * hi + r holds row r of
+    the block, channels 8 * hi .. 8 * hi + 7 of the 32).
+
+    w_1 (nn.Conv1d weight [F, D, KS]): [F/64 row quads][KS taps][D/32 k-steps][4 blocks][4 hi][16 r][8]
+    w_2 ([D, F, 1]):                   [D/64 row quads][F/32 k-steps][4 blocks][4 hi][16 r][8]"""
     F, D, ks = w1.shape
     assert w2.shape[:2] == (D, F) and (w2.dim() == 2 or w2.shape[2] == 1), (tuple(w1.shape), tuple(w2.shape))
-    pitch = _lib.fs2_ffn_pitch(ks, F)
-    out = torch.zeros(F + D, pitch, dtype=torch.bfloat16, device=w1.device)
-    out[:F, :ks * D] = w1.detach().float().permute(0, 2, 1).reshape(F, ks * D).to(torch.bfloat16)
-    out[F:, :F] = w2.detach().float().reshape(D, F).to(torch.bfloat16)
-    return out
+    assert F % 64 == 0 and D % 64 == 0, (F, D)
+    a = w1.detach().float().permute(0, 2, 1)  # [F][KS][D]
+    a = a.reshape(F // 64, 4, 16, ks, D // 32, 4, 8).permute(0, 3, 4, 1, 5, 2, 6)
+    b = w2.detach().float().reshape(D // 64, 4, 16, F // 32, 4, 8).permute(0, 3, 1, 4, 2, 5)
+    return torch.cat([a.reshape(-1), b.reshape(-1)]).to(torch.bfloat16).contiguous()
 
 
 def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=None, layout=None, out=None):
@@ -303,7 +309,7 @@ def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=No
         B, T, _ = x.shape
     D = x.shape[-1]
     F = b1.numel()
-    assert w_packed.is_contiguous() and w_packed.shape == (F + D, _lib.fs2_ffn_pitch(ks, F)), tuple(w_packed.shape)
+    assert w_packed.is_contiguous() and w_packed.numel() == _lib.fs2_ffn_weight_elems(ks, F), tuple(w_packed.shape)
     d = L.FfnDesc()
     d.x, d.x_row_stride = x.data_ptr(), _rows(x, "x")
     d.w, d.b1, d.b2 = w_packed.data_ptr(), b1.data_ptr(), b2.data_ptr()

@@ -165,9 +165,13 @@ int fs2_conv_cin_pad(int Cin, int compute);
  * 256-column chunk at a time, and accumulates w_2's product in registers (two fs2_conv1d launches
  * write and re-read it: 51 MB each way per cfg2 decoder block).
  * bf16 only. x / out: bf16 rows of D = 256 (out must not alias x). w: the FFN's two weight
- * matrices in one bf16 buffer, every row fs2_ffn_pitch(KS, F) = max(KS*D, F) elements long: F rows
- * of w_1 (row j = w_1.weight[j, :, :] transposed to [KS][D]) followed by D rows of w_2 (row n =
- * w_2.weight[n, :, 0], F elements). Shapes: D = 256, F in {512, 1024}, KS in {3, 9}, pad <= KS - 1
+ * matrices in one flat bf16 buffer of fs2_ffn_weight_elems(KS, F) elements, in MFMA fragment
+ * order (64-row quads, then k-steps of 32 channels, then 4 blocks of 16 rows, then 64 lanes x 8):
+ *   w_1 (Conv1d weight [F][D][KS]) as [F/64][KS][D/32][4][4][16][8], element (q, k, s, b, h, r, e) =
+ *       w_1[64q + 16b + r][32s + 8h + e][k];
+ *   then w_2 ([D][F][1]) as [D/64][F/32][4][4][16][8], element (q, s, b, h, r, e) =
+ *       w_2[64q + 16b + r][32s + 8h + e][0].
+ * Shapes: D = 256, F in {512, 1024}, KS in {3, 9}, pad <= KS - 1
  * (FS2_EUNSUPPORTED otherwise: the caller runs the two fs2_conv1d launches). Packed rows (rows_dev / row_pos, fs2_seq_layout) or padded [B, T] rows (lens /
  * addvec allowed) as in fs2_conv1d. Deterministic; each output row depends only on its own input
  * rows, so packed and padded launches agree bit for bit.
@@ -175,7 +179,7 @@ int fs2_conv_cin_pad(int Cin, int compute);
 typedef struct fs2_ffn_desc {
   const void *x;            /* bf16 [B*T, >= D]: the FFN input and the LayerNorm residual        */
   int64_t x_row_stride;
-  const void *w;            /* packed bf16 w_1 | w_2 rows, pitch fs2_ffn_pitch(KS, F) (see above)  */
+  const void *w;            /* bf16 w_1 | w_2 in fragment order (see above)                       */
   const float *b1;          /* [F]                                                               */
   const float *b2;          /* [D]                                                               */
   int B, T, D, F, KS, pad;
@@ -192,7 +196,7 @@ typedef struct fs2_ffn_desc {
 } fs2_ffn_desc;
 
 int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream);
-int fs2_ffn_pitch(int KS, int F);
+int64_t fs2_ffn_weight_elems(int KS, int F); /* F*KS*256 + 256*F */
 
 /*
  * fs2_attention — ScaledDotProductAttention with a key-padding mask, all heads.

@@ -108,7 +108,8 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     assert lib.fs2_ffn(ctypes.byref(fd), None) == _lib.FS2_EUNSUPPORTED
     fd.KS, fd.out = 9, fd.x  # out aliasing x
     assert lib.fs2_ffn(ctypes.byref(fd), None) == _lib.FS2_EINVAL
-    assert lib.fs2_ffn_pitch(9, 1024) == 2304 and lib.fs2_ffn_pitch(3, 1024) == 1024
+    assert lib.fs2_ffn_weight_elems(9, 1024) == 1024 * 9 * 256 + 256 * 1024
+    assert lib.fs2_ffn_weight_elems(3, 512) == 512 * 3 * 256 + 256 * 512
 
     assert lib.fs2_attention(None, 0, 768, None, 1, 1, 2, 128, 11.3, None, 256, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_lr_durations(None, 0, 1.0, 1, 1, None, None, None, None) == _lib.FS2_EINVAL
@@ -367,15 +368,19 @@ def test_checkpoint_resume_round_trip(tmp_path):
 
 
 def test_pack_ffn_weights_layout():
-    """fs2_ffn's weight buffer: w_1 rows as [KS][D], then w_2 rows, every row padded to the pitch."""
+    """fs2_ffn's weight buffer: w_1 then w_2 in MFMA fragment order (include/fs2hip.h, fs2_ffn)."""
     from fs2amd import ops
 
     g = torch.Generator().manual_seed(0)
     for F, ks in ((1024, 9), (1024, 3), (512, 3)):
         w1, w2 = torch.randn(F, 256, ks, generator=g), torch.randn(256, F, 1, generator=g)
         p = ops.pack_ffn_weights(w1, w2)
-        pitch = max(ks * 256, F)
-        assert p.shape == (F + 256, pitch) and p.dtype == torch.bfloat16
-        assert torch.equal(p[5, 3 * 256 + 7 if ks > 3 else 256 + 7], w1[5, 7, 3 if ks > 3 else 1].to(torch.bfloat16))
-        assert torch.equal(p[F + 9, 100], w2[9, 100, 0].to(torch.bfloat16))
-        assert not p[:F, ks * 256:].any() and not p[F:, F:].any()
+        assert p.shape == (F * ks * 256 + 256 * F,) and p.dtype == torch.bfloat16
+        a = p[:F * ks * 256].view(F // 64, ks, 8, 4, 4, 16, 8)
+        b = p[F * ks * 256:].view(4, F // 32, 4, 4, 16, 8)
+        for q, k, s_, bb, h, r, e in ((0, 0, 0, 0, 0, 0, 0), (3, ks - 1, 5, 2, 3, 11, 6), (F // 64 - 1, 1, 7, 3, 1, 15, 7)):
+            assert a[q, k, s_, bb, h, r, e] == w1[64 * q + 16 * bb + r, 32 * s_ + 8 * h + e, k].to(torch.bfloat16)
+        for q, s_, bb, h, r, e in ((0, 0, 0, 0, 0, 0), (2, F // 32 - 1, 1, 2, 9, 4), (3, 3, 3, 3, 15, 7)):
+            assert b[q, s_, bb, h, r, e] == w2[64 * q + 16 * bb + r, 32 * s_ + 8 * h + e, 0].to(torch.bfloat16)
+        # a permutation: every weight exactly once
+        assert torch.equal(p.float().sort().values, torch.cat([w1.reshape(-1), w2.reshape(-1)]).to(torch.bfloat16).float().sort().values)
