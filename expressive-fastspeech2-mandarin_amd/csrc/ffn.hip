@@ -35,8 +35,12 @@
 
 namespace {
 
+#ifndef FFN_TRACE
+#define FFN_TRACE 0  // analysis builds only: per-phase shader-clock stamps of wave 0 into spare output rows
+#endif
 #ifndef FFN_ABLATE
-#define FFN_ABLATE 0  // analysis builds only: bit 0 no MFMAs, bit 1 no weight loads, bit 2 no B-fragment reads
+#define FFN_ABLATE 0  // analysis builds only: bit 0 no MFMAs, bit 1 no weight loads, bit 2 no B-fragment reads, bit 3 every
+                      // weight load reads unit 0 (L1-resident), bit 4 no tap masking
 #endif
 
 constexpr int kD = 256;            // d_model (encoder_hidden / decoder_hidden)
@@ -81,16 +85,15 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   constexpr int F = NCH * kChunk;
   constexpr int B1_OFF = H_OFF + BM * 512;
   constexpr int ZERO_OFF = B1_OFF + F * 4;
-  constexpr int EPI_LD = 256 + 4;
-  constexpr int SMEM0 = ZERO_OFF + 16;
-  constexpr int SMEM = SMEM0 > BM * EPI_LD * 4 ? SMEM0 : BM * EPI_LD * 4;
+  constexpr int RED_OFF = ZERO_OFF + 16;            // LN row statistics: [BM rows][4 waves] f32
+  constexpr int SMEM = RED_OFF + BM * 16;
   static_assert(SMEM <= 163840, "LDS");
   constexpr int NK1 = KS * (kD / 32);  // GEMM1 units per chunk (tap-major, 8 k-steps per tap)
   constexpr int NK2 = kChunk / 32;     // GEMM2 units per chunk
   constexpr int NU = NK1 + NK2;
   constexpr int DEPTH = kDepth;
   static_assert(NK1 % DEPTH == 0 && NK2 % DEPTH == 0, "static register-ring slots");
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + (FFN_TRACE ? 256 : 0)];
 
   const ConvArgs &a = p.e;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b128(wr, lane_off + jb * 1024, so, 0);
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(wr, lane_off + jb * 1024, (FFN_ABLATE & 8) ? 0u : so, 0);
       pa[s][jb] = __builtin_bit_cast(bf16x8, v);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -188,17 +191,27 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   const int hi = lane >> 4;
   bf16x8 f0[MB], f1[MB];
   // GEMM1 unit (tap, k-step ks): x rows shifted by the tap; a 16-row block step keeps (row & 7)
-  auto read_x = [&](int tap, int ks, bf16x8 (&f)[MB]) {
-    if (FFN_ABLATE & 4) return;
-    const bool all_ok = ((need_mask >> tap) & 1u) == 0;
+  // LDS addresses of GEMM1 unit (tap, ks)'s fragments (computed a unit before the reads issue)
+  auto addr_x = [&](int tap, int ks, int (&ad)[MB]) {
+    const bool all_ok = (FFN_ABLATE & 16) || ((need_mask >> tap) & 1u) == 0;
     const int sh = tap - pad;
     const int r = hrow0 + tap;
     const int base = X_OFF + r * 512 + (xchunk(r, 4 * ks + hi) << 4);
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       const bool ok = all_ok || (unsigned)(tpos[mb] + sh) < (unsigned)tlen[mb];
-      f[mb] = *reinterpret_cast<const bf16x8 *>(smem + (ok ? base + mb * 8192 : ZERO_OFF));
+      ad[mb] = ok ? base + mb * 8192 : ZERO_OFF;
     }
+  };
+  auto issue_x = [&](const int (&ad)[MB], bf16x8 (&f)[MB]) {
+    if (FFN_ABLATE & 4) return;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) f[mb] = *reinterpret_cast<const bf16x8 *>(smem + ad[mb]);
+  };
+  auto read_x = [&](int tap, int ks, bf16x8 (&f)[MB]) {
+    int ad[MB];
+    addr_x(tap, ks, ad);
+    issue_x(ad, f);
   };
   // GEMM2 unit q (32 hidden columns of the chunk)
   auto read_h = [&](int q, bf16x8 (&f)[MB]) {
@@ -229,6 +242,16 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
+  // trace builds: wave 0 stamps the shader clock into an LDS slot past the kernel's own LDS
+  auto stamp = [&](int i) {
+    if (FFN_TRACE) {
+      __builtin_amdgcn_sched_barrier(0);
+      const uint64_t t = __builtin_readcyclecounter();
+      if (tid == 0) *reinterpret_cast<uint64_t *>(smem + SMEM + 8 * i) = t;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  stamp(0);
 
   // chunk c's hidden slice: H[m][j] = bf16(relu(acc1 + b1)); lane holds 4 consecutive j of row m
   auto write_h = [&](int c) {
@@ -257,6 +280,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * DEPTH) : "memory");
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   bar();
+  stamp(1);
   read_x(0, 0, f0);
 
   // One GEMM1 unit k = g * DEPTH + s (ring slot s): read the next unit's B fragments (LDS latency
@@ -285,10 +309,12 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
 #pragma nounroll
     for (int g = 0; g < NK1 / DEPTH; ++g) static_for<DEPTH>([&](auto S) { unit1(S, c, g); });
     // every wave is past its GEMM2 reads of the previous chunk's H: overwrite it; then H visible
+    stamp(2 + 2 * c);
     bar();
     write_h(c);
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     bar();
+    stamp(3 + 2 * c);
     read_h(0, f0);
     const uint32_t next1 = c + 1 < NCH ? base1(c + 1) : 0u;  // past the last unit: harmless reloads
     static_for<NK2>([&](auto Q) {
@@ -311,18 +337,141 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     });
   }
 
-  // ---- LN epilogue: Y^T accumulators -> E[m][n] f32 -> conv_common.h epilogue (RES_LN)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // ---- LN epilogue straight from the Y^T accumulators (Layers.py:28 residual + LayerNorm, the
+  // padding mask, the speaker / emotion adds). Lane (wave w, lane l) holds rows mb*16 + (l & 15),
+  // columns 64w + 16nb + 4(l >> 4) + i; a row's 256 values live in 4 lanes of each of the 4 waves:
+  // partial sums over the lane's 16 values, a butterfly over l >> 4, then the 4 waves' partials
+  // through LDS. The residual x rows are still in the LDS x tile; the bf16 result is staged in
+  // the H region and written out as whole 512-byte rows.
+  stamp(2 + 2 * NCH);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the harmless past-the-end weight loads
   __builtin_amdgcn_s_waitcnt(kLgkm0);
-  bar();  // every wave is past its last LDS read: E may overwrite the x tile / H
-  float *E = reinterpret_cast<float *>(smem);
+  stamp(4 + 2 * NCH);
+  {
+    float *red = reinterpret_cast<float *>(smem + RED_OFF);
+    const float inv_n = 1.0f / 256.0f;
+    float4 b2v[4], gv[4], bev[4];
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb)
+    for (int nb = 0; nb < 4; ++nb) {
+      const int n = w * 64 + nb * 16 + 4 * hi;
+      b2v[nb] = *reinterpret_cast<const float4 *>(a.bias + n);
+      gv[nb] = *reinterpret_cast<const float4 *>(a.gamma + n);
+      bev[nb] = *reinterpret_cast<const float4 *>(a.beta + n);
+    }
+    // v = acc + b2 + x (into acc2), row partial sums
+    float part[MB];
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
-      *reinterpret_cast<f32x4 *>(E + (hrow0 + mb * 16) * EPI_LD + w * 64 + nb * 16 + 4 * hi) = acc2[nb][mb];
-  __syncthreads();
-  epilogue<BM, 256, 4, true>(a, E, m0, 0, tid, M);
+    for (int mb = 0; mb < MB; ++mb) {
+      const int xr = mb * 16 + hrow0 + pad;  // the row's own x in the tile
+      float sum = 0.f;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int n = w * 64 + nb * 16 + 4 * hi;
+        const bf16x4 xv = *reinterpret_cast<const bf16x4 *>(smem + X_OFF + xr * 512 + (xchunk(xr, n >> 3) << 4) + (n & 7) * 2);
+        f32x4 v = acc2[nb][mb];
+        v[0] = v[0] + b2v[nb].x + (float)xv[0];
+        v[1] = v[1] + b2v[nb].y + (float)xv[1];
+        v[2] = v[2] + b2v[nb].z + (float)xv[2];
+        v[3] = v[3] + b2v[nb].w + (float)xv[3];
+        acc2[nb][mb] = v;
+        sum += (v[0] + v[1]) + (v[2] + v[3]);
+      }
+      part[mb] = sum;
+    }
+    // row statistic: 4 lanes (l >> 4) per wave, then the 4 waves through LDS
+    auto row_reduce = [&](float (&pv)[MB], float (&tot)[MB]) {
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        float v = pv[mb];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (hi == 0) red[(mb * 16 + hrow0) * 4 + w] = v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        const float4 r = *reinterpret_cast<const float4 *>(red + (mb * 16 + hrow0) * 4);
+        tot[mb] = (r.x + r.y) + (r.z + r.w);
+      }
+      __syncthreads();  // red is reused by the next statistic
+    };
+    float mean[MB], var[MB];
+    row_reduce(part, mean);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      mean[mb] *= inv_n;
+      float ss = 0.f;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        f32x4 d = acc2[nb][mb];
+        d[0] -= mean[mb];
+        d[1] -= mean[mb];
+        d[2] -= mean[mb];
+        d[3] -= mean[mb];
+        acc2[nb][mb] = d;
+        ss += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+      }
+      part[mb] = ss;
+    }
+    row_reduce(part, var);
+    // y = d * rstd * gamma + beta; padded rows: mask, then + addvec (FastSpeech2.forward adds the
+    // speaker / emotion vectors to every frame); bf16 into the H region (free since GEMM2 ended)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const float rstd = 1.0f / sqrtf(var[mb] * inv_n + a.eps);
+      const int m = mb * 16 + hrow0;
+      const int gm = m0 + m;
+      bool masked = false;
+      int bb = 0;
+      if (a.lens != nullptr || a.av1 != nullptr) {  // padded rows only (host-checked)
+        bb = gm / T;
+        masked = a.lens != nullptr && (int64_t)(gm - bb * T) >= a.lens[bb];
+      }
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int n = w * 64 + nb * 16 + 4 * hi;
+        const f32x4 d = acc2[nb][mb];
+        float y[4] = {d[0] * rstd * gv[nb].x + bev[nb].x, d[1] * rstd * gv[nb].y + bev[nb].y,
+                      d[2] * rstd * gv[nb].z + bev[nb].z, d[3] * rstd * gv[nb].w + bev[nb].w};
+        if (masked) y[0] = y[1] = y[2] = y[3] = 0.f;
+        if (a.av1 != nullptr) {
+          const float4 v1 = *reinterpret_cast<const float4 *>(a.av1 + (int64_t)bb * kD + n);
+          y[0] += v1.x; y[1] += v1.y; y[2] += v1.z; y[3] += v1.w;
+        }
+        if (a.av2 != nullptr) {
+          const float4 v2 = *reinterpret_cast<const float4 *>(a.av2 + (int64_t)bb * kD + n);
+          y[0] += v2.x; y[1] += v2.y; y[2] += v2.z; y[3] += v2.w;
+        }
+        bf16x4 o;
+        o[0] = (bf16)y[0];
+        o[1] = (bf16)y[1];
+        o[2] = (bf16)y[2];
+        o[3] = (bf16)y[3];
+        *reinterpret_cast<bf16x4 *>(smem + H_OFF + m * 512 + (xchunk(m, n >> 3) << 4) + (n & 7) * 2) = o;
+      }
+    }
+    __syncthreads();
+    // whole rows out: 16-byte chunks, 32 per row
+    const uint32_t orow = (uint32_t)a.os * 2u;
+    char *ob = static_cast<char *>(a.out);
+#pragma unroll 2
+    for (int i = tid; i < BM * 32; i += 256) {
+      const int m = i >> 5, ch = i & 31;
+      if (m0 + m < M)
+        *reinterpret_cast<uint4 *>(ob + (size_t)(m0 + m) * orow + ch * 16) =
+            *reinterpret_cast<const uint4 *>(smem + H_OFF + m * 512 + (xchunk(m, ch) << 4));
+    }
+  }
+  stamp(5 + 2 * NCH);
+  if (FFN_TRACE) {
+    stamp(3 + 2 * NCH);
+    __syncthreads();
+    if (tid == 0) {  // trace build: the stamps go to output row a.M - 1 - block (packed capacity tail)
+      uint64_t *o = reinterpret_cast<uint64_t *>(static_cast<char *>(a.out) + (size_t)(a.M - 1 - blockIdx.x) * a.os * 2);
+      for (int i = 0; i < 6 + 2 * NCH; ++i) o[i] = *reinterpret_cast<const uint64_t *>(smem + SMEM + 8 * i);
+      o[31] = (uint64_t)(6 + 2 * NCH);
+    }
+  }
 }
 
 }  // namespace
@@ -380,6 +529,9 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   a.row_pos = reinterpret_cast<const int2 *>(d->row_pos);
   a.out_scale = 1.0f;
   a.ln_pairs = 1;
+#ifdef FFN_EPI_DBG
+  a.dbg = FFN_EPI_DBG;  // analysis builds: conv_common.h epilogue ablation bits
+#endif
   a.x_bytes = (uint32_t)xb;
   a.w_bytes = (uint32_t)wb;
   p.w = reinterpret_cast<const bf16 *>(d->w);

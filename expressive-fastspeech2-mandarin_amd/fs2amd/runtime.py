@@ -146,8 +146,8 @@ def ffn_fused_ok(P, lp, h, layout):
     """fs2_ffn covers bf16 FFNs with d_model 256, kernel-1 w_2 and a hidden width of whole 256-column
     chunks; it pays where the launch has enough 112-row tiles to fill the chip (the decoder: cfg2
     24.9k packed rows; the 4k-row encoder keeps the two fs2_conv1d launches). FS2_FFN_FUSED=0: off
-    (A/B), =2: on at every size (tests)."""
-    mode = os.environ.get("FS2_FFN_FUSED", "0")
+    (A/B), =2: on at every size (tests); default 1."""
+    mode = os.environ.get("FS2_FFN_FUSED", "1")
     if mode == "0" or P.compute != L.FS2_BF16 or h.dtype != torch.bfloat16 or getattr(lp, "w12", None) is None:
         return False
     rows = layout.capacity if layout is not None else h.shape[0] * h.shape[1]

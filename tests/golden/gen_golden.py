@@ -78,7 +78,7 @@ def index_map(LR, duration, max_len):
     return (out[..., 0].round().to(torch.int64) - 1).numpy().astype(np.int32), mel_len.numpy()
 
 
-def run_case(model, LR, name, args, controls=(1.0, 1.0, 1.0), save_full=True):
+def run_case(model, LR, name, args, controls=(1.0, 1.0, 1.0), save_full=True, head=0, frames=()):
     p_c, e_c, d_c = controls
     with torch.no_grad():
         outs = model(**args, p_control=p_c, e_control=e_c, d_control=d_c)
@@ -106,6 +106,11 @@ def run_case(model, LR, name, args, controls=(1.0, 1.0, 1.0), save_full=True):
         for k in ("p_pred", "e_pred", "log_d", "d_rounded", "mel_lens_out", "src_masks", "mel_masks"):
             rec["out_" + k] = t2n(outs[OUT_NAMES.index(k)])
         rec["out_shape_mel"] = np.array(outs[0].shape)
+    if head:  # the full outputs of the first `head` utterances
+        rec["out_mel_head"] = t2n(outs[0][:head])
+        rec["out_postnet_mel_head"] = t2n(outs[1][:head])
+    for a, b in frames:  # frame slices of every utterance
+        rec[f"out_postnet_mel_f{a}_{b}"] = t2n(outs[1][:, a:b])
     path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **rec)
     print(f"{name}: {os.path.getsize(path) / 1e3:.1f} kB  mel {tuple(outs[0].shape)}")
@@ -135,7 +140,7 @@ def lr_cases(LR):
     print("lr_cases:", list(cases))
 
 
-def train_case(FastSpeech2, pc, mc, sd, name="train_grads", shape=(4, 10, 24), seed=11):
+def train_case(FastSpeech2, pc, mc, sd, name="train_grads", shape=(4, 10, 24), seed=11, d_range=(2, 10)):
     """One reference training step's gradients (train mode: BatchNorm batch statistics, decoder
     crop to max_seq_len), with every dropout disabled so the step is deterministic: nn.Dropout
     modules get p = 0 and the PostNet's hard-coded F.dropout(0.5) (transformer/Layers.py:133-134)
@@ -150,7 +155,7 @@ def train_case(FastSpeech2, pc, mc, sd, name="train_grads", shape=(4, 10, 24), s
     for mod in m.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.p = 0.0
-    args = synth_batch(*shape, seed=seed, with_mels=True, pe_targets=True)
+    args = synth_batch(*shape, seed=seed, with_mels=True, pe_targets=True, d_range=d_range)
     orig = F.dropout
     F.dropout = lambda x, p=0.5, training=False, inplace=False: x
     try:
@@ -179,6 +184,86 @@ def train_case(FastSpeech2, pc, mc, sd, name="train_grads", shape=(4, 10, 24), s
     path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **rec)
     print(f"{name}: {os.path.getsize(path) / 1e3:.1f} kB, {len(keys)} grads, losses {rec['losses']}")
+
+
+def tiny_model_config(mc):
+    """The reference architecture at toy width (checkpoint fixture): 1 encoder / 1 decoder FFT
+    block of width 16, FFN 32, VariancePredictor width 16. The PostNet keeps its fixed shape
+    (transformer/Layers.py PostNet defaults, 80 -> 512 x 5)."""
+    t = dict(mc["transformer"], encoder_layer=1, decoder_layer=1, encoder_hidden=16, decoder_hidden=16,
+             conv_filter_size=32)
+    return dict(mc, transformer=t, variance_predictor=dict(mc["variance_predictor"], filter_size=16))
+
+
+def ckpt_case(FastSpeech2, pc, mc):
+    """A checkpoint written by the reference's own train loop (train.py:82-97 step, :151-161
+    torch.save of {"model", "optimizer"}) after 2 steps of the reference ScheduledOptim
+    (model/optimizer.py: non-fused Adam, numpy-float learning rates) at the toy width of
+    tiny_model_config; then the reference's step 3: its clipped gradients, the learning rate and
+    every parameter after the update. The PostNet is zero and frozen (no gradient, no Adam state:
+    its 4.3 M zeros compress away) so the fixture stays small; every other parameter trains.
+    Dropout disabled as in train_case."""
+    import torch.nn.functional as F
+    from model import ScheduledOptim as RefOptim
+    from model.loss import FastSpeech2Loss
+    from fs2amd.data import loss_inputs
+
+    mct = tiny_model_config(mc)
+    tc = C.ESD_TRAIN_CONFIG
+    m = FastSpeech2(pc, mct)
+    fill_module(m, seed=5)
+    for p in m.postnet.parameters():
+        p.data.zero_()
+        p.requires_grad_(False)
+    m.train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    opt = RefOptim(m, tc, mct, 0)
+    loss_fn = FastSpeech2Loss(pc, mct)
+    orig = F.dropout
+    F.dropout = lambda x, p=0.5, training=False, inplace=False: x
+
+    def step(i, record=False):
+        args = synth_batch(2, 8, 12, seed=40 + i, with_mels=True, pe_targets=True)
+        out = m(**args)
+        losses = loss_fn(loss_inputs(args), out)
+        losses[0].backward()
+        torch.nn.utils.clip_grad_norm_(m.parameters(), tc["optimizer"]["grad_clip_thresh"])
+        grads = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None} if record else None
+        opt.step_and_update_lr()
+        opt.zero_grad()
+        return grads, losses
+
+    try:
+        step(1)
+        step(2)
+        d = os.path.join(HERE, "ref_ckpt")
+        os.makedirs(d, exist_ok=True)
+        raw = os.path.join(d, "2.pth.tar")
+        torch.save({"model": m.state_dict(), "optimizer": opt._optimizer.state_dict()}, raw)
+        # committed gzip-compressed (the zero PostNet is 17 MB of the file); the test restores the
+        # exact bytes the reference wrote
+        import gzip
+        import shutil
+        with open(raw, "rb") as fi, gzip.open(raw + ".gz", "wb", compresslevel=9) as fo:
+            shutil.copyfileobj(fi, fo)
+        os.remove(raw)
+        with open(os.path.join(d, "model_config.json"), "w") as f:
+            json.dump(mct, f, indent=1, sort_keys=True)
+        grads, losses = step(3, record=True)
+    finally:
+        F.dropout = orig
+    keys = sorted(grads)
+    params = dict(m.named_parameters())
+    rec = {"keys": np.array(keys), "lr": np.array(float(opt._optimizer.param_groups[0]["lr"])),
+           "current_step": np.array(opt.current_step), "losses": np.array([float(l.detach()) for l in losses])}
+    for i, k in enumerate(keys):
+        rec[f"g_{i}"] = t2n(grads[k])
+        rec[f"p_{i}"] = t2n(params[k])
+    np.savez_compressed(os.path.join(HERE, "ref_ckpt_next.npz"), **rec)
+    print(f"ref_ckpt: 2.pth.tar.gz {os.path.getsize(raw + '.gz') / 1e3:.0f} kB, {len(keys)} trained "
+          f"params, step-3 lr {rec['lr']}")
 
 
 def sub_batch(batch, rows, L=None, T=None):
@@ -327,6 +412,25 @@ def main(only=None, only2=None):
         return
     if only == "vocoder":
         vocoder_case()
+        return
+    if only == "round3":  # round-3 additions (earlier fixtures stay byte-identical)
+        if only2 in (None, "targets"):
+            # teacher-forced durations AND pitch / energy targets at the bench shapes: no bucket of
+            # the bf16 path can flip, so bf16 is checked against the reference at full size
+            run_case(model, LR, "cfg2_targets", synth_batch(64, 64, seed=1, pe_targets=True), save_full=False, head=4)
+            run_case(model, LR, "cfg4_targets", synth_batch(256, 16, 160, seed=1, pe_targets=True), save_full=False,
+                     head=2)
+        if only2 in (None, "long"):
+            # eval with 2004 phonemes / 2004 frames > max_seq_len 2000: both PE recompute branches
+            # (transformer/Models.py:82-87 encoder, :145-152 decoder)
+            run_case(model, LR, "long_eval", synth_batch(1, 2004, seed=8, d_range=(1, 1), pe_targets=True),
+                     save_full=False, frames=((0, 32), (1960, 2004)))
+        if only2 in (None, "crop"):
+            # train mode with mel lengths > max_seq_len: the decoder crops to 2000 frames
+            # (Models.py:154-162) and FastSpeech2Loss crops the targets to the mask (loss.py:33-36)
+            train_case(FastSpeech2, pc, mc, sd, name="train_crop", shape=(2, 200, 230), seed=13, d_range=(9, 10))
+        if only2 in (None, "ckpt"):
+            ckpt_case(FastSpeech2, pc, mc)
         return
     if only == "round2":  # round-2 additions (the round-1 fixtures above stay byte-identical)
         if only2 != "train16":

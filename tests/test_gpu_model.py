@@ -251,3 +251,76 @@ def test_cfg4_variable_length_fp32_checksums(model):
     ck = _checksums(got)
     np.testing.assert_allclose(ck["ck_mel_valid_sum"][keep], z["ck_mel_valid_sum"][keep], rtol=0, atol=1.0)
     np.testing.assert_allclose(ck["ck_post_sq"][keep], z["ck_post_sq"][keep], rtol=2e-5)
+
+
+# ---- round-3 fixtures: pitch / energy TARGETS at the bench shapes (no bucket can flip), so the
+# bf16 perf path is checked against the reference itself at full size; the eval PE-recompute
+# branch (> max_seq_len positions)
+def _valid_err(got_post, ref_post, ml):
+    T = ref_post.shape[1]
+    valid = (np.arange(T)[None, :] < ml[:, None])[..., None]
+    e = np.abs(got_post - ref_post) * valid
+    return float(e.max()), float(e.sum() / (valid.sum() * ref_post.shape[2]))
+
+
+@pytest.mark.parametrize("case,head", [("cfg2_targets", 4), ("cfg4_targets", 2)])
+def test_targets_fp32_vs_reference(model, case, head):
+    """fp32 at the bench shapes (cfg2 64 x 64, cfg4 256 x U{16..160}) with teacher-forced
+    durations and pitch / energy targets: the first utterances element-wise (2e-3, the fp32
+    tolerance), every utterance's checksums as test_cfg2_fp32_checksums, discrete outputs exact."""
+    args, controls, outs, z = load_case(case)
+    got = _run(model, args, controls, "fp32")
+    assert tuple(got[0].shape) == tuple(z["out_shape_mel"])
+    ml = _np(got[9])
+    np.testing.assert_array_equal(ml, outs["mel_lens_out"])
+    mx, _ = _valid_err(_np(got[1][:head]), outs["postnet_mel_head"], ml[:head])
+    assert mx <= 2e-3, mx
+    ck = _checksums(got)
+    for k in ("ck_mel_valid_sum", "ck_post_valid_sum", "ck_post_all_sum"):
+        np.testing.assert_allclose(ck[k], z[k], rtol=0, atol=0.5, err_msg=k)
+    for k in ("ck_post_valid_abs", "ck_post_sq"):
+        np.testing.assert_allclose(ck[k], z[k], rtol=1e-5, err_msg=k)
+    np.testing.assert_array_equal(_np(got[6]), outs["src_masks"])
+    np.testing.assert_array_equal(_np(got[7]), outs["mel_masks"])
+
+
+# bf16 perf path against the reference at the bench shapes (targets pinned: no discrete decision
+# differs). Measured round 3: see the prints; bounds are the small-case bf16 tolerance (0.15 max,
+# 0.02 mean) and per-utterance |postnet| checksums within 1 %.
+@pytest.mark.parametrize("case,head", [("cfg2_targets", 4), ("cfg4_targets", 2)])
+def test_targets_bf16_vs_reference(model, case, head):
+    args, controls, outs, z = load_case(case)
+    got = _run(model, args, controls, "bf16")
+    ml = _np(got[9])
+    np.testing.assert_array_equal(ml, outs["mel_lens_out"])
+    mx, mean = _valid_err(_np(got[1][:head]), outs["postnet_mel_head"], ml[:head])
+    ck = _checksums(got)
+    rel_abs = np.abs(ck["ck_post_valid_abs"] - z["ck_post_valid_abs"]) / z["ck_post_valid_abs"]
+    n_valid = ml.astype(np.float64) * 80
+    mean_sum_err = np.abs(ck["ck_post_valid_sum"] - z["ck_post_valid_sum"]) / n_valid
+    print(f"{case} bf16 vs reference: head max {mx:.4f} mean {mean:.5f}; |post| checksum rel max "
+          f"{rel_abs.max():.2e}; per-frame-value sum error max {mean_sum_err.max():.2e}")
+    assert mx <= 0.15 and mean <= 0.02, (mx, mean)
+    assert rel_abs.max() <= 1e-2, rel_abs.max()
+    assert mean_sum_err.max() <= 0.02, mean_sum_err.max()
+
+
+def test_long_eval_pe_recompute_fp32(model):
+    """Eval with 2004 phonemes and 2004 frames, past max_seq_len = 2000: the encoder and the
+    decoder recompute the sinusoid table for the sequence length (transformer/Models.py:82-87,
+    145-152) instead of slicing the 2001-row one. Frames 0-31 and 1960-2003 element-wise (2e-3),
+    checksums, exact lengths / masks."""
+    args, controls, outs, z = load_case("long_eval")
+    assert args["texts"].shape[1] == 2004 and args["max_mel_len"] == 2004
+    got = _run(model, args, controls, "fp32")
+    assert tuple(got[0].shape) == (1, 2004, 80)
+    post = _np(got[1])
+    for a, b in ((0, 32), (1960, 2004)):
+        e = float(np.abs(post[:, a:b] - z[f"out_postnet_mel_f{a}_{b}"]).max())
+        assert e <= 2e-3, (a, b, e)
+    ck = _checksums(got)
+    for k in ("ck_mel_valid_sum", "ck_post_valid_sum", "ck_post_all_sum"):
+        np.testing.assert_allclose(ck[k], z[k], rtol=0, atol=0.5, err_msg=k)
+    np.testing.assert_allclose(ck["ck_post_sq"], z["ck_post_sq"], rtol=1e-5)
+    np.testing.assert_array_equal(_np(got[9]), outs["mel_lens_out"])
+    np.testing.assert_array_equal(_np(got[7]), outs["mel_masks"])

@@ -42,9 +42,11 @@ def gpu():
         pytest.skip("no ROCm device")
 
 
-@pytest.mark.parametrize("case", ["train_grads", "train_b16"])
+@pytest.mark.parametrize("case", ["train_grads", "train_b16", "train_crop"])
 def test_train_step_fp32_matches_reference_gradients(gpu, case):
-    """train_grads: B=4; train_b16: the cfg3 per-GPU shape (B=16, lengths U{16..64})."""
+    """train_grads: B=4; train_b16: the cfg3 per-GPU shape (B=16, lengths U{16..64}); train_crop:
+    B=2 with mel lengths past max_seq_len = 2000 (train mode: the decoder crops to 2000 frames,
+    transformer/Models.py:154-162, and FastSpeech2Loss crops the targets to the mask)."""
     z, m, losses, out = _step("fp32", case)
     np.testing.assert_allclose([float(l) for l in losses], z["losses"], rtol=1e-4)
     np.testing.assert_array_equal(out[9].cpu().numpy(), z["out_mel_lens"])

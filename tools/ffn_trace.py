@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Phase timing inside the fused FFN from a trace build (FS2_LIB=abl/libfs2hip_trace.so, ffn.hip
+under -DFFN_TRACE=1): wave 0 of every workgroup stamps the shader clock at kernel start, after
+the prologue, around each chunk's H hand-off, before and after the LN epilogue; the stamps
+go to the packed buffer's spare tail rows. Prints per-phase mean / max cycles over workgroups."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "expressive-fastspeech2-mandarin_amd"))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+
+
+def main():
+    import bench
+    from fs2amd import ops
+    from fs2amd.data import synth_batch, to_device
+
+    dev = torch.device("cuda:0")
+    model, _, _ = bench.build_model(dev, "bf16")
+    bc = synth_batch(64, 64, seed=1)
+    b = to_device(bc, dev)
+    P = model.packed(dev)
+    B, T = 64, int(bc["max_mel_len"])
+    lp = P.dec_layers[0]
+    lay = ops.SeqLayout(b["mel_lens"], T)
+    h = torch.randn(B * T, 256, generator=torch.Generator().manual_seed(0)).to(dev, torch.bfloat16)
+    out = torch.empty_like(h)
+    for _ in range(3):
+        ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=9, pad=4, ln=lp.ln2, layout=lay, out=out)
+    torch.cuda.synchronize()
+    R = int(lay.cu[-1])
+    nwg = (R + 111) // 112
+    assert B * T - nwg >= R, "no spare capacity rows for the stamps"
+    st = out.view(torch.int64).reshape(B * T, -1)[B * T - nwg:].flip(0)[:, :32].cpu()
+    print("raw wg0:", st[0, :13].tolist())
+    n = int(st[0, 31])
+    t = st[:, :n].double()
+    t0 = t[:, 0].min()
+    names = ["prologue"] + [f"c{c}:{p}" for c in range(4) for p in ("gemm1", "h_handoff", "gemm2")] + ["epilogue"]
+    # stamps: 0 start, 1 after prologue, per chunk: before write_h, after write_h; then before / after epilogue
+    edges = [0, 1]
+    for c in range(4):
+        edges += [2 + 2 * c, 3 + 2 * c]
+    edges += [10, 11]
+    print(f"workgroups {t.shape[0]}, stamps {n}; total mean {float((t[:, 11] - t[:, 0]).mean()):.0f} cycles")
+    seg = []
+    for i in range(1, 12):
+        d = t[:, i] - t[:, i - 1]
+        seg.append((i, float(d.mean()), float(d.max())))
+    labels = ["prologue"]
+    for c in range(4):
+        labels += [f"c{c} gemm1 (+prev gemm2)" if c else "c0 gemm1", f"c{c} write_h"]
+    labels += ["c3 gemm2", "epilogue (all)"]
+    for (i, mean, mx), lab in zip(seg[:10], labels):
+        print(f"{lab:28s} mean {mean:9.0f}  max {mx:9.0f} cycles")
+    # epilogue split: 10 before drain, 12 after drain + barrier, 13 after E writes, 11 end
+    for lab, i0, i1 in (("  drain vmcnt + barrier", 10, 12), ("  E writes + barrier", 12, 13), ("  LN + stores", 13, 11)):
+        d = t[:, i1] - t[:, i0]
+        print(f"{lab:28s} mean {float(d.mean()):9.0f}  max {float(d.max()):9.0f} cycles")
+
+
+if __name__ == "__main__":
+    main()
