@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--mode", default="infer", choices=["infer", "train", "selftest"],
                     help="infer: the headline cfg2 forward; train: the cfg3 train.py step (B=16/GPU, DDP); "
                          "selftest: the launcher / process-group / timing bookkeeping only (gloo, no GPU)")
+    ap.add_argument("--ddp", type=int, default=0,
+                    help="train mode: gradient all-reduce over RCCL even at one rank (world > 1 always reduces)")
     ap.add_argument("--backend", default=None, choices=[None, "nccl", "gloo"],
                     help="process-group backend (default: nccl = RCCL; selftest: gloo)")
     return ap.parse_args()
@@ -348,7 +350,13 @@ def main_train(args, rank, world, device):
     batch_cpu = synth_batch(B, 16, 64, seed=1 + rank, with_mels=True, pe_targets=True)
     batch = to_device(batch_cpu, device)
     frames = int(batch_cpu["mel_lens"].sum())
-    step = TrainStep(model, pc, mc, tc, device=device, world_size=world, graph=bool(args.graph))
+    if args.ddp and world == 1 and not torch.distributed.is_initialized():
+        # a single-rank RCCL group, so the step's all-reduce path runs (and is timed) on one GPU
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        torch.distributed.init_process_group("nccl", init_method="env://", rank=0, world_size=1)
+    step = TrainStep(model, pc, mc, tc, device=device, world_size=world, graph=bool(args.graph),
+                     ddp=bool(args.ddp) or world > 1)
     for _ in range(max(1, args.warmup)):
         step(batch)
     torch.cuda.synchronize(device)
@@ -448,8 +456,9 @@ def extra_workloads(model, args, rank, device):
         res[name] = {"value": round(fr * steps / el, 1), "unit": "mel-frames/s", "ms_per_step": round(el / steps * 1e3, 4),
                      "steps": steps, "frames_per_step": fr, "hip_graph": graph, "dtype": model.precision, "note": note}
 
-    record("free_running_cfg2", synth_batch(args.batch, args.phonemes, seed=1 + rank, teacher=False), False,
-           "durations predicted + rounded (modules.py:131-137), one D2H read of max(mel_len), eager")
+    record("free_running_cfg2_eager", synth_batch(args.batch, args.phonemes, seed=1 + rank, teacher=False), False,
+           "durations predicted + rounded (modules.py:131-137), one D2H read of max(mel_len), eager launches")
+    res["free_running_cfg2"] = synth_graphs_workload(model, args, rank, device, steps)
     record("cfg4_b256", synth_batch(256, 16, 160, seed=1 + rank), True,
            "B=256 x U{16..160} phonemes, teacher-forced durations U{2..10}")
     if prec == "bf16":
@@ -462,6 +471,36 @@ def extra_workloads(model, args, rank, device):
     if args.vocoder:
         res["vocoder_cfg2"] = vocoder_workload(model, args, rank, device, steps)
     return res
+
+
+def synth_graphs_workload(model, args, rank, device, steps):
+    """The synthesis path (free-running cfg2: predicted durations, no max_mel_len) through
+    fs2amd.graphs.SynthGraphs: stage-1 graph, the one host read of max(mel_len), stage-2 graph
+    (captured on the first call for this T_out; warm-up). Each timed step is a whole synthesis
+    call including its host read, as a serving loop runs it."""
+    from fs2amd import parallel
+    from fs2amd.data import synth_batch, to_device
+    from fs2amd.graphs import SynthGraphs
+
+    b = to_device(synth_batch(args.batch, args.phonemes, seed=1 + rank, teacher=False), device)
+    synth = SynthGraphs(model)
+    for _ in range(2):
+        out = synth(**b)
+    torch.cuda.synchronize(device)
+    frames = int(out[9].sum())
+    parallel.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        synth(**b)
+    torch.cuda.synchronize(device)
+    parallel.barrier()
+    el, fr = parallel.aggregate(time.perf_counter() - t0, frames, device)
+    return {"value": round(fr * steps / el, 1), "unit": "mel-frames/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "steps": steps, "frames_per_step": fr, "hip_graph": True, "dtype": model.precision,
+            "graphs_captured": synth.captures,
+            "note": "durations predicted + rounded (modules.py:131-137); fs2amd.graphs.SynthGraphs: stage-1 graph, "
+                    "ONE device->host read (max(mel_len) + bad-id count), stage-2 graph keyed by T_out"}
 
 
 def vocoder_workload(model, args, rank, device, steps):

@@ -1,0 +1,129 @@
+"""Free-running synthesis as two captured HIP graphs around its one host read.
+
+The synthesis call of synthesize_chinese_pinyin.py:140-145 is an eval forward with predicted
+durations: the decoder length T_out = max(mel_len) is known only after the duration predictor
+has run, so the path has one device->host read (runtime.host_meta) and cannot be ONE graph.
+:class:`SynthGraphs` captures the two halves:
+
+* stage 1 (keyed by B, L_max and the control values): token embedding + PE, the encoder, the
+  variance adaptor and the LengthRegulator scan (duration rounding, cumulative frames, mel_len),
+  plus the two-int32 meta vector [max(mel_len), out-of-vocabulary count];
+* the host reads the meta vector (one sync), raises IndexError on bad ids;
+* stage 2 (keyed by stage 1's key and T_out; an LRU of ``max_stage2`` graphs): the
+  LengthRegulator gather + PE, the decoder, mel_linear, the PostNet and the mel mask.
+
+Each entry keeps the weight pack it was captured against (model.packed): when the weights change the
+pack is rebuilt, and the stale graphs are dropped and recaptured on the next call. Each call
+copies the batch into stage 1's static inputs and replays; the returned 10-tuple is
+the reference's (fastspeech2.py:138-148), freshly allocated (clones of the graphs' outputs).
+Graph replay replaces ~100 kernel launches and the host bubbles around the read; numerics are
+those of the eager path (same kernels, same order).
+"""
+from collections import OrderedDict
+from types import SimpleNamespace
+
+import torch
+
+from . import ops
+from . import runtime as R
+
+
+class SynthGraphs:
+    def __init__(self, model, max_stage2=8):
+        self.model = model
+        self.max_stage2 = max_stage2
+        self._g1 = {}
+        self._g2 = OrderedDict()
+        self.captures = 0
+
+    @staticmethod
+    def _inputs(dev, speakers, emotions, arousals, valences, texts, src_lens, p_targets, e_targets):
+        i64 = lambda t: None if t is None else torch.as_tensor(t).to(device=dev, dtype=torch.int64).contiguous()
+        f32 = lambda t: None if t is None else t.to(device=dev, dtype=torch.float32).contiguous()
+        return dict(speakers=i64(speakers), emotions=i64(emotions), arousals=i64(arousals), valences=i64(valences),
+                    texts=i64(texts), src_lens=i64(src_lens), p_targets=f32(p_targets), e_targets=f32(e_targets))
+
+    def _stage1_body(self, P, va, s, Lx, controls):
+        p_c, e_c, d_c = controls
+        g = SimpleNamespace(speakers=s["speakers"], emotions=s["emotions"], arousals=s["arousals"],
+                            valences=s["valences"], texts=s["texts"], lens_src=s["src_lens"], Lx=Lx,
+                            p_targets=s["p_targets"], e_targets=s["e_targets"], d_targets=None, mel_lens=None)
+        st = R._stage1(P, va, g, p_c, d_c)
+        c = ops.bad_id_counter(s["texts"].device)
+        meta = torch.cat([st.mel_len.max().to(torch.int32).reshape(1), c])
+        return g, st, R._mask(s["src_lens"], Lx), meta
+
+    def _capture(self, fn):
+        """Warm fn up on a side stream (allocates per-stream workspaces outside the capture), then
+        capture it there; returns (graph, outputs)."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            fn()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            out = fn()
+        self.captures += 1
+        return graph, out
+
+    def __call__(self, speakers, emotions, arousals, valences, texts, src_lens, max_src_len, p_targets=None,
+                 e_targets=None, p_control=1.0, e_control=1.0, d_control=1.0):
+        model = self.model
+        dev = texts.device
+        if dev.type != "cuda" or model.training:
+            raise RuntimeError("SynthGraphs: eval-mode synthesis on a ROCm device")
+        P = model.packed(dev)
+        va = model.variance_adaptor
+        B, Lx = texts.shape[0], int(max_src_len)
+        if texts.shape[1] != Lx or B == 0:
+            raise RuntimeError(f"SynthGraphs: texts {tuple(texts.shape)} vs max_src_len {Lx}")
+        controls = (float(p_control), float(e_control), float(d_control))
+        x = self._inputs(dev, speakers, emotions, arousals, valences, texts, src_lens, p_targets, e_targets)
+        key1 = (model._precision, model._vp_precision, B, Lx, controls,
+                tuple(k for k, v in x.items() if v is None))
+        ops.bad_id_counter(dev)  # allocated outside any capture
+        e1 = self._g1.get(key1)
+        if e1 is not None and e1.P is not P:
+            # the weights changed (a new pack): the graphs point at the old buffers. Drop this
+            # stage-1 graph and every stage-2 graph that reads its outputs before recapturing.
+            del self._g1[key1]
+            for k in [k for k in self._g2 if k[:-1] == key1]:
+                del self._g2[k]
+            e1 = None
+        if e1 is None:
+            static = {k: (None if v is None else v.clone()) for k, v in x.items()}
+            graph, (g, st, src_masks, meta) = self._capture(lambda: self._stage1_body(P, va, static, Lx, controls))
+            meta_host = torch.empty(meta.shape, dtype=meta.dtype, pin_memory=True)
+            e1 = self._g1[key1] = SimpleNamespace(graph=graph, static=static, g=g, st=st, src_masks=src_masks,
+                                                  meta=meta, meta_host=meta_host, P=P)
+        for k, v in x.items():
+            if v is not None:
+                e1.static[k].copy_(v, non_blocking=True)
+        e1.graph.replay()
+        # the one host read
+        e1.meta_host.copy_(e1.meta, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        R.HOST_READS[0] += 1
+        T_out, bad = int(e1.meta_host[0]), int(e1.meta_host[1])
+        if bad:
+            ops.bad_id_counter(dev).zero_()
+            raise IndexError(f"fs2amd: {bad} token id(s) outside the embedding table (their encoder rows are NaN)")
+        key2 = key1 + (T_out,)
+        e2 = self._g2.get(key2)
+        if e2 is None:
+            def body():
+                mel, post, st = R._stage2(P, e1.g, e1.st, T_out, T_out, controls[0])
+                return mel, post, R._mask(st.mel_len, T_out)
+            graph, outs = self._capture(body)
+            e2 = self._g2[key2] = SimpleNamespace(graph=graph, outs=outs)
+            while len(self._g2) > self.max_stage2:
+                self._g2.popitem(last=False)
+        else:
+            self._g2.move_to_end(key2)
+        e2.graph.replay()
+        mel, post, mel_masks = (t.clone() for t in e2.outs)
+        st = e1.st
+        return (mel, post, st.p_pred.clone(), st.e_pred.clone(), st.log_d.clone(), st.d_rounded.clone(),
+                e1.src_masks.clone(), mel_masks, src_lens.to(dev), st.mel_len.clone())

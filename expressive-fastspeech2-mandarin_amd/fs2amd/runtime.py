@@ -17,8 +17,9 @@ Mirrors model/fastspeech2.py:73-148 step by step (eval semantics, reference quir
 Every arithmetic step is a HIP kernel launched on torch.cuda.current_stream(); torch only
 allocates buffers and builds the two boolean mask tensors the 10-tuple returns. With
 ``max_mel_len`` given (teacher-forced / training-style batches) the path has no host sync;
-without it, one device->host read of max(mel_len) sizes the decoder (the reference does
-B*L_max .item() syncs in LengthRegulator.expand).
+without it, ONE device->host read (max(mel_len) and the out-of-vocabulary id count together,
+:func:`host_meta`) sizes the decoder (the reference does B*L_max .item() syncs in
+LengthRegulator.expand). fs2amd.graphs.SynthGraphs captures the two halves around that read.
 """
 import os
 from types import SimpleNamespace
@@ -421,14 +422,15 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
             fj.join(*[st.mel_len for st in sts])
             mel_len = torch.cat([st.mel_len for st in sts])
             fj.fork()
-    if max_mel_len:
-        T_out = int(max_mel_len)
+    if d_targets is None or not max_mel_len:
+        # the ONE host read of the free-running path: max(mel_len) and the out-of-vocabulary id
+        # count in one device->host copy
+        max_len = host_meta(mel_len, dev)
+        T_out = int(max_mel_len) if max_mel_len else max_len
     else:
-        # the one host read of the free-running path; out-of-vocabulary ids surface here too
-        T_out = int(mel_len.max().item()) if B else 0
-        ops.raise_if_bad_ids(dev)
+        T_out = int(max_mel_len)
     if d_targets is None:
-        mel_masks = _mask(mel_len, int(mel_len.max().item()) if B else 0)
+        mel_masks = _mask(mel_len, max_len)  # get_mask_from_lengths(mel_len): width max(mel_len)
     if mel_masks is None or mel_masks.shape[1] != T_out:
         raise RuntimeError(f"decoder mask width {None if mel_masks is None else mel_masks.shape[1]} != length-"
                            f"regulated length {T_out} (the reference fails here too: Models.py:157)")
@@ -454,6 +456,25 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     if d_targets is not None:
         d_rounded = d_targets
     return (mel, postnet_mel, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)
+
+
+HOST_READS = [0]  # device->host reads made by the forward path (tests assert one per free-running call)
+
+
+def host_meta(mel_len, dev):
+    """max(mel_len) with the fs2_embed_pe out-of-vocabulary counter in the same device->host copy;
+    IndexError (the reference's nn.Embedding error) when the counter is set."""
+    c = ops.bad_id_counter(dev)
+    parts = [mel_len.max().to(torch.int32).reshape(1) if mel_len.numel() else torch.zeros(1, dtype=torch.int32,
+                                                                                          device=dev)]
+    if c is not None:
+        parts.append(c)
+    meta = torch.cat(parts).cpu()
+    HOST_READS[0] += 1
+    if c is not None and int(meta[1]):
+        c.zero_()
+        raise IndexError(f"fs2amd: {int(meta[1])} token id(s) outside the embedding table (their encoder rows are NaN)")
+    return int(meta[0])
 
 
 def _mel_copy(P, x, bt):

@@ -124,6 +124,28 @@ def test_attention_backward_matches_autograd(gpu, compute, T, lens):
     assert float(gq[~ok].abs().max() if (~ok).any() else 0.0) == 0.0
 
 
+def _assert_params_close(pa, pb, lr_sum):
+    """Parameters after a few steps of two runs of the same training. The gradients are not
+    bit-reproducible (atomic accumulation in the embedding / attention backwards), and Adam turns a
+    roundoff-size gradient on an element whose gradient is ~0 into a full +-lr step: elementwise
+    rtol 1e-4 / atol 1e-6, except at most 16 elements of the 34.7 M that may differ by up to twice
+    the summed learning rates (a flipped step per step). A real divergence (a bucket not reduced,
+    a wrong scale) moves far more elements."""
+    nbad, worst = 0, 0.0
+    for k in pb:
+        bad = ~torch.isclose(pa[k], pb[k], rtol=1e-4, atol=1e-6)
+        nbad += int(bad.sum())
+        if bad.any():
+            worst = max(worst, float((pa[k] - pb[k]).abs()[bad].max()))
+    assert nbad <= 16 and worst <= 2 * lr_sum, (nbad, worst, lr_sum)
+
+
+def _lr_sum(tc, steps):
+    """Sum of the Noam learning rates of steps 1..steps (model/optimizer.py)."""
+    o = tc["optimizer"]
+    return sum(256 ** -0.5 * min(s ** -0.5, o["warm_up_step"] ** -1.5 * s) for s in range(1, steps + 1))
+
+
 def test_graphed_train_step_equals_eager(gpu):
     """TrainStep(graph=True): after the eager warm-up steps the captured whole-step graph (forward,
     loss, backward, clip, capturable Adam with the Noam lr in a device tensor) gives the same
@@ -157,8 +179,7 @@ def test_graphed_train_step_equals_eager(gpu):
     (le, pe, _), (lg, pg, stg) = runs
     assert stg._graph is not None, "the graph was never captured"
     np.testing.assert_allclose(lg, le, rtol=1e-5)
-    for k in pe:
-        assert torch.allclose(pg[k], pe[k], rtol=1e-4, atol=1e-6), k
+    _assert_params_close(pg, pe, _lr_sum(tc, 8))
 
 
 def test_ddp_step_over_rccl_equals_plain(gpu):
@@ -209,7 +230,6 @@ def test_ddp_step_over_rccl_equals_plain(gpu):
         lp, pp = runs[0]
         for ld, pd in runs[1:]:
             np.testing.assert_allclose(ld, lp, rtol=1e-5)
-            for k in pp:
-                assert torch.allclose(pd[k], pp[k], rtol=1e-4, atol=1e-6), k
+            _assert_params_close(pd, pp, _lr_sum(tc, 5))
     finally:
         dist.destroy_process_group()
