@@ -203,7 +203,7 @@ def _graph_mean_s(fn, device, reps):
             fn()
         torch.cuda.synchronize(device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             for _ in range(reps):
                 fn()
         g.replay()
@@ -414,7 +414,7 @@ def timed_steps(model, batch, device, steps, warmup, graph, frames_out=None):
         g = torch.cuda.CUDAGraph()
         # captured on the warm-up stream: its split-K workspace already exists, so the graph holds
         # no counter-zeroing memset (ops.splitk_workspace is per stream)
-        with torch.cuda.graph(g, stream=s):
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             out = step()
         g.replay()
         torch.cuda.synchronize(device)
@@ -536,7 +536,7 @@ def vocoder_workload(model, args, rank, device, steps):
         step()
     torch.cuda.current_stream(device).wait_stream(s)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
+    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
         step()
     g.replay()
     torch.cuda.synchronize(device)

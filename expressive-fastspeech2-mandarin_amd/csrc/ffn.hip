@@ -80,12 +80,13 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   constexpr int XROWS = BM + KS - 1;
   constexpr int XPIECES = (XROWS + 1) / 2;           // 1 KiB LDS-DMA pieces of 2 rows
   constexpr int XP_PER_WAVE = (XPIECES + 3) / 4;
-  constexpr int X_OFF = 0;
+  // the 16-byte zero slot sits at LDS offset 0: a masked fragment address is (address & 0)
+  constexpr int ZERO_OFF = 0;
+  constexpr int X_OFF = 128;
   constexpr int H_OFF = X_OFF + 4 * XP_PER_WAVE * 1024;
   constexpr int F = NCH * kChunk;
   constexpr int B1_OFF = H_OFF + BM * 512;
-  constexpr int ZERO_OFF = B1_OFF + F * 4;
-  constexpr int RED_OFF = ZERO_OFF + 16;            // LN row statistics: [BM rows][4 waves] f32
+  constexpr int RED_OFF = B1_OFF + F * 4;           // LN row statistics: [BM rows][4 waves] f32
   constexpr int SMEM = RED_OFF + BM * 16;
   static_assert(SMEM <= 163840, "LDS");
   constexpr int NK1 = KS * (kD / 32);  // GEMM1 units per chunk (tap-major, 8 k-steps per tap)
@@ -103,46 +104,34 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   if (m0 >= M) return;
   const int pad = a.pad, T = a.T;
 
-  // ---- tap validity of this lane's activation rows (sequence position / length)
-  int tpos[MB], tlen[MB];
+  // ---- tap validity of this lane's activation rows: bit tap of vmask[mb] is set when the row
+  // shifted by tap - pad stays inside its sequence (sequence position / length)
+  int vmask[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + mb * 16 + (lane & 15);
-    if (m >= M) {
-      tpos[mb] = 0;
-      tlen[mb] = 0;  // never valid (rows past M are not stored)
-    } else if (a.row_pos != nullptr) {
-      const int2 q = a.row_pos[m];
-      tpos[mb] = q.x;
-      tlen[mb] = q.y;
-    } else {
-      tpos[mb] = m % T;
-      tlen[mb] = T;
+    int tpos = 0, tlen = 0;  // rows past M: never valid (not stored)
+    if (m < M) {
+      if (a.row_pos != nullptr) {
+        const int2 q = a.row_pos[m];
+        tpos = q.x;
+        tlen = q.y;
+      } else {
+        tpos = m % T;
+        tlen = T;
+      }
     }
-  }
-  int tw = 0, lw = 0;
-  if (a.row_pos != nullptr) {
-    const int2 q = a.row_pos[m0];
-    tw = q.x;
-    lw = q.y;
-  } else {
-    tw = m0 % T;
-    lw = T;
-  }
-  const bool tile_inside = tw + BM <= lw && m0 + BM <= M;
-  // taps whose shifted rows may leave a sequence somewhere in the tile (bit tap): masked reads
-  uint32_t need_mask = 0;
+    int v = 0;
 #pragma unroll
-  for (int tap = 0; tap < KS; ++tap) {
-    const int sh = tap - pad;
-    if (!(tile_inside && tw + sh >= 0 && tw + BM - 1 + sh < lw)) need_mask |= 1u << tap;
+    for (int tap = 0; tap < KS; ++tap) v |= ((unsigned)(tpos + tap - pad) < (unsigned)tlen ? 1 : 0) << tap;
+    vmask[mb] = v;
   }
   // b1 -> LDS, the zero slot; consume the row_pos loads before the DMA stream starts
   for (int i = tid; i < F / 4; i += 256)
     *reinterpret_cast<float4 *>(smem + B1_OFF + 16 * i) = reinterpret_cast<const float4 *>(p.b1)[i];
   if (tid == 0) *reinterpret_cast<float4 *>(smem + ZERO_OFF) = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb) asm volatile("" ::"v"(tpos[mb]), "v"(tlen[mb]));
+  for (int mb = 0; mb < MB; ++mb) asm volatile("" ::"v"(vmask[mb]));
 
   // ---- x tile (rows m0 - pad .. m0 + BM + KS - 2, all 256 channels) -> LDS, once
   const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
@@ -193,14 +182,14 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   // GEMM1 unit (tap, k-step ks): x rows shifted by the tap; a 16-row block step keeps (row & 7)
   // LDS addresses of GEMM1 unit (tap, ks)'s fragments (computed a unit before the reads issue)
   auto addr_x = [&](int tap, int ks, int (&ad)[MB]) {
-    const bool all_ok = (FFN_ABLATE & 16) || ((need_mask >> tap) & 1u) == 0;
-    const int sh = tap - pad;
     const int r = hrow0 + tap;
     const int base = X_OFF + r * 512 + (xchunk(r, 4 * ks + hi) << 4);
+    // masked rows: address & 0 = the zero slot. Pure VALU (sign-extended bit extract + and): a
+    // compare into a lane mask and a select would put SGPR round trips on the MFMA issue path
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
-      const bool ok = all_ok || (unsigned)(tpos[mb] + sh) < (unsigned)tlen[mb];
-      ad[mb] = ok ? base + mb * 8192 : ZERO_OFF;
+      const int keep = (FFN_ABLATE & 16) ? -1 : __builtin_amdgcn_sbfe(vmask[mb], tap, 1);
+      ad[mb] = (base + mb * 8192) & keep;
     }
   };
   auto issue_x = [&](const int (&ad)[MB], bf16x8 (&f)[MB]) {

@@ -63,7 +63,7 @@ class SynthGraphs:
             fn()
         torch.cuda.current_stream(dev).wait_stream(s)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=s):
+        with torch.cuda.graph(graph, stream=s, capture_error_mode="thread_local"):
             out = fn()
         self.captures += 1
         return graph, out

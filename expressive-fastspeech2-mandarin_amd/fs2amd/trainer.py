@@ -171,7 +171,12 @@ class TrainStep:
             g = torch.cuda.CUDAGraph()
             cur = torch.cuda.current_stream(self.device)
             self._stream.wait_stream(cur)
-            with torch.cuda.graph(g, stream=self._stream):
+            # thread_local: with an RCCL process group, its watchdog thread queries events while
+            # this thread captures; under the default "global" mode such a call from ANY thread
+            # invalidates the capture and capture_end aborts (intermittently: it depends on the
+            # watchdog's timing). The warm-up steps ran on this stream with detached losses, so no
+            # autograd node of theirs (AccumulateGrad bound to another stream) reaches the capture.
+            with torch.cuda.graph(g, stream=self._stream, capture_error_mode="thread_local"):
                 losses = [l.detach() for l in self._step_body(static)]
             cur.wait_stream(self._stream)
             self._graph = (self._sig(batch), g, static, losses)

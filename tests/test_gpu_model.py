@@ -179,7 +179,8 @@ def test_cfg2_bf16_free_running_flip_rate(model):
     print("bf16 free-running:", r)
     assert r["dur"] <= FLIP_MAX_DUR and r["dur_step"] <= 1.0, r
     assert r["pitch"] <= FLIP_MAX_BUCKET and r["pitch_step"] <= 1 and r["dp"] <= PRED_MAX_ERR, r
-    assert r["energy"] <= 0.6, r  # compounded through flipped pitch embedding rows (see above)
+    # compounded through flipped pitch embedding rows (see above): measured 44.8 % (rounds 2 and 3)
+    assert r["energy"] <= 0.5, r
     # the output length follows the rounded durations exactly
     np.testing.assert_array_equal(_np(b[9]), _np(b[5]).sum(1).astype(np.int64))
     # energy on its own: pitch buckets pinned to the fp32 predictions
@@ -285,8 +286,8 @@ def test_targets_fp32_vs_reference(model, case, head):
 
 
 # bf16 perf path against the reference at the bench shapes (targets pinned: no discrete decision
-# differs). Measured round 3: see the prints; bounds are the small-case bf16 tolerance (0.15 max,
-# 0.02 mean) and per-utterance |postnet| checksums within 1 %.
+# differs). Measured round 3 (fused FFN): cfg2 head max 0.033 / mean 0.0061, |postnet| checksum
+# rel 1.7e-3, per-value sum error 1.5e-3; cfg4 0.036 / 0.0067 / 2.0e-3 / 1.7e-3. Bounds ~2x that.
 @pytest.mark.parametrize("case,head", [("cfg2_targets", 4), ("cfg4_targets", 2)])
 def test_targets_bf16_vs_reference(model, case, head):
     args, controls, outs, z = load_case(case)
@@ -300,9 +301,9 @@ def test_targets_bf16_vs_reference(model, case, head):
     mean_sum_err = np.abs(ck["ck_post_valid_sum"] - z["ck_post_valid_sum"]) / n_valid
     print(f"{case} bf16 vs reference: head max {mx:.4f} mean {mean:.5f}; |post| checksum rel max "
           f"{rel_abs.max():.2e}; per-frame-value sum error max {mean_sum_err.max():.2e}")
-    assert mx <= 0.15 and mean <= 0.02, (mx, mean)
-    assert rel_abs.max() <= 1e-2, rel_abs.max()
-    assert mean_sum_err.max() <= 0.02, mean_sum_err.max()
+    assert mx <= 0.075 and mean <= 0.0125, (mx, mean)
+    assert rel_abs.max() <= 4e-3, rel_abs.max()
+    assert mean_sum_err.max() <= 4e-3, mean_sum_err.max()
 
 
 def test_long_eval_pe_recompute_fp32(model):

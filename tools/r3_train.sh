@@ -10,3 +10,4 @@ timeout -k 10 200 python bench.py --mode train --graph 1 --steps 20 --warmup 5 >
 timeout -k 10 200 python bench.py --mode train --graph 1 --ddp 1 --steps 20 --warmup 5 > $O/train_graph_ddp.json 2>$O/train_graph_ddp.err && tail -1 $O/train_graph_ddp.json | cut -c1-300
 timeout -k 10 200 python bench.py --mode train --graph 0 --steps 10 --warmup 3 > $O/train_eager.json 2>$O/train_eager.err && tail -1 $O/train_eager.json | cut -c1-300
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_train_graph -o run -- python3 bench.py --mode train --graph 1 --steps 5 --warmup 3 > $O/prof_train_graph.log 2>&1; echo "rocprof train graph rc=$?"; tail -2 $O/prof_train_graph.log | cut -c1-300
+timeout -k 10 300 python -u -m pytest tests/test_gpu_graphs.py -q --timeout 200 --timeout-method thread -rf > $O/graphs_tests.log 2>&1; tail -3 $O/graphs_tests.log
