@@ -460,393 +460,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
   }
 }
 
-// Software-pipelined form of attn_bf16_kernel (64-key tiles, 16 queries per wave): in step kt a
-// wave issues the S^T = K Q^T MFMAs of tile kt+1 first, then the softmax VALU of tile kt (whose
-// scores were computed in step kt-1) and the O^T = V^T P^T MFMAs of tile kt, so the matrix pipe
-// works on tile kt+1 while the VALU exponentiates tile kt instead of each waiting on the other.
-// K and V have separate 2-slot rings shifted by one tile: step kt reads K(kt+1) and V(kt) and
-// DMAs K(kt+2) and V(kt+1) into the slots step kt-1 finished with; one vmcnt(0) + barrier per
-// step (as the 2-stage kernel). Same arithmetic, same order per score: bit-identical output.
-template <int NWV>
-__global__ __launch_bounds__(64 * NWV, 4) void attn_bf16_sp_kernel(const bf16 *__restrict__ qkv, int64_t qs,
-                                                                   uint32_t qkv_bytes, const int64_t *__restrict__ lens,
-                                                                   int B, int T, int H, int nqt, float scale_log2,
-                                                                   bf16 *__restrict__ out, int64_t os,
-                                                                   const int32_t *__restrict__ cu) {
-  constexpr int QTW = 16 * NWV;
-  constexpr int KTT = 64;
-  constexpr int PPW = KTT / 4 / NWV;  // 1 KiB pieces per wave per K (or V) tile
-  constexpr int HT = KTT * 256;       // bytes of one K (or V) tile
-  __shared__ __attribute__((aligned(16))) char smem[4 * HT];  // K0 K1 V0 V1
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, li = lane & 15;
-
-  const int nwg = gridDim.x, id = blockIdx.x;
-  const int q8 = nwg >> 3, rem = nwg & 7, xcd = id & 7;
-  const int t = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (id >> 3);
-  const int qt = t % nqt, bh = t / nqt, h = bh % H, b = bh / H;
-  const int q0 = qt * QTW;
-  int len;
-  uint32_t seq_base;
-  if (cu != nullptr) {
-    seq_base = (uint32_t)cu[b];
-    len = cu[b + 1] - cu[b];
-    T = len;
-  } else {
-    const int64_t len64 = lens[b];
-    len = (int)(len64 < 0 ? 0 : (len64 > T ? T : len64));
-    seq_base = (uint32_t)b * (uint32_t)T;
-  }
-  if (q0 >= T) return;
-  const bool active = q0 + 16 * w < T;
-
-  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16 *>(qkv), (short)0, (int)qkv_bytes, 0x00020000);
-  const uint32_t row_bytes = (uint32_t)qs * 2u;
-
-  const int qrow = q0 + 16 * w + li;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const uint32_t off = qrow < T ? (seq_base + qrow) * row_bytes + (uint32_t)(h * DK + 32 * s + 8 * g) * 2u : 0x80000000u;
-    auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-    qf[s] = *reinterpret_cast<bf16x8 *>(&v);
-  }
-
-  const int prow = lane >> 4, pch = lane & 15;
-  // DMA of the K (part 1) or V (part 2) rows of tile k0 into `dst`
-  auto dma = [&](int k0, char *dst, int part) {
-#pragma unroll
-    for (int it = 0; it < PPW; ++it) {
-      const int p = w + NWV * it;
-      const int r = 4 * p + prow;
-      const int lc = pch ^ kv_swz(r);
-      const int key = k0 + r;
-      const uint32_t off = key < T ? (seq_base + key) * row_bytes + (uint32_t)lc * 16u +
-                                         (uint32_t)((part * H + h) * DK) * 2u
-                                   : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(dst + p * 1024), 16, off,
-                                               0, 0, 0);
-    }
-  };
-  auto kbuf = [&](int kt) { return smem + (kt & 1) * HT; };
-  auto vbuf = [&](int kt) { return smem + 2 * HT + (kt & 1) * HT; };
-  auto sync = []() {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-
-  f32x4 oacc[DK / 16];
-#pragma unroll
-  for (int i = 0; i < DK / 16; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
-  const int ntiles = (len + KTT - 1) / KTT;
-  const int tq = li >> 2, tp = li & 3;
-  int voff[DK / 16];
-#pragma unroll
-  for (int nd = 0; nd < DK / 16; ++nd) voff[nd] = kv_off(4 * g + tq, nd * 2 + (tp >> 1)) + (tp & 1) * 8;
-
-  constexpr int NB = KTT / 16;
-  auto qk = [&](const char *Kb, f32x4 (&sacc)[NB]) {
-#pragma unroll
-    for (int ni = 0; ni < NB; ++ni) {
-      sacc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(Kb + kv_off(ni * 16 + li, 4 * s + g));
-        sacc[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], sacc[ni], 0, 0, 0);
-      }
-      // at most 2 key blocks of K fragments in registers (the other tile's scores are live here)
-      if (ni & 1) __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // softmax of one tile's scores (keys k0 + ni*16 + 4g + j) + O^T += V^T P^T
-  auto softmax_pv = [&](f32x4 (&sacc)[NB], const char *Vb, int k0, auto masked_tag) {
-    constexpr bool MASKED = decltype(masked_tag)::value;
-    if constexpr (MASKED) {
-      const int lim = len - k0 - 4 * g;
-#pragma unroll
-      for (int ni = 0; ni < NB; ++ni)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (ni * 16 + j >= lim) sacc[ni][j] = -INFINITY;
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int ni = 0; ni < NB; ++ni) mx = fmaxf(mx, fmaxf(fmaxf(sacc[ni][0], sacc[ni][1]), fmaxf(sacc[ni][2], sacc[ni][3])));
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    if (__builtin_amdgcn_ballot_w64(m_new != m_run) != 0) {
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2);
-      l_run *= alpha;
-#pragma unroll
-      for (int nd = 0; nd < DK / 16; ++nd) oacc[nd] *= alpha;
-    }
-    m_run = m_new;
-    const float mc = -m_new * scale_log2;
-    float sum = 0.f;
-    bf16x8 pf[NB / 2];
-#pragma unroll
-    for (int ni = 0; ni < NB; ++ni)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[ni][j], scale_log2, mc));
-        sum += p;
-        pf[ni >> 1][(ni & 1) * 4 + j] = (bf16)p;
-      }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    l_run += sum;
-#pragma unroll
-    for (int s2 = 0; s2 < NB / 2; ++s2) {
-#pragma unroll
-      for (int nd = 0; nd < DK / 16; ++nd) {
-        const char *vp = Vb + voff[nd] + s2 * 32 * 256;
-        auto lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)vp);
-        auto hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)(vp + 16 * 256));
-        bf16x8 vf;
-        __builtin_memcpy(&vf, &lo, 8);
-        __builtin_memcpy(reinterpret_cast<char *>(&vf) + 8, &hi, 8);
-        oacc[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[s2], oacc[nd], 0, 0, 0);
-      }
-    }
-  };
-
-  f32x4 cur[NB], nxt[NB];  // scores of tile kt (computed in step kt-1) / of tile kt+1
-  if (ntiles > 0) {
-    dma(0, kbuf(0), 1);
-    sync();  // K(0) landed (and the Q loads)
-    if (ntiles > 1) dma(KTT, kbuf(1), 1);
-    dma(0, vbuf(0), 2);
-    if (active) qk(kbuf(0), cur);
-  }
-  // step kt: K(kt+1), V(kt) landed; DMA K(kt+2) into K(kt)'s slot, V(kt+1) into V(kt-1)'s slot.
-  // Every step but the last has a next tile and no masked keys.
-  for (int kt = 0; kt + 1 < ntiles; ++kt) {
-    sync();
-    if (kt + 2 < ntiles) dma((kt + 2) * KTT, kbuf(kt + 2), 1);
-    dma((kt + 1) * KTT, vbuf(kt + 1), 2);
-    if (!active) continue;
-    qk(kbuf(kt + 1), nxt);
-    // keep tile kt's V reads below the QK MFMAs (register pressure); the MFMAs still run under
-    // the softmax VALU that follows
-    __builtin_amdgcn_sched_barrier(0);
-    softmax_pv(cur, vbuf(kt), kt * KTT, std::false_type{});
-#pragma unroll
-    for (int ni = 0; ni < NB; ++ni) cur[ni] = nxt[ni];
-  }
-  if (ntiles > 0) {
-    sync();
-    if (active) softmax_pv(cur, vbuf(ntiles - 1), (ntiles - 1) * KTT, std::true_type{});
-  }
-
-  const int q = q0 + 16 * w + li;
-  if (q < T) {
-    const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
-    bf16 *orow = out + ((int64_t)seq_base + q) * os + h * DK + 4 * g;
-#pragma unroll
-    for (int nd = 0; nd < DK / 16; ++nd) {
-      bf16x4 o = {(bf16)(oacc[nd][0] * inv), (bf16)(oacc[nd][1] * inv), (bf16)(oacc[nd][2] * inv),
-                  (bf16)(oacc[nd][3] * inv)};
-      *reinterpret_cast<bf16x4 *>(orow + nd * 16) = o;
-    }
-  }
-}
-
-// Two 16-query blocks per wave (32 queries): every K fragment and every transposed V fragment read
-// from LDS feeds two MFMAs instead of one, halving the LDS read bytes per FLOP — at 16 queries per
-// wave the 8 waves of a workgroup each re-read the whole K/V tile, and the LDS array, not the
-// matrix pipe, set the pace. Same data flow otherwise (S^T = K Q^T, per-lane softmax rows,
-// O^T = V^T P^T with P from registers).
-template <int NWV, int NST>
-__global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_q32_kernel(const bf16 *__restrict__ qkv, int64_t qs,
-                                                                    uint32_t qkv_bytes,
-                                                                    const int64_t *__restrict__ lens, int B, int T,
-                                                                    int H, int nqt, float scale_log2,
-                                                                    bf16 *__restrict__ out, int64_t os,
-                                                                    const int32_t *__restrict__ cu) {
-  constexpr int QTW = 32 * NWV;
-  constexpr int PPW = 16 / NWV;
-  constexpr int LPS = 2 * PPW;
-  constexpr int STG = 2 * KT * 256;
-  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, li = lane & 15;
-
-  const int nwg = gridDim.x, id = blockIdx.x;
-  const int q8 = nwg >> 3, rem = nwg & 7, xcd = id & 7;
-  const int t = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (id >> 3);
-  const int qt = t % nqt, bh = t / nqt, h = bh % H, b = bh / H;
-  const int q0 = qt * QTW;
-  int len;
-  uint32_t seq_base;
-  if (cu != nullptr) {
-    seq_base = (uint32_t)cu[b];
-    len = cu[b + 1] - cu[b];
-    T = len;
-  } else {
-    const int64_t len64 = lens[b];
-    len = (int)(len64 < 0 ? 0 : (len64 > T ? T : len64));
-    seq_base = (uint32_t)b * (uint32_t)T;
-  }
-  if (q0 >= T) return;
-  const bool active = q0 + 32 * w < T;
-
-  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16 *>(qkv), (short)0, (int)qkv_bytes, 0x00020000);
-  const uint32_t row_bytes = (uint32_t)qs * 2u;
-
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int qrow = q0 + 32 * w + 16 * qb + li;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const uint32_t off =
-          qrow < T ? (seq_base + qrow) * row_bytes + (uint32_t)(h * DK + 32 * s + 8 * g) * 2u : 0x80000000u;
-      auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-      qf[qb][s] = *reinterpret_cast<bf16x8 *>(&v);
-    }
-  }
-
-  const int prow = lane >> 4, pch = lane & 15;
-  auto dma = [&](int k0, int buf) {
-    char *Kb = smem + buf * STG;
-    char *Vb = Kb + KT * 256;
-#pragma unroll
-    for (int it = 0; it < PPW; ++it) {
-      const int p = w + NWV * it;
-      const int r = 4 * p + prow;
-      const int lc = pch ^ kv_swz(r);
-      const int key = k0 + r;
-      const uint32_t base = key < T ? (seq_base + key) * row_bytes + (uint32_t)lc * 16u : 0x80000000u;
-      const uint32_t koff = base == 0x80000000u ? base : base + (uint32_t)((H + h) * DK) * 2u;
-      const uint32_t voff = base == 0x80000000u ? base : base + (uint32_t)((2 * H + h) * DK) * 2u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(Kb + p * 1024), 16, koff,
-                                               0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(Vb + p * 1024), 16, voff,
-                                               0, 0, 0);
-    }
-  };
-
-  f32x4 oacc[2][DK / 16];
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-    for (int i = 0; i < DK / 16; ++i) oacc[qb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
-
-  const int ntiles = (len + KT - 1) / KT;
-#pragma unroll
-  for (int st = 0; st < NST - 1; ++st)
-    if (st < ntiles) dma(st * KT, st);
-  const int tq = li >> 2, tp = li & 3;
-  int voffs[DK / 16];
-#pragma unroll
-  for (int nd = 0; nd < DK / 16; ++nd) voffs[nd] = kv_off(4 * g + tq, nd * 2 + (tp >> 1)) + (tp & 1) * 8;
-  // one key tile; MASKED (the last tile only) sets the scores of keys >= len to -inf
-  auto tile = [&](int kt, auto masked_tag) {
-    constexpr bool MASKED = decltype(masked_tag)::value;
-    const int k0 = kt * KT;
-    const int ahead = ntiles - 1 - kt;
-    if (NST >= 3 && ahead >= NST - 2)
-      attn_vm_wait<LPS * (NST - 2)>();
-    else
-      attn_vm_wait<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + NST - 1 < ntiles) dma(k0 + (NST - 1) * KT, (kt + NST - 1) % NST);
-    if (!active) return;
-    const char *Kb = smem + (kt % NST) * STG;
-    const char *Vb = Kb + KT * 256;
-
-    f32x4 sacc[2][4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      sacc[0][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-      sacc[1][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(Kb + kv_off(ni * 16 + li, 4 * s + g));
-        sacc[0][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][s], sacc[0][ni], 0, 0, 0);
-        sacc[1][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][s], sacc[1][ni], 0, 0, 0);
-      }
-    }
-    bf16x8 pf[2][2];
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      if constexpr (MASKED) {
-        const int lim = len - k0 - 4 * g;
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (ni * 16 + j >= lim) sacc[qb][ni][j] = -INFINITY;
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        mx = fmaxf(mx, fmaxf(fmaxf(sacc[qb][ni][0], sacc[qb][ni][1]), fmaxf(sacc[qb][ni][2], sacc[qb][ni][3])));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run[qb], mx);
-      if (__builtin_amdgcn_ballot_w64(m_new != m_run[qb]) != 0) {  // exact: alpha == 1 otherwise
-        const float alpha = __builtin_amdgcn_exp2f((m_run[qb] - m_new) * scale_log2);
-        l_run[qb] *= alpha;
-#pragma unroll
-        for (int nd = 0; nd < DK / 16; ++nd) oacc[qb][nd] *= alpha;
-      }
-      m_run[qb] = m_new;
-      const float mc = -m_new * scale_log2;
-      float sum = 0.f;
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[qb][ni][j], scale_log2, mc));
-          sum += p;
-          pf[qb][ni >> 1][(ni & 1) * 4 + j] = (bf16)p;
-        }
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      l_run[qb] += sum;
-    }
-
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-      for (int nd = 0; nd < DK / 16; ++nd) {
-        const char *vp = Vb + voffs[nd] + s2 * 32 * 256;
-        auto lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)vp);
-        auto hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)(vp + 16 * 256));
-        bf16x8 vf;
-        __builtin_memcpy(&vf, &lo, 8);
-        __builtin_memcpy(reinterpret_cast<char *>(&vf) + 8, &hi, 8);
-        oacc[0][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[0][s2], oacc[0][nd], 0, 0, 0);
-        oacc[1][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1][s2], oacc[1][nd], 0, 0, 0);
-      }
-    }
-  };
-  for (int kt = 0; kt + 1 < ntiles; ++kt) tile(kt, std::false_type{});
-  if (ntiles > 0) tile(ntiles - 1, std::true_type{});
-
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    const int q = q0 + 32 * w + 16 * qb + li;
-    if (q < T) {
-      const float inv = l_run[qb] > 0.f ? 1.0f / l_run[qb] : 0.f;
-      bf16 *orow = out + ((int64_t)seq_base + q) * os + h * DK + 4 * g;
-#pragma unroll
-      for (int nd = 0; nd < DK / 16; ++nd) {
-        bf16x4 o = {(bf16)(oacc[qb][nd][0] * inv), (bf16)(oacc[qb][nd][1] * inv), (bf16)(oacc[qb][nd][2] * inv),
-                    (bf16)(oacc[qb][nd][3] * inv)};
-        *reinterpret_cast<bf16x4 *>(orow + nd * 16) = o;
-      }
-    }
-  }
-}
-
 }  // namespace
 
 extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
@@ -864,61 +477,21 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
   if (dtype == FS2_BF16) {
     const int64_t bytes = (int64_t)B * T * qkv_row_stride * 2;
     if (bytes >= (1LL << 31) || (out_row_stride & 3)) return FS2_EUNSUPPORTED;
-    // FS2_ATTN_VARIANT (A/B switch): 0 = 4 waves / 2 stages, 1 = 8 waves / 3 stages, 2 = 8 waves /
-    // 2 stages, 3 = 4 waves / 3 stages. Measured at the cfg2 decoder shape (packed, ~390 frames):
-    // 34.5 / 35.0 / 29.9 / 49.9 us: occupancy (16 waves per CU with 2 workgroups) hides the
-    // MFMA -> softmax -> MFMA chain better than a deeper K/V ring at 8 waves per CU. Default: 2
-    // for sequences longer than 64 (8 waves share each K/V tile), 0 otherwise (encoder, L <= 64:
-    // a 128-query workgroup would idle half its waves).
-    static const int forced = [] {
-      const char *e = getenv("FS2_ATTN_VARIANT");
-      return e != nullptr ? atoi(e) : -1;
-    }();
-    const int variant = forced >= 0 ? forced : (T > 64 ? 2 : 0);
-    if (variant == 0) {
-      const int nqt = (T + 63) / 64;
-      hipLaunchKernelGGL((attn_bf16_kernel<4, 2>), dim3(nqt * H * B), dim3(256), 0, s,
-                         reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
-                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
-    } else if (variant == 2) {
+    // 8 waves (128 queries) share each K/V tile for sequences longer than 64; 4 waves otherwise
+    // (encoder, L <= 64: a 128-query workgroup would idle half its waves). 2-stage K/V ring: at the
+    // cfg2 decoder shape (packed, ~390 frames) 16 waves per CU (2 workgroups) hide the MFMA ->
+    // softmax -> MFMA chain better than a deeper ring at 8 waves per CU (29.9 us vs 35.0 us with 3
+    // stages; 4 waves / 2 or 3 stages 34.5 / 49.9 us; the software-pipelined, 32-key-tile and
+    // 32-queries-per-wave variants measured 30.5, 31-32 and 27.4 us standalone / bench-neutral and
+    // were removed in round 3).
+    if (T > 64) {
       const int nqt = (T + 127) / 128;
       hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), dim3(nqt * H * B), dim3(512), 0, s,
                          reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
                          scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
-    } else if (variant == 3) {
+    } else {
       const int nqt = (T + 63) / 64;
-      hipLaunchKernelGGL((attn_bf16_kernel<4, 3>), dim3(nqt * H * B), dim3(256), 0, s,
-                         reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
-                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
-    } else if (variant == 8) {  // software-pipelined 8-wave kernel (QK of tile k+1 before softmax of tile k)
-      const int nqt = (T + 127) / 128;
-      hipLaunchKernelGGL((attn_bf16_sp_kernel<8>), dim3(nqt * H * B), dim3(512), 0, s,
-                         reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
-                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
-    } else if (variant == 6 || variant == 7) {  // 8 waves, 32-key tiles: 3 / 4-deep ring at 2 workgroups per CU
-      const int nqt = (T + 127) / 128;
-      if (variant == 6)
-        hipLaunchKernelGGL((attn_bf16_kernel<8, 3, 32>), dim3(nqt * H * B), dim3(512), 0, s,
-                           reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H,
-                           nqt, scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
-      else
-        hipLaunchKernelGGL((attn_bf16_kernel<8, 4, 32>), dim3(nqt * H * B), dim3(512), 0, s,
-                           reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H,
-                           nqt, scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
-    } else if (variant == 4 || variant == 5) {  // 32 queries per wave: 4 waves (128 q) or 8 waves (256 q)
-      const int qtw = variant == 4 ? 128 : 256;
-      const int nqt = (T + qtw - 1) / qtw;
-      if (variant == 4)
-        hipLaunchKernelGGL((attn_bf16_q32_kernel<4, 2>), dim3(nqt * H * B), dim3(256), 0, s,
-                           reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H,
-                           nqt, scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
-      else
-        hipLaunchKernelGGL((attn_bf16_q32_kernel<8, 2>), dim3(nqt * H * B), dim3(512), 0, s,
-                           reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H,
-                           nqt, scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
-    } else {  // 8 waves (128 queries) share each K/V tile, 3-deep ring
-      const int nqt = (T + 127) / 128;
-      hipLaunchKernelGGL((attn_bf16_kernel<8, 3>), dim3(nqt * H * B), dim3(512), 0, s,
+      hipLaunchKernelGGL((attn_bf16_kernel<4, 2>), dim3(nqt * H * B), dim3(256), 0, s,
                          reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
                          scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
     }

@@ -801,10 +801,7 @@ bool splitk_env() {
 // FS2_LN_SMALLM_ROWS (A/B): row tile of the small-M LayerNorm GEMMs (encoder / variance
 // predictors, M = B*L ~ 4k): 16 (default), 32 or 64 rows.
 int small_m_rows() {
-  static const int v = [] {
-    const char *e = getenv("FS2_LN_SMALLM_ROWS");
-    return e != nullptr ? atoi(e) : 16;
-  }();
+  constexpr int v = 16;
   return v;
 }
 
@@ -1079,10 +1076,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (NS == 2 && 16 * WMI * WGM <= 64) ?
 // FS2_L2PF (A/B): ring kernel L2 weight prefetch: 0 off, 1 on the small-M tiles (<= 32 rows,
 // default), 2 on every ring launch.
 int l2pf_env() {
-  static const int v = [] {
-    const char *e = getenv("FS2_L2PF");
-    return e != nullptr ? atoi(e) : 1;
-  }();
+  constexpr int v = 1;
   return v;
 }
 
@@ -1124,10 +1118,7 @@ void launch(ConvArgs a, hipStream_t s) {
   constexpr bool GL = std::is_same<TIn, typename CTraits<CT>::T>::value;  // LDS-DMA needs no conversion
   a.ntn = (a.N + BN - 1) / BN;
   a.ngr = a.ntn;
-  static const bool grouped = [] {
-    const char *e = getenv("FS2_CONV_NGROUP");
-    return e == nullptr || e[0] != '0';
-  }();
+  constexpr bool grouped = true;
   if (grouped && a.w_bytes > (2u << 20) && a.ntn > 4)  // weights > 2 MiB: groups of <= 4 N tiles
     for (int g = 4; g >= 1; --g)
       if (a.ntn % g == 0) {
@@ -1176,10 +1167,7 @@ constexpr int kTargetWGs = 512;
 // rows left -4 %), or with FS2_CONV_W8=0 the round-1 4 waves of 64 x 64
 template <int CT, typename TIn>
 void launch_128(ConvArgs a, hipStream_t s) {
-  static const bool w8 = [] {
-    const char *e = getenv("FS2_CONV_W8");
-    return e == nullptr || e[0] != '0';
-  }();
+  constexpr bool w8 = true;
   if (w8)
     launch<CT, 2, 4, 4, 9, TIn, 32>(a, s);
   else
@@ -1222,10 +1210,7 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       if (tiles256 <= S) {  // at most one round: the phased kernel alone
         // 224-row tiles when they still fit the one round (shorter tiles, more CUs busy);
         // FS2_CONV_8P224=0: off
-        static const bool r224 = [] {
-          const char *e = getenv("FS2_CONV_8P224");
-          return e == nullptr || e[0] != '0';
-        }();
+        constexpr bool r224 = true;
         const int64_t tiles224 = (int64_t)((a.M + 223) / 224) * ((a.N + 255) / 256);
         launch_8p(a, s, r224 && tiles224 <= S);
         return;
@@ -1243,10 +1228,7 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
   if constexpr (std::is_same<TIn, typename CTraits<CT>::T>::value && CT != FS2_FP8) {
     // split-precision / grouped elementwise GEMMs (the column-split variance predictor convs):
     // 128-column ring tiles, 64 rows when that still gives a workgroup per CU, else 32
-    static const int vpring = [] {
-      const char *e = getenv("FS2_VP_RING");
-      return e != nullptr ? atoi(e) : 2;
-    }();
+    constexpr int vpring = 2;
     if (!ln && vpring && (a.cin_block != 0 || a.group_n != 0)) {
       const int ntn = (a.N + 127) / 128;
       const bool rows64 = (int64_t)((a.M + 63) / 64) * ntn >= num_cus();
@@ -1260,31 +1242,19 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
     }
   }
   if constexpr (std::is_same<TIn, typename CTraits<CT>::T>::value) {
-    static const bool ring = [] {
-      const char *e = getenv("FS2_CONV_RING");
-      return e == nullptr || e[0] != '0';
-    }();
+    constexpr bool ring = true;
     if (ln && (ring || a.cin_block != 0)) {  // LDS-DMA deep ring (LN epilogues, N == 256)
       // 8 column waves on the small-M tiles (FS2_LN_W8=0: 4): the second wave per SIMD overlaps
       // LDS reads with the partner's MFMAs (encoder LN 14.5 -> 13.2 us, VP 50.8 -> 48.6 us)
-      static const bool w8 = [] {
-        const char *e = getenv("FS2_LN_W8");
-        return e == nullptr || e[0] != '0';
-      }();
+      constexpr bool w8 = true;
       // 16 waves (2 x 8 of 64 x 32) on the decoder's 128-row tiles, 4 per SIMD (FS2_LN_W16DEC=0:
       // 8 waves of 64 x 64): fc + LN 18.4 -> 16.6 us, conv-k1 + LN 31.9 -> 28.5 us
-      static const bool w16d = [] {
-        const char *e = getenv("FS2_LN_W16DEC");
-        return e == nullptr || e[0] != '0';
-      }();
+      constexpr bool w16d = true;
       // short-K decoder LN GEMMs (fc + residual + LN: K = 256, 4 k-steps): 64-row, 2-stage tiles,
       // two workgroups per CU, so one's LayerNorm epilogue and stores overlap the other's K loop
       // (fc + LN 17.0 -> 16.2 us; the K = 1024 conv-k1 + LN is neutral and keeps the 128-row tile).
       // FS2_LN_2WG: 0 off, 1 on for every decoder LN GEMM, default short K only.
-      static const int two = [] {
-        const char *e = getenv("FS2_LN_2WG");
-        return e != nullptr ? atoi(e) : 2;
-      }();
+      constexpr int two = 2;
       if (a.M >= 192 * 128 && (two == 1 || (two == 2 && a.KS * a.Cin_pad <= 256)))
         launch_ring<CT, 1, 4, 2, 8>(a, s);  // 64 x 256, 8 waves of 64 x 32, 2 stages (80 KiB)
       else if (a.M >= 192 * 128 && w16d)
@@ -1313,23 +1283,14 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
     const int ntn = (a.N + 127) / 128;
     const int nKd = a.KS * (a.Cin_pad / CTraits<CT>::KE);
     constexpr bool GLd = std::is_same<TIn, typename CTraits<CT>::T>::value;
-    static const bool w8s = [] {  // 8 waves of 32 columns on the 64-row tiles (FS2_CONV_W8S=0: 4
-      const char *e = getenv("FS2_CONV_W8S");  // of 64); encoder conv-k9 32.4 -> 31.1 us
-      return e == nullptr || e[0] != '0';
-    }();
-    static const int narrow = [] {  // FS2_CONV_NARROW=0: off (A/B)
-      const char *e = getenv("FS2_CONV_NARROW");
-      return e != nullptr ? atoi(e) : 1;
-    }();
+    constexpr bool w8s = true;  // 8 waves of 32 columns on the 64-row tiles (vs 4 of 64): encoder conv-k9 32.4 -> 31.1 us
+    constexpr int narrow = 1; // FS2_CONV_NARROW=0: off (A/B)
     if constexpr (CT == FS2_BF16 && GLd) {
       // FFN conv-k9 below the phased kernel's size (encoder, M = 4k): 128 x 128 tiles on the
       // LDS-DMA ring (4 stages, 3 k-steps in flight, one workgroup per CU) instead of the
       // double-buffered halo-reuse tiles: 36.8 -> 33.2 us. FS2_PLAIN_RING (A/B): 0 off,
       // 2 (default) this, 1: 64 x 128 / 6 stages (42 us), 3: 64 x 128 / 4 stages (43 us).
-      static const int pring = [] {
-        const char *e = getenv("FS2_PLAIN_RING");
-        return e != nullptr ? atoi(e) : 2;
-      }();
+      constexpr int pring = 2;
       if (pring && a.row_split == 0 && a.KS == 9 && a.Cin_pad == 256 && ntn > 1) {
         if (pring == 1)
           launch_ring<CT, 2, 2, 6, 4, 128>(a, s);
@@ -1471,10 +1432,7 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.row_split = 0;
   a.split_slots = 1;
   {
-    static const bool lnp = [] {  // FS2_LN_PAIRS=0: one row per wave-iteration (round-1 epilogue)
-      const char *e = getenv("FS2_LN_PAIRS");
-      return e == nullptr || e[0] != '0';
-    }();
+    constexpr bool lnp = true; // FS2_LN_PAIRS=0: one row per wave-iteration (round-1 epilogue)
     a.ln_pairs = lnp ? 1 : 0;
   }
   if (d->splitk_ws != nullptr && d->splitk_ws_bytes > kSkCntBytes && d->splitk_ws_bytes < (1LL << 31) + kSkCntBytes) {
@@ -1512,10 +1470,7 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   a.l2pf = 0;
   const bool xb = d->x_dtype == FS2_BF16;
   {  // short-K, wide-N bf16 projections (Q|K|V): the weight-resident kernel (gemm_wres.hip)
-    static const bool wres = [] {
-      const char *e = getenv("FS2_WRES");
-      return e == nullptr || e[0] != '0';
-    }();
+    constexpr bool wres = true;
     if (wres && d->compute == FS2_BF16 && xb && (d->out_dtype == FS2_BF16 || d->out_dtype == FS2_F32) && d->KS == 1 &&
         d->pad == 0 &&
         (epi == FS2_EPI_BIAS || epi == FS2_EPI_BIAS_RELU) && d->Cin == d->Cin_pad && d->Cin <= 256 &&

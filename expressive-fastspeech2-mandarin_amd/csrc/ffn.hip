@@ -57,9 +57,12 @@ struct FfnArgs {
 
 constexpr int64_t ffn_weight_elems(int KS, int F) { return (int64_t)F * KS * kD + (int64_t)kD * F; }
 
-// physical 16-byte chunk of logical chunk c in a 512-byte LDS row r: conflict-free ds_read_b128
-// for 16 consecutive rows starting anywhere (the tap shift) and for the H writes
-__device__ __forceinline__ int xchunk(int r, int c) { return c ^ ((r & 7) << 1); }
+// physical 16-byte chunk of logical chunk c in a 512-byte LDS row r: ds_read_b128 of 16
+// consecutive rows starting anywhere (the tap shift) conflict-free, and the 8-byte accesses of one
+// column across 16 rows (H writes, residual reads, output staging) 2-way -- the least possible for
+// that pattern (the swizzle `(r & 7) << 1` made them 4-way). Found by exhaustive search over XOR
+// maps of the row bits; depends on r & 7 only.
+__device__ __forceinline__ int xchunk(int r, int c) { return c ^ ((r & 3) << 1) ^ ((r & 4) ? 9 : 0); }
 
 template <int N, typename Fn, int... I>
 __device__ __forceinline__ void static_for_impl(Fn &&f, std::integer_sequence<int, I...>) {
@@ -86,7 +89,8 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   constexpr int H_OFF = X_OFF + 4 * XP_PER_WAVE * 1024;
   constexpr int F = NCH * kChunk;
   constexpr int B1_OFF = H_OFF + BM * 512;
-  constexpr int RED_OFF = B1_OFF + F * 4;           // LN row statistics: [BM rows][4 waves] f32
+  constexpr int EP_OFF = B1_OFF + F * 4;            // b2, gamma, beta: 3 x 256 f32
+  constexpr int RED_OFF = EP_OFF + 3 * kD * 4;      // LN row statistics: [BM rows][4 waves] f32
   constexpr int SMEM = RED_OFF + BM * 16;
   static_assert(SMEM <= 163840, "LDS");
   constexpr int NK1 = KS * (kD / 32);  // GEMM1 units per chunk (tap-major, 8 k-steps per tap)
@@ -129,6 +133,11 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   // b1 -> LDS, the zero slot; consume the row_pos loads before the DMA stream starts
   for (int i = tid; i < F / 4; i += 256)
     *reinterpret_cast<float4 *>(smem + B1_OFF + 16 * i) = reinterpret_cast<const float4 *>(p.b1)[i];
+  if (tid < 3 * kD / 4) {  // the LN epilogue's vectors, read once here instead of after the K loop
+    const float *src = tid < kD / 4 ? a.bias : tid < kD / 2 ? a.gamma : a.beta;
+    *reinterpret_cast<float4 *>(smem + EP_OFF + 16 * tid) =
+        reinterpret_cast<const float4 *>(src)[tid % (kD / 4)];
+  }
   if (tid == 0) *reinterpret_cast<float4 *>(smem + ZERO_OFF) = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) asm volatile("" ::"v"(vmask[mb]));
@@ -291,36 +300,43 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       mma(acc1, pa[s], f0);
     const bool more = g + 1 < NK1 / DEPTH;  // else: GEMM2 unit s of this chunk (scalar select)
     load_at(S, more ? base1(c) + (uint32_t)((g + 1) * DEPTH + s) * (uint32_t)kUnit
-                    : base2(c) + (uint32_t)(s * kUnit));
+                    : base2(c) + (uint32_t)(((2 * w + s) & (NK2 - 1)) * kUnit));
   };
 #pragma nounroll
   for (int c = 0; c < NCH; ++c) {
 #pragma nounroll
     for (int g = 0; g < NK1 / DEPTH; ++g) static_for<DEPTH>([&](auto S) { unit1(S, c, g); });
-    // every wave is past its GEMM2 reads of the previous chunk's H: overwrite it; then H visible
+    // every wave is past its GEMM2 reads of the previous chunk's H: overwrite it. GEMM2 walks the
+    // chunk's hidden columns starting at this wave's own block (units 2w, 2w + 1: its own writes,
+    // no barrier); the barrier that makes the other waves' blocks visible comes after that first
+    // unit, so it absorbs the skew between the waves' write_h instead of stalling on it.
     stamp(2 + 2 * c);
     bar();
     write_h(c);
     __builtin_amdgcn_s_waitcnt(kLgkm0);
-    bar();
     stamp(3 + 2 * c);
-    read_h(0, f0);
+    read_h(2 * w, f0);
     const uint32_t next1 = c + 1 < NCH ? base1(c + 1) : 0u;  // past the last unit: harmless reloads
     static_for<NK2>([&](auto Q) {
-      constexpr int q = decltype(Q)::value;
+      constexpr int q = decltype(Q)::value;  // this wave's q-th GEMM2 unit: hidden columns 32 * qq
       constexpr int s = q % DEPTH;
+      if constexpr (q == 1) {
+        __builtin_amdgcn_s_waitcnt(kLgkm0);
+        bar();  // every wave's H block written and visible
+      }
+      const int qn = (2 * w + q + 1) & (NK2 - 1);
       if constexpr (q + 1 == NK2)
         read_x(0, 0, f0);  // the next chunk's first unit (x is never overwritten)
       else if constexpr (q & 1)
-        read_h(q + 1, f0);
+        read_h(qn, f0);
       else
-        read_h(q + 1, f1);
+        read_h(qn, f1);
       if constexpr (q & 1)
         mma(acc2, pa[s], f1);
       else
         mma(acc2, pa[s], f0);
       if constexpr (q + DEPTH < NK2)
-        load_at(std::integral_constant<int, s>{}, base2(c) + (uint32_t)((q + DEPTH) * kUnit));
+        load_at(std::integral_constant<int, s>{}, base2(c) + (uint32_t)(((2 * w + q + DEPTH) & (NK2 - 1)) * kUnit));
       else
         load_at(std::integral_constant<int, s>{}, next1 + (uint32_t)((q + DEPTH - NK2) * kUnit));
     });
@@ -343,9 +359,9 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
       const int n = w * 64 + nb * 16 + 4 * hi;
-      b2v[nb] = *reinterpret_cast<const float4 *>(a.bias + n);
-      gv[nb] = *reinterpret_cast<const float4 *>(a.gamma + n);
-      bev[nb] = *reinterpret_cast<const float4 *>(a.beta + n);
+      b2v[nb] = *reinterpret_cast<const float4 *>(smem + EP_OFF + 4 * n);
+      gv[nb] = *reinterpret_cast<const float4 *>(smem + EP_OFF + 4 * (kD + n));
+      bev[nb] = *reinterpret_cast<const float4 *>(smem + EP_OFF + 4 * (2 * kD + n));
     }
     // v = acc + b2 + x (into acc2), row partial sums
     float part[MB];
@@ -369,13 +385,17 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     }
     // row statistic: 4 lanes (l >> 4) per wave, then the 4 waves through LDS
     auto row_reduce = [&](float (&pv)[MB], float (&tot)[MB]) {
+      // all rows' shuffles issued together (one LDS round trip per level, not one per row); the
+      // 4 lanes of a row store the same sum to the same slot (no divergent branch)
+      float t[MB];
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        float v = pv[mb];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        if (hi == 0) red[(mb * 16 + hrow0) * 4 + w] = v;
-      }
+      for (int mb = 0; mb < MB; ++mb) t[mb] = __shfl_xor(pv[mb], 16, 64);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) pv[mb] += t[mb];
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) t[mb] = __shfl_xor(pv[mb], 32, 64);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) red[(mb * 16 + hrow0) * 4 + w] = pv[mb] + t[mb];
       __syncthreads();
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) {
@@ -385,7 +405,9 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       __syncthreads();  // red is reused by the next statistic
     };
     float mean[MB], var[MB];
+    stamp(14);
     row_reduce(part, mean);
+    stamp(15);
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       mean[mb] *= inv_n;
@@ -402,44 +424,58 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       }
       part[mb] = ss;
     }
+    stamp(16);
     row_reduce(part, var);
+    stamp(17);
     // y = d * rstd * gamma + beta; padded rows: mask, then + addvec (FastSpeech2.forward adds the
-    // speaker / emotion vectors to every frame); bf16 into the H region (free since GEMM2 ended)
+    // speaker / emotion vectors to every frame); bf16 into the H region (free since GEMM2 ended).
+    // The padded-row extras are a separate instantiation: per-element branches for them made the
+    // packed (decoder) path's epilogue several times longer.
+    auto finish = [&](auto PADDED) {
+      constexpr bool padded = decltype(PADDED)::value;
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      const float rstd = 1.0f / sqrtf(var[mb] * inv_n + a.eps);
-      const int m = mb * 16 + hrow0;
-      const int gm = m0 + m;
-      bool masked = false;
-      int bb = 0;
-      if (a.lens != nullptr || a.av1 != nullptr) {  // padded rows only (host-checked)
-        bb = gm / T;
-        masked = a.lens != nullptr && (int64_t)(gm - bb * T) >= a.lens[bb];
-      }
+      for (int mb = 0; mb < MB; ++mb) {
+        const float rstd = 1.0f / sqrtf(var[mb] * inv_n + a.eps);
+        const int m = mb * 16 + hrow0;
+        bool masked = false;
+        int bb = 0;
+        if constexpr (padded) {
+          const int gm = m0 + m;
+          bb = gm / T;
+          masked = a.lens != nullptr && (int64_t)(gm - bb * T) >= a.lens[bb];
+        }
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const int n = w * 64 + nb * 16 + 4 * hi;
-        const f32x4 d = acc2[nb][mb];
-        float y[4] = {d[0] * rstd * gv[nb].x + bev[nb].x, d[1] * rstd * gv[nb].y + bev[nb].y,
-                      d[2] * rstd * gv[nb].z + bev[nb].z, d[3] * rstd * gv[nb].w + bev[nb].w};
-        if (masked) y[0] = y[1] = y[2] = y[3] = 0.f;
-        if (a.av1 != nullptr) {
-          const float4 v1 = *reinterpret_cast<const float4 *>(a.av1 + (int64_t)bb * kD + n);
-          y[0] += v1.x; y[1] += v1.y; y[2] += v1.z; y[3] += v1.w;
+        for (int nb = 0; nb < 4; ++nb) {
+          const int n = w * 64 + nb * 16 + 4 * hi;
+          const f32x4 d = acc2[nb][mb];
+          float y[4] = {d[0] * rstd * gv[nb].x + bev[nb].x, d[1] * rstd * gv[nb].y + bev[nb].y,
+                        d[2] * rstd * gv[nb].z + bev[nb].z, d[3] * rstd * gv[nb].w + bev[nb].w};
+          if constexpr (padded) {
+            if (masked) y[0] = y[1] = y[2] = y[3] = 0.f;
+            if (a.av1 != nullptr) {
+              const float4 v1 = *reinterpret_cast<const float4 *>(a.av1 + (int64_t)bb * kD + n);
+              y[0] += v1.x; y[1] += v1.y; y[2] += v1.z; y[3] += v1.w;
+            }
+            if (a.av2 != nullptr) {
+              const float4 v2 = *reinterpret_cast<const float4 *>(a.av2 + (int64_t)bb * kD + n);
+              y[0] += v2.x; y[1] += v2.y; y[2] += v2.z; y[3] += v2.w;
+            }
+          }
+          bf16x4 o;
+          o[0] = (bf16)y[0];
+          o[1] = (bf16)y[1];
+          o[2] = (bf16)y[2];
+          o[3] = (bf16)y[3];
+          *reinterpret_cast<bf16x4 *>(smem + H_OFF + m * 512 + (xchunk(m, n >> 3) << 4) + (n & 7) * 2) = o;
         }
-        if (a.av2 != nullptr) {
-          const float4 v2 = *reinterpret_cast<const float4 *>(a.av2 + (int64_t)bb * kD + n);
-          y[0] += v2.x; y[1] += v2.y; y[2] += v2.z; y[3] += v2.w;
-        }
-        bf16x4 o;
-        o[0] = (bf16)y[0];
-        o[1] = (bf16)y[1];
-        o[2] = (bf16)y[2];
-        o[3] = (bf16)y[3];
-        *reinterpret_cast<bf16x4 *>(smem + H_OFF + m * 512 + (xchunk(m, n >> 3) << 4) + (n & 7) * 2) = o;
       }
-    }
+    };
+    if (a.lens != nullptr || a.av1 != nullptr || a.av2 != nullptr)
+      finish(std::true_type{});
+    else
+      finish(std::false_type{});
     __syncthreads();
+    stamp(18);
     // whole rows out: 16-byte chunks, 32 per row
     const uint32_t orow = (uint32_t)a.os * 2u;
     char *ob = static_cast<char *>(a.out);
@@ -457,8 +493,8 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     __syncthreads();
     if (tid == 0) {  // trace build: the stamps go to output row a.M - 1 - block (packed capacity tail)
       uint64_t *o = reinterpret_cast<uint64_t *>(static_cast<char *>(a.out) + (size_t)(a.M - 1 - blockIdx.x) * a.os * 2);
-      for (int i = 0; i < 6 + 2 * NCH; ++i) o[i] = *reinterpret_cast<const uint64_t *>(smem + SMEM + 8 * i);
-      o[31] = (uint64_t)(6 + 2 * NCH);
+      for (int i = 0; i < 19; ++i) o[i] = *reinterpret_cast<const uint64_t *>(smem + SMEM + 8 * i);
+      o[31] = (uint64_t)19;
     }
   }
 }

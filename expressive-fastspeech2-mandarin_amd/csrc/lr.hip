@@ -182,25 +182,13 @@ void launch_expand_v(const void *x, const int32_t *cum, const int64_t *mel_len, 
                        index_map, out_cu);
 }
 
-// FS2_LR_VARIANT (A/B): 0 = 32 rows per workgroup, 1 = 64 rows, 2 = 32 rows + non-temporal output
-// stores (default), 3 = 64 rows + non-temporal stores. Measured (same box, us per launch, cfg2 /
-// cfg4 stress): 9.5 / 26.1, 9.4 / 33.4, 9.2 / 24.2, 9.3 / 28.4 -- cfg4 moves 152 MB, so variant 2
-// streams 6.3 TB/s (79 % of the 8 TB/s HBM peak); the bf16 bench is neutral to it.
+// 32 rows per workgroup + non-temporal output stores. Measured against 64 rows and / or plain
+// stores (same box, us per launch, cfg2 / cfg4 stress): 9.2 / 24.2 vs 9.3-9.5 / 26.1-33.4 -- cfg4
+// moves 152 MB, so this form streams 6.3 TB/s (79 % of the 8 TB/s HBM peak).
 template <typename TX, typename TO>
 void launch_expand(const void *x, const int32_t *cum, const int64_t *mel_len, int B, int L, int D, int T_out,
                    const float *pe, void *out, int32_t *index_map, const int32_t *out_cu, hipStream_t s) {
-  static const int v = [] {
-    const char *e = getenv("FS2_LR_VARIANT");
-    return e != nullptr ? atoi(e) : 2;
-  }();
-  if (v == 1)
-    launch_expand_v<TX, TO, 64, false>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
-  else if (v == 2)
-    launch_expand_v<TX, TO, 32, true>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
-  else if (v == 3)
-    launch_expand_v<TX, TO, 64, true>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
-  else
-    launch_expand_v<TX, TO, 32, false>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
+  launch_expand_v<TX, TO, 32, true>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
 }
 
 // get_mask_from_lengths (utils/tools.py:152-160): mask[b, t] = t >= lens[b]  (True = padding)

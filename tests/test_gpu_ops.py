@@ -393,48 +393,6 @@ print('ok')
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
-def test_attention_pipelined_variant_bit_identical(tmp_path):
-    """The software-pipelined attention kernel (FS2_ATTN_VARIANT=8: QK of tile k+1 issued before
-    the softmax of tile k, K / V rings shifted by one tile) does the same arithmetic in the same
-    order as the default 8-wave kernel (variant 2): bit-identical outputs on packed cfg2-shaped
-    rows (lengths 1..430, incl. one-tile and exact-multiple-of-64 sequences) and on padded rows
-    with key lengths 0..T. Child processes (the switch is read once per process)."""
-    import subprocess
-    import sys
-
-    code = r"""
-import sys, torch
-sys.path.insert(0, 'expressive-fastspeech2-mandarin_amd')
-from fs2amd import ops
-g = torch.Generator().manual_seed(3)
-T = 430
-lens = torch.randint(1, T + 1, (40,), generator=g)
-lens[:5] = torch.tensor([1, 64, 128, 430, 65])
-lay = ops.SeqLayout(lens.cuda(), T)
-qkv = (torch.randn(40 * T, 768, generator=g) * 2).to('cuda', torch.bfloat16)
-a = ops.attention(qkv, None, 2, 128, 128 ** 0.5, layout=lay)
-lp = torch.randint(0, T + 1, (12,), generator=g)
-lp[:3] = torch.tensor([0, T, 64])
-qp = torch.randn(12, T, 768, generator=g).to('cuda', torch.bfloat16)
-b = ops.attention(qp, lp.cuda(), 2, 128, 128 ** 0.5)
-torch.cuda.synchronize()
-R = int(lay.cu[-1])
-valid = torch.arange(T)[None, :] < lp[:, None]
-torch.save([a[:R].cpu(), b.cpu()[valid]], sys.argv[1])
-print('ok')
-"""
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    outs = []
-    for v in ("2", "8"):
-        p = str(tmp_path / f"attn{v}.pt")
-        r = subprocess.run([sys.executable, "-c", code, p], cwd=repo, env=dict(os.environ, FS2_ATTN_VARIANT=v),
-                           capture_output=True, text=True, timeout=120)
-        assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
-        outs.append(torch.load(p, weights_only=True))
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
-
-
 def test_split_precision_variance_predictor_matches_f32():
     """VariancePredictor in bf16x3 split precision (bf16 MFMA, channel-block map, two-plane LN
     output) vs exact-f32 MFMA on the same bf16 input: |d| <= 2e-4 + 2e-4 |y| (the split keeps
@@ -515,13 +473,12 @@ def test_vp_columns_match_f32_and_embed(B, L):
     (3, 50, False, None),      # all-tail launch (16 tiles)
     (1, 10400, False, None),   # 3 segments per tail tile: they start mid channel block
     (64, 430, True, None),     # cfg2 decoder shape on packed rows (bf16: phased kernel + 128x128 rows left)
-    (1, 40000, False, None),   # bf16 phased: 2 whole rounds (+ a 116-tile stream-K tail with FS2_CONV_8PSK=1)
-    (1, 16796, False, None),   # bf16 phased: 1 round + an 8-tile tail (32 ranges of 9 k-tiles under FS2_CONV_8PSK=1)
+    (1, 40000, False, None),   # bf16 phased: 2 whole rounds
+    (1, 16796, False, None),   # bf16 phased: 1 round + an 8-tile tail
     (1, 40000, False, (512, 512, 5))])  # PostNet conv shape (40 k-tiles)
 def test_conv_splitk_tail(ops, compute, B, T, packed, shape):
     """Split-K tail (ops.splitk_enabled): tail tiles cut along K across idle workgroups, summed
-    in segment order by the last arriver (128x128 kernel), or (FS2_CONV_8PSK=1) the phased
-    256x256 kernel's stream-K tail. Against the unsplit launches (ops.splitk_enabled(False)): f32 2e-5 /
+    in segment order by the last arriver (128x128 kernel). Against the unsplit launches (ops.splitk_enabled(False)): f32 2e-5 /
     bf16 2.5e-2 of the output scale; and bit-identical across repeated launches (fixed
     summation order, counters reset themselves)."""
     L = _L()

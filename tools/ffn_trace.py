@@ -56,7 +56,10 @@ def main():
     for (i, mean, mx), lab in zip(seg[:10], labels):
         print(f"{lab:28s} mean {mean:9.0f}  max {mx:9.0f} cycles")
     # epilogue split: 10 before drain, 12 after drain + barrier, 13 after E writes, 11 end
-    for lab, i0, i1 in (("  drain vmcnt + barrier", 10, 12), ("  E writes + barrier", 12, 13), ("  LN + stores", 13, 11)):
+    for lab, i0, i1 in (("  drain vmcnt + barrier", 10, 12), ("  epilogue: v + partial sums", 12, 14),
+                        ("  epilogue: mean reduce", 14, 15), ("  epilogue: var partials", 15, 16),
+                        ("  epilogue: var reduce", 16, 17), ("  epilogue: y + staging + sync", 17, 18),
+                        ("  epilogue: stores", 18, 13), ("  after", 13, 11)):
         d = t[:, i1] - t[:, i0]
         print(f"{lab:28s} mean {float(d.mean()):9.0f}  max {float(d.max()):9.0f} cycles")
 
