@@ -81,11 +81,16 @@ template <int KS, int NCH>
 __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   constexpr int MB = 7, BM = 16 * MB;
   constexpr int XROWS = BM + KS - 1;
-  constexpr int XPIECES = (XROWS + 1) / 2;           // 1 KiB LDS-DMA pieces of 2 rows
+  // x tile rows at a 544-byte pitch (512 + 32): the 16 rows of a fragment read fall in 16 distinct
+  // bank groups for any tap shift with NO swizzle, so a unit's k-step is a constant byte offset
+  // (the ds_read immediate) and the per-unit address work disappears
+  constexpr int XPITCH = 544;
+  constexpr int XPIECES = (XROWS * XPITCH + 1023) / 1024;  // 1 KiB LDS-DMA pieces
   constexpr int XP_PER_WAVE = (XPIECES + 3) / 4;
-  // the 16-byte zero slot sits at LDS offset 0: a masked fragment address is (address & 0)
+  // a 512-byte zero region at LDS offset 0: a masked row's fragment address is (address & 0) plus
+  // the k-step offset, which stays inside it
   constexpr int ZERO_OFF = 0;
-  constexpr int X_OFF = 128;
+  constexpr int X_OFF = 512;
   constexpr int H_OFF = X_OFF + 4 * XP_PER_WAVE * 1024;
   constexpr int F = NCH * kChunk;
   constexpr int B1_OFF = H_OFF + BM * 512;
@@ -138,7 +143,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     *reinterpret_cast<float4 *>(smem + EP_OFF + 16 * tid) =
         reinterpret_cast<const float4 *>(src)[tid % (kD / 4)];
   }
-  if (tid == 0) *reinterpret_cast<float4 *>(smem + ZERO_OFF) = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (tid < 32) *reinterpret_cast<float4 *>(smem + ZERO_OFF + 16 * tid) = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) asm volatile("" ::"v"(vmask[mb]));
 
@@ -147,16 +152,16 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   const rsrc_t wr = make_rsrc(p.w, p.w_bytes);
   const uint32_t xrow = (uint32_t)a.xs * 2u;
   {
-    const int prow = lane >> 5, pch = lane & 31;
 #pragma unroll
     for (int i = 0; i < XP_PER_WAVE; ++i) {
       const int pc = w + 4 * i;
-      const int r = 2 * pc + prow;
+      const int o = pc * 1024 + lane * 16;  // lane-linear LDS image: row o / XPITCH, byte o % XPITCH
+      const int r = o / XPITCH, within = o - r * XPITCH;
       const int gm = m0 - pad + r;
-      const bool ok = r < XROWS && gm >= 0 && gm < M;
+      const bool ok = r < XROWS && within < 512 && gm >= 0 && gm < M;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           xr, (__attribute__((address_space(3))) void *)(smem + X_OFF + pc * 1024), 16,
-          ok ? (uint32_t)gm * xrow + (uint32_t)xchunk(r, pch) * 16u : kOOB, 0, 0, 0);
+          ok ? (uint32_t)gm * xrow + (uint32_t)within : kOOB, 0, 0, 0);
     }
   }
 
@@ -188,28 +193,22 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   const int hrow0 = lane & 15;  // activation row (tile-relative) of block 0
   const int hi = lane >> 4;
   bf16x8 f0[MB], f1[MB];
-  // GEMM1 unit (tap, k-step ks): x rows shifted by the tap; a 16-row block step keeps (row & 7)
-  // LDS addresses of GEMM1 unit (tap, ks)'s fragments (computed a unit before the reads issue)
-  auto addr_x = [&](int tap, int ks, int (&ad)[MB]) {
-    const int r = hrow0 + tap;
-    const int base = X_OFF + r * 512 + (xchunk(r, 4 * ks + hi) << 4);
-    // masked rows: address & 0 = the zero slot. Pure VALU (sign-extended bit extract + and): a
-    // compare into a lane mask and a select would put SGPR round trips on the MFMA issue path
+  // GEMM1 fragment addresses of a tap: row (lane row + tap + 16 mb) of the x tile, channel group
+  // hi; a masked row's address is 0 (the zero region). Computed once per tap; a unit (tap, ks)
+  // reads base + 64 ks (an immediate offset).
+  auto bases_x = [&](int tap, int (&ad)[MB]) {
+    const int base = X_OFF + (hrow0 + tap) * XPITCH + hi * 16;
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       const int keep = (FFN_ABLATE & 16) ? -1 : __builtin_amdgcn_sbfe(vmask[mb], tap, 1);
-      ad[mb] = (base + mb * 8192) & keep;
+      ad[mb] = (base + mb * 16 * XPITCH) & keep;
     }
   };
-  auto issue_x = [&](const int (&ad)[MB], bf16x8 (&f)[MB]) {
+  auto issue_x = [&](const int (&ad)[MB], auto KSI, bf16x8 (&f)[MB]) {
     if (FFN_ABLATE & 4) return;
+    constexpr int off = decltype(KSI)::value * 64;
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) f[mb] = *reinterpret_cast<const bf16x8 *>(smem + ad[mb]);
-  };
-  auto read_x = [&](int tap, int ks, bf16x8 (&f)[MB]) {
-    int ad[MB];
-    addr_x(tap, ks, ad);
-    issue_x(ad, f);
+    for (int mb = 0; mb < MB; ++mb) f[mb] = *reinterpret_cast<const bf16x8 *>(smem + ad[mb] + off);
   };
   // GEMM2 unit q (32 hidden columns of the chunk)
   auto read_h = [&](int q, bf16x8 (&f)[MB]) {
@@ -279,33 +278,48 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   bar();
   stamp(1);
-  read_x(0, 0, f0);
+  int bxc[MB], bxn[MB];  // fragment bases of the current and the next tap
+  bases_x(0, bxc);
+  issue_x(bxc, std::integral_constant<int, 0>{}, f0);
 
-  // One GEMM1 unit k = g * DEPTH + s (ring slot s): read the next unit's B fragments (LDS latency
-  // hidden behind this unit's MFMAs), 28 MFMAs, then refill slot s with the unit DEPTH ahead
-  // (GEMM1 unit k + DEPTH, or in the last group GEMM2 unit s). Units alternate f0 / f1 by parity;
-  // NK1 and NK2 are even.
-  auto unit1 = [&](auto S, int c, int g) {
-    constexpr int s = decltype(S)::value;
-    // the next unit's fragments; after the chunk's last GEMM1 unit this reads "tap KS" (rows past the
-    // x tile, still inside LDS; overwritten by H's first unit): one loop body for every group
-    const int kn = g * DEPTH + s + 1;
-    if constexpr (s & 1)
-      read_x(kn >> 3, kn & 7, f0);
-    else
-      read_x(kn >> 3, kn & 7, f1);
-    if constexpr (s & 1)
+  // GEMM1, tap by tap: 8 units (k-steps of 32 channels) per tap, unit k = 8 tap + ks in ring slot
+  // ks % DEPTH. A unit reads the next unit's B fragments (LDS latency hidden behind its 28 MFMAs;
+  // after ks 7 with the next tap's bases), then refills its slot with the unit DEPTH ahead (GEMM1,
+  // or for the last tap's second half GEMM2 unit ks - 4 of this wave's rotated order). Units
+  // alternate f0 / f1 by parity. After the last tap the read is of "tap KS" (masked: zeros).
+  static_assert(DEPTH == 4 && kD / 32 == 8, "8 units per tap, 4-unit ring");
+  auto unit1 = [&](auto KSI, int c, int tap) {
+    constexpr int ks = decltype(KSI)::value, s = ks % DEPTH;
+    if constexpr (ks + 1 < 8) {
+      if constexpr (ks & 1)
+        issue_x(bxc, std::integral_constant<int, ks + 1>{}, f0);
+      else
+        issue_x(bxc, std::integral_constant<int, ks + 1>{}, f1);
+    } else {
+      issue_x(bxn, std::integral_constant<int, 0>{}, f0);
+    }
+    if constexpr (ks & 1)
       mma(acc1, pa[s], f1);
     else
       mma(acc1, pa[s], f0);
-    const bool more = g + 1 < NK1 / DEPTH;  // else: GEMM2 unit s of this chunk (scalar select)
-    load_at(S, more ? base1(c) + (uint32_t)((g + 1) * DEPTH + s) * (uint32_t)kUnit
-                    : base2(c) + (uint32_t)(((2 * w + s) & (NK2 - 1)) * kUnit));
+    const uint32_t k1 = (uint32_t)(tap * 8 + ks + DEPTH) * (uint32_t)kUnit;
+    if constexpr (ks + DEPTH < 8) {
+      load_at(std::integral_constant<int, s>{}, base1(c) + k1);
+    } else {
+      const bool more = tap + 1 < KS;  // scalar select: GEMM1 of the next tap, or GEMM2
+      load_at(std::integral_constant<int, s>{},
+              more ? base1(c) + k1 : base2(c) + (uint32_t)(((2 * w + ks - DEPTH) & (NK2 - 1)) * kUnit));
+    }
   };
 #pragma nounroll
   for (int c = 0; c < NCH; ++c) {
 #pragma nounroll
-    for (int g = 0; g < NK1 / DEPTH; ++g) static_for<DEPTH>([&](auto S) { unit1(S, c, g); });
+    for (int tap = 0; tap < KS; ++tap) {
+      bases_x(tap + 1, bxn);
+      static_for<8>([&](auto KSI) { unit1(KSI, c, tap); });
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) bxc[mb] = bxn[mb];
+    }
     // every wave is past its GEMM2 reads of the previous chunk's H: overwrite it. GEMM2 walks the
     // chunk's hidden columns starting at this wave's own block (units 2w, 2w + 1: its own writes,
     // no barrier); the barrier that makes the other waves' blocks visible comes after that first
@@ -325,8 +339,10 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
         bar();  // every wave's H block written and visible
       }
       const int qn = (2 * w + q + 1) & (NK2 - 1);
-      if constexpr (q + 1 == NK2)
-        read_x(0, 0, f0);  // the next chunk's first unit (x is never overwritten)
+      if constexpr (q + 1 == NK2) {  // the next chunk's first unit (x is never overwritten)
+        bases_x(0, bxc);
+        issue_x(bxc, std::integral_constant<int, 0>{}, f0);
+      }
       else if constexpr (q & 1)
         read_h(qn, f0);
       else
@@ -372,7 +388,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) {
         const int n = w * 64 + nb * 16 + 4 * hi;
-        const bf16x4 xv = *reinterpret_cast<const bf16x4 *>(smem + X_OFF + xr * 512 + (xchunk(xr, n >> 3) << 4) + (n & 7) * 2);
+        const bf16x4 xv = *reinterpret_cast<const bf16x4 *>(smem + X_OFF + xr * XPITCH + n * 2);
         f32x4 v = acc2[nb][mb];
         v[0] = v[0] + b2v[nb].x + (float)xv[0];
         v[1] = v[1] + b2v[nb].y + (float)xv[1];
