@@ -7,10 +7,11 @@ has run, so the path has one device->host read (runtime.host_meta) and cannot be
 
 * stage 1 (keyed by B, L_max and the control values): token embedding + PE, the encoder, the
   variance adaptor and the LengthRegulator scan (duration rounding, cumulative frames, mel_len),
-  plus the two-int32 meta vector [max(mel_len), out-of-vocabulary count];
+  plus the int32 meta vector [max(mel_len), sum(mel_len), out-of-vocabulary count];
 * the host reads the meta vector (one sync), raises IndexError on bad ids;
-* stage 2 (keyed by stage 1's key and T_out; an LRU of ``max_stage2`` graphs): the
-  LengthRegulator gather + PE, the decoder, mel_linear, the PostNet and the mel mask.
+* stage 2 (keyed by stage 1's key, T_out and the PostNet form; an LRU of ``max_stage2``
+  graphs): the LengthRegulator gather + PE, the decoder, mel_linear, the PostNet (valid-region
+  form when the batch is mostly padding, runtime._postnet) and the mel mask.
 
 Each entry keeps the weight pack it was captured against (model.packed): when the weights change the
 pack is rebuilt, and the stale graphs are dropped and recaptured on the next call. Each call
@@ -49,9 +50,7 @@ class SynthGraphs:
                             valences=s["valences"], texts=s["texts"], lens_src=s["src_lens"], Lx=Lx,
                             p_targets=s["p_targets"], e_targets=s["e_targets"], d_targets=None, mel_lens=None)
         st = R._stage1(P, va, g, p_c, d_c)
-        c = ops.bad_id_counter(s["texts"].device)
-        meta = torch.cat([st.mel_len.max().to(torch.int32).reshape(1), c])
-        return g, st, R._mask(s["src_lens"], Lx), meta
+        return g, st, R._mask(s["src_lens"], Lx), R.meta_vector(st.mel_len, s["texts"].device)
 
     def _capture(self, fn):
         """Warm fn up on a side stream (allocates per-stream workspaces outside the capture), then
@@ -106,15 +105,14 @@ class SynthGraphs:
         e1.meta_host.copy_(e1.meta, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()
         R.HOST_READS[0] += 1
-        T_out, bad = int(e1.meta_host[0]), int(e1.meta_host[1])
-        if bad:
-            ops.bad_id_counter(dev).zero_()
-            raise IndexError(f"fs2amd: {bad} token id(s) outside the embedding table (their encoder rows are NaN)")
-        key2 = key1 + (T_out,)
+        T_out, sum_len = R.check_meta(e1.meta_host, dev)
+        pn_valid = R.postnet_valid_rows(B, T_out, sum_len)
+        fused = sum_len >= R.FFN_FUSED_MIN_ROWS  # the decoder FFN's launch form (runtime.ffn_fused_ok)
+        key2 = key1 + (T_out, pn_valid, fused)
         e2 = self._g2.get(key2)
         if e2 is None:
             def body():
-                mel, post, st = R._stage2(P, e1.g, e1.st, T_out, T_out, controls[0])
+                mel, post, st = R._stage2(P, e1.g, e1.st, T_out, T_out, controls[0], pn_valid, sum_len)
                 return mel, post, R._mask(st.mel_len, T_out)
             graph, outs = self._capture(body)
             e2 = self._g2[key2] = SimpleNamespace(graph=graph, outs=outs)

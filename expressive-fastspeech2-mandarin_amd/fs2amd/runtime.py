@@ -151,7 +151,10 @@ def ffn_fused_ok(P, lp, h, layout):
     mode = os.environ.get("FS2_FFN_FUSED", "1")
     if mode == "0" or P.compute != L.FS2_BF16 or h.dtype != torch.bfloat16 or getattr(lp, "w12", None) is None:
         return False
-    rows = layout.capacity if layout is not None else h.shape[0] * h.shape[1]
+    # rows: the active packed rows when the host knows them (free-running: from the one host read),
+    # else the capacity. A launch is one round of 112-row tiles taking about one tile's time, so
+    # below ~146 tiles the two fs2_conv1d launches (many more, smaller tiles) are faster.
+    rows = h.shape[0] * h.shape[1] if layout is None else (getattr(layout, "rows_hint", None) or layout.capacity)
     return mode == "2" or rows >= FFN_FUSED_MIN_ROWS
 
 
@@ -334,7 +337,7 @@ def _stage1(P, va, g, p_control, d_control):
     return st
 
 
-def _stage2(P, g, st, T_out, T_dec, p_control):
+def _stage2(P, g, st, T_out, T_dec, p_control, postnet_valid=False, rows_hint=None):
     """LengthRegulator gather, decoder, mel_linear, PostNet for one utterance group."""
     dec_lens = st.mel_len if g.d_targets is None else g.mel_lens
     frame_level = not (st.phoneme_p and st.phoneme_e)
@@ -343,13 +346,14 @@ def _stage2(P, g, st, T_out, T_dec, p_control):
         # packed decoder: only the dec_lens frames of each utterance are computed
         # (cfg2: 24.9k of 27.5k rows, cfg4: 135k of 249k); mel_linear scatters back to [B, T, n_mel]
         lay = ops.SeqLayout(dec_lens, T_dec)
+        lay.rows_hint = rows_hint  # active rows when known on the host (free-running)
         x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype,
                           out_layout=lay)
         x = _stack(P, P.dec_layers, x, None, layout=lay, timed=True)
         mel_bf = _mel_copy(P, x, (lay.B, lay.T))
         mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
                          out_dtype=L.FS2_F32, src_layout=lay, out2=mel_bf)
-        return mel, _postnet(P, mel, mel_bf), st
+        return mel, _postnet(P, mel, mel_bf, dec_lens if postnet_valid else None), st
     # LR gather with the decoder's position encoding fused (frame-level variance needs the bare
     # expanded x first, so the PE add moves to a second pass in that configuration)
     if frame_level:
@@ -370,7 +374,7 @@ def _stage2(P, g, st, T_out, T_dec, p_control):
     mel_bf = _mel_copy(P, x, x.shape[:2])
     mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
                      out_dtype=L.FS2_F32, out2=mel_bf)
-    return mel, _postnet(P, mel, mel_bf), st
+    return mel, _postnet(P, mel, mel_bf, dec_lens if postnet_valid else None), st
 
 
 def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, max_src_len, mels, mel_lens,
@@ -425,7 +429,7 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     if d_targets is None or not max_mel_len:
         # the ONE host read of the free-running path: max(mel_len) and the out-of-vocabulary id
         # count in one device->host copy
-        max_len = host_meta(mel_len, dev)
+        max_len, sum_len = host_meta(mel_len, dev)
         T_out = int(max_mel_len) if max_mel_len else max_len
     else:
         T_out = int(max_mel_len)
@@ -434,6 +438,8 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     if mel_masks is None or mel_masks.shape[1] != T_out:
         raise RuntimeError(f"decoder mask width {None if mel_masks is None else mel_masks.shape[1]} != length-"
                            f"regulated length {T_out} (the reference fails here too: Models.py:157)")
+    # free-running batches padded to one long utterance: the PostNet's valid-region form
+    pn_valid = d_targets is None and T_out == max_len and postnet_valid_rows(B, T_out, sum_len)
     T_dec = min(T_out, P.max_seq_len) if model.training else T_out
     if T_dec != T_out:
         mel_masks = mel_masks[:, :T_dec]
@@ -441,7 +447,8 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     res = []
     for i, (g, st) in enumerate(zip(groups, sts)):
         with fj.ctx(i):
-            res.append(_stage2(P, g, st, T_out, T_dec, p_control))
+            res.append(_stage2(P, g, st, T_out, T_dec, p_control, pn_valid,
+                               sum_len if (d_targets is None and n == 1) else None))
     if n == 1:
         mel, postnet_mel, st = res[0]
         out = (mel, postnet_mel, st.p_pred, st.e_pred, st.log_d, st.d_rounded, st.mel_len)
@@ -461,20 +468,38 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
 HOST_READS = [0]  # device->host reads made by the forward path (tests assert one per free-running call)
 
 
-def host_meta(mel_len, dev):
-    """max(mel_len) with the fs2_embed_pe out-of-vocabulary counter in the same device->host copy;
-    IndexError (the reference's nn.Embedding error) when the counter is set."""
+def meta_vector(mel_len, dev):
+    """[max(mel_len), sum(mel_len), out-of-vocabulary count] as int32 on the device (one copy)."""
     c = ops.bad_id_counter(dev)
-    parts = [mel_len.max().to(torch.int32).reshape(1) if mel_len.numel() else torch.zeros(1, dtype=torch.int32,
-                                                                                          device=dev)]
-    if c is not None:
-        parts.append(c)
-    meta = torch.cat(parts).cpu()
+    if mel_len.numel():
+        parts = [mel_len.max().to(torch.int32).reshape(1), mel_len.sum().to(torch.int32).reshape(1)]
+    else:
+        parts = [torch.zeros(2, dtype=torch.int32, device=dev)]
+    parts.append(c if c is not None else torch.zeros(1, dtype=torch.int32, device=dev))
+    return torch.cat(parts)
+
+
+def check_meta(meta, dev):
+    """Host side of the one read: IndexError (the reference's nn.Embedding error) when the
+    out-of-vocabulary counter is set; returns (max(mel_len), sum(mel_len))."""
+    if int(meta[2]):
+        ops.bad_id_counter(dev).zero_()
+        raise IndexError(f"fs2amd: {int(meta[2])} token id(s) outside the embedding table (their encoder rows are NaN)")
+    return int(meta[0]), int(meta[1])
+
+
+def host_meta(mel_len, dev):
+    """The free-running path's ONE device->host read: max(mel_len), sum(mel_len) and the
+    out-of-vocabulary counter in one copy."""
+    meta = meta_vector(mel_len, dev).cpu()
     HOST_READS[0] += 1
-    if c is not None and int(meta[1]):
-        c.zero_()
-        raise IndexError(f"fs2amd: {int(meta[1])} token id(s) outside the embedding table (their encoder rows are NaN)")
-    return int(meta[0])
+    return check_meta(meta, dev)
+
+
+def postnet_valid_rows(B, T, sum_len):
+    """Use the PostNet's valid-region form when the padded batch is mostly padding (free-running
+    synthesis: one long utterance sets T for all): its rows <= sum(len) + 20 B against B * T."""
+    return postnet_valid_region_on() and B > 0 and sum_len + POSTNET_MARGIN * B < 0.5 * B * T
 
 
 def _mel_copy(P, x, bt):
@@ -486,10 +511,45 @@ def _mel_copy(P, x, bt):
     return torch.empty(*bt, P.mel_w.shape[0], device=x.device, dtype=torch.bfloat16)
 
 
-def _postnet(P, mel, mel_bf=None):
-    """PostNet (BN folded, transformer/Layers.py:92-137) + residual (fastspeech2.py:136), padded
-    [B, T, n_mel] like the reference: its padded frames (bias values) feed the k5 taps. mel_bf:
-    optional bf16 copy of mel, the first conv's input (the residual stays f32)."""
+# PostNet = 5 Conv1d(k=5, pad=2): an output frame depends on input frames within +-10.
+POSTNET_REACH = 10
+POSTNET_MARGIN = 2 * POSTNET_REACH
+
+
+def postnet_valid_region_on():
+    return os.environ.get("FS2_POSTNET_VALID", "1") != "0"
+
+
+def _postnet_consts(P, mel_bf_like):
+    """The PostNet output wherever its input is all padding: every padded mel frame is mel_linear's
+    bias (the decoder output there is masked to 0), so away from the valid frames the output is
+    one constant row c, and its last POSTNET_REACH frames before T (zero padding beyond T) are one
+    fixed block. Both come from one [1, 40, n_mel] run of the same kernels on bias-valued frames
+    (row 20 and rows 30..39), cached per weight pack; computed outside any graph capture."""
+    ent = getattr(P, "_postnet_consts", None)
+    if ent is None:
+        if mel_bf_like is not None and mel_bf_like.is_cuda and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("PostNet constants must be computed before graph capture (run the forward once)")
+        b = P.mel_b.float().reshape(1, 1, -1).expand(1, 2 * POSTNET_MARGIN, -1).contiguous()
+        y = _postnet(P, b, b.to(torch.bfloat16) if mel_bf_like is not None else None)
+        ent = (y[0, POSTNET_MARGIN].clone(), y[0, 2 * POSTNET_MARGIN - POSTNET_REACH:].clone())
+        P._postnet_consts = ent
+    return ent
+
+
+def _postnet(P, mel, mel_bf=None, mel_len=None):
+    """PostNet (BN folded, transformer/Layers.py:92-137) + residual (fastspeech2.py:136) with the
+    reference's padded [B, T, n_mel] semantics: padded frames (bias values) feed the k5 taps and
+    get outputs too. mel_bf: optional bf16 copy of mel, the first conv's input (the residual stays
+    f32).
+
+    mel_len given: the convs run on packed rows over each utterance's valid frames + 20 (the rest
+    of an utterance more than 40 frames shorter than T is constant input): its outputs are exact
+    on the first len + 10 frames; frames from len + 10 to T - 10 are the constant row and the last
+    10 the fixed block (_postnet_consts). An utterance within 40 frames of T runs whole. Free-
+    running cfg2 (T = 959 for 11.1k valid frames) computes 12.4k rows instead of 61.4k."""
+    if mel_len is not None and postnet_valid_region_on() and mel.shape[0] > 0:
+        return _postnet_valid(P, mel, mel_bf, mel_len)
     y = mel if mel_bf is None else mel_bf
     n_pn = len(P.postnet)
     for i, lp in enumerate(P.postnet):
@@ -500,6 +560,42 @@ def _postnet(P, mel, mel_bf=None):
             y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute, epilogue=L.EPI_BIAS_RES,
                            out_dtype=L.FS2_F32, residual=mel)
     return y
+
+
+def _postnet_valid(P, mel, mel_bf, mel_len):
+    B, T, C = mel.shape
+    c, tail = _postnet_consts(P, mel_bf)
+    ml = mel_len.to(torch.int64)
+    lens2 = torch.where(ml + 2 * POSTNET_MARGIN > T, torch.full_like(ml, T), ml + POSTNET_MARGIN)
+    lay = ops.SeqLayout(lens2, T)
+    cap = lay.capacity
+    rm = lay.rowmap.to(torch.int64)
+    dst = torch.where(rm >= 0, rm, torch.full_like(rm, cap))  # padded row -> packed row (cap: dropped)
+
+    def pack(t):
+        out = torch.empty(cap + 1, t.shape[-1], device=t.device, dtype=t.dtype)
+        out.index_copy_(0, dst, t.reshape(B * T, -1))
+        return out[:cap]
+
+    y = pack(mel if mel_bf is None else mel_bf)
+    res = pack(mel)
+    n_pn = len(P.postnet)
+    for i, lp in enumerate(P.postnet):
+        if i < n_pn - 1:
+            y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute,
+                           epilogue=L.EPI_BIAS_TANH, out_dtype=P.act_dtype, layout=lay)
+        else:
+            y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute, epilogue=L.EPI_BIAS_RES,
+                           out_dtype=L.FS2_F32, residual=res, layout=lay)
+    # assemble [B, T, C]: computed rows where exact, else the constant row / the tail block
+    t = torch.arange(T, device=mel.device)
+    whole = (lens2 == T)[:, None]
+    keep = whole | (t[None, :] < (lens2 - POSTNET_REACH)[:, None])            # [B, T]
+    in_tail = t[None, :] >= T - POSTNET_REACH
+    const = torch.where(in_tail[..., None], tail[(t - (T - POSTNET_REACH)).clamp(min=0)][None], c[None, None])
+    src = torch.where(keep.reshape(-1), rm, torch.full_like(rm, cap))
+    y_ext = torch.cat([y, y.new_zeros(1, C)])
+    return torch.where(keep[..., None], y_ext.index_select(0, src).view(B, T, C), const)
 
 
 def _add_pe(x, pe):

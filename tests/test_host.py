@@ -219,6 +219,23 @@ class _FakeForkJoin:
         pass
 
 
+def stub_seq_layout(monkeypatch, ops):
+    """With the kernels stubbed fs2_seq_layout writes nothing: fill cu / rowmap on the host (the
+    PostNet's valid-region path indexes with the row map in torch)."""
+    real_layout_init = ops.SeqLayout.__init__
+
+    def layout_init(self, lens, T):
+        real_layout_init(self, lens, T)
+        ln = lens.to(torch.int64).clamp(0, T)
+        cu = torch.cat([ln.new_zeros(1), ln.cumsum(0)])
+        t = torch.arange(T)
+        rm = torch.where(t[None, :] < ln[:, None], cu[:-1, None] + t[None, :], torch.full((1,), -1))
+        self.rowmap.copy_(rm.reshape(-1).to(torch.int32))
+        self.cu.copy_(cu.to(torch.int32))
+
+    monkeypatch.setattr(ops.SeqLayout, "__init__", layout_init)
+
+
 @pytest.mark.parametrize("packed", ["1", "0"])
 @pytest.mark.parametrize("teacher", [True, False])
 @pytest.mark.parametrize("streams", ["1", "2"])
@@ -236,6 +253,7 @@ def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher, streams):
     monkeypatch.setenv("FS2_PACKED_DECODER", packed)
     monkeypatch.setenv("FS2_STREAMS", streams)
     monkeypatch.setattr(runtime, "_ForkJoin", _FakeForkJoin)
+    stub_seq_layout(monkeypatch, ops)
     m = _model().eval()
     args = synth_batch(17, 6, 11, seed=2, teacher=teacher)
     if not teacher:
@@ -254,7 +272,8 @@ def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher, streams):
     assert out[0].shape[0] == 17 and out[9].shape == (17,)
     n_conv = rec.calls.count("fs2_conv1d")
     k = int(streams)
-    # per group: 10 FFT blocks x 4 GEMMs + 3 VPs x 2 + mel_linear + 5 PostNet convs
+    # per group: 10 FFT blocks x 4 GEMMs + 3 VPs x 2 + mel_linear + 5 PostNet convs (these batches
+    # are not mostly padding: the padded PostNet form)
     assert n_conv == k * (10 * 4 + 6 + 1 + 5), rec.calls
     assert rec.calls.count("fs2_attention") == k * 10
     assert ("fs2_seq_layout" in rec.calls) == (packed == "1")

@@ -140,9 +140,10 @@ def test_positional_call_dry_run(corpus, monkeypatch):
     from fs2amd import ops, runtime, _lib
     from fs2amd.model import FastSpeech2
     from fs2amd.pipeline import Dataset, TextDataset, to_device
-    from test_host import _FakeForkJoin, _RecordingLib
+    from test_host import _FakeForkJoin, _RecordingLib, stub_seq_layout
     from _common import oracle_state_dict
 
+    stub_seq_layout(monkeypatch, ops)
     rec = _RecordingLib(_lib.load())
     monkeypatch.setattr(ops, "_lib", rec)
     monkeypatch.setattr(ops, "_gpu", lambda *a: None)
