@@ -50,6 +50,16 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class WconvDesc(ctypes.Structure):
+    """Mirror of ``fs2_wconv_desc`` (include/fs2hip.h)."""
+
+    _fields_ = [
+        ("x", _p), ("x_row_stride", _i64), ("w", _p), ("bias", _p),
+        ("B", _i), ("T", _i), ("Cin", _i), ("N", _i), ("KS", _i), ("pad", _i), ("epilogue", _i),
+        ("out", _p), ("out_row_stride", _i64),
+    ]
+
+
 class FfnDesc(ctypes.Structure):
     """Mirror of ``fs2_ffn_desc`` (include/fs2hip.h)."""
 
@@ -72,6 +82,8 @@ SIGNATURES = {
     "fs2_conv1d": (_i, [ctypes.POINTER(ConvDesc), _p]),
     "fs2_ffn": (_i, [ctypes.POINTER(FfnDesc), _p]),
     "fs2_ffn_weight_elems": (ctypes.c_int64, [_i, _i]),
+    "fs2_wconv": (_i, [ctypes.POINTER(WconvDesc), _p]),
+    "fs2_wconv_weight_elems": (ctypes.c_int64, [_i, _i, _i]),
     "fs2_attention": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p]),
     "fs2_embed_pe": (_i, [_p, _p, _i, _p, _i, _i, _i, _p, _i, _p, _p]),
     "fs2_attention_bwd": (_i, [_p, _i, _i64, _p, _i64, _p, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p, _i64, _p]),

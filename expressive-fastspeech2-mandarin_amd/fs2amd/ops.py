@@ -295,6 +295,39 @@ def pack_ffn_weights(w1, w2):
     return torch.cat([a.reshape(-1), b.reshape(-1)]).to(torch.bfloat16).contiguous()
 
 
+def pack_wconv_weight(w, scale=None):
+    """nn.Conv1d weight [N, Cin, KS] (optionally scaled per output channel: BatchNorm folding, in
+    f32 then rounded once like pack_conv_weight) -> the fs2_wconv buffer, flat bf16 in MFMA
+    fragment order [N/64][KS][Cin/32][4][4][16][8] (include/fs2hip.h)."""
+    w = w.detach().float()
+    if scale is not None:
+        w = w * scale.detach().float().view(-1, 1, 1)
+    N, cin, ks = w.shape
+    assert N % 64 == 0 and cin % 32 == 0, (N, cin)
+    a = w.permute(0, 2, 1).reshape(N // 64, 4, 16, ks, cin // 32, 4, 8).permute(0, 3, 4, 1, 5, 2, 6)
+    return a.reshape(-1).to(torch.bfloat16).contiguous()
+
+
+def wconv(x, w_packed, bias, *, ks, pad, out=None):
+    """PostNet Conv1d(512, 512, k=5) + folded BatchNorm + tanh on padded bf16 rows [B, T, 512]
+    (fs2_wconv; w_packed from :func:`pack_wconv_weight`)."""
+    _gpu(x, w_packed, bias)
+    if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
+        raise TypeError("fs2amd.wconv: bf16 activations and weights only")
+    B, T, cin = x.shape
+    N = bias.numel()
+    assert w_packed.is_contiguous() and w_packed.numel() == _lib.fs2_wconv_weight_elems(ks, cin, N)
+    if out is None:
+        out = torch.empty(B, T, N, device=x.device, dtype=torch.bfloat16)
+    d = L.WconvDesc()
+    d.x, d.x_row_stride = x.data_ptr(), _rows(x, "x")
+    d.w, d.bias = w_packed.data_ptr(), bias.data_ptr()
+    d.B, d.T, d.Cin, d.N, d.KS, d.pad, d.epilogue = B, T, cin, N, ks, pad, L.EPI_BIAS_TANH
+    d.out, d.out_row_stride = out.data_ptr(), _rows(out, "out")
+    L.check(_lib.fs2_wconv(ctypes.byref(d), _stream(x)), "fs2_wconv")
+    return out
+
+
 def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=None, layout=None, out=None):
     """PositionwiseFeedForward + residual + LayerNorm + mask in one launch (fs2_ffn): bf16 rows of
     256 (padded [B, T, 256] or packed [B*T, 256] in ``layout``); ``w_packed`` from

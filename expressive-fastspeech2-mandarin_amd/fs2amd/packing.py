@@ -20,7 +20,8 @@ from types import SimpleNamespace
 import torch
 
 from . import _lib as L
-from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split, pack_ffn_weights
+from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split, pack_ffn_weights, \
+    pack_wconv_weight
 
 
 def _f32(t, device):
@@ -126,9 +127,13 @@ def _postnet(pn, device, compute):
         conv, bn = seq[0].conv, seq[1]
         s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
         b = (conv.bias.detach().float() - bn.running_mean.detach().float()) * s + bn.bias.detach().float()
+        wfr = None
+        if compute == L.FS2_BF16 and conv.in_channels == 512 and conv.out_channels == 512 and conv.kernel_size[0] == 5:
+            # the weight-streamed kernel's fragment order (fs2_wconv)
+            wfr = pack_wconv_weight(conv.weight.to(device), scale=s.to(device))
         layers.append(SimpleNamespace(w=pack_conv_weight(conv.weight.to(device), compute, scale=s.to(device)),
                                       b=_f32(b, device), k=conv.kernel_size[0], p=conv.padding[0],
-                                      cin=conv.in_channels, cout=conv.out_channels))
+                                      cin=conv.in_channels, cout=conv.out_channels, wfr=wfr))
     return layers
 
 

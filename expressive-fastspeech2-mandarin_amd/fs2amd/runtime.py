@@ -516,6 +516,10 @@ POSTNET_REACH = 10
 POSTNET_MARGIN = 2 * POSTNET_REACH
 
 
+def wconv_on():
+    return os.environ.get("FS2_WCONV", "1") != "0"
+
+
 def postnet_valid_region_on():
     return os.environ.get("FS2_POSTNET_VALID", "1") != "0"
 
@@ -553,7 +557,10 @@ def _postnet(P, mel, mel_bf=None, mel_len=None):
     y = mel if mel_bf is None else mel_bf
     n_pn = len(P.postnet)
     for i, lp in enumerate(P.postnet):
-        if i < n_pn - 1:
+        if i < n_pn - 1 and getattr(lp, "wfr", None) is not None and wconv_on() and y.dtype == torch.bfloat16:
+            # 512 -> 512 convs: the weight-streamed kernel (fs2_wconv)
+            y = ops.wconv(y, lp.wfr, lp.b, ks=lp.k, pad=lp.p)
+        elif i < n_pn - 1:
             y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute,
                            epilogue=L.EPI_BIAS_TANH, out_dtype=P.act_dtype)
         else:

@@ -199,6 +199,29 @@ int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream);
 int64_t fs2_ffn_weight_elems(int KS, int F); /* F*KS*256 + 256*F */
 
 /*
+ * fs2_wconv — a PostNet convolution (transformer/Layers.py:92-137: Conv1d(512, 512, k=5, pad=2) +
+ * BatchNorm1d (eval: folded into w / bias on the host) + tanh) on padded [B, T] rows:
+ *   y[m, n] = tanh( sum_{k<KS} sum_c x[m + k - pad, c] * w[n][c][k] + bias[n] )   (per-sequence zero taps)
+ * bf16 x / out (out must not alias x), f32 accumulation and tanh. w in MFMA fragment order:
+ * [N/64][KS][Cin/32][4][4][16][8], element (q, k, s, b, h, r, e) = w[64q + 16b + r][32s + 8h + e][k]
+ * (fs2_wconv_weight_elems(KS, Cin, N) elements). Shapes: Cin = N = 512, KS = 5, pad <= KS - 1,
+ * epilogue FS2_EPI_BIAS_TANH (FS2_EUNSUPPORTED otherwise: use fs2_conv1d).
+ */
+typedef struct fs2_wconv_desc {
+  const void *x;            /* bf16 [B*T, >= Cin]                                                 */
+  int64_t x_row_stride;
+  const void *w;            /* bf16, fragment order (see above)                                   */
+  const float *bias;        /* [N] (BatchNorm folded)                                             */
+  int B, T, Cin, N, KS, pad;
+  int epilogue;             /* FS2_EPI_BIAS_TANH                                                  */
+  void *out;                /* bf16 [B*T, >= N]                                                   */
+  int64_t out_row_stride;
+} fs2_wconv_desc;
+
+int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream);
+int64_t fs2_wconv_weight_elems(int KS, int Cin, int N); /* N*KS*Cin */
+
+/*
  * fs2_attention — ScaledDotProductAttention with a key-padding mask, all heads.
  * Replaces transformer/Modules.py:14-25 (bmm, /temperature, masked_fill(-inf), softmax(dim=2),
  * bmm) and the head split/merge permutes of SubLayers.py:42-52.

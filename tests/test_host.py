@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
     lib = _lib.load()
     declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
-    assert len(declared) == len(_lib.SIGNATURES) == 18
+    assert len(declared) == len(_lib.SIGNATURES) == 20
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
@@ -58,17 +58,20 @@ int main(void){ P(x) P(x_row_stride) P(w) P(B) P(compute) P(residual) P(res_row_
             assert getattr(_lib.ConvDesc, name).offset == int(off), name
 
 
-def test_ffn_desc_layout_matches_header():
-    """ctypes mirror of fs2_ffn_desc has the C layout (every field's offset, and the size)."""
+@pytest.mark.parametrize("cname,pyname", [("fs2_ffn_desc", "FfnDesc"), ("fs2_wconv_desc", "WconvDesc")])
+def test_ffn_desc_layout_matches_header(cname, pyname):
+    """ctypes mirrors of fs2_ffn_desc / fs2_wconv_desc have the C layout (every field's offset, and
+    the size)."""
     import subprocess
     import tempfile
 
     from fs2amd import _lib
 
-    names = [f[0] for f in _lib.FfnDesc._fields_]
+    cls = getattr(_lib, pyname)
+    names = [f[0] for f in cls._fields_]
     src = "#include <stdio.h>\n#include <stddef.h>\n#include \"fs2hip.h\"\nint main(void){" + "".join(
-        f'printf("{n} %zu\\n", offsetof(fs2_ffn_desc, {n}));' for n in names) + \
-        'printf("size %zu\\n", sizeof(fs2_ffn_desc)); }\n'
+        f'printf("{n} %zu\\n", offsetof({cname}, {n}));' for n in names) + \
+        f'printf("size %zu\\n", sizeof({cname})); }}\n'
     d = tempfile.mkdtemp()
     with open(os.path.join(d, "t.c"), "w") as f:
         f.write(src)
@@ -81,9 +84,9 @@ def test_ffn_desc_layout_matches_header():
             continue
         name, off = line.split()
         if name == "size":
-            assert int(off) == ctypes.sizeof(_lib.FfnDesc)
+            assert int(off) == ctypes.sizeof(cls)
         else:
-            assert getattr(_lib.FfnDesc, name).offset == int(off), name
+            assert getattr(cls, name).offset == int(off), name
             seen += 1
     assert seen == len(names)
 
@@ -110,6 +113,17 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     assert lib.fs2_ffn(ctypes.byref(fd), None) == _lib.FS2_EINVAL
     assert lib.fs2_ffn_weight_elems(9, 1024) == 1024 * 9 * 256 + 256 * 1024
     assert lib.fs2_ffn_weight_elems(3, 512) == 512 * 3 * 256 + 256 * 512
+    wd = _lib.WconvDesc()
+    assert lib.fs2_wconv(ctypes.byref(wd), None) == _lib.FS2_EINVAL
+    wd.x, wd.w, wd.bias, wd.out = 512, 256, 256, 1024
+    wd.B, wd.T, wd.Cin, wd.N, wd.KS, wd.pad, wd.x_row_stride, wd.out_row_stride = 2, 8, 512, 512, 5, 2, 512, 512
+    wd.epilogue = _lib.EPI_BIAS_RELU
+    assert lib.fs2_wconv(ctypes.byref(wd), None) == _lib.FS2_EUNSUPPORTED
+    wd.epilogue, wd.KS = _lib.EPI_BIAS_TANH, 3
+    assert lib.fs2_wconv(ctypes.byref(wd), None) == _lib.FS2_EUNSUPPORTED
+    wd.KS, wd.out = 5, wd.x
+    assert lib.fs2_wconv(ctypes.byref(wd), None) == _lib.FS2_EINVAL
+    assert lib.fs2_wconv_weight_elems(5, 512, 512) == 512 * 5 * 512
 
     assert lib.fs2_attention(None, 0, 768, None, 1, 1, 2, 128, 11.3, None, 256, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_lr_durations(None, 0, 1.0, 1, 1, None, None, None, None) == _lib.FS2_EINVAL

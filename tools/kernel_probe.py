@@ -83,6 +83,10 @@ def main():
         pl = P.postnet[1]
         fn = lambda: ops.conv1d(y, pl.w, pl.b, cin=512, ks=5, pad=2, compute=P.compute, epilogue=L.EPI_BIAS_TANH,
                                 out_dtype=P.act_dtype)
+    elif a.kernel == "wconv":  # the same PostNet conv on the weight-streamed kernel (fs2_wconv)
+        y = rnd(B, T, 512)
+        pl = P.postnet[1]
+        fn = lambda: ops.wconv(y, pl.wfr, pl.b, ks=5, pad=2)
     elif a.kernel in ("postnet_first", "postnet_first_bf", "postnet_last"):
         # PostNet 80->512 (f32 mel in, or its bf16 copy) / 512->80 + residual
         mel = torch.randn(B, T, 80, generator=g).to(dev)
