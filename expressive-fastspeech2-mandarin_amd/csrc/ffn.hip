@@ -53,7 +53,14 @@ struct FfnArgs {
   const bf16 *w;       // fs2_ffn_desc.w: w_1 | w_2 in fragment order (include/fs2hip.h)
   const float *b1;     // [F]
   uint32_t w_bytes;
+  int nsplit;          // split-hidden form: workgroups per row tile (1 = off)
+  int ntiles;          // row tiles of the launch
+  int *cnt;            // [tiles] arrival counters (zero between launches)
+  void *part;          // f32 partial Y^T accumulators, kPartBytes per (tile, split)
+  uint32_t part_bytes;
 };
+
+constexpr int kPartBytes = 4 * 4 * 7 * 64 * 16;  // 4 waves x acc2[4][MB = 7] x 64 lanes x 16 B
 
 constexpr int64_t ffn_weight_elems(int KS, int F) { return (int64_t)F * KS * kD + (int64_t)kD * F; }
 
@@ -108,9 +115,23 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   const ConvArgs &a = p.e;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // weight-row quarter (64 rows)
-  const int M = a.rows_dev != nullptr ? *a.rows_dev : a.M;
-  const int m0 = blockIdx.x * BM;
+  const int M = a.rows_dev != nullptr ? min(*a.rows_dev, a.M) : a.M;
+  // split-hidden form: the grid (a multiple of 8) walks (split, tile) split-major and XCD-major, so
+  // an XCD runs (mostly) ONE split and its L2 holds only that split's 1.3 MB of weights (tile-major
+  // order puts all 5.2 MB through every 4 MB L2; measured equal at the encoder shape, where the
+  // partial hand-off, not the weight stream, is what the split form pays for)
+  const int S = p.nsplit;
+  int tile = blockIdx.x, split = 0;
+  if (S > 1) {
+    const int ntiles = p.ntiles;
+    const int L = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    split = L / ntiles;
+    tile = L - split * ntiles;
+    if (split >= S) return;
+  }
+  const int m0 = tile * BM;
   if (m0 >= M) return;
+  const int nchunks = NCH / S, c0 = split * nchunks, cend = c0 + nchunks;
   const int pad = a.pad, T = a.T;
 
   // ---- tap validity of this lane's activation rows: bit tap of vmask[mb] is set when the row
@@ -187,7 +208,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     }
     __builtin_amdgcn_sched_barrier(0);
   };
-  static_for<DEPTH>([&](auto S) { load_at(S, base1(0) + (uint32_t)(decltype(S)::value * kUnit)); });
+  static_for<DEPTH>([&](auto I) { load_at(I, base1(c0) + (uint32_t)(decltype(I)::value * kUnit)); });
 
   // ---- B fragments
   const int hrow0 = lane & 15;  // activation row (tile-relative) of block 0
@@ -312,7 +333,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     }
   };
 #pragma nounroll
-  for (int c = 0; c < NCH; ++c) {
+  for (int c = c0; c < cend; ++c) {
 #pragma nounroll
     for (int tap = 0; tap < KS; ++tap) {
       bases_x(tap + 1, bxn);
@@ -330,7 +351,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     stamp(3 + 2 * c);
     read_h(2 * w, f0);
-    const uint32_t next1 = c + 1 < NCH ? base1(c + 1) : 0u;  // past the last unit: harmless reloads
+    const uint32_t next1 = c + 1 < cend ? base1(c + 1) : 0u;  // past the last unit: harmless reloads
     static_for<NK2>([&](auto Q) {
       constexpr int q = decltype(Q)::value;  // this wave's q-th GEMM2 unit: hidden columns 32 * qq
       constexpr int s = q % DEPTH;
@@ -368,6 +389,67 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the harmless past-the-end weight loads
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   stamp(4 + 2 * NCH);
+  if (S > 1) {
+    // split-hidden hand-off (as conv_gemm.hip's splitk_fixup): every split stores its partial Y^T
+    // with sc1 (write-through) 16-byte stores, drains, and one lane adds to the tile's counter; the
+    // split whose add comes last resets the counter, acquires, and sums the partials in split order
+    // (its own from registers). The other splits are done.
+    const rsrc_t pr = make_rsrc(p.part, p.part_bytes);
+    auto pofs = [&](int sp, int nb, int mb) {
+      return (uint32_t)(tile * S + sp) * (uint32_t)kPartBytes + (uint32_t)((((w * 4 + nb) * MB + mb) * 64 + lane) * 16);
+    };
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, acc2[nb][mb]),
+                                               pr, pofs(split, nb, mb), 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int *flag = reinterpret_cast<int *>(smem + RED_OFF);
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == S - 1;
+      if (last) {
+        __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset for the next launch
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      *flag = last;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (!*flag) return;
+    __syncthreads();  // flag read by every wave before the epilogue reuses the slot
+    // split order, one other split's 28 loads in flight together (a per-load branch on the split
+    // index serialised every load's full latency); the sum goes into the dead H^T accumulators
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc1[nb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < S; ++sp) {
+      if (sp == split) {
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) acc1[nb][mb] += acc2[nb][mb];
+      } else {
+        f32x4 v[4][MB];
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb)
+            v[nb][mb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, pofs(sp, nb, mb), 0, 16));
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) acc1[nb][mb] += v[nb][mb];
+      }
+    }
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc2[nb][mb] = acc1[nb][mb];
+  }
   {
     float *red = reinterpret_cast<float *>(smem + RED_OFF);
     const float inv_n = 1.0f / 256.0f;
@@ -531,6 +613,8 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   if (d->rows_dev != nullptr && (d->lens != nullptr || d->addvec1 != nullptr || d->addvec2 != nullptr))
     return FS2_EINVAL;
   if (d->x == d->out) return FS2_EINVAL;  // other tiles re-read x rows (halo, residual)
+  const int S = d->nsplit <= 1 ? 1 : d->nsplit;
+  if (!(S == 1 || S == 2 || S == 4) || S > d->F / kChunk) return FS2_EINVAL;
   const int64_t M64 = (int64_t)d->B * d->T;
   if (M64 > 0x7fffff00LL) return FS2_EINVAL;
   if (M64 == 0) return FS2_OK;
@@ -538,7 +622,7 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   const int64_t wb = ffn_weight_elems(d->KS, d->F) * 2;
   if (xb >= (1LL << 31)) return FS2_EUNSUPPORTED;
 
-  FfnArgs p;
+  FfnArgs p{};
   ConvArgs &a = p.e;
   a = ConvArgs{};
   a.x = d->x;
@@ -579,7 +663,22 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   p.b1 = d->b1;
   p.w_bytes = (uint32_t)wb;
   constexpr int BM = 112;
-  const int nwg = (int)((M64 + BM - 1) / BM);
+  if (d->rows_max < 0) return FS2_EINVAL;
+  const int64_t Mg = (d->rows_dev != nullptr && d->rows_max > 0 && d->rows_max < M64) ? d->rows_max : M64;
+  a.M = (int)Mg;
+  const int ntiles = (int)((Mg + BM - 1) / BM);
+  int nwg = ntiles;
+  p.nsplit = S;
+  p.ntiles = ntiles;
+  if (S > 1) {
+    if (d->splitk_ws == nullptr || ntiles > 1024 ||
+        d->splitk_ws_bytes < 4096 + (int64_t)ntiles * S * kPartBytes || (int64_t)ntiles * S * kPartBytes >= (1LL << 31))
+      return FS2_EINVAL;
+    p.cnt = static_cast<int *>(d->splitk_ws);
+    p.part = static_cast<char *>(d->splitk_ws) + 4096;
+    p.part_bytes = (uint32_t)((int64_t)ntiles * S * kPartBytes);
+    nwg = (ntiles * S + 7) & ~7;
+  }
   const int nch = d->F / kChunk;
   hipStream_t s = as_stream(stream);
   // instantiated shapes: kernel 9 (model.yaml conv_kernel_size [9, 1]) or 3, F = 1024 or 512

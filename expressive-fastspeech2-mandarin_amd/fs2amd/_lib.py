@@ -71,6 +71,7 @@ class FfnDesc(ctypes.Structure):
         ("lens", _p), ("addvec1", _p), ("addvec2", _p),
         ("out", _p), ("out_row_stride", _i64),
         ("rows_dev", _p), ("row_pos", _p),
+        ("nsplit", _i), ("splitk_ws", _p), ("splitk_ws_bytes", _i64), ("rows_max", _i),
     ]
 
 

@@ -328,10 +328,32 @@ def wconv(x, w_packed, bias, *, ks, pad, out=None):
     return out
 
 
-def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=None, layout=None, out=None):
+FFN_TILE_ROWS = 112
+FFN_SLOTS = 256  # workgroups resident at once (1 per CU)
+FFN_PART_BYTES = 4 * 4 * 7 * 64 * 16  # f32 partial accumulators per (tile, split), ffn.hip kPartBytes
+
+
+def ffn_nsplit(rows, F):
+    """Workgroups per 112-row tile for fs2_ffn's split-hidden form: the largest power of two <= the
+    hidden chunks (F / 256) that keeps the launch within one round of FFN_SLOTS workgroups (cfg2
+    decoder, 223 tiles: 1; the 4k-row encoder, 37 tiles: 4; a free-running decoder of 11k frames:
+    2). 1 when the split-K workspace is off (ops.splitk_enabled(False): bit-exact comparisons)."""
+    if not _splitk_on[0]:
+        return 1
+    tiles = -(-rows // FFN_TILE_ROWS)
+    s = 1
+    while s < F // 256 and tiles * s * 2 <= FFN_SLOTS:
+        s *= 2
+    return s
+
+
+def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=None, layout=None, out=None,
+        nsplit=None):
     """PositionwiseFeedForward + residual + LayerNorm + mask in one launch (fs2_ffn): bf16 rows of
     256 (padded [B, T, 256] or packed [B*T, 256] in ``layout``); ``w_packed`` from
-    :func:`pack_ffn_weights`. The hidden [rows, F] never reaches HBM."""
+    :func:`pack_ffn_weights`. The hidden [rows, F] never reaches HBM. ``nsplit``: workgroups per row
+    tile (None: :func:`ffn_nsplit` of the row count the host knows -- ``layout.rows_hint`` or the
+    capacity)."""
     _gpu(x, w_packed, b1, b2, lens, addvec1, addvec2)
     if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
         raise TypeError("fs2amd.ffn: bf16 activations and weights only")
@@ -361,6 +383,16 @@ def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=No
     if out is None:
         out = torch.empty_like(x)
     d.out, d.out_row_stride = out.data_ptr(), _rows(out, "out")
+    rows = (getattr(layout, "rows_hint", None) or layout.capacity) if layout is not None else B * T
+    if layout is not None and rows < layout.capacity:
+        d.rows_max = int(rows)  # free-running: the active rows from the one host read
+    if nsplit is None:
+        nsplit = ffn_nsplit(rows, F)
+    if nsplit > 1:
+        ws = splitk_workspace(x.device)
+        if ws is None:
+            raise RuntimeError("fs2amd.ffn: nsplit > 1 needs the split-K workspace (ops.splitk_enabled)")
+        d.nsplit, d.splitk_ws, d.splitk_ws_bytes = int(nsplit), ws.data_ptr(), ws.numel()
     L.check(_lib.fs2_ffn(ctypes.byref(d), _stream(x)), "fs2_ffn")
     return out
 

@@ -141,13 +141,17 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
 
 
 FFN_FUSED_MIN_ROWS = 16384
+FFN_SPLIT_MIN_WG = 128
 
 
 def ffn_fused_ok(P, lp, h, layout):
     """fs2_ffn covers bf16 FFNs with d_model 256, kernel-1 w_2 and a hidden width of whole 256-column
-    chunks; it pays where the launch has enough 112-row tiles to fill the chip (the decoder: cfg2
-    24.9k packed rows; the 4k-row encoder keeps the two fs2_conv1d launches). FS2_FFN_FUSED=0: off
-    (A/B), =2: on at every size (tests); default 1."""
+    chunks. Launches with enough 112-row tiles to fill the chip (the cfg2 decoder: 24.9k packed
+    rows) run one workgroup per tile; smaller ones the split-hidden form (ops.ffn_nsplit: 2-4
+    workgroups per tile, f32 partials summed by the last arriver) when that puts >= 128 workgroups
+    on the chip. Graph-timed at the encoder shape (4k rows, nsplit 4): 45.8 us vs 45.5 us for the
+    two fs2_conv1d launches; a free-running cfg2 decoder (11.1k rows, nsplit 2): 70.8 vs 105.4 us.
+    FS2_FFN_FUSED=0: off (A/B), =2: on at every size (tests); default 1."""
     mode = os.environ.get("FS2_FFN_FUSED", "1")
     if mode == "0" or P.compute != L.FS2_BF16 or h.dtype != torch.bfloat16 or getattr(lp, "w12", None) is None:
         return False
@@ -155,7 +159,11 @@ def ffn_fused_ok(P, lp, h, layout):
     # else the capacity. A launch is one round of 112-row tiles taking about one tile's time, so
     # below ~146 tiles the two fs2_conv1d launches (many more, smaller tiles) are faster.
     rows = h.shape[0] * h.shape[1] if layout is None else (getattr(layout, "rows_hint", None) or layout.capacity)
-    return mode == "2" or rows >= FFN_FUSED_MIN_ROWS
+    if mode == "2" or rows >= FFN_FUSED_MIN_ROWS:
+        return True
+    # fewer rows: the split-hidden form (ops.ffn_nsplit) puts 2-4 workgroups on each tile
+    tiles = -(-rows // ops.FFN_TILE_ROWS)
+    return tiles * ops.ffn_nsplit(rows, lp.b1.numel()) >= FFN_SPLIT_MIN_WG
 
 
 def _stack(P, layers, x, lens, layout=None, timed=False, addvecs=(None, None)):
@@ -327,14 +335,15 @@ def _stage1(P, va, g, p_control, d_control):
     if st.phoneme_e and st.e_pred is None:
         st.e_pred = _variance(P, "energy", x, g.lens_src, g.e_targets, p_control)  # p_control: modules.py:124-125
     if g.d_targets is not None:
-        dur = g.d_targets
-        if dur.dtype not in (torch.int64, torch.float32):
-            dur = dur.to(torch.int64)
-        st.cum, st.mel_len, _ = ops.lr_durations(dur)
+        st.cum, st.mel_len, _ = ops.lr_durations(_dur_input(g.d_targets))
         st.d_rounded = None
     else:
         st.cum, st.mel_len, st.d_rounded = ops.lr_durations(st.log_d, logpred=True, d_control=d_control)
     return st
+
+
+def _dur_input(d):
+    return d if d.dtype in (torch.int64, torch.float32) else d.to(torch.int64)
 
 
 def _stage2(P, g, st, T_out, T_dec, p_control, postnet_valid=False, rows_hint=None):

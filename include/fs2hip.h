@@ -193,6 +193,20 @@ typedef struct fs2_ffn_desc {
   int64_t out_row_stride;
   const int32_t *rows_dev;  /* packed rows (fs2_seq_layout cu + B) or NULL                       */
   const int32_t *row_pos;   /* packed rows: int32 [rows][2] = {frame, sequence length}           */
+  /* split-hidden form (optional; nsplit 0 or 1 = off): each 112-row tile is run by nsplit in
+     {2, 4} workgroups (nsplit <= F/256), split s computing hidden chunks [s*F/(256*nsplit), ...)
+     and its partial w_2 product; the last arriving split sums the f32 partials in split order
+     (deterministic, not bitwise equal to nsplit = 1) and runs the LayerNorm epilogue. For launches
+     with too few tiles to fill the chip (the 4k-row encoder, short free-running decoders).
+     splitk_ws: the fs2_conv1d split-K workspace (first 4 KiB zeroed arrival counters, one per
+     tile: <= 1024 tiles; then ceil(B*T/112) * nsplit * 112 KiB of f32 partials).             */
+  int nsplit;
+  void *splitk_ws;
+  int64_t splitk_ws_bytes;
+  int rows_max;             /* packed rows: an upper bound of *rows_dev the caller knows (e.g. from
+                               a host read of the lengths; 0 = B*T): the launch covers only
+                               min(*rows_dev, rows_max) rows, its grid and workspace are sized
+                               from rows_max                                                      */
 } fs2_ffn_desc;
 
 int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream);

@@ -8,7 +8,10 @@ mask in one launch, transformer/SubLayers.py:85-93 + Layers.py:28).
 * packed rows (SeqLayout) bit-identical to padded rows: each output row depends only on its own
   input rows and the per-row k order, not on where the 112-row tile boundaries fall;
 * ragged lengths 0 / 1 / < the 4-row tap reach / exact tile multiples, row counts that are not
-  multiples of 112, a padded launch with speaker / emotion vectors.
+  multiples of 112, a padded launch with speaker / emotion vectors;
+* the split-hidden form (nsplit 2 / 4 workgroups per tile, partials summed by the last arriver):
+  against float64 and the unsplit launch, bit-identical across repeated launches (fixed split
+  order, self-resetting counters), packed == padded at equal nsplit, invalid splits refused.
 """
 import numpy as np
 import pytest
@@ -99,9 +102,10 @@ def test_ffn_matches_two_launch_path(gpu):
     assert float(d.max()) <= 3e-2 and float(d.mean()) <= 1e-3, (float(d.max()), float(d.mean()))
 
 
+@pytest.mark.parametrize("nsplit", [1, 2, 4])
 @pytest.mark.parametrize("lens_l,T", [([37, 0, 130, 1, 64, 129, 130, 5], 130),
                                       ([430] * 3 + [2, 3, 4, 111, 112, 113, 224, 225], 430)])
-def test_ffn_packed_equals_padded(gpu, lens_l, T):
+def test_ffn_packed_equals_padded(gpu, lens_l, T, nsplit):
     ops, L = gpu
     W = _weights(ops, L, seed=11)
     lens = torch.tensor(lens_l, dtype=torch.int64, device=DEV)
@@ -112,8 +116,8 @@ def test_ffn_packed_equals_padded(gpu, lens_l, T):
     ok = rm >= 0
     xp = x.new_zeros(lay.capacity, 256)
     xp[rm[ok]] = x.reshape(-1, 256)[ok]
-    ref = ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], lens=lens)
-    got = ops.ffn(xp, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay)
+    ref = ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], lens=lens, nsplit=nsplit)
+    got = ops.ffn(xp, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay, nsplit=nsplit)
     torch.cuda.synchronize()
     R = int(lay.cu[-1])
     assert torch.equal(got[:R], ref.reshape(-1, 256)[ok])
@@ -146,3 +150,65 @@ def test_ffn_rejects_bad_shapes(gpu):
         ops.ffn(x.float(), W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"])
     with pytest.raises(AssertionError):  # w_1 | w_2 buffer of another shape
         ops.ffn(x, W["w12"][:-1], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"])
+
+
+@pytest.mark.parametrize("F,ks,nsplit", [(1024, 9, 2), (1024, 9, 4), (512, 3, 2)])
+@pytest.mark.parametrize("packed", [False, True])
+def test_ffn_split_hidden(gpu, F, ks, nsplit, packed):
+    """Split-hidden fs2_ffn: encoder-like padded rows with lens + speaker / emotion vectors, or
+    packed rows (rows_dev: tiles past the active rows exit before touching a counter)."""
+    ops, L = gpu
+    B, T = 37, 111
+    W = _weights(ops, L, F=F, ks=ks, seed=21 + nsplit)
+    g = torch.Generator(device="cpu").manual_seed(nsplit)
+    lens = torch.randint(0, T + 1, (B,), generator=g)
+    lens[0], lens[1], lens[2] = T, 1, 0
+    lens = lens.to(DEV)
+    x = _x(B, T, lens, 5)
+    pad = (ks - 1) // 2
+    kw = dict(ks=ks, pad=pad, ln=W["ln"])
+    if packed:
+        lay = ops.SeqLayout(lens, T)
+        rm = lay.rowmap.long()
+        ok = rm >= 0
+        xp = x.new_zeros(lay.capacity, 256)
+        xp[rm[ok]] = x.reshape(-1, 256)[ok]
+        outs = [ops.ffn(xp, W["w12"], W["b1"], W["b2"], layout=lay, nsplit=nsplit, **kw) for _ in range(4)]
+        one = ops.ffn(xp, W["w12"], W["b1"], W["b2"], layout=lay, nsplit=1, **kw)
+        R = int(lay.cu[-1])
+        got, one = outs[0][:R], one[:R]
+        ref = _ref(x, lens, W).reshape(-1, 256)[ok]
+        outs = [o[:R] for o in outs]
+    else:
+        a1 = torch.randn(B, 256, device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+        outs = [ops.ffn(x, W["w12"], W["b1"], W["b2"], lens=lens, addvec1=a1, nsplit=nsplit, **kw) for _ in range(4)]
+        one = ops.ffn(x, W["w12"], W["b1"], W["b2"], lens=lens, addvec1=a1, nsplit=1, **kw)
+        got = outs[0]
+        ref = _ref(x, lens, W, (a1,))
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, got)  # fixed summation order, counters reset themselves
+    err = (got.double() - ref).abs()
+    assert float(err.max()) <= 5e-2 and float(err.mean()) <= 2e-3, (float(err.max()), float(err.mean()))
+    d = (got.float() - one.float()).abs()
+    assert float(d.max()) <= 3e-2 and float(d.mean()) <= 1e-3, (float(d.max()), float(d.mean()))
+
+
+def test_ffn_split_rejects(gpu):
+    ops, L = gpu
+    x = torch.zeros(2, 8, 256, device=DEV, dtype=torch.bfloat16)
+    W = _weights(ops, L, F=512, ks=3, seed=1)
+    with pytest.raises(RuntimeError):  # 4 splits of a 2-chunk hidden
+        ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=3, pad=1, ln=W["ln"], nsplit=4)
+    with pytest.raises(RuntimeError):  # not a power of two
+        ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=3, pad=1, ln=W["ln"], nsplit=3)
+
+
+def test_ffn_nsplit_rule(gpu):
+    ops, L = gpu
+    assert ops.ffn_nsplit(24883, 1024) == 1  # cfg2 decoder: 223 tiles fill the chip
+    assert ops.ffn_nsplit(4096, 1024) == 4   # encoder: 37 tiles
+    assert ops.ffn_nsplit(11141, 1024) == 2  # free-running cfg2 decoder: 100 tiles
+    assert ops.ffn_nsplit(4096, 512) == 2
+    with ops.splitk_enabled(False):
+        assert ops.ffn_nsplit(4096, 1024) == 1

@@ -128,16 +128,17 @@ def _assert_params_close(pa, pb, lr_sum):
     """Parameters after a few steps of two runs of the same training. The gradients are not
     bit-reproducible (atomic accumulation in the embedding / attention backwards), and Adam turns a
     roundoff-size gradient on an element whose gradient is ~0 into a full +-lr step: elementwise
-    rtol 1e-4 / atol 1e-6, except at most 16 elements of the 34.7 M that may differ by up to twice
-    the summed learning rates (a flipped step per step). A real divergence (a bucket not reduced,
-    a wrong scale) moves far more elements."""
+    rtol 1e-4 / atol 1e-6, except at most 256 elements of the 34.7 M (7e-6 of them) that may differ
+    by up to twice the summed learning rates (a flipped step per step; measured 1 to 44 such
+    elements after 8 steps, depending on the box). A real divergence (a bucket not reduced, a wrong
+    scale) moves far more elements."""
     nbad, worst = 0, 0.0
     for k in pb:
         bad = ~torch.isclose(pa[k], pb[k], rtol=1e-4, atol=1e-6)
         nbad += int(bad.sum())
         if bad.any():
             worst = max(worst, float((pa[k] - pb[k]).abs()[bad].max()))
-    assert nbad <= 16 and worst <= 2 * lr_sum, (nbad, worst, lr_sum)
+    assert nbad <= 256 and worst <= 2 * lr_sum, (nbad, worst, lr_sum)
 
 
 def _lr_sum(tc, steps):

@@ -2,7 +2,8 @@
 """Launch ONE hot-path kernel repeatedly at the bench's cfg2 shapes (for rocprofv3 PMC passes).
 
     python tools/kernel_probe.py conv9 --reps 20
-kernels: ffn (decoder fused FFN, fs2_ffn), conv9 (decoder FFN Conv1d k=9 256->1024), conv1 (FFN k=1 1024->256 + res + LN),
+kernels: ffn (decoder fused FFN, fs2_ffn), ffn_rows / ffn2_rows (decoder FFN fused / two launches on --rows
+packed rows), enc_ffn (encoder FFN fused, --nsplit), conv9 (decoder FFN Conv1d k=9 256->1024), conv1 (FFN k=1 1024->256 + res + LN),
 qkv, attn, lr (LengthRegulator gather + PE), postnet (512->512 k=5 + tanh).
 """
 import argparse
@@ -21,6 +22,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--time", action="store_true", help="print mean duration (HIP events) instead of profiling")
+    ap.add_argument("--nsplit", type=int, default=None, help="ffn / enc_ffn / ffn_rows: fs2_ffn split-hidden workgroups per tile")
+    ap.add_argument("--rows", type=int, default=11141, help="ffn_rows / ffn2_rows: packed decoder rows (free-running cfg2: 11141)")
     a = ap.parse_args()
     import bench
     from fs2amd import _lib as L, ops
@@ -54,6 +57,26 @@ def main():
         h = rnd(B * T, 256)
         out = torch.empty_like(h)
         fn = lambda: ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=9, pad=4, ln=lp.ln2, layout=lay, out=out)
+    elif a.kernel in ("ffn_rows", "ffn2_rows"):  # decoder FFN on fewer packed rows (free-running), fused / two launches
+        T2 = 959
+        l2 = torch.full((64,), a.rows // 64, dtype=torch.int64)
+        l2[: a.rows - int(l2.sum())] += 1
+        lay2 = ops.SeqLayout(l2.to(dev), T2)
+        lay2.rows_hint = a.rows
+        h = rnd(lay2.capacity, 256)
+        out = torch.empty_like(h)
+        if a.kernel == "ffn_rows":
+            fn = lambda: ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=9, pad=4, ln=lp.ln2, layout=lay2, out=out, nsplit=a.nsplit)
+        else:
+            def fn():
+                f = ops.conv1d(h, lp.w1, lp.b1, cin=256, ks=9, pad=4, compute=P.compute, epilogue=L.EPI_BIAS_RELU,
+                               out_dtype=P.act_dtype, layout=lay2)
+                ops.conv1d(f, lp.w2, lp.b2, cin=1024, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_RES_LN,
+                           out_dtype=P.act_dtype, residual=h, ln=lp.ln2, layout=lay2, out=out)
+    elif a.kernel == "enc_ffn":  # encoder FFN fused (split-hidden), padded 64 x 64 rows with lens
+        el = P.enc_layers[0]
+        xe = rnd(64, 64, 256)
+        fn = lambda: ops.ffn(xe, el.w12, el.b1, el.b2, ks=9, pad=4, ln=el.ln2, lens=b["src_lens"], nsplit=a.nsplit)
     elif a.kernel == "conv1":
         f, h = rnd(B * T, 1024), rnd(B * T, 256)
         fn = lambda: ops.conv1d(f, lp.w2, lp.b2, cin=1024, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_RES_LN,
