@@ -56,11 +56,12 @@ struct FfnArgs {
   int nsplit;          // split-hidden form: workgroups per row tile (1 = off)
   int ntiles;          // row tiles of the launch
   int *cnt;            // [tiles] arrival counters (zero between launches)
-  void *part;          // f32 partial Y^T accumulators, kPartBytes per (tile, split)
+  void *part;          // f32 partial Y^T accumulators, part_bytes(MB) per (tile, split)
   uint32_t part_bytes;
 };
 
-constexpr int kPartBytes = 4 * 4 * 7 * 64 * 16;  // 4 waves x acc2[4][MB = 7] x 64 lanes x 16 B
+// f32 partial Y^T accumulators per (tile, split): 4 waves x acc2[4][MB] x 64 lanes x 16 B
+constexpr int part_bytes(int MB) { return 4 * 4 * MB * 64 * 16; }
 
 constexpr int64_t ffn_weight_elems(int KS, int F) { return (int64_t)F * KS * kD + (int64_t)kD * F; }
 
@@ -84,9 +85,12 @@ __device__ __forceinline__ void static_for(Fn &&f) {
 // (bits 3:0 and 15:14), expcnt 7, lgkmcnt 0
 constexpr int kLgkm0 = 0xC07F;
 
-template <int KS, int NCH>
+// MB = 16-row activation blocks per tile: 7 (112 rows: the full-chip decoder launches) or 4 (64 rows:
+// the split-hidden form of small launches, whose 4 splits x 64-row tiles fill the chip)
+template <int KS, int NCH, int MB>
 __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
-  constexpr int MB = 7, BM = 16 * MB;
+  constexpr int BM = 16 * MB;
+  constexpr uint32_t kPartBytes = (uint32_t)part_bytes(MB);
   constexpr int XROWS = BM + KS - 1;
   // x tile rows at a 544-byte pitch (512 + 32): the 16 rows of a fragment read fall in 16 distinct
   // bank groups for any tap shift with NO swizzle, so a unit's k-step is a constant byte offset
@@ -420,29 +424,57 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     __syncthreads();
     if (!*flag) return;
     __syncthreads();  // flag read by every wave before the epilogue reuses the slot
-    // split order, one other split's 28 loads in flight together (a per-load branch on the split
-    // index serialised every load's full latency); the sum goes into the dead H^T accumulators
+    // sum in split order into the dead H^T accumulators. MB = 4: every other split's partial is
+    // loaded at once (3 x 16 x 4 registers), one memory round trip; MB = 7: one other split's 28
+    // loads in flight at a time (a per-load branch on the split index serialised every load's
+    // full latency)
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) acc1[nb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sp = 0; sp < S; ++sp) {
-      if (sp == split) {
+    if constexpr (MB <= 4) {
+      f32x4 v[3][4][MB];
+      static_for<3>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if (j < S - 1) {
+          const int sp = j + (j >= split ? 1 : 0);
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
+          for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-          for (int mb = 0; mb < MB; ++mb) acc1[nb][mb] += acc2[nb][mb];
-      } else {
-        f32x4 v[4][MB];
+            for (int mb = 0; mb < MB; ++mb)
+              v[j][nb][mb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, pofs(sp, nb, mb), 0, 16));
+        }
+      });
+      static_for<4>([&](auto SP) {
+        constexpr int sp = decltype(SP)::value;
+        constexpr int jlo = sp < 3 ? sp : 2, jhi = sp > 0 ? sp - 1 : 0;
+        if (sp < S) {
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
+          for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-          for (int mb = 0; mb < MB; ++mb)
-            v[nb][mb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, pofs(sp, nb, mb), 0, 16));
+            for (int mb = 0; mb < MB; ++mb)
+              acc1[nb][mb] += sp < split ? v[jlo][nb][mb] : (sp == split ? acc2[nb][mb] : v[jhi][nb][mb]);
+        }
+      });
+    } else {
+      for (int sp = 0; sp < S; ++sp) {
+        if (sp == split) {
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
+          for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-          for (int mb = 0; mb < MB; ++mb) acc1[nb][mb] += v[nb][mb];
+            for (int mb = 0; mb < MB; ++mb) acc1[nb][mb] += acc2[nb][mb];
+        } else {
+          f32x4 v[4][MB];
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb)
+              v[nb][mb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(pr, pofs(sp, nb, mb), 0, 16));
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb) acc1[nb][mb] += v[nb][mb];
+        }
       }
     }
 #pragma unroll
@@ -662,8 +694,9 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   p.w = reinterpret_cast<const bf16 *>(d->w);
   p.b1 = d->b1;
   p.w_bytes = (uint32_t)wb;
-  constexpr int BM = 112;
-  if (d->rows_max < 0) return FS2_EINVAL;
+  if (d->rows_max < 0 || !(d->tile_rows == 0 || d->tile_rows == 112 || d->tile_rows == 64)) return FS2_EINVAL;
+  const int MB = d->tile_rows == 64 ? 4 : 7, BM = 16 * MB;
+  const int64_t kPartBytes = part_bytes(MB);
   const int64_t Mg = (d->rows_dev != nullptr && d->rows_max > 0 && d->rows_max < M64) ? d->rows_max : M64;
   a.M = (int)Mg;
   const int ntiles = (int)((Mg + BM - 1) / BM);
@@ -682,14 +715,25 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   const int nch = d->F / kChunk;
   hipStream_t s = as_stream(stream);
   // instantiated shapes: kernel 9 (model.yaml conv_kernel_size [9, 1]) or 3, F = 1024 or 512
+  auto go = [&](auto KSC, auto NCHC) {
+    constexpr int ks = decltype(KSC)::value, nc = decltype(NCHC)::value;
+    if (MB == 4)
+      hipLaunchKernelGGL((ffn_fused_kernel<ks, nc, 4>), dim3(nwg), dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((ffn_fused_kernel<ks, nc, 7>), dim3(nwg), dim3(256), 0, s, p);
+  };
+  using I9 = std::integral_constant<int, 9>;
+  using I3 = std::integral_constant<int, 3>;
+  using C4 = std::integral_constant<int, 4>;
+  using C2 = std::integral_constant<int, 2>;
   if (d->KS == 9 && nch == 4)
-    hipLaunchKernelGGL((ffn_fused_kernel<9, 4>), dim3(nwg), dim3(256), 0, s, p);
+    go(I9{}, C4{});
   else if (d->KS == 9 && nch == 2)
-    hipLaunchKernelGGL((ffn_fused_kernel<9, 2>), dim3(nwg), dim3(256), 0, s, p);
+    go(I9{}, C2{});
   else if (d->KS == 3 && nch == 4)
-    hipLaunchKernelGGL((ffn_fused_kernel<3, 4>), dim3(nwg), dim3(256), 0, s, p);
+    go(I3{}, C4{});
   else if (d->KS == 3 && nch == 2)
-    hipLaunchKernelGGL((ffn_fused_kernel<3, 2>), dim3(nwg), dim3(256), 0, s, p);
+    go(I3{}, C2{});
   else
     return FS2_EUNSUPPORTED;
   FS2_CHECK_LAUNCH();

@@ -72,6 +72,7 @@ class FfnDesc(ctypes.Structure):
         ("out", _p), ("out_row_stride", _i64),
         ("rows_dev", _p), ("row_pos", _p),
         ("nsplit", _i), ("splitk_ws", _p), ("splitk_ws_bytes", _i64), ("rows_max", _i),
+        ("tile_rows", _i),
     ]
 
 

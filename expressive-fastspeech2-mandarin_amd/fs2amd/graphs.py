@@ -107,8 +107,8 @@ class SynthGraphs:
         R.HOST_READS[0] += 1
         T_out, sum_len = R.check_meta(e1.meta_host, dev)
         pn_valid = R.postnet_valid_rows(B, T_out, sum_len)
-        fused = sum_len >= R.FFN_FUSED_MIN_ROWS  # the decoder FFN's launch form (runtime.ffn_fused_ok)
-        key2 = key1 + (T_out, pn_valid, fused)
+        # the decoder's packed launches are sized from the bucketed row count (runtime._stage2)
+        key2 = key1 + (T_out, pn_valid, ops.rows_bucket(sum_len, B * T_out))
         e2 = self._g2.get(key2)
         if e2 is None:
             def body():

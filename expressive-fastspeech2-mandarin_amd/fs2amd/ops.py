@@ -328,32 +328,61 @@ def wconv(x, w_packed, bias, *, ks, pad, out=None):
     return out
 
 
-FFN_TILE_ROWS = 112
 FFN_SLOTS = 256  # workgroups resident at once (1 per CU)
-FFN_PART_BYTES = 4 * 4 * 7 * 64 * 16  # f32 partial accumulators per (tile, split), ffn.hip kPartBytes
+
+
+def ffn_part_bytes(tile_rows):
+    """f32 partial accumulators per (tile, split) of fs2_ffn's split-hidden form (ffn.hip part_bytes)."""
+    return 4 * 4 * (tile_rows // 16) * 64 * 16
+
+
+def rows_bucket(rows, capacity, step=1024):
+    """A host-known active row count rounded up to a multiple of ``step`` (capped at the capacity):
+    the upper bound packed launches are sized with (fs2_ffn rows_max), so that one captured graph
+    serves every batch whose count falls in the bucket."""
+    return min(capacity, -(-int(rows) // step) * step)
+
+
+# fs2_ffn cost model (us, one round of workgroups at one per CU; graph-timed probes at the encoder
+# shape, tools/kernel_probe.py enc_ffn): per 256-column hidden chunk, fixed cost (x tile, LN
+# epilogue), and the split hand-off (partial stores, arrival counter, partial loads) per nsplit.
+# Measured: 112-row tiles 90 / 59.6 / 45.8 us at nsplit 1 / 2 / 4; 64-row tiles 57.3 / 40.2 / 38.8.
+FFN_COST = {112: (20.0, 10.0, {1: 0.0, 2: 10.0, 4: 16.0}), 64: (13.0, 5.0, {1: 0.0, 2: 9.0, 4: 21.0})}
+
+
+def ffn_form(rows, F):
+    """fs2_ffn launch form (tile_rows, nsplit) for ``rows`` rows and hidden width F: the least
+    modelled time (FFN_COST) over rounds of FFN_SLOTS workgroups. The cfg2 decoder (24.9k rows) ->
+    (112, 1); the 4k-row encoder -> (64, 4); a free-running cfg2 decoder (11.1k rows) -> (64, 1).
+    (112, 1) when the split-K workspace is off (ops.splitk_enabled(False): bit-exact comparisons)."""
+    nch = F // 256
+    if not _splitk_on[0]:
+        return 112, 1
+    best = None
+    for tr, (chunk, base, over) in FFN_COST.items():
+        tiles = -(-rows // tr)
+        for s in (1, 2, 4):
+            if s > nch:
+                continue
+            if s > 1 and (tiles > 1024 or 4096 + tiles * s * ffn_part_bytes(tr) > SPLITK_WS_BYTES):
+                continue
+            t = -(-tiles * s // FFN_SLOTS) * (nch // s * chunk + base + over[s])
+            if best is None or t < best[0] - 1e-9:
+                best = (t, tr, s)
+    return best[1], best[2]
 
 
 def ffn_nsplit(rows, F):
-    """Workgroups per 112-row tile for fs2_ffn's split-hidden form: the largest power of two <= the
-    hidden chunks (F / 256) that keeps the launch within one round of FFN_SLOTS workgroups (cfg2
-    decoder, 223 tiles: 1; the 4k-row encoder, 37 tiles: 4; a free-running decoder of 11k frames:
-    2). 1 when the split-K workspace is off (ops.splitk_enabled(False): bit-exact comparisons)."""
-    if not _splitk_on[0]:
-        return 1
-    tiles = -(-rows // FFN_TILE_ROWS)
-    s = 1
-    while s < F // 256 and tiles * s * 2 <= FFN_SLOTS:
-        s *= 2
-    return s
+    return ffn_form(rows, F)[1]
 
 
 def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=None, layout=None, out=None,
-        nsplit=None):
+        nsplit=None, tile_rows=None):
     """PositionwiseFeedForward + residual + LayerNorm + mask in one launch (fs2_ffn): bf16 rows of
     256 (padded [B, T, 256] or packed [B*T, 256] in ``layout``); ``w_packed`` from
-    :func:`pack_ffn_weights`. The hidden [rows, F] never reaches HBM. ``nsplit``: workgroups per row
-    tile (None: :func:`ffn_nsplit` of the row count the host knows -- ``layout.rows_hint`` or the
-    capacity)."""
+    :func:`pack_ffn_weights`. The hidden [rows, F] never reaches HBM. ``tile_rows`` (112 / 64) and
+    ``nsplit`` (workgroups per row tile): None = :func:`ffn_form` of the row count the host knows
+    (``layout.rows_hint`` or the capacity)."""
     _gpu(x, w_packed, b1, b2, lens, addvec1, addvec2)
     if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
         raise TypeError("fs2amd.ffn: bf16 activations and weights only")
@@ -386,8 +415,12 @@ def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=No
     rows = (getattr(layout, "rows_hint", None) or layout.capacity) if layout is not None else B * T
     if layout is not None and rows < layout.capacity:
         d.rows_max = int(rows)  # free-running: the active rows from the one host read
+    tr, ns = ffn_form(rows, F)
+    if tile_rows is None:
+        tile_rows = tr if nsplit is None else 112
     if nsplit is None:
-        nsplit = ffn_nsplit(rows, F)
+        nsplit = ns
+    d.tile_rows = int(tile_rows)
     if nsplit > 1:
         ws = splitk_workspace(x.device)
         if ws is None:

@@ -147,10 +147,12 @@ FFN_SPLIT_MIN_WG = 128
 def ffn_fused_ok(P, lp, h, layout):
     """fs2_ffn covers bf16 FFNs with d_model 256, kernel-1 w_2 and a hidden width of whole 256-column
     chunks. Launches with enough 112-row tiles to fill the chip (the cfg2 decoder: 24.9k packed
-    rows) run one workgroup per tile; smaller ones the split-hidden form (ops.ffn_nsplit: 2-4
-    workgroups per tile, f32 partials summed by the last arriver) when that puts >= 128 workgroups
-    on the chip. Graph-timed at the encoder shape (4k rows, nsplit 4): 45.8 us vs 45.5 us for the
-    two fs2_conv1d launches; a free-running cfg2 decoder (11.1k rows, nsplit 2): 70.8 vs 105.4 us.
+    rows) run one workgroup per 112-row tile; smaller ones 64-row tiles and / or the split-hidden
+    form (ops.ffn_form: 2-4 workgroups per tile, f32 partials summed by the last arriver) when that
+    puts >= 128 workgroups
+    on the chip. Graph-timed at the encoder shape (4k rows, 64-row tiles x 4 splits): 38.8 us vs
+    45.5 us for the two fs2_conv1d launches; a free-running cfg2 decoder (11.1k rows, 64-row tiles):
+    71 vs 105 us.
     FS2_FFN_FUSED=0: off (A/B), =2: on at every size (tests); default 1."""
     mode = os.environ.get("FS2_FFN_FUSED", "1")
     if mode == "0" or P.compute != L.FS2_BF16 or h.dtype != torch.bfloat16 or getattr(lp, "w12", None) is None:
@@ -161,9 +163,9 @@ def ffn_fused_ok(P, lp, h, layout):
     rows = h.shape[0] * h.shape[1] if layout is None else (getattr(layout, "rows_hint", None) or layout.capacity)
     if mode == "2" or rows >= FFN_FUSED_MIN_ROWS:
         return True
-    # fewer rows: the split-hidden form (ops.ffn_nsplit) puts 2-4 workgroups on each tile
-    tiles = -(-rows // ops.FFN_TILE_ROWS)
-    return tiles * ops.ffn_nsplit(rows, lp.b1.numel()) >= FFN_SPLIT_MIN_WG
+    # fewer rows: the split-hidden form (ops.ffn_form) puts 2-4 workgroups on each tile
+    tr, ns = ops.ffn_form(rows, lp.b1.numel())
+    return -(-rows // tr) * ns >= FFN_SPLIT_MIN_WG
 
 
 def _stack(P, layers, x, lens, layout=None, timed=False, addvecs=(None, None)):
@@ -355,7 +357,9 @@ def _stage2(P, g, st, T_out, T_dec, p_control, postnet_valid=False, rows_hint=No
         # packed decoder: only the dec_lens frames of each utterance are computed
         # (cfg2: 24.9k of 27.5k rows, cfg4: 135k of 249k); mel_linear scatters back to [B, T, n_mel]
         lay = ops.SeqLayout(dec_lens, T_dec)
-        lay.rows_hint = rows_hint  # active rows when known on the host (free-running)
+        # active rows when known on the host (free-running), rounded up (ops.rows_bucket) so that
+        # a captured stage-2 graph serves every batch of the bucket
+        lay.rows_hint = None if rows_hint is None else ops.rows_bucket(rows_hint, lay.capacity)
         x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype,
                           out_layout=lay)
         x = _stack(P, P.dec_layers, x, None, layout=lay, timed=True)

@@ -199,7 +199,7 @@ typedef struct fs2_ffn_desc {
      (deterministic, not bitwise equal to nsplit = 1) and runs the LayerNorm epilogue. For launches
      with too few tiles to fill the chip (the 4k-row encoder, short free-running decoders).
      splitk_ws: the fs2_conv1d split-K workspace (first 4 KiB zeroed arrival counters, one per
-     tile: <= 1024 tiles; then ceil(B*T/112) * nsplit * 112 KiB of f32 partials).             */
+     tile: <= 1024 tiles; then tiles * nsplit * tile_rows KiB of f32 partials).                 */
   int nsplit;
   void *splitk_ws;
   int64_t splitk_ws_bytes;
@@ -207,6 +207,9 @@ typedef struct fs2_ffn_desc {
                                a host read of the lengths; 0 = B*T): the launch covers only
                                min(*rows_dev, rows_max) rows, its grid and workspace are sized
                                from rows_max                                                      */
+  int tile_rows;            /* rows per workgroup tile: 0 / 112 (default) or 64 (the split-hidden
+                               form of small launches: 4 splits x 64-row tiles fill the chip, and
+                               the last arriver loads the other partials in one round trip)       */
 } fs2_ffn_desc;
 
 int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream);

@@ -102,10 +102,10 @@ def test_ffn_matches_two_launch_path(gpu):
     assert float(d.max()) <= 3e-2 and float(d.mean()) <= 1e-3, (float(d.max()), float(d.mean()))
 
 
-@pytest.mark.parametrize("nsplit", [1, 2, 4])
+@pytest.mark.parametrize("tile_rows,nsplit", [(112, 1), (112, 2), (112, 4), (64, 1), (64, 4)])
 @pytest.mark.parametrize("lens_l,T", [([37, 0, 130, 1, 64, 129, 130, 5], 130),
                                       ([430] * 3 + [2, 3, 4, 111, 112, 113, 224, 225], 430)])
-def test_ffn_packed_equals_padded(gpu, lens_l, T, nsplit):
+def test_ffn_packed_equals_padded(gpu, lens_l, T, tile_rows, nsplit):
     ops, L = gpu
     W = _weights(ops, L, seed=11)
     lens = torch.tensor(lens_l, dtype=torch.int64, device=DEV)
@@ -116,8 +116,9 @@ def test_ffn_packed_equals_padded(gpu, lens_l, T, nsplit):
     ok = rm >= 0
     xp = x.new_zeros(lay.capacity, 256)
     xp[rm[ok]] = x.reshape(-1, 256)[ok]
-    ref = ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], lens=lens, nsplit=nsplit)
-    got = ops.ffn(xp, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay, nsplit=nsplit)
+    kw = dict(ks=9, pad=4, ln=W["ln"], nsplit=nsplit, tile_rows=tile_rows)
+    ref = ops.ffn(x, W["w12"], W["b1"], W["b2"], lens=lens, **kw)
+    got = ops.ffn(xp, W["w12"], W["b1"], W["b2"], layout=lay, **kw)
     torch.cuda.synchronize()
     R = int(lay.cu[-1])
     assert torch.equal(got[:R], ref.reshape(-1, 256)[ok])
@@ -152,9 +153,10 @@ def test_ffn_rejects_bad_shapes(gpu):
         ops.ffn(x, W["w12"][:-1], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"])
 
 
-@pytest.mark.parametrize("F,ks,nsplit", [(1024, 9, 2), (1024, 9, 4), (512, 3, 2)])
+@pytest.mark.parametrize("F,ks,nsplit,tile_rows", [(1024, 9, 2, 112), (1024, 9, 4, 112), (512, 3, 2, 112),
+                                                   (1024, 9, 4, 64), (1024, 9, 2, 64), (1024, 9, 1, 64)])
 @pytest.mark.parametrize("packed", [False, True])
-def test_ffn_split_hidden(gpu, F, ks, nsplit, packed):
+def test_ffn_split_hidden(gpu, F, ks, nsplit, tile_rows, packed):
     """Split-hidden fs2_ffn: encoder-like padded rows with lens + speaker / emotion vectors, or
     packed rows (rows_dev: tiles past the active rows exit before touching a counter)."""
     ops, L = gpu
@@ -166,7 +168,7 @@ def test_ffn_split_hidden(gpu, F, ks, nsplit, packed):
     lens = lens.to(DEV)
     x = _x(B, T, lens, 5)
     pad = (ks - 1) // 2
-    kw = dict(ks=ks, pad=pad, ln=W["ln"])
+    kw = dict(ks=ks, pad=pad, ln=W["ln"], tile_rows=tile_rows)
     if packed:
         lay = ops.SeqLayout(lens, T)
         rm = lay.rowmap.long()
@@ -174,7 +176,7 @@ def test_ffn_split_hidden(gpu, F, ks, nsplit, packed):
         xp = x.new_zeros(lay.capacity, 256)
         xp[rm[ok]] = x.reshape(-1, 256)[ok]
         outs = [ops.ffn(xp, W["w12"], W["b1"], W["b2"], layout=lay, nsplit=nsplit, **kw) for _ in range(4)]
-        one = ops.ffn(xp, W["w12"], W["b1"], W["b2"], layout=lay, nsplit=1, **kw)
+        one = ops.ffn(xp, W["w12"], W["b1"], W["b2"], layout=lay, nsplit=1, ks=ks, pad=pad, ln=W["ln"])
         R = int(lay.cu[-1])
         got, one = outs[0][:R], one[:R]
         ref = _ref(x, lens, W).reshape(-1, 256)[ok]
@@ -182,7 +184,7 @@ def test_ffn_split_hidden(gpu, F, ks, nsplit, packed):
     else:
         a1 = torch.randn(B, 256, device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
         outs = [ops.ffn(x, W["w12"], W["b1"], W["b2"], lens=lens, addvec1=a1, nsplit=nsplit, **kw) for _ in range(4)]
-        one = ops.ffn(x, W["w12"], W["b1"], W["b2"], lens=lens, addvec1=a1, nsplit=1, **kw)
+        one = ops.ffn(x, W["w12"], W["b1"], W["b2"], lens=lens, addvec1=a1, nsplit=1, ks=ks, pad=pad, ln=W["ln"])
         got = outs[0]
         ref = _ref(x, lens, W, (a1,))
     torch.cuda.synchronize()
@@ -204,11 +206,14 @@ def test_ffn_split_rejects(gpu):
         ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=3, pad=1, ln=W["ln"], nsplit=3)
 
 
-def test_ffn_nsplit_rule(gpu):
+def test_ffn_form_rule(gpu):
     ops, L = gpu
-    assert ops.ffn_nsplit(24883, 1024) == 1  # cfg2 decoder: 223 tiles fill the chip
-    assert ops.ffn_nsplit(4096, 1024) == 4   # encoder: 37 tiles
-    assert ops.ffn_nsplit(11141, 1024) == 2  # free-running cfg2 decoder: 100 tiles
-    assert ops.ffn_nsplit(4096, 512) == 2
+    assert ops.ffn_form(24883, 1024) == (112, 1)  # cfg2 decoder: 223 tiles fill the chip
+    tr, ns = ops.ffn_form(4096, 1024)            # encoder: 37 tiles of 112 -> a split form
+    assert ns > 1 and -(-4096 // tr) * ns <= ops.FFN_SLOTS
+    for rows in (1, 500, 4096, 11141, 24883, 200000):
+        tr, ns = ops.ffn_form(rows, 1024)
+        assert tr in (112, 64) and ns in (1, 2, 4)
+        assert ns == 1 or 4096 + -(-rows // tr) * ns * ops.ffn_part_bytes(tr) <= ops.SPLITK_WS_BYTES
     with ops.splitk_enabled(False):
-        assert ops.ffn_nsplit(4096, 1024) == 1
+        assert ops.ffn_form(4096, 1024) == (112, 1)

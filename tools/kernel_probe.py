@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--time", action="store_true", help="print mean duration (HIP events) instead of profiling")
     ap.add_argument("--nsplit", type=int, default=None, help="ffn / enc_ffn / ffn_rows: fs2_ffn split-hidden workgroups per tile")
+    ap.add_argument("--tile-rows", type=int, default=None, help="ffn / enc_ffn / ffn_rows: fs2_ffn tile rows (112 / 64)")
     ap.add_argument("--rows", type=int, default=11141, help="ffn_rows / ffn2_rows: packed decoder rows (free-running cfg2: 11141)")
     a = ap.parse_args()
     import bench
@@ -56,7 +57,7 @@ def main():
     elif a.kernel == "ffn":  # fused FFN (fs2_ffn): conv-k9 + ReLU + conv-k1 + res + LN, packed rows
         h = rnd(B * T, 256)
         out = torch.empty_like(h)
-        fn = lambda: ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=9, pad=4, ln=lp.ln2, layout=lay, out=out)
+        fn = lambda: ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=9, pad=4, ln=lp.ln2, layout=lay, out=out, nsplit=a.nsplit, tile_rows=a.tile_rows)
     elif a.kernel in ("ffn_rows", "ffn2_rows"):  # decoder FFN on fewer packed rows (free-running), fused / two launches
         T2 = 959
         l2 = torch.full((64,), a.rows // 64, dtype=torch.int64)
@@ -66,7 +67,8 @@ def main():
         h = rnd(lay2.capacity, 256)
         out = torch.empty_like(h)
         if a.kernel == "ffn_rows":
-            fn = lambda: ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=9, pad=4, ln=lp.ln2, layout=lay2, out=out, nsplit=a.nsplit)
+            fn = lambda: ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=9, pad=4, ln=lp.ln2, layout=lay2, out=out, nsplit=a.nsplit,
+                                 tile_rows=a.tile_rows)
         else:
             def fn():
                 f = ops.conv1d(h, lp.w1, lp.b1, cin=256, ks=9, pad=4, compute=P.compute, epilogue=L.EPI_BIAS_RELU,
@@ -76,7 +78,8 @@ def main():
     elif a.kernel == "enc_ffn":  # encoder FFN fused (split-hidden), padded 64 x 64 rows with lens
         el = P.enc_layers[0]
         xe = rnd(64, 64, 256)
-        fn = lambda: ops.ffn(xe, el.w12, el.b1, el.b2, ks=9, pad=4, ln=el.ln2, lens=b["src_lens"], nsplit=a.nsplit)
+        fn = lambda: ops.ffn(xe, el.w12, el.b1, el.b2, ks=9, pad=4, ln=el.ln2, lens=b["src_lens"], nsplit=a.nsplit,
+                              tile_rows=a.tile_rows)
     elif a.kernel == "conv1":
         f, h = rnd(B * T, 1024), rnd(B * T, 256)
         fn = lambda: ops.conv1d(f, lp.w2, lp.b2, cin=1024, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_RES_LN,
