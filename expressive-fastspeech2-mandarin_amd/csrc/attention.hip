@@ -258,7 +258,28 @@ __device__ __forceinline__ int kv_swz(int row) { return ((row & 7) << 1) | ((row
 __device__ __forceinline__ int kv_off(int row, int chunk) { return row * 256 + ((chunk ^ kv_swz(row)) << 4); }
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+// scores are never NaN (masked keys are -inf): max without NaN canonicalisation. (Inline-asm
+// v_max3_f32 here read MFMA results with no wait states -- the hazard recognizer does not see into
+// asm -- and took stale accumulator values: a timing-dependent wrong row max.)
+__device__ __forceinline__ float max_nn(float a, float b) { return __builtin_fmaxf(a, b); }
+// reductions over the 4 lanes of one query (lane groups g = lane >> 4) with the gfx950 row-swap
+// permutes: v_permlane16_swap pairs rows (0, 1) / (2, 3), v_permlane32_swap the two halves. No LDS
+// round trip (ds_bpermute + lgkmcnt(0), which also waited for the in-flight K / V reads).
+__device__ __forceinline__ float rows_sum(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float s1 = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s1), __float_as_uint(s1), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+__device__ __forceinline__ float rows_max(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float s1 = max_nn(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s1), __float_as_uint(s1), false, false);
+  return max_nn(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
 
 template <int N>
 __device__ __forceinline__ void attn_vm_wait() {
@@ -396,12 +417,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
         for (int j = 0; j < 4; ++j)
           if (ni * 16 + j >= lim) sacc[ni][j] = -INFINITY;
     }
-    float mx = -INFINITY;
+    float mx = m_run;
 #pragma unroll
-    for (int ni = 0; ni < NB; ++ni) mx = fmaxf(mx, fmaxf(fmaxf(sacc[ni][0], sacc[ni][1]), fmaxf(sacc[ni][2], sacc[ni][3])));
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
+    for (int ni = 0; ni < NB; ++ni) {
+      mx = max_nn(max_nn(mx, sacc[ni][0]), sacc[ni][1]);
+      mx = max_nn(max_nn(mx, sacc[ni][2]), sacc[ni][3]);
+    }
+    const float m_new = rows_max(mx);  // includes m_run
     // rescale only when some query's running max moved (alpha == 1 exactly for the others): after
     // the first tiles of a sequence the max rarely moves, and the O rescale is 32 VALU per wave
     if (__builtin_amdgcn_ballot_w64(m_new != m_run) != 0) {
@@ -412,33 +434,46 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
       for (int nd = 0; nd < DK / 16; ++nd) oacc[nd] *= alpha;
     }
     m_run = m_new;
+    // p = exp2(s * c - m * c): the fma on score pairs (v_pk_fma_f32), pair sums (v_pk_add_f32)
     const float mc = -m_new * scale_log2;
-    float sum = 0.f;
+    const f32x2 c2 = {scale_log2, scale_log2}, mc2 = {mc, mc};
+    f32x2 sum2 = {0.f, 0.f};
     bf16x8 pf[NB / 2];
 #pragma unroll
     for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[ni][j], scale_log2, mc));
-        sum += p;
-        pf[ni >> 1][(ni & 1) * 4 + j] = (bf16)p;
+      for (int jp = 0; jp < 2; ++jp) {
+        const f32x2 sv = {sacc[ni][2 * jp], sacc[ni][2 * jp + 1]};
+        const f32x2 e = __builtin_elementwise_fma(sv, c2, mc2);
+        const f32x2 pv = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+        sum2 += pv;
+        pf[ni >> 1][(ni & 1) * 4 + 2 * jp] = (bf16)pv.x;
+        pf[ni >> 1][(ni & 1) * 4 + 2 * jp + 1] = (bf16)pv.y;
       }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    l_run += sum;
+    l_run += rows_sum(sum2.x + sum2.y);
 
+    // V^T fragments 4 at a time ahead of their MFMAs (one read / wait / MFMA chain per fragment
+    // left every MFMA waiting out an LDS round trip)
+    auto vread = [&](int s2, int nd) {
+      const char *vp = Vb + voff[nd] + s2 * 32 * 256;
+      auto lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)vp);
+      auto hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)(vp + 16 * 256));
+      bf16x8 vf;
+      __builtin_memcpy(&vf, &lo, 8);
+      __builtin_memcpy(reinterpret_cast<char *>(&vf) + 8, &hi, 8);
+      return vf;
+    };
 #pragma unroll
     for (int s2 = 0; s2 < NB / 2; ++s2) {
       // this lane's address row r0 = 32*s2 + 4g + tq (block 1), r0 + 16 for block 2
 #pragma unroll
-      for (int nd = 0; nd < DK / 16; ++nd) {
-        const char *vp = Vb + voff[nd] + s2 * 32 * 256;
-        auto lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)vp);
-        auto hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)(vp + 16 * 256));
-        bf16x8 vf;
-        __builtin_memcpy(&vf, &lo, 8);
-        __builtin_memcpy(reinterpret_cast<char *>(&vf) + 8, &hi, 8);
-        oacc[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[s2], oacc[nd], 0, 0, 0);
+      for (int h4 = 0; h4 < DK / 64; ++h4) {
+        bf16x8 vf[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vf[i] = vread(s2, 4 * h4 + i);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          oacc[4 * h4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[i], pf[s2], oacc[4 * h4 + i], 0, 0, 0);
       }
     }
   };

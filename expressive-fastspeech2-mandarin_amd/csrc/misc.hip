@@ -139,6 +139,51 @@ __global__ __launch_bounds__(256) void variance_embed_kernel(TX *__restrict__ x,
   }
 }
 
+// PostNet valid-region form (runtime._postnet_valid): padded rows -> packed rows. Padded row i
+// goes to packed row rowmap[i] (>= 0) of a SeqLayout; 16-byte chunks, rows of row_bytes; two
+// tensors (the f32 mel and its bf16 copy) in one launch.
+__global__ __launch_bounds__(256) void pack_rows_kernel(const char *__restrict__ a, int a_bytes, char *__restrict__ pa,
+                                                        const char *__restrict__ b, int b_bytes, char *__restrict__ pb,
+                                                        const int32_t *__restrict__ rowmap, int64_t n) {
+  const int ca = a_bytes >> 4, cb = b_bytes >> 4, cpr = ca + cb;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * cpr) return;
+  const int64_t i = e / cpr;
+  const int c = (int)(e - i * cpr);
+  const int r = rowmap[i];
+  if (r < 0) return;
+  if (c < ca)
+    *reinterpret_cast<uint4 *>(pa + (int64_t)r * a_bytes + 16 * c) =
+        *reinterpret_cast<const uint4 *>(a + i * a_bytes + 16 * c);
+  else
+    *reinterpret_cast<uint4 *>(pb + (int64_t)r * b_bytes + 16 * (c - ca)) =
+        *reinterpret_cast<const uint4 *>(b + i * b_bytes + 16 * (c - ca));
+}
+
+// ... and back: out[b, t] = y[rowmap[b*T + t]] where exact (t < len2[b] - reach, or the whole
+// utterance when len2[b] == T), else the constant row c (the PostNet of all-padding input) or,
+// in the last `reach` frames before T, row t - (T - reach) of the tail block.
+__global__ __launch_bounds__(256) void postnet_assemble_kernel(const float *__restrict__ y, const int32_t *__restrict__ rowmap,
+                                                               const int64_t *__restrict__ len2, int T, int C,
+                                                               const float *__restrict__ crow, const float *__restrict__ tail,
+                                                               int reach, int64_t n, float *__restrict__ out) {
+  const int v4 = C >> 2;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * v4) return;
+  const int64_t i = e / v4;
+  const int c = (int)(e - i * v4) * 4;
+  const int bq = (int)(i / T), t = (int)(i - (int64_t)bq * T);
+  const int64_t l2 = len2[bq];
+  const float *src;
+  if (l2 >= T || t < l2 - reach)
+    src = y + (int64_t)rowmap[i] * C;
+  else if (t >= T - reach)
+    src = tail + (int64_t)(t - (T - reach)) * C;
+  else
+    src = crow;
+  *reinterpret_cast<float4 *>(out + i * C + c) = *reinterpret_cast<const float4 *>(src + c);
+}
+
 }  // namespace
 
 extern "C" int fs2_embed_pe(const int64_t *tokens, const float *table, int vocab, const float *pe, int B, int L, int D,
@@ -214,4 +259,33 @@ extern "C" const char *fs2_status_string(int status) {
     case FS2_EUNSUPPORTED: return "unsupported dtype/configuration";
     default: return "unknown status";
   }
+}
+
+extern "C" int fs2_pack_rows(const void *a, int a_row_bytes, void *packed_a, const void *b, int b_row_bytes,
+                             void *packed_b, const int32_t *rowmap, int64_t n_rows, fs2_stream_t stream) {
+  if (a == nullptr || packed_a == nullptr || rowmap == nullptr || n_rows < 0 || a_row_bytes <= 0 || (a_row_bytes & 15))
+    return FS2_EINVAL;
+  if (b != nullptr && (packed_b == nullptr || b_row_bytes <= 0 || (b_row_bytes & 15))) return FS2_EINVAL;
+  if (b == nullptr) b_row_bytes = 0;
+  const int64_t work = n_rows * ((a_row_bytes + b_row_bytes) >> 4);
+  if (work == 0) return FS2_OK;
+  hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     static_cast<const char *>(a), a_row_bytes, static_cast<char *>(packed_a),
+                     static_cast<const char *>(b), b_row_bytes, static_cast<char *>(packed_b), rowmap, n_rows);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_postnet_assemble(const float *y_packed, const int32_t *rowmap, const int64_t *len2, int B, int T,
+                                    int C, const float *const_row, const float *tail, int reach, float *out,
+                                    fs2_stream_t stream) {
+  if (y_packed == nullptr || rowmap == nullptr || len2 == nullptr || const_row == nullptr || tail == nullptr ||
+      out == nullptr || B < 0 || T < 0 || C <= 0 || (C & 3) || reach < 0 || reach > T)
+    return FS2_EINVAL;
+  const int64_t n = (int64_t)B * T, work = n * (C >> 2);
+  if (work == 0) return FS2_OK;
+  hipLaunchKernelGGL(postnet_assemble_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     y_packed, rowmap, len2, T, C, const_row, tail, reach, n, out);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
 }

@@ -585,6 +585,33 @@ def _dur_kind(dur, logpred):
     raise TypeError(f"fs2amd: durations must be int64 or float32, got {dur.dtype}")
 
 
+def pack_rows(lay, a, b=None):
+    """Padded [B, T, C] rows -> packed [capacity, C] rows of SeqLayout ``lay`` (fs2_pack_rows); a
+    second tensor ``b`` in the same launch. Rows past the layout's active rows are not written."""
+    _gpu(a, b)
+    outs = []
+    for t in (a, b):
+        if t is None:
+            outs.append(None)
+            continue
+        assert t.is_contiguous() and t.shape[0] * t.shape[1] == lay.capacity, (tuple(t.shape), lay.capacity)
+        outs.append(torch.empty(lay.capacity, t.shape[-1], device=t.device, dtype=t.dtype))
+    rb = lambda t: t.shape[-1] * t.element_size()
+    L.check(_lib.fs2_pack_rows(_ptr(a), rb(a), _ptr(outs[0]), _ptr(b), rb(b) if b is not None else 0, _ptr(outs[1]),
+                               _ptr(lay.rowmap), lay.capacity, _stream(a)), "fs2_pack_rows")
+    return outs[0], outs[1]
+
+
+def postnet_assemble(y, lay, len2, const_row, tail):
+    """The PostNet valid-region output back to [B, T, C] f32 (fs2_postnet_assemble)."""
+    _gpu(y, len2, const_row, tail)
+    C = y.shape[-1]
+    out = torch.empty(lay.B, lay.T, C, device=y.device, dtype=torch.float32)
+    L.check(_lib.fs2_postnet_assemble(_ptr(y), _ptr(lay.rowmap), _ptr(len2), lay.B, lay.T, C, _ptr(const_row),
+                                      _ptr(tail), tail.shape[0], _ptr(out), _stream(y)), "fs2_postnet_assemble")
+    return out
+
+
 def lr_durations(dur, logpred=False, d_control=1.0):
     """Frame counts -> (cum int32 [B, L], mel_len int64 [B], d_rounded f32 [B, L] or None)."""
     _gpu(dur)

@@ -588,17 +588,10 @@ def _postnet_valid(P, mel, mel_bf, mel_len):
     ml = mel_len.to(torch.int64)
     lens2 = torch.where(ml + 2 * POSTNET_MARGIN > T, torch.full_like(ml, T), ml + POSTNET_MARGIN)
     lay = ops.SeqLayout(lens2, T)
-    cap = lay.capacity
-    rm = lay.rowmap.to(torch.int64)
-    dst = torch.where(rm >= 0, rm, torch.full_like(rm, cap))  # padded row -> packed row (cap: dropped)
-
-    def pack(t):
-        out = torch.empty(cap + 1, t.shape[-1], device=t.device, dtype=t.dtype)
-        out.index_copy_(0, dst, t.reshape(B * T, -1))
-        return out[:cap]
-
-    y = pack(mel if mel_bf is None else mel_bf)
-    res = pack(mel)
+    # the f32 mel (the residual) and its bf16 copy (the first conv's input) packed in one launch
+    res, y = ops.pack_rows(lay, mel.contiguous(), None if mel_bf is None else mel_bf.contiguous())
+    if y is None:
+        y = res
     n_pn = len(P.postnet)
     for i, lp in enumerate(P.postnet):
         if i < n_pn - 1:
@@ -607,15 +600,8 @@ def _postnet_valid(P, mel, mel_bf, mel_len):
         else:
             y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute, epilogue=L.EPI_BIAS_RES,
                            out_dtype=L.FS2_F32, residual=res, layout=lay)
-    # assemble [B, T, C]: computed rows where exact, else the constant row / the tail block
-    t = torch.arange(T, device=mel.device)
-    whole = (lens2 == T)[:, None]
-    keep = whole | (t[None, :] < (lens2 - POSTNET_REACH)[:, None])            # [B, T]
-    in_tail = t[None, :] >= T - POSTNET_REACH
-    const = torch.where(in_tail[..., None], tail[(t - (T - POSTNET_REACH)).clamp(min=0)][None], c[None, None])
-    src = torch.where(keep.reshape(-1), rm, torch.full_like(rm, cap))
-    y_ext = torch.cat([y, y.new_zeros(1, C)])
-    return torch.where(keep[..., None], y_ext.index_select(0, src).view(B, T, C), const)
+    # [B, T, C]: computed rows where exact, else the constant row / the tail block
+    return ops.postnet_assemble(y, lay, lens2, c.contiguous(), tail.contiguous())
 
 
 def _add_pe(x, pe):

@@ -377,6 +377,22 @@ int fs2_seq_layout(const int64_t *lens, int B, int T, int32_t *cu, int32_t *row_
 const char *fs2_version(void);
 const char *fs2_status_string(int status);
 
+/*
+ * The PostNet's valid-region form for mostly-padding batches (free-running synthesis; the
+ * reference computes the PostNet, transformer/Layers.py:92-137, on every padded frame):
+ * fs2_pack_rows — padded rows -> packed rows: row i of a (and of b, optional) goes to row
+ *   rowmap[i] (>= 0; fs2_seq_layout's rowmap) of packed_a (packed_b); rows of a_row_bytes /
+ *   b_row_bytes bytes (multiples of 16).
+ * fs2_postnet_assemble — packed PostNet output back to [B, T, C] f32: out[b, t] = y_packed[rowmap[b*T+t]]
+ *   where the packed rows are exact (t < len2[b] - reach, or every t when len2[b] == T), else the
+ *   row t - (T - reach) of tail [reach, C] for the last reach frames, else const_row [C] (the
+ *   PostNet of all-padding input). C % 4 == 0.
+ */
+int fs2_pack_rows(const void *a, int a_row_bytes, void *packed_a, const void *b, int b_row_bytes, void *packed_b,
+                  const int32_t *rowmap, int64_t n_rows, fs2_stream_t stream);
+int fs2_postnet_assemble(const float *y_packed, const int32_t *rowmap, const int64_t *len2, int B, int T, int C,
+                         const float *const_row, const float *tail, int reach, float *out, fs2_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
