@@ -110,9 +110,12 @@ def build_model(device, dtype):
     return model, pc, mc
 
 
-def time_kernel_in_forward(model, batch, n_fwd=3):
-    """Mean duration of the decoder FFN conv-k9 GEMM launches inside real (eager) forwards:
-    HIP events recorded around each launch on its stream (fs2amd.runtime.TIMERS)."""
+def time_kernel_in_forward(model, batch, n_fwd=6):
+    """Mean duration of the decoder FFN launches inside real (eager) forwards: HIP events recorded
+    around each launch on its stream (fs2amd.runtime.TIMERS entries (start, end, tag)). Returns
+    {tag: (mean seconds, launches)}: "ffn" the plain fused FFN (the last decoder block), "ffn+qkv"
+    the launches that also project the next block's Q|K|V (blocks 1..5), "conv9" the unfused
+    conv-k9 op."""
     from fs2amd import runtime
 
     # one utterance group: the timed launches have the chip to themselves (with stream groups,
@@ -124,13 +127,15 @@ def time_kernel_in_forward(model, batch, n_fwd=3):
         for _ in range(n_fwd):
             model(**batch)
     torch.cuda.synchronize()
-    ts = [a.elapsed_time(b) / 1e3 for a, b in runtime.TIMERS]
+    by = {}
+    for a, b, tag in runtime.TIMERS:
+        by.setdefault(tag, []).append(a.elapsed_time(b) / 1e3)
     runtime.TIMERS = None
     if prev is None:
         del os.environ["FS2_STREAMS"]
     else:
         os.environ["FS2_STREAMS"] = prev
-    return sum(ts) / len(ts), len(ts)
+    return {k: (sum(v) / len(v), len(v)) for k, v in by.items()}
 
 
 def ffn_fused(model, batch, device):
@@ -612,7 +617,8 @@ def main():
     elapsed, tot_frames = parallel.aggregate(elapsed, frames, device)
     extra = extra_workloads(model, args, rank, device) if args.extra else {}
 
-    eager_s, n_launch = time_kernel_in_forward(model, batch)
+    timed = time_kernel_in_forward(model, batch)
+    eager_s, n_launch = timed.get("ffn", timed.get("conv9", (float("nan"), 0)))
     standalone_s, kernel_flops = time_dominant_kernel(model, batch_cpu, device, args.kernel_reps)
     table = None
     if args.dtype == "bf16":
@@ -624,8 +630,9 @@ def main():
     # back-to-back calls (decoder_ops) run slower (likely clocks under sustained MFMA load)
     kernel_s = eager_s
     fused = ffn_fused(model, batch_cpu, device)
-    timing = ("HIP events around each decoder fused-FFN launch in 3 eager forwards" if fused else
-              "HIP events around each decoder conv-k9 op call (both launches) in 3 eager forwards")
+    timing = ("HIP events around the last decoder block's fused-FFN launch in 6 eager forwards (blocks 1-5 "
+              "also project the next block's Q|K|V: 'with_next_qkv')" if fused else
+              "HIP events around each decoder conv-k9 op call (both launches) in 6 eager forwards")
     ms_per_step = elapsed / args.steps * 1e3
     value = tot_frames * args.steps / elapsed
     peak = {"bf16": BF16_PEAK_TFLOPS, "fp8": FP8_PEAK_TFLOPS}.get(args.dtype, F32_PEAK_TFLOPS)
@@ -664,6 +671,11 @@ def main():
                      "op_calls_timed": n_launch,
                      "kernel_ms_standalone_random": round(standalone_s * 1e3, 4),
                      "flops_per_launch": kernel_flops,
+                     **({"with_next_qkv": {
+                         "kernel_ms": round(timed["ffn+qkv"][0] * 1e3, 4), "launches": timed["ffn+qkv"][1],
+                         "flops_per_launch": kernel_flops * (1 + 2 * 256 * 768 / 5242880),
+                         "achieved": round(kernel_flops * (1 + 2 * 256 * 768 / 5242880) / timed["ffn+qkv"][0] / 1e12, 2)}}
+                        if "ffn+qkv" in timed else {}),
                      "traffic_note": "2*FETCH_SIZE + WRITE_SIZE per launch (rocprofv3 PMC, profiles/"
                                      + ("ffn_traffic.json)" if fused else "conv9_traffic.json)")},
     }

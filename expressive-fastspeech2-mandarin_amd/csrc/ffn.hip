@@ -58,6 +58,13 @@ struct FfnArgs {
   int *cnt;            // [tiles] arrival counters (zero between launches)
   void *part;          // f32 partial Y^T accumulators, part_bytes(MB) per (tile, split)
   uint32_t part_bytes;
+  // the NEXT FFT block's Q|K|V projection of y (optional): qkv[m, :] = y[m, :] . wq^T + bq
+  const bf16 *wq;      // [nq][256] in fragment order [nq/64][8][4][4][16][8]
+  const float *bq;     // [nq]
+  bf16 *qkv;           // [rows, >= nq]
+  int64_t qs;          // qkv row stride (elements)
+  uint32_t wq_bytes;
+  int nq;              // multiple of 256
 };
 
 // f32 partial Y^T accumulators per (tile, split): 4 waves x acc2[4][MB] x 64 lanes x 16 B
@@ -109,6 +116,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   constexpr int RED_OFF = EP_OFF + 3 * kD * 4;      // LN row statistics: [BM rows][4 waves] f32
   constexpr int SMEM = RED_OFF + BM * 16;
   static_assert(SMEM <= 163840, "LDS");
+  static_assert(BM * 528 <= 4 * XP_PER_WAVE * 1024, "Q|K|V staging fits in the x region");
   constexpr int NK1 = KS * (kD / 32);  // GEMM1 units per chunk (tap-major, 8 k-steps per tap)
   constexpr int NK2 = kChunk / 32;     // GEMM2 units per chunk
   constexpr int NU = NK1 + NK2;
@@ -616,6 +624,92 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
         *reinterpret_cast<uint4 *>(ob + (size_t)(m0 + m) * orow + ch * 16) =
             *reinterpret_cast<const uint4 *>(smem + H_OFF + m * 512 + (xchunk(m, ch) << 4));
     }
+    // ---- the next block's Q|K|V projection (transformer/SubLayers.py:39-41 of block i+1) while
+    // y is still on chip: GEMM3 Q|K|V^T[n, m] = sum_c Wq[n, c] . y[m, c] in passes of 256 output
+    // columns (wave w: 64 of them, the accumulators of the dead H^T registers), y read from the H
+    // region exactly as GEMM2 read H, weights through the same register ring; + bias, bf16,
+    // staged in the x region (pitch 528: the 8-byte column writes of 16 rows conflict-free) and
+    // stored as whole 512-byte row segments. Saves the Q|K|V launch's re-read of y and its tiles.
+    if (p.wq != nullptr) {
+      const rsrc_t qr = make_rsrc(p.wq, p.wq_bytes);
+      auto qload = [&](auto S, uint32_t so) {
+        constexpr int s = decltype(S)::value;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          auto v = __builtin_amdgcn_raw_buffer_load_b128(qr, lane_off + jb * 1024, so, 0);
+          pa[s][jb] = __builtin_bit_cast(bf16x8, v);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      constexpr int SPITCH = 528;
+      const uint32_t qrow = (uint32_t)p.qs * 2u;
+      char *qb = reinterpret_cast<char *>(p.qkv);
+      const int npass = p.nq / 256;
+      auto qbase = [&](int ps) { return (uint32_t)((ps * 4 + w) * 8) * (uint32_t)kUnit; };
+      // raw barrier: LDS traffic retired, global stores left in flight (they overlap the next pass)
+      auto lbar = [&]() {
+        __builtin_amdgcn_s_waitcnt(kLgkm0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      static_for<DEPTH>([&](auto I) { qload(I, qbase(0) + (uint32_t)(decltype(I)::value * kUnit)); });
+#pragma nounroll
+      for (int ps = 0; ps < npass; ++ps) {
+        const uint32_t base = qbase(ps);
+        float z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) acc1[jb][mb] = f32x4{z, z, z, z};
+        read_h(0, f0);
+        static_for<8>([&](auto Q) {
+          constexpr int q = decltype(Q)::value, sl = q % DEPTH;
+          if constexpr (q + 1 < 8) {
+            if constexpr (q & 1)
+              read_h(q + 1, f0);
+            else
+              read_h(q + 1, f1);
+          }
+          if constexpr (q & 1)
+            mma(acc1, pa[sl], f1);
+          else
+            mma(acc1, pa[sl], f0);
+          if constexpr (q + DEPTH < 8)
+            qload(std::integral_constant<int, sl>{}, base + (uint32_t)((q + DEPTH) * kUnit));
+          else  // the next pass's first units (past the last pass: harmless reloads of pass 0)
+            qload(std::integral_constant<int, sl>{},
+                  (ps + 1 < npass ? qbase(ps + 1) : qbase(0)) + (uint32_t)((q + DEPTH - 8) * kUnit));
+        });
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          const int c = w * 64 + jb * 16 + 4 * hi;  // column inside this pass
+          const float4 bb = *reinterpret_cast<const float4 *>(p.bq + ps * 256 + c);
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) {
+            const f32x4 v = acc1[jb][mb];
+            bf16x4 o;
+            o[0] = (bf16)(v[0] + bb.x);
+            o[1] = (bf16)(v[1] + bb.y);
+            o[2] = (bf16)(v[2] + bb.z);
+            o[3] = (bf16)(v[3] + bb.w);
+            *reinterpret_cast<bf16x4 *>(smem + X_OFF + (hrow0 + mb * 16) * SPITCH + c * 2) = o;
+          }
+        }
+        lbar();
+#pragma unroll 2
+        for (int i = tid; i < BM * 32; i += 256) {
+          const int m = i >> 5, ch = i & 31;
+          if (m0 + m < M)
+            *reinterpret_cast<uint4 *>(qb + (size_t)(m0 + m) * qrow + ps * 512 + ch * 16) =
+                *reinterpret_cast<const uint4 *>(smem + X_OFF + m * SPITCH + ch * 16);
+        }
+        lbar();  // the staging region is rewritten by the next pass
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the harmless past-the-end reloads
+    }
   }
   stamp(5 + 2 * NCH);
   if (FFN_TRACE) {
@@ -694,6 +788,17 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   p.w = reinterpret_cast<const bf16 *>(d->w);
   p.b1 = d->b1;
   p.w_bytes = (uint32_t)wb;
+  if (d->wqkv != nullptr) {
+    if (d->bqkv == nullptr || d->qkv_out == nullptr || d->nqkv <= 0 || (d->nqkv % 256) ||
+        d->qkv_row_stride < d->nqkv || (d->qkv_row_stride & 7) || d->qkv_out == d->x || d->qkv_out == d->out)
+      return FS2_EINVAL;
+    p.wq = reinterpret_cast<const bf16 *>(d->wqkv);
+    p.bq = d->bqkv;
+    p.qkv = reinterpret_cast<bf16 *>(d->qkv_out);
+    p.qs = d->qkv_row_stride;
+    p.nq = d->nqkv;
+    p.wq_bytes = (uint32_t)((int64_t)d->nqkv * kD * 2);
+  }
   if (d->rows_max < 0 || !(d->tile_rows == 0 || d->tile_rows == 112 || d->tile_rows == 64)) return FS2_EINVAL;
   const int MB = d->tile_rows == 64 ? 4 : 7, BM = 16 * MB;
   const int64_t kPartBytes = part_bytes(MB);

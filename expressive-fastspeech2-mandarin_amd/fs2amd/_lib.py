@@ -73,6 +73,7 @@ class FfnDesc(ctypes.Structure):
         ("rows_dev", _p), ("row_pos", _p),
         ("nsplit", _i), ("splitk_ws", _p), ("splitk_ws_bytes", _i64), ("rows_max", _i),
         ("tile_rows", _i),
+        ("wqkv", _p), ("bqkv", _p), ("qkv_out", _p), ("qkv_row_stride", _i64), ("nqkv", _i),
     ]
 
 

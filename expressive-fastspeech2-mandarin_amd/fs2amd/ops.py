@@ -376,13 +376,24 @@ def ffn_nsplit(rows, F):
     return ffn_form(rows, F)[1]
 
 
+def pack_frag_rows(w):
+    """A [N, K] weight (N, K multiples of 64 / 32) in the MFMA fragment order the fused kernels
+    stream to registers: [N/64][K/32][4 blocks][4 hi][16 r][8] (fs2_ffn w_2, fs2_ffn wqkv)."""
+    N, K = w.shape[0], w.shape[1]
+    assert N % 64 == 0 and K % 32 == 0, (N, K)
+    b = w.detach().float().reshape(N // 64, 4, 16, K // 32, 4, 8).permute(0, 3, 1, 4, 2, 5)
+    return b.reshape(-1).to(torch.bfloat16).contiguous()
+
+
 def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=None, layout=None, out=None,
-        nsplit=None, tile_rows=None):
+        nsplit=None, tile_rows=None, next_qkv=None):
     """PositionwiseFeedForward + residual + LayerNorm + mask in one launch (fs2_ffn): bf16 rows of
     256 (padded [B, T, 256] or packed [B*T, 256] in ``layout``); ``w_packed`` from
     :func:`pack_ffn_weights`. The hidden [rows, F] never reaches HBM. ``tile_rows`` (112 / 64) and
     ``nsplit`` (workgroups per row tile): None = :func:`ffn_form` of the row count the host knows
-    (``layout.rows_hint`` or the capacity)."""
+    (``layout.rows_hint`` or the capacity). ``next_qkv`` = (wqkv in :func:`pack_frag_rows` order,
+    bqkv f32): the epilogue also projects the output rows to the next block's Q|K|V; returns
+    (out, qkv) then (qkv None otherwise)."""
     _gpu(x, w_packed, b1, b2, lens, addvec1, addvec2)
     if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
         raise TypeError("fs2amd.ffn: bf16 activations and weights only")
@@ -426,8 +437,15 @@ def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=No
         if ws is None:
             raise RuntimeError("fs2amd.ffn: nsplit > 1 needs the split-K workspace (ops.splitk_enabled)")
         d.nsplit, d.splitk_ws, d.splitk_ws_bytes = int(nsplit), ws.data_ptr(), ws.numel()
+    qkv = None
+    if next_qkv is not None:
+        wq, bq = next_qkv
+        nq = bq.numel()
+        assert wq.is_contiguous() and wq.numel() == nq * D, (tuple(wq.shape), nq, D)
+        qkv = torch.empty(*x.shape[:-1], nq, device=x.device, dtype=torch.bfloat16)
+        d.wqkv, d.bqkv, d.qkv_out, d.qkv_row_stride, d.nqkv = wq.data_ptr(), bq.data_ptr(), qkv.data_ptr(), nq, nq
     L.check(_lib.fs2_ffn(ctypes.byref(d), _stream(x)), "fs2_ffn")
-    return out
+    return (out, qkv) if next_qkv is not None else out
 
 
 def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None):

@@ -20,7 +20,7 @@ from types import SimpleNamespace
 import torch
 
 from . import _lib as L
-from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split, pack_ffn_weights, \
+from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split, pack_ffn_weights, pack_frag_rows, \
     pack_wconv_weight
 
 
@@ -55,6 +55,9 @@ def _fft_layer(layer, device, compute, key=None, fp8_scales=None):
         k2=f.w_2.kernel_size[0], p2=f.w_2.padding[0], c2=f.w_2.in_channels,
         ln2=(_f32(f.layer_norm.weight, device), _f32(f.layer_norm.bias, device), f.layer_norm.eps),
         w12=_ffn_pair(f, device, compute),
+        # Q|K|V in fragment order for the previous block's fused FFN epilogue (fs2_ffn wqkv)
+        wqf=pack_frag_rows(wqkv) if compute == L.FS2_BF16 and wqkv.shape[0] % 256 == 0 and wqkv.shape[1] == 256
+        else None,
     )
 
 

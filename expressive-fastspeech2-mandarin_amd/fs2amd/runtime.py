@@ -66,11 +66,15 @@ def _fp8_like(x, layout, width):
     return torch.empty(*x.shape[:-1], width, device=x.device, dtype=torch.float8_e4m3fn)
 
 
-def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=None, x8=None, next_s=None):
-    """One FFT block (transformer/Layers.py:21-30) = 5 launches. With ``layout`` (ops.SeqLayout)
+def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=None, x8=None, next_s=None,
+              qkv=None, nxt=None):
+    """One FFT block (transformer/Layers.py:21-30) = 4 launches. With ``layout`` (ops.SeqLayout)
     x is packed [B*T, d_model]: only valid frames exist and no mask is applied (nothing to mask).
     fp8 (cfg5): ``x8`` is the fp8 copy of x for the Q|K|V GEMM; ``next_s`` asks for an fp8 copy
-    of the block output at that scale (the next block's Q|K|V input). Returns (out, out8|None)."""
+    of the block output at that scale (the next block's Q|K|V input). ``qkv``: this block's Q|K|V
+    projection, already computed by the previous block's fused FFN; ``nxt``: the next block's
+    packed layer, whose Q|K|V projection the fused FFN then computes in its epilogue.
+    Returns (out, out8|None, next block's qkv|None)."""
     c = P.compute
     dt = P.act_dtype
     H, dk = lp.n_head, lp.d_k
@@ -82,7 +86,9 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
         rows = int(layout.cu[-1]) if layout is not None else None
         xv = x[:rows] if rows is not None else x
         CALIB.setdefault(lp.key, {})["x"] = float(xv.float().abs().max()) if xv.numel() else 0.0
-    if q is not None and q.wqkv is not None and x8 is not None:
+    if qkv is not None:
+        pass
+    elif q is not None and q.wqkv is not None and x8 is not None:
         qkv = ops.conv1d(x8, q.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=L.FS2_FP8, epilogue=L.EPI_BIAS,
                          out_dtype=dt, col_scale=q.cs_qkv, layout=layout)
     else:
@@ -107,41 +113,50 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
                         layout=layout)
         if timed and TIMERS is not None:
             e1.record()
-            TIMERS.append((e0, e1))
+            TIMERS.append((e0, e1, "conv9"))
         y8 = _fp8_like(x, layout, d_model) if next_s is not None else None
         y = ops.conv1d(f8, q.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=L.FS2_FP8,
                        epilogue=L.EPI_RES_LN, out_dtype=dt, residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1,
                        addvec2=addvec2, layout=layout, col_scale=q.cs2, out2=y8,
                        out2_scale=1.0 / next_s if next_s is not None else 1.0)
-        return y, y8
+        return y, y8, None
     if timed and TIMERS is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
     if ffn_fused_ok(P, lp, h, layout) and CALIB is None:
         # the whole FFN (conv-k9 + ReLU + conv-k1 + residual + LN + mask) as one launch: the
         # [rows, 1024] hidden stays on chip
-        y = ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, lens=lens, addvec1=addvec1,
-                    addvec2=addvec2, layout=layout)
+        fuse_qkv = nxt is not None and getattr(nxt, "wqf", None) is not None and \
+            (nxt.fp8 is None or nxt.fp8.wqkv is None) and qkv_fused_on()
+        r = ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, lens=lens, addvec1=addvec1,
+                    addvec2=addvec2, layout=layout, next_qkv=(nxt.wqf, nxt.bqkv) if fuse_qkv else None)
+        y, qn = r if fuse_qkv else (r, None)
         if timed and TIMERS is not None:
             e1.record()
-            TIMERS.append((e0, e1))
-        return y, None
+            TIMERS.append((e0, e1, "ffn+qkv" if fuse_qkv else "ffn"))
+        return y, None, qn
     f = ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=c, epilogue=L.EPI_BIAS_RELU, out_dtype=dt,
                    layout=layout)
     if timed and TIMERS is not None:
         e1.record()
-        TIMERS.append((e0, e1))
+        TIMERS.append((e0, e1, "conv9"))
     if CALIB is not None and lp.key is not None:
         rows = int(layout.cu[-1]) if layout is not None else None
         hv, fv = (h[:rows], f[:rows]) if rows is not None else (h, f)
         CALIB[lp.key]["h"] = float(hv.float().abs().max()) if hv.numel() else 0.0
         CALIB[lp.key]["f"] = float(fv.float().abs().max()) if fv.numel() else 0.0
     return ops.conv1d(f, lp.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
-                      residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2, layout=layout), None
+                      residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2, layout=layout), None, None
 
 
 FFN_FUSED_MIN_ROWS = 16384
 FFN_SPLIT_MIN_WG = 128
+
+
+def qkv_fused_on():
+    """The next block's Q|K|V projection in the fused FFN's epilogue (fs2_ffn wqkv). FS2_QKV_FUSED=0:
+    separate Q|K|V launches (A/B)."""
+    return os.environ.get("FS2_QKV_FUSED", "1") != "0"
 
 
 def ffn_fused_ok(P, lp, h, layout):
@@ -170,14 +185,14 @@ def ffn_fused_ok(P, lp, h, layout):
 
 def _stack(P, layers, x, lens, layout=None, timed=False, addvecs=(None, None)):
     """FFT-block stack; in fp8 mode each block hands the next one an fp8 copy of its output."""
-    x8 = None
+    x8 = qkv = None
     n = len(layers)
     for i, lp in enumerate(layers):
         nxt = layers[i + 1] if i + 1 < n else None
         next_s = nxt.fp8.s_x if (nxt is not None and nxt.fp8 is not None and nxt.fp8.wqkv is not None) else None
         last = i == n - 1
-        x, x8 = fft_block(P, lp, x, lens, addvecs[0] if last else None, addvecs[1] if last else None, timed=timed,
-                          layout=layout, x8=x8, next_s=next_s)
+        x, x8, qkv = fft_block(P, lp, x, lens, addvecs[0] if last else None, addvecs[1] if last else None,
+                               timed=timed, layout=layout, x8=x8, next_s=next_s, qkv=qkv, nxt=nxt)
     return x
 
 

@@ -210,6 +210,16 @@ typedef struct fs2_ffn_desc {
   int tile_rows;            /* rows per workgroup tile: 0 / 112 (default) or 64 (the split-hidden
                                form of small launches: 4 splits x 64-row tiles fill the chip, and
                                the last arriver loads the other partials in one round trip)       */
+  /* the NEXT FFT block's Q|K|V projection fused into the epilogue (optional, wqkv NULL = off):
+     qkv_out[m, n] = bf16( sum_c y[m, c] * wqkv[n][c] + bqkv[n] ), n < nqkv (a multiple of 256),
+     for every stored row m (transformer/SubLayers.py:39-41 of block i+1, on block i's output).
+     wqkv in fragment order [nqkv/64][D/32][4][4][16][8], element (q, s, b, h, r, e) =
+     W[64q + 16b + r][32s + 8h + e] (W = [w_qs; w_ks; w_vs], [nqkv][D]).                     */
+  const void *wqkv;
+  const float *bqkv;
+  void *qkv_out;
+  int64_t qkv_row_stride;
+  int nqkv;
 } fs2_ffn_desc;
 
 int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream);

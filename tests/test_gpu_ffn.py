@@ -217,3 +217,43 @@ def test_ffn_form_rule(gpu):
         assert ns == 1 or 4096 + -(-rows // tr) * ns * ops.ffn_part_bytes(tr) <= ops.SPLITK_WS_BYTES
     with ops.splitk_enabled(False):
         assert ops.ffn_form(4096, 1024) == (112, 1)
+
+
+@pytest.mark.parametrize("tile_rows,nsplit,packed", [(112, 1, True), (64, 4, False), (112, 2, True), (64, 1, False)])
+def test_ffn_next_qkv_epilogue(gpu, tile_rows, nsplit, packed):
+    """fs2_ffn with the next block's Q|K|V projection in its epilogue: qkv = bf16(y . W^T + b) on
+    the kernel's own bf16 output rows (float64 reference of the same operands: bf16 output
+    rounding), y unchanged by the extra epilogue, rows past the active packed rows untouched."""
+    ops, L = gpu
+    B, T = 19, 140
+    W = _weights(ops, L, seed=31)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    lens = torch.randint(1, T + 1, (B,), generator=g)
+    lens[0] = T
+    lens = lens.to(DEV)
+    x = _x(B, T, lens, 31)
+    gd = torch.Generator(device=DEV).manual_seed(32)
+    wq = torch.randn(768, 256, device=DEV, generator=gd) / 16
+    bq = 0.1 * torch.randn(768, device=DEV, generator=gd)
+    wqf = ops.pack_frag_rows(wq)
+    kw = dict(ks=9, pad=4, ln=W["ln"], nsplit=nsplit, tile_rows=tile_rows)
+    if packed:
+        lay = ops.SeqLayout(lens, T)
+        rm = lay.rowmap.long()
+        ok = rm >= 0
+        xp = x.new_zeros(lay.capacity, 256)
+        xp[rm[ok]] = x.reshape(-1, 256)[ok]
+        y0 = ops.ffn(xp, W["w12"], W["b1"], W["b2"], layout=lay, **kw)
+        y, qkv = ops.ffn(xp, W["w12"], W["b1"], W["b2"], layout=lay, next_qkv=(wqf, bq), **kw)
+        R = int(lay.cu[-1])
+        y0, y, qkv = y0[:R], y[:R], qkv[:R]
+    else:
+        y0 = ops.ffn(x, W["w12"], W["b1"], W["b2"], lens=lens, **kw)
+        y, qkv = ops.ffn(x, W["w12"], W["b1"], W["b2"], lens=lens, next_qkv=(wqf, bq), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+    ref = y.double().reshape(-1, 256) @ wq.to(torch.bfloat16).double().t() + bq.double()
+    err = (qkv.double().reshape(-1, 768) - ref).abs()
+    scale = float(ref.abs().max())
+    assert float(err.max()) <= 1e-2 * scale, (float(err.max()), scale)
+    assert float(err.mean()) <= 1e-3 * scale, (float(err.mean()), scale)
