@@ -246,14 +246,16 @@ __global__ __launch_bounds__(256) void seq_rows_kernel(const int32_t *__restrict
 constexpr int kSeqMaxB = 4096;
 __global__ __launch_bounds__(256) void seq_layout_kernel(const int64_t *__restrict__ lens, int B, int T,
                                                          int32_t *__restrict__ cu, int2 *__restrict__ row_pos,
-                                                         int32_t *__restrict__ rowmap) {
+                                                         int32_t *__restrict__ rowmap, int margin) {
   __shared__ int32_t scu[kSeqMaxB + 1];
   __shared__ int32_t wsum[4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (B + 255) / 256;
   const int i0 = min(tid * per, B), i1 = min(i0 + per, B);
+  // margin > 0 (the PostNet valid-region rows): len + margin frames, or all T when len + 2 margin > T
   auto clen = [&](int i) {
-    const int64_t l = lens[i];
+    int64_t l = lens[i];
+    if (margin > 0) l = l + 2 * (int64_t)margin > T ? T : l + margin;
     return (int32_t)(l < 0 ? 0 : (l > T ? T : l));
   };
   int32_t local = 0;
@@ -284,19 +286,60 @@ __global__ __launch_bounds__(256) void seq_layout_kernel(const int64_t *__restri
   if (row_pos != nullptr && t < len) row_pos[c + t] = make_int2(t, len);
 }
 
+// [max(len), sum(len), *bad] as int32 (lengths clamped to [0, 2^31 - 1]): the free-running
+// path's one host read in one launch. One workgroup.
+__global__ __launch_bounds__(256) void len_stats_kernel(const int64_t *__restrict__ lens, int B,
+                                                        const int32_t *__restrict__ bad, int32_t *__restrict__ meta) {
+  __shared__ int64_t smax[4], ssum[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int64_t mx = 0, sm = 0;
+  for (int i = tid; i < B; i += 256) {
+    const int64_t l = lens[i] < 0 ? 0 : lens[i];
+    mx = l > mx ? l : mx;
+    sm += l;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(mx, o), b = __shfl_xor(sm, o);
+    mx = a > mx ? a : mx;
+    sm += b;
+  }
+  if (lane == 0) {
+    smax[wv] = mx;
+    ssum[wv] = sm;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int64_t m = 0, t = 0;
+    for (int w = 0; w < 4; ++w) {
+      m = smax[w] > m ? smax[w] : m;
+      t += ssum[w];
+    }
+    meta[0] = (int32_t)(m < 0x7fffffff ? m : 0x7fffffff);
+    meta[1] = (int32_t)(t < 0x7fffffff ? t : 0x7fffffff);
+    meta[2] = bad != nullptr ? *bad : 0;
+  }
+}
+
 }  // namespace
+
+extern "C" int fs2_seq_layout_margin(const int64_t *lens, int B, int T, int margin, int32_t *cu, int32_t *row_pos,
+                                     int32_t *rowmap, fs2_stream_t stream) {
+  if (lens == nullptr || cu == nullptr || B < 0 || T < 0 || margin < 0 || B > kSeqMaxB ||
+      (int64_t)B * T > 0x7fffff00LL)
+    return FS2_EINVAL;
+  const int64_t n = (int64_t)B * T;
+  hipLaunchKernelGGL(seq_layout_kernel, dim3((unsigned)(n > 0 ? (n + 255) / 256 : 1)), dim3(256), 0, as_stream(stream),
+                     lens, B, T, cu, reinterpret_cast<int2 *>(row_pos), rowmap, margin);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
 
 extern "C" int fs2_seq_layout(const int64_t *lens, int B, int T, int32_t *cu, int32_t *row_pos, int32_t *rowmap,
                               fs2_stream_t stream) {
   if (lens == nullptr || cu == nullptr || B < 0 || T < 0 || (int64_t)B * T > 0x7fffff00LL) return FS2_EINVAL;
   hipStream_t s = as_stream(stream);
-  if (B <= kSeqMaxB) {
-    const int64_t n = (int64_t)B * T;
-    hipLaunchKernelGGL(seq_layout_kernel, dim3((unsigned)(n > 0 ? (n + 255) / 256 : 1)), dim3(256), 0, s, lens, B, T,
-                       cu, reinterpret_cast<int2 *>(row_pos), rowmap);
-    FS2_CHECK_LAUNCH();
-    return FS2_OK;
-  }
+  if (B <= kSeqMaxB) return fs2_seq_layout_margin(lens, B, T, 0, cu, row_pos, rowmap, stream);
   hipLaunchKernelGGL(seq_cu_kernel, dim3(1), dim3(256), 0, s, lens, B, T, cu);
   FS2_CHECK_LAUNCH();
   if ((rowmap != nullptr || row_pos != nullptr) && (int64_t)B * T > 0) {
@@ -357,4 +400,11 @@ extern "C" int fs2_length_regulate(const void *x, int x_dtype, const void *dur, 
   int rc = fs2_lr_durations(dur, dur_kind, d_control, B, L, cum, mel_len, d_rounded, stream);
   if (rc != FS2_OK) return rc;
   return fs2_lr_expand(x, x_dtype, cum, mel_len, B, L, D, T_out, pe, out, out_dtype, index_map, nullptr, stream);
+}
+
+extern "C" int fs2_len_stats(const int64_t *lens, int B, const int32_t *bad_counter, int32_t *meta, fs2_stream_t stream) {
+  if (lens == nullptr || meta == nullptr || B < 0) return FS2_EINVAL;
+  hipLaunchKernelGGL(len_stats_kernel, dim3(1), dim3(256), 0, as_stream(stream), lens, B, bad_counter, meta);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
 }

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const char *__restrict__
 // utterance when len2[b] == T), else the constant row c (the PostNet of all-padding input) or,
 // in the last `reach` frames before T, row t - (T - reach) of the tail block.
 __global__ __launch_bounds__(256) void postnet_assemble_kernel(const float *__restrict__ y, const int32_t *__restrict__ rowmap,
-                                                               const int64_t *__restrict__ len2, int T, int C,
+                                                               const int32_t *__restrict__ cu, int T, int C,
                                                                const float *__restrict__ crow, const float *__restrict__ tail,
                                                                int reach, int64_t n, float *__restrict__ out) {
   const int v4 = C >> 2;
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void postnet_assemble_kernel(const float *__re
   const int64_t i = e / v4;
   const int c = (int)(e - i * v4) * 4;
   const int bq = (int)(i / T), t = (int)(i - (int64_t)bq * T);
-  const int64_t l2 = len2[bq];
+  const int l2 = cu[bq + 1] - cu[bq];
   const float *src;
   if (l2 >= T || t < l2 - reach)
     src = y + (int64_t)rowmap[i] * C;
@@ -276,16 +276,16 @@ extern "C" int fs2_pack_rows(const void *a, int a_row_bytes, void *packed_a, con
   return FS2_OK;
 }
 
-extern "C" int fs2_postnet_assemble(const float *y_packed, const int32_t *rowmap, const int64_t *len2, int B, int T,
+extern "C" int fs2_postnet_assemble(const float *y_packed, const int32_t *rowmap, const int32_t *cu, int B, int T,
                                     int C, const float *const_row, const float *tail, int reach, float *out,
                                     fs2_stream_t stream) {
-  if (y_packed == nullptr || rowmap == nullptr || len2 == nullptr || const_row == nullptr || tail == nullptr ||
+  if (y_packed == nullptr || rowmap == nullptr || cu == nullptr || const_row == nullptr || tail == nullptr ||
       out == nullptr || B < 0 || T < 0 || C <= 0 || (C & 3) || reach < 0 || reach > T)
     return FS2_EINVAL;
   const int64_t n = (int64_t)B * T, work = n * (C >> 2);
   if (work == 0) return FS2_OK;
   hipLaunchKernelGGL(postnet_assemble_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, as_stream(stream),
-                     y_packed, rowmap, len2, T, C, const_row, tail, reach, n, out);
+                     y_packed, rowmap, cu, T, C, const_row, tail, reach, n, out);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

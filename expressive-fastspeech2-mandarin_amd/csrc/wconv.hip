@@ -49,24 +49,30 @@ __device__ __forceinline__ void static_for(Fn &&f) {
 
 constexpr int kLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0) the compiler's wait-count pass sees
 
+// CIN % 32 != 0 (the PostNet's first conv, 80 -> 512): the K dimension is (tap, channel) flattened,
+// k = tap * CIN + c, in 32-wide steps ("flat" units); a lane group's 8 consecutive k stay inside one
+// tap (CIN % 8 == 0), so each lane addresses its own (row + tap, channel) per unit.
 template <int KS, int CIN, int WQ>
 __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
+  constexpr bool FLAT = CIN % 32 != 0;
+  static_assert(CIN % 8 == 0, "8-channel lane groups");
   // WQ: 64-column quads per wave (1: 8 waves, two per SIMD; 2: 4 waves, 128 columns each)
   constexpr int MB = 7, BM = 16 * MB, NWV = 8 / WQ, NT = 64 * NWV, NCOL = 512, JB = 4 * WQ;
   constexpr int XROWS = BM + KS - 1;
-  constexpr int XPITCH = CIN * 2 + 32;
+  constexpr int XPITCH = FLAT ? CIN * 2 + 16 : CIN * 2 + 32;  // 80 ch: 176 B, rows in distinct bank quads
   constexpr int XPIECES = (XROWS * XPITCH + 1023) / 1024;
   constexpr int XP_PER_WAVE = (XPIECES + NWV - 1) / NWV;
-  constexpr int NKS = CIN / 32;                        // k-steps (units) per tap
-  constexpr int ZBYTES = NKS * 64;                      // zero region: a masked row reads base 0 + 64 ks
+  constexpr int NKS = FLAT ? 1 : CIN / 32;             // k-steps (units) per tap
+  constexpr int ZBYTES = FLAT ? 64 : NKS * 64;          // zero region: a masked row reads base 0 + 64 ks
   constexpr int X_OFF = ZBYTES;
-  constexpr int BIAS_OFF = X_OFF + NWV * XP_PER_WAVE * 1024;
-  constexpr int SMEM = BIAS_OFF + NCOL * 4;
   constexpr int OPITCH = NCOL * 2 + 16;                 // output staging pitch
-  static_assert(BM * OPITCH <= NWV * XP_PER_WAVE * 1024, "staging fits in the x region");
+  // the x region doubles as the output staging area (sized for the larger of the two)
+  constexpr int XREG = NWV * XP_PER_WAVE * 1024 > BM * OPITCH ? NWV * XP_PER_WAVE * 1024 : BM * OPITCH;
+  constexpr int BIAS_OFF = X_OFF + XREG;
+  constexpr int SMEM = BIAS_OFF + NCOL * 4;
   static_assert(SMEM <= 163840, "LDS");
   constexpr int DEPTH = WQ == 1 ? 4 : 2;
-  static_assert(NKS % DEPTH == 0, "static ring slots");
+  static_assert(FLAT || NKS % DEPTH == 0, "static ring slots");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -110,7 +116,7 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
   }
 
   // weight stream: unit u = tap * NKS + ks of this wave's 64 rows; past the last unit a harmless reload
-  constexpr int NU = KS * NKS;
+  constexpr int NU = FLAT ? (KS * CIN + 31) / 32 : KS * NKS;
   const uint32_t wbase = (uint32_t)(w * WQ * NU) * (uint32_t)kUnitB, lane_off = (uint32_t)lane * 16u;
   bf16x8 pa[DEPTH][JB];
   auto load_at = [&](auto S, int u) {
@@ -155,6 +161,36 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * DEPTH) : "memory");
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   __syncthreads();
+  if constexpr (FLAT) {
+    // unit u, lane group hi: k = 32u + 8hi -> (tap, channel); k >= KS * CIN: zero weights, any
+    // in-tile address (the zero region)
+    auto bases_flat = [&](int u, int (&ad)[MB]) {
+      const int k = 32 * u + 8 * hi;
+      const int tap = k / CIN, c = k - tap * CIN;
+      const int base = X_OFF + (hrow0 + tap) * XPITCH + c * 2;
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+        ad[mb] = tap < KS ? (base + mb * 16 * XPITCH) & __builtin_amdgcn_sbfe(vmask[mb], tap, 1) : 0;
+    };
+    int ad[MB];
+    bases_flat(0, ad);
+    issue_x(ad, std::integral_constant<int, 0>{}, f0);
+    static_for<NU>([&](auto UI) {
+      constexpr int u = decltype(UI)::value;
+      if constexpr (u + 1 < NU) {
+        bases_flat(u + 1, ad);
+        if constexpr (u & 1)
+          issue_x(ad, std::integral_constant<int, 0>{}, f0);
+        else
+          issue_x(ad, std::integral_constant<int, 0>{}, f1);
+      }
+      if constexpr (u & 1)
+        mma(pa[u % DEPTH], f1);
+      else
+        mma(pa[u % DEPTH], f0);
+      load_at(std::integral_constant<int, u % DEPTH>{}, u + DEPTH);
+    });
+  } else {
   int bxc[MB], bxn[MB];
   bases_x(0, bxc);
   issue_x(bxc, std::integral_constant<int, 0>{}, f0);
@@ -179,6 +215,7 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
     });
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) bxc[mb] = bxn[mb];
+  }
   }
 
   // epilogue: + bias, tanh, bf16 -> LDS staging (the x region) -> whole-row stores
@@ -215,7 +252,7 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
 
 }  // namespace
 
-extern "C" int64_t fs2_wconv_weight_elems(int KS, int Cin, int N) { return (int64_t)N * KS * Cin; }
+extern "C" int64_t fs2_wconv_weight_elems(int KS, int Cin, int N) { return (int64_t)N * ((KS * Cin + 31) / 32 * 32); }
 
 extern "C" int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream) {
   if (d == nullptr || d->x == nullptr || d->w == nullptr || d->bias == nullptr || d->out == nullptr)
@@ -223,7 +260,8 @@ extern "C" int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream) {
   if (d->B < 0 || d->T < 0 || d->pad < 0 || d->x_row_stride < d->Cin || (d->x_row_stride & 7) ||
       d->out_row_stride < d->N || (d->out_row_stride & 7))
     return FS2_EINVAL;
-  if (d->Cin != 512 || d->N != 512 || d->KS != 5 || d->pad > d->KS - 1 || d->epilogue != FS2_EPI_BIAS_TANH)
+  if (!(d->Cin == 512 || d->Cin == 80) || d->N != 512 || d->KS != 5 || d->pad > d->KS - 1 ||
+      d->epilogue != FS2_EPI_BIAS_TANH)
     return FS2_EUNSUPPORTED;
   if (d->x == d->out) return FS2_EINVAL;  // other tiles re-read x rows (halo)
   const int64_t M64 = (int64_t)d->B * d->T;
@@ -247,7 +285,10 @@ extern "C" int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream) {
 #ifndef WCONV_WQ
 #define WCONV_WQ 1  // 8 waves x 64 columns (2 quads per wave: 224 accumulators + the ring spill; analysis only)
 #endif
-  hipLaunchKernelGGL((wconv_kernel<5, 512, WCONV_WQ>), dim3(nwg), dim3(512 / WCONV_WQ), 0, as_stream(stream), p);
+  if (d->Cin == 80)
+    hipLaunchKernelGGL((wconv_kernel<5, 80, 1>), dim3(nwg), dim3(512), 0, as_stream(stream), p);
+  else
+    hipLaunchKernelGGL((wconv_kernel<5, 512, WCONV_WQ>), dim3(nwg), dim3(512 / WCONV_WQ), 0, as_stream(stream), p);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

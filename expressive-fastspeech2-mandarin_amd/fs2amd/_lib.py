@@ -97,6 +97,8 @@ SIGNATURES = {
     "fs2_lr_expand": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p]),
     "fs2_pack_rows": (_i, [_p, _i, _p, _p, _i, _p, _p, _i64, _p]),
     "fs2_postnet_assemble": (_i, [_p, _p, _p, _i, _i, _i, _p, _p, _i, _p, _p]),
+    "fs2_seq_layout_margin": (_i, [_p, _i, _i, _i, _p, _p, _p, _p]),
+    "fs2_len_stats": (_i, [_p, _i, _p, _p, _p]),
     "fs2_seq_layout": (_i, [_p, _i, _i, _p, _p, _p, _p]),
     "fs2_vp_norm": (_i, [_p, _i64, _i, _i, _i, _p, _p, _f, _p, _i64, _p]),
     "fs2_vp_head": (_i, [_p, _i64, _i, _i, _i, _i, _p, _p, _f, _p, _p, _p, _p, _i, _p, _i, _i64, _i, _p, _f, _p, _i, _p,

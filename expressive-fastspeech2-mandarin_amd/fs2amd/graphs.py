@@ -97,9 +97,8 @@ class SynthGraphs:
             meta_host = torch.empty(meta.shape, dtype=meta.dtype, pin_memory=True)
             e1 = self._g1[key1] = SimpleNamespace(graph=graph, static=static, g=g, st=st, src_masks=src_masks,
                                                   meta=meta, meta_host=meta_host, P=P)
-        for k, v in x.items():
-            if v is not None:
-                e1.static[k].copy_(v, non_blocking=True)
+        ks = [k for k, v in x.items() if v is not None]
+        torch._foreach_copy_([e1.static[k] for k in ks], [x[k] for k in ks], non_blocking=True)  # one launch
         e1.graph.replay()
         # the one host read
         e1.meta_host.copy_(e1.meta, non_blocking=True)
@@ -121,7 +120,12 @@ class SynthGraphs:
         else:
             self._g2.move_to_end(key2)
         e2.graph.replay()
-        mel, post, mel_masks = (t.clone() for t in e2.outs)
         st = e1.st
-        return (mel, post, st.p_pred.clone(), st.e_pred.clone(), st.log_d.clone(), st.d_rounded.clone(),
-                e1.src_masks.clone(), mel_masks, src_lens.to(dev), st.mel_len.clone())
+        # fresh output tensors (the graphs' buffers are overwritten by the next call), copied in one
+        # multi-tensor launch instead of one copy each
+        srcs = [e2.outs[0], e2.outs[1], st.p_pred, st.e_pred, st.log_d, st.d_rounded, e1.src_masks, e2.outs[2],
+                st.mel_len]
+        outs = [torch.empty_like(t) for t in srcs]
+        torch._foreach_copy_(outs, srcs)
+        mel, post, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, mel_len = outs
+        return (mel, post, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens.to(dev), mel_len)

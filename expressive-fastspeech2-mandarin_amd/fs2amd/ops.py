@@ -87,7 +87,9 @@ class SeqLayout:
     the device), ``row_pos`` int32 [B*T, 2] = (frame, length) per packed row, ``rowmap`` int32
     [B*T] padded row -> packed row (-1 = padding). Built with two launches, no host sync."""
 
-    def __init__(self, lens, T):
+    def __init__(self, lens, T, margin=0):
+        """margin > 0: sequence b holds min(lens[b] + margin, T) frames, or all T when
+        lens[b] + 2 * margin > T (fs2_seq_layout_margin: the PostNet valid-region rows)."""
         _gpu(lens)
         lens = lens.to(torch.int64).contiguous()
         self.B, self.T = int(lens.shape[0]), int(T)
@@ -95,8 +97,13 @@ class SeqLayout:
         self.cu = torch.empty(self.B + 1, device=dev, dtype=torch.int32)
         self.row_pos = torch.empty(self.B * self.T, 2, device=dev, dtype=torch.int32)
         self.rowmap = torch.empty(self.B * self.T, device=dev, dtype=torch.int32)
-        L.check(_lib.fs2_seq_layout(_ptr(lens), self.B, self.T, _ptr(self.cu), _ptr(self.row_pos),
-                                    _ptr(self.rowmap), _stream(lens)), "fs2_seq_layout")
+        if margin:
+            L.check(_lib.fs2_seq_layout_margin(_ptr(lens), self.B, self.T, int(margin), _ptr(self.cu),
+                                               _ptr(self.row_pos), _ptr(self.rowmap), _stream(lens)),
+                    "fs2_seq_layout_margin")
+        else:
+            L.check(_lib.fs2_seq_layout(_ptr(lens), self.B, self.T, _ptr(self.cu), _ptr(self.row_pos),
+                                        _ptr(self.rowmap), _stream(lens)), "fs2_seq_layout")
 
     @property
     def capacity(self):
@@ -297,15 +304,19 @@ def pack_ffn_weights(w1, w2):
 
 def pack_wconv_weight(w, scale=None):
     """nn.Conv1d weight [N, Cin, KS] (optionally scaled per output channel: BatchNorm folding, in
-    f32 then rounded once like pack_conv_weight) -> the fs2_wconv buffer, flat bf16 in MFMA
-    fragment order [N/64][KS][Cin/32][4][4][16][8] (include/fs2hip.h)."""
+    f32 then rounded once like pack_conv_weight) -> the fs2_wconv buffer: K = (tap, channel)
+    flattened (k = tap * Cin + c), zero-padded to a multiple of 32, in MFMA fragment order
+    [N/64][K/32][4][4][16][8] (include/fs2hip.h; for Cin % 32 == 0 this is [N/64][KS][Cin/32]...)."""
     w = w.detach().float()
     if scale is not None:
         w = w * scale.detach().float().view(-1, 1, 1)
     N, cin, ks = w.shape
-    assert N % 64 == 0 and cin % 32 == 0, (N, cin)
-    a = w.permute(0, 2, 1).reshape(N // 64, 4, 16, ks, cin // 32, 4, 8).permute(0, 3, 4, 1, 5, 2, 6)
-    return a.reshape(-1).to(torch.bfloat16).contiguous()
+    assert N % 64 == 0 and cin % 8 == 0, (N, cin)
+    k = w.permute(0, 2, 1).reshape(N, ks * cin)
+    kp = -(-ks * cin // 32) * 32
+    if kp != ks * cin:
+        k = torch.cat([k, k.new_zeros(N, kp - ks * cin)], 1)
+    return pack_frag_rows(k)
 
 
 def wconv(x, w_packed, bias, *, ks, pad, out=None):
@@ -620,14 +631,24 @@ def pack_rows(lay, a, b=None):
     return outs[0], outs[1]
 
 
-def postnet_assemble(y, lay, len2, const_row, tail):
-    """The PostNet valid-region output back to [B, T, C] f32 (fs2_postnet_assemble)."""
-    _gpu(y, len2, const_row, tail)
+def postnet_assemble(y, lay, const_row, tail):
+    """The PostNet valid-region output back to [B, T, C] f32 (fs2_postnet_assemble; each
+    utterance's exact rows from the margin layout ``lay``)."""
+    _gpu(y, const_row, tail)
     C = y.shape[-1]
     out = torch.empty(lay.B, lay.T, C, device=y.device, dtype=torch.float32)
-    L.check(_lib.fs2_postnet_assemble(_ptr(y), _ptr(lay.rowmap), _ptr(len2), lay.B, lay.T, C, _ptr(const_row),
+    L.check(_lib.fs2_postnet_assemble(_ptr(y), _ptr(lay.rowmap), _ptr(lay.cu), lay.B, lay.T, C, _ptr(const_row),
                                       _ptr(tail), tail.shape[0], _ptr(out), _stream(y)), "fs2_postnet_assemble")
     return out
+
+
+def len_stats(lens, bad=None):
+    """int32 [max(lens), sum(lens), *bad or 0] on the device in one launch (fs2_len_stats)."""
+    _gpu(lens, bad)
+    lens = lens.to(torch.int64).contiguous()
+    meta = torch.empty(3, device=lens.device, dtype=torch.int32)
+    L.check(_lib.fs2_len_stats(_ptr(lens), lens.numel(), _ptr(bad), _ptr(meta), _stream(lens)), "fs2_len_stats")
+    return meta
 
 
 def lr_durations(dur, logpred=False, d_control=1.0):

@@ -131,7 +131,8 @@ def _postnet(pn, device, compute):
         s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
         b = (conv.bias.detach().float() - bn.running_mean.detach().float()) * s + bn.bias.detach().float()
         wfr = None
-        if compute == L.FS2_BF16 and conv.in_channels == 512 and conv.out_channels == 512 and conv.kernel_size[0] == 5:
+        if compute == L.FS2_BF16 and conv.in_channels in (512, 80) and conv.out_channels == 512 \
+                and conv.kernel_size[0] == 5:
             # the weight-streamed kernel's fragment order (fs2_wconv)
             wfr = pack_wconv_weight(conv.weight.to(device), scale=s.to(device))
         layers.append(SimpleNamespace(w=pack_conv_weight(conv.weight.to(device), compute, scale=s.to(device)),

@@ -498,13 +498,7 @@ HOST_READS = [0]  # device->host reads made by the forward path (tests assert on
 
 def meta_vector(mel_len, dev):
     """[max(mel_len), sum(mel_len), out-of-vocabulary count] as int32 on the device (one copy)."""
-    c = ops.bad_id_counter(dev)
-    if mel_len.numel():
-        parts = [mel_len.max().to(torch.int32).reshape(1), mel_len.sum().to(torch.int32).reshape(1)]
-    else:
-        parts = [torch.zeros(2, dtype=torch.int32, device=dev)]
-    parts.append(c if c is not None else torch.zeros(1, dtype=torch.int32, device=dev))
-    return torch.cat(parts)
+    return ops.len_stats(mel_len, ops.bad_id_counter(dev))
 
 
 def check_meta(meta, dev):
@@ -600,9 +594,8 @@ def _postnet(P, mel, mel_bf=None, mel_len=None):
 def _postnet_valid(P, mel, mel_bf, mel_len):
     B, T, C = mel.shape
     c, tail = _postnet_consts(P, mel_bf)
-    ml = mel_len.to(torch.int64)
-    lens2 = torch.where(ml + 2 * POSTNET_MARGIN > T, torch.full_like(ml, T), ml + POSTNET_MARGIN)
-    lay = ops.SeqLayout(lens2, T)
+    # each utterance's frames + POSTNET_MARGIN, or all T when within 2 margins of it
+    lay = ops.SeqLayout(mel_len, T, margin=POSTNET_MARGIN)
     # the f32 mel (the residual) and its bf16 copy (the first conv's input) packed in one launch
     res, y = ops.pack_rows(lay, mel.contiguous(), None if mel_bf is None else mel_bf.contiguous())
     if y is None:
@@ -616,7 +609,7 @@ def _postnet_valid(P, mel, mel_bf, mel_len):
             y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute, epilogue=L.EPI_BIAS_RES,
                            out_dtype=L.FS2_F32, residual=res, layout=lay)
     # [B, T, C]: computed rows where exact, else the constant row / the tail block
-    return ops.postnet_assemble(y, lay, lens2, c.contiguous(), tail.contiguous())
+    return ops.postnet_assemble(y, lay, c.contiguous(), tail.contiguous())
 
 
 def _add_pe(x, pe):

@@ -229,10 +229,12 @@ int64_t fs2_ffn_weight_elems(int KS, int F); /* F*KS*256 + 256*F */
  * fs2_wconv — a PostNet convolution (transformer/Layers.py:92-137: Conv1d(512, 512, k=5, pad=2) +
  * BatchNorm1d (eval: folded into w / bias on the host) + tanh) on padded [B, T] rows:
  *   y[m, n] = tanh( sum_{k<KS} sum_c x[m + k - pad, c] * w[n][c][k] + bias[n] )   (per-sequence zero taps)
- * bf16 x / out (out must not alias x), f32 accumulation and tanh. w in MFMA fragment order:
- * [N/64][KS][Cin/32][4][4][16][8], element (q, k, s, b, h, r, e) = w[64q + 16b + r][32s + 8h + e][k]
- * (fs2_wconv_weight_elems(KS, Cin, N) elements). Shapes: Cin = N = 512, KS = 5, pad <= KS - 1,
- * epilogue FS2_EPI_BIAS_TANH (FS2_EUNSUPPORTED otherwise: use fs2_conv1d).
+ * bf16 x / out (out must not alias x), f32 accumulation and tanh. w with K = (tap, channel) flattened
+ * (k = tap * Cin + c, zero-padded to a multiple of 32) in MFMA fragment order [N/64][K/32][4][4][16][8],
+ * element (q, s, b, h, r, e) = W[64q + 16b + r][32s + 8h + e], W[n][tap * Cin + c] = w[n][c][tap]
+ * (fs2_wconv_weight_elems(KS, Cin, N) elements). Shapes: N = 512, Cin = 512 (the middle convs) or 80
+ * (the first), KS = 5, pad <= KS - 1, epilogue FS2_EPI_BIAS_TANH (FS2_EUNSUPPORTED otherwise: use
+ * fs2_conv1d).
  */
 typedef struct fs2_wconv_desc {
   const void *x;            /* bf16 [B*T, >= Cin]                                                 */
@@ -394,14 +396,27 @@ const char *fs2_status_string(int status);
  *   rowmap[i] (>= 0; fs2_seq_layout's rowmap) of packed_a (packed_b); rows of a_row_bytes /
  *   b_row_bytes bytes (multiples of 16).
  * fs2_postnet_assemble — packed PostNet output back to [B, T, C] f32: out[b, t] = y_packed[rowmap[b*T+t]]
- *   where the packed rows are exact (t < len2[b] - reach, or every t when len2[b] == T), else the
+ *   where the packed rows are exact (with len2 = cu[b+1] - cu[b] of the layout (fs2_seq_layout_margin):
+ *   t < len2 - reach, or every t when len2 == T), else the
  *   row t - (T - reach) of tail [reach, C] for the last reach frames, else const_row [C] (the
  *   PostNet of all-padding input). C % 4 == 0.
  */
 int fs2_pack_rows(const void *a, int a_row_bytes, void *packed_a, const void *b, int b_row_bytes, void *packed_b,
                   const int32_t *rowmap, int64_t n_rows, fs2_stream_t stream);
-int fs2_postnet_assemble(const float *y_packed, const int32_t *rowmap, const int64_t *len2, int B, int T, int C,
+int fs2_postnet_assemble(const float *y_packed, const int32_t *rowmap, const int32_t *cu, int B, int T, int C,
                          const float *const_row, const float *tail, int reach, float *out, fs2_stream_t stream);
+
+/*
+ * fs2_seq_layout_margin — fs2_seq_layout over transformed lengths: len'[b] = T when
+ *   lens[b] + 2*margin > T, else lens[b] + margin (the PostNet valid-region rows: each utterance's
+ *   frames + margin frames of its padding), clamped to [0, T]; margin 0 = fs2_seq_layout. B <= 4096.
+ * fs2_len_stats — meta[0..2] = {max(lens), sum(lens), *bad_counter (0 if NULL)} as int32 (lengths
+ *   clamped at 0 and saturated at 2^31 - 1): the free-running path's one device->host read
+ *   (synthesize_chinese_pinyin.py:140-145 sizes the decoder from max(mel_len)) in one launch.
+ */
+int fs2_seq_layout_margin(const int64_t *lens, int B, int T, int margin, int32_t *cu, int32_t *row_pos,
+                          int32_t *rowmap, fs2_stream_t stream);
+int fs2_len_stats(const int64_t *lens, int B, const int32_t *bad_counter, int32_t *meta, fs2_stream_t stream);
 
 #ifdef __cplusplus
 }

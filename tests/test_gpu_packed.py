@@ -78,6 +78,28 @@ def test_seq_layout(gpu, case):
         assert (rp[cu[b]:cu[b] + l, 1] == l).all()
 
 
+def test_seq_layout_margin_and_len_stats(gpu):
+    """fs2_seq_layout_margin (PostNet valid-region rows: len + 10 frames, or all T within 20 of T;
+    clamped) against the plain layout of the transformed lengths, and fs2_len_stats (the free-
+    running host read's [max, sum, bad ids])."""
+    ops, _ = gpu
+    T, m = 120, 10
+    lens = [0, 1, 50, 99, 100, 101, 120, 200, -4, 79, 80, 81]
+    lens_t = torch.tensor(lens, dtype=torch.int64, device=DEV)
+    lay = ops.SeqLayout(lens_t, T, margin=m)
+    l2 = [T if l + 2 * m > T else l + m for l in lens]
+    ref = ops.SeqLayout(torch.tensor(l2, dtype=torch.int64, device=DEV), T)
+    for a, b in ((lay.cu, ref.cu), (lay.rowmap, ref.rowmap)):
+        assert torch.equal(a, b)
+    R = int(ref.cu[-1])
+    assert torch.equal(lay.row_pos[:R], ref.row_pos[:R])
+    bad = torch.tensor([3], dtype=torch.int32, device=DEV)
+    big = torch.randint(0, 5000, (777,), dtype=torch.int64)
+    for lt, bd, exp in ((lens_t, bad, [200, sum(max(l, 0) for l in lens), 3]),
+                        (big.to(DEV), None, [int(big.max()), int(big.sum()), 0])):
+        assert ops.len_stats(lt, bd).cpu().tolist() == exp
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("cin,n,ks,epi", [(256, 1024, 9, "relu"), (1024, 256, 1, "res_ln"), (256, 768, 1, "bias")])
 def test_conv_packed_equals_padded(gpu, prec, cin, n, ks, epi):

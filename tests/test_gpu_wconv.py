@@ -1,4 +1,4 @@
-"""fs2_wconv — the PostNet's 512 -> 512, k=5 Conv1d + folded BatchNorm + tanh on the
+"""fs2_wconv — the PostNet's 512 -> 512 and 80 -> 512, k=5 Conv1d + folded BatchNorm + tanh on the
 weight-streamed kernel (transformer/Layers.py:92-137).
 
 * against a float64 PyTorch statement of the same op on the same bf16 operands (per-sequence zero
@@ -24,26 +24,27 @@ def gpu():
     return ops, L
 
 
-def _case(ops, L, B, T, seed):
+def _case(ops, L, B, T, seed, cin=512):
     g = torch.Generator(device=DEV).manual_seed(seed)
-    w = torch.randn(512, 512, 5, device=DEV, generator=g) / (512 * 5) ** 0.5
+    w = torch.randn(512, cin, 5, device=DEV, generator=g) / (cin * 5) ** 0.5
     s = 1 + 0.1 * torch.randn(512, device=DEV, generator=g)  # a folded BatchNorm scale
     b = 0.1 * torch.randn(512, device=DEV, generator=g)
-    x = torch.randn(B, T, 512, device=DEV, generator=g).to(torch.bfloat16)
+    x = torch.randn(B, T, cin, device=DEV, generator=g).to(torch.bfloat16)
     return x, w, s, b
 
 
+@pytest.mark.parametrize("cin", [512, 80])  # 80: the PostNet's first conv, K = (tap, channel) flattened
 @pytest.mark.parametrize("B,T,seed", [(64, 430, 1), (3, 37, 2), (1, 1, 3), (5, 113, 4)])
-def test_wconv_matches_float64_and_conv1d(gpu, B, T, seed):
+def test_wconv_matches_float64_and_conv1d(gpu, B, T, seed, cin):
     ops, L = gpu
-    x, w, s, b = _case(ops, L, B, T, seed)
+    x, w, s, b = _case(ops, L, B, T, seed, cin)
     wq = (w * s[:, None, None]).to(torch.bfloat16)  # the operands both kernels see
     got = ops.wconv(x, ops.pack_wconv_weight(w, scale=s), b, ks=5, pad=2)
     ref = torch.tanh(torch.nn.functional.conv1d(x.double().transpose(1, 2), wq.double(), b.double(),
                                                 padding=2).transpose(1, 2))
     err = (got.double() - ref).abs()
     assert float(err.max()) <= 8e-3 and float(err.mean()) <= 1e-3, (float(err.max()), float(err.mean()))
-    two = ops.conv1d(x, ops.pack_conv_weight(w, L.FS2_BF16, scale=s), b, cin=512, ks=5, pad=2, compute=L.FS2_BF16,
+    two = ops.conv1d(x, ops.pack_conv_weight(w, L.FS2_BF16, scale=s), b, cin=cin, ks=5, pad=2, compute=L.FS2_BF16,
                      epilogue=L.EPI_BIAS_TANH, out_dtype=L.FS2_BF16)
     d = (got.float() - two.float()).abs()
     ulp = two.float().abs().clamp(min=2 ** -10) * 2 ** -7
