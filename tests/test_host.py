@@ -235,12 +235,16 @@ class _FakeForkJoin:
 
 def stub_seq_layout(monkeypatch, ops):
     """With the kernels stubbed fs2_seq_layout writes nothing: fill cu / rowmap on the host (the
-    PostNet's valid-region path indexes with the row map in torch)."""
+    PostNet's valid-region path indexes with the row map in torch); likewise the free-running host
+    read's [max, sum, bad ids] (fs2_len_stats) from torch."""
     real_layout_init = ops.SeqLayout.__init__
 
-    def layout_init(self, lens, T):
-        real_layout_init(self, lens, T)
-        ln = lens.to(torch.int64).clamp(0, T)
+    def layout_init(self, lens, T, margin=0):
+        real_layout_init(self, lens, T, margin)
+        ln = lens.to(torch.int64)
+        if margin:
+            ln = torch.where(ln + 2 * margin > T, torch.full_like(ln, T), ln + margin)
+        ln = ln.clamp(0, T)
         cu = torch.cat([ln.new_zeros(1), ln.cumsum(0)])
         t = torch.arange(T)
         rm = torch.where(t[None, :] < ln[:, None], cu[:-1, None] + t[None, :], torch.full((1,), -1))
@@ -248,6 +252,8 @@ def stub_seq_layout(monkeypatch, ops):
         self.cu.copy_(cu.to(torch.int32))
 
     monkeypatch.setattr(ops.SeqLayout, "__init__", layout_init)
+    monkeypatch.setattr(ops, "len_stats", lambda lens, bad=None: torch.stack(
+        [lens.max(), lens.sum(), torch.zeros((), dtype=lens.dtype)]).to(torch.int32))
 
 
 @pytest.mark.parametrize("packed", ["1", "0"])
@@ -280,9 +286,6 @@ def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher, streams):
             return cum, ml, dr
 
         monkeypatch.setattr(ops, "lr_durations", lr_durations)
-        # the stubbed kernel writes nothing: the one host read's [max, sum, bad ids] from torch
-        monkeypatch.setattr(ops, "len_stats", lambda lens, bad=None: torch.stack(
-            [lens.max(), lens.sum(), torch.zeros((), dtype=lens.dtype)]).to(torch.int32))
     with torch.no_grad():
         out = m(**args)
     assert len(out) == 10 and out[0].shape[-1] == 80 and out[1].shape == out[0].shape

@@ -2,7 +2,7 @@
 # Round-3 (late) evidence: full bench line (headline + extras + CPU baseline), rocprofv3 kernel
 # trace + stats of the bench, FETCH/WRITE passes of the fused FFN, SQ counters of attention and the
 # fused FFN, the free-running cfg2 trace, the graphed cfg3 train line.
-TAG=${1:-r3c}
+TAG=${1:-r3d}
 O=gpurun_out/prof_$TAG; mkdir -p gpurun_out/$TAG $O
 export TMPDIR=/tmp
 timeout -k 10 500 python bench.py > gpurun_out/$TAG/bench.log 2>&1 || exit $?
@@ -24,4 +24,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $O/free -o free --outpu
   python3 tools/free_probe.py > $O/free.log 2>&1 || exit $?
 python3 tools/fwd_gaps.py $(ls $O/free/*kernel_trace.csv | head -1) > $O/free_kernels.txt
 tail -1 $O/free.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$TAG/smoke.log 2>&1 || exit $?
+tail -2 gpurun_out/$TAG/smoke.log
 echo round profile done
