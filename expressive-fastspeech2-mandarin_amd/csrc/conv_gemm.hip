@@ -1301,6 +1301,19 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         return;
       }
     }
+    // thin GEMMs gathered through a row map (mel_linear: packed decoder rows -> padded [B, T, 80],
+    // K = 256): FS2_MEL_TILE (A/B) picks the row tile
+    static const int mel_tile = [] {
+      const char *e = getenv("FS2_MEL_TILE");
+      return e == nullptr ? 0 : atoi(e);
+    }();
+    if (GLd && mel_tile != 0 && a.a_rowmap != nullptr && ntn == 1 && a.KS == 1) {
+      if (mel_tile == 128)
+        launch_128<CT, TIn>(a, s);
+      else
+        launch<CT, 2, 4, 2, 9, TIn, 32>(a, s);  // 64 x 128
+      return;
+    }
     if (narrow && GLd && ntn == 1 && nKd >= 32 && splitk_env() && a.sk_cnt != nullptr &&
         (int64_t)((a.M + 127) / 128) >= 64)
       // one N tile and a long K (PostNet's last conv: N = 80, K = 2560): 128-row tiles and the

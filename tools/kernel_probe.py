@@ -80,6 +80,11 @@ def main():
         xe = rnd(64, 64, 256)
         fn = lambda: ops.ffn(xe, el.w12, el.b1, el.b2, ks=9, pad=4, ln=el.ln2, lens=b["src_lens"], nsplit=a.nsplit,
                               tile_rows=a.tile_rows)
+    elif a.kernel == "mel":  # mel_linear: packed decoder rows -> padded [B, T, 80] f32 + the bf16 copy
+        h = rnd(B * T, 256)
+        mel_bf = torch.empty(B, T, 80, device=dev, dtype=torch.bfloat16)
+        fn = lambda: ops.conv1d(h, P.mel_w, P.mel_b, cin=256, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
+                                out_dtype=L.FS2_F32, src_layout=lay, out2=mel_bf)
     elif a.kernel == "conv1":
         f, h = rnd(B * T, 1024), rnd(B * T, 256)
         fn = lambda: ops.conv1d(f, lp.w2, lp.b2, cin=1024, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_RES_LN,
