@@ -392,6 +392,9 @@ def main_train(args, rank, world, device):
     }
     if rank == 0:
         print(json.dumps(rec), flush=True)
+    # the graph holds the captured RCCL all-reduces: release it (device drained) before the
+    # communicator is destroyed
+    step.close()
     parallel.shutdown()
 
 

@@ -5,7 +5,8 @@ durations: the decoder length T_out = max(mel_len) is known only after the durat
 has run, so the path has one device->host read (runtime.host_meta) and cannot be ONE graph.
 :class:`SynthGraphs` captures the two halves:
 
-* stage 1 (keyed by B, L_max and the control values): token embedding + PE, the encoder, the
+* stage 1 (keyed by B, L_max and the control values; an LRU of ``max_stage1`` graphs): token
+  embedding + PE, the encoder, the
   variance adaptor and the LengthRegulator scan (duration rounding, cumulative frames, mel_len),
   plus the int32 meta vector [max(mel_len), sum(mel_len), out-of-vocabulary count];
 * the host reads the meta vector (one sync), raises IndexError on bad ids;
@@ -30,12 +31,26 @@ from . import runtime as R
 
 
 class SynthGraphs:
-    def __init__(self, model, max_stage2=8):
+    def __init__(self, model, max_stage2=8, max_stage1=4):
         self.model = model
         self.max_stage2 = max_stage2
-        self._g1 = {}
+        self.max_stage1 = max_stage1
+        self._g1 = OrderedDict()
         self._g2 = OrderedDict()
         self.captures = 0
+
+    def _drop_stage1(self, key1):
+        """Drop a stage-1 graph and every stage-2 graph captured on its outputs (key2 starts with
+        key1): those read the dropped graph's buffers."""
+        self._g1.pop(key1, None)
+        for k in [k for k in self._g2 if k[:len(key1)] == key1]:
+            del self._g2[k]
+
+    def close(self):
+        """Release every captured graph (and the memory pools they hold)."""
+        torch.cuda.synchronize()
+        self._g1.clear()
+        self._g2.clear()
 
     @staticmethod
     def _inputs(dev, speakers, emotions, arousals, valences, texts, src_lens, p_targets, e_targets):
@@ -87,9 +102,7 @@ class SynthGraphs:
         if e1 is not None and e1.P is not P:
             # the weights changed (a new pack): the graphs point at the old buffers. Drop this
             # stage-1 graph and every stage-2 graph that reads its outputs before recapturing.
-            del self._g1[key1]
-            for k in [k for k in self._g2 if k[:-1] == key1]:
-                del self._g2[k]
+            self._drop_stage1(key1)
             e1 = None
         if e1 is None:
             static = {k: (None if v is None else v.clone()) for k, v in x.items()}
@@ -97,6 +110,10 @@ class SynthGraphs:
             meta_host = torch.empty(meta.shape, dtype=meta.dtype, pin_memory=True)
             e1 = self._g1[key1] = SimpleNamespace(graph=graph, static=static, g=g, st=st, src_masks=src_masks,
                                                   meta=meta, meta_host=meta_host, P=P)
+            while len(self._g1) > self.max_stage1:
+                self._drop_stage1(next(iter(self._g1)))
+        else:
+            self._g1.move_to_end(key1)
         ks = [k for k, v in x.items() if v is not None]
         torch._foreach_copy_([e1.static[k] for k in ks], [x[k] for k in ks], non_blocking=True)  # one launch
         e1.graph.replay()
@@ -109,12 +126,15 @@ class SynthGraphs:
         # the decoder's packed launches are sized from the bucketed row count (runtime._stage2)
         key2 = key1 + (T_out, pn_valid, ops.rows_bucket(sum_len, B * T_out))
         e2 = self._g2.get(key2)
+        if e2 is not None and e2.e1 is not e1:  # captured on another (dropped) stage-1 entry's buffers
+            del self._g2[key2]
+            e2 = None
         if e2 is None:
             def body():
                 mel, post, st = R._stage2(P, e1.g, e1.st, T_out, T_out, controls[0], pn_valid, sum_len)
                 return mel, post, R._mask(st.mel_len, T_out)
             graph, outs = self._capture(body)
-            e2 = self._g2[key2] = SimpleNamespace(graph=graph, outs=outs)
+            e2 = self._g2[key2] = SimpleNamespace(graph=graph, outs=outs, e1=e1)
             while len(self._g2) > self.max_stage2:
                 self._g2.popitem(last=False)
         else:

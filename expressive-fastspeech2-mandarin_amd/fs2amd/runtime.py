@@ -468,6 +468,12 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
                            f"regulated length {T_out} (the reference fails here too: Models.py:157)")
     # free-running batches padded to one long utterance: the PostNet's valid-region form
     pn_valid = d_targets is None and T_out == max_len and postnet_valid_rows(B, T_out, sum_len)
+    if pn_valid:
+        # the valid-region PostNet's constant row / tail block (cached per weight pack) made on the
+        # caller's stream before the groups' streams are released again: no group reads them
+        # before they are written
+        _postnet_consts(P, _mel_copy_on(P))
+        fj.fork()
     T_dec = min(T_out, P.max_seq_len) if model.training else T_out
     if T_dec != T_out:
         mel_masks = mel_masks[:, :T_dec]
@@ -524,11 +530,15 @@ def postnet_valid_rows(B, T, sum_len):
     return postnet_valid_region_on() and B > 0 and sum_len + POSTNET_MARGIN * B < 0.5 * B * T
 
 
+def _mel_copy_on(P):
+    return P.compute == L.FS2_BF16 and os.environ.get("FS2_MEL_BF16", "1") != "0"
+
+
 def _mel_copy(P, x, bt):
     """bf16 copy of mel_linear's output, written by the same epilogue (fs2_conv_desc.out2): PostNet's
     first conv then reads bf16 through LDS-DMA instead of converting f32 in registers. The bf16
     GEMM rounds its f32 input to bf16 the same way, so the conv's operands are unchanged."""
-    if P.compute != L.FS2_BF16 or os.environ.get("FS2_MEL_BF16", "1") == "0":
+    if not _mel_copy_on(P):
         return None
     return torch.empty(*bt, P.mel_w.shape[0], device=x.device, dtype=torch.bfloat16)
 
@@ -546,7 +556,7 @@ def postnet_valid_region_on():
     return os.environ.get("FS2_POSTNET_VALID", "1") != "0"
 
 
-def _postnet_consts(P, mel_bf_like):
+def _postnet_consts(P, bf16_input):
     """The PostNet output wherever its input is all padding: every padded mel frame is mel_linear's
     bias (the decoder output there is masked to 0), so away from the valid frames the output is
     one constant row c, and its last POSTNET_REACH frames before T (zero padding beyond T) are one
@@ -554,10 +564,10 @@ def _postnet_consts(P, mel_bf_like):
     (row 20 and rows 30..39), cached per weight pack; computed outside any graph capture."""
     ent = getattr(P, "_postnet_consts", None)
     if ent is None:
-        if mel_bf_like is not None and mel_bf_like.is_cuda and torch.cuda.is_current_stream_capturing():
+        if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("PostNet constants must be computed before graph capture (run the forward once)")
         b = P.mel_b.float().reshape(1, 1, -1).expand(1, 2 * POSTNET_MARGIN, -1).contiguous()
-        y = _postnet(P, b, b.to(torch.bfloat16) if mel_bf_like is not None else None)
+        y = _postnet(P, b, b.to(torch.bfloat16) if bf16_input else None)
         ent = (y[0, POSTNET_MARGIN].clone(), y[0, 2 * POSTNET_MARGIN - POSTNET_REACH:].clone())
         P._postnet_consts = ent
     return ent
@@ -593,7 +603,7 @@ def _postnet(P, mel, mel_bf=None, mel_len=None):
 
 def _postnet_valid(P, mel, mel_bf, mel_len):
     B, T, C = mel.shape
-    c, tail = _postnet_consts(P, mel_bf)
+    c, tail = _postnet_consts(P, mel_bf is not None)
     # each utterance's frames + POSTNET_MARGIN, or all T when within 2 margins of it
     lay = ops.SeqLayout(mel_len, T, margin=POSTNET_MARGIN)
     # the f32 mel (the residual) and its bf16 copy (the first conv's input) packed in one launch

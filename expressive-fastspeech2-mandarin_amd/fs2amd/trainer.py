@@ -74,6 +74,8 @@ class TrainStep:
         self.step_no = current_step + 1
         self._flat = None
         self._stream = None
+        self._closed = False
+        self._acc_pending = 0
         if self.flat:
             self._setup_flat_grads()
         if self.graph_mode:
@@ -82,14 +84,51 @@ class TrainStep:
     def __call__(self, batch):
         """One step on this rank's shard (a dict of forward kwargs + mels / targets on the device).
         Returns the 6 loss tensors (train.py:85-86)."""
+        if self._closed:
+            raise RuntimeError("TrainStep: step after close()")
         if self.graph_mode and self.grad_acc_step == 1:
             return self._graphed(batch)
         if self.flat:
+            if self.grad_acc_step > 1:
+                return self._flat_accumulate(batch)
             self.optimizer._update_learning_rate()
             losses = [l.detach() for l in self._step_body(batch)]
             self.step_no += 1
             return losses
         return self._eager(batch)
+
+    def close(self):
+        """Release the captured step graph (it holds RCCL all-reduces on the process group's
+        communicator), its static inputs / outputs and the DDP reducer, after the device has
+        drained. Call before ``dist.destroy_process_group()``: tearing the communicator down
+        while a graph that captured collectives on it is alive aborts the process (round-3
+        GPU suite). Idempotent; the model keeps its parameters (gradients are detached from the
+        flat buffer)."""
+        if self._closed:
+            return
+        if self.device is not None and self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        if self._graph is not None:
+            g = self._graph[1]
+            self._graph = None
+            g.reset()
+        if self._flat is not None:
+            for p in self.model.parameters():
+                p.grad = None
+            self._flat = None
+            self._buckets = []
+        self.net = self.model
+        self._stream = None
+        self._closed = True
+        if self.device is not None and self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
     def _eager(self, batch):
         output = self.net(**batch)
@@ -129,6 +168,26 @@ class TrainStep:
             flat = torch.cat([b.reshape(-1) for b in self._bn_buffers])
             dist.broadcast(flat, 0)
             torch._foreach_copy_(self._bn_buffers, list(flat.split([b.numel() for b in self._bn_buffers])))
+
+    def _flat_accumulate(self, batch):
+        """grad_acc_step > 1 on the flat buffer (train.py:89-97): the loss is divided by
+        grad_acc_step and its gradient accumulated; every grad_acc_step-th call reduces, clips,
+        takes the Noam lr step and zeroes the buffer (eager launches: a replayed graph would
+        re-zero the buffer each call)."""
+        if self._acc_pending == 0:
+            self._flat.zero_()
+            self._sync_buffers()
+        output = self.net(**batch)
+        losses = self.loss(loss_inputs(batch), output)
+        (losses[0] / self.grad_acc_step).backward()
+        self._acc_pending += 1
+        if self.step_no % self.grad_acc_step == 0:
+            self._reduce_grads()
+            nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip_thresh)
+            self.optimizer.step_and_update_lr()
+            self._acc_pending = 0
+        self.step_no += 1
+        return [l.detach() for l in losses]
 
     def _step_body(self, batch):
         """zero grads, forward, loss, backward, all-reduce, clip, Adam: the captured step."""

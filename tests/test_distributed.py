@@ -166,3 +166,42 @@ def test_bench_launcher_starts_n_ranks():
     assert rec["n_gpus"] == 2
     assert rec["config"]["frames_total"] == 1000 + 2000  # SUM over both ranks
     assert rec["ms_per_step"] >= 20.0 - 1e-6  # MAX over ranks (rank 1 sleeps 20 ms)
+
+
+def test_flat_grads_accumulation_matches_eager(monkeypatch):
+    """grad_acc_step = 2 on the flat-gradient path (the one graph=True / flat_grads=True take) has
+    train.py:89-97's semantics: loss / grad_acc_step accumulated over two batches, one clip + Noam
+    step every second call. Same parameters as the eager step after 4 calls (2 optimizer steps);
+    close() detaches the gradients and refuses further steps."""
+    import copy
+
+    from _common import configs
+    from _stubs import install_training_stubs
+    from fs2amd.model import FastSpeech2
+    from fs2amd.synth_weights import fill_module
+    from fs2amd.trainer import TrainStep
+
+    install_training_stubs(monkeypatch.setattr)
+    pc, mc, tc = configs()
+    tc = copy.deepcopy(tc)
+    tc["optimizer"]["grad_acc_step"] = 2
+    sds = []
+    for flat in (False, True):
+        torch.manual_seed(0)
+        m = FastSpeech2(pc, mc)
+        fill_module(m, seed=0)
+        m.train_dropout = False
+        st = TrainStep(m, pc, mc, tc, device=None, flat_grads=flat)
+        assert st.flat == flat
+        for i in range(4):
+            b = synth_batch(3, 6, 10, seed=20 + i, with_mels=True, pe_targets=True)
+            st(b)
+        assert st.optimizer.current_step == 2
+        sds.append({k: v.detach().clone() for k, v in m.state_dict().items()})
+        st.close()
+        if flat:
+            assert all(p.grad is None for p in m.parameters())
+            with pytest.raises(RuntimeError):
+                st(b)
+    for k in sds[0]:
+        torch.testing.assert_close(sds[1][k], sds[0][k], rtol=1e-6, atol=1e-8, msg=k)

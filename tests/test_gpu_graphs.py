@@ -110,3 +110,48 @@ def test_bad_ids_raise(model):
         # the counter was reset: a clean batch runs
         out = synth(**b)
     assert np.isfinite(out[1].float().cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_weight_change_recaptures_both_stages(model, prec):
+    """A parameter changed in place between two calls (a training step, a checkpoint load) builds a
+    new weight pack: the stage-1 graph AND the stage-2 graphs captured on its outputs must be
+    dropped and recaptured (a replayed stale stage-2 graph would read the old pack and the freed
+    stage-1 buffers). Both calls must equal the eager forward on the weights of the time."""
+    from fs2amd.graphs import SynthGraphs
+
+    model.set_precision(prec)
+    args, _, _, _ = load_case("cfg2_free")
+    b = _dev(args)
+    synth = SynthGraphs(model)
+    w = model.decoder.layer_stack[0].pos_ffn.w_1.weight
+    saved = w.detach().clone()
+    try:
+        with torch.no_grad():
+            _same(synth(**b), model(**b))
+            n = synth.captures
+            w.mul_(1.25)  # decoder-only change: T_out and the stage-2 key stay the same
+            _same(synth(**b), model(**b))
+            assert synth.captures == n + 2, (synth.captures, n)
+    finally:
+        with torch.no_grad():
+            w.copy_(saved)
+    synth.close()
+
+
+def test_stage1_lru_bound(model):
+    """Stage-1 graphs are an LRU too (a serving loop with many batch shapes / controls must not grow
+    GPU memory without bound); evicting one drops the stage-2 graphs that read its outputs."""
+    from fs2amd.graphs import SynthGraphs
+
+    model.set_precision("bf16")
+    args, _, _, _ = load_case("cfg2_free")
+    b = _dev(args)
+    synth = SynthGraphs(model, max_stage1=2)
+    with torch.no_grad():
+        for d in (1.0, 1.1, 1.2):
+            _same(synth(**b, d_control=d), model(**b, d_control=d))
+    assert len(synth._g1) == 2
+    keys1 = list(synth._g1)
+    assert all(any(k[:len(k1)] == k1 for k1 in keys1) for k in synth._g2)
+    synth.close()

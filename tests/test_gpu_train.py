@@ -177,60 +177,46 @@ def test_graphed_train_step_equals_eager(gpu):
             kept.append(st(to_device(b, DEV))[0])
         torch.cuda.synchronize()
         runs.append(([float(l) for l in kept], {k: p.detach().clone() for k, p in m.named_parameters()}, st))
-    (le, pe, _), (lg, pg, stg) = runs
+    (le, pe, ste), (lg, pg, stg) = runs
     assert stg._graph is not None, "the graph was never captured"
+    ste.close()
+    stg.close()
+    assert stg._graph is None
     np.testing.assert_allclose(lg, le, rtol=1e-5)
     _assert_params_close(pg, pe, _lr_sum(tc, 8))
 
 
-def test_ddp_step_over_rccl_equals_plain(gpu):
+def test_ddp_step_over_rccl_equals_plain(gpu, tmp_path):
     """The data-parallel training path (train.py:52-53 DataParallel -> one process per GPU, DDP over
     RCCL): a single-rank "nccl" process group wraps TrainStep in DistributedDataParallel, so every
-    step runs DDP's gradient buckets through RCCL all-reduce on the MI355X. With one rank the
-    average is the identity: losses and parameters equal the un-wrapped step (fp32, dropout off)."""
-    import os
-    import socket
+    step runs DDP's gradient buckets through RCCL all-reduce on the MI355X; a third run captures the
+    flat-gradient all-reduce (4 MB slices) inside the step's HIP graph. With one rank the average is
+    the identity: losses and parameters equal the un-wrapped step (fp32, dropout off).
 
-    import torch.distributed as dist
+    The runs happen in a child process (tests/rccl_train_child.py) that owns the process group's
+    whole lifecycle, closes every TrainStep (graph with captured collectives reset) before
+    destroy_process_group, and must exit 0 after printing TEARDOWN_OK."""
+    import json
+    import os
+    import subprocess
+    import sys
 
     from fs2amd import config as C
-    from fs2amd.data import synth_batch, to_device
-    from fs2amd.model import FastSpeech2
-    from fs2amd.trainer import TrainStep
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    torch.cuda.set_device(0)
-    dist.init_process_group("nccl", init_method="env://", rank=0, world_size=1)
-    try:
-        assert dist.get_backend() == "nccl"
-        t = torch.ones(1024, device=DEV)
-        dist.all_reduce(t)
-        assert float(t.sum()) == 1024.0
-        pc, mc, _ = configs()
-        tc = C.ESD_TRAIN_CONFIG
-        runs = []
-        # plain eager; DDP (eager, RCCL bucket all-reduces); graph + explicit RCCL all-reduce of the
-        # flat gradient buffer in 4 MB slices captured inside the step's HIP graph
-        for ddp, graph in ((False, False), (True, False), (True, True)):
-            m = FastSpeech2(pc, mc)
-            m.load_state_dict(oracle_state_dict())
-            m = m.to(DEV).set_precision("fp32")
-            m.train_dropout = False
-            st = TrainStep(m, pc, mc, tc, device=torch.device(DEV), ddp=ddp, bucket_mb=4, graph=graph, warmup=2)
-            assert isinstance(st.net, torch.nn.parallel.DistributedDataParallel) == (ddp and not graph)
-            base = synth_batch(4, 8, 20, seed=41, with_mels=True, pe_targets=True)
-            losses = [float(st(to_device(dict(base, mels=base["mels"] * (1 + 0.1 * i)), DEV))[0]) for i in range(5)]
-            torch.cuda.synchronize()
-            if graph:
-                assert st._graph is not None and st.reduce and len(st._buckets) > 1
-            runs.append((losses, {k: p.detach().clone() for k, p in m.named_parameters()}))
-        lp, pp = runs[0]
-        for ld, pd in runs[1:]:
-            np.testing.assert_allclose(ld, lp, rtol=1e-5)
-            _assert_params_close(pd, pp, _lr_sum(tc, 5))
-    finally:
-        dist.destroy_process_group()
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rccl_train_child.py")
+    r = subprocess.run([sys.executable, "-u", child, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    tail = (r.stdout[-3000:] + "\n--- stderr ---\n" + r.stderr[-3000:])
+    assert r.returncode == 0, tail
+    assert "TEARDOWN_OK" in r.stdout, tail
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["backend"] == "nccl" and res["allreduce_sum"] == 1024.0
+    runs = res["runs"]
+    for run in runs:
+        assert run["is_ddp"] == (run["ddp"] and not run["graph"]), run
+    assert runs[2]["captured"] and runs[2]["reduce"] and runs[2]["nbuckets"] > 1, runs[2]
+    tc = C.ESD_TRAIN_CONFIG
+    pp = torch.load(os.path.join(tmp_path, "params_0.pt"), weights_only=True)
+    for i in (1, 2):
+        np.testing.assert_allclose(runs[i]["losses"], runs[0]["losses"], rtol=1e-5)
+        pd = torch.load(os.path.join(tmp_path, f"params_{i}.pt"), weights_only=True)
+        _assert_params_close(pd, pp, _lr_sum(tc, 5))
