@@ -235,6 +235,7 @@ def decoder_op_table(model, batch_cpu, device, reps):
       qkv    fused Q|K|V projection   F*256*2 in + F*768*2 out + W bytes    HBM
       attn   SDPA, 2 heads of 128     sum_b 4*len_b^2*128*2 FLOP          MFMA
       lr     LengthRegulator gather + decoder PE   B*L*256*2 + B*L*8 in + F*256*2 out  HBM
+      lr_fused  the forward's one-launch LR (scan + layout + gather + PE)  lr + cum + layout  HBM
     (F = valid frames; random bf16 inputs of the forward's shapes). bf16 only (the fp8 / fp32 lines
     report the conv-k9 roofline alone). Back-to-back calls of one op keep the matrix pipe busier than
     the forward does, so the MFMA-heavy conv9 reads ~10 % slower here than inside real forwards."""
@@ -276,6 +277,11 @@ def decoder_op_table(model, batch_cpu, device, reps):
                  "mfma", float(sum(4.0 * int(n) ** 2 * 128 * 2 for n in lens))),
         "lr": (lambda: ops.lr_expand(x, cum, ml, T, pe=P.dec_pe, out_dtype=P.act_dtype, out_layout=lay),
                "hbm", B * Lp * 256 * 2.0 + B * Lp * 8.0 + F * 256 * 2.0),
+        # the forward's LengthRegulator launch (fs2_lr_fused): duration scan + packed layout + gather
+        # + PE; algorithmic bytes as "lr" plus the layout it writes (cu, rowmap, row_pos)
+        "lr_fused": (lambda: ops.lr_fused(x, b["mel_lens"], T, pe=P.dec_pe, out_dtype=P.act_dtype,
+                                          dur=b["d_targets"]),
+                     "hbm", B * Lp * 256 * 2.0 + B * Lp * 8.0 * 2 + F * 256 * 2.0 + B * T * 4.0 + F * 8.0 + B * 8.0),
     }
     out = {}
     for name, (fn, bound, work) in ops_.items():

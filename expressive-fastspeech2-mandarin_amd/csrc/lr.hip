@@ -191,6 +191,166 @@ void launch_expand(const void *x, const int32_t *cum, const int64_t *mel_len, in
   launch_expand_v<TX, TO, 32, true>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
 }
 
+// The whole LengthRegulator stage in ONE launch (round 4): each workgroup (32 frames of one
+// utterance) (1) re-derives the utterance's cumulative frame counts in LDS -- from the durations
+// (scan) or from a cum row computed before the free-running host read --, (2) the decoder's packed
+// layout offset cu[b] = sum_{j<b} clamp(lens[j], 0, T) by a block reduction over the B lengths
+// (B <= 4096: at most 16 loads per thread), (3) its frames' rowmap / row_pos entries and (4) the
+// gather (+ PE) into the packed rows. The utterance's first workgroup also stores cum, mel_len,
+// d_rounded and cu[b] (cu[B] by the last utterance). Replaces lr_durations + seq_layout +
+// lr_expand (three dependent launches; cfg2 ~25 us with the gaps).
+struct LrFusedArgs {
+  const void *x;
+  const void *dur;
+  int dur_kind;
+  float d_control;
+  const int32_t *cum_in;
+  const int64_t *mel_len_in;
+  const int64_t *lens;  // layout lengths (the decoder's mel lengths)
+  int B, L, D, T;
+  const float *pe;
+  void *out;
+  int32_t *cum;
+  int64_t *mel_len;
+  float *d_rounded;
+  int32_t *cu;
+  int2 *row_pos;
+  int32_t *rowmap;
+};
+
+template <typename TX, typename TO, bool HAS_PE>
+__global__ __launch_bounds__(256) void lr_fused_kernel(LrFusedArgs a) {
+  constexpr int ROWS = 32, UNR = ROWS / 8;
+  const int b = blockIdx.y, t0 = blockIdx.x * ROWS;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int L = a.L, T = a.T, D = a.D;
+  __shared__ int32_t scum[kLdsCum];
+  __shared__ int src[ROWS];
+  __shared__ int64_t wtot[4];
+  __shared__ int32_t wcu[4];
+  __shared__ int64_t s_ml;
+  const bool first = blockIdx.x == 0;
+
+  // (2) cumulative frames of utterance b
+  if (a.dur != nullptr) {
+    const int per = (L + 255) / 256;
+    const int i0 = min(tid * per, L), i1 = min(i0 + per, L);
+    const int64_t base = (int64_t)b * L;
+    int64_t local = 0;
+    for (int i = i0; i < i1; ++i) local += frames_of(a.dur, a.dur_kind, a.d_control, base + i, nullptr);
+    int64_t incl = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wtot[wv] = incl;
+    __syncthreads();
+    int64_t run = incl - local;
+    for (int w = 0; w < wv; ++w) run += wtot[w];
+    for (int i = i0; i < i1; ++i) {
+      run += frames_of(a.dur, a.dur_kind, a.d_control, base + i, first ? a.d_rounded : nullptr);
+      const int32_t c = (int32_t)(run < 0x7fffffff ? run : 0x7fffffff);
+      scum[i] = c;
+      if (first) a.cum[base + i] = c;
+    }
+    if (tid == 0) {
+      const int64_t total = (wtot[0] + wtot[1]) + (wtot[2] + wtot[3]);
+      s_ml = total;
+      if (first) a.mel_len[b] = total;
+    }
+  } else {
+    const int32_t *c = a.cum_in + (int64_t)b * L;
+    for (int i = tid; i < L; i += 256) scum[i] = c[i];
+    if (tid == 0) s_ml = a.mel_len_in[b];
+  }
+
+  // (1) packed offset of utterance b and its clamped length
+  auto clen = [&](int j) {
+    const int64_t l = a.lens[j];
+    return (int32_t)(l < 0 ? 0 : (l > T ? T : l));
+  };
+  int32_t part = 0;
+  for (int j = tid; j < b; j += 256) part += clen(j);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  if (lane == 0) wcu[wv] = part;
+  __syncthreads();
+  const int32_t cu_b = (wcu[0] + wcu[1]) + (wcu[2] + wcu[3]);
+  const int32_t len_b = clen(b);
+  if (first && tid == 0) {
+    a.cu[b] = cu_b;
+    if (b == a.B - 1) a.cu[a.B] = cu_b + len_b;
+  }
+
+  // (3) source phoneme of each frame; the layout entries of this workgroup's frames
+  const int64_t ml = s_ml;
+  const int lim = (int)(ml < (int64_t)T ? ml : (int64_t)T);
+  if (tid < ROWS) {
+    const int t = t0 + tid;
+    int sidx = -1;
+    if (t < lim) {
+      int lo = 0, hi = L - 1;  // first i with cum[i] > t (exists because t < mel_len)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (scum[mid] > t) hi = mid; else lo = mid + 1;
+      }
+      sidx = lo;
+    }
+    src[tid] = sidx;
+    if (t < T) {
+      if (a.rowmap != nullptr) a.rowmap[(int64_t)b * T + t] = t < len_b ? cu_b + t : -1;
+      if (a.row_pos != nullptr && t < len_b) a.row_pos[cu_b + t] = make_int2(t, len_b);
+    }
+  }
+  __syncthreads();
+
+  // (4) gather (+ PE) of the frames t < len_b into packed rows cu_b + t
+  const int rows = min(ROWS, min(T, (int)len_b) - t0);
+  if (rows <= 0) return;
+  const int vpr = D >> 3, total = rows * vpr;
+  const TX *xb = reinterpret_cast<const TX *>(a.x) + (int64_t)b * L * D;
+  TO *ob = reinterpret_cast<TO *>(a.out) + ((int64_t)cu_b + t0) * D;
+  for (int base = tid; base < total; base += 256 * UNR) {
+    float v[UNR][8];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int e = base + u * 256;
+      const int r = e / vpr;
+      const int col = (e - r * vpr) << 3;
+      const int sidx = e < total ? src[r] : -1;
+      if (sidx >= 0) {
+        load8(xb + (int64_t)sidx * D + col, v[u]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[u][q] = 0.0f;
+      }
+      if constexpr (HAS_PE) {
+        if (e < total) {
+          float pv[8];
+          load8(a.pe + (int64_t)(t0 + r) * D + col, pv);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[u][q] += pv[q];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int e = base + u * 256;
+      if (e < total) {
+        if constexpr (sizeof(TO) == 2) {
+          bf16x8 o;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] = (bf16)v[u][q];
+          __builtin_nontemporal_store(o, reinterpret_cast<bf16x8 *>(ob + (int64_t)e * 8));
+        } else {
+          store8(ob + (int64_t)e * 8, v[u]);
+        }
+      }
+    }
+  }
+}
+
 // get_mask_from_lengths (utils/tools.py:152-160): mask[b, t] = t >= lens[b]  (True = padding)
 __global__ __launch_bounds__(256) void length_mask_kernel(const int64_t *__restrict__ lens, int width, int64_t n,
                                                           bool *__restrict__ mask) {
@@ -405,6 +565,73 @@ extern "C" int fs2_length_regulate(const void *x, int x_dtype, const void *dur, 
 extern "C" int fs2_len_stats(const int64_t *lens, int B, const int32_t *bad_counter, int32_t *meta, fs2_stream_t stream) {
   if (lens == nullptr || meta == nullptr || B < 0) return FS2_EINVAL;
   hipLaunchKernelGGL(len_stats_kernel, dim3(1), dim3(256), 0, as_stream(stream), lens, B, bad_counter, meta);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_lr_fused(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control,
+                            const int32_t *cum_in, const int64_t *mel_len_in, int B, int L, int D, int T_out,
+                            const float *pe, const int64_t *layout_lens, int32_t *cu, int32_t *row_pos,
+                            int32_t *rowmap, void *out, int out_dtype, int32_t *cum, int64_t *mel_len,
+                            float *d_rounded, fs2_stream_t stream) {
+  if (x == nullptr || out == nullptr || layout_lens == nullptr || cu == nullptr) return FS2_EINVAL;
+  if (B < 0 || L <= 0 || D <= 0 || (D & 7) != 0 || T_out < 0 || B > kSeqMaxB || L > kLdsCum) return FS2_EINVAL;
+  if ((int64_t)B * T_out > 0x7fffff00LL) return FS2_EINVAL;
+  if (dur != nullptr) {  // scan mode: durations in, cum / mel_len out
+    if (cum == nullptr || mel_len == nullptr || dur_kind < FS2_DUR_I64 || dur_kind > FS2_DUR_LOGPRED) return FS2_EINVAL;
+    if (dur_kind == FS2_DUR_LOGPRED && d_rounded == nullptr) return FS2_EINVAL;
+  } else if (cum_in == nullptr || mel_len_in == nullptr) {
+    return FS2_EINVAL;
+  }
+  if (B == 0) return FS2_OK;
+  if (T_out == 0) {
+    // nothing to gather, but the scan outputs and cu are still due: one frame block of work
+    if (dur != nullptr) {
+      int rc = fs2_lr_durations(dur, dur_kind, d_control, B, L, cum, mel_len, d_rounded, stream);
+      if (rc != FS2_OK) return rc;
+    }
+    return fs2_seq_layout(layout_lens, B, 0, cu, row_pos, rowmap, stream);
+  }
+  LrFusedArgs a{};
+  a.x = x;
+  a.dur = dur;
+  a.dur_kind = dur_kind;
+  a.d_control = d_control;
+  a.cum_in = cum_in;
+  a.mel_len_in = mel_len_in;
+  a.lens = layout_lens;
+  a.B = B;
+  a.L = L;
+  a.D = D;
+  a.T = T_out;
+  a.pe = pe;
+  a.out = out;
+  a.cum = cum;
+  a.mel_len = mel_len;
+  a.d_rounded = d_rounded;
+  a.cu = cu;
+  a.row_pos = reinterpret_cast<int2 *>(row_pos);
+  a.rowmap = rowmap;
+  const dim3 grid((unsigned)((T_out + 31) / 32), (unsigned)B);
+  hipStream_t s = as_stream(stream);
+  auto go = [&](auto TXv, auto TOv) {
+    using TX = decltype(TXv);
+    using TO = decltype(TOv);
+    if (pe != nullptr)
+      hipLaunchKernelGGL((lr_fused_kernel<TX, TO, true>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((lr_fused_kernel<TX, TO, false>), grid, dim3(256), 0, s, a);
+  };
+  if (x_dtype == FS2_BF16 && out_dtype == FS2_BF16)
+    go(bf16{}, bf16{});
+  else if (x_dtype == FS2_F32 && out_dtype == FS2_F32)
+    go(0.0f, 0.0f);
+  else if (x_dtype == FS2_F32 && out_dtype == FS2_BF16)
+    go(0.0f, bf16{});
+  else if (x_dtype == FS2_BF16 && out_dtype == FS2_F32)
+    go(bf16{}, 0.0f);
+  else
+    return FS2_EUNSUPPORTED;
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

@@ -77,6 +77,17 @@ class FfnDesc(ctypes.Structure):
     ]
 
 
+class VpFusedDesc(ctypes.Structure):
+    """Mirror of ``fs2_vp_fused_desc`` (include/fs2hip.h)."""
+
+    _fields_ = [
+        ("x", _p), ("x_row_stride", _i64), ("w", _p), ("vec", _p), ("lin_b", _p), ("ln_eps", _f),
+        ("B", _i), ("L", _i), ("G", _i), ("lens", _p), ("pred", _p), ("embed_group", _i),
+        ("x_out", _p), ("x_out_row_stride", _i64), ("target", _p), ("control", _f), ("bins", _p),
+        ("n_bins", _i), ("table", _p),
+    ]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "fs2_version": (ctypes.c_char_p, []),
@@ -103,6 +114,9 @@ SIGNATURES = {
     "fs2_vp_norm": (_i, [_p, _i64, _i, _i, _i, _p, _p, _f, _p, _i64, _p]),
     "fs2_vp_head": (_i, [_p, _i64, _i, _i, _i, _i, _p, _p, _f, _p, _p, _p, _p, _i, _p, _i, _i64, _i, _p, _f, _p, _i, _p,
                          _p]),
+    "fs2_vp_fused": (_i, [ctypes.POINTER(VpFusedDesc), _p]),
+    "fs2_vp_fused_weight_elems": (ctypes.c_int64, [_i]),
+    "fs2_lr_fused": (_i, [_p, _i, _p, _i, _f, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "fs2_length_masks": (_i, [_p, _i, _i, _p, _p]),
     "fs2_length_regulate": (_i, [_p, _i, _p, _i, _f, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p, _p, _p]),
 }

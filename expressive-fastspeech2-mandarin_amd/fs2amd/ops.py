@@ -105,6 +105,17 @@ class SeqLayout:
             L.check(_lib.fs2_seq_layout(_ptr(lens), self.B, self.T, _ptr(self.cu), _ptr(self.row_pos),
                                         _ptr(self.rowmap), _stream(lens)), "fs2_seq_layout")
 
+    @classmethod
+    def deferred(cls, B, T, device):
+        """Allocated, not computed: a launch that builds the layout itself fills cu / row_pos /
+        rowmap (fs2_lr_fused)."""
+        lay = cls.__new__(cls)
+        lay.B, lay.T = int(B), int(T)
+        lay.cu = torch.empty(lay.B + 1, device=device, dtype=torch.int32)
+        lay.row_pos = torch.empty(lay.B * lay.T, 2, device=device, dtype=torch.int32)
+        lay.rowmap = torch.empty(lay.B * lay.T, device=device, dtype=torch.int32)
+        return lay
+
     @property
     def capacity(self):
         return self.B * self.T
@@ -594,6 +605,58 @@ def vp_head(y, gamma, beta, eps, lin_w, lin_b, lens, embed=None):
     return pred
 
 
+def pack_vp_fused(convs):
+    """The fs2_vp_fused weight buffer of G VariancePredictors: ``convs`` = [(conv1.weight,
+    conv2.weight), ...] (nn.Conv1d [256, 256, 3] each). Per predictor and conv, K = (tap, channel)
+    flattened, split into bf16 parts w = w_hi + w_lo, each in pack_frag_rows order; a wave's stream
+    [2 convs][24 k-steps][hi, lo] is contiguous (include/fs2hip.h)."""
+    out = []
+    for pair in convs:
+        per_conv = []
+        for w in pair:
+            w = w.detach().float()
+            N, cin, ks = w.shape
+            k = w.permute(0, 2, 1).reshape(N, ks * cin)
+            hi = k.to(torch.bfloat16).float()
+            lo = (k - hi).to(torch.bfloat16).float()
+            parts = [pack_frag_rows(t).view(N // 64, ks * cin // 32, 2048) for t in (hi, lo)]
+            per_conv.append(torch.stack(parts, 2))  # [N/64][K/32][2][2048]
+        out.append(torch.stack(per_conv, 1).reshape(-1))  # [N/64][2 convs][K/32][2][2048]
+    return torch.cat(out).contiguous()
+
+
+def vp_fused(x, F, lens, embed=None):
+    """fs2_vp_fused: F.G VariancePredictors (bf16x3) on bf16 rows x [B, L, 256] in one launch ->
+    pred f32 [G, B, L]; embed = (g, target, control, bins, table): group g also writes
+    x_out = x + table[bucketize(...)] (a new tensor; returned as the second value, else None)."""
+    _gpu(x, F.w, F.vec, F.lin_b, lens)
+    if x.dtype != torch.bfloat16 or x.shape[-1] != 256:
+        raise TypeError("fs2amd.vp_fused: bf16 [B, L, 256] input only")
+    B, Lx, _ = x.shape
+    assert lens.dtype == torch.int64 and lens.numel() == B
+    assert F.w.numel() == _lib.fs2_vp_fused_weight_elems(F.G)
+    pred = torch.empty(F.G, B, Lx, device=x.device, dtype=torch.float32)
+    d = L.VpFusedDesc()
+    d.x, d.x_row_stride = x.data_ptr(), _rows(x, "x")
+    d.w, d.vec, d.lin_b, d.ln_eps = F.w.data_ptr(), F.vec.data_ptr(), F.lin_b.data_ptr(), float(F.eps)
+    d.B, d.L, d.G = B, Lx, F.G
+    d.lens, d.pred, d.embed_group = lens.data_ptr(), pred.data_ptr(), -1
+    x_out = None
+    if embed is not None:
+        g, target, control, bins, table = embed
+        _gpu(target, bins, table)
+        assert table.shape[1] == 256 and table.dtype == torch.float32 and bins.dtype == torch.float32
+        if target is not None:
+            assert target.dtype == torch.float32 and target.is_contiguous() and target.numel() == B * Lx
+        x_out = torch.empty_like(x)
+        d.embed_group = int(g)
+        d.x_out, d.x_out_row_stride = x_out.data_ptr(), 256
+        d.target, d.control = (target.data_ptr() if target is not None else None), float(control)
+        d.bins, d.n_bins, d.table = bins.data_ptr(), bins.numel() + 1, table.data_ptr()
+    L.check(_lib.fs2_vp_fused(ctypes.byref(d), _stream(x)), "fs2_vp_fused")
+    return pred, x_out
+
+
 def length_mask(lens, width):
     """get_mask_from_lengths (utils/tools.py:152-160) in one launch: bool [B, width], True = pad."""
     _gpu(lens)
@@ -686,6 +749,35 @@ def lr_expand(x, cum, mel_len, T_out, pe=None, out_dtype=None, index_map=False, 
                                _ptr(im), _ptr(out_layout.cu) if out_layout is not None else None, _stream(x)),
             "fs2_lr_expand")
     return (out, im) if index_map else out
+
+
+def lr_fused(x, lens, T_out, pe=None, out_dtype=None, dur=None, logpred=False, d_control=1.0, cum=None, mel_len=None):
+    """fs2_lr_fused: LengthRegulator gather (+ PE) into the packed decoder rows of the layout of
+    ``lens`` over T_out, the layout built by the same launch. Durations scanned here (``dur``:
+    returns (out, layout, cum, mel_len, d_rounded)) or from fs2_lr_durations (``cum``, ``mel_len``:
+    returns (out, layout))."""
+    _gpu(x, lens, pe, dur, cum, mel_len)
+    x = x.contiguous()
+    B, Lx, D = x.shape
+    dev = x.device
+    od = _dt(x) if out_dtype is None else out_dtype
+    lens = lens.to(torch.int64).contiguous()
+    lay = SeqLayout.deferred(B, T_out, dev)
+    out = lay.empty(D, torch_dtype(od))
+    if dur is not None:
+        dur = dur.contiguous()
+        cum = torch.empty(B, Lx, device=dev, dtype=torch.int32)
+        mel_len = torch.empty(B, device=dev, dtype=torch.int64)
+        d_rounded = torch.empty(B, Lx, device=dev, dtype=torch.float32) if logpred else None
+        L.check(_lib.fs2_lr_fused(_ptr(x), _dt(x), _ptr(dur), _dur_kind(dur, logpred), float(d_control), None, None,
+                                  B, Lx, D, int(T_out), _ptr(pe), _ptr(lens), _ptr(lay.cu), _ptr(lay.row_pos),
+                                  _ptr(lay.rowmap), _ptr(out), od, _ptr(cum), _ptr(mel_len), _ptr(d_rounded),
+                                  _stream(x)), "fs2_lr_fused")
+        return out, lay, cum, mel_len, d_rounded
+    L.check(_lib.fs2_lr_fused(_ptr(x), _dt(x), None, 0, 1.0, _ptr(cum), _ptr(mel_len), B, Lx, D, int(T_out), _ptr(pe),
+                              _ptr(lens), _ptr(lay.cu), _ptr(lay.row_pos), _ptr(lay.rowmap), _ptr(out), od, None,
+                              None, None, _stream(x)), "fs2_lr_fused")
+    return out, lay
 
 
 def length_regulate(x, duration, max_len=None, return_index_map=False):

@@ -21,7 +21,7 @@ import torch
 
 from . import _lib as L
 from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split, pack_ffn_weights, pack_frag_rows, \
-    pack_wconv_weight
+    pack_vp_fused, pack_wconv_weight
 
 
 def _f32(t, device):
@@ -124,6 +124,25 @@ def _vp_columns(vps, device):
     )
 
 
+def _vp_fused(vps, device):
+    """fs2_vp_fused form of G VariancePredictors that read the same input (bf16x3): the conv
+    weights as hi / lo parts in fragment order, the seven 256-vectors per predictor."""
+    cls = [vp.conv_layer for vp in vps]
+    convs = [(cl.conv1d_1.conv, cl.conv1d_2.conv) for cl in cls]
+    ok = all(c.in_channels == 256 and c.out_channels == 256 and c.kernel_size[0] == 3 and c.padding[0] == 1
+             for pair in convs for c in pair)
+    eps = {cl.layer_norm_1.eps for cl in cls} | {cl.layer_norm_2.eps for cl in cls}
+    if not ok or len(eps) != 1:
+        return None
+    vec = torch.stack([torch.stack([_f32(t, device).reshape(-1) for t in (
+        cl.conv1d_1.conv.bias, cl.layer_norm_1.weight, cl.layer_norm_1.bias, cl.conv1d_2.conv.bias,
+        cl.layer_norm_2.weight, cl.layer_norm_2.bias, vp.linear_layer.weight)]) for cl, vp in zip(cls, vps)])
+    return SimpleNamespace(
+        G=len(vps), eps=eps.pop(), vec=vec.contiguous(),
+        w=pack_vp_fused([(c1.weight.to(device), c2.weight.to(device)) for c1, c2 in convs]),
+        lin_b=torch.cat([_f32(vp.linear_layer.bias, device).reshape(-1) for vp in vps]).contiguous())
+
+
 def _postnet(pn, device, compute):
     layers = []
     for seq in pn.convolutions:
@@ -160,11 +179,16 @@ def pack_model(model, device, precision, vp_precision="fp32", fp8_scales=None):
     P.vp = {k: _vp(getattr(va, f"{k}_predictor"), device, vpc, vsplit) for k in ("duration", "pitch", "energy")}
     # bf16x3 VariancePredictors in their column-split form (duration + pitch side by side, energy)
     P.vpcols = None
+    P.vpfused = None
     if vsplit:
         dp = _vp_columns([va.duration_predictor, va.pitch_predictor], device)
         en = _vp_columns([va.energy_predictor], device)
         if dp is not None and en is not None:
             P.vpcols = SimpleNamespace(dp=dp, energy=en)
+        # ... and as whole fused predictors (fs2_vp_fused: one launch per set)
+        fdp = _vp_fused([va.duration_predictor, va.pitch_predictor], device)
+        fen = _vp_fused([va.energy_predictor], device)
+        P.vpfused = SimpleNamespace(dp=fdp, energy=fen) if fdp is not None and fen is not None else None
     P.bins = {k: _f32(getattr(va, f"{k}_bins"), device) for k in ("pitch", "energy")}
     P.var_table = {k: _f32(getattr(va, f"{k}_embedding").weight, device) for k in ("pitch", "energy")}
     P.mel_w = pack_conv_weight(model.mel_linear.weight.to(device), big)

@@ -225,6 +225,11 @@ def variance_predictor(vp, x, lens):
                       epilogue=L.EPI_RELU_LN_DOT, ln=vp.ln2, lens=lens, dot=(vp.lin_w, vp.lin_b))
 
 
+def vp_fused_on():
+    """FS2_VP_FUSED=0: the column-split launches (round-2 form) instead of fs2_vp_fused (A/B)."""
+    return os.environ.get("FS2_VP_FUSED", "1") != "0"
+
+
 def vp_columns_on():
     """FS2_VP_COLUMNS=0: the bf16x3 predictors as LayerNorm-epilogue GEMMs (round-1 form, A/B)."""
     return os.environ.get("FS2_VP_COLUMNS", "1") != "0"
@@ -318,8 +323,10 @@ class _ForkJoin:
                     t.record_stream(self.main)
 
 
-def _stage1(P, va, g, p_control, d_control):
-    """Encoder (+ conditioning), variance predictors, duration scan for one utterance group."""
+def _stage1(P, va, g, p_control, d_control, defer_lr=False):
+    """Encoder (+ conditioning), variance predictors, duration scan for one utterance group.
+    defer_lr (teacher-forced durations, decoder length known): the duration scan is left to the
+    one-launch LengthRegulator of stage 2 (fs2_lr_fused)."""
     x = ops.embed_pe(g.texts, P.enc_emb, _pe(P, "enc", g.Lx), P.act_dtype)
     spk_vec = emo_vec = None
     if P.spk_table is not None or P.emo_table is not None:
@@ -336,7 +343,19 @@ def _stage1(P, va, g, p_control, d_control):
     st = SimpleNamespace(x=x, p_pred=None, e_pred=None)
     st.phoneme_p = va.pitch_feature_level == "phoneme_level"
     st.phoneme_e = va.energy_feature_level == "phoneme_level"
-    if P.vpcols is not None and st.phoneme_p and st.phoneme_e and vp_columns_on():
+    if getattr(P, "vpfused", None) is not None and st.phoneme_p and st.phoneme_e and x.dtype == torch.bfloat16 \
+            and vp_fused_on():
+        # duration + pitch as ONE launch (each a whole predictor per 32-row tile; the pitch group
+        # writes x + pitch embedding to a new buffer), then energy on it (modules.py:110-126)
+        V = P.vpfused
+        dp, x = ops.vp_fused(x, V.dp, g.lens_src, embed=(1, g.p_targets, p_control, P.bins["pitch"],
+                                                           P.var_table["pitch"]))
+        st.log_d, st.p_pred = dp[0], dp[1]
+        en, x = ops.vp_fused(x, V.energy, g.lens_src, embed=(0, g.e_targets, p_control, P.bins["energy"],
+                                                             P.var_table["energy"]))  # p_control: :124-125
+        st.e_pred = en[0]
+        st.x = x
+    elif P.vpcols is not None and st.phoneme_p and st.phoneme_e and vp_columns_on():
         # duration + pitch in one set of launches (both read x; the pitch embedding is added to x
         # by the head), then energy on x + pitch embedding (modules.py:110-126)
         V = P.vpcols
@@ -352,8 +371,12 @@ def _stage1(P, va, g, p_control, d_control):
     if st.phoneme_e and st.e_pred is None:
         st.e_pred = _variance(P, "energy", x, g.lens_src, g.e_targets, p_control)  # p_control: modules.py:124-125
     if g.d_targets is not None:
-        st.cum, st.mel_len, _ = ops.lr_durations(_dur_input(g.d_targets))
         st.d_rounded = None
+        if defer_lr:
+            st.cum = st.mel_len = None
+            st.dur_pending = _dur_input(g.d_targets)
+        else:
+            st.cum, st.mel_len, _ = ops.lr_durations(_dur_input(g.d_targets))
     else:
         st.cum, st.mel_len, st.d_rounded = ops.lr_durations(st.log_d, logpred=True, d_control=d_control)
     return st
@@ -361,6 +384,21 @@ def _stage1(P, va, g, p_control, d_control):
 
 def _dur_input(d):
     return d if d.dtype in (torch.int64, torch.float32) else d.to(torch.int64)
+
+
+def _ensure_lr(st):
+    """The duration scan of a deferred stage 1, where stage 2 does not take fs2_lr_fused."""
+    if st.cum is None:
+        st.cum, st.mel_len, _ = ops.lr_durations(st.dur_pending)
+
+
+def lr_fused_on():
+    """FS2_LR_FUSED=0: the LengthRegulator as lr_durations + seq_layout + lr_expand (A/B)."""
+    return os.environ.get("FS2_LR_FUSED", "1") != "0"
+
+
+def lr_fused_ok(x):
+    return lr_fused_on() and x.shape[1] <= 2048 and x.shape[0] <= 4096
 
 
 def _stage2(P, g, st, T_out, T_dec, p_control, postnet_valid=False, rows_hint=None):
@@ -371,12 +409,22 @@ def _stage2(P, g, st, T_out, T_dec, p_control, postnet_valid=False, rows_hint=No
     if not frame_level and T_dec == T_out and packed_decoder_ok(P):
         # packed decoder: only the dec_lens frames of each utterance are computed
         # (cfg2: 24.9k of 27.5k rows, cfg4: 135k of 249k); mel_linear scatters back to [B, T, n_mel]
-        lay = ops.SeqLayout(dec_lens, T_dec)
+        if lr_fused_ok(x):
+            # scan (teacher-forced) + packed layout + gather (+ PE) in one launch
+            if st.cum is None:
+                x, lay, st.cum, st.mel_len, _ = ops.lr_fused(x, dec_lens, T_out, pe=_pe(P, "dec", T_out),
+                                                             out_dtype=P.act_dtype, dur=st.dur_pending)
+            else:
+                x, lay = ops.lr_fused(x, dec_lens, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype,
+                                      cum=st.cum, mel_len=st.mel_len)
+        else:
+            _ensure_lr(st)
+            lay = ops.SeqLayout(dec_lens, T_dec)
+            x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype,
+                              out_layout=lay)
         # active rows when known on the host (free-running), rounded up (ops.rows_bucket) so that
         # a captured stage-2 graph serves every batch of the bucket
         lay.rows_hint = None if rows_hint is None else ops.rows_bucket(rows_hint, lay.capacity)
-        x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype,
-                          out_layout=lay)
         x = _stack(P, P.dec_layers, x, None, layout=lay, timed=True)
         mel_bf = _mel_copy(P, x, (lay.B, lay.T))
         mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
@@ -384,6 +432,7 @@ def _stage2(P, g, st, T_out, T_dec, p_control, postnet_valid=False, rows_hint=No
         return mel, _postnet(P, mel, mel_bf, dec_lens if postnet_valid else None), st
     # LR gather with the decoder's position encoding fused (frame-level variance needs the bare
     # expanded x first, so the PE add moves to a second pass in that configuration)
+    _ensure_lr(st)
     if frame_level:
         x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=None, out_dtype=P.act_dtype)
         if not st.phoneme_p:
@@ -443,9 +492,12 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     fj = _ForkJoin(dev, n)
     fj.fork()
     sts = []
+    # teacher-forced with the decoder length given: the duration scan joins the LengthRegulator's
+    # one launch in stage 2
+    defer = d_targets is not None and bool(max_mel_len)
     for i, g in enumerate(groups):
         with fj.ctx(i):
-            sts.append(_stage1(P, va, g, p_control, d_control))
+            sts.append(_stage1(P, va, g, p_control, d_control, defer_lr=defer))
 
     mel_len = sts[0].mel_len if n == 1 else None
     if not max_mel_len or d_targets is None:

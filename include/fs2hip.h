@@ -339,6 +339,45 @@ int fs2_vp_head(const float *y, int64_t y_row_stride, int B, int T, int G, int C
                 fs2_stream_t stream);
 
 /*
+ * fs2_vp_fused — G (1 or 2) whole VariancePredictors on the same bf16 input in ONE launch
+ * (model/modules.py:197-250; VarianceAdaptor.forward :110-126), split-precision bf16x3 like the
+ * column-split form above (w = w_hi + w_lo; conv1 x.w_hi + x.w_lo, h = h_hi + h_lo as bf16 planes,
+ * conv2 h_hi.w_hi + h_hi.w_lo + h_lo.w_hi; f32 accumulation, LayerNorm, dot):
+ *   h = LN1(relu(conv1_k3(x) + b1)); y = LN2(relu(conv2_k3(h) + b2))      (padding = 1 per utterance)
+ *   pred[g*B*L + m] = (t >= lens[b]) ? 0 : dot(y[m], lin_w[g]) + lin_b[g]  (m = b*L + t)
+ *   g == embed_group: v = target ? target[m] : (pred *= control);
+ *                     x_out[m, :256] = bf16(x[m, :256] + table[bucketize(v, bins)])   (x_out != x)
+ * Replaces conv1 + fs2_vp_norm + conv2 + fs2_vp_head (4 launches, 4 HBM intermediates) per set.
+ * Channels 256 (filter_size = d_model), kernel 3. w: fs2_vp_fused_weight_elems(G) bf16 elements,
+ * per predictor [4 quads][2 convs][24 k-steps][2 parts (hi, lo)][4][4][16][8]: element (q, c, s,
+ * e, b, h, r, i) = part_e(W_c)[64q + 16b + r][32s + 8h + i] with W_c[n][tap*256 + ch] =
+ * conv_c.weight[n][ch][tap]. vec: f32 [G][7][256] = conv1 bias, LN1 gamma, LN1 beta, conv2 bias,
+ * LN2 gamma, LN2 beta, linear weight.
+ */
+typedef struct fs2_vp_fused_desc {
+  const void *x;            /* bf16 [B*L, >= 256]                                                  */
+  int64_t x_row_stride;
+  const void *w;            /* bf16, fragment order (see above)                                    */
+  const float *vec;         /* f32 [G][7][256]                                                     */
+  const float *lin_b;       /* f32 [G]                                                             */
+  float ln_eps;
+  int B, L, G;
+  const int64_t *lens;      /* [B] phoneme lengths (masked_fill)                                   */
+  float *pred;              /* f32 [G, B*L]                                                        */
+  int embed_group;          /* -1: none                                                            */
+  void *x_out;              /* bf16 [B*L, >= 256]                                                  */
+  int64_t x_out_row_stride;
+  const float *target;      /* f32 [B*L] or NULL                                                   */
+  float control;
+  const float *bins;        /* f32 [n_bins - 1]                                                    */
+  int n_bins;
+  const float *table;       /* f32 [n_bins, 256]                                                   */
+} fs2_vp_fused_desc;
+
+int fs2_vp_fused(const fs2_vp_fused_desc *d, fs2_stream_t stream);
+int64_t fs2_vp_fused_weight_elems(int G);
+
+/*
  * LengthRegulator (model/modules.py:161-194 + utils/tools.py:360-378), split in two launches
  * so a caller without max_mel_len can read max(mel_len) in between (one D2H read per batch,
  * where the reference does B*L_max .item() syncs).
@@ -363,6 +402,21 @@ int fs2_lr_durations(const void *dur, int dur_kind, float d_control, int B, int 
 int fs2_lr_expand(const void *x, int x_dtype, const int32_t *cum, const int64_t *mel_len, int B, int L, int D,
                   int T_out, const float *pe, void *out, int out_dtype, int32_t *index_map, const int32_t *out_cu,
                   fs2_stream_t stream);
+
+/*
+ * fs2_lr_fused — the LengthRegulator + pad (model/modules.py:161-194, utils/tools.py:360-378) AND
+ * the decoder's packed layout (fs2_seq_layout of layout_lens over T_out) in ONE launch, the
+ * frames written packed: out[cu[b] + t, :] = x[b, src(b,t), :] (+ pe[t, :]) for t < clamp(
+ * layout_lens[b], 0, T_out) (zeros for t >= mel_len[b]); cu / row_pos / rowmap as fs2_seq_layout.
+ * Durations either scanned here (dur != NULL, dur_kind / d_control as fs2_lr_durations; cum,
+ * mel_len and, for FS2_DUR_LOGPRED, d_rounded are written) or taken from an earlier
+ * fs2_lr_durations (dur == NULL: cum_in, mel_len_in; the free-running path, whose host read of
+ * max(mel_len) sits between the two). L <= 2048, B <= 4096, D % 8 == 0.
+ */
+int fs2_lr_fused(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control, const int32_t *cum_in,
+                 const int64_t *mel_len_in, int B, int L, int D, int T_out, const float *pe,
+                 const int64_t *layout_lens, int32_t *cu, int32_t *row_pos, int32_t *rowmap, void *out,
+                 int out_dtype, int32_t *cum, int64_t *mel_len, float *d_rounded, fs2_stream_t stream);
 
 /* Convenience: both launches with a caller-known T_out (the teacher-forced / max_mel_len path). */
 int fs2_length_regulate(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control, int B, int L,

@@ -467,6 +467,59 @@ def test_vp_columns_match_f32_and_embed(B, L):
     assert torch.equal(p3[1], dp[1]) and torch.equal(x3, embedded(tgt))
 
 
+@pytest.mark.parametrize("B,L", [(64, 64), (3, 45), (5, 17), (2, 1), (7, 160), (1, 33)])
+def test_vp_fused_matches_f32_and_columns(B, L):
+    """fs2_vp_fused (one launch per predictor set: conv1 + LN1 + conv2 + LN2 + Linear + mask, bf16x3,
+    32-row tiles with the conv halo recomputed; ragged utterance / tile boundaries: L = 45, 17, 1,
+    160, 33) vs each predictor on exact-f32 MFMA within |d| <= 2e-4 + 2e-4 |y| (the column-split
+    form's bound), padded positions exactly 0. The embedding group's x_out = x + table[bucketize(v)]
+    is exact against torch on the kernel's own predictions: v = pred * control (pred scaled) or the
+    target (pred kept); x itself is not modified."""
+    from fs2amd import ops
+    from fs2amd.runtime import variance_predictor, variance_predictors
+    from fs2amd.model import FastSpeech2
+    from fs2amd.synth_weights import fill_module
+    from _common import configs
+
+    pc, mc, _ = configs()
+    m = FastSpeech2(pc, mc)
+    fill_module(m, seed=0)
+    m = m.to("cuda").eval()
+    P32 = m.set_precision("bf16", "fp32").packed("cuda")
+    P3 = m.set_precision("bf16", "bf16x3").packed("cuda")
+    assert P3.vpfused is not None
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(B, L, 256, generator=g).to("cuda", torch.bfloat16)
+    lens = torch.randint(1, L + 1, (B,), generator=g).to("cuda")
+    x0 = x.clone()
+    dp, none = ops.vp_fused(x, P3.vpfused.dp, lens)
+    en, _ = ops.vp_fused(x, P3.vpfused.energy, lens)
+    assert none is None and dp.shape == (2, B, L) and en.shape == (1, B, L)
+    pad = torch.arange(L, device="cuda")[None, :] >= lens[:, None]
+    cols = variance_predictors(P3.vpcols.dp, x, lens)
+    for got, k in ((dp[0], "duration"), (dp[1], "pitch"), (en[0], "energy")):
+        ref = variance_predictor(P32.vp[k], x, lens)
+        err = (ref - got).abs()
+        assert bool((err <= 2e-4 + 2e-4 * ref.abs()).all()), (k, float(err.max()))
+        assert bool((got[pad] == 0).all())
+    assert float((cols - dp).abs().max()) <= 4e-4 * max(1.0, float(cols.abs().max()))
+    bins, table = P3.bins["pitch"], P3.var_table["pitch"]
+
+    def embedded(v):
+        return (x.float() + table[torch.bucketize(v, bins)]).to(torch.bfloat16)
+
+    p2, x2 = ops.vp_fused(x, P3.vpfused.dp, lens, embed=(1, None, 1.3, bins, table))
+    assert torch.equal(p2[0], dp[0]) and torch.equal(p2[1], dp[1] * 1.3)
+    assert torch.equal(x2, embedded(p2[1])) and torch.equal(x, x0)
+    tgt = torch.randn(B, L, generator=g).to("cuda")
+    p3, x3 = ops.vp_fused(x, P3.vpfused.dp, lens, embed=(1, tgt, 1.0, bins, table))
+    assert torch.equal(p3[1], dp[1]) and torch.equal(x3, embedded(tgt))
+    e4, x4 = ops.vp_fused(x, P3.vpfused.energy, lens, embed=(0, None, 0.8, P3.bins["energy"], P3.var_table["energy"]))
+    assert torch.equal(e4[0], en[0] * 0.8)
+    assert torch.equal(x4, (x.float() + P3.var_table["energy"][torch.bucketize(e4[0], P3.bins["energy"])]).to(
+        torch.bfloat16))
+
+
 @pytest.mark.parametrize("compute", [0, 1])
 @pytest.mark.parametrize("B,T,packed,shape", [
     (1, 8576, False, None),    # 67 x 8 tiles: one full round + a 24-tile tail (256 CUs)

@@ -252,3 +252,53 @@ torch.save(outs, sys.argv[1])
                     assert torch.equal(x, y), (prec, other, i, float((x.float() - y.float()).abs().max()))
                 else:
                     assert torch.equal(x, y), (prec, other, i)
+
+
+@pytest.mark.parametrize("mode", ["i64", "f32", "logpred", "cum"])
+def test_lr_fused_equals_three_launches(gpu, mode):
+    """fs2_lr_fused (one launch: duration scan or a given cum row, packed layout, gather + PE) is
+    bit-identical to fs2_lr_durations + fs2_seq_layout + fs2_lr_expand(out_layout): frames, cum,
+    mel_len, d_rounded (logpred: ties and d_control), cu / rowmap / row_pos. Layout lengths differ
+    from mel_len (longer, shorter, cut at T, zero, negative), an all-zero-duration utterance, L = 70
+    phonemes (scan chunks of 1), and the cfg4 stress shape's L = 160."""
+    ops, L = gpu
+    g = torch.Generator(device=DEV).manual_seed(21)
+    for B, Lx in ((7, 70), (3, 160), (1, 1)):
+        D = 256
+        if mode == "logpred":
+            d = torch.randn(B, Lx, device=DEV, generator=g) * 1.0 + 1.2
+            d[0, :3] = torch.log(torch.tensor([1.5, 2.5, 0.5], device=DEV) + 1)[: min(3, Lx)]
+        elif mode == "f32":
+            d = torch.rand(B, Lx, device=DEV, generator=g) * 9 - 1
+        else:
+            d = torch.randint(-1, 9, (B, Lx), device=DEV, generator=g)
+        if B > 1:
+            d[1] = 0
+        x = torch.randn(B, Lx, D, device=DEV, generator=g).to(torch.bfloat16)
+        dc = 1.3 if mode == "logpred" else 1.0
+        cum, mel_len, dr = ops.lr_durations(d, logpred=mode == "logpred", d_control=dc)
+        T = max(int(mel_len.max()) + 3, 1)
+        dec = mel_len.clone()
+        dec[0] += 2
+        if B > 2:
+            dec[2] = -5
+        if B > 3:
+            dec[3] = T + 7
+        if B > 4:
+            dec[4] = max(int(dec[4]) - 4, 0)
+        pe = torch.randn(T, D, device=DEV, generator=g)
+        lay = ops.SeqLayout(dec, T)
+        ref = ops.lr_expand(x, cum, mel_len, T, pe=pe, out_dtype=L.FS2_BF16, out_layout=lay)
+        if mode == "cum":
+            got, lay2 = ops.lr_fused(x, dec, T, pe=pe, out_dtype=L.FS2_BF16, cum=cum, mel_len=mel_len)
+        else:
+            got, lay2, cum2, ml2, dr2 = ops.lr_fused(x, dec, T, pe=pe, out_dtype=L.FS2_BF16, dur=d,
+                                                    logpred=mode == "logpred", d_control=dc)
+            assert torch.equal(cum2, cum) and torch.equal(ml2, mel_len)
+            assert (dr2 is None) == (dr is None) and (dr is None or torch.equal(dr2, dr))
+        torch.cuda.synchronize()
+        assert torch.equal(lay2.cu, lay.cu)
+        assert torch.equal(lay2.rowmap, lay.rowmap)
+        R = int(lay.cu[-1])
+        assert torch.equal(lay2.row_pos[:R], lay.row_pos[:R])
+        assert torch.equal(got[:R], ref[:R]), (B, Lx, mode)

@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
     lib = _lib.load()
     declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
-    assert len(declared) == len(_lib.SIGNATURES) == 24
+    assert len(declared) == len(_lib.SIGNATURES) == 27
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
@@ -58,7 +58,8 @@ int main(void){ P(x) P(x_row_stride) P(w) P(B) P(compute) P(residual) P(res_row_
             assert getattr(_lib.ConvDesc, name).offset == int(off), name
 
 
-@pytest.mark.parametrize("cname,pyname", [("fs2_ffn_desc", "FfnDesc"), ("fs2_wconv_desc", "WconvDesc")])
+@pytest.mark.parametrize("cname,pyname", [("fs2_ffn_desc", "FfnDesc"), ("fs2_wconv_desc", "WconvDesc"),
+                                          ("fs2_vp_fused_desc", "VpFusedDesc")])
 def test_ffn_desc_layout_matches_header(cname, pyname):
     """ctypes mirrors of fs2_ffn_desc / fs2_wconv_desc have the C layout (every field's offset, and
     the size)."""
@@ -132,6 +133,17 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     assert lib.fs2_vp_head(None, 512, 1, 1, 2, 256, None, None, 1e-5, None, None, None, None, -1, None, 0, 256, 256,
                            None, 1.0, None, 256, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_seq_layout(None, 1, 1, None, None, None, None) == _lib.FS2_EINVAL
+    vd = _lib.VpFusedDesc()
+    assert lib.fs2_vp_fused(ctypes.byref(vd), None) == _lib.FS2_EINVAL
+    for k in ("x", "w", "vec", "lin_b", "lens", "pred"):
+        setattr(vd, k, 256)
+    vd.x, vd.B, vd.L, vd.G, vd.x_row_stride, vd.embed_group = 512, 2, 8, 3, 256, -1
+    assert lib.fs2_vp_fused(ctypes.byref(vd), None) == _lib.FS2_EINVAL  # G = 3
+    vd.G, vd.embed_group = 2, 1
+    assert lib.fs2_vp_fused(ctypes.byref(vd), None) == _lib.FS2_EINVAL  # embedding without x_out / bins / table
+    vd.x_out, vd.bins, vd.table, vd.n_bins, vd.x_out_row_stride = vd.x, 256, 256, 256, 256
+    assert lib.fs2_vp_fused(ctypes.byref(vd), None) == _lib.FS2_EINVAL  # x_out aliasing x
+    assert lib.fs2_vp_fused_weight_elems(2) == 2 * 4 * 2 * 24 * 2 * 2048
 
 
 def _model():
@@ -238,9 +250,9 @@ def stub_seq_layout(monkeypatch, ops):
     PostNet's valid-region path indexes with the row map in torch); likewise the free-running host
     read's [max, sum, bad ids] (fs2_len_stats) from torch."""
     real_layout_init = ops.SeqLayout.__init__
+    real_lr_fused = ops.lr_fused
 
-    def layout_init(self, lens, T, margin=0):
-        real_layout_init(self, lens, T, margin)
+    def fill(self, lens, T, margin=0):
         ln = lens.to(torch.int64)
         if margin:
             ln = torch.where(ln + 2 * margin > T, torch.full_like(ln, T), ln + margin)
@@ -251,7 +263,17 @@ def stub_seq_layout(monkeypatch, ops):
         self.rowmap.copy_(rm.reshape(-1).to(torch.int32))
         self.cu.copy_(cu.to(torch.int32))
 
+    def layout_init(self, lens, T, margin=0):
+        real_layout_init(self, lens, T, margin)
+        fill(self, lens, T, margin)
+
+    def lr_fused(x, lens, T_out, **kw):  # the one-launch LR builds its layout on the device
+        r = real_lr_fused(x, lens, T_out, **kw)
+        fill(r[1], lens, T_out)
+        return r
+
     monkeypatch.setattr(ops.SeqLayout, "__init__", layout_init)
+    monkeypatch.setattr(ops, "lr_fused", lr_fused)
     monkeypatch.setattr(ops, "len_stats", lambda lens, bad=None: torch.stack(
         [lens.max(), lens.sum(), torch.zeros((), dtype=lens.dtype)]).to(torch.int32))
 
@@ -296,7 +318,9 @@ def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher, streams):
     # are not mostly padding: the padded PostNet form)
     assert n_conv == k * (10 * 4 + 6 + 1 + 5), rec.calls
     assert rec.calls.count("fs2_attention") == k * 10
-    assert ("fs2_seq_layout" in rec.calls) == (packed == "1")
+    # the packed decoder's layout: built by the one-launch LengthRegulator (fs2_lr_fused)
+    assert ("fs2_lr_fused" in rec.calls) == (packed == "1")
+    assert ("fs2_lr_expand" in rec.calls) == (packed == "0")
 
 
 def test_training_step_dry_run(monkeypatch):
