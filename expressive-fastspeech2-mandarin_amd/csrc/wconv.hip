@@ -36,7 +36,21 @@ struct WconvArgs {
   int64_t os;
   int B, T, M, pad;
   uint32_t x_bytes, w_bytes;
+  const int2 *row_pos;     // packed rows: {frame, length} per row (NULL: padded [B, T] rows)
+  const int32_t *rows_dev; // packed rows: the active row count (device)
 };
+
+// position and length of row m's sequence: packed rows from row_pos, padded rows t = m mod T
+__device__ __forceinline__ void seq_pos(const int2 *row_pos, int m, int T, int &tpos, int &tlen) {
+  if (row_pos != nullptr) {
+    const int2 q = row_pos[m];
+    tpos = q.x;
+    tlen = q.y;
+  } else {
+    tpos = m % T;
+    tlen = T;
+  }
+}
 
 template <int N, typename Fn, int... I>
 __device__ __forceinline__ void static_for_impl(Fn &&f, std::integer_sequence<int, I...>) {
@@ -77,17 +91,18 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int M = p.M, T = p.T, pad = p.pad;
+  const int M = p.rows_dev != nullptr ? min(*p.rows_dev, p.M) : p.M, T = p.T, pad = p.pad;
   const int m0 = blockIdx.x * BM;
   if (m0 >= M) return;
   const int hrow0 = lane & 15, hi = lane >> 4;
 
-  // tap validity (padded rows: position t mod T in a sequence of T frames)
+  // tap validity (padded rows: position t mod T in a sequence of T frames; packed: row_pos)
   int vmask[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + mb * 16 + hrow0;
-    const int tpos = m < M ? m % T : 0, tlen = m < M ? T : 0;
+    int tpos = 0, tlen = 0;
+    if (m < M) seq_pos(p.row_pos, m, T, tpos, tlen);
     int v = 0;
 #pragma unroll
     for (int tap = 0; tap < KS; ++tap) v |= ((unsigned)(tpos + tap - pad) < (unsigned)tlen ? 1 : 0) << tap;
@@ -250,6 +265,427 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
   }
 }
 
+
+// The PostNet's first two convolutions in ONE launch (transformer/Layers.py:92-137, layers 0 and 1):
+//   y1 = tanh(conv_k5(mel; w1) + b1)   80 -> 512      (K = (tap, channel) flattened: 13 units)
+//   y2 = tanh(conv_k5(y1; w2) + b2)    512 -> 512
+// A workgroup owns BM = 112 rows of y2; it computes y1 on the 116 rows its taps read (m0-2 ..
+// m0+113; the 4 halo rows recomputed, 3.6 %) from a 120-row mel tile, keeps y1 in LDS as the
+// second conv's x tile (bf16, the wconv pitch) and runs wconv's main loop on it. The 28 MB y1
+// write + re-read and the second launch's x-tile prologue (116 KB per workgroup from HBM) are gone.
+struct PnHeadArgs {
+  const bf16 *x;  // mel (bf16) [M, >= 80]
+  int64_t xs;
+  const bf16 *w1, *w2;
+  const float *b1, *b2;
+  bf16 *out;
+  int64_t os;
+  int T, M, pad;
+  uint32_t x_bytes, w1_bytes, w2_bytes;
+  const int2 *row_pos;
+  const int32_t *rows_dev;
+};
+
+__global__ __launch_bounds__(512, 1) void pn_head_kernel(PnHeadArgs p) {
+  constexpr int KS = 5, CIN1 = 80, NCOL = 512, MB = 7, BM = 112, NWV = 8, NT = 512, JB = 4, DEPTH = 4;
+  constexpr int YR = BM + KS - 1;            // y1 rows: m0 - 2 .. m0 + 113
+  constexpr int XR = BM + 2 * (KS - 1);      // mel rows: m0 - 4 .. m0 + 115
+  constexpr int YPITCH = NCOL * 2 + 32;      // 1056: conflict-free fragment reads for any tap
+  constexpr int XPITCH = CIN1 * 2 + 16;      // 176
+  constexpr int OPITCH = NCOL * 2 + 16;      // output staging
+  constexpr int XPIECES = (XR * XPITCH + 1023) / 1024;
+  constexpr int XPW = (XPIECES + NWV - 1) / NWV;
+  constexpr int NU1 = (KS * CIN1 + 31) / 32;  // 13 flat units
+  constexpr int NKS = NCOL / 32;              // 16 k-steps per tap (conv2)
+  constexpr int NU2 = KS * NKS;               // 80
+  constexpr int ZBYTES = NKS * 64;            // masked conv2 rows read base 0 + 64 ks (+16 hi)
+  constexpr int Y_OFF = ZBYTES;
+  constexpr int YREG = YR * YPITCH > BM * OPITCH ? YR * YPITCH : BM * OPITCH;
+  constexpr int X_OFF = Y_OFF + YREG;
+  constexpr int B1_OFF = X_OFF + NWV * XPW * 1024;
+  constexpr int B2_OFF = B1_OFF + NCOL * 4;
+  constexpr int SMEM = B2_OFF + NCOL * 4;
+  static_assert(SMEM <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = p.rows_dev != nullptr ? min(*p.rows_dev, p.M) : p.M, T = p.T, pad = p.pad;
+  const int m0 = blockIdx.x * BM;
+  if (m0 >= M) return;
+  const int hrow0 = lane & 15, hi = lane >> 4;
+  auto taps = [&](int gm) {  // bit tap: row gm's tap stays inside its sequence
+    int v = 0;
+    if (gm >= 0 && gm < M) {
+      int tpos, tlen;
+      seq_pos(p.row_pos, gm, T, tpos, tlen);
+#pragma unroll
+      for (int tap = 0; tap < KS; ++tap) v |= ((unsigned)(tpos + tap - pad) < (unsigned)tlen ? 1 : 0) << tap;
+    }
+    return v;
+  };
+  for (int i = tid; i < ZBYTES / 16; i += NT) *reinterpret_cast<float4 *>(smem + 16 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (tid < NCOL / 4) {
+    *reinterpret_cast<float4 *>(smem + B1_OFF + 16 * tid) = reinterpret_cast<const float4 *>(p.b1)[tid];
+    *reinterpret_cast<float4 *>(smem + B2_OFF + 16 * tid) = reinterpret_cast<const float4 *>(p.b2)[tid];
+  }
+
+  // mel tile -> LDS (lane-linear 1 KiB pieces at the padded pitch)
+  const rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+  const rsrc_t w1r = make_rsrc(p.w1, p.w1_bytes), w2r = make_rsrc(p.w2, p.w2_bytes);
+  const uint32_t xrow = (uint32_t)p.xs * 2u;
+#pragma unroll
+  for (int i = 0; i < XPW; ++i) {
+    const int pc = w + NWV * i;
+    const int o = pc * 1024 + lane * 16;
+    const int r = o / XPITCH, within = o - r * XPITCH;
+    const int gm = m0 - 2 * pad + r;
+    const bool ok = r < XR && within < CIN1 * 2 && gm >= 0 && gm < M;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)(smem + X_OFF + pc * 1024),
+                                             16, ok ? (uint32_t)gm * xrow + (uint32_t)within : kOOB, 0, 0, 0);
+  }
+
+  // one weight stream per wave: units 0..12 of conv1 twice (two row passes), then conv2's 80
+  const uint32_t lane_off = (uint32_t)lane * 16u;
+  const uint32_t wb1 = (uint32_t)(w * NU1) * (uint32_t)kUnitB, wb2 = (uint32_t)(w * NU2) * (uint32_t)kUnitB;
+  bf16x8 pa[DEPTH][JB];
+  auto load_at = [&](auto S, int u) {  // u: position in the stream (past the end: a harmless reload)
+    constexpr int s = decltype(S)::value;
+    const bool c1 = u < 2 * NU1;
+    const int uu = c1 ? (u < NU1 ? u : u - NU1) : (u - 2 * NU1 < NU2 ? u - 2 * NU1 : 0);
+    const rsrc_t r = c1 ? w1r : w2r;
+    const uint32_t so = (c1 ? wb1 : wb2) + (uint32_t)uu * (uint32_t)kUnitB;
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int jb = 0; jb < JB; ++jb)
+      pa[s][jb] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, lane_off + jb * 1024, so, 0));
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  static_for<DEPTH>([&](auto S) { load_at(S, decltype(S)::value); });
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * DEPTH) : "memory");
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __syncthreads();
+
+  // ---- conv1 in two passes of 4 row blocks (y1 rows 0..63, 64..127; rows >= 116 are dropped)
+  static_for<2>([&](auto PASS) {
+    constexpr int ps = decltype(PASS)::value;
+    int vm1[4];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) vm1[mb] = taps(m0 - pad + (4 * ps + mb) * 16 + hrow0);
+    f32x4 acc[JB][4];
+#pragma unroll
+    for (int i = 0; i < JB; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // flat unit u, lane group hi: k = 32u + 8hi -> (tap, channel); k >= 400: zero weights
+    auto bases = [&](int u, int (&ad)[4]) {
+      const int k = 32 * u + 8 * hi;
+      const int tap = k / CIN1, c = k - tap * CIN1;
+      const int base = X_OFF + ((4 * ps) * 16 + hrow0 + tap) * XPITCH + c * 2;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+        ad[mb] = tap < KS ? (base + mb * 16 * XPITCH) & __builtin_amdgcn_sbfe(vm1[mb], tap, 1) : 0;
+    };
+    bf16x8 f0[4], f1[4];
+    auto rd = [&](const int (&ad)[4], bf16x8 (&f)[4]) {
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) f[mb] = *reinterpret_cast<const bf16x8 *>(smem + ad[mb]);
+    };
+    int ad[4];
+    bases(0, ad);
+    rd(ad, f0);
+    static_for<NU1>([&](auto UI) {
+      constexpr int u = decltype(UI)::value, sl = (ps * NU1 + u) % DEPTH;
+      if constexpr (u + 1 < NU1) {
+        bases(u + 1, ad);
+        if constexpr (u & 1) rd(ad, f0); else rd(ad, f1);
+      }
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int jb = 0; jb < JB; ++jb)
+          acc[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[sl][jb], (u & 1) ? f1[mb] : f0[mb], acc[jb][mb], 0, 0, 0);
+      load_at(std::integral_constant<int, sl>{}, ps * NU1 + u + DEPTH);
+    });
+    // + b1, tanh, bf16 -> y1 rows (the conv2 x tile); rows past YR are not needed
+#pragma unroll
+    for (int jb = 0; jb < JB; ++jb) {
+      const int n = w * 64 + jb * 16 + 4 * hi;
+      const float4 bb = *reinterpret_cast<const float4 *>(smem + B1_OFF + 4 * n);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const int r = (4 * ps + mb) * 16 + hrow0;
+        const f32x4 v = acc[jb][mb];
+        bf16x4 o;
+        o[0] = (bf16)tanhf(v[0] + bb.x);
+        o[1] = (bf16)tanhf(v[1] + bb.y);
+        o[2] = (bf16)tanhf(v[2] + bb.z);
+        o[3] = (bf16)tanhf(v[3] + bb.w);
+        if (r < YR) *reinterpret_cast<bf16x4 *>(smem + Y_OFF + r * YPITCH + n * 2) = o;
+      }
+    }
+  });
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __syncthreads();  // y1 visible
+
+  // ---- conv2 on the y1 tile (wconv's main loop)
+  int vm2[MB];  // (computed here: kept live through conv1 they cost a spill)
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) vm2[mb] = taps(m0 + mb * 16 + hrow0);
+  auto bases_x = [&](int tap, int (&ad)[MB]) {
+    const int base = Y_OFF + (hrow0 + tap) * YPITCH + hi * 16;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) ad[mb] = (base + mb * 16 * YPITCH) & __builtin_amdgcn_sbfe(vm2[mb], tap, 1);
+  };
+  bf16x8 f0[MB], f1[MB];
+  auto issue_x = [&](const int (&ad)[MB], auto KSI, bf16x8 (&f)[MB]) {
+    constexpr int off = decltype(KSI)::value * 64;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) f[mb] = *reinterpret_cast<const bf16x8 *>(smem + ad[mb] + off);
+  };
+  f32x4 acc[JB][MB];
+#pragma unroll
+  for (int i = 0; i < JB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8 (&fa)[JB], const bf16x8 (&fb)[MB]) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int jb = 0; jb < JB; ++jb)
+        acc[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[jb], fb[mb], acc[jb][mb], 0, 0, 0);
+  };
+  constexpr int S0 = 2 * NU1;  // stream position of conv2's unit 0
+  int bxc[MB], bxn[MB];
+  bases_x(0, bxc);
+  issue_x(bxc, std::integral_constant<int, 0>{}, f0);
+#pragma nounroll
+  for (int tap = 0; tap < KS; ++tap) {
+    bases_x(tap + 1, bxn);  // tap KS: every row masked (zero region), a harmless read
+    static_for<NKS>([&](auto KSI) {
+      constexpr int ks = decltype(KSI)::value, sl = (S0 + ks) % DEPTH;
+      if constexpr (ks + 1 < NKS) {
+        if constexpr (ks & 1)
+          issue_x(bxc, std::integral_constant<int, ks + 1>{}, f0);
+        else
+          issue_x(bxc, std::integral_constant<int, ks + 1>{}, f1);
+      } else {
+        issue_x(bxn, std::integral_constant<int, 0>{}, f0);
+      }
+      if constexpr (ks & 1)
+        mma(pa[sl], f1);
+      else
+        mma(pa[sl], f0);
+      load_at(std::integral_constant<int, sl>{}, S0 + tap * NKS + ks + DEPTH);
+    });
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) bxc[mb] = bxn[mb];
+  }
+
+  // epilogue: + b2, tanh, bf16 -> LDS staging (the y1 region) -> whole-row stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __syncthreads();
+#pragma unroll
+  for (int nb = 0; nb < JB; ++nb) {
+    const int n = w * 64 + nb * 16 + 4 * hi;
+    const float4 bb = *reinterpret_cast<const float4 *>(smem + B2_OFF + 4 * n);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const f32x4 v = acc[nb][mb];
+      bf16x4 o;
+      o[0] = (bf16)tanhf(v[0] + bb.x);
+      o[1] = (bf16)tanhf(v[1] + bb.y);
+      o[2] = (bf16)tanhf(v[2] + bb.z);
+      o[3] = (bf16)tanhf(v[3] + bb.w);
+      *reinterpret_cast<bf16x4 *>(smem + Y_OFF + (hrow0 + mb * 16) * OPITCH + n * 2) = o;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = NCOL * 2 / 16;
+  char *ob = reinterpret_cast<char *>(p.out);
+  const uint32_t orow = (uint32_t)p.os * 2u;
+#pragma unroll 2
+  for (int i = tid; i < BM * CPR; i += NT) {
+    const int m = i / CPR, ch = i - m * CPR;
+    if (m0 + m < M)
+      *reinterpret_cast<uint4 *>(ob + (size_t)(m0 + m) * orow + ch * 16) =
+          *reinterpret_cast<const uint4 *>(smem + Y_OFF + m * OPITCH + ch * 16);
+  }
+}
+
+
+// The PostNet's last convolution + the residual (transformer/Layers.py:129-137, fastspeech2.py:136):
+//   out[m, n] = sum_{tap, c} x[m + tap - 2, c] w[n, c, tap] + b[n] + res[m, n]     N = 80, Cin = 512
+// N = 80 fills 62.5 % of a 128-wide tile (the conv_gemm launch: 40 us at cfg2, 0.11 of peak). Here
+// the 80 output columns are 5 MFMA blocks that EVERY wave computes for its own rows: 4 waves x 2
+// row blocks of the 112-row tile (the 8th block is a masked dummy), so the weights are shared
+// by all waves and go through LDS: a 4-stage ring of k-steps (5 x 1 KiB fragment-ordered blocks,
+// LDS-DMA, one counted vmcnt + barrier per k-step), the x tile DMA'd once as in wconv. Per k-step
+// and wave: 5 + 2 fragment reads, 10 MFMAs. f32 out through an LDS staging tile (whole rows).
+struct PnTailArgs {
+  const bf16 *x;
+  int64_t xs;
+  const bf16 *w;  // [80 k-steps][5 blocks][4][16][8]
+  const float *bias;
+  const float *res;
+  int64_t rs;
+  float *out;
+  int64_t os;
+  int T, M, pad;
+  uint32_t x_bytes, w_bytes;
+  const int2 *row_pos;
+  const int32_t *rows_dev;
+};
+
+__global__ __launch_bounds__(256, 1) void pn_tail_kernel(PnTailArgs p) {
+  constexpr int KS = 5, CIN = 512, NB = 5, NCOL = 80, BM = 112, NST = 3, KPS = 2;
+  constexpr int XR = BM + KS - 1;
+  constexpr int XPITCH = CIN * 2 + 32;
+  constexpr int XPIECES = (XR * XPITCH + 1023) / 1024;
+  constexpr int XPW = (XPIECES + 3) / 4;
+  constexpr int NKS = CIN / 32, NU = KS * NKS;  // 16 k-steps per tap, 80 in all
+  constexpr int NS = NU / KPS;                  // ring stages of 2 k-steps
+  constexpr int PPS = 12;                       // 10 weight pieces + 2 dummies: every wave issues 3
+  constexpr int STG = PPS * 1024;
+  constexpr int ZBYTES = NKS * 64;
+  constexpr int X_OFF = ZBYTES;
+  constexpr int W_OFF = X_OFF + 4 * XPW * 1024;
+  constexpr int B_OFF = W_OFF + NST * STG;
+  constexpr int SMEM = B_OFF + NCOL * 4;
+  constexpr int OPITCH = NCOL * 4 + 16;         // f32 staging (in the x region)
+  static_assert(BM * OPITCH <= 4 * XPW * 1024, "staging fits the x region");
+  static_assert(SMEM <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = p.rows_dev != nullptr ? min(*p.rows_dev, p.M) : p.M, T = p.T, pad = p.pad;
+  const int m0 = blockIdx.x * BM;
+  if (m0 >= M) return;
+  const int hrow0 = lane & 15, hi = lane >> 4;
+  int vm[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int rb = 2 * w + j;
+    const int m = m0 + rb * 16 + hrow0;
+    int v = 0;
+    if (rb * 16 < BM && m < M) {
+      int tpos, tlen;
+      seq_pos(p.row_pos, m, T, tpos, tlen);
+#pragma unroll
+      for (int tap = 0; tap < KS; ++tap) v |= ((unsigned)(tpos + tap - pad) < (unsigned)tlen ? 1 : 0) << tap;
+    }
+    vm[j] = v;
+  }
+  for (int i = tid; i < ZBYTES / 16; i += 256) *reinterpret_cast<float4 *>(smem + 16 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (tid < NCOL / 4)
+    *reinterpret_cast<float4 *>(smem + B_OFF + 16 * tid) = reinterpret_cast<const float4 *>(p.bias)[tid];
+
+  const rsrc_t xr = make_rsrc(p.x, p.x_bytes), wr = make_rsrc(p.w, p.w_bytes);
+  const uint32_t xrow = (uint32_t)p.xs * 2u;
+#pragma unroll
+  for (int i = 0; i < XPW; ++i) {
+    const int pc = w + 4 * i;
+    const int o = pc * 1024 + lane * 16;
+    const int r = o / XPITCH, within = o - r * XPITCH;
+    const int gm = m0 - pad + r;
+    const bool ok = r < XR && within < CIN * 2 && gm >= 0 && gm < M;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)(smem + X_OFF + pc * 1024),
+                                             16, ok ? (uint32_t)gm * xrow + (uint32_t)within : kOOB, 0, 0, 0);
+  }
+  // stage s (k-steps 2s, 2s + 1) -> ring slot s % NST: wave w DMAs pieces w, w + 4, w + 8 (pieces
+  // 10, 11: dummies, zeros)
+  auto wdma = [&](int st_idx) {
+    char *st = smem + W_OFF + (st_idx % NST) * STG;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int pc = w + 4 * j;
+      const uint32_t off = pc < KPS * NB ? (uint32_t)(st_idx * KPS * NB + pc) * 1024u + (uint32_t)lane * 16u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void *)(st + pc * 1024), 16, off,
+                                               0, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st) wdma(st);
+
+  f32x4 acc[NB][2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[b][0] = acc[b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // stage s: k-steps u = 2s + q (tap = u / 16): every fragment read first, then the 20 MFMAs
+  auto stage = [&](int st_idx) {
+    const char *st = smem + W_OFF + (st_idx % NST) * STG;
+    bf16x8 fa[KPS][NB], fb[KPS][2];
+#pragma unroll
+    for (int q = 0; q < KPS; ++q) {
+      const int u = st_idx * KPS + q, tap = u >> 4, ks = u & 15;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ad = (X_OFF + ((2 * w + j) * 16 + hrow0 + tap) * XPITCH + hi * 16) & __builtin_amdgcn_sbfe(vm[j], tap, 1);
+        fb[q][j] = *reinterpret_cast<const bf16x8 *>(smem + ad + ks * 64);
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b) fa[q][b] = *reinterpret_cast<const bf16x8 *>(st + (q * NB + b) * 1024 + lane * 16);
+    }
+#pragma unroll
+    for (int q = 0; q < KPS; ++q)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          acc[b][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q][b], fb[q][j], acc[b][j], 0, 0, 0);
+  };
+  // the x tile (issued first) and stage 0 landed; stage 1 may stay in flight
+  asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __syncthreads();
+#pragma nounroll
+  for (int st = 0; st < NS; ++st) {
+    if (st > 0) {
+      // stage st landed (this wave's pieces; the next stage may stay in flight) and visible to all
+      // waves; every wave is past stage st - 1, whose slot the DMA below refills
+      if (st + 1 < NS)
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (st + NST - 1 < NS) wdma(st + NST - 1);
+    stage(st);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __syncthreads();  // every wave is done with the x tile: it becomes the f32 staging tile
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int n = b * 16 + 4 * hi;
+    const float4 bb = *reinterpret_cast<const float4 *>(smem + B_OFF + 4 * n);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = (2 * w + j) * 16 + hrow0;
+      if (r < BM) {
+        const f32x4 v = acc[b][j];
+        *reinterpret_cast<float4 *>(smem + X_OFF + r * OPITCH + n * 4) =
+            make_float4(v[0] + bb.x, v[1] + bb.y, v[2] + bb.z, v[3] + bb.w);
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = NCOL * 4 / 16;  // 20 16-byte chunks per row
+  for (int i = tid; i < BM * CPR; i += 256) {
+    const int m = i / CPR, ch = i - m * CPR;
+    if (m0 + m < M) {
+      const float4 a = *reinterpret_cast<const float4 *>(smem + X_OFF + m * OPITCH + ch * 16);
+      const float4 r = *reinterpret_cast<const float4 *>(p.res + (size_t)(m0 + m) * p.rs + ch * 4);
+      *reinterpret_cast<float4 *>(p.out + (size_t)(m0 + m) * p.os + ch * 4) =
+          make_float4(a.x + r.x, a.y + r.y, a.z + r.z, a.w + r.w);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int64_t fs2_wconv_weight_elems(int KS, int Cin, int N) { return (int64_t)N * ((KS * Cin + 31) / 32 * 32); }
@@ -260,14 +696,46 @@ extern "C" int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream) {
   if (d->B < 0 || d->T < 0 || d->pad < 0 || d->x_row_stride < d->Cin || (d->x_row_stride & 7) ||
       d->out_row_stride < d->N || (d->out_row_stride & 7))
     return FS2_EINVAL;
-  if (!(d->Cin == 512 || d->Cin == 80) || d->N != 512 || d->KS != 5 || d->pad > d->KS - 1 ||
-      d->epilogue != FS2_EPI_BIAS_TANH)
+  const bool tail = d->epilogue == FS2_EPI_BIAS_RES;  // the last conv: N = 80, + residual, f32 out
+  if (tail) {
+    if (d->Cin != 512 || d->N != 80 || d->KS != 5 || d->pad != 2 || d->w2 != nullptr) return FS2_EUNSUPPORTED;
+    if (d->residual == nullptr || d->res_row_stride < 80 || (d->res_row_stride & 3) || (d->out_row_stride & 3))
+      return FS2_EINVAL;
+  } else if (!(d->Cin == 512 || d->Cin == 80) || d->N != 512 || d->KS != 5 || d->pad > d->KS - 1 ||
+             d->epilogue != FS2_EPI_BIAS_TANH) {
     return FS2_EUNSUPPORTED;
+  }
   if (d->x == d->out) return FS2_EINVAL;  // other tiles re-read x rows (halo)
+  if ((d->rows_dev == nullptr) != (d->row_pos == nullptr)) return FS2_EINVAL;
   const int64_t M64 = (int64_t)d->B * d->T;
   if (M64 == 0) return FS2_OK;
   const int64_t xb = M64 * d->x_row_stride * 2;
   if (xb >= (1LL << 31) || M64 > 0x7fffff00LL) return FS2_EUNSUPPORTED;
+  const int2 *row_pos = reinterpret_cast<const int2 *>(d->row_pos);
+  // packed rows: the grid covers rows_max (the host's bound on the device row count) when given
+  const int64_t Mg = (d->rows_dev != nullptr && d->rows_max > 0 && d->rows_max < M64) ? d->rows_max : M64;
+  if (tail) {
+    PnTailArgs q;
+    q.x = reinterpret_cast<const bf16 *>(d->x);
+    q.xs = d->x_row_stride;
+    q.w = reinterpret_cast<const bf16 *>(d->w);
+    q.bias = d->bias;
+    q.res = d->residual;
+    q.rs = d->res_row_stride;
+    q.out = reinterpret_cast<float *>(d->out);
+    q.os = d->out_row_stride;
+    q.T = d->T;
+    q.M = (int)M64;
+    q.pad = d->pad;
+    q.x_bytes = (uint32_t)xb;
+    q.w_bytes = (uint32_t)(fs2_wconv_weight_elems(d->KS, d->Cin, d->N) * 2);
+    q.row_pos = row_pos;
+    q.rows_dev = d->rows_dev;
+    q.M = (int)Mg;
+    hipLaunchKernelGGL(pn_tail_kernel, dim3((unsigned)((Mg + 111) / 112)), dim3(256), 0, as_stream(stream), q);
+    FS2_CHECK_LAUNCH();
+    return FS2_OK;
+  }
   WconvArgs p;
   p.x = reinterpret_cast<const bf16 *>(d->x);
   p.xs = d->x_row_stride;
@@ -281,11 +749,35 @@ extern "C" int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream) {
   p.pad = d->pad;
   p.x_bytes = (uint32_t)xb;
   p.w_bytes = (uint32_t)(fs2_wconv_weight_elems(d->KS, d->Cin, d->N) * 2);
-  const int nwg = (int)((M64 + 111) / 112);
+  p.row_pos = row_pos;
+  p.rows_dev = d->rows_dev;
+  p.M = (int)Mg;
+  const int nwg = (int)((Mg + 111) / 112);
 #ifndef WCONV_WQ
 #define WCONV_WQ 1  // 8 waves x 64 columns (2 quads per wave: 224 accumulators + the ring spill; analysis only)
 #endif
-  if (d->Cin == 80)
+  if (d->w2 != nullptr) {
+    // the PostNet's first two layers fused (80 -> 512 -> 512, both tanh)
+    if (d->Cin != 80 || d->bias2 == nullptr || d->pad != 2) return FS2_EUNSUPPORTED;
+    PnHeadArgs q;
+    q.x = p.x;
+    q.xs = p.xs;
+    q.w1 = p.w;
+    q.w2 = reinterpret_cast<const bf16 *>(d->w2);
+    q.b1 = d->bias;
+    q.b2 = d->bias2;
+    q.out = p.out;
+    q.os = p.os;
+    q.T = p.T;
+    q.M = p.M;
+    q.pad = p.pad;
+    q.x_bytes = p.x_bytes;
+    q.w1_bytes = p.w_bytes;
+    q.w2_bytes = (uint32_t)(fs2_wconv_weight_elems(d->KS, 512, 512) * 2);
+    q.row_pos = row_pos;
+    q.rows_dev = d->rows_dev;
+    hipLaunchKernelGGL(pn_head_kernel, dim3(nwg), dim3(512), 0, as_stream(stream), q);
+  } else if (d->Cin == 80)
     hipLaunchKernelGGL((wconv_kernel<5, 80, 1>), dim3(nwg), dim3(512), 0, as_stream(stream), p);
   else
     hipLaunchKernelGGL((wconv_kernel<5, 512, WCONV_WQ>), dim3(nwg), dim3(512 / WCONV_WQ), 0, as_stream(stream), p);

@@ -56,7 +56,8 @@ class WconvDesc(ctypes.Structure):
     _fields_ = [
         ("x", _p), ("x_row_stride", _i64), ("w", _p), ("bias", _p),
         ("B", _i), ("T", _i), ("Cin", _i), ("N", _i), ("KS", _i), ("pad", _i), ("epilogue", _i),
-        ("out", _p), ("out_row_stride", _i64),
+        ("out", _p), ("out_row_stride", _i64), ("w2", _p), ("bias2", _p), ("residual", _p), ("res_row_stride", _i64),
+        ("rows_dev", _p), ("row_pos", _p), ("rows_max", _i),
     ]
 
 

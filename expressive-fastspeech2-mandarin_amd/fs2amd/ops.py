@@ -330,22 +330,82 @@ def pack_wconv_weight(w, scale=None):
     return pack_frag_rows(k)
 
 
-def wconv(x, w_packed, bias, *, ks, pad, out=None):
+def pack_wconv_tail(w, scale=None):
+    """The PostNet's last conv (nn.Conv1d [80, 512, 5], BatchNorm folded like pack_conv_weight) for
+    fs2_wconv's FS2_EPI_BIAS_RES form: K = (tap, channel) flattened, k-step-major fragment order
+    [K/32][N/16][4][16][8] (every wave reads all 80 columns of a k-step from the LDS ring)."""
+    w = w.detach().float()
+    if scale is not None:
+        w = w * scale.detach().float().view(-1, 1, 1)
+    N, cin, ks = w.shape
+    assert N % 16 == 0 and (ks * cin) % 32 == 0, (N, cin, ks)
+    k = w.permute(0, 2, 1).reshape(N, ks * cin)
+    b = k.reshape(N // 16, 16, ks * cin // 32, 4, 8).permute(2, 0, 3, 1, 4)
+    return b.reshape(-1).to(torch.bfloat16).contiguous()
+
+
+def _wconv_rows(x, layout):
+    """(B, T, cin, out row shape) of a fs2_wconv operand: padded [B, T, C] or packed [B*T, C]."""
+    if layout is not None:
+        assert x.dim() == 2 and x.shape[0] == layout.capacity, (tuple(x.shape), layout.capacity)
+        return layout.B, layout.T, x.shape[1], (layout.capacity,)
+    B, T, cin = x.shape
+    return B, T, cin, (B, T)
+
+
+def _wconv_layout(d, layout):
+    if layout is not None:
+        d.rows_dev, d.row_pos = layout.rows_dev, layout.row_pos.data_ptr()
+        hint = getattr(layout, "rows_hint", None)
+        d.rows_max = int(hint) if hint else 0
+
+
+def wconv_tail(x, w_packed, bias, residual, *, ks=5, pad=2, out=None, layout=None):
+    """PostNet last conv + residual: out f32 [B, T, 80] = conv(x; w) + bias + residual (fs2_wconv,
+    FS2_EPI_BIAS_RES; w_packed from :func:`pack_wconv_tail`). layout: packed rows (ops.SeqLayout)."""
+    _gpu(x, w_packed, bias, residual)
+    if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16 or residual.dtype != torch.float32:
+        raise TypeError("fs2amd.wconv_tail: bf16 x / weights, f32 residual")
+    B, T, cin, rs = _wconv_rows(x, layout)
+    N = bias.numel()
+    assert tuple(residual.shape) == (*rs, N) and w_packed.numel() == _lib.fs2_wconv_weight_elems(ks, cin, N)
+    if out is None:
+        out = torch.empty(*rs, N, device=x.device, dtype=torch.float32)
+    d = L.WconvDesc()
+    _wconv_layout(d, layout)
+    d.x, d.x_row_stride = x.data_ptr(), _rows(x, "x")
+    d.w, d.bias = w_packed.data_ptr(), bias.data_ptr()
+    d.B, d.T, d.Cin, d.N, d.KS, d.pad, d.epilogue = B, T, cin, N, ks, pad, L.EPI_BIAS_RES
+    d.out, d.out_row_stride = out.data_ptr(), _rows(out, "out")
+    d.residual, d.res_row_stride = residual.data_ptr(), _rows(residual, "residual")
+    L.check(_lib.fs2_wconv(ctypes.byref(d), _stream(x)), "fs2_wconv")
+    return out
+
+
+def wconv(x, w_packed, bias, *, ks, pad, out=None, second=None, layout=None):
     """PostNet Conv1d(512, 512, k=5) + folded BatchNorm + tanh on padded bf16 rows [B, T, 512]
-    (fs2_wconv; w_packed from :func:`pack_wconv_weight`)."""
+    (fs2_wconv; w_packed from :func:`pack_wconv_weight`). second = (w2_packed, bias2): the next
+    512 -> 512 conv applied in the same launch (the PostNet's layers 0 and 1, Cin = 80). layout:
+    packed rows [B*T, C] (ops.SeqLayout; the valid-region PostNet)."""
     _gpu(x, w_packed, bias)
     if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
         raise TypeError("fs2amd.wconv: bf16 activations and weights only")
-    B, T, cin = x.shape
+    B, T, cin, rs = _wconv_rows(x, layout)
     N = bias.numel()
     assert w_packed.is_contiguous() and w_packed.numel() == _lib.fs2_wconv_weight_elems(ks, cin, N)
+    if second is not None:
+        _gpu(*second)
+        assert second[0].numel() == _lib.fs2_wconv_weight_elems(ks, N, N) and second[1].numel() == N
     if out is None:
-        out = torch.empty(B, T, N, device=x.device, dtype=torch.bfloat16)
+        out = torch.empty(*rs, N, device=x.device, dtype=torch.bfloat16)
     d = L.WconvDesc()
+    _wconv_layout(d, layout)
     d.x, d.x_row_stride = x.data_ptr(), _rows(x, "x")
     d.w, d.bias = w_packed.data_ptr(), bias.data_ptr()
     d.B, d.T, d.Cin, d.N, d.KS, d.pad, d.epilogue = B, T, cin, N, ks, pad, L.EPI_BIAS_TANH
     d.out, d.out_row_stride = out.data_ptr(), _rows(out, "out")
+    if second is not None:
+        d.w2, d.bias2 = second[0].data_ptr(), second[1].data_ptr()
     L.check(_lib.fs2_wconv(ctypes.byref(d), _stream(x)), "fs2_wconv")
     return out
 

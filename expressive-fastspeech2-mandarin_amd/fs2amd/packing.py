@@ -21,7 +21,7 @@ import torch
 
 from . import _lib as L
 from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split, pack_ffn_weights, pack_frag_rows, \
-    pack_vp_fused, pack_wconv_weight
+    pack_vp_fused, pack_wconv_tail, pack_wconv_weight
 
 
 def _f32(t, device):
@@ -149,14 +149,18 @@ def _postnet(pn, device, compute):
         conv, bn = seq[0].conv, seq[1]
         s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
         b = (conv.bias.detach().float() - bn.running_mean.detach().float()) * s + bn.bias.detach().float()
-        wfr = None
+        wfr = wtail = None
         if compute == L.FS2_BF16 and conv.in_channels in (512, 80) and conv.out_channels == 512 \
                 and conv.kernel_size[0] == 5:
             # the weight-streamed kernel's fragment order (fs2_wconv)
             wfr = pack_wconv_weight(conv.weight.to(device), scale=s.to(device))
+        if compute == L.FS2_BF16 and conv.in_channels == 512 and conv.out_channels == 80 \
+                and conv.kernel_size[0] == 5 and conv.padding[0] == 2:
+            # the last conv + residual on fs2_wconv's N = 80 form
+            wtail = pack_wconv_tail(conv.weight.to(device), scale=s.to(device))
         layers.append(SimpleNamespace(w=pack_conv_weight(conv.weight.to(device), compute, scale=s.to(device)),
                                       b=_f32(b, device), k=conv.kernel_size[0], p=conv.padding[0],
-                                      cin=conv.in_channels, cout=conv.out_channels, wfr=wfr))
+                                      cin=conv.in_channels, cout=conv.out_channels, wfr=wfr, wtail=wtail))
     return layers
 
 

@@ -429,7 +429,7 @@ def _stage2(P, g, st, T_out, T_dec, p_control, postnet_valid=False, rows_hint=No
         mel_bf = _mel_copy(P, x, (lay.B, lay.T))
         mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
                          out_dtype=L.FS2_F32, src_layout=lay, out2=mel_bf)
-        return mel, _postnet(P, mel, mel_bf, dec_lens if postnet_valid else None), st
+        return mel, _postnet(P, mel, mel_bf, dec_lens if postnet_valid else None, rows_hint), st
     # LR gather with the decoder's position encoding fused (frame-level variance needs the bare
     # expanded x first, so the PE add moves to a second pass in that configuration)
     _ensure_lr(st)
@@ -451,7 +451,7 @@ def _stage2(P, g, st, T_out, T_dec, p_control, postnet_valid=False, rows_hint=No
     mel_bf = _mel_copy(P, x, x.shape[:2])
     mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
                      out_dtype=L.FS2_F32, out2=mel_bf)
-    return mel, _postnet(P, mel, mel_bf, dec_lens if postnet_valid else None), st
+    return mel, _postnet(P, mel, mel_bf, dec_lens if postnet_valid else None, rows_hint), st
 
 
 def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, max_src_len, mels, mel_lens,
@@ -604,6 +604,11 @@ def wconv_on():
     return os.environ.get("FS2_WCONV", "1") != "0"
 
 
+def pn_head_on():
+    """FS2_PN_HEAD=0: the PostNet's first two convs as two fs2_wconv launches (A/B)."""
+    return os.environ.get("FS2_PN_HEAD", "1") != "0"
+
+
 def postnet_valid_region_on():
     return os.environ.get("FS2_POSTNET_VALID", "1") != "0"
 
@@ -625,7 +630,7 @@ def _postnet_consts(P, bf16_input):
     return ent
 
 
-def _postnet(P, mel, mel_bf=None, mel_len=None):
+def _postnet(P, mel, mel_bf=None, mel_len=None, sum_len=None):
     """PostNet (BN folded, transformer/Layers.py:92-137) + residual (fastspeech2.py:136) with the
     reference's padded [B, T, n_mel] semantics: padded frames (bias values) feed the k5 taps and
     get outputs too. mel_bf: optional bf16 copy of mel, the first conv's input (the residual stays
@@ -637,39 +642,59 @@ def _postnet(P, mel, mel_bf=None, mel_len=None):
     10 the fixed block (_postnet_consts). An utterance within 40 frames of T runs whole. Free-
     running cfg2 (T = 959 for 11.1k valid frames) computes 12.4k rows instead of 61.4k."""
     if mel_len is not None and postnet_valid_region_on() and mel.shape[0] > 0:
-        return _postnet_valid(P, mel, mel_bf, mel_len)
+        return _postnet_valid(P, mel, mel_bf, mel_len, sum_len)
     y = mel if mel_bf is None else mel_bf
+    return _postnet_convs(P, y, mel)
+
+
+def _postnet_convs(P, y, res, layout=None):
+    """The PostNet's convs (BN folded) on y (mel's bf16 copy, or the f32 mel) + the residual res
+    (f32 mel); padded [B, T, C] rows, or packed rows of ``layout`` (the valid-region form). Both
+    forms take the same kernels: fs2_wconv for layers 0 + 1 (one launch), 2, 3 and the last conv +
+    residual (its N = 80 form); fs2_conv1d where those shapes do not apply."""
     n_pn = len(P.postnet)
+    first = 0
+    if n_pn > 2 and y.dtype == torch.bfloat16 and wconv_on() and pn_head_on() and \
+            getattr(P.postnet[0], "wfr", None) is not None and getattr(P.postnet[1], "wfr", None) is not None and \
+            P.postnet[0].cin == 80 and P.postnet[0].k == 5 and P.postnet[0].p == 2 and P.postnet[1].p == 2:
+        # layers 0 and 1 (80 -> 512 -> 512) in one launch: the first conv's output stays on chip
+        l0, l1 = P.postnet[0], P.postnet[1]
+        y = ops.wconv(y, l0.wfr, l0.b, ks=l0.k, pad=l0.p, second=(l1.wfr, l1.b), layout=layout)
+        first = 2
     for i, lp in enumerate(P.postnet):
+        if i < first:
+            continue
         if i < n_pn - 1 and getattr(lp, "wfr", None) is not None and wconv_on() and y.dtype == torch.bfloat16:
             # 512 -> 512 convs: the weight-streamed kernel (fs2_wconv)
-            y = ops.wconv(y, lp.wfr, lp.b, ks=lp.k, pad=lp.p)
+            y = ops.wconv(y, lp.wfr, lp.b, ks=lp.k, pad=lp.p, layout=layout)
         elif i < n_pn - 1:
             y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute,
-                           epilogue=L.EPI_BIAS_TANH, out_dtype=P.act_dtype)
+                           epilogue=L.EPI_BIAS_TANH, out_dtype=P.act_dtype, layout=layout)
+        elif getattr(lp, "wtail", None) is not None and wconv_on() and y.dtype == torch.bfloat16 \
+                and res.dtype == torch.float32:
+            # 512 -> 80 + residual: all 80 columns per wave, weights through an LDS ring
+            y = ops.wconv_tail(y, lp.wtail, lp.b, res.contiguous(), ks=lp.k, pad=lp.p, layout=layout)
         else:
             y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute, epilogue=L.EPI_BIAS_RES,
-                           out_dtype=L.FS2_F32, residual=mel)
+                           out_dtype=L.FS2_F32, residual=res, layout=layout)
     return y
 
 
-def _postnet_valid(P, mel, mel_bf, mel_len):
+def _postnet_valid(P, mel, mel_bf, mel_len, sum_len=None):
     B, T, C = mel.shape
     c, tail = _postnet_consts(P, mel_bf is not None)
     # each utterance's frames + POSTNET_MARGIN, or all T when within 2 margins of it
     lay = ops.SeqLayout(mel_len, T, margin=POSTNET_MARGIN)
+    # the host's bound on the packed rows (free-running: sum(mel_len) from the one host read),
+    # bucketed so a captured graph serves every batch of the bucket: sizes the wconv grids
+    # (a function of the decoder's row bucket only, as the stage-2 graph key: rows <= sum + 20 B)
+    lay.rows_hint = None if sum_len is None else \
+        min(ops.rows_bucket(sum_len, B * T) + POSTNET_MARGIN * B, lay.capacity)
     # the f32 mel (the residual) and its bf16 copy (the first conv's input) packed in one launch
     res, y = ops.pack_rows(lay, mel.contiguous(), None if mel_bf is None else mel_bf.contiguous())
     if y is None:
         y = res
-    n_pn = len(P.postnet)
-    for i, lp in enumerate(P.postnet):
-        if i < n_pn - 1:
-            y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute,
-                           epilogue=L.EPI_BIAS_TANH, out_dtype=P.act_dtype, layout=lay)
-        else:
-            y = ops.conv1d(y, lp.w, lp.b, cin=lp.cin, ks=lp.k, pad=lp.p, compute=P.compute, epilogue=L.EPI_BIAS_RES,
-                           out_dtype=L.FS2_F32, residual=res, layout=lay)
+    y = _postnet_convs(P, y, res, layout=lay)
     # [B, T, C]: computed rows where exact, else the constant row / the tail block
     return ops.postnet_assemble(y, lay, c.contiguous(), tail.contiguous())
 

@@ -245,6 +245,22 @@ typedef struct fs2_wconv_desc {
   int epilogue;             /* FS2_EPI_BIAS_TANH                                                  */
   void *out;                /* bf16 [B*T, >= N]                                                   */
   int64_t out_row_stride;
+  /* optional second conv on the first one's output, in the same launch (the PostNet's layers 0
+     and 1: Cin = 80, N = 512, then 512 -> 512, both k = 5, pad 2, tanh): out = tanh(conv(tanh(
+     conv(x; w) + bias); w2) + bias2). w2: fs2_wconv_weight_elems(5, 512, 512) elements, NULL = off */
+  const void *w2;
+  const float *bias2;
+  /* epilogue FS2_EPI_BIAS_RES (the PostNet's last conv + the residual, fastspeech2.py:136): Cin = 512,
+     N = 80, KS = 5, pad 2; out f32 [B*T, >= 80] = conv(x; w) + bias + residual (f32 [B*T, >= 80]);
+     w in the k-step-major order [K/32][N/16][4][16][8], element (s, b, h, r, e) = W[16b + r][32s + 8h + e] */
+  const float *residual;
+  int64_t res_row_stride;
+  /* packed rows (fs2_seq_layout / fs2_seq_layout_margin; both NULL = padded [B, T] rows): row r is
+     frame row_pos[2r] of a sequence of row_pos[2r+1] frames, taps outside it read zeros; the active
+     row count is *rows_dev (device), the grid covers rows_max rows when 0 < rows_max < B*T */
+  const int32_t *rows_dev;
+  const int32_t *row_pos;
+  int rows_max;
 } fs2_wconv_desc;
 
 int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream);

@@ -5,7 +5,7 @@ TAG=${1:-check}
 O=gpurun_out/$TAG
 mkdir -p $O
 if [ -n "${FIRST_TESTS:-}" ]; then
-  timeout -k 10 300 python -u -m pytest $FIRST_TESTS -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
+  timeout -k 10 300 python -u -m pytest $FIRST_TESTS ${FIRST_K:+-k "$FIRST_K"} -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
     > $O/first.log 2>&1 || { tail -40 $O/first.log; exit 1; }
   tail -3 $O/first.log
 fi
