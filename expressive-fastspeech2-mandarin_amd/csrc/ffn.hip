@@ -65,6 +65,14 @@ struct FfnArgs {
   int64_t qs;          // qkv row stride (elements)
   uint32_t wq_bytes;
   int nq;              // multiple of 256
+  // the block's attention output projection + residual + LayerNorm in the prologue (PRE kernels):
+  // the FFN input h = LN1(att . wfc^T + bfc + x) of the tile and its halo rows, computed on chip
+  const bf16 *att;     // [rows, >= 256]
+  int64_t as;
+  uint32_t att_bytes;
+  const bf16 *wfc;     // [256][256] in fragment order [4][8][4][4][16][8]
+  const float *bfc, *g1, *be1;
+  float eps1;
 };
 
 // f32 partial Y^T accumulators per (tile, split): 4 waves x acc2[4][MB] x 64 lanes x 16 B
@@ -94,7 +102,7 @@ constexpr int kLgkm0 = 0xC07F;
 
 // MB = 16-row activation blocks per tile: 7 (112 rows: the full-chip decoder launches) or 4 (64 rows:
 // the split-hidden form of small launches, whose 4 splits x 64-row tiles fill the chip)
-template <int KS, int NCH, int MB>
+template <int KS, int NCH, int MB, bool PRE = false>
 __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   constexpr int BM = 16 * MB;
   constexpr uint32_t kPartBytes = (uint32_t)part_bytes(MB);
@@ -114,7 +122,12 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   constexpr int B1_OFF = H_OFF + BM * 512;
   constexpr int EP_OFF = B1_OFF + F * 4;            // b2, gamma, beta: 3 x 256 f32
   constexpr int RED_OFF = EP_OFF + 3 * kD * 4;      // LN row statistics: [BM rows][4 waves] f32
-  constexpr int SMEM = RED_OFF + BM * 16;
+  // PRE: the attention-output tile (XROWS rows at the x pitch) over the H / vector regions, and
+  // its LN row statistics after it; both dead before GEMM1 starts
+  constexpr int ATT_OFF = H_OFF;
+  constexpr int RED0_OFF = ATT_OFF + 4 * XP_PER_WAVE * 1024;
+  constexpr int SMEM0 = RED_OFF + BM * 16;
+  constexpr int SMEM = PRE && RED0_OFF + 64 * 16 > SMEM0 ? RED0_OFF + 64 * 16 : SMEM0;
   static_assert(SMEM <= 163840, "LDS");
   static_assert(BM * 528 <= 4 * XP_PER_WAVE * 1024, "Q|K|V staging fits in the x region");
   constexpr int NK1 = KS * (kD / 32);  // GEMM1 units per chunk (tap-major, 8 k-steps per tap)
@@ -168,23 +181,26 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     for (int tap = 0; tap < KS; ++tap) v |= ((unsigned)(tpos + tap - pad) < (unsigned)tlen ? 1 : 0) << tap;
     vmask[mb] = v;
   }
-  // b1 -> LDS, the zero slot; consume the row_pos loads before the DMA stream starts
-  for (int i = tid; i < F / 4; i += 256)
-    *reinterpret_cast<float4 *>(smem + B1_OFF + 16 * i) = reinterpret_cast<const float4 *>(p.b1)[i];
-  if (tid < 3 * kD / 4) {  // the LN epilogue's vectors, read once here instead of after the K loop
-    const float *src = tid < kD / 4 ? a.bias : tid < kD / 2 ? a.gamma : a.beta;
-    *reinterpret_cast<float4 *>(smem + EP_OFF + 16 * tid) =
-        reinterpret_cast<const float4 *>(src)[tid % (kD / 4)];
-  }
+  auto load_vectors = [&]() {
+    // b1 -> LDS; the LN epilogue's vectors, read once here instead of after the K loop
+    for (int i = tid; i < F / 4; i += 256)
+      *reinterpret_cast<float4 *>(smem + B1_OFF + 16 * i) = reinterpret_cast<const float4 *>(p.b1)[i];
+    if (tid < 3 * kD / 4) {
+      const float *src = tid < kD / 4 ? a.bias : tid < kD / 2 ? a.gamma : a.beta;
+      *reinterpret_cast<float4 *>(smem + EP_OFF + 16 * tid) =
+          reinterpret_cast<const float4 *>(src)[tid % (kD / 4)];
+    }
+  };
+  if constexpr (!PRE) load_vectors();
   if (tid < 32) *reinterpret_cast<float4 *>(smem + ZERO_OFF + 16 * tid) = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) asm volatile("" ::"v"(vmask[mb]));
 
-  // ---- x tile (rows m0 - pad .. m0 + BM + KS - 2, all 256 channels) -> LDS, once
-  const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const rsrc_t wr = make_rsrc(p.w, p.w_bytes);
-  const uint32_t xrow = (uint32_t)a.xs * 2u;
-  {
+  // lane-linear 1 KiB LDS-DMA pieces of a [XROWS x 512 B] row tile at the 544-byte pitch
+  auto tile_dma = [&](const void *src, uint32_t bytes, int64_t stride, int off) {
+    const rsrc_t sr = make_rsrc(src, bytes);
+    const uint32_t srow = (uint32_t)stride * 2u;
 #pragma unroll
     for (int i = 0; i < XP_PER_WAVE; ++i) {
       const int pc = w + 4 * i;
@@ -193,9 +209,139 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       const int gm = m0 - pad + r;
       const bool ok = r < XROWS && within < 512 && gm >= 0 && gm < M;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          xr, (__attribute__((address_space(3))) void *)(smem + X_OFF + pc * 1024), 16,
-          ok ? (uint32_t)gm * xrow + (uint32_t)within : kOOB, 0, 0, 0);
+          sr, (__attribute__((address_space(3))) void *)(smem + off + pc * 1024), 16,
+          ok ? (uint32_t)gm * srow + (uint32_t)within : kOOB, 0, 0, 0);
     }
+  };
+  if constexpr (!PRE) {
+    // ---- x tile (rows m0 - pad .. m0 + BM + KS - 2, all 256 channels) -> LDS, once
+    tile_dma(a.x, a.x_bytes, a.xs, X_OFF);
+  } else {
+    // ---- prologue GEMM0 (SubLayers.py:54-55 + Layers.py:25: fc + residual + LayerNorm): the FFN
+    // input h of the tile's XROWS rows (halo included: the taps of GEMM1 read them), written as
+    // the x tile. fc^T[n, m] = sum_d Wfc[n, d] att[m, d]: the 8 weight k-steps of this wave's 64
+    // output channels stay in registers for both row passes (4 blocks = 64 rows each); the att
+    // tile is DMA'd to LDS at the x pitch; residual rows from global; LN statistics via LDS.
+    tile_dma(p.att, p.att_bytes, p.as, ATT_OFF);
+    const rsrc_t fr = make_rsrc(p.wfc, (uint32_t)(kD * kD * 2));
+    const uint32_t lane_o = (uint32_t)lane * 16u;
+    bf16x8 wf[8][4];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+        wf[ks][jb] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    fr, lane_o + (uint32_t)(jb * 1024), (uint32_t)((w * 8 + ks) * kUnit), 0));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+    float *red0 = reinterpret_cast<float *>(smem + RED0_OFF);
+    const int hr = lane & 15, hq = lane >> 4;
+    const bf16 *xres = reinterpret_cast<const bf16 *>(a.x);
+    static_for<(XROWS + 63) / 64>([&](auto PS) {
+      constexpr int ps = decltype(PS)::value;
+      f32x4 a0[4][4];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) a0[jb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        bf16x8 fb[4];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          const int r = min(64 * ps + 16 * mb + hr, XROWS - 1);  // rows past the tile: never stored
+          fb[mb] = *reinterpret_cast<const bf16x8 *>(smem + ATT_OFF + r * XPITCH + ks * 64 + hq * 16);
+        }
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+          for (int jb = 0; jb < 4; ++jb)
+            a0[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][jb], fb[mb], a0[jb][mb], 0, 0, 0);
+      }
+      // + bfc + residual; row statistics over the 4 waves' 64 columns each
+      float part[4], mean[4], var[4];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const int r = 64 * ps + 16 * mb + hr, gm = m0 - pad + r;
+        const bool ok = r < XROWS && gm >= 0 && gm < M;
+        float sum = 0.f;
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          const int n = w * 64 + jb * 16 + 4 * hq;
+          const float4 bb = *reinterpret_cast<const float4 *>(p.bfc + n);
+          bf16x4 xv = {(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+          if (ok) xv = *reinterpret_cast<const bf16x4 *>(xres + (int64_t)gm * a.xs + n);
+          f32x4 v = a0[jb][mb];
+          v[0] = v[0] + bb.x + (float)xv[0];
+          v[1] = v[1] + bb.y + (float)xv[1];
+          v[2] = v[2] + bb.z + (float)xv[2];
+          v[3] = v[3] + bb.w + (float)xv[3];
+          a0[jb][mb] = v;
+          sum += (v[0] + v[1]) + (v[2] + v[3]);
+        }
+        part[mb] = sum;
+      }
+      auto reduce4 = [&](float (&pv)[4], float (&tot)[4]) {
+        float t[4];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) t[mb] = __shfl_xor(pv[mb], 16, 64);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) pv[mb] += t[mb];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) t[mb] = __shfl_xor(pv[mb], 32, 64);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) red0[(mb * 16 + hr) * 4 + w] = pv[mb] + t[mb];
+        __builtin_amdgcn_s_waitcnt(kLgkm0);
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          const float4 r4 = *reinterpret_cast<const float4 *>(red0 + (mb * 16 + hr) * 4);
+          tot[mb] = (r4.x + r4.y) + (r4.z + r4.w);
+        }
+        __builtin_amdgcn_s_waitcnt(kLgkm0);
+        __builtin_amdgcn_s_barrier();
+      };
+      reduce4(part, mean);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        mean[mb] *= 1.0f / kD;
+        float ss = 0.f;
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          f32x4 d = a0[jb][mb];
+          d[0] -= mean[mb];
+          d[1] -= mean[mb];
+          d[2] -= mean[mb];
+          d[3] -= mean[mb];
+          a0[jb][mb] = d;
+          ss += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+        }
+        part[mb] = ss;
+      }
+      reduce4(part, var);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const int r = 64 * ps + 16 * mb + hr;
+        const float rstd = 1.0f / sqrtf(var[mb] * (1.0f / kD) + p.eps1);
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          const int n = w * 64 + jb * 16 + 4 * hq;
+          const float4 g = *reinterpret_cast<const float4 *>(p.g1 + n);
+          const float4 be = *reinterpret_cast<const float4 *>(p.be1 + n);
+          const f32x4 d = a0[jb][mb];
+          bf16x4 o;
+          o[0] = (bf16)(d[0] * rstd * g.x + be.x);
+          o[1] = (bf16)(d[1] * rstd * g.y + be.y);
+          o[2] = (bf16)(d[2] * rstd * g.z + be.z);
+          o[3] = (bf16)(d[3] * rstd * g.w + be.w);
+          if (r < XROWS) *reinterpret_cast<bf16x4 *>(smem + X_OFF + r * XPITCH + n * 2) = o;
+        }
+      }
+    });
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();  // every wave past its att reads: the vectors overwrite the region
+    load_vectors();
   }
 
   // ---- weight units: register ring of DEPTH units. Every load site is static (its unit is known
@@ -799,6 +945,23 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
     p.nq = d->nqkv;
     p.wq_bytes = (uint32_t)((int64_t)d->nqkv * kD * 2);
   }
+  const bool pre = d->pre_att != nullptr;
+  if (pre) {
+    if (d->pre_w == nullptr || d->pre_b == nullptr || d->pre_gamma == nullptr || d->pre_beta == nullptr ||
+        d->pre_att_row_stride < kD || (d->pre_att_row_stride & 7) || d->pre_att == d->out)
+      return FS2_EINVAL;
+    if (d->rows_dev == nullptr || S != 1 || d->tile_rows == 64 || d->KS != 9 || d->F != 1024) return FS2_EUNSUPPORTED;
+    const int64_t ab = M64 * d->pre_att_row_stride * 2;
+    if (ab >= (1LL << 31)) return FS2_EUNSUPPORTED;
+    p.att = reinterpret_cast<const bf16 *>(d->pre_att);
+    p.as = d->pre_att_row_stride;
+    p.att_bytes = (uint32_t)ab;
+    p.wfc = reinterpret_cast<const bf16 *>(d->pre_w);
+    p.bfc = d->pre_b;
+    p.g1 = d->pre_gamma;
+    p.be1 = d->pre_beta;
+    p.eps1 = d->pre_eps;
+  }
   if (d->rows_max < 0 || !(d->tile_rows == 0 || d->tile_rows == 112 || d->tile_rows == 64)) return FS2_EINVAL;
   const int MB = d->tile_rows == 64 ? 4 : 7, BM = 16 * MB;
   const int64_t kPartBytes = part_bytes(MB);
@@ -831,7 +994,9 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   using I3 = std::integral_constant<int, 3>;
   using C4 = std::integral_constant<int, 4>;
   using C2 = std::integral_constant<int, 2>;
-  if (d->KS == 9 && nch == 4)
+  if (pre)
+    hipLaunchKernelGGL((ffn_fused_kernel<9, 4, 7, true>), dim3(nwg), dim3(256), 0, s, p);
+  else if (d->KS == 9 && nch == 4)
     go(I9{}, C4{});
   else if (d->KS == 9 && nch == 2)
     go(I9{}, C2{});

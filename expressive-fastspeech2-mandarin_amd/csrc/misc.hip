@@ -85,6 +85,7 @@ __global__ __launch_bounds__(256) void cond_kernel(const int64_t *speakers, cons
     const float *wr = lin_w + (int64_t)n * dc;
     if ((dc & 15) == 0) {
       const int kper = dc >> 2, k0 = kq * kper;
+#pragma unroll 16
       for (int k = k0; k < k0 + kper; k += 4) {
         const float4 wv = *reinterpret_cast<const float4 *>(wr + k);
 #pragma unroll

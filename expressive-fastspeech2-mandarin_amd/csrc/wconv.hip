@@ -63,6 +63,15 @@ __device__ __forceinline__ void static_for(Fn &&f) {
 
 constexpr int kLgkm0 = 0xC07F;  // s_waitcnt lgkmcnt(0) the compiler's wait-count pass sees
 
+// tanh for the bf16 epilogues: 1 - 2 / (1 + e^(2x)) with the hardware exp2 / reciprocal (5
+// instructions; libm tanhf is ~35 with its range branches, and the PostNet epilogues evaluate
+// 57k of them per workgroup). |error| <= ~2e-7 absolute: far below the bf16 rounding of the result;
+// saturates to +-1 (e^(2x) = inf -> 1, 0 -> -1).
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // 2 log2(e)
+  return fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + e), 1.0f);
+}
+
 // CIN % 32 != 0 (the PostNet's first conv, 80 -> 512): the K dimension is (tap, channel) flattened,
 // k = tap * CIN + c, in 32-wide steps ("flat" units); a lane group's 8 consecutive k stay inside one
 // tap (CIN % 8 == 0), so each lane addresses its own (row + tap, channel) per unit.
@@ -245,10 +254,10 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
     for (int mb = 0; mb < MB; ++mb) {
       const f32x4 v = acc[nb][mb];
       bf16x4 o;
-      o[0] = (bf16)tanhf(v[0] + bb.x);
-      o[1] = (bf16)tanhf(v[1] + bb.y);
-      o[2] = (bf16)tanhf(v[2] + bb.z);
-      o[3] = (bf16)tanhf(v[3] + bb.w);
+      o[0] = (bf16)tanh_fast(v[0] + bb.x);
+      o[1] = (bf16)tanh_fast(v[1] + bb.y);
+      o[2] = (bf16)tanh_fast(v[2] + bb.z);
+      o[3] = (bf16)tanh_fast(v[3] + bb.w);
       *reinterpret_cast<bf16x4 *>(smem + X_OFF + (hrow0 + mb * 16) * OPITCH + n * 2) = o;
     }
   }
@@ -417,10 +426,10 @@ __global__ __launch_bounds__(512, 1) void pn_head_kernel(PnHeadArgs p) {
         const int r = (4 * ps + mb) * 16 + hrow0;
         const f32x4 v = acc[jb][mb];
         bf16x4 o;
-        o[0] = (bf16)tanhf(v[0] + bb.x);
-        o[1] = (bf16)tanhf(v[1] + bb.y);
-        o[2] = (bf16)tanhf(v[2] + bb.z);
-        o[3] = (bf16)tanhf(v[3] + bb.w);
+        o[0] = (bf16)tanh_fast(v[0] + bb.x);
+        o[1] = (bf16)tanh_fast(v[1] + bb.y);
+        o[2] = (bf16)tanh_fast(v[2] + bb.z);
+        o[3] = (bf16)tanh_fast(v[3] + bb.w);
         if (r < YR) *reinterpret_cast<bf16x4 *>(smem + Y_OFF + r * YPITCH + n * 2) = o;
       }
     }
@@ -494,10 +503,10 @@ __global__ __launch_bounds__(512, 1) void pn_head_kernel(PnHeadArgs p) {
     for (int mb = 0; mb < MB; ++mb) {
       const f32x4 v = acc[nb][mb];
       bf16x4 o;
-      o[0] = (bf16)tanhf(v[0] + bb.x);
-      o[1] = (bf16)tanhf(v[1] + bb.y);
-      o[2] = (bf16)tanhf(v[2] + bb.z);
-      o[3] = (bf16)tanhf(v[3] + bb.w);
+      o[0] = (bf16)tanh_fast(v[0] + bb.x);
+      o[1] = (bf16)tanh_fast(v[1] + bb.y);
+      o[2] = (bf16)tanh_fast(v[2] + bb.z);
+      o[3] = (bf16)tanh_fast(v[3] + bb.w);
       *reinterpret_cast<bf16x4 *>(smem + Y_OFF + (hrow0 + mb * 16) * OPITCH + n * 2) = o;
     }
   }

@@ -75,6 +75,8 @@ class FfnDesc(ctypes.Structure):
         ("nsplit", _i), ("splitk_ws", _p), ("splitk_ws_bytes", _i64), ("rows_max", _i),
         ("tile_rows", _i),
         ("wqkv", _p), ("bqkv", _p), ("qkv_out", _p), ("qkv_row_stride", _i64), ("nqkv", _i),
+        ("pre_att", _p), ("pre_att_row_stride", _i64), ("pre_w", _p), ("pre_b", _p), ("pre_gamma", _p),
+        ("pre_beta", _p), ("pre_eps", _f),
     ]
 
 

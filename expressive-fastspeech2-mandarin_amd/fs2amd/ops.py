@@ -467,15 +467,30 @@ def pack_frag_rows(w):
     return b.reshape(-1).to(torch.bfloat16).contiguous()
 
 
+def ffn_launch_rows(x, layout):
+    """The row count an fs2_ffn launch is sized for (the host's bound when it knows one)."""
+    if layout is None:
+        return x.shape[0] * x.shape[1]
+    return getattr(layout, "rows_hint", None) or layout.capacity
+
+
+def ffn_pre_ok(x, layout, F, ks):
+    """fs2_ffn's fc + residual + LN prologue (pre_att) covers packed 112-row, unsplit launches of the
+    k = 9, F = 1024 FFN (the decoder's)."""
+    return layout is not None and ks == 9 and F == 1024 and ffn_form(ffn_launch_rows(x, layout), F) == (112, 1)
+
+
 def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=None, layout=None, out=None,
-        nsplit=None, tile_rows=None, next_qkv=None):
+        nsplit=None, tile_rows=None, next_qkv=None, pre=None):
     """PositionwiseFeedForward + residual + LayerNorm + mask in one launch (fs2_ffn): bf16 rows of
     256 (padded [B, T, 256] or packed [B*T, 256] in ``layout``); ``w_packed`` from
     :func:`pack_ffn_weights`. The hidden [rows, F] never reaches HBM. ``tile_rows`` (112 / 64) and
     ``nsplit`` (workgroups per row tile): None = :func:`ffn_form` of the row count the host knows
     (``layout.rows_hint`` or the capacity). ``next_qkv`` = (wqkv in :func:`pack_frag_rows` order,
     bqkv f32): the epilogue also projects the output rows to the next block's Q|K|V; returns
-    (out, qkv) then (qkv None otherwise)."""
+    (out, qkv) then (qkv None otherwise). ``pre`` = (att, wfc in :func:`pack_frag_rows` order, bfc,
+    (gamma1, beta1, eps1)): x is the FFT block's input and the FFN input h = LN1(att wfc^T + bfc + x)
+    is computed in the launch's prologue (:func:`ffn_pre_ok` forms only)."""
     _gpu(x, w_packed, b1, b2, lens, addvec1, addvec2)
     if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
         raise TypeError("fs2amd.ffn: bf16 activations and weights only")
@@ -505,7 +520,7 @@ def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=No
     if out is None:
         out = torch.empty_like(x)
     d.out, d.out_row_stride = out.data_ptr(), _rows(out, "out")
-    rows = (getattr(layout, "rows_hint", None) or layout.capacity) if layout is not None else B * T
+    rows = ffn_launch_rows(x, layout)
     if layout is not None and rows < layout.capacity:
         d.rows_max = int(rows)  # free-running: the active rows from the one host read
     tr, ns = ffn_form(rows, F)
@@ -526,6 +541,13 @@ def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=No
         assert wq.is_contiguous() and wq.numel() == nq * D, (tuple(wq.shape), nq, D)
         qkv = torch.empty(*x.shape[:-1], nq, device=x.device, dtype=torch.bfloat16)
         d.wqkv, d.bqkv, d.qkv_out, d.qkv_row_stride, d.nqkv = wq.data_ptr(), bq.data_ptr(), qkv.data_ptr(), nq, nq
+    if pre is not None:
+        att, wfc, bfc, (g1, b1n, eps1) = pre
+        _gpu(att, wfc, bfc, g1, b1n)
+        assert att.shape == x.shape and att.dtype == torch.bfloat16 and wfc.numel() == D * D
+        d.pre_att, d.pre_att_row_stride = att.data_ptr(), _rows(att, "att")
+        d.pre_w, d.pre_b, d.pre_gamma, d.pre_beta, d.pre_eps = wfc.data_ptr(), bfc.data_ptr(), g1.data_ptr(), \
+            b1n.data_ptr(), float(eps1)
     L.check(_lib.fs2_ffn(ctypes.byref(d), _stream(x)), "fs2_ffn")
     return (out, qkv) if next_qkv is not None else out
 

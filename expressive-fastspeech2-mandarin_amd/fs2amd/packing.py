@@ -58,6 +58,9 @@ def _fft_layer(layer, device, compute, key=None, fp8_scales=None):
         # Q|K|V in fragment order for the previous block's fused FFN epilogue (fs2_ffn wqkv)
         wqf=pack_frag_rows(wqkv) if compute == L.FS2_BF16 and wqkv.shape[0] % 256 == 0 and wqkv.shape[1] == 256
         else None,
+        # the attention output projection in fragment order for the fused FFN's prologue (fs2_ffn pre_w)
+        wfcf=pack_frag_rows(a.fc.weight.to(device)) if compute == L.FS2_BF16 and tuple(a.fc.weight.shape) == (256, 256)
+        else None,
     )
 
 

@@ -97,6 +97,22 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
     att = ops.attention(qkv, lens, H, dk, float(np.power(dk, 0.5)), layout=layout)
     # cfg5: the fc+LN epilogue also writes the fp8 copy of h the e4m3 k=9 conv reads (one launch)
     h8 = None
+    if q is None and getattr(lp, "wfcf", None) is not None and CALIB is None and ffn_pre_on() and \
+            ffn_fused_ok(P, lp, x, layout) and ops.ffn_pre_ok(x, layout, lp.b1.numel(), lp.k1):
+        # fc + residual + LN (SubLayers.py:54-55) in the fused FFN's prologue: no h round trip,
+        # one launch less per block (the decoder's packed 112-row launches)
+        if timed and TIMERS is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        fuse_qkv = nxt is not None and getattr(nxt, "wqf", None) is not None and \
+            (nxt.fp8 is None or nxt.fp8.wqkv is None) and qkv_fused_on()
+        r = ops.ffn(x, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, layout=layout,
+                    next_qkv=(nxt.wqf, nxt.bqkv) if fuse_qkv else None, pre=(att, lp.wfcf, lp.bfc, lp.ln1))
+        y, qn = r if fuse_qkv else (r, None)
+        if timed and TIMERS is not None:
+            e1.record()
+            TIMERS.append((e0, e1, "fc+ffn+qkv" if fuse_qkv else "fc+ffn"))
+        return y, None, qn
     if q is not None:
         h8 = (layout.empty(d_model, torch.float8_e4m3fn) if layout is not None
               else torch.empty(*x.shape[:-1], d_model, device=x.device, dtype=torch.float8_e4m3fn))
@@ -151,6 +167,11 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
 
 FFN_FUSED_MIN_ROWS = 16384
 FFN_SPLIT_MIN_WG = 128
+
+
+def ffn_pre_on():
+    """FS2_FFN_PRE=0: the attention output projection + LN as its own fs2_conv1d launch (A/B)."""
+    return os.environ.get("FS2_FFN_PRE", "1") != "0"
 
 
 def qkv_fused_on():

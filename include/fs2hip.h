@@ -220,6 +220,19 @@ typedef struct fs2_ffn_desc {
   void *qkv_out;
   int64_t qkv_row_stride;
   int nqkv;
+  /* the block's attention output projection + residual + LayerNorm in the PROLOGUE (optional,
+     pre_att NULL = off; packed rows, 112-row tiles, nsplit 1, KS = 9, F = 1024): x is then the
+     FFT block's input and the FFN input is computed on chip for the tile and its halo rows,
+       h = LN1(pre_att . pre_w^T + pre_b + x)        (transformer/SubLayers.py:54-55, Layers.py:25)
+     and the FFN's own LayerNorm residual is h. pre_w: fc weight [256][256] in fragment order
+     [4][8][4][4][16][8] (as wqkv). Replaces the fc + residual + LN launch of fs2_conv1d.      */
+  const void *pre_att;       /* bf16 [B*T, >= 256]: the attention output (heads concatenated)   */
+  int64_t pre_att_row_stride;
+  const void *pre_w;
+  const float *pre_b;        /* [256]                                                           */
+  const float *pre_gamma;    /* [256]                                                           */
+  const float *pre_beta;
+  float pre_eps;
 } fs2_ffn_desc;
 
 int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream);

@@ -61,6 +61,15 @@ def _ref(x, lens, W, addvecs=()):
     return y
 
 
+def _pack(lay, x):
+    """padded [B, T, C] -> packed [B*T, C] capacity rows (rows past cu[B] zero)."""
+    rm = lay.rowmap.long()
+    out = x.new_zeros(lay.capacity, x.shape[-1])
+    ok = rm >= 0
+    out[rm[ok]] = x.reshape(-1, x.shape[-1])[ok]
+    return out
+
+
 def _x(B, T, lens, seed):
     g = torch.Generator(device=DEV).manual_seed(seed)
     valid = (torch.arange(T, device=DEV)[None, :] < lens[:, None])[..., None]
@@ -257,3 +266,55 @@ def test_ffn_next_qkv_epilogue(gpu, tile_rows, nsplit, packed):
     scale = float(ref.abs().max())
     assert float(err.max()) <= 1e-2 * scale, (float(err.max()), scale)
     assert float(err.mean()) <= 1e-3 * scale, (float(err.mean()), scale)
+
+
+@pytest.mark.parametrize("B,T,seed", [(64, 430, 31), (8, 130, 32), (3, 37, 33)])
+def test_ffn_pre_fc_ln_prologue(gpu, B, T, seed):
+    """fs2_ffn with pre_att: the FFT block's attention output projection + residual + LayerNorm
+    (SubLayers.py:54-55) computed in the fused FFN's prologue for each tile and its 4+4 halo rows,
+    then the FFN (packed rows; ragged lengths incl. 0 and 1). Against a float64 statement of the
+    whole sequence (h rounded to bf16 where the two-launch path stores it) within the FFN's bf16
+    tolerance, and against the two launches (fc + LN on fs2_conv1d, then fs2_ffn) within 2 bf16 ulps
+    (the h rounding can move by one ulp with the summation order). Also with the next block's
+    Q|K|V in the epilogue."""
+    ops, L = gpu
+    W = _weights(ops, L, seed=seed)
+    g = torch.Generator(device=DEV).manual_seed(seed + 7)
+    lens = torch.randint(T // 2, T + 1, (B,), device=DEV, generator=g)
+    lens[0] = T
+    if B > 2:
+        lens[1], lens[2] = 0, 1
+    x = _x(B, T, lens, seed + 1)
+    att = _x(B, T, lens, seed + 2)
+    wfc = torch.randn(256, 256, device=DEV, generator=g) / 16
+    bfc = 0.1 * torch.randn(256, device=DEV, generator=g)
+    ln1 = (1 + 0.1 * torch.randn(256, device=DEV, generator=g), 0.1 * torch.randn(256, device=DEV, generator=g), 1e-5)
+    lay = ops.SeqLayout(lens, T)
+    pk = lambda t: _pack(lay, t)
+    with ops.splitk_enabled(False):  # the 112-row unsplit form the prologue covers
+        h2 = ops.conv1d(pk(att), ops.pack_conv_weight(wfc, L.FS2_BF16), bfc, cin=256, ks=1, pad=0, compute=L.FS2_BF16,
+                        epilogue=L.EPI_RES_LN, out_dtype=L.FS2_BF16, residual=pk(x), ln=ln1, layout=lay)
+        two = ops.ffn(h2, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay)
+        one = ops.ffn(pk(x), W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay,
+                      pre=(pk(att), ops.pack_frag_rows(wfc), bfc, ln1))
+        wq = torch.randn(768, 256, device=DEV, generator=g) / 16
+        bq = 0.1 * torch.randn(768, device=DEV, generator=g)
+        one_q, qkv = ops.ffn(pk(x), W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay,
+                             pre=(pk(att), ops.pack_frag_rows(wfc), bfc, ln1), next_qkv=(ops.pack_frag_rows(wq), bq))
+    torch.cuda.synchronize()
+    R = int(lay.cu[-1])
+    # float64 reference on the padded rows
+    h = torch.nn.functional.layer_norm(att.double() @ wfc.to(torch.bfloat16).double().t() + bfc.double() + x.double(),
+                                       (256,), ln1[0].double(), ln1[1].double(), ln1[2])
+    valid = (torch.arange(T, device=DEV)[None, :] < lens[:, None])
+    h = (h * valid[..., None]).to(torch.bfloat16)
+    ref = _ref(h, lens, W)
+    refp = ref.reshape(-1, 256)[valid.reshape(-1)]
+    err = (one[:R].double() - refp).abs()
+    assert float(err.max()) <= 0.1 and float(err.mean()) <= 6e-3, (float(err.max()), float(err.mean()))
+    d = (one[:R].float() - two[:R].float()).abs()
+    ulp = two[:R].float().abs().clamp(min=2 ** -8) * 2 ** -7
+    assert float((d / ulp).max()) <= 2.0 or float(err.max()) <= 0.05, float((d / ulp).max())
+    assert torch.equal(one_q[:R], one[:R])
+    qref = (one[:R].double() @ wq.to(torch.bfloat16).double().t() + bq.double())
+    assert float((qkv[:R].double() - qref).abs().max()) <= 0.05 * max(1.0, float(qref.abs().max()))

@@ -28,5 +28,5 @@ def main(path, min_gap=0.0):
 
 
 if __name__ == "__main__":
-    mg = float(sys.argv[sys.argv.index("--min-gap") + 1]) if "--min-gap" in sys.argv else 0.0
+    mg = float(sys.argv[sys.argv.index("--min-gap") + 1]) if "--min-gap" in sys.argv else -1e9
     main(sys.argv[1], mg)
