@@ -50,6 +50,19 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class Ffn8Desc(ctypes.Structure):
+    """Mirror of ``fs2_ffn8_desc`` (include/fs2hip.h)."""
+
+    _fields_ = [
+        ("x8", _p), ("x8_row_stride", _i64), ("res", _p), ("res_row_stride", _i64), ("w", _p),
+        ("cs1", _p), ("b1", _p), ("inv_sf", _f), ("cs2", _p), ("b2", _p),
+        ("B", _i), ("T", _i), ("D", _i), ("F", _i), ("KS", _i), ("pad", _i),
+        ("ln_gamma", _p), ("ln_beta", _p), ("ln_eps", _f),
+        ("out", _p), ("out_row_stride", _i64), ("out8", _p), ("out8_row_stride", _i64), ("out8_scale", _f),
+        ("rows_dev", _p), ("row_pos", _p), ("rows_max", _i),
+    ]
+
+
 class WconvDesc(ctypes.Structure):
     """Mirror of ``fs2_wconv_desc`` (include/fs2hip.h)."""
 
@@ -99,6 +112,8 @@ SIGNATURES = {
     "fs2_conv1d": (_i, [ctypes.POINTER(ConvDesc), _p]),
     "fs2_ffn": (_i, [ctypes.POINTER(FfnDesc), _p]),
     "fs2_ffn_weight_elems": (ctypes.c_int64, [_i, _i]),
+    "fs2_ffn8": (_i, [ctypes.POINTER(Ffn8Desc), _p]),
+    "fs2_ffn8_weight_bytes": (ctypes.c_int64, [_i, _i]),
     "fs2_wconv": (_i, [ctypes.POINTER(WconvDesc), _p]),
     "fs2_wconv_weight_elems": (ctypes.c_int64, [_i, _i, _i]),
     "fs2_attention": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p]),

@@ -313,6 +313,46 @@ def pack_ffn_weights(w1, w2):
     return torch.cat([a.reshape(-1), b.reshape(-1)]).to(torch.bfloat16).contiguous()
 
 
+def pack_ffn8_weights(q1, q2):
+    """The e4m3 FFN pair (pack_conv_weight_fp8 outputs: q1 [F, KS, 256], q2 [256, 1, F]) -> the
+    fs2_ffn8 byte buffer: 8 KiB units of 64 rows x 128 k, each lane's 32 bytes as two 16-byte halves
+    (include/fs2hip.h: [q][u][b][h][g][r][e], element = W[64q + 16b + r][128u + 32g + 16h + e])."""
+    F, KS, D = q1.shape
+    assert q2.shape[0] == D and q2.shape[-1] == F and D % 128 == 0 and F % 128 == 0, (tuple(q1.shape), tuple(q2.shape))
+    perm = (0, 3, 1, 5, 4, 2, 6)
+    b1 = q1.contiguous().view(torch.uint8).reshape(F // 64, 4, 16, KS * D // 128, 4, 2, 16).permute(*perm)
+    b2 = q2.contiguous().view(torch.uint8).reshape(D // 64, 4, 16, F // 128, 4, 2, 16).permute(*perm)
+    return torch.cat([b1.reshape(-1), b2.reshape(-1)]).contiguous()
+
+
+def ffn8(x8, res, w8, cs1, b1, inv_sf, cs2, b2, *, ln, layout, out=None, out8=None, out8_scale=1.0, ks=9, pad=4):
+    """fs2_ffn8: the fused FFN on e4m3 MFMA (cfg5) over packed rows: x8 the e4m3 input [B*T, 256], res
+    the bf16 LayerNorm residual (the same rows), w8 from :func:`pack_ffn8_weights`; out bf16 and
+    optionally out8 = e4m3(out * out8_scale) (the next block's fp8 Q|K|V input)."""
+    _gpu(x8, res, w8, cs1, b1, cs2, b2)
+    assert layout is not None and x8.dim() == 2 and x8.shape[0] == layout.capacity and res.shape == x8.shape
+    F = b1.numel()
+    assert w8.numel() == _lib.fs2_ffn8_weight_bytes(ks, F)
+    if out is None:
+        out = torch.empty(res.shape, device=res.device, dtype=torch.bfloat16)
+    d = L.Ffn8Desc()
+    d.x8, d.x8_row_stride = x8.data_ptr(), _rows(x8, "x8")
+    d.res, d.res_row_stride = res.data_ptr(), _rows(res, "res")
+    d.w, d.cs1, d.b1, d.inv_sf, d.cs2, d.b2 = w8.data_ptr(), cs1.data_ptr(), b1.data_ptr(), float(inv_sf), \
+        cs2.data_ptr(), b2.data_ptr()
+    d.B, d.T, d.D, d.F, d.KS, d.pad = layout.B, layout.T, x8.shape[1], F, ks, pad
+    g, b, eps = ln
+    d.ln_gamma, d.ln_beta, d.ln_eps = g.data_ptr(), b.data_ptr(), float(eps)
+    d.out, d.out_row_stride = out.data_ptr(), _rows(out, "out")
+    if out8 is not None:
+        d.out8, d.out8_row_stride, d.out8_scale = out8.data_ptr(), _rows(out8, "out8"), float(out8_scale)
+    d.rows_dev, d.row_pos = layout.rows_dev, layout.row_pos.data_ptr()
+    hint = getattr(layout, "rows_hint", None)
+    d.rows_max = int(hint) if hint else 0
+    L.check(_lib.fs2_ffn8(ctypes.byref(d), _stream(x8)), "fs2_ffn8")
+    return out
+
+
 def pack_wconv_weight(w, scale=None):
     """nn.Conv1d weight [N, Cin, KS] (optionally scaled per output channel: BatchNorm folding, in
     f32 then rounded once like pack_conv_weight) -> the fs2_wconv buffer: K = (tap, channel)

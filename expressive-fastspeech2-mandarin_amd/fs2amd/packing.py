@@ -20,8 +20,8 @@ from types import SimpleNamespace
 import torch
 
 from . import _lib as L
-from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split, pack_ffn_weights, pack_frag_rows, \
-    pack_vp_fused, pack_wconv_tail, pack_wconv_weight
+from .ops import FP8_MAX, pack_conv_weight, pack_conv_weight_fp8, pack_conv_weight_split, pack_ffn8_weights, \
+    pack_ffn_weights, pack_frag_rows, pack_vp_fused, pack_wconv_tail, pack_wconv_weight
 
 
 def _f32(t, device):
@@ -39,7 +39,9 @@ def _fft_layer(layer, device, compute, key=None, fp8_scales=None):
         w1, sw1 = pack_conv_weight_fp8(f.w_1.weight.to(device))
         w2, sw2 = pack_conv_weight_fp8(f.w_2.weight.to(device))
         fp8 = SimpleNamespace(s_h=s_h, s_f=s_f, s_x=s_x, w1=w1, w2=w2, cs1=(sw1 * s_h).contiguous(),
-                              cs2=(sw2 * s_f).contiguous(), wqkv=None, cs_qkv=None)
+                              cs2=(sw2 * s_f).contiguous(), wqkv=None, cs_qkv=None, w12_8=None)
+        if tuple(w1.shape) == (1024, 9, 256) and w2.shape[0] == 256 and w2.shape[-1] == 1024:
+            fp8.w12_8 = pack_ffn8_weights(w1, w2)  # the fused e4m3 FFN (fs2_ffn8)
         if key[1] > 0:  # input produced by the previous block's LN epilogue, which writes the fp8 copy
             wq, swq = pack_conv_weight_fp8(wqkv)
             fp8.wqkv, fp8.cs_qkv = wq, (swq * s_x).contiguous()

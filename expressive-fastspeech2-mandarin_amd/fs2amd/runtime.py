@@ -119,6 +119,19 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
     h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
                    residual=x, ln=lp.ln1, lens=lens, layout=layout, out2=h8,
                    out2_scale=1.0 / q.s_h if q is not None else 1.0)
+    if q is not None and layout is not None and getattr(q, "w12_8", None) is not None and ffn8_on() \
+            and CALIB is None and lp.k1 == 9 and lp.p1 == 4:
+        # cfg5: the whole FFN as ONE e4m3 launch (fs2_ffn8: hidden quantised on chip, never in HBM)
+        if timed and TIMERS is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        y8 = _fp8_like(x, layout, d_model) if next_s is not None else None
+        y = ops.ffn8(h8, h, q.w12_8, q.cs1, lp.b1, 1.0 / q.s_f, q.cs2, lp.b2, ln=lp.ln2, layout=layout, out8=y8,
+                     out8_scale=1.0 / next_s if next_s is not None else 1.0)
+        if timed and TIMERS is not None:
+            e1.record()
+            TIMERS.append((e0, e1, "ffn8"))
+        return y, y8, None
     if q is not None:
         # cfg5: the FFN pair on e4m3 MFMA; the k=9 epilogue writes relu(.) directly as fp8 for w_2
         if timed and TIMERS is not None:
@@ -167,6 +180,11 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
 
 FFN_FUSED_MIN_ROWS = 16384
 FFN_SPLIT_MIN_WG = 128
+
+
+def ffn8_on():
+    """FS2_FFN8=0: the cfg5 FFN as the two e4m3 fs2_conv1d launches (A/B)."""
+    return os.environ.get("FS2_FFN8", "1") != "0"
 
 
 def ffn_pre_on():

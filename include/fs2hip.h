@@ -239,6 +239,45 @@ int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream);
 int64_t fs2_ffn_weight_elems(int KS, int F); /* F*KS*256 + 256*F */
 
 /*
+ * fs2_ffn8 — the fused PositionwiseFeedForward + residual + LayerNorm on e4m3 MFMA (cfg5; the fp8
+ * form of fs2_ffn, v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales). Quantisation points
+ * and scales of the two-launch fp8 path (fs2_conv1d, FS2_FP8):
+ *   f[m, j] = e4m3( relu(sum_{tap,c} x8[m + tap - pad, c] w1q[j][c][tap] * cs1[j] + b1[j]) * inv_sf )
+ *   y[m, n] = LN( sum_j f[m, j] w2q[n][j] * cs2[n] + b2[n] + res[m, n] ),  out8 = e4m3(y * out8_scale)
+ * Packed rows only (fs2_seq_layout: rows_dev / row_pos), KS = 9, pad = 4, D = 256, F = 1024.
+ * w: fs2_ffn8_weight_bytes(KS, F) e4m3 bytes, w1 then w2, each in 8 KiB units of 64 rows x 128 k:
+ *   w1: [F/64][KS*2 units (tap, 128-channel step)][4 blocks][2 halves][4 g][16 r][16 e]
+ *   w2: [256/64][F/128 units][4 blocks][2 halves][4 g][16 r][16 e]
+ *   element (.., b, h, g, r, e) = W[64q + 16b + r][128u + 32g + 16h + e] (W1[j][tap*256 + c]).
+ */
+typedef struct fs2_ffn8_desc {
+  const void *x8;           /* e4m3 [B*T, >= 256]: the FFN input (fc + LN epilogue's fp8 copy)     */
+  int64_t x8_row_stride;
+  const void *res;          /* bf16 [B*T, >= 256]: the LayerNorm residual (the same h in bf16)     */
+  int64_t res_row_stride;
+  const void *w;
+  const float *cs1;         /* [F] dequantisation of GEMM1 (input scale x per-row weight scale)    */
+  const float *b1;          /* [F]                                                                */
+  float inv_sf;             /* 1 / the hidden's quantisation scale                                */
+  const float *cs2;         /* [D]                                                                */
+  const float *b2;
+  int B, T, D, F, KS, pad;
+  const float *ln_gamma, *ln_beta;
+  float ln_eps;
+  void *out;                /* bf16 [B*T, >= 256]                                                 */
+  int64_t out_row_stride;
+  void *out8;               /* optional e4m3 copy of out (the next block's Q|K|V input) or NULL    */
+  int64_t out8_row_stride;
+  float out8_scale;
+  const int32_t *rows_dev;
+  const int32_t *row_pos;
+  int rows_max;             /* as fs2_ffn                                                         */
+} fs2_ffn8_desc;
+
+int fs2_ffn8(const fs2_ffn8_desc *d, fs2_stream_t stream);
+int64_t fs2_ffn8_weight_bytes(int KS, int F);
+
+/*
  * fs2_wconv — a PostNet convolution (transformer/Layers.py:92-137: Conv1d(512, 512, k=5, pad=2) +
  * BatchNorm1d (eval: folded into w / bias on the host) + tanh) on padded [B, T] rows:
  *   y[m, n] = tanh( sum_{k<KS} sum_c x[m + k - pad, c] * w[n][c][k] + bias[n] )   (per-sequence zero taps)

@@ -127,3 +127,52 @@ def test_fp8_model_vs_bf16_reported(gpu):
           f"mel max {float(mel_err.max()):.4f} mean {float(mel_err.mean()):.5f}")
     assert float(err.mean()) <= 0.1 and float(err.max()) <= 1.0
     assert torch.equal(got[9], ref[9])
+
+
+@pytest.mark.parametrize("B,T,seed", [(64, 430, 1), (8, 130, 2), (3, 37, 3)])
+def test_ffn8_fused_matches_two_launches(gpu, B, T, seed):
+    """fs2_ffn8 (the whole cfg5 FFN in one e4m3 launch: hidden quantised e4m3(relu(.) / s_f) on chip)
+    against the two fp8 fs2_conv1d launches it replaces (same quantised operands, same quantisation
+    points and scales; only the f32 summation order of the k=9 product differs, which can move a
+    hidden value across an e4m3 rounding boundary): max |d| <= 0.03, mean <= 1e-3 on the LN output
+    (O(1)); packed ragged rows incl. lengths 1 and < the tap reach. The e4m3 copy of the output is
+    e4m3(y * scale) of the kernel's own y within one e4m3 step."""
+    ops, L = gpu
+    g = torch.Generator().manual_seed(seed)
+    lens = torch.randint(1, T + 1, (B,), generator=g)
+    lens[0] = T
+    if B > 2:
+        lens[1], lens[2] = 1, 3
+    w1 = torch.randn(1024, 256, 9, generator=g) / (256 * 9) ** 0.5
+    w2 = torch.randn(256, 1024, 1, generator=g) / 1024 ** 0.5
+    b1 = (0.1 * torch.randn(1024, generator=g)).to(DEV)
+    b2 = (0.1 * torch.randn(256, generator=g)).to(DEV)
+    ln = ((1 + 0.1 * torch.randn(256, generator=g)).to(DEV), (0.1 * torch.randn(256, generator=g)).to(DEV), 1e-5)
+    q1, sw1 = ops.pack_conv_weight_fp8(w1.to(DEV))
+    q2, sw2 = ops.pack_conv_weight_fp8(w2.to(DEV))
+    lay = ops.SeqLayout(lens.to(DEV), T)
+    R = int(lay.cu[-1])
+    h = torch.zeros(B * T, 256)
+    h[:R] = torch.randn(R, 256, generator=g)
+    h = h.to(DEV).to(torch.bfloat16)
+    s_h = float(h.float().abs().max()) / 448.0
+    h8 = (h.float() / s_h).clamp(-448, 448).to(torch.float8_e4m3fn)
+    cs1 = (sw1 * s_h).contiguous()
+    # hidden scale from the two-launch path's own f32 hidden (as calibrate_fp8 does)
+    f32 = ops.conv1d(h8, q1, b1, cin=256, ks=9, pad=4, compute=L.FS2_FP8, epilogue=L.EPI_BIAS_RELU,
+                     out_dtype=L.FS2_F32, col_scale=cs1, layout=lay)
+    s_f = float(f32[:R].abs().max()) / 448.0
+    cs2 = (sw2 * s_f).contiguous()
+    f8 = ops.conv1d(h8, q1, b1, cin=256, ks=9, pad=4, compute=L.FS2_FP8, epilogue=L.EPI_BIAS_RELU,
+                    out_dtype=L.FS2_FP8, out_scale=1.0 / s_f, col_scale=cs1, layout=lay)
+    two = ops.conv1d(f8, q2, b2, cin=1024, ks=1, pad=0, compute=L.FS2_FP8, epilogue=L.EPI_RES_LN,
+                     out_dtype=L.FS2_BF16, residual=h, ln=ln, layout=lay, col_scale=cs2)
+    y8 = torch.empty(B * T, 256, device=DEV, dtype=torch.float8_e4m3fn)
+    one = ops.ffn8(h8, h, ops.pack_ffn8_weights(q1, q2), cs1, b1, 1.0 / s_f, cs2, b2, ln=ln, layout=lay, out8=y8,
+                   out8_scale=0.5)
+    torch.cuda.synchronize()
+    d = (one[:R].float() - two[:R].float()).abs()
+    assert float(d.max()) <= 0.03 and float(d.mean()) <= 1e-3, (float(d.max()), float(d.mean()))
+    ref8 = one[:R].float() * 0.5
+    e8 = (y8[:R].float() - ref8).abs()
+    assert bool((e8 <= 0.07 * ref8.abs() + 2 ** -9).all()), float((e8 - 0.07 * ref8.abs()).max())
