@@ -499,8 +499,20 @@ def extra_workloads(model, args, rank, device):
         cal = synth_batch(args.batch, args.phonemes, seed=1000 + rank)
         model.set_precision("fp8")
         model.calibrate_fp8(**to_device(cal, device))
-        record("cfg5_fp8", synth_batch(args.batch, args.phonemes, seed=1 + rank), True,
+        b5 = synth_batch(args.batch, args.phonemes, seed=1 + rank)
+        record("cfg5_fp8", b5, True,
                "cfg2 with e4m3 FFN + Q|K|V GEMMs (static calibrated scales); tolerance vs bf16 in tests/test_gpu_fp8.py")
+        # the fused e4m3 FFN (fs2_ffn8) against the dense fp8 peak: HIP events around its launches in
+        # eager forwards (all 6 decoder blocks)
+        t8 = time_kernel_in_forward(model, to_device(b5, device))
+        if "ffn8" in t8:
+            s8, n8 = t8["ffn8"]
+            fl8 = 2.0 * int(b5["mel_lens"].sum()) * (256 * 9 * 1024 + 1024 * 256)
+            res["cfg5_fp8"]["roofline"] = {
+                "bound": "mfma", "kernel": "ffn8_fused_kernel (decoder FFN, e4m3 v_mfma_scale_f32_16x16x128_f8f6f4)",
+                "achieved": round(fl8 / s8 / 1e12, 2), "peak": FP8_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(fl8 / s8 / 1e12 / FP8_PEAK_TFLOPS, 4), "kernel_ms": round(s8 * 1e3, 4),
+                "launches_timed": n8, "flops_per_launch": fl8}
         model.set_precision(prec)
     if args.vocoder:
         res["vocoder_cfg2"] = vocoder_workload(model, args, rank, device, steps)
