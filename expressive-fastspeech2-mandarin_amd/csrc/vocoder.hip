@@ -1,0 +1,308 @@
+// HiFi-GAN V1 multi-receptive-field fusion (hifigan/models.py:20-45 ResBlock1 + :152-158) as ONE
+// kernel per upsampling stage, for the narrow late stages (C = 64, 32 channels):
+//
+//   xs = sum_{k in (3, 7, 11)} ResBlock_k(x);   out = leaky_relu(xs / 3, slope)
+//   ResBlock_k(x): for d in (1, 3, 5):  x = conv_k,1(lrelu(conv_k,d(lrelu(x)) + b1)) + b2 + x
+//
+// As 18 separate conv launches per stage each conv read and wrote a [B, T*128 or *256, C] tensor
+// (451 MB at cfg2) with C = 32 / 64 filling an MFMA tile's N side a quarter / half: stages 3 and 4
+// took 11.2 and 15.5 ms of a 43 ms vocoder call. Here a workgroup owns L = 256 output samples of
+// one utterance and runs all 18 convs on chip: the input tile with a 64-sample halo (each k chain
+// reaches 6 (k - 1) <= 60 samples) is DMA'd to LDS, the chains' intermediates never leave the CU,
+// and only lrelu(xs / 3) is written (the next upsampler's / conv_post's input).
+//
+// * Conv step = implicit GEMM D[ch][row] = sum_{tap, c} W[ch][c][tap] . IN[row + (tap - hk) d][c]:
+//   weights are the MFMA A operand (16-channel blocks, fragment-ordered, read from L2/L1 one k-step
+//   ahead), activations the B operand from LDS; output rows in 16-row blocks dealt round-robin to
+//   the 4 waves. Each step computes only the rows later steps need (the halo shrinks along the chain).
+// * LDS: three [384 rows x C] bf16 buffers -- CUR (the chain's running x), ACT (lrelu(CUR)), T
+//   (lrelu(conv1 + b1)) -- with a row XOR swizzle on the 16-byte chunk (found by exhaustive search:
+//   the 16 rows x 16 bytes of a fragment read are conflict-free for any tap shift).
+// * Sequence edges: rows outside [0, T) are written as zeros after every step (nn.Conv1d's zero
+//   padding); the chains' sums xs stay in f32 registers (the last conv of each chain produces the
+//   same rows on the same waves).
+#include <type_traits>
+#include <utility>
+
+#include "conv_common.h"
+#include "fs2_common.h"
+
+namespace {
+
+constexpr int kMrfL = 256;              // output samples per workgroup
+constexpr int kMrfH = 64;               // halo rows each side (>= 6 (11 - 1) = 60)
+constexpr int kMrfR = kMrfL + 2 * kMrfH;  // 384 buffer rows
+constexpr int kMrfNB = kMrfR / 16;      // 24 row blocks
+constexpr int kMrfNBW = kMrfNB / 4;     // at most 6 blocks per wave
+constexpr int kMrfLgkm0 = 0xC07F;
+
+struct MrfArgs {
+  const bf16 *x;     // ups output [B, T, C]
+  const bf16 *a0;    // lrelu(x) [B, T, C] (the ups epilogue's second output)
+  const bf16 *w;     // 18 convs, fragment order (see mrf_woff)
+  const float *bias; // [18][C]
+  bf16 *out;         // lrelu(xs / 3, slope) [B, T, C]
+  int T, ntiles;     // samples per utterance, tiles per utterance
+  float slope;       // output leaky_relu slope (0.1 before an upsampler, 0.01 before conv_post)
+  uint32_t x_bytes;
+};
+
+template <typename Fn, int... I>
+__device__ __forceinline__ void mrf_static_for_impl(Fn &&f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void mrf_static_for(Fn &&f) {
+  mrf_static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// chunk swizzle of a C-channel bf16 row (C / 8 chunks of 16 bytes)
+template <int C>
+__device__ __forceinline__ int mrf_swz(int r) {
+  if constexpr (C == 32) return (r & 4) ? 2 : 0;
+  else return ((r & 2) ? 2 : 0) ^ ((r & 4) ? 4 : 0);
+}
+
+__device__ __forceinline__ float lrelu(float v, float s) { return v > 0.f ? v : v * s; }
+
+// element offset of conv (chain j, pair p, second) in the packed weights: per conv [k * C/32 k-steps]
+// [C/16 blocks][64 lanes][8]
+template <int C>
+__host__ __device__ constexpr int mrf_conv_elems(int k) { return k * C * C; }
+template <int C>
+__host__ __device__ constexpr int mrf_woff(int j, int p, int second) {
+  int off = 0;
+  const int ks[3] = {3, 7, 11};
+  for (int jj = 0; jj < j; ++jj) off += 6 * mrf_conv_elems<C>(ks[jj]);
+  return off + (2 * p + second) * mrf_conv_elems<C>(ks[j]);
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
+  constexpr int RB = C * 2;          // row bytes
+  constexpr int NCB = C / 16;        // channel blocks (MFMA A blocks)
+  constexpr int KC = C / 32;         // 32-channel k-steps per tap
+  constexpr int BUF = kMrfR * RB;
+  constexpr int CUR_OFF = 0, ACT_OFF = BUF, T_OFF = 2 * BUF;
+  constexpr int SMEM = 3 * BUF;
+  static_assert(SMEM <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int utt = blockIdx.y, tile = blockIdx.x;
+  const int T = p.T;
+  const int t0 = tile * kMrfL - kMrfH;  // global sample of buffer row 0
+  const int64_t ubase = (int64_t)utt * T;
+  const int r16 = lane & 15, g = lane >> 4;
+
+  // buffer row R holds sample t0 + R: inside the utterance?
+  auto inside = [&](int R) { return (unsigned)(t0 + R) < (unsigned)T; };
+
+  // ---- DMA of the chain input: CUR <- x, ACT <- lrelu(x) (rows outside [0, T): zeros)
+  const rsrc_t xr = make_rsrc(p.x, p.x_bytes), ar = make_rsrc(p.a0, p.x_bytes);
+  auto load_input = [&]() {
+    constexpr int RPP = 1024 / RB;  // rows per 1 KiB piece
+    constexpr int NP = BUF / 1024;
+#pragma unroll
+    for (int i = 0; i < (NP + 3) / 4; ++i) {
+      const int pc = w + 4 * i;
+      if (pc < NP) {
+        const int R = pc * RPP + lane / (RB / 16), phys = lane % (RB / 16);
+        const int logical = phys ^ mrf_swz<C>(R);
+        const uint32_t off = inside(R) ? (uint32_t)((ubase + t0 + R) * RB + logical * 16) : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)(smem + CUR_OFF + pc * 1024),
+                                                 16, off, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ar, (__attribute__((address_space(3))) void *)(smem + ACT_OFF + pc * 1024),
+                                                 16, off, 0, 0, 0);
+      }
+    }
+  };
+  auto sync = []() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // LDS byte address of (row R, 8-channel group q)
+  auto addr = [&](int buf, int R, int q) { return buf + R * RB + ((q ^ mrf_swz<C>(R)) << 4); };
+
+  f32x4 xs[4][NCB];  // the chains' sum over output rows [64, 320): blocks 4 + w + 4i
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) xs[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // one conv step: output blocks [blo, bhi), kernel K (taps), dilation D, input buffer IN;
+  // kind 0: T = lrelu(acc + b) ; 1: CUR = acc + b + CUR, ACT = lrelu(CUR) ; 2: xs += acc + b + CUR
+  auto step = [&](auto KC_, auto KIND_, int K, int D, int IN, const bf16 *wc, const float *bc, int blo, int bhi) {
+    constexpr int kind = decltype(KIND_)::value;
+    const int hk = (K - 1) / 2;
+    const rsrc_t wr = make_rsrc(wc, (uint32_t)(K * C * C * 2));
+    f32x4 acc[kMrfNBW][NCB];
+#pragma unroll
+    for (int i = 0; i < kMrfNBW; ++i)
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int first = blo + ((w - blo) % 4 + 4) % 4;  // this wave's first block (b = w mod 4)
+    const int nks = K * KC;
+    bf16x8 wa[2][NCB];
+    auto wload = [&](int s, bf16x8 (&f)[NCB]) {
+#pragma unroll
+      for (int c = 0; c < NCB; ++c)
+        f[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                              wr, (uint32_t)lane * 16u, (uint32_t)((s * NCB + c) * 1024), 0));
+    };
+    // k-step s with its weights in wc (loaded one step ahead into wn)
+    auto kstep = [&](int s, const bf16x8 (&wc)[NCB], bf16x8 (&wn)[NCB]) {
+      if (s + 1 < nks) {
+        wload(s + 1, wn);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCB) : "memory");  // this k-step's weights (the next may fly)
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      const int tap = s / KC, kc = s - tap * KC;
+      const int shift = (tap - hk) * D;
+#pragma unroll
+      for (int i = 0; i < kMrfNBW; ++i) {
+        const int b = first + 4 * i;
+        if (b < bhi) {  // wave-uniform
+          const int R = min(max(b * 16 + r16 + shift, 0), kMrfR - 1);
+          const bf16x8 fb = *reinterpret_cast<const bf16x8 *>(smem + addr(IN, R, 4 * kc + g));
+#pragma unroll
+          for (int c = 0; c < NCB; ++c)
+            acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc[c], fb, acc[i][c], 0, 0, 0);
+        }
+      }
+    };
+    wload(0, wa[0]);
+    int s = 0;
+    for (; s + 1 < nks; s += 2) {
+      kstep(s, wa[0], wa[1]);
+      kstep(s + 1, wa[1], wa[0]);
+    }
+    if (s < nks) kstep(s, wa[0], wa[1]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
+    __builtin_amdgcn_s_barrier();  // every wave done reading IN (and T may be rewritten)
+    // epilogue: lane holds channels 16c + 4g .. +3 of row 16b + r16
+#pragma unroll
+    for (int i = 0; i < kMrfNBW; ++i) {
+      const int b = first + 4 * i;
+      if (b < bhi) {
+        const int R = b * 16 + r16;
+        const bool in = inside(R);
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+          const int ch = 16 * c + 4 * g;
+          const float4 bb = *reinterpret_cast<const float4 *>(bc + ch);
+          f32x4 v = acc[i][c];
+          v[0] += bb.x;
+          v[1] += bb.y;
+          v[2] += bb.z;
+          v[3] += bb.w;
+          const int o = R * RB + (((ch >> 3) ^ mrf_swz<C>(R)) << 4) + (ch & 7) * 2;
+          if constexpr (kind == 0) {
+            bf16x4 t;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t[q] = (bf16)(in ? lrelu(v[q], 0.1f) : 0.f);
+            *reinterpret_cast<bf16x4 *>(smem + T_OFF + o) = t;
+          } else {
+            const bf16x4 xo = *reinterpret_cast<const bf16x4 *>(smem + CUR_OFF + o);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] += (float)xo[q];
+            if constexpr (kind == 1) {
+              bf16x4 nc, na;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                nc[q] = (bf16)(in ? v[q] : 0.f);
+                na[q] = (bf16)(in ? lrelu(v[q], 0.1f) : 0.f);
+              }
+              *reinterpret_cast<bf16x4 *>(smem + CUR_OFF + o) = nc;
+              *reinterpret_cast<bf16x4 *>(smem + ACT_OFF + o) = na;
+            } else if (i < 4) {
+              xs[i & 3][c] += v;  // the last conv of a chain: blocks 4 + w + 4i (i < 4), rows 64..319
+            }
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
+    __builtin_amdgcn_s_barrier();  // the step's output visible
+  };
+
+  const int ks[3] = {3, 7, 11};
+  mrf_static_for<3>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    const int K = ks[j], hk = (K - 1) / 2;
+    load_input();
+    sync();
+    const int dil[3] = {1, 3, 5};
+    // rows each step must produce: [64 - e, 320 + e) with e = 11hk, 10hk, 7hk, 6hk, hk, 0
+    const int e1[3] = {11 * hk, 7 * hk, hk}, e2[3] = {10 * hk, 6 * hk, 0};
+    mrf_static_for<3>([&](auto P) {
+      constexpr int pp = decltype(P)::value;
+      const bf16 *w1 = p.w + mrf_woff<C>(j, pp, 0), *w2 = p.w + mrf_woff<C>(j, pp, 1);
+      const float *b1 = p.bias + (j * 6 + 2 * pp) * C, *b2 = p.bias + (j * 6 + 2 * pp + 1) * C;
+      const int lo1 = (kMrfH - e1[pp]) / 16, hi1 = (kMrfH + kMrfL + e1[pp] + 15) / 16;
+      step(std::integral_constant<int, KC>{}, std::integral_constant<int, 0>{}, K, dil[pp], ACT_OFF, w1, b1, lo1, hi1);
+      const int lo2 = (kMrfH - e2[pp]) / 16, hi2 = (kMrfH + kMrfL + e2[pp] + 15) / 16;
+      if constexpr (pp < 2)
+        step(std::integral_constant<int, KC>{}, std::integral_constant<int, 1>{}, K, 1, T_OFF, w2, b2, lo2, hi2);
+      else
+        step(std::integral_constant<int, KC>{}, std::integral_constant<int, 2>{}, K, 1, T_OFF, w2, b2, lo2, hi2);
+    });
+  });
+
+  // ---- out = lrelu(xs / 3, slope) over the tile's 256 samples (blocks 4..19, 4 per wave)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = 4 + w + 4 * i;
+    const int R = b * 16 + r16, t = t0 + R;
+    if (t < T) {
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        const f32x4 v = xs[i][c];
+        bf16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (bf16)lrelu(v[q] * (1.0f / 3.0f), p.slope);
+        *reinterpret_cast<bf16x4 *>(p.out + (ubase + t) * C + 16 * c + 4 * g) = o;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t fs2_hifigan_mrf_weight_elems(int C) {
+  return C == 32 ? mrf_woff<32>(3, 0, 0) : C == 64 ? mrf_woff<64>(3, 0, 0) : C == 128 ? mrf_woff<128>(3, 0, 0) : -1;
+}
+
+extern "C" int fs2_hifigan_mrf(const void *x, const void *x_act, const void *w, const float *bias, int B, int T, int C,
+                               float out_slope, void *out, fs2_stream_t stream) {
+  if (x == nullptr || x_act == nullptr || w == nullptr || bias == nullptr || out == nullptr || B < 0 || T < 0)
+    return FS2_EINVAL;
+  if (!(C == 32 || C == 64)) return FS2_EUNSUPPORTED;
+  if (out == x || out == x_act) return FS2_EINVAL;  // other tiles re-read the input's halo rows
+  if (B == 0 || T == 0) return FS2_OK;
+  const int64_t bytes = (int64_t)B * T * C * 2;
+  if (bytes >= (1LL << 31)) return FS2_EUNSUPPORTED;
+  MrfArgs p;
+  p.x = reinterpret_cast<const bf16 *>(x);
+  p.a0 = reinterpret_cast<const bf16 *>(x_act);
+  p.w = reinterpret_cast<const bf16 *>(w);
+  p.bias = bias;
+  p.out = reinterpret_cast<bf16 *>(out);
+  p.T = T;
+  p.ntiles = (T + kMrfL - 1) / kMrfL;
+  p.slope = out_slope;
+  p.x_bytes = (uint32_t)bytes;
+  const dim3 grid((unsigned)p.ntiles, (unsigned)B);
+  if (C == 32)
+    hipLaunchKernelGGL(mrf_kernel<32>, grid, dim3(256), 0, as_stream(stream), p);
+  else
+    hipLaunchKernelGGL(mrf_kernel<64>, grid, dim3(256), 0, as_stream(stream), p);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}

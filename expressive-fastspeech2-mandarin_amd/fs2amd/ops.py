@@ -422,6 +422,21 @@ def wconv_tail(x, w_packed, bias, residual, *, ks=5, pad=2, out=None, layout=Non
     return out
 
 
+def hifigan_mrf(x, x_act, w_packed, bias, out_slope, out=None):
+    """fs2_hifigan_mrf: one HiFi-GAN stage's multi-receptive-field block (3 ResBlock1 chains, their
+    average, the next leaky_relu) in one launch: x / x_act = the upsampler's output and its
+    leaky_relu, bf16 [B, T, C] (C = 32 / 64) -> lrelu(xs / 3, out_slope) bf16 [B, T, C]."""
+    _gpu(x, x_act, w_packed, bias)
+    B, T, C = x.shape
+    assert x_act.shape == x.shape and x.dtype == torch.bfloat16 and x_act.dtype == torch.bfloat16
+    assert w_packed.numel() == _lib.fs2_hifigan_mrf_weight_elems(C) and bias.numel() == 18 * C
+    if out is None:
+        out = torch.empty_like(x)
+    L.check(_lib.fs2_hifigan_mrf(_ptr(x.contiguous()), _ptr(x_act.contiguous()), _ptr(w_packed), _ptr(bias), B, T, C,
+                                 float(out_slope), _ptr(out), _stream(x)), "fs2_hifigan_mrf")
+    return out
+
+
 def wconv(x, w_packed, bias, *, ks, pad, out=None, second=None, layout=None):
     """PostNet Conv1d(512, 512, k=5) + folded BatchNorm + tanh on padded bf16 rows [B, T, 512]
     (fs2_wconv; w_packed from :func:`pack_wconv_weight`). second = (w2_packed, bias2): the next

@@ -178,6 +178,23 @@ class Generator(nn.Module):
                              "u": u, "cout": w.shape[0] // u})
         for rb in self.resblocks:
             P["rb"].append([(conv(c1), conv(c2)) for c1, c2 in zip(rb.convs1, rb.convs2)])
+        # the narrow stages' multi-receptive-field blocks as one fused launch each (fs2_hifigan_mrf)
+        P["mrf"] = {}
+        if c == L.FS2_BF16 and list(self.h.resblock_kernel_sizes) == [3, 7, 11] and \
+                all(list(d) == [1, 3, 5] for d in self.h.resblock_dilation_sizes) and str(self.h.resblock) == "1":
+            nk = self.num_kernels
+            for i in range(self.num_upsamples):
+                ch = self.h.upsample_initial_channel // (2 ** (i + 1))
+                if ch not in (32, 64):
+                    continue
+                ws, bs = [], []
+                for j in range(nk):
+                    rb = self.resblocks[i * nk + j]
+                    for c1, c2 in zip(rb.convs1, rb.convs2):
+                        for m in (c1, c2):
+                            ws.append(ops.pack_wconv_tail(_weight(m).float().to(dev)))
+                            bs.append(m.bias.detach().float().to(dev))
+                P["mrf"][i] = (torch.cat(ws).contiguous(), torch.cat(bs).contiguous())
         wp = _weight(self.conv_post).float().to(dev)
         w4 = torch.zeros(4, wp.shape[1], wp.shape[2], device=dev)
         w4[:1] = wp
@@ -218,8 +235,13 @@ class Generator(nn.Module):
             a0 = torch.empty_like(xu)                                    # leaky_relu(xu): convs1 input of pair 0
             run(h, up, L.EPI_BIAS, xu, T, out2=a0.view(B, T, -1), out2_act=True, out2_slope=LRELU_SLOPE)
             T = T2
-            xs = torch.empty_like(xu)                                    # multi-receptive-field sum
             last_stage = i == len(P["ups"]) - 1
+            if i in P["mrf"] and os.environ.get("FS2_VOC_MRF", "1") != "0":
+                # the stage's 18 ResBlock convs, their average and the next leaky_relu in one launch
+                wm, bm = P["mrf"][i]
+                h = ops.hifigan_mrf(xu, a0, wm, bm, 0.01 if last_stage else LRELU_SLOPE)
+                continue
+            xs = torch.empty_like(xu)                                    # multi-receptive-field sum
             nxt = torch.empty_like(xu)                                   # leaky_relu(xs / nk): next stage's input
             xa, xb, aa, tt = (torch.empty_like(xu) for _ in range(4))
             for j in range(nk):

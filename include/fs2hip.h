@@ -507,6 +507,23 @@ int fs2_length_masks(const int64_t *lens, int B, int width, bool *mask, fs2_stre
 int fs2_seq_layout(const int64_t *lens, int B, int T, int32_t *cu, int32_t *row_pos, int32_t *rowmap,
                    fs2_stream_t stream);
 
+/*
+ * fs2_hifigan_mrf — one HiFi-GAN V1 upsampling stage's multi-receptive-field block in ONE launch
+ * (hifigan/models.py:20-45 ResBlock1 with kernels (3, 7, 11) x dilations (1, 3, 5), summed and
+ * averaged, :152-158), for C = 32 or 64 channels (the last two stages):
+ *   xs = sum_k ResBlock_k(x);  out = leaky_relu(xs / 3, out_slope)
+ *   ResBlock_k: for d in (1, 3, 5): x = conv2(lrelu(conv1_d(lrelu(x, 0.1)) + b1, 0.1)) + b2 + x
+ * x: the upsampler output bf16 [B, T, C]; x_act = lrelu(x, 0.1) (its second output); out bf16
+ * [B, T, C] (must not alias either). Per-utterance zero padding at [0, T) for every conv.
+ * w: fs2_hifigan_mrf_weight_elems(C) bf16, conv (chain j, pair p, second s) at element offset
+ * sum_{j' < j} 6 k_{j'} C^2 + (2p + s) k_j C^2, each [k C/32 k-steps][C/16 blocks][4 h][16 r][8 e],
+ * element (s, b, h, r, e) = W[16b + r][32s + 8h + e], W[n][tap C + c] = conv.weight[n][c][tap]
+ * (weight norm folded); bias f32 [18][C] in the same conv order.
+ */
+int fs2_hifigan_mrf(const void *x, const void *x_act, const void *w, const float *bias, int B, int T, int C,
+                    float out_slope, void *out, fs2_stream_t stream);
+int64_t fs2_hifigan_mrf_weight_elems(int C);
+
 /* Library identification. */
 const char *fs2_version(void);
 const char *fs2_status_string(int status);

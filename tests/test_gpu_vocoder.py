@@ -131,3 +131,47 @@ def test_res_sum_epilogue(gen):
                epilogue=L.EPI_RES_SUM, out=out, residual=r.to(DEV), residual2=out, out_div=3.0)
     ref = (F.conv1d(x.transpose(1, 2), w, b, padding=3).transpose(1, 2) + r + acc) / 3.0
     assert float((out.cpu() - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("C,T", [(32, 1100), (64, 600), (32, 256), (64, 77)])
+def test_hifigan_mrf_fused_stage(gen, C, T):
+    """fs2_hifigan_mrf (a stage's 3 ResBlock1 chains of 6 convs each, their average and the next
+    leaky_relu in one launch; 256-sample tiles with a 64-sample halo, intermediates on chip)
+    against a float64 statement of hifigan/models.py:20-45,152-158 on the same bf16 input and
+    bf16-rounded weights, with the kernel's bf16 rounding points (each conv output and the running
+    x stored as bf16; xs summed in f32): max |err| <= 3e-2 of the output scale, mean <= 2e-3. Tile
+    edges and utterance edges (T not a multiple of 256, T < 256) included."""
+    from fs2amd import ops
+
+    g = torch.Generator().manual_seed(C + T)
+    B = 3
+    ws = [torch.randn(C, C, k, generator=g) / (C * k) ** 0.5 for k in (3, 7, 11) for _ in range(6)]
+    bs = [0.05 * torch.randn(C, generator=g) for _ in range(18)]
+    x = (0.5 * torch.randn(B, T, C, generator=g)).to(torch.bfloat16)
+    xa = F.leaky_relu(x.float(), 0.1).to(torch.bfloat16)
+    wp = torch.cat([ops.pack_wconv_tail(w.to(DEV)) for w in ws]).contiguous()
+    bp = torch.cat(bs).to(DEV).contiguous()
+    out = ops.hifigan_mrf(x.to(DEV), xa.to(DEV), wp, bp, 0.01)
+    torch.cuda.synchronize()
+
+    def conv(z, w, b, d):
+        k = w.shape[-1]
+        wq = w.to(torch.bfloat16).double()
+        return F.conv1d(z.transpose(1, 2), wq, b.double(), dilation=d, padding=(k * d - d) // 2).transpose(1, 2)
+
+    bf = lambda t: t.to(torch.bfloat16).double()
+    xs = 0
+    for j, k in enumerate((3, 7, 11)):
+        cur = x.double()
+        act = xa.double()
+        for pi, d in enumerate((1, 3, 5)):
+            t = bf(F.leaky_relu(conv(act, ws[6 * j + 2 * pi], bs[6 * j + 2 * pi], d), 0.1))
+            v = conv(t, ws[6 * j + 2 * pi + 1], bs[6 * j + 2 * pi + 1], 1) + cur
+            if pi < 2:
+                cur, act = bf(v), bf(F.leaky_relu(v, 0.1))
+            else:
+                xs = xs + v
+    ref = F.leaky_relu(xs / 3, 0.01)
+    err = (out.double().cpu() - ref).abs()
+    scale = float(ref.abs().max())
+    assert float(err.max()) <= 3e-2 * scale and float(err.mean()) <= 2e-3 * scale, (float(err.max()), float(err.mean()), scale)
