@@ -541,6 +541,12 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
       } else if (epi == FS2_EPI_BIAS_LRELU) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.0f ? v[q] : v[q] * a.slope;
+      } else if (epi == FS2_EPI_RELU_GRAD) {
+        float rv[8];
+        load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n, rv);
+        load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n + 4, rv + 4);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = rv[q] > 0.0f ? v[q] : 0.0f;
       }
       const int64_t o = (int64_t)m * a.os + n;
       if (a.out_dt == FS2_BF16)
@@ -605,6 +611,11 @@ __device__ __forceinline__ void epilogue(const ConvArgs &a, const float *E, int 
     } else if (epi == FS2_EPI_BIAS_LRELU) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.0f ? v[q] : v[q] * a.slope;
+    } else if (epi == FS2_EPI_RELU_GRAD) {
+      float rv[4];
+      load_any4(a.res, a.res_dt, (int64_t)m * a.rs + n, rv);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = rv[q] > 0.0f ? v[q] : 0.0f;
     }
     store_any4(a.out, a.out_dt, (int64_t)m * a.os + n, v, a.out_scale);
     if (a.out2 != nullptr) {

@@ -1372,14 +1372,15 @@ extern "C" int fs2_conv1d(const fs2_conv_desc *d, fs2_stream_t stream) {
   if ((d->x_row_stride % ce) != 0) return FS2_EINVAL;
   if (d->out_split && (d->out_dtype != FS2_BF16 || d->out_row_stride < 2 * (int64_t)d->N)) return FS2_EINVAL;
   const int epi = d->epilogue;
-  if (epi < FS2_EPI_BIAS || epi > FS2_EPI_RES_SUM) return FS2_EINVAL;
+  if (epi < FS2_EPI_BIAS || epi > FS2_EPI_RELU_GRAD) return FS2_EINVAL;
   const bool ln = epi == FS2_EPI_RES_LN || epi == FS2_EPI_RELU_LN || epi == FS2_EPI_RELU_LN_DOT;
   if (ln && (d->N != 256 || d->ln_gamma == nullptr || d->ln_beta == nullptr || d->bias == nullptr)) return FS2_EINVAL;
-  if ((epi == FS2_EPI_RES_LN || epi == FS2_EPI_BIAS_RES || epi == FS2_EPI_RES_SUM) && d->residual == nullptr)
+  if ((epi == FS2_EPI_RES_LN || epi == FS2_EPI_BIAS_RES || epi == FS2_EPI_RES_SUM || epi == FS2_EPI_RELU_GRAD) &&
+      d->residual == nullptr)
     return FS2_EINVAL;
   if (epi == FS2_EPI_RELU_LN_DOT && (d->dot_w == nullptr || d->out_dtype != FS2_F32)) return FS2_EINVAL;
   if (epi != FS2_EPI_RELU_LN_DOT && (d->out_row_stride < d->N || (d->out_row_stride & 3) != 0)) return FS2_EINVAL;
-  if ((epi == FS2_EPI_RES_LN || epi == FS2_EPI_BIAS_RES || epi == FS2_EPI_RES_SUM) &&
+  if ((epi == FS2_EPI_RES_LN || epi == FS2_EPI_BIAS_RES || epi == FS2_EPI_RES_SUM || epi == FS2_EPI_RELU_GRAD) &&
       (d->res_row_stride < d->N || (d->res_row_stride & 3)))
     return FS2_EINVAL;
   const int64_t M64 = (int64_t)d->B * d->T;

@@ -1,0 +1,664 @@
+// Training-step kernels around the GEMMs (train.py step, cfg3): the FFT block's
+//   y = masked_fill(LayerNorm(dropout(a) + res), pad, 0)            (transformer/SubLayers.py:54-57,90-93,
+//                                                                      transformer/Layers.py:27-30)
+// forward in one pass per row, its backward (input, residual, gamma/beta and the producing
+// conv's bias gradients) in one pass plus a deterministic column reduction, and a generic
+// deterministic column sum (bias gradients of the other convs).
+//
+// Dropout keep bits come from a counter hash of (seed, salt, row, column): the backward
+// regenerates them instead of storing a mask. The seed lives in device memory (one int64 that the
+// trainer advances once per step inside the captured graph), so graph replays draw fresh masks.
+#include "fs2_common.h"
+
+namespace {
+
+constexpr int kD = 256;       // d_model (transformer.encoder_hidden / decoder_hidden)
+constexpr int kLnBlocks = 256; // partial-sum blocks of the LN backward
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t drop_key(const int64_t *seed, uint32_t salt) {
+  const uint64_t s = seed != nullptr ? (uint64_t)*seed : 0ull;
+  return mix32((uint32_t)s ^ mix32((uint32_t)(s >> 32) + salt * 0x9E3779B9U));
+}
+
+// keep mask of 4 consecutive columns as 4 bits
+__device__ __forceinline__ unsigned keep4(uint32_t key, uint32_t idx0, uint32_t thr) {
+  unsigned m = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) m |= ((mix32((idx0 + q) ^ key) >> 8) >= thr ? 1u : 0u) << q;
+  return m;
+}
+
+__device__ __forceinline__ bool row_masked(const int64_t *lens, int64_t row, int T) {
+  if (lens == nullptr) return false;
+  const int64_t b = row / T;
+  return row - b * T >= lens[b];
+}
+
+template <typename TR>
+__global__ __launch_bounds__(256) void res_ln_fwd_kernel(const float *__restrict__ a, const TR *__restrict__ res,
+                                                         const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                         const int64_t *__restrict__ lens, int64_t R, int T, float eps,
+                                                         uint32_t thr, float scale, const int64_t *seed, uint32_t salt,
+                                                         float *__restrict__ y, bf16 *__restrict__ y_bf,
+                                                         float *__restrict__ xhat, float *__restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane * 4;
+  const uint32_t key = drop_key(seed, salt);
+  float g[4], bt[4];
+  load4(gamma + c, g);
+  load4(beta + c, bt);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < R; row += nw) {
+    float v[4], r[4];
+    load4(a + row * kD + c, v);
+    load4(res + row * kD + c, r);
+    if (thr != 0) {
+      const unsigned k = keep4(key, (uint32_t)(row * kD + c), thr);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = ((k >> q) & 1) ? v[q] * scale : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] += r[q];
+    const float mean = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / kD);
+    float s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] -= mean;
+      s2 += v[q] * v[q];
+    }
+    const float rs = rsqrtf(wave_sum(s2) * (1.0f / kD) + eps);
+    const bool masked = row_masked(lens, row, T);
+    float o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] *= rs;
+      o[q] = masked ? 0.0f : v[q] * g[q] + bt[q];
+    }
+    store4(xhat + row * kD + c, v);
+    store4(y + row * kD + c, o);
+    if (y_bf != nullptr) store4(y_bf + row * kD + c, o);
+    if (lane == 0) rstd_out[row] = rs;
+  }
+}
+
+// dv = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)); dres = dv; da = dv * keep * scale.
+// part[blk][0..3][kD]: sum dy*xhat (gamma), sum dy (beta), sum da (the producing conv's bias).
+__global__ __launch_bounds__(256) void res_ln_bwd_kernel(const float *__restrict__ dy, const float *__restrict__ xhat,
+                                                         const float *__restrict__ rstd, const float *__restrict__ gamma,
+                                                         const int64_t *__restrict__ lens, int64_t R, int T, uint32_t thr,
+                                                         float scale, const int64_t *seed, uint32_t salt,
+                                                         float *__restrict__ dres, bf16 *__restrict__ da,
+                                                         float *__restrict__ part) {
+  __shared__ float red[3][4][kD];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = lane * 4;
+  const uint32_t key = drop_key(seed, salt);
+  float g[4];
+  load4(gamma + c, g);
+  float pg[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f}, pa[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wv; row < R; row += nw) {
+    if (row_masked(lens, row, T)) {  // masked_fill's gradient: nothing flows through a padding row
+      const float z[4] = {0.f, 0.f, 0.f, 0.f};
+      store4(dres + row * kD + c, z);
+      store4(da + row * kD + c, z);
+      continue;
+    }
+    float d[4], xh[4], gd[4];
+    load4(dy + row * kD + c, d);
+    load4(xhat + row * kD + c, xh);
+    const float rs = rstd[row];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      gd[q] = g[q] * d[q];
+      s1 += gd[q];
+      s2 += gd[q] * xh[q];
+      pg[q] += d[q] * xh[q];
+      pb[q] += d[q];
+    }
+    const float m1 = wave_sum(s1) * (1.0f / kD), m2 = wave_sum(s2) * (1.0f / kD);
+    float dv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dv[q] = rs * (gd[q] - m1 - xh[q] * m2);
+    store4(dres + row * kD + c, dv);
+    if (thr != 0) {
+      const unsigned k = keep4(key, (uint32_t)(row * kD + c), thr);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dv[q] = ((k >> q) & 1) ? dv[q] * scale : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pa[q] += dv[q];
+    store4(da + row * kD + c, dv);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    red[0][wv][c + q] = pg[q];
+    red[1][wv][c + q] = pb[q];
+    red[2][wv][c + q] = pa[q];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * kD; i += 256) {
+    const int k = i / kD, col = i - k * kD;
+    part[(int64_t)blockIdx.x * 3 * kD + i] = (red[k][0][col] + red[k][1][col]) + (red[k][2][col] + red[k][3][col]);
+  }
+}
+
+// Column sums, pass 1: block (256-column stripe, row chunk) -> part[chunk][N]; 4 columns per
+// thread, 4 rows in flight per block (one per wave).
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_part_kernel(const T *__restrict__ x, int64_t R, int N, int64_t rs,
+                                                          int rows_per_chunk, float *__restrict__ part) {
+  __shared__ float red[4][256];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + lane * 4;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = r0 + rows_per_chunk < R ? r0 + rows_per_chunk : R;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < N)
+    for (int64_t r = r0 + wv; r < r1; r += 4) {
+      float v[4];
+      load4(x + r * rs + c, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[q] += v[q];
+    }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[wv][lane * 4 + q] = s[q];
+  __syncthreads();
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col < N)
+    part[(int64_t)blockIdx.y * N + col] =
+        (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+// pass 2: out[n] (+)= sum over chunks of part[chunk][n], chunks in order (deterministic)
+__global__ __launch_bounds__(256) void colsum_finish_kernel(const float *__restrict__ part, int chunks, int N,
+                                                            float *__restrict__ out, int accumulate) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int k = 0; k < chunks; ++k) s += part[(int64_t)k * N + n];
+  out[n] = accumulate ? out[n] + s : s;
+}
+
+// LN backward pass 2: (dgamma, dbeta, dbias)[n] (+)= sum over blocks, in block order
+__global__ __launch_bounds__(256) void ln_finish_kernel(const float *__restrict__ part, int chunks, float *dgamma,
+                                                        float *dbeta, float *dbias, int accumulate) {
+  const int which = blockIdx.x, n = threadIdx.x;
+  float *out = which == 0 ? dgamma : (which == 1 ? dbeta : dbias);
+  if (out == nullptr) return;
+  float s = 0.f;
+  for (int k = 0; k < chunks; ++k) s += part[((int64_t)k * 3 + which) * kD + n];
+  out[n] = accumulate ? out[n] + s : s;
+}
+
+uint32_t drop_threshold(float p) {
+  if (!(p > 0.0f)) return 0u;
+  const double t = (double)p * 16777216.0;
+  return t >= 16777216.0 ? 16777216u : (uint32_t)t;
+}
+
+}  // namespace
+
+extern "C" int fs2_res_ln_fwd(const float *a, const void *res, int res_dtype, const float *gamma, const float *beta,
+                              const int64_t *lens, int64_t R, int T, int D, float eps, float p_drop,
+                              const int64_t *seed, int salt, float *y, void *y_bf, float *xhat, float *rstd,
+                              fs2_stream_t stream) {
+  if (a == nullptr || res == nullptr || gamma == nullptr || beta == nullptr || y == nullptr || xhat == nullptr ||
+      rstd == nullptr)
+    return FS2_EINVAL;
+  if (D != kD) return FS2_EUNSUPPORTED;
+  if (R < 0 || T <= 0 || !(p_drop >= 0.0f && p_drop < 1.0f) || (p_drop > 0.0f && seed == nullptr)) return FS2_EINVAL;
+  if (lens != nullptr && R % T) return FS2_EINVAL;
+  if (R == 0) return FS2_OK;
+  const uint32_t thr = drop_threshold(p_drop);
+  const float scale = 1.0f / (1.0f - p_drop);
+  const int64_t blocks64 = (R + 3) / 4;
+  const unsigned grid = (unsigned)(blocks64 < 2048 ? blocks64 : 2048);
+  hipStream_t s = as_stream(stream);
+  if (res_dtype == FS2_F32)
+    hipLaunchKernelGGL(res_ln_fwd_kernel<float>, dim3(grid), dim3(256), 0, s, a, reinterpret_cast<const float *>(res),
+                       gamma, beta, lens, R, T, eps, thr, scale, seed, (uint32_t)salt, y,
+                       reinterpret_cast<bf16 *>(y_bf), xhat, rstd);
+  else if (res_dtype == FS2_BF16)
+    hipLaunchKernelGGL(res_ln_fwd_kernel<bf16>, dim3(grid), dim3(256), 0, s, a, reinterpret_cast<const bf16 *>(res),
+                       gamma, beta, lens, R, T, eps, thr, scale, seed, (uint32_t)salt, y,
+                       reinterpret_cast<bf16 *>(y_bf), xhat, rstd);
+  else
+    return FS2_EUNSUPPORTED;
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int64_t fs2_res_ln_bwd_ws_bytes(int D) { return (int64_t)kLnBlocks * 3 * D * (int64_t)sizeof(float); }
+
+extern "C" int fs2_res_ln_bwd(const float *dy, const float *xhat, const float *rstd, const float *gamma,
+                              const int64_t *lens, int64_t R, int T, int D, float p_drop, const int64_t *seed, int salt,
+                              float *dres, void *da, float *dgamma, float *dbeta, float *dbias, int accumulate,
+                              float *ws, int64_t ws_bytes, fs2_stream_t stream) {
+  if (dy == nullptr || xhat == nullptr || rstd == nullptr || gamma == nullptr || dres == nullptr || da == nullptr ||
+      dgamma == nullptr || dbeta == nullptr || ws == nullptr)
+    return FS2_EINVAL;
+  if (D != kD) return FS2_EUNSUPPORTED;
+  if (R < 0 || T <= 0 || !(p_drop >= 0.0f && p_drop < 1.0f) || (p_drop > 0.0f && seed == nullptr)) return FS2_EINVAL;
+  if (lens != nullptr && R % T) return FS2_EINVAL;
+  if (ws_bytes < fs2_res_ln_bwd_ws_bytes(D)) return FS2_EINVAL;
+  hipStream_t s = as_stream(stream);
+  if (R == 0) {
+    if (!accumulate) {
+      (void)hipMemsetAsync(dgamma, 0, kD * sizeof(float), s);
+      (void)hipMemsetAsync(dbeta, 0, kD * sizeof(float), s);
+      if (dbias != nullptr) (void)hipMemsetAsync(dbias, 0, kD * sizeof(float), s);
+    }
+    return FS2_OK;
+  }
+  const uint32_t thr = drop_threshold(p_drop);
+  const float scale = 1.0f / (1.0f - p_drop);
+  const int64_t b64 = (R + 3) / 4;
+  const int grid = (int)(b64 < kLnBlocks ? b64 : kLnBlocks);
+  hipLaunchKernelGGL(res_ln_bwd_kernel, dim3(grid), dim3(256), 0, s, dy, xhat, rstd, gamma, lens, R, T, thr, scale,
+                     seed, (uint32_t)salt, dres, reinterpret_cast<bf16 *>(da), ws);
+  hipLaunchKernelGGL(ln_finish_kernel, dim3(3), dim3(kD), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int64_t fs2_colsum_ws_bytes(int N) { return 64LL * ((N + 255) / 256 * 256) * (int64_t)sizeof(float); }
+
+extern "C" int fs2_colsum(const void *x, int dtype, int64_t R, int N, int64_t row_stride, float *out, int accumulate,
+                          float *ws, int64_t ws_bytes, fs2_stream_t stream) {
+  if (x == nullptr || out == nullptr || ws == nullptr) return FS2_EINVAL;
+  if (R < 0 || N <= 0 || (N & 3) || row_stride < N || (row_stride & 3)) return FS2_EINVAL;
+  if (ws_bytes < fs2_colsum_ws_bytes(N)) return FS2_EINVAL;
+  hipStream_t s = as_stream(stream);
+  int chunks = (int)((R + 127) / 128);
+  if (chunks > 64) chunks = 64;
+  if (chunks < 1) chunks = 1;
+  const int rpc = (int)((R + chunks - 1) / chunks);
+  dim3 g1((unsigned)((N + 255) / 256), (unsigned)chunks);
+  if (dtype == FS2_F32)
+    hipLaunchKernelGGL(colsum_part_kernel<float>, g1, dim3(256), 0, s, reinterpret_cast<const float *>(x), R, N,
+                       row_stride, rpc, ws);
+  else if (dtype == FS2_BF16)
+    hipLaunchKernelGGL(colsum_part_kernel<bf16>, g1, dim3(256), 0, s, reinterpret_cast<const bf16 *>(x), R, N,
+                       row_stride, rpc, ws);
+  else
+    return FS2_EUNSUPPORTED;
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, ws, chunks, N, out,
+                     accumulate);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Conv1d / Linear weight gradient (Conv1dFn.backward's dW, training.py):
+//   dW[n][c][k] = sum_{b, t} dy[b, t, n] * x[b, t + k - pad, c]     (x zero outside [0, T) per sequence)
+// and optionally db[n] = sum_{b, t} dy[b, t, n]. No unfolded copy of x: per 32-row chunk of one
+// sequence the block stages dy [32 x NB] and the x window [32 + KS - 1 rows x CB] in LDS (plain
+// rows, chunk-XOR swizzled), and both MFMA operands come out of them with ds_read_b64_tr_b16 (the
+// reduction index m is the row index of both tiles). The KS taps share one x window: a lane reads
+// rows 8g .. 8g + 7 + KS - 1 of its column once and forms tap k's 8-row fragment from registers
+// (even k: a dword offset; odd k: v_alignbit of neighbouring dwords).
+// Block = 4 waves stacked along n (wave tile 16*WN x 64*WCB, all KS taps in accumulators); grid
+// (n tiles x c tiles, S row splits); split partials part[s][k][n][c] are summed in order by
+// wgrad_reduce_kernel (deterministic; optionally accumulated into an existing gradient).
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+struct WgArgs {
+  const void *dy;
+  int64_t dys;
+  const bf16 *x;
+  int64_t xs;
+  float *part;
+  float *pbias;
+  int B, T, N, C, pad, S, tiles_c, CT;  // CT = 32-row chunks per sequence
+};
+
+// 128-byte LDS rows (64 bf16), 16-byte chunk XOR: conflict-free ds_read_b64_tr_b16 for 8-row
+// separated lane groups at any base row (exhaustive search over linear XOR maps).
+__device__ __forceinline__ int wg_off(int row, int colbyte) {
+  const int ch = (colbyte >> 4) ^ (((row >> 1) & 1) << 1) ^ (((row >> 3) & 1) << 2);
+  return row * 128 + (ch << 4) + (colbyte & 15);
+}
+
+__device__ __forceinline__ uint2 tr_read(const char *lds_base, int off) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)(lds_base + off));
+  uint2 r;
+  __builtin_memcpy(&r, &v, 8);
+  return r;
+}
+
+__device__ __forceinline__ uint4 f32x8_to_bf16(float4 a, float4 b) {
+  float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  bf16x8 o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
+  uint4 r;
+  __builtin_memcpy(&r, &o, 16);
+  return r;
+}
+
+template <int KS, int WN, int WCB, bool DYF32>
+__global__ __launch_bounds__(256, 1) void wgrad_kernel(WgArgs a) {
+  constexpr int NB = 64 * WN;            // n columns per block
+  constexpr int CB = 64 * WCB;           // c columns per block
+  constexpr int NR = (KS + 7 + 3) / 4;   // 4-row transposed reads per x fragment group
+  constexpr int XR = 24 + 4 * NR;        // x window rows held in LDS (>= 32 + KS - 1)
+  constexpr int DY_BYTES = WN * 32 * 128;
+  constexpr int X_BYTES = WCB * XR * 128;
+  constexpr int BUF = DY_BYTES + X_BYTES;
+  constexpr int DY_LD = NB / 8 * 32 / 256 > 0 ? NB / 8 * 32 / 256 : 1;  // 16-byte dy loads per thread
+  constexpr int X_CHUNKS = XR * CB / 8;
+  constexpr int X_LD = (X_CHUNKS + 255) / 256;
+  constexpr int DYW = DYF32 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int tile = blockIdx.x, s = blockIdx.y;
+  const int n0 = (tile / a.tiles_c) * NB, c0 = (tile % a.tiles_c) * CB;
+  const int Q = a.B * a.CT;
+  const bool do_bias = a.pbias != nullptr && (tile % a.tiles_c) == 0;
+
+  uint4 rdy[DY_LD][DYW];
+  uint4 rx[X_LD];
+  float bsum[DY_LD][8];
+#pragma unroll
+  for (int i = 0; i < DY_LD; ++i)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bsum[i][q] = 0.f;
+
+  auto load = [&](int q) {
+    const int b = q / a.CT, t0 = (q - b * a.CT) * 32;
+#pragma unroll
+    for (int i = 0; i < DY_LD; ++i) {
+      const int e = tid + 256 * i;              // 16-byte chunk: row e / (NB/8), col group e % (NB/8)
+      const int r = e / (NB / 8), cg = e % (NB / 8);
+      const int t = t0 + r, n = n0 + cg * 8;
+      if (t < a.T && n < a.N) {
+        const int64_t row = (int64_t)b * a.T + t;
+        if constexpr (DYF32) {
+          const float4 *p = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(a.dy) + row * a.dys + n);
+          float4 v0 = p[0], v1 = p[1];
+          __builtin_memcpy(&rdy[i][0], &v0, 16);
+          __builtin_memcpy(&rdy[i][1], &v1, 16);
+        } else {
+          rdy[i][0] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const bf16 *>(a.dy) + row * a.dys + n);
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < DYW; ++h) rdy[i][h] = make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < X_LD; ++i) {
+      const int e = tid + 256 * i;
+      const int r = e / (CB / 8), cg = e % (CB / 8);
+      const int t = t0 - a.pad + r, c = c0 + cg * 8;
+      rx[i] = make_uint4(0, 0, 0, 0);
+      if (e < X_CHUNKS && r < 32 + KS - 1 && t >= 0 && t < a.T && c < a.C)
+        rx[i] = *reinterpret_cast<const uint4 *>(a.x + ((int64_t)b * a.T + t) * a.xs + c);
+    }
+  };
+  auto store = [&](int buf) {
+    char *base = lds + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < DY_LD; ++i) {
+      const int e = tid + 256 * i;
+      const int r = e / (NB / 8), cg = e % (NB / 8);
+      uint4 v;
+      if constexpr (DYF32) {
+        float4 v0, v1;
+        __builtin_memcpy(&v0, &rdy[i][0], 16);
+        __builtin_memcpy(&v1, &rdy[i][1], 16);
+        if (do_bias) {
+          bsum[i][0] += v0.x; bsum[i][1] += v0.y; bsum[i][2] += v0.z; bsum[i][3] += v0.w;
+          bsum[i][4] += v1.x; bsum[i][5] += v1.y; bsum[i][6] += v1.z; bsum[i][7] += v1.w;
+        }
+        v = f32x8_to_bf16(v0, v1);
+      } else {
+        v = rdy[i][0];
+        if (do_bias) {
+          const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            bsum[i][2 * h] += __uint_as_float(wd[h] << 16);
+            bsum[i][2 * h + 1] += __uint_as_float(wd[h] & 0xffff0000u);
+          }
+        }
+      }
+      *reinterpret_cast<uint4 *>(base + (cg >> 3) * 32 * 128 + wg_off(r, (cg & 7) * 16)) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < X_LD; ++i) {
+      const int e = tid + 256 * i;
+      if (e < X_CHUNKS) {
+        const int r = e / (CB / 8), cg = e % (CB / 8);
+        *reinterpret_cast<uint4 *>(base + DY_BYTES + (cg >> 3) * XR * 128 + wg_off(r, (cg & 7) * 16)) = rx[i];
+      }
+    }
+  };
+
+  f32x4 acc[KS][WN][4 * WCB];
+#pragma unroll
+  for (int k = 0; k < KS; ++k)
+#pragma unroll
+    for (int wn = 0; wn < WN; ++wn)
+#pragma unroll
+      for (int j = 0; j < 4 * WCB; ++j) acc[k][wn][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int q = s;
+  int cur = 0;
+  if (q < Q) {
+    load(q);
+    store(0);
+  }
+  __syncthreads();
+  // lane's transposed-read address parts: row q4 = li >> 2 of a 4-row block, 8-byte column piece
+  const int trow = 8 * g + (li >> 2), tcol = 8 * (li & 3);
+  for (; q < Q; q += a.S) {
+    const bool more = q + a.S < Q;
+    if (more) load(q + a.S);
+    const char *base = lds + cur * BUF;
+    bf16x8 A[WN];
+#pragma unroll
+    for (int wn = 0; wn < WN; ++wn) {
+      const int nl = w * 16 * WN + wn * 16;  // wave's n block within the tile
+      const char *sb = base + (nl >> 6) * 32 * 128;
+      const uint2 lo = tr_read(sb, wg_off(trow, (nl & 63) * 2 + tcol));
+      const uint2 hi = tr_read(sb, wg_off(trow + 4, (nl & 63) * 2 + tcol));
+      uint4 u = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      __builtin_memcpy(&A[wn], &u, 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 4 * WCB; ++j) {
+      const char *xb = base + DY_BYTES + (j >> 2) * XR * 128;
+      uint32_t xw[2 * NR];
+#pragma unroll
+      for (int u = 0; u < NR; ++u) {
+        const uint2 v = tr_read(xb, wg_off(trow + 4 * u, (j & 3) * 32 + tcol));
+        xw[2 * u] = v.x;
+        xw[2 * u + 1] = v.y;
+      }
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        uint32_t f[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          f[d] = (k & 1) ? __builtin_amdgcn_alignbit(xw[(k + 1) / 2 + d], xw[(k - 1) / 2 + d], 16) : xw[k / 2 + d];
+        bf16x8 Bf;
+        __builtin_memcpy(&Bf, f, 16);
+#pragma unroll
+        for (int wn = 0; wn < WN; ++wn)
+          acc[k][wn][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[wn], Bf, acc[k][wn][j], 0, 0, 0);
+      }
+    }
+    if (more) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // split partial: part[s][k][n][c]
+#pragma unroll
+  for (int k = 0; k < KS; ++k)
+#pragma unroll
+    for (int wn = 0; wn < WN; ++wn)
+#pragma unroll
+      for (int j = 0; j < 4 * WCB; ++j) {
+        const int c = c0 + 16 * j + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + w * 16 * WN + wn * 16 + 4 * g + r;
+          if (n < a.N && c < a.C) a.part[(((int64_t)s * KS + k) * a.N + n) * a.C + c] = acc[k][wn][j][r];
+        }
+      }
+  if (do_bias) {  // rows of the block's dy loads -> per-column sums, in a fixed order
+    constexpr int RPP = 256 / (NB / 8);  // rows per load pass
+    float *red = reinterpret_cast<float *>(lds);
+#pragma unroll
+    for (int i = 0; i < DY_LD; ++i) {
+      const int e = tid + 256 * i;
+      const int r = e / (NB / 8), cg = e % (NB / 8);
+#pragma unroll
+      for (int qq = 0; qq < 8; ++qq) red[((i * RPP) + (r % RPP)) * NB + cg * 8 + qq] = bsum[i][qq];
+    }
+    __syncthreads();
+    if (tid < NB) {
+      float sacc = 0.f;
+      for (int r = 0; r < DY_LD * RPP; ++r) sacc += red[r * NB + tid];
+      if (n0 + tid < a.N) a.pbias[(int64_t)s * a.N + n0 + tid] = sacc;
+    }
+  }
+}
+
+// out[n][c][k] (+)= sum over splits of part[s][k][n][c]; rows n >= split go to the next output
+// (parts of one gradient that are separate parameters: Q | K | V)
+struct WgOut {
+  float *dw[3];
+  float *db[3];
+  int split;
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restrict__ part, int S, int KS, int N, int C,
+                                                           WgOut o, int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (n, c)
+  if (e >= (int64_t)N * C) return;
+  const int64_t NC = (int64_t)N * C;
+  const int n = (int)(e / C), which = n / o.split;
+  const int64_t el = e - (int64_t)which * o.split * C;
+  for (int k = 0; k < KS; ++k) {
+    float sacc = 0.f;
+    for (int s = 0; s < S; ++s) sacc += part[((int64_t)s * KS + k) * NC + e];
+    float *dst = o.dw[which] + el * KS + k;
+    *dst = accumulate ? *dst + sacc : sacc;
+  }
+}
+
+__global__ __launch_bounds__(256) void bias_reduce_kernel(const float *__restrict__ part, int S, int N, WgOut o,
+                                                          int accumulate) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int k = 0; k < S; ++k) s += part[(int64_t)k * N + n];
+  const int which = n / o.split;
+  float *dst = o.db[which] + (n - which * o.split);
+  *dst = accumulate ? *dst + s : s;
+}
+
+template <int KS, int WN, int WCB>
+void wgrad_launch(const WgArgs &a, bool dy_f32, int tiles, hipStream_t s) {
+  if (dy_f32)
+    hipLaunchKernelGGL((wgrad_kernel<KS, WN, WCB, true>), dim3(tiles, a.S), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<KS, WN, WCB, false>), dim3(tiles, a.S), dim3(256), 0, s, a);
+}
+
+int wgrad_splits(int tiles, int Q) {
+  int S = (512 + tiles - 1) / tiles;
+  if (S > Q) S = Q;
+  if (S > 64) S = 64;
+  return S < 1 ? 1 : S;
+}
+
+}  // namespace
+
+extern "C" int64_t fs2_conv_wgrad_ws_bytes(int B, int T, int N, int C, int KS) {
+  if (B <= 0 || T <= 0 || N <= 0 || C <= 0 || KS <= 0) return 0;
+  const int WN = KS == 1 ? 2 : 1, WCB = KS == 1 ? 2 : 1;
+  const int tiles = ((N + 64 * WN - 1) / (64 * WN)) * ((C + 64 * WCB - 1) / (64 * WCB));
+  const int S = wgrad_splits(tiles, B * ((T + 31) / 32));
+  return ((int64_t)S * KS * N * C + (int64_t)S * N) * (int64_t)sizeof(float);
+}
+
+extern "C" int fs2_conv_wgrad(const void *dy, int dy_dtype, int64_t dy_row_stride, const void *x,
+                              int64_t x_row_stride, int B, int T, int N, int C, int KS, int pad, float *dw,
+                              float *db, int accumulate, int split_rows, float *dw1, float *dw2, float *db1,
+                              float *db2, float *ws, int64_t ws_bytes, fs2_stream_t stream) {
+  if (dy == nullptr || x == nullptr || dw == nullptr || ws == nullptr) return FS2_EINVAL;
+  WgOut o;
+  o.dw[0] = dw, o.dw[1] = dw1, o.dw[2] = dw2;
+  o.db[0] = db, o.db[1] = db1, o.db[2] = db2;
+  o.split = N;
+  if (split_rows > 0) {  // N = 2 or 3 equal row parts, each its own tensor
+    if (N % split_rows || N / split_rows > 3 || N / split_rows < 2) return FS2_EINVAL;
+    for (int i = 1; i < N / split_rows; ++i)
+      if (o.dw[i] == nullptr || (db != nullptr && o.db[i] == nullptr)) return FS2_EINVAL;
+    o.split = split_rows;
+  }
+  if (B < 0 || T < 0 || N <= 0 || C <= 0 || (N & 7) || (C & 7) || pad < 0 || pad >= KS) return FS2_EINVAL;
+  if (dy_row_stride < N || x_row_stride < C || (dy_row_stride & 7) || (x_row_stride & 7)) return FS2_EINVAL;
+  if (dy_dtype != FS2_BF16 && dy_dtype != FS2_F32) return FS2_EUNSUPPORTED;
+  if (KS != 1 && KS != 3 && KS != 5 && KS != 9) return FS2_EUNSUPPORTED;
+  hipStream_t s = as_stream(stream);
+  if ((int64_t)B * T == 0) {
+    if (!accumulate)
+      for (int i = 0; i * o.split < N; ++i) {
+        (void)hipMemsetAsync(o.dw[i], 0, (size_t)o.split * C * KS * sizeof(float), s);
+        if (db != nullptr) (void)hipMemsetAsync(o.db[i], 0, (size_t)o.split * sizeof(float), s);
+      }
+    return FS2_OK;
+  }
+  if (ws_bytes < fs2_conv_wgrad_ws_bytes(B, T, N, C, KS)) return FS2_EINVAL;
+  const int WN = KS == 1 ? 2 : 1, WCB = KS == 1 ? 2 : 1;
+  WgArgs a;
+  a.dy = dy;
+  a.dys = dy_row_stride;
+  a.x = reinterpret_cast<const bf16 *>(x);
+  a.xs = x_row_stride;
+  a.B = B;
+  a.T = T;
+  a.N = N;
+  a.C = C;
+  a.pad = pad;
+  a.CT = (T + 31) / 32;
+  a.tiles_c = (C + 64 * WCB - 1) / (64 * WCB);
+  const int tiles = ((N + 64 * WN - 1) / (64 * WN)) * a.tiles_c;
+  a.S = wgrad_splits(tiles, B * a.CT);
+  a.part = ws;
+  a.pbias = db != nullptr ? ws + (int64_t)a.S * KS * N * C : nullptr;
+  const bool f32 = dy_dtype == FS2_F32;
+  switch (KS) {
+    case 1: wgrad_launch<1, 2, 2>(a, f32, tiles, s); break;
+    case 3: wgrad_launch<3, 1, 1>(a, f32, tiles, s); break;
+    case 5: wgrad_launch<5, 1, 1>(a, f32, tiles, s); break;
+    default: wgrad_launch<9, 1, 1>(a, f32, tiles, s); break;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(((int64_t)N * C + 255) / 256)), dim3(256), 0, s, ws, a.S,
+                     KS, N, C, o, accumulate);
+  if (db != nullptr)
+    hipLaunchKernelGGL(bias_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, a.pbias, a.S, N, o,
+                       accumulate);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}

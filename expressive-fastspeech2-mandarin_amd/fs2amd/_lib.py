@@ -18,7 +18,7 @@ DEFAULT_LIB = os.path.join(HERE, "_lib", "libfs2hip.so")
 FS2_F32, FS2_BF16, FS2_FP8 = 0, 1, 2
 FS2_OK, FS2_EINVAL, FS2_ELAUNCH, FS2_EUNSUPPORTED = 0, 1, 2, 3
 (EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_TANH, EPI_BIAS_RES, EPI_RES_LN, EPI_RELU_LN, EPI_RELU_LN_DOT, EPI_BIAS_LRELU,
- EPI_RES_SUM) = range(9)
+ EPI_RES_SUM, EPI_RELU_GRAD) = range(10)
 DUR_I64, DUR_F32, DUR_LOGPRED = 0, 1, 2
 
 _p = ctypes.c_void_p
@@ -137,6 +137,14 @@ SIGNATURES = {
     "fs2_lr_fused": (_i, [_p, _i, _p, _i, _f, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "fs2_hifigan_mrf": (_i, [_p, _p, _p, _p, _i, _i, _i, _f, _p, _p]),
     "fs2_hifigan_mrf_weight_elems": (ctypes.c_int64, [_i]),
+    "fs2_res_ln_fwd": (_i, [_p, _p, _i, _p, _p, _p, _i64, _i, _i, _f, _f, _p, _i, _p, _p, _p, _p, _p]),
+    "fs2_res_ln_bwd_ws_bytes": (_i64, [_i]),
+    "fs2_res_ln_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p, _i, _p, _p, _p, _p, _p, _i, _p, _i64, _p]),
+    "fs2_colsum_ws_bytes": (_i64, [_i]),
+    "fs2_colsum": (_i, [_p, _i, _i64, _i, _i64, _p, _i, _p, _i64, _p]),
+    "fs2_conv_wgrad_ws_bytes": (_i64, [_i, _i, _i, _i, _i]),
+    "fs2_conv_wgrad": (_i, [_p, _i, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p, _p, _p, _p, _i64,
+                            _p]),
     "fs2_length_masks": (_i, [_p, _i, _i, _p, _p]),
     "fs2_length_regulate": (_i, [_p, _i, _p, _i, _f, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p, _p, _p]),
 }

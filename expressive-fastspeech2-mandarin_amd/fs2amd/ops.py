@@ -932,3 +932,88 @@ def length_regulate(x, duration, max_len=None, return_index_map=False):
     if return_index_map:
         return res[0], mel_len, res[1]
     return res, mel_len
+
+
+# ---- training-step kernels (train.hip) ------------------------------------------------------------
+def res_ln_fwd(a, res, gamma, beta, eps, lens=None, p_drop=0.0, seed=None, salt=0, want_bf16=True):
+    """y = masked_fill(LayerNorm(dropout(a) + res), t >= lens[b], 0) (fs2_res_ln_fwd): a f32
+    [B, T, 256], res f32 / bf16. Returns (y f32, y bf16 or None, xhat f32, rstd f32 [B*T])."""
+    _gpu(a, res, gamma, beta, lens, seed)
+    B, T, D = a.shape
+    assert a.dtype == torch.float32 and a.is_contiguous() and res.shape == a.shape and res.is_contiguous()
+    y = torch.empty_like(a)
+    yb = torch.empty(a.shape, device=a.device, dtype=torch.bfloat16) if want_bf16 else None
+    xhat = torch.empty_like(a)
+    rstd = torch.empty(B * T, device=a.device, dtype=torch.float32)
+    L.check(_lib.fs2_res_ln_fwd(_ptr(a), _ptr(res), _dt(res), _ptr(gamma), _ptr(beta), _ptr(lens), B * T, T, D,
+                                float(eps), float(p_drop), _ptr(seed), int(salt), _ptr(y), _ptr(yb), _ptr(xhat),
+                                _ptr(rstd), _stream(a)), "fs2_res_ln_fwd")
+    return y, yb, xhat, rstd
+
+
+def res_ln_bwd(dy, xhat, rstd, gamma, lens=None, p_drop=0.0, seed=None, salt=0, dgamma=None, dbeta=None, dbias=None,
+               want_dbias=True, accumulate=False):
+    """Backward of :func:`res_ln_fwd` (fs2_res_ln_bwd): returns (dres f32, da bf16, dgamma, dbeta,
+    dbias) — dbias is the bias gradient of the conv that produced a (None unless wanted / given);
+    accumulate adds into the given dgamma / dbeta / dbias."""
+    _gpu(dy, xhat, rstd, gamma, lens, seed)
+    B, T, D = xhat.shape
+    dy = dy.contiguous()
+    dres = torch.empty_like(xhat)
+    da = torch.empty(xhat.shape, device=xhat.device, dtype=torch.bfloat16)
+    new = lambda: torch.empty(D, device=xhat.device, dtype=torch.float32)
+    dgamma = new() if dgamma is None else dgamma
+    dbeta = new() if dbeta is None else dbeta
+    if dbias is None and want_dbias:
+        dbias = new()
+    ws = torch.empty(_lib.fs2_res_ln_bwd_ws_bytes(D) // 4, device=xhat.device, dtype=torch.float32)
+    L.check(_lib.fs2_res_ln_bwd(_ptr(dy), _ptr(xhat), _ptr(rstd), _ptr(gamma), _ptr(lens), B * T, T, D,
+                                float(p_drop), _ptr(seed), int(salt), _ptr(dres), _ptr(da), _ptr(dgamma), _ptr(dbeta),
+                                _ptr(dbias), 1 if accumulate else 0, _ptr(ws), ws.numel() * 4, _stream(xhat)),
+            "fs2_res_ln_bwd")
+    return dres, da, dgamma, dbeta, dbias
+
+
+def colsum(x, out=None, accumulate=False):
+    """out[n] (+)= sum over rows of x [..., N] (f32 / bf16), deterministic (fs2_colsum)."""
+    _gpu(x, out)
+    N = x.shape[-1]
+    x2 = x.reshape(-1, N)
+    if out is None:
+        out = torch.empty(N, device=x.device, dtype=torch.float32)
+    ws = torch.empty(_lib.fs2_colsum_ws_bytes(N) // 4, device=x.device, dtype=torch.float32)
+    L.check(_lib.fs2_colsum(_ptr(x2), _dt(x2), x2.shape[0], N, _rows(x2, "x"), _ptr(out), 1 if accumulate else 0,
+                            _ptr(ws), ws.numel() * 4, _stream(x)), "fs2_colsum")
+    return out
+
+
+def conv_wgrad(dy, x, ks, pad, dw=None, db=None, want_db=False, accumulate=False, parts=None):
+    """Conv1d weight gradient (fs2_conv_wgrad): dy [B, T, N] f32 / bf16, x [B, T, C] bf16 ->
+    dw f32 [N, C, ks] (and db f32 [N] when want_db / db given); accumulate adds into dw / db.
+    parts = ([dw_0, dw_1(, dw_2)], [db_0, ...] or None): N split into equal row parts written to
+    separate tensors (Q / K / V); dw / db are then ignored."""
+    _gpu(dy, x, dw, db)
+    B, T, N = dy.shape
+    C = x.shape[-1]
+    assert x.shape[:2] == (B, T) and x.dtype == torch.bfloat16
+    split, extra = 0, [None] * 4
+    if parts is not None:
+        dws, dbs = parts
+        split = N // len(dws)
+        for t in dws:
+            assert t.is_contiguous() and t.numel() == split * C * ks and t.dtype == torch.float32
+        dw = dws[0]
+        db = dbs[0] if dbs is not None else None
+        extra = [dws[1], dws[2] if len(dws) > 2 else None,
+                 dbs[1] if dbs is not None else None, dbs[2] if dbs is not None and len(dbs) > 2 else None]
+    else:
+        if dw is None:
+            dw = torch.empty(N, C, ks, device=dy.device, dtype=torch.float32)
+        if db is None and want_db:
+            db = torch.empty(N, device=dy.device, dtype=torch.float32)
+        assert dw.is_contiguous() and dw.numel() == N * C * ks and dw.dtype == torch.float32
+    ws = torch.empty(max(1, _lib.fs2_conv_wgrad_ws_bytes(B, T, N, C, ks) // 4), device=dy.device, dtype=torch.float32)
+    L.check(_lib.fs2_conv_wgrad(_ptr(dy), _dt(dy), _rows(dy, "dy"), _ptr(x), _rows(x, "x"), B, T, N, C, ks, pad,
+                                _ptr(dw), _ptr(db), 1 if accumulate else 0, split, *[_ptr(t) for t in extra],
+                                _ptr(ws), ws.numel() * 4, _stream(dy)), "fs2_conv_wgrad")
+    return dw, db

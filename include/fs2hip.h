@@ -53,6 +53,9 @@ enum fs2_epilogue {
   FS2_EPI_RES_SUM = 8,     /* y = (acc + bias + residual [+ residual2]) / out_div
                               (ResBlock residual x = xt + x :104; the multi-receptive-field sum
                               xs += resblock(x), x = xs / num_kernels, hifigan/models.py:152-158) */
+  FS2_EPI_RELU_GRAD = 9,   /* y = (residual > 0) ? acc + bias : 0
+                              (training backward through the FFN's relu, SubLayers.py:88: the
+                              input gradient of w_2 masked by the saved relu output)           */
 };
 
 /*
@@ -523,6 +526,40 @@ int fs2_seq_layout(const int64_t *lens, int B, int T, int32_t *cu, int32_t *row_
 int fs2_hifigan_mrf(const void *x, const void *x_act, const void *w, const float *bias, int B, int T, int C,
                     float out_slope, void *out, fs2_stream_t stream);
 int64_t fs2_hifigan_mrf_weight_elems(int C);
+
+/*
+ * Training-step kernels (train.py step; training.py's FFTBlockFn / Conv1dFn backward):
+ * fs2_res_ln_fwd — y = masked_fill(LayerNorm(dropout(a, p_drop) + res), t >= lens[b], 0) over
+ *   R = B*T rows of D = 256 (transformer/SubLayers.py:54-57,90-93, Layers.py:27-30): a f32, res
+ *   f32 or bf16, y f32 (+ optional bf16 copy y_bf), saved xhat f32 [R, D] and rstd f32 [R]. Dropout
+ *   keep bits are a counter hash of (*seed, salt, row, column) (seed: one device int64, may be
+ *   advanced between steps inside a captured graph); p_drop = 0 -> no dropout (seed unused).
+ * fs2_res_ln_bwd — its backward: dres = dLN (f32 [R, D]), da = dres * keep / (1 - p) (bf16 [R, D]),
+ *   dgamma, dbeta f32 [D] and dbias f32 [D] (optional: sum over rows of da = the producing conv's
+ *   bias gradient); accumulate != 0 adds into them. Deterministic (fixed-order partial sums in ws).
+ * fs2_colsum — out[n] (+)= sum over R rows of x[r, n] (f32 or bf16), deterministic.
+ * fs2_conv_wgrad — Conv1d weight gradient without an unfolded copy:
+ *   dw[n][c][k] (+)= sum_{b,t} dy[b,t,n] x[b, t+k-pad, c] (x zero outside [0, T) per sequence),
+ *   db[n] (+)= sum dy[b,t,n] (optional); dy f32 or bf16 [B*T, N], x bf16 [B*T, C], KS in
+ *   {1, 3, 5, 9}, N and C multiples of 8. MFMA bf16, f32 accumulation, deterministic.
+ *   split_rows > 0: rows [i*split_rows, (i+1)*split_rows) of dw / db go to (dw, dw1, dw2)[i] /
+ *   (db, db1, db2)[i] (2 or 3 parts: the separate Q, K, V parameters of one fused projection).
+ */
+int fs2_res_ln_fwd(const float *a, const void *res, int res_dtype, const float *gamma, const float *beta,
+                   const int64_t *lens, int64_t R, int T, int D, float eps, float p_drop, const int64_t *seed,
+                   int salt, float *y, void *y_bf, float *xhat, float *rstd, fs2_stream_t stream);
+int64_t fs2_res_ln_bwd_ws_bytes(int D);
+int fs2_res_ln_bwd(const float *dy, const float *xhat, const float *rstd, const float *gamma, const int64_t *lens,
+                   int64_t R, int T, int D, float p_drop, const int64_t *seed, int salt, float *dres, void *da,
+                   float *dgamma, float *dbeta, float *dbias, int accumulate, float *ws, int64_t ws_bytes,
+                   fs2_stream_t stream);
+int64_t fs2_colsum_ws_bytes(int N);
+int fs2_colsum(const void *x, int dtype, int64_t R, int N, int64_t row_stride, float *out, int accumulate, float *ws,
+               int64_t ws_bytes, fs2_stream_t stream);
+int64_t fs2_conv_wgrad_ws_bytes(int B, int T, int N, int C, int KS);
+int fs2_conv_wgrad(const void *dy, int dy_dtype, int64_t dy_row_stride, const void *x, int64_t x_row_stride, int B,
+                   int T, int N, int C, int KS, int pad, float *dw, float *db, int accumulate, int split_rows,
+                   float *dw1, float *dw2, float *db1, float *db2, float *ws, int64_t ws_bytes, fs2_stream_t stream);
 
 /* Library identification. */
 const char *fs2_version(void);

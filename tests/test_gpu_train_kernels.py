@@ -1,0 +1,178 @@
+"""Training-step kernels (train.hip + the conv's FS2_EPI_RELU_GRAD epilogue) against float64
+PyTorch statements of the same ops, through the C ABI.
+
+* fs2_res_ln_fwd / fs2_res_ln_bwd: masked_fill(LayerNorm(dropout(a) + res)) and its autograd
+  gradient (transformer/SubLayers.py:54-57,90-93, Layers.py:27-30). f32 throughout: outputs within
+  2e-5 of the output scale; da (stored bf16) within 1e-2 relative. With dropout the keep mask is
+  read back from the kernel itself (a = 1, res = 0: xhat > 0 exactly on kept elements) and the
+  reference is evaluated with that mask; the keep fraction must be 1 - p within 1 %.
+* fs2_colsum: float64 column sums, 1e-5 relative.
+* fs2_conv_wgrad: dW[n, c, k] = sum dy[t, n] x[t + k - pad, c] per sequence, from the bf16-rounded
+  operands in float64 (the kernel's MFMA products are exact, f32 accumulation): 2e-4 of the
+  gradient scale. Sequence edges, T not a multiple of the 32-row chunk, N / C = 80 partial tiles,
+  f32 and bf16 dy, bias gradient, accumulation and Q|K|V row parts.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from fs2amd import ops as o
+    return o
+
+
+def _mask(lens, T):
+    return torch.arange(T)[None, :] >= lens[:, None]
+
+
+def _keep_mask(ops, B, T, p, seed, salt):
+    ones = torch.ones(B, T, 256, device=DEV)
+    g, b = torch.ones(256, device=DEV), torch.zeros(256, device=DEV)
+    _, _, xh, _ = ops.res_ln_fwd(ones, torch.zeros_like(ones), g, b, 1e-5, None, p, seed, salt, want_bf16=False)
+    return (xh > 0).cpu()
+
+
+@pytest.mark.parametrize("p,res_bf16", [(0.0, False), (0.2, False), (0.1, True)])
+def test_res_ln_fwd_bwd(ops, p, res_bf16):
+    torch.manual_seed(1)
+    B, T, D = 5, 37, 256
+    lens = torch.tensor([37, 20, 1, 0, 33])
+    a = torch.randn(B, T, D)
+    res = torch.randn(B, T, D)
+    if res_bf16:
+        res = res.to(torch.bfloat16).float()
+    gam, bet = 1 + 0.1 * torch.randn(D), 0.1 * torch.randn(D)
+    seed = torch.tensor([1234567], dtype=torch.int64, device=DEV)
+    salt = 7
+    y, yb, xh, rs = ops.res_ln_fwd(a.to(DEV), (res.to(torch.bfloat16) if res_bf16 else res).to(DEV), gam.to(DEV),
+                                   bet.to(DEV), 1e-5, lens.to(DEV), p, seed, salt)
+    keep = _keep_mask(ops, B, T, p, seed, salt) if p > 0 else torch.ones(B, T, D, dtype=torch.bool)
+    if p > 0:
+        assert abs(float(keep.float().mean()) - (1 - p)) < 0.01
+    ad, rd = a.double().requires_grad_(), res.double().requires_grad_()
+    v = ad * keep / (1 - p) + rd
+    ref = F.layer_norm(v, (D,), gam.double(), bet.double(), 1e-5).masked_fill(_mask(lens, T)[..., None], 0)
+    torch.cuda.synchronize()
+    scale = float(ref.abs().max())
+    assert float((y.cpu().double() - ref).abs().max()) <= 2e-5 * scale
+    assert float((yb.cpu().double() - ref).abs().max()) <= 1e-2 * scale
+    dy = torch.randn(B, T, D)
+    gd, bd = gam.double().requires_grad_(), bet.double().requires_grad_()
+    ref2 = F.layer_norm(v, (D,), gd, bd, 1e-5).masked_fill(_mask(lens, T)[..., None], 0)
+    ref2.backward(dy.double())
+    # a's producer is a conv with a bias: its gradient is sum over rows of da
+    dres, da, dg, dbe, dbias = ops.res_ln_bwd(dy.to(DEV), xh, rs, gam.to(DEV), lens.to(DEV), p, seed, salt)
+    torch.cuda.synchronize()
+    sc = float(rd.grad.abs().max())
+    assert float((dres.cpu().double() - rd.grad).abs().max()) <= 2e-5 * sc
+    assert float((da.cpu().double() - ad.grad).abs().max()) <= 1e-2 * float(ad.grad.abs().max())
+    assert torch.allclose(dg.cpu().double(), gd.grad, rtol=1e-4, atol=1e-4 * float(gd.grad.abs().max()))
+    assert torch.allclose(dbe.cpu().double(), bd.grad, rtol=1e-4, atol=1e-4 * float(bd.grad.abs().max()))
+    dsum = ad.grad.sum((0, 1))
+    assert torch.allclose(dbias.cpu().double(), dsum, rtol=1e-3, atol=1e-4 * float(dsum.abs().max()))
+    # accumulate: a second call adds
+    ops.res_ln_bwd(dy.to(DEV), xh, rs, gam.to(DEV), lens.to(DEV), p, seed, salt, dgamma=dg, dbeta=dbe, dbias=dbias,
+                   accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.allclose(dg.cpu().double(), 2 * gd.grad, rtol=1e-4, atol=2e-4 * float(gd.grad.abs().max()))
+
+
+def test_res_ln_seed_advances_mask(ops):
+    seed = torch.tensor([5], dtype=torch.int64, device=DEV)
+    k1 = _keep_mask(ops, 2, 16, 0.3, seed, 3)
+    k1b = _keep_mask(ops, 2, 16, 0.3, seed, 3)
+    seed.add_(1)
+    k2 = _keep_mask(ops, 2, 16, 0.3, seed, 3)
+    k3 = _keep_mask(ops, 2, 16, 0.3, seed, 4)
+    assert torch.equal(k1, k1b)
+    assert not torch.equal(k1, k2) and not torch.equal(k2, k3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_colsum(ops, dtype):
+    torch.manual_seed(2)
+    x = torch.randn(3, 1111, 768).to(dtype)
+    out = ops.colsum(x.to(DEV))
+    torch.cuda.synchronize()
+    ref = x.double().sum((0, 1))
+    assert torch.allclose(out.cpu().double(), ref, rtol=1e-5, atol=1e-4)
+    out2 = ops.colsum(x.to(DEV), out=out.clone(), accumulate=True)
+    assert torch.allclose(out2.cpu().double(), 2 * ref, rtol=1e-5, atol=2e-4)
+
+
+def _ref_wgrad(dy, x, ks, pad):
+    # dW[n, c, k] = sum_{b,t} dy[b,t,n] x[b,t+k-pad,c]   (x zero outside [0, T))
+    B, T, N = dy.shape
+    C = x.shape[-1]
+    xp = F.pad(x.double(), (0, 0, pad, ks - 1 - pad))
+    xu = xp.unfold(1, ks, 1)  # [B, T, C, ks]
+    return torch.einsum("btn,btck->nck", dy.double(), xu)
+
+
+@pytest.mark.parametrize("N,C,ks,pad,T,dy_f32", [
+    (1024, 256, 9, 4, 93, False),   # FFN w_1
+    (256, 1024, 1, 0, 70, False),   # FFN w_2
+    (768, 256, 1, 0, 64, True),     # Q|K|V (dqkv f32 from the attention backward)
+    (256, 256, 3, 1, 45, False),    # VariancePredictor conv
+    (512, 80, 5, 2, 40, False),     # PostNet first conv
+    (80, 512, 5, 2, 33, True),      # PostNet last conv
+    (80, 256, 1, 0, 17, False),     # mel_linear
+])
+def test_conv_wgrad(ops, N, C, ks, pad, T, dy_f32):
+    torch.manual_seed(N + C + ks)
+    B = 3
+    dy = torch.randn(B, T, N)
+    dy = dy if dy_f32 else dy.to(torch.bfloat16)
+    x = torch.randn(B, T, C).to(torch.bfloat16)
+    dw, db = ops.conv_wgrad(dy.to(DEV), x.to(DEV), ks, pad, want_db=True)
+    torch.cuda.synchronize()
+    dyr = dy.to(torch.bfloat16) if dy_f32 else dy   # the kernel's MFMA operands are bf16
+    ref = _ref_wgrad(dyr, x, ks, pad)
+    sc = float(ref.abs().max())
+    err = float((dw.cpu().double() - ref).abs().max())
+    assert err <= 2e-4 * sc, (err, sc)
+    dbr = dy.double().sum((0, 1))
+    assert torch.allclose(db.cpu().double(), dbr, rtol=1e-4, atol=1e-4 * float(dbr.abs().max()))
+    dw2, db2 = ops.conv_wgrad(dy.to(DEV), x.to(DEV), ks, pad, dw=dw.clone(), db=db.clone(), accumulate=True)
+    torch.cuda.synchronize()
+    assert float((dw2.cpu().double() - 2 * ref).abs().max()) <= 4e-4 * sc
+
+
+def test_conv_wgrad_qkv_parts(ops):
+    torch.manual_seed(3)
+    B, T, N, C = 2, 50, 768, 256
+    dy = torch.randn(B, T, N)
+    x = torch.randn(B, T, C).to(torch.bfloat16)
+    dws = [torch.full((256, 256), 1.0, device=DEV) for _ in range(3)]
+    dbs = [torch.full((256,), 1.0, device=DEV) for _ in range(3)]
+    ops.conv_wgrad(dy.to(DEV), x.to(DEV), 1, 0, parts=(dws, dbs), accumulate=True)
+    torch.cuda.synchronize()
+    ref = _ref_wgrad(dy.to(torch.bfloat16), x, 1, 0)[..., 0] + 1.0
+    dbr = dy.double().sum((0, 1)) + 1.0
+    for i in range(3):
+        assert float((dws[i].cpu().double() - ref[256 * i:256 * (i + 1)]).abs().max()) <= 2e-4 * float(ref.abs().max())
+        assert torch.allclose(dbs[i].cpu().double(), dbr[256 * i:256 * (i + 1)], rtol=1e-4, atol=1e-3)
+
+
+def test_conv_relu_grad_epilogue(ops):
+    """FS2_EPI_RELU_GRAD: the input gradient of w_2 (its transposed conv) masked by relu(u) > 0."""
+    from fs2amd import _lib as L
+    torch.manual_seed(4)
+    B, T, Cin, N = 2, 61, 256, 1024
+    d = torch.randn(B, T, Cin).to(torch.bfloat16)
+    w = torch.randn(N, Cin) / 16
+    u = torch.relu(torch.randn(B, T, N)).to(torch.bfloat16)
+    wp = ops.pack_conv_weight(w.to(DEV), L.FS2_BF16)
+    out = ops.conv1d(d.to(DEV), wp, None, cin=Cin, ks=1, pad=0, compute=L.FS2_BF16, epilogue=L.EPI_RELU_GRAD,
+                     out_dtype=L.FS2_BF16, residual=u.to(DEV))
+    torch.cuda.synchronize()
+    ref = (d.double() @ w.to(torch.bfloat16).double().t()) * (u.double() > 0)
+    assert float((out.cpu().double() - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
+    assert bool(((out.cpu() == 0) | (u > 0)).all())
