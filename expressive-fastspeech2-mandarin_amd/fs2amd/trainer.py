@@ -28,6 +28,7 @@ import torch.nn as nn
 from .data import loss_inputs
 from .loss import FastSpeech2Loss
 from .optimizer import ScheduledOptim
+from .training import grad_sink
 
 
 class TrainStep:
@@ -179,7 +180,8 @@ class TrainStep:
             self._sync_buffers()
         output = self.net(**batch)
         losses = self.loss(loss_inputs(batch), output)
-        (losses[0] / self.grad_acc_step).backward()
+        with grad_sink():
+            (losses[0] / self.grad_acc_step).backward()
         self._acc_pending += 1
         if self.step_no % self.grad_acc_step == 0:
             self._reduce_grads()
@@ -195,7 +197,8 @@ class TrainStep:
         self._sync_buffers()
         output = self.net(**batch)
         losses = self.loss(loss_inputs(batch), output)
-        losses[0].backward()
+        with grad_sink():  # the fused blocks accumulate straight into the flat buffer's views
+            losses[0].backward()
         self._reduce_grads()
         nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip_thresh)
         self.optimizer._optimizer.step()

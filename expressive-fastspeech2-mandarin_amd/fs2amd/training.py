@@ -62,6 +62,11 @@ class Conv1dFn(torch.autograd.Function):
                 wtp = ops.pack_conv_weight(w3.flip(-1).transpose(0, 1), compute)
             dx = ops.conv1d(dyc, wtp, None, cin=N, ks=KS, pad=KS - 1 - pad,
                             compute=compute, epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+        if ctx.needs_input_grad[1] and _wgrad_kernel_ok(compute, N, Cin, KS, xc):
+            # fs2_conv_wgrad: no unfolded copy of x, the bias gradient from the same pass
+            dw, db = ops.conv_wgrad(dyc, xc, KS, pad, want_db=ctx.has_bias and ctx.needs_input_grad[2])
+            dw = dw.view(N, Cin) if ctx.linear else dw
+            return dx, dw, db, None, None
         if ctx.needs_input_grad[1]:
             B, T, _ = xc.shape
             if KS == 1:
@@ -74,6 +79,12 @@ class Conv1dFn(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum((0, 1))
         return dx, dw, db, None, None
+
+
+def _wgrad_kernel_ok(compute, N, Cin, KS, xc):
+    import os
+    return (compute == L.FS2_BF16 and xc.is_cuda and xc.dim() == 3 and KS in (1, 3, 5, 9) and N % 8 == 0
+            and Cin % 8 == 0 and xc.shape[-1] == Cin and os.environ.get("FS2_WGRAD_KERNEL", "1") != "0")
 
 
 def _wgrad_chunks(rows, B, N, K):
@@ -153,6 +164,150 @@ def fft_block(blk, x, mask, lens, p_drop, training, compute):
     return _layer_norm(y + h, f.layer_norm).masked_fill(mask.unsqueeze(-1), 0)
 
 
+# ---- the FFT block as one autograd node on the training kernels (train.hip) -------------------------
+_SINK = [False]
+
+
+class grad_sink:
+    """Inside: FFTBlockFn writes its parameter gradients straight into the existing ``p.grad``
+    tensors (accumulating: the trainer's flat buffer, zeroed at the start of the step) and hands
+    autograd nothing for them — no per-parameter AccumulateGrad add. Only for the flat-gradient
+    step (TrainStep(graph=True / flat_grads=True)); DDP needs its autograd hooks."""
+
+    def __enter__(self):
+        self.prev = _SINK[0]
+        _SINK[0] = True
+
+    def __exit__(self, *exc):
+        _SINK[0] = self.prev
+
+
+def fused_block_on(blk, compute):
+    """FS2_TRAIN_FUSED=0 restores the per-op autograd form (Conv1dFn / AttentionFn / torch)."""
+    import os
+    if os.environ.get("FS2_TRAIN_FUSED", "1") == "0" or compute != L.FS2_BF16:
+        return False
+    f = blk.pos_ffn
+    return (blk.slf_attn.w_qs.in_features == 256 and f.w_1.kernel_size[0] in (1, 3, 5, 9)
+            and f.w_2.kernel_size[0] in (1, 3, 5, 9) and f.w_1.out_channels % 8 == 0)
+
+
+def _block_params(blk):
+    a, f = blk.slf_attn, blk.pos_ffn
+    return [a.w_qs.weight, a.w_qs.bias, a.w_ks.weight, a.w_ks.bias, a.w_vs.weight, a.w_vs.bias, a.fc.weight, a.fc.bias,
+            a.layer_norm.weight, a.layer_norm.bias, f.w_1.weight, f.w_1.bias, f.w_2.weight, f.w_2.bias,
+            f.layer_norm.weight, f.layer_norm.bias]
+
+
+def _packT(w):
+    """Input-gradient weight of a conv [N, Cin, KS] (Linear [N, Cin]): the conv of dy with taps
+    flipped and W transposed, packed [Cin][KS][N] bf16."""
+    w3 = w if w.dim() == 3 else w.unsqueeze(-1)
+    return torch.empty(w3.shape[1], w3.shape[2], w3.shape[0], dtype=torch.bfloat16, device=w.device).copy_(
+        w3.detach().flip(-1).permute(1, 2, 0))
+
+
+class FFTBlockFn(torch.autograd.Function):
+    """transformer/Layers.py:21-30 (MHA SubLayers.py:29-57, FFN :85-93) in train mode as one node:
+    forward Q|K|V conv (bf16 out) -> fs2_attention -> fc conv -> fs2_res_ln_fwd (dropout +
+    residual + LN + mask) -> w_1 conv (relu, bf16 out) -> w_2 conv -> fs2_res_ln_fwd; backward
+    fs2_res_ln_bwd (+ the conv bias gradient) -> w_2 input gradient with the relu mask in its
+    epilogue (FS2_EPI_RELU_GRAD) -> w_1 input gradient + residual gradient in one epilogue ->
+    fs2_res_ln_bwd -> fc input gradient -> fs2_attention_bwd -> Q|K|V input gradient + residual;
+    every weight gradient on fs2_conv_wgrad (no unfolded copies). Returns (y f32, y bf16): the
+    bf16 copy is the next block's MFMA input (not differentiable)."""
+
+    @staticmethod
+    def forward(ctx, x, x_bf, lens, seed, meta, *params):
+        blk, p_drop, salt = meta
+        (wq, bq, wk, bk, wv, bv, wfc, bfc, g1, be1, w1, b1, w2, b2, g2, be2) = params
+        a, f = blk.slf_attn, blk.pos_ffn
+        H, dk = a.n_head, a.d_k
+        temp = float(np.power(dk, 0.5))
+        k1, k2 = f.w_1.kernel_size[0], f.w_2.kernel_size[0]
+        BF = L.FS2_BF16
+        xb = x_bf if x_bf is not None else x.to(torch.bfloat16)
+        wqkv = torch.cat([wq, wk, wv], 0).detach()
+        qkv = ops.conv1d(xb, ops.pack_conv_weight(wqkv, BF), torch.cat([bq, bk, bv]).detach(), cin=256, ks=1, pad=0,
+                         compute=BF, epilogue=L.EPI_BIAS, out_dtype=BF)
+        att = ops.attention(qkv, lens, H, dk, temp)
+        a1 = ops.conv1d(att, ops.pack_conv_weight(wfc, BF), bfc.detach(), cin=256, ks=1, pad=0, compute=BF,
+                        epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+        h, hb, xh1, rs1 = ops.res_ln_fwd(a1, x.contiguous(), g1.detach(), be1.detach(), a.layer_norm.eps, lens,
+                                         p_drop, seed, salt)
+        u = ops.conv1d(hb, ops.pack_conv_weight(w1, BF), b1.detach(), cin=256, ks=k1, pad=(k1 - 1) // 2, compute=BF,
+                       epilogue=L.EPI_BIAS_RELU, out_dtype=BF)
+        a2 = ops.conv1d(u, ops.pack_conv_weight(w2, BF), b2.detach(), cin=w2.shape[1], ks=k2, pad=(k2 - 1) // 2,
+                        compute=BF, epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+        y, yb, xh2, rs2 = ops.res_ln_fwd(a2, h, g2.detach(), be2.detach(), f.layer_norm.eps, lens, p_drop, seed,
+                                         salt + 1)
+        ctx.save_for_backward(xb, qkv, att, hb, u, xh1, rs1, xh2, rs2, lens, *params)
+        ctx.packT = (_packT(wqkv), _packT(wfc), _packT(w1), _packT(w2))
+        ctx.meta = (H, dk, temp, k1, k2, p_drop, salt, seed)
+        ctx.mark_non_differentiable(yb)
+        return y, yb
+
+    @staticmethod
+    def backward(ctx, dy, _dyb):
+        xb, qkv, att, hb, u, xh1, rs1, xh2, rs2, lens, *params = ctx.saved_tensors
+        (wq, bq, wk, bk, wv, bv, wfc, bfc, g1, be1, w1, b1, w2, b2, g2, be2) = params
+        H, dk, temp, k1, k2, p_drop, salt, seed = ctx.meta
+        wqkvT, wfcT, w1T, w2T = ctx.packT
+        BF = L.FS2_BF16
+        sink = _SINK[0] and all(p.grad is not None for p in params)
+        acc = sink
+        G = (lambda p: p.grad) if sink else (lambda p: None)
+        pad1, pad2 = (k1 - 1) // 2, (k2 - 1) // 2
+        F_ = w1.shape[0]
+        # FFN: LN backward, w_2 gradients, relu-masked input gradient, w_1 gradients, + residual
+        dres2, da2, dg2, dbe2, db2 = ops.res_ln_bwd(dy, xh2, rs2, g2.detach(), lens, p_drop, seed, salt + 1,
+                                                    dgamma=G(g2), dbeta=G(be2), dbias=G(b2), accumulate=acc)
+        dw2, _ = ops.conv_wgrad(da2, u, k2, pad2, dw=G(w2), accumulate=acc)
+        du = ops.conv1d(da2, w2T, None, cin=256, ks=k2, pad=k2 - 1 - pad2, compute=BF, epilogue=L.EPI_RELU_GRAD,
+                        out_dtype=BF, residual=u)
+        dw1, db1 = ops.conv_wgrad(du, hb, k1, pad1, dw=G(w1), db=G(b1), want_db=True, accumulate=acc)
+        dh = ops.conv1d(du, w1T, None, cin=F_, ks=k1, pad=k1 - 1 - pad1, compute=BF, epilogue=L.EPI_BIAS_RES,
+                        out_dtype=L.FS2_F32, residual=dres2)
+        # attention sub-layer
+        dres1, da1, dg1, dbe1, dbfc = ops.res_ln_bwd(dh, xh1, rs1, g1.detach(), lens, p_drop, seed, salt,
+                                                     dgamma=G(g1), dbeta=G(be1), dbias=G(bfc), accumulate=acc)
+        dwfc, _ = ops.conv_wgrad(da1, att, 1, 0, dw=G(wfc), accumulate=acc)
+        datt = ops.conv1d(da1, wfcT, None, cin=256, ks=1, pad=0, compute=BF, epilogue=L.EPI_BIAS,
+                          out_dtype=L.FS2_F32)
+        dqkv = ops.attention_bwd(qkv, att, datt, lens, H, dk, temp)
+        if sink:
+            ops.conv_wgrad(dqkv, xb, 1, 0, parts=([wq.grad, wk.grad, wv.grad], [bq.grad, bk.grad, bv.grad]),
+                           accumulate=True)
+            gq = [None] * 6
+        else:
+            dws = [torch.empty_like(w) for w in (wq, wk, wv)]
+            dbs = [torch.empty_like(b) for b in (bq, bk, bv)]
+            ops.conv_wgrad(dqkv, xb, 1, 0, parts=(dws, dbs))
+            gq = [dws[0], dbs[0], dws[1], dbs[1], dws[2], dbs[2]]
+        dx = ops.conv1d(dqkv.to(torch.bfloat16), wqkvT, None, cin=3 * H * dk, ks=1, pad=0, compute=BF,
+                        epilogue=L.EPI_BIAS_RES, out_dtype=L.FS2_F32, residual=dres1)
+        if sink:
+            grads = gq + [None] * 10
+        else:
+            grads = gq + [dwfc.view_as(wfc), dbfc, dg1, dbe1, dw1.view_as(w1), db1, dw2.view_as(w2), db2, dg2, dbe2]
+        return (dx, None, None, None, None, *grads)
+
+
+def fft_block_fused(blk, x, x_bf, lens, seed, salt, p_drop):
+    y, yb = FFTBlockFn.apply(x, x_bf, lens, seed, (blk, float(p_drop), int(salt)), *_block_params(blk))
+    return y, yb
+
+
+def _train_seed(model, dev):
+    """The dropout seed of the fused blocks: one device int64 advanced once per forward (inside a
+    captured step too, so every replay draws new masks)."""
+    s = getattr(model, "_fs2_train_seed", None)
+    if s is None or s.device != dev:
+        s = torch.tensor([int(torch.randint(0, 2 ** 62, (1,)).item())], dtype=torch.int64, device=dev)
+        model._fs2_train_seed = s
+    return s
+
+
 def variance_predictor(vp, x, mask, training, compute):
     """model/modules.py:209-250 (conv1d_2 padding hard-coded to 1, :230)."""
     cl = vp.conv_layer
@@ -217,9 +372,18 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
     lens_src = src_lens.to(torch.int64).contiguous()
 
     # encoder (transformer/Models.py:73-100; training never recomputes the PE table)
+    fused = all(fused_block_on(b, compute) for b in list(enc.layer_stack) + list(dec.layer_stack))
+    if fused:
+        seed = _train_seed(model, dev)
+        if training:
+            seed.add_(1)
     x = enc.src_word_emb(texts) + enc.position_enc[:, :Lx, :]
-    for blk in enc.layer_stack:
-        x = fft_block(blk, x, src_masks, lens_src, tr["encoder_dropout"], training, compute)
+    xb = None
+    for i, blk in enumerate(enc.layer_stack):
+        if fused:
+            x, xb = fft_block_fused(blk, x, xb, lens_src, seed, 2 * i, tr["encoder_dropout"] if training else 0.0)
+        else:
+            x = fft_block(blk, x, src_masks, lens_src, tr["encoder_dropout"], training, compute)
     if model.speaker_emb is not None:
         x = x + model.speaker_emb(speakers).unsqueeze(1)
     if model.emotion_emb is not None:
@@ -254,8 +418,13 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
     x = x[:, :T] + dec.position_enc[:, :T, :]
     mel_masks = mel_masks[:, :T]
     dec_lens = torch.clamp((~mel_masks).sum(1), max=T)
-    for blk in dec.layer_stack:
-        x = fft_block(blk, x, mel_masks, dec_lens, tr["decoder_dropout"], training, compute)
+    xb = None
+    for i, blk in enumerate(dec.layer_stack):
+        if fused:
+            x, xb = fft_block_fused(blk, x.contiguous(), xb, dec_lens, seed, 2 * (len(enc.layer_stack) + i),
+                                    tr["decoder_dropout"] if training else 0.0)
+        else:
+            x = fft_block(blk, x, mel_masks, dec_lens, tr["decoder_dropout"], training, compute)
 
     # mel_linear + PostNet (+ residual) (fastspeech2.py:134-136, transformer/Layers.py:129-137)
     mel = linear(x, model.mel_linear, compute)
