@@ -662,3 +662,82 @@ extern "C" int fs2_conv_wgrad(const void *dy, int dy_dtype, int64_t dy_row_strid
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// All of a step's MFMA weight images in ONE launch (the FFT blocks' Q|K|V, fc, w_1, w_2): per
+// f32 weight [N][C][KS] (nn.Conv1d; Linear KS = 1) the forward image fwd bf16 [N_tot][KS][C] at row
+// n_off and the input-gradient image tr bf16 [C][KS][N_tot] (taps flipped, W transposed) at
+// column n_off; f32 descriptors copy a vector (Q|K|V biases) into one f32 buffer. 32 x 32 (n, c)
+// tiles; the transposed image goes through LDS so both stores are coalesced.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+__global__ __launch_bounds__(256) void pack_train_kernel(const fs2_pack_desc *__restrict__ descs, int nd) {
+  __shared__ float t[9][32][33];
+  int i = 0;
+  for (int j = 1; j < nd; ++j)
+    if (descs[j].blk0 <= (int)blockIdx.x) i = j;
+  const fs2_pack_desc d = descs[i];
+  const int tile = blockIdx.x - d.blk0;
+  const int tn = tile / d.tiles_c, tc = tile - tn * d.tiles_c;
+  const int cl = threadIdx.x & 31, nl0 = threadIdx.x >> 5;
+  const int c = tc * 32 + cl;
+  if (d.f32_copy) {  // vector copy: N elements at n_off
+    const int n = tile * 256 + threadIdx.x;
+    if (n < d.N) reinterpret_cast<float *>(d.fwd)[d.n_off + n] = d.src[n];
+    return;
+  }
+  const int KS = d.KS;
+  for (int r = 0; r < 4; ++r) {
+    const int nl = nl0 + 8 * r, n = tn * 32 + nl;
+    if (n < d.N && c < d.C) {
+      const float *s = d.src + ((int64_t)n * d.C + c) * KS;
+      for (int k = 0; k < KS; ++k) {
+        const float v = s[k];
+        if (d.fwd != nullptr) reinterpret_cast<bf16 *>(d.fwd)[((int64_t)(d.n_off + n) * KS + k) * d.C + c] = (bf16)v;
+        t[k][nl][cl] = v;
+      }
+    }
+  }
+  if (d.tr == nullptr) return;
+  __syncthreads();
+  const int nl = threadIdx.x & 31, cl0 = threadIdx.x >> 5;
+  const int n = tn * 32 + nl;
+  for (int r = 0; r < 4; ++r) {
+    const int clr = cl0 + 8 * r, cc = tc * 32 + clr;
+    if (n < d.N && cc < d.C)
+      for (int k = 0; k < KS; ++k)
+        reinterpret_cast<bf16 *>(d.tr)[((int64_t)cc * KS + k) * d.N_tot + d.n_off + n] = (bf16)t[KS - 1 - k][nl][clr];
+  }
+}
+
+}  // namespace
+
+extern "C" int fs2_pack_train_plan(fs2_pack_desc *descs, int nd, int *blocks) {
+  if (descs == nullptr || nd <= 0 || blocks == nullptr) return FS2_EINVAL;
+  int blk = 0;
+  for (int i = 0; i < nd; ++i) {
+    fs2_pack_desc &d = descs[i];
+    if (d.src == nullptr || (d.fwd == nullptr && d.tr == nullptr)) return FS2_EINVAL;
+    if (d.f32_copy) {
+      if (d.N <= 0 || d.tr != nullptr) return FS2_EINVAL;
+      d.tiles_c = 1;
+      d.blk0 = blk;
+      blk += (d.N + 255) / 256;
+      continue;
+    }
+    if (d.N <= 0 || d.C <= 0 || d.KS < 1 || d.KS > 9 || d.n_off < 0 || d.n_off + d.N > d.N_tot) return FS2_EINVAL;
+    d.tiles_c = (d.C + 31) / 32;
+    d.blk0 = blk;
+    blk += ((d.N + 31) / 32) * d.tiles_c;
+  }
+  *blocks = blk;
+  return FS2_OK;
+}
+
+extern "C" int fs2_pack_train(const fs2_pack_desc *descs_dev, int nd, int blocks, fs2_stream_t stream) {
+  if (descs_dev == nullptr || nd <= 0 || blocks <= 0) return FS2_EINVAL;
+  hipLaunchKernelGGL(pack_train_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), descs_dev, nd);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}

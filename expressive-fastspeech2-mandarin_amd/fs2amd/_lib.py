@@ -27,6 +27,13 @@ _i64 = ctypes.c_int64
 _f = ctypes.c_float
 
 
+class PackDesc(ctypes.Structure):
+    """Mirror of ``fs2_pack_desc`` (include/fs2hip.h)."""
+
+    _fields_ = [("src", _p), ("fwd", _p), ("tr", _p), ("N", _i), ("C", _i), ("KS", _i), ("n_off", _i),
+                ("N_tot", _i), ("f32_copy", _i), ("tiles_c", _i), ("blk0", _i)]
+
+
 class ConvDesc(ctypes.Structure):
     """Mirror of ``fs2_conv_desc`` (include/fs2hip.h)."""
 
@@ -139,6 +146,8 @@ SIGNATURES = {
     "fs2_hifigan_mrf_weight_elems": (ctypes.c_int64, [_i]),
     "fs2_res_ln_fwd": (_i, [_p, _p, _i, _p, _p, _p, _i64, _i, _i, _f, _f, _p, _i, _p, _p, _p, _p, _p]),
     "fs2_res_ln_bwd_ws_bytes": (_i64, [_i]),
+    "fs2_pack_train_plan": (_i, [_p, _i, _p]),
+    "fs2_pack_train": (_i, [_p, _i, _i, _p]),
     "fs2_res_ln_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p, _i, _p, _p, _p, _p, _p, _i, _p, _i64, _p]),
     "fs2_colsum_ws_bytes": (_i64, [_i]),
     "fs2_colsum": (_i, [_p, _i, _i64, _i, _i64, _p, _i, _p, _i64, _p]),

@@ -18,6 +18,9 @@ Where the arithmetic runs:
   * LayerNorm, dropout, BatchNorm, embeddings, losses: torch on the device.
 Parity: tests/test_gpu_train.py against the reference's own gradients (train_grads.npz).
 """
+import ctypes
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -207,6 +210,70 @@ def _packT(w):
         w3.detach().flip(-1).permute(1, 2, 0))
 
 
+class _TrainPack:
+    """Every FFT block's MFMA weight images (forward and input-gradient forms, Q|K|V fused, Q|K|V
+    bias concatenated) in persistent buffers, refreshed by ONE fs2_pack_train launch per forward
+    (captured with the step). Built outside graph capture; rebuilt if a parameter moved."""
+
+    def __init__(self, blocks, dev):
+        from . import _lib as LL
+        self.key = _pack_key(blocks)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        descs, self.per_block = [], []
+
+        def add(src, fwd=None, tr=None, N=0, C=1, KS=1, n_off=0, N_tot=0, f32=0):
+            d = LL.PackDesc()
+            d.src = src.data_ptr()
+            d.fwd = fwd.data_ptr() if fwd is not None else None
+            d.tr = tr.data_ptr() if tr is not None else None
+            d.N, d.C, d.KS, d.n_off, d.N_tot, d.f32_copy = N, C, KS, n_off, N_tot or N, f32
+            descs.append(d)
+
+        for blk in blocks:
+            a, f = blk.slf_attn, blk.pos_ffn
+            k1, k2, F_ = f.w_1.kernel_size[0], f.w_2.kernel_size[0], f.w_1.out_channels
+            D = a.w_qs.in_features
+            P = dict(qkv=torch.empty(3 * D, 1, D, **bf), qkvT=torch.empty(D, 1, 3 * D, **bf),
+                     bqkv=torch.empty(3 * D, dtype=torch.float32, device=dev),
+                     fc=torch.empty(D, 1, D, **bf), fcT=torch.empty(D, 1, D, **bf),
+                     w1=torch.empty(F_, k1, D, **bf), w1T=torch.empty(D, k1, F_, **bf),
+                     w2=torch.empty(D, k2, F_, **bf), w2T=torch.empty(F_, k2, D, **bf))
+            for j, lin in enumerate((a.w_qs, a.w_ks, a.w_vs)):
+                add(lin.weight, P["qkv"], P["qkvT"], D, D, 1, j * D, 3 * D)
+                add(lin.bias, P["bqkv"], None, D, 1, 1, j * D, 3 * D, f32=1)
+            add(a.fc.weight, P["fc"], P["fcT"], D, D, 1, 0, D)
+            add(f.w_1.weight, P["w1"], P["w1T"], F_, D, k1, 0, F_)
+            add(f.w_2.weight, P["w2"], P["w2T"], D, F_, k2, 0, D)
+            self.per_block.append(P)
+        n = len(descs)
+        arr = (LL.PackDesc * n)(*descs)
+        blocks_out = ctypes.c_int(0)
+        L.check(LL.load().fs2_pack_train_plan(arr, n, ctypes.byref(blocks_out)), "fs2_pack_train_plan")
+        raw = bytes(memoryview(arr).cast("B"))
+        self.dev_descs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+        self.n, self.grid = n, blocks_out.value
+
+    def run(self, stream_of):
+        from . import _lib as LL
+        L.check(LL.load().fs2_pack_train(ctypes.c_void_p(self.dev_descs.data_ptr()), self.n, self.grid,
+                                         ops._stream(stream_of)), "fs2_pack_train")
+
+
+def _pack_key(blocks):
+    return tuple(p.data_ptr() for b in blocks for p in _block_params(b))
+
+
+def _train_pack(model, blocks, dev):
+    """The model's _TrainPack (None while capturing before one exists: per-block packing then)."""
+    tp = getattr(model, "_fs2_train_pack", None)
+    if tp is not None and tp.key == _pack_key(blocks):
+        return tp
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    tp = model._fs2_train_pack = _TrainPack(blocks, dev)
+    return tp
+
+
 class FFTBlockFn(torch.autograd.Function):
     """transformer/Layers.py:21-30 (MHA SubLayers.py:29-57, FFN :85-93) in train mode as one node:
     forward Q|K|V conv (bf16 out) -> fs2_attention -> fc conv -> fs2_res_ln_fwd (dropout +
@@ -219,7 +286,7 @@ class FFTBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, x_bf, lens, seed, meta, *params):
-        blk, p_drop, salt = meta
+        blk, p_drop, salt, pk = meta
         (wq, bq, wk, bk, wv, bv, wfc, bfc, g1, be1, w1, b1, w2, b2, g2, be2) = params
         a, f = blk.slf_attn, blk.pos_ffn
         H, dk = a.n_head, a.d_k
@@ -227,22 +294,27 @@ class FFTBlockFn(torch.autograd.Function):
         k1, k2 = f.w_1.kernel_size[0], f.w_2.kernel_size[0]
         BF = L.FS2_BF16
         xb = x_bf if x_bf is not None else x.to(torch.bfloat16)
-        wqkv = torch.cat([wq, wk, wv], 0).detach()
-        qkv = ops.conv1d(xb, ops.pack_conv_weight(wqkv, BF), torch.cat([bq, bk, bv]).detach(), cin=256, ks=1, pad=0,
-                         compute=BF, epilogue=L.EPI_BIAS, out_dtype=BF)
+        if pk is None:  # per-block packing (no persistent pack yet)
+            wqkv = torch.cat([wq, wk, wv], 0).detach()
+            pk = dict(qkv=ops.pack_conv_weight(wqkv, BF), bqkv=torch.cat([bq, bk, bv]).detach(),
+                      fc=ops.pack_conv_weight(wfc, BF), w1=ops.pack_conv_weight(w1, BF),
+                      w2=ops.pack_conv_weight(w2, BF), qkvT=_packT(wqkv), fcT=_packT(wfc), w1T=_packT(w1),
+                      w2T=_packT(w2))
+        qkv = ops.conv1d(xb, pk["qkv"], pk["bqkv"], cin=256, ks=1, pad=0, compute=BF, epilogue=L.EPI_BIAS,
+                         out_dtype=BF)
         att = ops.attention(qkv, lens, H, dk, temp)
-        a1 = ops.conv1d(att, ops.pack_conv_weight(wfc, BF), bfc.detach(), cin=256, ks=1, pad=0, compute=BF,
-                        epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+        a1 = ops.conv1d(att, pk["fc"], bfc.detach(), cin=256, ks=1, pad=0, compute=BF, epilogue=L.EPI_BIAS,
+                        out_dtype=L.FS2_F32)
         h, hb, xh1, rs1 = ops.res_ln_fwd(a1, x.contiguous(), g1.detach(), be1.detach(), a.layer_norm.eps, lens,
                                          p_drop, seed, salt)
-        u = ops.conv1d(hb, ops.pack_conv_weight(w1, BF), b1.detach(), cin=256, ks=k1, pad=(k1 - 1) // 2, compute=BF,
+        u = ops.conv1d(hb, pk["w1"], b1.detach(), cin=256, ks=k1, pad=(k1 - 1) // 2, compute=BF,
                        epilogue=L.EPI_BIAS_RELU, out_dtype=BF)
-        a2 = ops.conv1d(u, ops.pack_conv_weight(w2, BF), b2.detach(), cin=w2.shape[1], ks=k2, pad=(k2 - 1) // 2,
-                        compute=BF, epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+        a2 = ops.conv1d(u, pk["w2"], b2.detach(), cin=w2.shape[1], ks=k2, pad=(k2 - 1) // 2, compute=BF,
+                        epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
         y, yb, xh2, rs2 = ops.res_ln_fwd(a2, h, g2.detach(), be2.detach(), f.layer_norm.eps, lens, p_drop, seed,
                                          salt + 1)
         ctx.save_for_backward(xb, qkv, att, hb, u, xh1, rs1, xh2, rs2, lens, *params)
-        ctx.packT = (_packT(wqkv), _packT(wfc), _packT(w1), _packT(w2))
+        ctx.packT = (pk["qkvT"], pk["fcT"], pk["w1T"], pk["w2T"])
         ctx.meta = (H, dk, temp, k1, k2, p_drop, salt, seed)
         ctx.mark_non_differentiable(yb)
         return y, yb
@@ -293,8 +365,8 @@ class FFTBlockFn(torch.autograd.Function):
         return (dx, None, None, None, None, *grads)
 
 
-def fft_block_fused(blk, x, x_bf, lens, seed, salt, p_drop):
-    y, yb = FFTBlockFn.apply(x, x_bf, lens, seed, (blk, float(p_drop), int(salt)), *_block_params(blk))
+def fft_block_fused(blk, x, x_bf, lens, seed, salt, p_drop, packed=None):
+    y, yb = FFTBlockFn.apply(x, x_bf, lens, seed, (blk, float(p_drop), int(salt), packed), *_block_params(blk))
     return y, yb
 
 
@@ -373,15 +445,22 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
 
     # encoder (transformer/Models.py:73-100; training never recomputes the PE table)
     fused = all(fused_block_on(b, compute) for b in list(enc.layer_stack) + list(dec.layer_stack))
+    packs = [None] * (len(enc.layer_stack) + len(dec.layer_stack))
     if fused:
         seed = _train_seed(model, dev)
         if training:
             seed.add_(1)
+        if os.environ.get("FS2_TRAIN_PACK", "1") != "0":
+            tp = _train_pack(model, list(enc.layer_stack) + list(dec.layer_stack), dev)
+            if tp is not None:
+                tp.run(texts)
+                packs = tp.per_block
     x = enc.src_word_emb(texts) + enc.position_enc[:, :Lx, :]
     xb = None
     for i, blk in enumerate(enc.layer_stack):
         if fused:
-            x, xb = fft_block_fused(blk, x, xb, lens_src, seed, 2 * i, tr["encoder_dropout"] if training else 0.0)
+            x, xb = fft_block_fused(blk, x, xb, lens_src, seed, 2 * i, tr["encoder_dropout"] if training else 0.0,
+                                    packs[i])
         else:
             x = fft_block(blk, x, src_masks, lens_src, tr["encoder_dropout"], training, compute)
     if model.speaker_emb is not None:
@@ -421,8 +500,9 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
     xb = None
     for i, blk in enumerate(dec.layer_stack):
         if fused:
-            x, xb = fft_block_fused(blk, x.contiguous(), xb, dec_lens, seed, 2 * (len(enc.layer_stack) + i),
-                                    tr["decoder_dropout"] if training else 0.0)
+            ne = len(enc.layer_stack)
+            x, xb = fft_block_fused(blk, x.contiguous(), xb, dec_lens, seed, 2 * (ne + i),
+                                    tr["decoder_dropout"] if training else 0.0, packs[ne + i])
         else:
             x = fft_block(blk, x, mel_masks, dec_lens, tr["decoder_dropout"], training, compute)
 

@@ -561,6 +561,26 @@ int fs2_conv_wgrad(const void *dy, int dy_dtype, int64_t dy_row_stride, const vo
                    int T, int N, int C, int KS, int pad, float *dw, float *db, int accumulate, int split_rows,
                    float *dw1, float *dw2, float *db1, float *db2, float *ws, int64_t ws_bytes, fs2_stream_t stream);
 
+/*
+ * fs2_pack_train_plan / fs2_pack_train — every MFMA weight image of a training step in one launch.
+ * Per descriptor (a host array completed by fs2_pack_train_plan, then copied to device memory
+ * for fs2_pack_train):
+ *   f32_copy = 0: src f32 [N][C][KS] -> fwd bf16 [N_tot][KS][C] rows n_off.. (optional) and
+ *                 tr bf16 [C][KS][N_tot] columns n_off.. with tr[c][k][n] = src[n][c][KS-1-k]
+ *                 (the input-gradient conv's weight; optional);
+ *   f32_copy = 1: src f32 [N] -> ((float *)fwd)[n_off + n] (a fused projection's bias).
+ * fs2_pack_train_plan fills tiles_c / blk0 and *blocks (the fs2_pack_train grid size).
+ */
+typedef struct fs2_pack_desc {
+  const float *src;
+  void *fwd;
+  void *tr;
+  int N, C, KS, n_off, N_tot, f32_copy;
+  int tiles_c, blk0; /* filled by fs2_pack_train_plan */
+} fs2_pack_desc;
+int fs2_pack_train_plan(fs2_pack_desc *descs, int nd, int *blocks);
+int fs2_pack_train(const fs2_pack_desc *descs_dev, int nd, int blocks, fs2_stream_t stream);
+
 /* Library identification. */
 const char *fs2_version(void);
 const char *fs2_status_string(int status);

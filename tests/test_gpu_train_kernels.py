@@ -176,3 +176,27 @@ def test_conv_relu_grad_epilogue(ops):
     ref = (d.double() @ w.to(torch.bfloat16).double().t()) * (u.double() > 0)
     assert float((out.cpu().double() - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
     assert bool(((out.cpu() == 0) | (u > 0)).all())
+
+
+def test_pack_train_images(ops):
+    """fs2_pack_train (one launch for every block's weight images) equals the per-weight torch
+    packing (pack_conv_weight / the flipped-transposed input-gradient form) bit for bit."""
+    from fs2amd import _lib as L
+    from fs2amd.model import _FFTBlock
+    from fs2amd.training import _TrainPack, _packT
+
+    torch.manual_seed(5)
+    blocks = [_FFTBlock(256, 2, 1024, (9, 1)).to(DEV), _FFTBlock(256, 2, 1024, (9, 3)).to(DEV)]
+    tp = _TrainPack(blocks, torch.device(DEV))
+    tp.run(torch.zeros(1, device=DEV))
+    torch.cuda.synchronize()
+    for blk, P in zip(blocks, tp.per_block):
+        a, f = blk.slf_attn, blk.pos_ffn
+        wqkv = torch.cat([a.w_qs.weight, a.w_ks.weight, a.w_vs.weight], 0).detach()
+        exp = dict(qkv=ops.pack_conv_weight(wqkv, L.FS2_BF16), fc=ops.pack_conv_weight(a.fc.weight, L.FS2_BF16),
+                   w1=ops.pack_conv_weight(f.w_1.weight, L.FS2_BF16), w2=ops.pack_conv_weight(f.w_2.weight, L.FS2_BF16),
+                   qkvT=_packT(wqkv), fcT=_packT(a.fc.weight), w1T=_packT(f.w_1.weight), w2T=_packT(f.w_2.weight),
+                   bqkv=torch.cat([a.w_qs.bias, a.w_ks.bias, a.w_vs.bias]).detach())
+        for k, v in exp.items():
+            assert P[k].shape == v.shape, k
+            assert torch.equal(P[k], v), k

@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
     lib = _lib.load()
     declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
-    assert len(declared) == len(_lib.SIGNATURES) == 38
+    assert len(declared) == len(_lib.SIGNATURES) == 40
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
@@ -59,7 +59,8 @@ int main(void){ P(x) P(x_row_stride) P(w) P(B) P(compute) P(residual) P(res_row_
 
 
 @pytest.mark.parametrize("cname,pyname", [("fs2_ffn_desc", "FfnDesc"), ("fs2_wconv_desc", "WconvDesc"),
-                                          ("fs2_vp_fused_desc", "VpFusedDesc"), ("fs2_ffn8_desc", "Ffn8Desc")])
+                                          ("fs2_vp_fused_desc", "VpFusedDesc"), ("fs2_ffn8_desc", "Ffn8Desc"),
+                                          ("fs2_pack_desc", "PackDesc")])
 def test_ffn_desc_layout_matches_header(cname, pyname):
     """ctypes mirrors of fs2_ffn_desc / fs2_wconv_desc have the C layout (every field's offset, and
     the size)."""
@@ -447,3 +448,22 @@ def test_pack_ffn_weights_layout():
             assert b[q, s_, bb, h, r, e] == w2[64 * q + 16 * bb + r, 32 * s_ + 8 * h + e, 0].to(torch.bfloat16)
         # a permutation: every weight exactly once
         assert torch.equal(p.float().sort().values, torch.cat([w1.reshape(-1), w2.reshape(-1)]).to(torch.bfloat16).float().sort().values)
+
+
+def test_pack_train_plan_on_host():
+    """fs2_pack_train_plan (host-only): workgroups per descriptor = 32 x 32 (n, c) tiles, 256
+    elements per f32 copy; invalid descriptors rejected."""
+    from fs2amd import _lib
+
+    lib = _lib.load()
+    arr = (_lib.PackDesc * 3)()
+    for d in arr:
+        d.src, d.fwd = 4096, 8192
+    arr[0].N, arr[0].C, arr[0].KS, arr[0].N_tot = 1024, 256, 9, 1024
+    arr[1].N, arr[1].C, arr[1].KS, arr[1].N_tot, arr[1].n_off = 256, 1024, 1, 512, 256
+    arr[2].N, arr[2].f32_copy = 768, 1
+    nb = ctypes.c_int(0)
+    assert lib.fs2_pack_train_plan(arr, 3, ctypes.byref(nb)) == _lib.FS2_OK
+    assert (arr[0].blk0, arr[1].blk0, arr[2].blk0) == (0, 256, 512) and nb.value == 515
+    arr[1].n_off = 300  # past N_tot
+    assert lib.fs2_pack_train_plan(arr, 3, ctypes.byref(nb)) == _lib.FS2_EINVAL
