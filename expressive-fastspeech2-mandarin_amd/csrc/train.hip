@@ -153,6 +153,108 @@ __global__ __launch_bounds__(256) void res_ln_bwd_kernel(const float *__restrict
   }
 }
 
+// VariancePredictor layer (model/modules.py:218-235, train mode): y = dropout(LN(relu(a))).
+// Saves xhat / rstd; the backward reads a again for the relu mask.
+__global__ __launch_bounds__(256) void relu_ln_fwd_kernel(const float *__restrict__ a, const float *__restrict__ gamma,
+                                                          const float *__restrict__ beta, int64_t R, float eps,
+                                                          uint32_t thr, float scale, const int64_t *seed, uint32_t salt,
+                                                          float *__restrict__ y, bf16 *__restrict__ y_bf,
+                                                          float *__restrict__ xhat, float *__restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane * 4;
+  const uint32_t key = drop_key(seed, salt);
+  float g[4], bt[4];
+  load4(gamma + c, g);
+  load4(beta + c, bt);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < R; row += nw) {
+    float v[4];
+    load4(a + row * kD + c, v);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.0f);
+    const float mean = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / kD);
+    float s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] -= mean;
+      s2 += v[q] * v[q];
+    }
+    const float rs = rsqrtf(wave_sum(s2) * (1.0f / kD) + eps);
+    float o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] *= rs;
+      o[q] = v[q] * g[q] + bt[q];
+    }
+    if (thr != 0) {
+      const unsigned k = keep4(key, (uint32_t)(row * kD + c), thr);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = ((k >> q) & 1) ? o[q] * scale : 0.0f;
+    }
+    store4(xhat + row * kD + c, v);
+    store4(y + row * kD + c, o);
+    if (y_bf != nullptr) store4(y_bf + row * kD + c, o);
+    if (lane == 0) rstd_out[row] = rs;
+  }
+}
+
+// dz = dy * keep * scale; dr = rstd * (g*dz - mean(g*dz) - xhat * mean(g*dz*xhat)); da = dr * (a > 0)
+// (bf16). part[blk][0..3][kD]: sum dz*xhat (gamma), sum dz (beta), sum da (the conv's bias).
+__global__ __launch_bounds__(256) void relu_ln_bwd_kernel(const float *__restrict__ dy, const float *__restrict__ a,
+                                                          const float *__restrict__ xhat, const float *__restrict__ rstd,
+                                                          const float *__restrict__ gamma, int64_t R, uint32_t thr,
+                                                          float scale, const int64_t *seed, uint32_t salt,
+                                                          bf16 *__restrict__ da, float *__restrict__ part) {
+  __shared__ float red[3][4][kD];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = lane * 4;
+  const uint32_t key = drop_key(seed, salt);
+  float g[4];
+  load4(gamma + c, g);
+  float pg[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f}, pa[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wv; row < R; row += nw) {
+    float d[4], xh[4], av[4], gd[4];
+    load4(dy + row * kD + c, d);
+    load4(xhat + row * kD + c, xh);
+    load4(a + row * kD + c, av);
+    if (thr != 0) {
+      const unsigned k = keep4(key, (uint32_t)(row * kD + c), thr);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = ((k >> q) & 1) ? d[q] * scale : 0.0f;
+    }
+    const float rs = rstd[row];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      gd[q] = g[q] * d[q];
+      s1 += gd[q];
+      s2 += gd[q] * xh[q];
+      pg[q] += d[q] * xh[q];
+      pb[q] += d[q];
+    }
+    const float m1 = wave_sum(s1) * (1.0f / kD), m2 = wave_sum(s2) * (1.0f / kD);
+    float dr[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      dr[q] = av[q] > 0.0f ? rs * (gd[q] - m1 - xh[q] * m2) : 0.0f;
+      pa[q] += dr[q];
+    }
+    store4(da + row * kD + c, dr);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    red[0][wv][c + q] = pg[q];
+    red[1][wv][c + q] = pb[q];
+    red[2][wv][c + q] = pa[q];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * kD; i += 256) {
+    const int k = i / kD, col = i - k * kD;
+    part[(int64_t)blockIdx.x * 3 * kD + i] = (red[k][0][col] + red[k][1][col]) + (red[k][2][col] + red[k][3][col]);
+  }
+}
+
 // Column sums, pass 1: block (256-column stripe, row chunk) -> part[chunk][N]; 4 columns per
 // thread, 4 rows in flight per block (one per wave).
 template <typename T>
@@ -267,6 +369,51 @@ extern "C" int fs2_res_ln_bwd(const float *dy, const float *xhat, const float *r
   const int grid = (int)(b64 < kLnBlocks ? b64 : kLnBlocks);
   hipLaunchKernelGGL(res_ln_bwd_kernel, dim3(grid), dim3(256), 0, s, dy, xhat, rstd, gamma, lens, R, T, thr, scale,
                      seed, (uint32_t)salt, dres, reinterpret_cast<bf16 *>(da), ws);
+  hipLaunchKernelGGL(ln_finish_kernel, dim3(3), dim3(kD), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_relu_ln_fwd(const float *a, const float *gamma, const float *beta, int64_t R, int D, float eps,
+                               float p_drop, const int64_t *seed, int salt, float *y, void *y_bf, float *xhat,
+                               float *rstd, fs2_stream_t stream) {
+  if (a == nullptr || gamma == nullptr || beta == nullptr || y == nullptr || xhat == nullptr || rstd == nullptr)
+    return FS2_EINVAL;
+  if (D != kD) return FS2_EUNSUPPORTED;
+  if (R < 0 || !(p_drop >= 0.0f && p_drop < 1.0f) || (p_drop > 0.0f && seed == nullptr)) return FS2_EINVAL;
+  if (R == 0) return FS2_OK;
+  const int64_t b64 = (R + 3) / 4;
+  hipLaunchKernelGGL(relu_ln_fwd_kernel, dim3((unsigned)(b64 < 2048 ? b64 : 2048)), dim3(256), 0, as_stream(stream), a,
+                     gamma, beta, R, eps, drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt, y,
+                     reinterpret_cast<bf16 *>(y_bf), xhat, rstd);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xhat, const float *rstd,
+                               const float *gamma, int64_t R, int D, float p_drop, const int64_t *seed, int salt,
+                               void *da, float *dgamma, float *dbeta, float *dbias, int accumulate, float *ws,
+                               int64_t ws_bytes, fs2_stream_t stream) {
+  if (dy == nullptr || a == nullptr || xhat == nullptr || rstd == nullptr || gamma == nullptr || da == nullptr ||
+      dgamma == nullptr || dbeta == nullptr || ws == nullptr)
+    return FS2_EINVAL;
+  if (D != kD) return FS2_EUNSUPPORTED;
+  if (R < 0 || !(p_drop >= 0.0f && p_drop < 1.0f) || (p_drop > 0.0f && seed == nullptr)) return FS2_EINVAL;
+  if (ws_bytes < fs2_res_ln_bwd_ws_bytes(D)) return FS2_EINVAL;
+  hipStream_t s = as_stream(stream);
+  if (R == 0) {
+    if (!accumulate) {
+      (void)hipMemsetAsync(dgamma, 0, kD * sizeof(float), s);
+      (void)hipMemsetAsync(dbeta, 0, kD * sizeof(float), s);
+      if (dbias != nullptr) (void)hipMemsetAsync(dbias, 0, kD * sizeof(float), s);
+    }
+    return FS2_OK;
+  }
+  const int64_t b64 = (R + 3) / 4;
+  const int grid = (int)(b64 < kLnBlocks ? b64 : kLnBlocks);
+  hipLaunchKernelGGL(relu_ln_bwd_kernel, dim3(grid), dim3(256), 0, s, dy, a, xhat, rstd, gamma, R,
+                     drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt,
+                     reinterpret_cast<bf16 *>(da), ws);
   hipLaunchKernelGGL(ln_finish_kernel, dim3(3), dim3(kD), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
   FS2_CHECK_LAUNCH();
   return FS2_OK;

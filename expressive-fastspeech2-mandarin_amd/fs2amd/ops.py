@@ -974,6 +974,40 @@ def res_ln_bwd(dy, xhat, rstd, gamma, lens=None, p_drop=0.0, seed=None, salt=0, 
     return dres, da, dgamma, dbeta, dbias
 
 
+def relu_ln_fwd(a, gamma, beta, eps, p_drop=0.0, seed=None, salt=0, want_bf16=True):
+    """y = dropout(LayerNorm(relu(a))) over rows of 256 (fs2_relu_ln_fwd): returns (y f32, y bf16
+    or None, xhat f32, rstd f32)."""
+    _gpu(a, gamma, beta, seed)
+    assert a.dtype == torch.float32 and a.is_contiguous() and a.shape[-1] == 256
+    R = a.numel() // 256
+    y = torch.empty_like(a)
+    yb = torch.empty(a.shape, device=a.device, dtype=torch.bfloat16) if want_bf16 else None
+    xhat = torch.empty_like(a)
+    rstd = torch.empty(R, device=a.device, dtype=torch.float32)
+    L.check(_lib.fs2_relu_ln_fwd(_ptr(a), _ptr(gamma), _ptr(beta), R, 256, float(eps), float(p_drop), _ptr(seed),
+                                 int(salt), _ptr(y), _ptr(yb), _ptr(xhat), _ptr(rstd), _stream(a)), "fs2_relu_ln_fwd")
+    return y, yb, xhat, rstd
+
+
+def relu_ln_bwd(dy, a, xhat, rstd, gamma, p_drop=0.0, seed=None, salt=0, dgamma=None, dbeta=None, dbias=None,
+                want_dbias=True, accumulate=False):
+    """Backward of :func:`relu_ln_fwd` (fs2_relu_ln_bwd): (da bf16, dgamma, dbeta, dbias)."""
+    _gpu(dy, a, xhat, rstd, gamma, seed)
+    dy = dy.contiguous()
+    R = a.numel() // 256
+    da = torch.empty(a.shape, device=a.device, dtype=torch.bfloat16)
+    new = lambda: torch.empty(256, device=a.device, dtype=torch.float32)
+    dgamma = new() if dgamma is None else dgamma
+    dbeta = new() if dbeta is None else dbeta
+    if dbias is None and want_dbias:
+        dbias = new()
+    ws = torch.empty(_lib.fs2_res_ln_bwd_ws_bytes(256) // 4, device=a.device, dtype=torch.float32)
+    L.check(_lib.fs2_relu_ln_bwd(_ptr(dy), _ptr(a), _ptr(xhat), _ptr(rstd), _ptr(gamma), R, 256, float(p_drop),
+                                 _ptr(seed), int(salt), _ptr(da), _ptr(dgamma), _ptr(dbeta), _ptr(dbias),
+                                 1 if accumulate else 0, _ptr(ws), ws.numel() * 4, _stream(a)), "fs2_relu_ln_bwd")
+    return da, dgamma, dbeta, dbias
+
+
 def colsum(x, out=None, accumulate=False):
     """out[n] (+)= sum over rows of x [..., N] (f32 / bf16), deterministic (fs2_colsum)."""
     _gpu(x, out)

@@ -380,8 +380,71 @@ def _train_seed(model, dev):
     return s
 
 
-def variance_predictor(vp, x, mask, training, compute):
+class VPLayerFn(torch.autograd.Function):
+    """One VariancePredictor layer in train mode (model/modules.py:218-235): Conv (fs2_conv1d, f32
+    out) -> fs2_relu_ln_fwd (relu + LayerNorm + dropout, bf16 copy for the next conv); backward
+    fs2_relu_ln_bwd (+ the conv's bias gradient) -> input gradient conv -> fs2_conv_wgrad."""
+
+    @staticmethod
+    def forward(ctx, x, x_bf, meta, w, b, g, be):
+        pad, p_drop, seed, salt, eps = meta
+        N, Cin, KS = w.shape
+        BF = L.FS2_BF16
+        xb = x_bf if x_bf is not None else x.to(torch.bfloat16)
+        a = ops.conv1d(xb, ops.pack_conv_weight(w, BF), b.detach(), cin=Cin, ks=KS, pad=pad, compute=BF,
+                       epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+        y, yb, xh, rs = ops.relu_ln_fwd(a, g.detach(), be.detach(), eps, p_drop, seed, salt)
+        ctx.save_for_backward(xb, a, xh, rs, w, b, g, be)
+        ctx.meta = meta
+        ctx.wT = _packT(w)
+        ctx.mark_non_differentiable(yb)
+        return y, yb
+
+    @staticmethod
+    def backward(ctx, dy, _dyb):
+        xb, a, xh, rs, w, b, g, be = ctx.saved_tensors
+        pad, p_drop, seed, salt, eps = ctx.meta
+        N, Cin, KS = w.shape
+        sink = _SINK[0] and all(t.grad is not None for t in (w, b, g, be))
+        G = (lambda t: t.grad) if sink else (lambda t: None)
+        da, dg, dbe, db = ops.relu_ln_bwd(dy, a, xh, rs, g.detach(), p_drop, seed, salt, dgamma=G(g), dbeta=G(be),
+                                          dbias=G(b), accumulate=sink)
+        dw, _ = ops.conv_wgrad(da, xb, KS, pad, dw=G(w), accumulate=sink)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.conv1d(da, ctx.wT, None, cin=N, ks=KS, pad=KS - 1 - pad, compute=L.FS2_BF16,
+                            epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+        if sink:
+            return dx, None, None, None, None, None, None
+        return dx, None, None, dw, db, dg, dbe
+
+
+def _vp_fused(vp, x, mask, training, seed, salt):
+    cl = vp.conv_layer
+    c1, c2 = cl.conv1d_1.conv, cl.conv1d_2.conv
+    k = c1.kernel_size[0]
+    p1 = cl.dropout_1.p if training else 0.0
+    p2 = cl.dropout_2.p if training else 0.0
+    h, hb = VPLayerFn.apply(x.contiguous(), None, ((k - 1) // 2, p1, seed, salt, cl.layer_norm_1.eps), c1.weight,
+                            c1.bias, cl.layer_norm_1.weight, cl.layer_norm_1.bias)
+    h, _ = VPLayerFn.apply(h, hb, (1, p2, seed, salt + 1, cl.layer_norm_2.eps), c2.weight, c2.bias,
+                           cl.layer_norm_2.weight, cl.layer_norm_2.bias)
+    out = F.linear(h, vp.linear_layer.weight, vp.linear_layer.bias).squeeze(-1)
+    return out.masked_fill(mask, 0.0)
+
+
+def _vp_fused_ok(vp, compute):
+    cl = vp.conv_layer
+    c1, c2 = cl.conv1d_1.conv, cl.conv1d_2.conv
+    return (os.environ.get("FS2_TRAIN_FUSED", "1") != "0" and compute == L.FS2_BF16 and c1.out_channels == 256
+            and c2.out_channels == 256 and c1.kernel_size[0] in (1, 3, 5, 9) and c2.kernel_size[0] in (1, 3, 5, 9)
+            and c1.in_channels % 8 == 0)
+
+
+def variance_predictor(vp, x, mask, training, compute, seed=None, salt=0):
     """model/modules.py:209-250 (conv1d_2 padding hard-coded to 1, :230)."""
+    if seed is not None and _vp_fused_ok(vp, compute):
+        return _vp_fused(vp, x, mask, training, seed, salt)
     cl = vp.conv_layer
     k = cl.conv1d_1.conv.kernel_size[0]
     h = torch.relu(conv1d(x, cl.conv1d_1.conv, (k - 1) // 2, compute))
@@ -392,9 +455,9 @@ def variance_predictor(vp, x, mask, training, compute):
     return out.masked_fill(mask, 0.0)
 
 
-def _variance_embed(va, kind, x, target, mask, control, training, compute):
+def _variance_embed(va, kind, x, target, mask, control, training, compute, seed=None, salt=0):
     """model/modules.py:80-100,117-126 (energy is scaled by p_control in the reference)."""
-    pred = variance_predictor(getattr(va, f"{kind}_predictor"), x, mask, training, compute)
+    pred = variance_predictor(getattr(va, f"{kind}_predictor"), x, mask, training, compute, seed, salt)
     bins = getattr(va, f"{kind}_bins")
     table = getattr(va, f"{kind}_embedding")
     if target is not None:
@@ -470,13 +533,15 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
         x = x + model.emotion_linear(emb).unsqueeze(1)
 
     # variance adaptor (model/modules.py:102-158)
-    log_d = variance_predictor(va.duration_predictor, x, src_masks, training, compute)
+    vseed = seed if fused else None
+    log_d = variance_predictor(va.duration_predictor, x, src_masks, training, compute, vseed, 1000)
     p_pred = e_pred = None
     if va.pitch_feature_level == "phoneme_level":
-        p_pred, emb = _variance_embed(va, "pitch", x, p_targets, src_masks, p_control, training, compute)
+        p_pred, emb = _variance_embed(va, "pitch", x, p_targets, src_masks, p_control, training, compute, vseed, 1002)
         x = x + emb
     if va.energy_feature_level == "phoneme_level":
-        e_pred, emb = _variance_embed(va, "energy", x, e_targets, src_masks, p_control, training, compute)
+        e_pred, emb = _variance_embed(va, "energy", x, e_targets, src_masks, p_control, training, compute, vseed,
+                                      1004)
         x = x + emb
     if d_targets is not None:
         x, mel_len = _length_regulate(x, d_targets, max_mel_len)
@@ -486,10 +551,12 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
         x, mel_len = _length_regulate(x, d_rounded, None)
         mel_masks = _mask(mel_len, int(mel_len.max().item()))
     if va.pitch_feature_level == "frame_level":
-        p_pred, emb = _variance_embed(va, "pitch", x, p_targets, mel_masks, p_control, training, compute)
+        p_pred, emb = _variance_embed(va, "pitch", x, p_targets, mel_masks, p_control, training, compute, vseed,
+                                      1002)
         x = x + emb
     if va.energy_feature_level == "frame_level":
-        e_pred, emb = _variance_embed(va, "energy", x, e_targets, mel_masks, p_control, training, compute)
+        e_pred, emb = _variance_embed(va, "energy", x, e_targets, mel_masks, p_control, training, compute, vseed,
+                                      1004)
         x = x + emb
 
     # decoder (transformer/Models.py:139-171, training: crop to max_seq_len)

@@ -553,6 +553,17 @@ int fs2_res_ln_bwd(const float *dy, const float *xhat, const float *rstd, const 
                    int64_t R, int T, int D, float p_drop, const int64_t *seed, int salt, float *dres, void *da,
                    float *dgamma, float *dbeta, float *dbias, int accumulate, float *ws, int64_t ws_bytes,
                    fs2_stream_t stream);
+/* fs2_relu_ln_fwd / fs2_relu_ln_bwd — one VariancePredictor layer after its conv in train mode,
+ *   y = dropout(LayerNorm(relu(a)))  (model/modules.py:218-235; R rows of D = 256), y f32 (+ optional
+ *   bf16 copy), saved xhat / rstd; the backward takes a again (relu mask) and gives da bf16 and
+ *   dgamma / dbeta / dbias (the conv's bias gradient, optional), accumulate as fs2_res_ln_bwd.
+ *   ws: fs2_res_ln_bwd_ws_bytes(D). */
+int fs2_relu_ln_fwd(const float *a, const float *gamma, const float *beta, int64_t R, int D, float eps, float p_drop,
+                    const int64_t *seed, int salt, float *y, void *y_bf, float *xhat, float *rstd,
+                    fs2_stream_t stream);
+int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xhat, const float *rstd, const float *gamma,
+                    int64_t R, int D, float p_drop, const int64_t *seed, int salt, void *da, float *dgamma,
+                    float *dbeta, float *dbias, int accumulate, float *ws, int64_t ws_bytes, fs2_stream_t stream);
 int64_t fs2_colsum_ws_bytes(int N);
 int fs2_colsum(const void *x, int dtype, int64_t R, int N, int64_t row_stride, float *out, int accumulate, float *ws,
                int64_t ws_bytes, fs2_stream_t stream);

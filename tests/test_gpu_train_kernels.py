@@ -200,3 +200,37 @@ def test_pack_train_images(ops):
         for k, v in exp.items():
             assert P[k].shape == v.shape, k
             assert torch.equal(P[k], v), k
+
+
+@pytest.mark.parametrize("p", [0.0, 0.5])
+def test_relu_ln_fwd_bwd(ops, p):
+    """fs2_relu_ln_fwd / _bwd: y = dropout(LayerNorm(relu(a))) (a VariancePredictor layer,
+    model/modules.py:218-235) and its gradient against float64 autograd with the kernel's keep
+    mask; same tolerances as the residual form."""
+    torch.manual_seed(6)
+    R, D = 333, 256
+    a = torch.randn(R, D)
+    gam, bet = 1 + 0.1 * torch.randn(D), 0.1 * torch.randn(D)
+    seed = torch.tensor([99], dtype=torch.int64, device=DEV)
+    salt = 11
+    y, yb, xh, rs = ops.relu_ln_fwd(a.to(DEV), gam.to(DEV), bet.to(DEV), 1e-5, p, seed, salt)
+    if p > 0:  # keep bits: the same hash as fs2_res_ln_fwd's (row * 256 + column, seed, salt)
+        keep = _keep_mask(ops, 1, R, p, seed, salt).view(R, D)
+    else:
+        keep = torch.ones(R, D, dtype=torch.bool)
+    ad = a.double().requires_grad_()
+    gd, bd = gam.double().requires_grad_(), bet.double().requires_grad_()
+    ref = F.layer_norm(torch.relu(ad), (D,), gd, bd, 1e-5) * keep / (1 - p)
+    torch.cuda.synchronize()
+    sc = float(ref.abs().max())
+    assert float((y.cpu().double() - ref).abs().max()) <= 2e-5 * sc
+    assert float((yb.cpu().double() - ref).abs().max()) <= 1e-2 * sc
+    dy = torch.randn(R, D)
+    ref.backward(dy.double())
+    da, dg, dbe, db = ops.relu_ln_bwd(dy.to(DEV), a.to(DEV), xh, rs, gam.to(DEV), p, seed, salt)
+    torch.cuda.synchronize()
+    assert float((da.cpu().double() - ad.grad).abs().max()) <= 1e-2 * float(ad.grad.abs().max())
+    assert torch.allclose(dg.cpu().double(), gd.grad, rtol=1e-4, atol=1e-4 * float(gd.grad.abs().max()))
+    assert torch.allclose(dbe.cpu().double(), bd.grad, rtol=1e-4, atol=1e-4 * float(bd.grad.abs().max()))
+    dsum = ad.grad.sum(0)
+    assert torch.allclose(db.cpu().double(), dsum, rtol=1e-3, atol=1e-3 * float(dsum.abs().max()))
