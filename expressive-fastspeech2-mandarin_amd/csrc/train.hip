@@ -255,6 +255,40 @@ __global__ __launch_bounds__(256) void relu_ln_bwd_kernel(const float *__restric
   }
 }
 
+// Embedding backward (nn.Embedding autograd; src_word_emb with padding_idx, pitch / energy
+// bucket embeddings, speaker / emotion tables): workgroup v sums the dy rows of every position i
+// with tokens[i] == v in increasing i (chunks of 256 positions compacted in order through LDS),
+// so the result is deterministic (no atomics). Row padding_idx gets no gradient.
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t *__restrict__ tokens, int64_t n,
+                                                        const float *__restrict__ dy, int64_t dys, int D,
+                                                        int padding_idx, float *__restrict__ out, int accumulate) {
+  __shared__ int list[256];
+  __shared__ int wcnt[4];
+  const int v = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float acc = 0.f;
+  const bool skip = v == padding_idx;
+  if (!skip)
+    for (int64_t base = 0; base < n; base += 256) {
+      const int64_t i = base + tid;
+      const bool hit = i < n && tokens[i] == (int64_t)v;
+      const uint64_t m = __ballot(hit);
+      if (lane == 0) wcnt[wv] = __popcll(m);
+      __syncthreads();
+      int off = 0;
+      for (int w = 0; w < wv; ++w) off += wcnt[w];
+      const int total = (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
+      if (hit) list[off + __popcll(m & ((1ull << lane) - 1ull))] = tid;
+      __syncthreads();
+      if (tid < D)
+        for (int j = 0; j < total; ++j) acc += dy[(base + list[j]) * dys + tid];
+      __syncthreads();
+    }
+  if (tid < D) {
+    float *o = out + (int64_t)v * D + tid;
+    *o = accumulate ? *o + acc : acc;
+  }
+}
+
 // Column sums, pass 1: block (256-column stripe, row chunk) -> part[chunk][N]; 4 columns per
 // thread, 4 rows in flight per block (one per wave).
 template <typename T>
@@ -415,6 +449,16 @@ extern "C" int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xha
                      drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt,
                      reinterpret_cast<bf16 *>(da), ws);
   hipLaunchKernelGGL(ln_finish_kernel, dim3(3), dim3(kD), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_embedding_bwd(const int64_t *tokens, int64_t n, const float *dy, int64_t dy_row_stride, int V,
+                                 int D, int padding_idx, float *out, int accumulate, fs2_stream_t stream) {
+  if (tokens == nullptr || out == nullptr || (n > 0 && dy == nullptr)) return FS2_EINVAL;
+  if (n < 0 || V <= 0 || D <= 0 || D > 256 || dy_row_stride < D) return FS2_EINVAL;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)V), dim3(256), 0, as_stream(stream), tokens, n, dy,
+                     dy_row_stride, D, padding_idx, out, accumulate);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

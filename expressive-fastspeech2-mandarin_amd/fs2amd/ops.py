@@ -1008,6 +1008,23 @@ def relu_ln_bwd(dy, a, xhat, rstd, gamma, p_drop=0.0, seed=None, salt=0, dgamma=
     return da, dgamma, dbeta, dbias
 
 
+def embedding_bwd(tokens, dy, V, padding_idx=None, out=None, accumulate=False):
+    """nn.Embedding weight gradient (fs2_embedding_bwd): tokens int64 [...], dy f32 [..., D] ->
+    out f32 [V, D], deterministic; padding_idx row zero (or untouched when accumulating)."""
+    _gpu(tokens, dy, out)
+    D = dy.shape[-1]
+    tok = tokens.reshape(-1).to(torch.int64).contiguous()
+    d2 = dy.reshape(-1, D)
+    if d2.dtype != torch.float32 or d2.stride(-1) != 1:
+        d2 = d2.float().contiguous()
+    if out is None:
+        out = torch.empty(V, D, device=dy.device, dtype=torch.float32)
+    L.check(_lib.fs2_embedding_bwd(_ptr(tok), tok.numel(), _ptr(d2), d2.stride(0), int(V), D,
+                                   -1 if padding_idx is None else int(padding_idx), _ptr(out), 1 if accumulate else 0,
+                                   _stream(dy)), "fs2_embedding_bwd")
+    return out
+
+
 def colsum(x, out=None, accumulate=False):
     """out[n] (+)= sum over rows of x [..., N] (f32 / bf16), deterministic (fs2_colsum)."""
     _gpu(x, out)

@@ -365,6 +365,31 @@ class FFTBlockFn(torch.autograd.Function):
         return (dx, None, None, None, None, *grads)
 
 
+class EmbeddingFn(torch.autograd.Function):
+    """nn.Embedding with its weight gradient on fs2_embedding_bwd (deterministic, no atomics;
+    padding_idx honoured); gradient sink as FFTBlockFn."""
+
+    @staticmethod
+    def forward(ctx, idx, weight, padding_idx):
+        ctx.save_for_backward(idx, weight)
+        ctx.padding_idx = padding_idx
+        return F.embedding(idx, weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        idx, weight = ctx.saved_tensors
+        if _SINK[0] and weight.grad is not None:
+            ops.embedding_bwd(idx, dy, weight.shape[0], ctx.padding_idx, out=weight.grad, accumulate=True)
+            return None, None, None
+        return None, ops.embedding_bwd(idx, dy, weight.shape[0], ctx.padding_idx), None
+
+
+def _embed(emb, idx, fused):
+    if not fused:
+        return emb(idx)
+    return EmbeddingFn.apply(idx, emb.weight, emb.padding_idx)
+
+
 def fft_block_fused(blk, x, x_bf, lens, seed, salt, p_drop, packed=None):
     y, yb = FFTBlockFn.apply(x, x_bf, lens, seed, (blk, float(p_drop), int(salt), packed), *_block_params(blk))
     return y, yb
@@ -460,11 +485,12 @@ def _variance_embed(va, kind, x, target, mask, control, training, compute, seed=
     pred = variance_predictor(getattr(va, f"{kind}_predictor"), x, mask, training, compute, seed, salt)
     bins = getattr(va, f"{kind}_bins")
     table = getattr(va, f"{kind}_embedding")
+    fused = seed is not None
     if target is not None:
-        emb = table(torch.bucketize(target, bins))
+        emb = _embed(table, torch.bucketize(target, bins), fused)
     else:
         pred = pred * control
-        emb = table(torch.bucketize(pred, bins))
+        emb = _embed(table, torch.bucketize(pred, bins), fused)
     return pred, emb
 
 
@@ -518,7 +544,7 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
             if tp is not None:
                 tp.run(texts)
                 packs = tp.per_block
-    x = enc.src_word_emb(texts) + enc.position_enc[:, :Lx, :]
+    x = _embed(enc.src_word_emb, texts, fused) + enc.position_enc[:, :Lx, :]
     xb = None
     for i, blk in enumerate(enc.layer_stack):
         if fused:
@@ -527,9 +553,10 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
         else:
             x = fft_block(blk, x, src_masks, lens_src, tr["encoder_dropout"], training, compute)
     if model.speaker_emb is not None:
-        x = x + model.speaker_emb(speakers).unsqueeze(1)
+        x = x + _embed(model.speaker_emb, speakers, fused).unsqueeze(1)
     if model.emotion_emb is not None:
-        emb = torch.cat([model.emotion_emb(emotions), model.arousal_emb(arousals), model.valence_emb(valences)], -1)
+        emb = torch.cat([_embed(model.emotion_emb, emotions, fused), _embed(model.arousal_emb, arousals, fused),
+                         _embed(model.valence_emb, valences, fused)], -1)
         x = x + model.emotion_linear(emb).unsqueeze(1)
 
     # variance adaptor (model/modules.py:102-158)

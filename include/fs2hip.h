@@ -564,6 +564,13 @@ int fs2_relu_ln_fwd(const float *a, const float *gamma, const float *beta, int64
 int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xhat, const float *rstd, const float *gamma,
                     int64_t R, int D, float p_drop, const int64_t *seed, int salt, void *da, float *dgamma,
                     float *dbeta, float *dbias, int accumulate, float *ws, int64_t ws_bytes, fs2_stream_t stream);
+/* fs2_embedding_bwd — nn.Embedding's weight gradient (transformer/Models.py:82 src_word_emb with
+ *   padding_idx, model/modules.py:80-100 pitch / energy tables, fastspeech2.py:101-110 speaker /
+ *   emotion tables): out[v][:] (+)= sum over i with tokens[i] == v, in increasing i, of dy[i][:]
+ *   (deterministic, no atomics); row padding_idx (< 0: none) untouched unless accumulate == 0 (then
+ *   zero). D <= 256. */
+int fs2_embedding_bwd(const int64_t *tokens, int64_t n, const float *dy, int64_t dy_row_stride, int V, int D,
+                      int padding_idx, float *out, int accumulate, fs2_stream_t stream);
 int64_t fs2_colsum_ws_bytes(int N);
 int fs2_colsum(const void *x, int dtype, int64_t R, int N, int64_t row_stride, float *out, int accumulate, float *ws,
                int64_t ws_bytes, fs2_stream_t stream);

@@ -234,3 +234,21 @@ def test_relu_ln_fwd_bwd(ops, p):
     assert torch.allclose(dbe.cpu().double(), bd.grad, rtol=1e-4, atol=1e-4 * float(bd.grad.abs().max()))
     dsum = ad.grad.sum(0)
     assert torch.allclose(db.cpu().double(), dsum, rtol=1e-3, atol=1e-3 * float(dsum.abs().max()))
+
+
+@pytest.mark.parametrize("V,D,n,pad", [(300, 256, 1024, 0), (256, 256, 7000, None), (5, 64, 16, None)])
+def test_embedding_bwd(ops, V, D, n, pad):
+    """fs2_embedding_bwd against a float64 index_add (the nn.Embedding weight gradient), padding
+    row zero; deterministic: two calls bit-identical."""
+    torch.manual_seed(V + n)
+    tok = torch.randint(0, V, (n,))
+    tok[: n // 8] = 3  # a hot row
+    dy = torch.randn(n, D)
+    ref = torch.zeros(V, D, dtype=torch.float64).index_add_(0, tok, dy.double())
+    if pad is not None:
+        ref[pad] = 0
+    o1 = ops.embedding_bwd(tok.to(DEV), dy.to(DEV), V, pad)
+    o2 = ops.embedding_bwd(tok.to(DEV), dy.to(DEV), V, pad)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert float((o1.cpu().double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
