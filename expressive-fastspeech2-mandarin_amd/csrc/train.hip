@@ -932,3 +932,178 @@ extern "C" int fs2_pack_train(const fs2_pack_desc *descs_dev, int nd, int blocks
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// FastSpeech2Loss (model/loss.py:5-92): the five masked means and their total in one reduction
+// (fixed-order partials: deterministic) and every prediction's gradient in one elementwise pass.
+//   mel / postnet: L1 over the valid frames' n_mel channels; pitch / energy / log-duration: MSE
+//   over their masks (log_d target = log(d + 1)); empty masks give NaN, as masked_select().mean().
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kLossBlocks = 256;
+constexpr int kLossQ = 9;  // s_mel, s_post, n_rows, s_p, n_p, s_e, n_e, s_d, n_d
+
+__global__ __launch_bounds__(256) void loss_part_kernel(fs2_loss_args a, float *__restrict__ part) {
+  __shared__ float red[4][kLossQ];
+  float q[kLossQ];
+#pragma unroll
+  for (int i = 0; i < kLossQ; ++i) q[i] = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t g0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c4n = a.n_mel / 4;
+  const int64_t nmel = (int64_t)a.B * a.T * c4n;
+  for (int64_t i = g0; i < nmel; i += stride) {
+    const int64_t row = i / c4n;
+    const int c = (int)(i - row * c4n) * 4;
+    if (!a.mel_valid[row]) continue;
+    const int64_t b = row / a.T, t = row - b * a.T;
+    float m[4], p[4], tg[4];
+    load4(a.mel + row * a.n_mel + c, m);
+    load4(a.postnet + row * a.n_mel + c, p);
+    load4(a.mel_tgt + b * a.tgt_bs + t * a.tgt_ts + c, tg);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      q[0] += fabsf(m[k] - tg[k]);
+      q[1] += fabsf(p[k] - tg[k]);
+    }
+    if (c == 0) q[2] += 1.f;
+  }
+  for (int64_t i = g0; i < a.n_p; i += stride)
+    if (a.p_mask[i]) {
+      const float d = a.p_pred[i] - a.p_tgt[i];
+      q[3] += d * d;
+      q[4] += 1.f;
+    }
+  for (int64_t i = g0; i < a.n_e; i += stride)
+    if (a.e_mask[i]) {
+      const float d = a.e_pred[i] - a.e_tgt[i];
+      q[5] += d * d;
+      q[6] += 1.f;
+    }
+  for (int64_t i = g0; i < a.n_d; i += stride)
+    if (a.d_mask[i]) {
+      const float d = a.logd_pred[i] - logf((float)a.d_tgt[i] + 1.0f);
+      q[7] += d * d;
+      q[8] += 1.f;
+    }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < kLossQ; ++i) {
+    const float v = wave_sum(q[i]);
+    if (lane == 0) red[wv][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kLossQ)
+    part[(int64_t)blockIdx.x * kLossQ + threadIdx.x] =
+        (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+// out[0..5] = total, mel, postnet, pitch, energy, duration; stats[0..3] = n_mel_elems, n_p, n_e, n_d
+__global__ __launch_bounds__(64) void loss_finish_kernel(const float *__restrict__ part, int blocks, int n_mel,
+                                                         float *__restrict__ out, float *__restrict__ stats) {
+  __shared__ float s[kLossQ];
+  if (threadIdx.x < kLossQ) {
+    float v = 0.f;
+    for (int k = 0; k < blocks; ++k) v += part[(int64_t)k * kLossQ + threadIdx.x];
+    s[threadIdx.x] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float nm = s[2] * (float)n_mel;
+    const float mel = s[0] / nm, post = s[1] / nm, pl = s[3] / s[4], el = s[5] / s[6], dl = s[7] / s[8];
+    out[1] = mel;
+    out[2] = post;
+    out[3] = pl;
+    out[4] = el;
+    out[5] = dl;
+    out[0] = (((mel + post) + dl) + pl) + el;  // model/loss.py:84-86 order
+    stats[0] = nm;
+    stats[1] = s[4];
+    stats[2] = s[6];
+    stats[3] = s[8];
+  }
+}
+
+// gradients: g[0..5] upstream of (total, mel, postnet, pitch, energy, duration); stats = out[6..9]
+__global__ __launch_bounds__(256) void loss_bwd_kernel(fs2_loss_args a, const float *__restrict__ g,
+                                                       const float *__restrict__ stats, float *__restrict__ d_mel,
+                                                       float *__restrict__ d_post, float *__restrict__ d_p,
+                                                       float *__restrict__ d_e, float *__restrict__ d_logd) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t g0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const float gt = g[0];
+  const float km = (gt + g[1]) / stats[0], kp = (gt + g[2]) / stats[0];
+  const int c4n = a.n_mel / 4;
+  const int64_t nmel = (int64_t)a.B * a.T * c4n;
+  for (int64_t i = g0; i < nmel; i += stride) {
+    const int64_t row = i / c4n;
+    const int c = (int)(i - row * c4n) * 4;
+    float dm[4] = {0.f, 0.f, 0.f, 0.f}, dp[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.mel_valid[row]) {
+      const int64_t b = row / a.T, t = row - b * a.T;
+      float m[4], p[4], tg[4];
+      load4(a.mel + row * a.n_mel + c, m);
+      load4(a.postnet + row * a.n_mel + c, p);
+      load4(a.mel_tgt + b * a.tgt_bs + t * a.tgt_ts + c, tg);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float e1 = m[k] - tg[k], e2 = p[k] - tg[k];
+        dm[k] = e1 > 0.f ? km : (e1 < 0.f ? -km : 0.f);
+        dp[k] = e2 > 0.f ? kp : (e2 < 0.f ? -kp : 0.f);
+      }
+    }
+    store4(d_mel + row * a.n_mel + c, dm);
+    store4(d_post + row * a.n_mel + c, dp);
+  }
+  const float kpi = 2.f * (gt + g[3]) / stats[1], ke = 2.f * (gt + g[4]) / stats[2],
+              kd = 2.f * (gt + g[5]) / stats[3];
+  for (int64_t i = g0; i < a.n_p; i += stride) d_p[i] = a.p_mask[i] ? kpi * (a.p_pred[i] - a.p_tgt[i]) : 0.f;
+  for (int64_t i = g0; i < a.n_e; i += stride) d_e[i] = a.e_mask[i] ? ke * (a.e_pred[i] - a.e_tgt[i]) : 0.f;
+  for (int64_t i = g0; i < a.n_d; i += stride)
+    d_logd[i] = a.d_mask[i] ? kd * (a.logd_pred[i] - logf((float)a.d_tgt[i] + 1.0f)) : 0.f;
+}
+
+int loss_check(const fs2_loss_args *a) {
+  if (a == nullptr || a->mel == nullptr || a->postnet == nullptr || a->mel_tgt == nullptr || a->mel_valid == nullptr ||
+      a->p_pred == nullptr || a->p_tgt == nullptr || a->p_mask == nullptr || a->e_pred == nullptr ||
+      a->e_tgt == nullptr || a->e_mask == nullptr || a->logd_pred == nullptr || a->d_tgt == nullptr ||
+      a->d_mask == nullptr)
+    return FS2_EINVAL;
+  if (a->B < 0 || a->T < 0 || a->n_mel <= 0 || (a->n_mel & 3) || a->n_p < 0 || a->n_e < 0 || a->n_d < 0 ||
+      (a->tgt_ts & 3) || (a->tgt_bs & 3))
+    return FS2_EINVAL;
+  return FS2_OK;
+}
+
+}  // namespace
+
+extern "C" int64_t fs2_loss_ws_bytes(void) { return (int64_t)kLossBlocks * kLossQ * (int64_t)sizeof(float); }
+
+extern "C" int fs2_loss_fwd(const fs2_loss_args *a, float *out, float *stats, float *ws, int64_t ws_bytes,
+                            fs2_stream_t stream) {
+  const int st = loss_check(a);
+  if (st != FS2_OK) return st;
+  if (out == nullptr || stats == nullptr || ws == nullptr || ws_bytes < fs2_loss_ws_bytes()) return FS2_EINVAL;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(loss_part_kernel, dim3(kLossBlocks), dim3(256), 0, s, *a, ws);
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(64), 0, s, ws, kLossBlocks, a->n_mel, out, stats);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_loss_bwd(const fs2_loss_args *a, const float *grad_out, const float *stats, float *d_mel,
+                            float *d_postnet, float *d_pitch, float *d_energy, float *d_logd, fs2_stream_t stream) {
+  const int st = loss_check(a);
+  if (st != FS2_OK) return st;
+  if (grad_out == nullptr || stats == nullptr || d_mel == nullptr || d_postnet == nullptr || d_pitch == nullptr ||
+      d_energy == nullptr || d_logd == nullptr)
+    return FS2_EINVAL;
+  const int64_t work = (int64_t)a->B * a->T * (a->n_mel / 4);
+  int64_t blocks = (work + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), *a, grad_out, stats,
+                     d_mel, d_postnet, d_pitch, d_energy, d_logd);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}

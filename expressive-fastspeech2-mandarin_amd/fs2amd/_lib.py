@@ -34,6 +34,15 @@ class PackDesc(ctypes.Structure):
                 ("N_tot", _i), ("f32_copy", _i), ("tiles_c", _i), ("blk0", _i)]
 
 
+class LossArgs(ctypes.Structure):
+    """Mirror of ``fs2_loss_args`` (include/fs2hip.h)."""
+
+    _fields_ = [("mel", _p), ("postnet", _p), ("mel_tgt", _p), ("tgt_bs", _i64), ("tgt_ts", _i64), ("mel_valid", _p),
+                ("B", _i), ("T", _i), ("n_mel", _i), ("p_pred", _p), ("p_tgt", _p), ("p_mask", _p), ("n_p", _i64),
+                ("e_pred", _p), ("e_tgt", _p), ("e_mask", _p), ("n_e", _i64), ("logd_pred", _p), ("d_tgt", _p),
+                ("d_mask", _p), ("n_d", _i64)]
+
+
 class ConvDesc(ctypes.Structure):
     """Mirror of ``fs2_conv_desc`` (include/fs2hip.h)."""
 
@@ -152,6 +161,9 @@ SIGNATURES = {
     "fs2_relu_ln_fwd": (_i, [_p, _p, _p, _i64, _i, _f, _f, _p, _i, _p, _p, _p, _p, _p]),
     "fs2_relu_ln_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i, _f, _p, _i, _p, _p, _p, _p, _i, _p, _i64, _p]),
     "fs2_embedding_bwd": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _p, _i, _p]),
+    "fs2_loss_ws_bytes": (_i64, []),
+    "fs2_loss_fwd": (_i, [_p, _p, _p, _p, _i64, _p]),
+    "fs2_loss_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "fs2_colsum_ws_bytes": (_i64, [_i]),
     "fs2_colsum": (_i, [_p, _i, _i64, _i, _i64, _p, _i, _p, _i64, _p]),
     "fs2_conv_wgrad_ws_bytes": (_i64, [_i, _i, _i, _i, _i]),

@@ -1025,6 +1025,46 @@ def embedding_bwd(tokens, dy, V, padding_idx=None, out=None, accumulate=False):
     return out
 
 
+def loss_fwd(mel, post, p, e, logd, mel_tgt, p_tgt, e_tgt, d_tgt, mv, pm, em, dm):
+    """FastSpeech2Loss forward (fs2_loss_fwd): returns (losses f32 [6] = total, mel, postnet, pitch,
+    energy, duration; stats [4]; the argument struct; the tensors it points at)."""
+    _gpu(mel, post, p, e, logd, mel_tgt, p_tgt, e_tgt, d_tgt, mv, pm, em, dm)
+    f = lambda t: t.detach().float().contiguous()
+    u8 = lambda t: t.contiguous().to(torch.bool)
+    keep = [f(mel), f(post), f(p), f(e), f(logd), mel_tgt.detach().float(), f(p_tgt), f(e_tgt),
+            d_tgt.detach().to(torch.int64).contiguous(), u8(mv), u8(pm), u8(em), u8(dm)]
+    mel_, post_, p_, e_, ld_, mt, pt, et, dt, mv_, pm_, em_, dm_ = keep
+    if mt.stride(-1) != 1:
+        mt = keep[5] = mt.contiguous()
+    B, T, C = mel_.shape
+    assert post_.shape == mel_.shape and mt.shape[0] == B and mt.shape[1] >= T and mt.shape[2] == C
+    assert mv_.shape == (B, T) and p_.shape == pt.shape == pm_.shape and e_.shape == et.shape == em_.shape
+    assert ld_.shape == dt.shape == dm_.shape
+    a = L.LossArgs()
+    a.mel, a.postnet, a.mel_tgt = mel_.data_ptr(), post_.data_ptr(), mt.data_ptr()
+    a.tgt_bs, a.tgt_ts, a.mel_valid = mt.stride(0), mt.stride(1), mv_.data_ptr()
+    a.B, a.T, a.n_mel = B, T, C
+    a.p_pred, a.p_tgt, a.p_mask, a.n_p = p_.data_ptr(), pt.data_ptr(), pm_.data_ptr(), p_.numel()
+    a.e_pred, a.e_tgt, a.e_mask, a.n_e = e_.data_ptr(), et.data_ptr(), em_.data_ptr(), e_.numel()
+    a.logd_pred, a.d_tgt, a.d_mask, a.n_d = ld_.data_ptr(), dt.data_ptr(), dm_.data_ptr(), ld_.numel()
+    out = torch.empty(6, device=mel.device, dtype=torch.float32)
+    stats = torch.empty(4, device=mel.device, dtype=torch.float32)
+    ws = torch.empty(_lib.fs2_loss_ws_bytes() // 4, device=mel.device, dtype=torch.float32)
+    L.check(_lib.fs2_loss_fwd(ctypes.byref(a), _ptr(out), _ptr(stats), _ptr(ws), ws.numel() * 4, _stream(mel)),
+            "fs2_loss_fwd")
+    return out, stats, a, keep
+
+
+def loss_bwd(args, keep, grad_out, stats, shapes):
+    """FastSpeech2Loss backward (fs2_loss_bwd): gradients of (mel, postnet, pitch, energy, log_d)."""
+    mel = keep[0]
+    g = grad_out.float().contiguous()
+    outs = [torch.empty(s, device=mel.device, dtype=torch.float32) for s in shapes]
+    L.check(_lib.fs2_loss_bwd(ctypes.byref(args), _ptr(g), _ptr(stats), *[_ptr(t) for t in outs], _stream(mel)),
+            "fs2_loss_bwd")
+    return outs
+
+
 def colsum(x, out=None, accumulate=False):
     """out[n] (+)= sum over rows of x [..., N] (f32 / bf16), deterministic (fs2_colsum)."""
     _gpu(x, out)

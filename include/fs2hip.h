@@ -599,6 +599,36 @@ typedef struct fs2_pack_desc {
 int fs2_pack_train_plan(fs2_pack_desc *descs, int nd, int *blocks);
 int fs2_pack_train(const fs2_pack_desc *descs_dev, int nd, int blocks, fs2_stream_t stream);
 
+/*
+ * FastSpeech2Loss (model/loss.py:5-92) on device, no host sync:
+ * fs2_loss_fwd — out[0..5] = (total, mel L1, postnet L1, pitch MSE, energy MSE, log-duration MSE)
+ *   over the masks, stats[0..3] = the element counts (kept for the backward); ws: fs2_loss_ws_bytes().
+ *   mel / postnet f32 [B, T, n_mel] contiguous, mel_tgt f32 rows at b*tgt_bs + t*tgt_ts (the target
+ *   cropped to T frames), masks bool (1 = valid), log_d target = log(d_tgt + 1). Deterministic.
+ * fs2_loss_bwd — d(prediction) for all five from the upstream gradients grad_out[6] of out[0..5]
+ *   and the forward's stats (sign(err) for the L1 terms, 0 at err == 0, as torch's abs backward).
+ */
+typedef struct fs2_loss_args {
+  const float *mel, *postnet, *mel_tgt;
+  int64_t tgt_bs, tgt_ts;
+  const unsigned char *mel_valid;
+  int B, T, n_mel;
+  const float *p_pred, *p_tgt;
+  const unsigned char *p_mask;
+  int64_t n_p;
+  const float *e_pred, *e_tgt;
+  const unsigned char *e_mask;
+  int64_t n_e;
+  const float *logd_pred;
+  const int64_t *d_tgt;
+  const unsigned char *d_mask;
+  int64_t n_d;
+} fs2_loss_args;
+int64_t fs2_loss_ws_bytes(void);
+int fs2_loss_fwd(const fs2_loss_args *a, float *out, float *stats, float *ws, int64_t ws_bytes, fs2_stream_t stream);
+int fs2_loss_bwd(const fs2_loss_args *a, const float *grad_out, const float *stats, float *d_mel, float *d_postnet,
+                 float *d_pitch, float *d_energy, float *d_logd, fs2_stream_t stream);
+
 /* Library identification. */
 const char *fs2_version(void);
 const char *fs2_status_string(int status);

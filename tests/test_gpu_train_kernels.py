@@ -252,3 +252,45 @@ def test_embedding_bwd(ops, V, D, n, pad):
     torch.cuda.synchronize()
     assert torch.equal(o1, o2)
     assert float((o1.cpu().double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("frame_level", [False, True])
+def test_loss_fused_equals_torch(ops, frame_level, monkeypatch):
+    """FastSpeech2Loss on fs2_loss_fwd / _bwd against its torch statement (FS2_LOSS_FUSED=0): the six
+    losses rtol 1e-5, every prediction gradient within 1e-6 of its scale (same sign / count
+    arithmetic), incl. a mel target longer than the prediction (cropped) and an exact-zero error."""
+    from fs2amd.loss import FastSpeech2Loss
+
+    torch.manual_seed(7)
+    B, L, T, C = 4, 23, 57, 80
+    lvl = "frame_level" if frame_level else "phoneme_level"
+    pc = {"preprocessing": {"pitch": {"feature": lvl}, "energy": {"feature": "phoneme_level"}}}
+    src_lens, mel_lens = torch.tensor([23, 10, 1, 17]), torch.tensor([57, 30, 3, 44])
+    src_m = (torch.arange(L)[None] >= src_lens[:, None]).to(DEV)
+    mel_m = (torch.arange(T)[None] >= mel_lens[:, None]).to(DEV)
+
+    def run(fused):
+        monkeypatch.setenv("FS2_LOSS_FUSED", "1" if fused else "0")
+        torch.manual_seed(8)
+        mel = torch.randn(B, T, C, device=DEV, requires_grad=True)
+        post = torch.randn(B, T, C, device=DEV, requires_grad=True)
+        PL = T if frame_level else L
+        pp = torch.randn(B, PL, device=DEV, requires_grad=True)
+        ep = torch.randn(B, L, device=DEV, requires_grad=True)
+        ld = torch.randn(B, L, device=DEV, requires_grad=True)
+        tgt = torch.randn(B, T + 9, C, device=DEV)
+        with torch.no_grad():
+            tgt[0, 0, 0] = mel[0, 0, 0]  # exact zero error: zero L1 gradient
+        inputs = (None,) * 9 + (tgt, mel_lens.to(DEV), T + 9, torch.randn(B, PL, device=DEV),
+                                torch.randn(B, L, device=DEV), torch.randint(1, 9, (B, L), device=DEV))
+        preds = (mel, post, pp, ep, ld, None, src_m, mel_m, None, None)
+        losses = FastSpeech2Loss(pc, None)(inputs, preds)
+        (losses[0] + 0.5 * losses[2] + 0.25 * losses[5]).backward()
+        return [float(l) for l in losses], [t.grad.detach().clone() for t in (mel, post, pp, ep, ld)]
+
+    lf, gf = run(True)
+    lt, gt = run(False)
+    np = pytest.importorskip("numpy")
+    np.testing.assert_allclose(lf, lt, rtol=1e-5)
+    for a, b in zip(gf, gt):
+        assert float((a - b).abs().max()) <= 1e-6 * max(1e-3, float(b.abs().max()))
