@@ -1107,3 +1107,323 @@ extern "C" int fs2_loss_bwd(const fs2_loss_args *a, const float *grad_out, const
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// PostNet layer in train mode (transformer/Layers.py:92-137, training.py): BatchNorm1d on batch
+// statistics over all B*T frames (running stats updated with momentum, unbiased variance), tanh
+// (layers 0..3), F.dropout(0.5). Statistics: per block a two-pass (mean, M2) over its row chunk,
+// combined in block order with Chan's formula (deterministic, no E[z^2] - E[z]^2 cancellation).
+// The backward recomputes zhat and tanh from z and regenerates the dropout bits.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kBnBlocks = 256;
+
+struct BnGeom {
+  int G, RPI, cg, rsub;  // column groups of 4, rows per iteration, this thread's group / row slot
+  bool active;
+};
+
+__device__ __forceinline__ BnGeom bn_geom(int C) {
+  BnGeom g;
+  g.G = C >> 2;
+  g.RPI = 256 / g.G;
+  g.cg = threadIdx.x % g.G;
+  g.rsub = threadIdx.x / g.G;
+  g.active = g.rsub < g.RPI;
+  return g;
+}
+
+// reduce v[4] (this thread's 4 columns) over the RPI row slots through LDS; result for columns
+// [4*cg, 4*cg+4) left in v on threads with rsub == 0
+__device__ __forceinline__ void bn_row_reduce(float *red, const BnGeom &g, int C, float v[4]) {
+  __syncthreads();
+  if (g.active)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[g.rsub * C + g.cg * 4 + q] = v[q];
+  __syncthreads();
+  if (g.active && g.rsub == 0)
+    for (int r = 1; r < g.RPI; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += red[r * C + g.cg * 4 + q];
+}
+
+// part[blk][c] = (n, mean, M2) of the block's rows
+__global__ __launch_bounds__(256) void bn_stats_part_kernel(const float *__restrict__ z, int64_t R, int C, int rpb,
+                                                            float *__restrict__ part) {
+  extern __shared__ float red[];
+  const BnGeom g = bn_geom(C);
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < R ? r0 + rpb : R;
+  const float n = (float)(r1 > r0 ? r1 - r0 : 0);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (g.active)
+    for (int64_t r = r0 + g.rsub; r < r1; r += g.RPI) {
+      float v[4];
+      load4(z + r * C + g.cg * 4, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[q] += v[q];
+    }
+  bn_row_reduce(red, g, C, s);
+  __shared__ float mean_s[1024];
+  if (g.active && g.rsub == 0)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) mean_s[g.cg * 4 + q] = n > 0.f ? s[q] / n : 0.f;
+  __syncthreads();
+  float m[4], m2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (g.active) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m[q] = mean_s[g.cg * 4 + q];
+    for (int64_t r = r0 + g.rsub; r < r1; r += g.RPI) {
+      float v[4];
+      load4(z + r * C + g.cg * 4, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m2[q] += (v[q] - m[q]) * (v[q] - m[q]);
+    }
+  }
+  bn_row_reduce(red, g, C, m2);
+  if (g.active && g.rsub == 0)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float *p = part + ((int64_t)blockIdx.x * C + g.cg * 4 + q) * 3;
+      p[0] = n;
+      p[1] = m[q];
+      p[2] = m2[q];
+    }
+}
+
+__global__ __launch_bounds__(256) void bn_stats_finish_kernel(const float *__restrict__ part, int blocks, int C,
+                                                              float eps, float momentum, float *running_mean,
+                                                              float *running_var, float *__restrict__ mean_out,
+                                                              float *__restrict__ rstd_out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double n = 0.0, mean = 0.0, m2 = 0.0;  // Chan's combination in block order
+  for (int k = 0; k < blocks; ++k) {
+    const float *p = part + ((int64_t)k * C + c) * 3;
+    const double nb = p[0];
+    if (nb == 0.0) continue;
+    const double nab = n + nb, d = (double)p[1] - mean;
+    mean += d * nb / nab;
+    m2 += (double)p[2] + d * d * n * nb / nab;
+    n = nab;
+  }
+  const float var = (float)(m2 / n);
+  mean_out[c] = (float)mean;
+  rstd_out[c] = rsqrtf(var + eps);
+  if (running_mean != nullptr) {
+    running_mean[c] = (1.0f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.0f - momentum) * running_var[c] + momentum * (float)(m2 / (n > 1.0 ? n - 1.0 : 1.0));
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float *__restrict__ z, int64_t R, int C,
+                                                       const float *__restrict__ mean, const float *__restrict__ rstd,
+                                                       const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                       int use_tanh, uint32_t thr, float scale, const int64_t *seed,
+                                                       uint32_t salt, const float *__restrict__ residual,
+                                                       bf16 *__restrict__ y_bf, float *__restrict__ y_f32) {
+  const uint32_t key = drop_key(seed, salt);
+  const int64_t n4 = R * (C >> 2);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / (C >> 2);
+    const int c = (int)(i - row * (C >> 2)) * 4;
+    float v[4], mu[4], rs[4], g[4], b[4];
+    load4(z + row * C + c, v);
+    load4(mean + c, mu);
+    load4(rstd + c, rs);
+    load4(gamma + c, g);
+    load4(beta + c, b);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] = (v[q] - mu[q]) * rs[q] * g[q] + b[q];
+      if (use_tanh) v[q] = tanhf(v[q]);
+    }
+    if (thr != 0) {
+      const unsigned k = keep4(key, (uint32_t)(row * C + c), thr);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = ((k >> q) & 1) ? v[q] * scale : 0.0f;
+    }
+    if (residual != nullptr) {
+      float r[4];
+      load4(residual + row * C + c, r);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += r[q];
+    }
+    if (y_bf != nullptr) store4(y_bf + row * C + c, v);
+    if (y_f32 != nullptr) store4(y_f32 + row * C + c, v);
+  }
+}
+
+// backward pass 1: per block, per column: sum dpre and sum dpre * zhat, dpre = dy * keep * scale * tanh'
+__device__ __forceinline__ void bn_dpre(const float *dy, const float *z, int64_t row, int C, int c, const float *mu,
+                                        const float *rs, const float *g, const float *b, int use_tanh, uint32_t key,
+                                        uint32_t thr, float scale, float dp[4], float zh[4]) {
+  float d[4], v[4];
+  load4(dy + row * C + c, d);
+  load4(z + row * C + c, v);
+  unsigned k = 0xf;
+  if (thr != 0) k = keep4(key, (uint32_t)(row * C + c), thr);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    zh[q] = (v[q] - mu[q]) * rs[q];
+    float t = ((k >> q) & 1) ? d[q] * scale : 0.0f;
+    if (use_tanh) {
+      const float a = tanhf(zh[q] * g[q] + b[q]);
+      t *= 1.0f - a * a;
+    }
+    dp[q] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_part_kernel(const float *__restrict__ dy, const float *__restrict__ z,
+                                                          int64_t R, int C, int rpb, const float *__restrict__ mean,
+                                                          const float *__restrict__ rstd, const float *__restrict__ gamma,
+                                                          const float *__restrict__ beta, int use_tanh, uint32_t thr,
+                                                          float scale, const int64_t *seed, uint32_t salt,
+                                                          float *__restrict__ part) {
+  extern __shared__ float red[];
+  const BnGeom g = bn_geom(C);
+  const uint32_t key = drop_key(seed, salt);
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < R ? r0 + rpb : R;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (g.active) {
+    const int c = g.cg * 4;
+    float mu[4], rs[4], ga[4], be[4];
+    load4(mean + c, mu);
+    load4(rstd + c, rs);
+    load4(gamma + c, ga);
+    load4(beta + c, be);
+    for (int64_t r = r0 + g.rsub; r < r1; r += g.RPI) {
+      float dp[4], zh[4];
+      bn_dpre(dy, z, r, C, c, mu, rs, ga, be, use_tanh, key, thr, scale, dp, zh);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s1[q] += dp[q];
+        s2[q] += dp[q] * zh[q];
+      }
+    }
+  }
+  bn_row_reduce(red, g, C, s1);
+  bn_row_reduce(red, g, C, s2);
+  if (g.active && g.rsub == 0)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float *p = part + ((int64_t)blockIdx.x * C + g.cg * 4 + q) * 2;
+      p[0] = s1[q];
+      p[1] = s2[q];
+    }
+}
+
+// dbeta = sum dpre, dgamma = sum dpre * zhat (in block order); sums kept for pass 2 in sums[2][C]
+__global__ __launch_bounds__(256) void bn_bwd_finish_kernel(const float *__restrict__ part, int blocks, int C,
+                                                            float *dgamma, float *dbeta, int accumulate,
+                                                            float *__restrict__ sums) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < blocks; ++k) {
+    const float *p = part + ((int64_t)k * C + c) * 2;
+    a += p[0];
+    b += p[1];
+  }
+  sums[c] = a;
+  sums[C + c] = b;
+  dbeta[c] = accumulate ? dbeta[c] + a : a;
+  dgamma[c] = accumulate ? dgamma[c] + b : b;
+}
+
+// dz = gamma * rstd * (dpre - sum(dpre)/N - zhat * sum(dpre * zhat)/N) -> bf16
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float *__restrict__ dy, const float *__restrict__ z,
+                                                           int64_t R, int C, const float *__restrict__ mean,
+                                                           const float *__restrict__ rstd,
+                                                           const float *__restrict__ gamma,
+                                                           const float *__restrict__ beta, int use_tanh, uint32_t thr,
+                                                           float scale, const int64_t *seed, uint32_t salt,
+                                                           const float *__restrict__ sums, bf16 *__restrict__ dz) {
+  const uint32_t key = drop_key(seed, salt);
+  const float invn = 1.0f / (float)R;
+  const int64_t n4 = R * (C >> 2);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / (C >> 2);
+    const int c = (int)(i - row * (C >> 2)) * 4;
+    float mu[4], rs[4], ga[4], be[4], s1[4], s2[4], dp[4], zh[4], o[4];
+    load4(mean + c, mu);
+    load4(rstd + c, rs);
+    load4(gamma + c, ga);
+    load4(beta + c, be);
+    load4(sums + c, s1);
+    load4(sums + C + c, s2);
+    bn_dpre(dy, z, row, C, c, mu, rs, ga, be, use_tanh, key, thr, scale, dp, zh);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = ga[q] * rs[q] * (dp[q] - s1[q] * invn - zh[q] * s2[q] * invn);
+    store4(dz + row * C + c, o);
+  }
+}
+
+int bn_blocks(int64_t R, int *rpb) {
+  int nb = (int)(R < kBnBlocks ? (R > 0 ? R : 1) : kBnBlocks);
+  *rpb = (int)((R + nb - 1) / nb);
+  return nb;
+}
+
+unsigned bn_grid(int64_t R, int C) {
+  const int64_t n = (R * (C >> 2) + 255) / 256;
+  return (unsigned)(n < 1 ? 1 : (n > 4096 ? 4096 : n));
+}
+
+}  // namespace
+
+extern "C" int64_t fs2_bn_train_ws_bytes(int C) { return (int64_t)kBnBlocks * C * 3 * (int64_t)sizeof(float) + 2LL * C * 4; }
+
+extern "C" int fs2_bn_train_fwd(const float *z, int64_t R, int C, const float *gamma, const float *beta, float eps,
+                                float momentum, float *running_mean, float *running_var, int use_tanh, float p_drop,
+                                const int64_t *seed, int salt, const float *residual, void *y_bf, float *y_f32,
+                                float *mean, float *rstd, float *ws, int64_t ws_bytes, fs2_stream_t stream) {
+  if (z == nullptr || gamma == nullptr || beta == nullptr || mean == nullptr || rstd == nullptr || ws == nullptr ||
+      (y_bf == nullptr && y_f32 == nullptr))
+    return FS2_EINVAL;
+  if (R <= 0 || C <= 0 || (C & 3) || C > 1024 || !(p_drop >= 0.0f && p_drop < 1.0f) ||
+      (p_drop > 0.0f && seed == nullptr) || ((running_mean == nullptr) != (running_var == nullptr)))
+    return FS2_EINVAL;
+  if (ws_bytes < fs2_bn_train_ws_bytes(C)) return FS2_EINVAL;
+  hipStream_t s = as_stream(stream);
+  int rpb;
+  const int nb = bn_blocks(R, &rpb);
+  const size_t lds = (size_t)(256 / (C >> 2)) * C * sizeof(float);
+  hipLaunchKernelGGL(bn_stats_part_kernel, dim3(nb), dim3(256), lds, s, z, R, C, rpb, ws);
+  hipLaunchKernelGGL(bn_stats_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, nb, C, eps, momentum,
+                     running_mean, running_var, mean, rstd);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(bn_grid(R, C)), dim3(256), 0, s, z, R, C, mean, rstd, gamma, beta, use_tanh,
+                     drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt, residual,
+                     reinterpret_cast<bf16 *>(y_bf), y_f32);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_bn_train_bwd(const float *dy, const float *z, int64_t R, int C, const float *gamma,
+                                const float *beta, const float *mean, const float *rstd, int use_tanh, float p_drop,
+                                const int64_t *seed, int salt, void *dz, float *dgamma, float *dbeta, int accumulate,
+                                float *ws, int64_t ws_bytes, fs2_stream_t stream) {
+  if (dy == nullptr || z == nullptr || gamma == nullptr || beta == nullptr || mean == nullptr || rstd == nullptr ||
+      dz == nullptr || dgamma == nullptr || dbeta == nullptr || ws == nullptr)
+    return FS2_EINVAL;
+  if (R <= 0 || C <= 0 || (C & 3) || C > 1024 || !(p_drop >= 0.0f && p_drop < 1.0f) ||
+      (p_drop > 0.0f && seed == nullptr))
+    return FS2_EINVAL;
+  if (ws_bytes < fs2_bn_train_ws_bytes(C)) return FS2_EINVAL;
+  hipStream_t s = as_stream(stream);
+  int rpb;
+  const int nb = bn_blocks(R, &rpb);
+  const size_t lds = (size_t)(256 / (C >> 2)) * C * sizeof(float);
+  const uint32_t thr = drop_threshold(p_drop);
+  const float scale = 1.0f / (1.0f - p_drop);
+  float *sums = ws + (int64_t)kBnBlocks * C * 3;
+  hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(nb), dim3(256), lds, s, dy, z, R, C, rpb, mean, rstd, gamma, beta,
+                     use_tanh, thr, scale, seed, (uint32_t)salt, ws);
+  hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, nb, C, dgamma, dbeta, accumulate,
+                     sums);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_grid(R, C)), dim3(256), 0, s, dy, z, R, C, mean, rstd, gamma, beta,
+                     use_tanh, thr, scale, seed, (uint32_t)salt, sums, reinterpret_cast<bf16 *>(dz));
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}

@@ -164,6 +164,9 @@ SIGNATURES = {
     "fs2_loss_ws_bytes": (_i64, []),
     "fs2_loss_fwd": (_i, [_p, _p, _p, _p, _i64, _p]),
     "fs2_loss_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "fs2_bn_train_ws_bytes": (_i64, [_i]),
+    "fs2_bn_train_fwd": (_i, [_p, _i64, _i, _p, _p, _f, _f, _p, _p, _i, _f, _p, _i, _p, _p, _p, _p, _p, _p, _i64, _p]),
+    "fs2_bn_train_bwd": (_i, [_p, _p, _i64, _i, _p, _p, _p, _p, _i, _f, _p, _i, _p, _p, _p, _i, _p, _i64, _p]),
     "fs2_colsum_ws_bytes": (_i64, [_i]),
     "fs2_colsum": (_i, [_p, _i, _i64, _i, _i64, _p, _i, _p, _i64, _p]),
     "fs2_conv_wgrad_ws_bytes": (_i64, [_i, _i, _i, _i, _i]),

@@ -1065,6 +1065,47 @@ def loss_bwd(args, keep, grad_out, stats, shapes):
     return outs
 
 
+def bn_train_fwd(z, gamma, beta, eps, momentum, running_mean=None, running_var=None, use_tanh=True, p_drop=0.0,
+                 seed=None, salt=0, residual=None, want_bf16=True, want_f32=False):
+    """PostNet BatchNorm (batch statistics) + tanh + dropout (+ residual) over z f32 [..., C]
+    (fs2_bn_train_fwd): returns (y bf16 or None, y f32 or None, mean, rstd); running stats updated
+    in place."""
+    _gpu(z, gamma, beta, running_mean, running_var, seed, residual)
+    C = z.shape[-1]
+    R = z.numel() // C
+    assert z.dtype == torch.float32 and z.is_contiguous()
+    yb = torch.empty(z.shape, device=z.device, dtype=torch.bfloat16) if want_bf16 else None
+    yf = torch.empty_like(z) if want_f32 else None
+    mean = torch.empty(C, device=z.device, dtype=torch.float32)
+    rstd = torch.empty(C, device=z.device, dtype=torch.float32)
+    ws = torch.empty(_lib.fs2_bn_train_ws_bytes(C) // 4, device=z.device, dtype=torch.float32)
+    if residual is not None:
+        residual = residual.contiguous()
+    L.check(_lib.fs2_bn_train_fwd(_ptr(z), R, C, _ptr(gamma), _ptr(beta), float(eps), float(momentum),
+                                  _ptr(running_mean), _ptr(running_var), 1 if use_tanh else 0, float(p_drop),
+                                  _ptr(seed), int(salt), _ptr(residual), _ptr(yb), _ptr(yf), _ptr(mean), _ptr(rstd),
+                                  _ptr(ws), ws.numel() * 4, _stream(z)), "fs2_bn_train_fwd")
+    return yb, yf, mean, rstd
+
+
+def bn_train_bwd(dy, z, gamma, beta, mean, rstd, use_tanh=True, p_drop=0.0, seed=None, salt=0, dgamma=None,
+                 dbeta=None, accumulate=False):
+    """Backward of :func:`bn_train_fwd` (fs2_bn_train_bwd): (dz bf16, dgamma, dbeta)."""
+    _gpu(dy, z, gamma, beta, mean, rstd, seed)
+    C = z.shape[-1]
+    R = z.numel() // C
+    dy = dy.contiguous()
+    dz = torch.empty(z.shape, device=z.device, dtype=torch.bfloat16)
+    dgamma = torch.empty(C, device=z.device, dtype=torch.float32) if dgamma is None else dgamma
+    dbeta = torch.empty(C, device=z.device, dtype=torch.float32) if dbeta is None else dbeta
+    ws = torch.empty(_lib.fs2_bn_train_ws_bytes(C) // 4, device=z.device, dtype=torch.float32)
+    L.check(_lib.fs2_bn_train_bwd(_ptr(dy), _ptr(z), R, C, _ptr(gamma), _ptr(beta), _ptr(mean), _ptr(rstd),
+                                  1 if use_tanh else 0, float(p_drop), _ptr(seed), int(salt), _ptr(dz), _ptr(dgamma),
+                                  _ptr(dbeta), 1 if accumulate else 0, _ptr(ws), ws.numel() * 4, _stream(z)),
+            "fs2_bn_train_bwd")
+    return dz, dgamma, dbeta
+
+
 def colsum(x, out=None, accumulate=False):
     """out[n] (+)= sum over rows of x [..., N] (f32 / bf16), deterministic (fs2_colsum)."""
     _gpu(x, out)

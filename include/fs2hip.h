@@ -629,6 +629,26 @@ int fs2_loss_fwd(const fs2_loss_args *a, float *out, float *stats, float *ws, in
 int fs2_loss_bwd(const fs2_loss_args *a, const float *grad_out, const float *stats, float *d_mel, float *d_postnet,
                  float *d_pitch, float *d_energy, float *d_logd, fs2_stream_t stream);
 
+/*
+ * PostNet layer in train mode (transformer/Layers.py:92-137 with BatchNorm1d on batch statistics):
+ * fs2_bn_train_fwd — z f32 [R, C] (the conv output, R = B*T frames, C % 4 == 0, C <= 1024):
+ *   mean / var over the R rows (biased; deterministic Chan combination of per-block two-pass
+ *   moments), running_mean / running_var updated with momentum (unbiased variance; both may be
+ *   null), y = dropout(act(gamma * (z - mean) * rstd + beta)) (+ residual) with act = tanh when
+ *   use_tanh; y_bf (bf16) and / or y_f32 written; mean / rstd [C] saved.
+ * fs2_bn_train_bwd — dz bf16 [R, C] from dy f32 (recomputing zhat, tanh and the dropout bits);
+ *   dgamma / dbeta (+)=. ws: fs2_bn_train_ws_bytes(C) for both.
+ */
+int64_t fs2_bn_train_ws_bytes(int C);
+int fs2_bn_train_fwd(const float *z, int64_t R, int C, const float *gamma, const float *beta, float eps,
+                     float momentum, float *running_mean, float *running_var, int use_tanh, float p_drop,
+                     const int64_t *seed, int salt, const float *residual, void *y_bf, float *y_f32, float *mean,
+                     float *rstd, float *ws, int64_t ws_bytes, fs2_stream_t stream);
+int fs2_bn_train_bwd(const float *dy, const float *z, int64_t R, int C, const float *gamma, const float *beta,
+                     const float *mean, const float *rstd, int use_tanh, float p_drop, const int64_t *seed, int salt,
+                     void *dz, float *dgamma, float *dbeta, int accumulate, float *ws, int64_t ws_bytes,
+                     fs2_stream_t stream);
+
 /* Library identification. */
 const char *fs2_version(void);
 const char *fs2_status_string(int status);
