@@ -390,6 +390,103 @@ def _embed(emb, idx, fused):
     return EmbeddingFn.apply(idx, emb.weight, emb.padding_idx)
 
 
+def _packT_any(w):
+    """Input-gradient weight of a conv whose output width may need channel padding as the
+    transposed conv's input (PostNet's 80 mel channels)."""
+    N = w.shape[0]
+    if N == ops.cin_pad(N, L.FS2_BF16):
+        return _packT(w)
+    return ops.pack_conv_weight(w.detach().flip(-1).transpose(0, 1), L.FS2_BF16)
+
+
+class PostNetFn(torch.autograd.Function):
+    """The PostNet (transformer/Layers.py:92-137) in train mode + the residual (fastspeech2.py:136)
+    as one node: per layer fs2_conv1d (f32 out) -> fs2_bn_train_fwd (batch-statistic BatchNorm with
+    running-stat update, tanh on layers 0..3, dropout 0.5, bf16 copy for the next conv; the last
+    adds mel); backward per layer fs2_bn_train_bwd -> fs2_conv_wgrad (+ bias) -> input-gradient
+    conv (the first one adds the residual's gradient in its epilogue)."""
+
+    @staticmethod
+    def forward(ctx, mel, meta, *params):
+        postnet, p_drop, seed, salt = meta
+        convs = postnet.convolutions
+        n = len(convs)
+        BF = L.FS2_BF16
+        x_bf = mel.detach().to(torch.bfloat16)
+        saved = []
+        out = None
+        for i, seq in enumerate(convs):
+            bn = seq[1]
+            w, b, g, be = params[4 * i:4 * i + 4]
+            N, Cin, KS = w.shape
+            pad = (KS - 1) // 2
+            z = ops.conv1d(x_bf, ops.pack_conv_weight(w, BF), b.detach(), cin=Cin, ks=KS, pad=pad, compute=BF,
+                           epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+            last = i == n - 1
+            yb, yf, mean, rstd = ops.bn_train_fwd(z, g.detach(), be.detach(), bn.eps, bn.momentum, bn.running_mean,
+                                                  bn.running_var, use_tanh=not last, p_drop=p_drop, seed=seed,
+                                                  salt=salt + i, residual=mel.detach() if last else None,
+                                                  want_bf16=not last, want_f32=last)
+            if bn.num_batches_tracked is not None:
+                bn.num_batches_tracked.add_(1)
+            saved.append((x_bf, z, mean, rstd, _packT_any(w), pad, KS))
+            x_bf, out = yb, yf
+        ctx.saved = saved
+        ctx.meta = (p_drop, seed, salt)
+        ctx.save_for_backward(*params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        params = ctx.saved_tensors
+        p_drop, seed, salt = ctx.meta
+        n = len(ctx.saved)
+        dout = dout.contiguous()
+        sink = _SINK[0] and all(t.grad is not None for t in params)
+        grads = [None] * len(params)
+        dy = dout
+        dmel = None
+        for i in reversed(range(n)):
+            x_bf, z, mean, rstd, wT, pad, KS = ctx.saved[i]
+            w, b, g, be = params[4 * i:4 * i + 4]
+            N = w.shape[0]
+            last = i == n - 1
+            dz, dg, dbe = ops.bn_train_bwd(dy, z, g.detach(), be.detach(), mean, rstd, use_tanh=not last,
+                                           p_drop=p_drop, seed=seed, salt=salt + i,
+                                           dgamma=g.grad if sink else None, dbeta=be.grad if sink else None,
+                                           accumulate=sink)
+            dw, db = ops.conv_wgrad(dz, x_bf, KS, pad, dw=w.grad if sink else None, db=b.grad if sink else None,
+                                    want_db=True, accumulate=sink)
+            if not sink:
+                grads[4 * i:4 * i + 4] = [dw, db, dg, dbe]
+            if i > 0:
+                dy = ops.conv1d(dz, wT, None, cin=N, ks=KS, pad=KS - 1 - pad, compute=L.FS2_BF16,
+                                epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+            else:
+                dmel = ops.conv1d(dz, wT, None, cin=N, ks=KS, pad=KS - 1 - pad, compute=L.FS2_BF16,
+                                  epilogue=L.EPI_BIAS_RES, out_dtype=L.FS2_F32, residual=dout)
+        return (dmel, None, *grads)
+
+
+def _postnet_fused_ok(postnet, compute):
+    if os.environ.get("FS2_TRAIN_FUSED", "1") == "0" or compute != L.FS2_BF16:
+        return False
+    for seq in postnet.convolutions:
+        conv, bn = seq[0].conv, seq[1]
+        if conv.kernel_size[0] not in (1, 3, 5, 9) or conv.out_channels % 8 or conv.in_channels % 8 or \
+                conv.out_channels > 1024 or bn.momentum is None or not bn.track_running_stats:
+            return False
+    return True
+
+
+def _postnet_params(postnet):
+    ps = []
+    for seq in postnet.convolutions:
+        conv, bn = seq[0].conv, seq[1]
+        ps += [conv.weight, conv.bias, bn.weight, bn.bias]
+    return ps
+
+
 def fft_block_fused(blk, x, x_bf, lens, seed, salt, p_drop, packed=None):
     y, yb = FFTBlockFn.apply(x, x_bf, lens, seed, (blk, float(p_drop), int(salt), packed), *_block_params(blk))
     return y, yb
@@ -602,9 +699,12 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
 
     # mel_linear + PostNet (+ residual) (fastspeech2.py:134-136, transformer/Layers.py:129-137)
     mel = linear(x, model.mel_linear, compute)
+    p_post = 0.5 if training else 0.0
+    if fused and model.training and _postnet_fused_ok(model.postnet, compute):
+        postnet_mel = PostNetFn.apply(mel, (model.postnet, p_post, seed, 2000), *_postnet_params(model.postnet))
+        return (mel, postnet_mel, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)
     y = mel
     n = len(model.postnet.convolutions)
-    p_post = 0.5 if training else 0.0
     for i, seq in enumerate(model.postnet.convolutions):
         conv, bn = seq[0].conv, seq[1]
         z = conv1d(y, conv, (conv.kernel_size[0] - 1) // 2, compute)

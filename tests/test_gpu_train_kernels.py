@@ -294,3 +294,48 @@ def test_loss_fused_equals_torch(ops, frame_level, monkeypatch):
     np.testing.assert_allclose(lf, lt, rtol=1e-5)
     for a, b in zip(gf, gt):
         assert float((a - b).abs().max()) <= 1e-6 * max(1e-3, float(b.abs().max()))
+
+
+@pytest.mark.parametrize("C,use_tanh,p", [(512, True, 0.5), (80, False, 0.5), (512, True, 0.0)])
+def test_bn_train_fwd_bwd(ops, C, use_tanh, p):
+    """fs2_bn_train_fwd / _bwd (a PostNet layer in train mode: BatchNorm1d on batch statistics with
+    the running-stat update, tanh, dropout; transformer/Layers.py:92-137) against float64 autograd
+    of F.batch_norm(training=True) with the kernel's keep mask (read back with gamma = 0, beta = 1):
+    y within 2e-5 (f32 path) / 1e-2 (bf16 copy) of its scale, running stats rtol 1e-5, dz within
+    1e-2 (bf16), dgamma / dbeta rtol 1e-4."""
+    torch.manual_seed(C + int(use_tanh))
+    R = 3 * 37
+    z = torch.randn(R, C) * 2 + 0.5
+    g, b = 1 + 0.1 * torch.randn(C), 0.1 * torch.randn(C)
+    res = torch.randn(R, C)
+    seed = torch.tensor([77], dtype=torch.int64, device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    yb, yf, mean, rstd = ops.bn_train_fwd(z.to(DEV), g.to(DEV), b.to(DEV), 1e-5, 0.1, rm, rv, use_tanh, p, seed, 3,
+                                          residual=None if use_tanh else res.to(DEV), want_bf16=True, want_f32=True)
+    if p > 0:
+        kb, kf, _, _ = ops.bn_train_fwd(z.to(DEV), torch.zeros(C, device=DEV), torch.ones(C, device=DEV), 1e-5, 0.1,
+                                        None, None, True, p, seed, 3, want_bf16=False, want_f32=True)
+        keep = (kf != 0).cpu()
+        assert abs(float(keep.float().mean()) - (1 - p)) < 0.02
+    else:
+        keep = torch.ones(R, C, dtype=torch.bool)
+    zd = z.double().requires_grad_()
+    gd, bd = g.double().requires_grad_(), b.double().requires_grad_()
+    rmr, rvr = torch.zeros(C, dtype=torch.float64), torch.ones(C, dtype=torch.float64)
+    v = F.batch_norm(zd, rmr, rvr, gd, bd, True, 0.1, 1e-5)
+    if use_tanh:
+        v = torch.tanh(v)
+    ref = v * keep / (1 - p) + (0 if use_tanh else res.double())
+    torch.cuda.synchronize()
+    sc = float(ref.abs().max())
+    assert float((yf.cpu().double() - ref).abs().max()) <= 2e-5 * sc
+    assert float((yb.cpu().double() - ref).abs().max()) <= 1e-2 * sc
+    assert torch.allclose(rm.cpu().double(), rmr, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(rv.cpu().double(), rvr, rtol=1e-5, atol=1e-6)
+    dy = torch.randn(R, C)
+    ref.backward(dy.double())
+    dz, dg, dbe = ops.bn_train_bwd(dy.to(DEV), z.to(DEV), g.to(DEV), b.to(DEV), mean, rstd, use_tanh, p, seed, 3)
+    torch.cuda.synchronize()
+    assert float((dz.cpu().double() - zd.grad).abs().max()) <= 1e-2 * float(zd.grad.abs().max())
+    assert torch.allclose(dg.cpu().double(), gd.grad, rtol=1e-4, atol=1e-4 * float(gd.grad.abs().max()))
+    assert torch.allclose(dbe.cpu().double(), bd.grad, rtol=1e-4, atol=1e-4 * float(bd.grad.abs().max()))
