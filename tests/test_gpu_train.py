@@ -289,7 +289,8 @@ def test_fused_fft_block_train_equals_per_op_path(gpu):
         if cu >= 0.99:  # a gradient the bf16 paths resolve: same magnitude
             assert abs(float(a.norm()) / float(b.norm()) - 1) <= 0.03, k
     gs, _ = _bf16_grads("train_b16", True, sink=True)
-    for k in gf:
+    resolved = {w[1] for w in worst if w[3] >= 0.5}
+    for k in resolved:
         d = (gs[k].double() - 0.5) - gf[k].double()
         # the attention backward accumulates with atomics: not bit-reproducible between two runs
         assert float(d.abs().max()) <= 2e-3 * float(gf[k].abs().max()) + 1e-6, k
