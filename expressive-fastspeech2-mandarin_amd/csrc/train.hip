@@ -43,6 +43,30 @@ __device__ __forceinline__ bool row_masked(const int64_t *lens, int64_t row, int
   return row - b * T >= lens[b];
 }
 
+// Deterministic split-partial sums for the finish kernels: a 256-thread block = 4 row groups x 64
+// columns; row group g sums partials g, g+4, ... (two independent accumulators, unrolled loads),
+// the 4 group sums are added in a fixed order through LDS. Every thread of the block must call it
+// (it synchronises); the result is valid in all threads of the column.
+__device__ __forceinline__ float parts_col_sum(const float *__restrict__ part, int S, int64_t M, int64_t col) {
+  __shared__ float red[4][64];
+  const int rg = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  float a0 = 0.f, a1 = 0.f;
+  if (col < M) {
+    int k = rg;
+#pragma unroll 4
+    for (; k + 4 < S; k += 8) {
+      a0 += part[(int64_t)k * M + col];
+      a1 += part[(int64_t)(k + 4) * M + col];
+    }
+    if (k < S) a0 += part[(int64_t)k * M + col];
+  }
+  red[rg][cl] = a0 + a1;
+  __syncthreads();
+  const float r = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+  __syncthreads();
+  return r;
+}
+
 template <typename TR>
 __global__ __launch_bounds__(256) void res_ln_fwd_kernel(const float *__restrict__ a, const TR *__restrict__ res,
                                                          const float *__restrict__ gamma, const float *__restrict__ beta,
@@ -316,25 +340,22 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const T *__restrict__ 
         (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
-// pass 2: out[n] (+)= sum over chunks of part[chunk][n], chunks in order (deterministic)
+// pass 2: out[n] (+)= sum over chunks of part[chunk][n] (parts_col_sum: deterministic)
 __global__ __launch_bounds__(256) void colsum_finish_kernel(const float *__restrict__ part, int chunks, int N,
                                                             float *__restrict__ out, int accumulate) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int k = 0; k < chunks; ++k) s += part[(int64_t)k * N + n];
-  out[n] = accumulate ? out[n] + s : s;
+  const int64_t n = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const float s = parts_col_sum(part, chunks, N, n);
+  if (threadIdx.x < 64 && n < N) out[n] = accumulate ? out[n] + s : s;
 }
 
-// LN backward pass 2: (dgamma, dbeta, dbias)[n] (+)= sum over blocks, in block order
+// LN backward pass 2: (dgamma, dbeta, dbias)[n] (+)= sum over the partial blocks (part[blk][3][kD])
 __global__ __launch_bounds__(256) void ln_finish_kernel(const float *__restrict__ part, int chunks, float *dgamma,
                                                         float *dbeta, float *dbias, int accumulate) {
-  const int which = blockIdx.x, n = threadIdx.x;
+  const int64_t col = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);  // which * kD + n
+  const float s = parts_col_sum(part, chunks, 3 * kD, col);
+  const int which = (int)(col / kD), n = (int)(col - (int64_t)which * kD);
   float *out = which == 0 ? dgamma : (which == 1 ? dbeta : dbias);
-  if (out == nullptr) return;
-  float s = 0.f;
-  for (int k = 0; k < chunks; ++k) s += part[((int64_t)k * 3 + which) * kD + n];
-  out[n] = accumulate ? out[n] + s : s;
+  if (threadIdx.x < 64 && out != nullptr) out[n] = accumulate ? out[n] + s : s;
 }
 
 uint32_t drop_threshold(float p) {
@@ -403,7 +424,7 @@ extern "C" int fs2_res_ln_bwd(const float *dy, const float *xhat, const float *r
   const int grid = (int)(b64 < kLnBlocks ? b64 : kLnBlocks);
   hipLaunchKernelGGL(res_ln_bwd_kernel, dim3(grid), dim3(256), 0, s, dy, xhat, rstd, gamma, lens, R, T, thr, scale,
                      seed, (uint32_t)salt, dres, reinterpret_cast<bf16 *>(da), ws);
-  hipLaunchKernelGGL(ln_finish_kernel, dim3(3), dim3(kD), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
+  hipLaunchKernelGGL(ln_finish_kernel, dim3(3 * kD / 64), dim3(256), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
@@ -448,7 +469,7 @@ extern "C" int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xha
   hipLaunchKernelGGL(relu_ln_bwd_kernel, dim3(grid), dim3(256), 0, s, dy, a, xhat, rstd, gamma, R,
                      drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt,
                      reinterpret_cast<bf16 *>(da), ws);
-  hipLaunchKernelGGL(ln_finish_kernel, dim3(3), dim3(kD), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
+  hipLaunchKernelGGL(ln_finish_kernel, dim3(3 * kD / 64), dim3(256), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
@@ -484,7 +505,7 @@ extern "C" int fs2_colsum(const void *x, int dtype, int64_t R, int N, int64_t ro
                        row_stride, rpc, ws);
   else
     return FS2_EUNSUPPORTED;
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, ws, chunks, N, out,
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, s, ws, chunks, N, out,
                      accumulate);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
@@ -743,25 +764,22 @@ struct WgOut {
 
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restrict__ part, int S, int KS, int N, int C,
                                                            WgOut o, int accumulate) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (n, c)
-  if (e >= (int64_t)N * C) return;
   const int64_t NC = (int64_t)N * C;
-  const int n = (int)(e / C), which = n / o.split;
-  const int64_t el = e - (int64_t)which * o.split * C;
-  for (int k = 0; k < KS; ++k) {
-    float sacc = 0.f;
-    for (int s = 0; s < S; ++s) sacc += part[((int64_t)s * KS + k) * NC + e];
-    float *dst = o.dw[which] + el * KS + k;
-    *dst = accumulate ? *dst + sacc : sacc;
-  }
+  const int64_t e = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);  // (k, n, c) of part's rows
+  const float sacc = parts_col_sum(part, S, NC * KS, e);
+  if (threadIdx.x >= 64 || e >= NC * KS) return;
+  const int k = (int)(e / NC);
+  const int64_t nc = e - (int64_t)k * NC;
+  const int n = (int)(nc / C), which = n / o.split;
+  float *dst = o.dw[which] + (nc - (int64_t)which * o.split * C) * KS + k;
+  *dst = accumulate ? *dst + sacc : sacc;
 }
 
 __global__ __launch_bounds__(256) void bias_reduce_kernel(const float *__restrict__ part, int S, int N, WgOut o,
                                                           int accumulate) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int k = 0; k < S; ++k) s += part[(int64_t)k * N + n];
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float s = parts_col_sum(part, S, N, n);
+  if (threadIdx.x >= 64 || n >= N) return;
   const int which = n / o.split;
   float *dst = o.db[which] + (n - which * o.split);
   *dst = accumulate ? *dst + s : s;
@@ -778,7 +796,7 @@ void wgrad_launch(const WgArgs &a, bool dy_f32, int tiles, hipStream_t s) {
 int wgrad_splits(int tiles, int Q) {
   int S = (512 + tiles - 1) / tiles;
   if (S > Q) S = Q;
-  if (S > 64) S = 64;
+  if (S > 32) S = 32;
   return S < 1 ? 1 : S;
 }
 
@@ -845,10 +863,10 @@ extern "C" int fs2_conv_wgrad(const void *dy, int dy_dtype, int64_t dy_row_strid
     case 5: wgrad_launch<5, 1, 1>(a, f32, tiles, s); break;
     default: wgrad_launch<9, 1, 1>(a, f32, tiles, s); break;
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(((int64_t)N * C + 255) / 256)), dim3(256), 0, s, ws, a.S,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(((int64_t)N * C * KS + 63) / 64)), dim3(256), 0, s, ws, a.S,
                      KS, N, C, o, accumulate);
   if (db != nullptr)
-    hipLaunchKernelGGL(bias_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, a.pbias, a.S, N, o,
+    hipLaunchKernelGGL(bias_reduce_kernel, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, s, a.pbias, a.S, N, o,
                        accumulate);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
@@ -1000,16 +1018,14 @@ __global__ __launch_bounds__(256) void loss_part_kernel(fs2_loss_args a, float *
 }
 
 // out[0..5] = total, mel, postnet, pitch, energy, duration; stats[0..3] = n_mel_elems, n_p, n_e, n_d
-__global__ __launch_bounds__(64) void loss_finish_kernel(const float *__restrict__ part, int blocks, int n_mel,
-                                                         float *__restrict__ out, float *__restrict__ stats) {
-  __shared__ float s[kLossQ];
-  if (threadIdx.x < kLossQ) {
-    float v = 0.f;
-    for (int k = 0; k < blocks; ++k) v += part[(int64_t)k * kLossQ + threadIdx.x];
-    s[threadIdx.x] = v;
-  }
+__global__ __launch_bounds__(256) void loss_finish_kernel(const float *__restrict__ part, int blocks, int n_mel,
+                                                          float *__restrict__ out, float *__restrict__ stats) {
+  __shared__ float sv[kLossQ];
+  const float v = parts_col_sum(part, blocks, kLossQ, threadIdx.x & 63);
+  if (threadIdx.x < kLossQ) sv[threadIdx.x] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
+    const float *s = sv;
     const float nm = s[2] * (float)n_mel;
     const float mel = s[0] / nm, post = s[1] / nm, pl = s[3] / s[4], el = s[5] / s[6], dl = s[7] / s[8];
     out[1] = mel;
@@ -1087,7 +1103,7 @@ extern "C" int fs2_loss_fwd(const fs2_loss_args *a, float *out, float *stats, fl
   if (out == nullptr || stats == nullptr || ws == nullptr || ws_bytes < fs2_loss_ws_bytes()) return FS2_EINVAL;
   hipStream_t s = as_stream(stream);
   hipLaunchKernelGGL(loss_part_kernel, dim3(kLossBlocks), dim3(256), 0, s, *a, ws);
-  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(64), 0, s, ws, kLossBlocks, a->n_mel, out, stats);
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(256), 0, s, ws, kLossBlocks, a->n_mel, out, stats);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
@@ -1195,16 +1211,34 @@ __global__ __launch_bounds__(256) void bn_stats_finish_kernel(const float *__res
                                                               float eps, float momentum, float *running_mean,
                                                               float *running_var, float *__restrict__ mean_out,
                                                               float *__restrict__ rstd_out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  double n = 0.0, mean = 0.0, m2 = 0.0;  // Chan's combination in block order
-  for (int k = 0; k < blocks; ++k) {
-    const float *p = part + ((int64_t)k * C + c) * 3;
-    const double nb = p[0];
+  // Chan's combination: row group g combines partial blocks g, g+4, ... in order, then the four
+  // group results are combined in order (deterministic)
+  __shared__ double red[3][4][64];
+  const int rg = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + cl;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  if (c < C)
+    for (int k = rg; k < blocks; k += 4) {
+      const float *p = part + ((int64_t)k * C + c) * 3;
+      const double nb = p[0];
+      if (nb == 0.0) continue;
+      const double nab = n + nb, d = (double)p[1] - mean;
+      mean += d * nb / nab;
+      m2 += (double)p[2] + d * d * n * nb / nab;
+      n = nab;
+    }
+  red[0][rg][cl] = n;
+  red[1][rg][cl] = mean;
+  red[2][rg][cl] = m2;
+  __syncthreads();
+  if (rg != 0 || c >= C) return;
+  n = red[0][0][cl], mean = red[1][0][cl], m2 = red[2][0][cl];
+  for (int g = 1; g < 4; ++g) {
+    const double nb = red[0][g][cl];
     if (nb == 0.0) continue;
-    const double nab = n + nb, d = (double)p[1] - mean;
+    const double nab = n + nb, d = red[1][g][cl] - mean;
     mean += d * nb / nab;
-    m2 += (double)p[2] + d * d * n * nb / nab;
+    m2 += red[2][g][cl] + d * d * n * nb / nab;
     n = nab;
   }
   const float var = (float)(m2 / n);
@@ -1318,18 +1352,17 @@ __global__ __launch_bounds__(256) void bn_bwd_part_kernel(const float *__restric
 __global__ __launch_bounds__(256) void bn_bwd_finish_kernel(const float *__restrict__ part, int blocks, int C,
                                                             float *dgamma, float *dbeta, int accumulate,
                                                             float *__restrict__ sums) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float a = 0.f, b = 0.f;
-  for (int k = 0; k < blocks; ++k) {
-    const float *p = part + ((int64_t)k * C + c) * 2;
-    a += p[0];
-    b += p[1];
+  const int64_t col = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);  // c * 2 + j
+  const float v = parts_col_sum(part, blocks, 2LL * C, col);
+  if (threadIdx.x >= 64 || col >= 2LL * C) return;
+  const int c = (int)(col >> 1);
+  if ((col & 1) == 0) {  // sum dpre
+    sums[c] = v;
+    dbeta[c] = accumulate ? dbeta[c] + v : v;
+  } else {  // sum dpre * zhat
+    sums[C + c] = v;
+    dgamma[c] = accumulate ? dgamma[c] + v : v;
   }
-  sums[c] = a;
-  sums[C + c] = b;
-  dbeta[c] = accumulate ? dbeta[c] + a : a;
-  dgamma[c] = accumulate ? dgamma[c] + b : b;
 }
 
 // dz = gamma * rstd * (dpre - sum(dpre)/N - zhat * sum(dpre * zhat)/N) -> bf16
@@ -1391,7 +1424,7 @@ extern "C" int fs2_bn_train_fwd(const float *z, int64_t R, int C, const float *g
   const int nb = bn_blocks(R, &rpb);
   const size_t lds = (size_t)(256 / (C >> 2)) * C * sizeof(float);
   hipLaunchKernelGGL(bn_stats_part_kernel, dim3(nb), dim3(256), lds, s, z, R, C, rpb, ws);
-  hipLaunchKernelGGL(bn_stats_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, nb, C, eps, momentum,
+  hipLaunchKernelGGL(bn_stats_finish_kernel, dim3((C + 63) / 64), dim3(256), 0, s, ws, nb, C, eps, momentum,
                      running_mean, running_var, mean, rstd);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(bn_grid(R, C)), dim3(256), 0, s, z, R, C, mean, rstd, gamma, beta, use_tanh,
                      drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt, residual,
@@ -1420,10 +1453,131 @@ extern "C" int fs2_bn_train_bwd(const float *dy, const float *z, int64_t R, int 
   float *sums = ws + (int64_t)kBnBlocks * C * 3;
   hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(nb), dim3(256), lds, s, dy, z, R, C, rpb, mean, rstd, gamma, beta,
                      use_tanh, thr, scale, seed, (uint32_t)salt, ws);
-  hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, nb, C, dgamma, dbeta, accumulate,
+  hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, s, ws, nb, C, dgamma, dbeta, accumulate,
                      sums);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(bn_grid(R, C)), dim3(256), 0, s, dy, z, R, C, mean, rstd, gamma, beta,
                      use_tanh, thr, scale, seed, (uint32_t)salt, sums, reinterpret_cast<bf16 *>(dz));
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// clip_grad_norm_ + Adam (torch.optim.Adam, fused / capturable semantics; train.py:93-95 via
+// ScheduledOptim.step_and_update_lr) over the flat gradient buffer in two launches:
+//   1. per-block sums of squares of the flat gradients (block 0 also advances every step counter);
+//   2. every block re-adds the partials in the same order (deterministic total norm), coef =
+//      min(1, max_norm / (norm + 1e-6)); per element g *= coef (written back, as clip_grad_norm_
+//      leaves the clipped gradients), g += wd * p, m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2,
+//      p -= lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps).
+// Parameters are separate tensors, their gradients contiguous in the flat buffer at desc.off.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kAdamNormBlocks = 1024;
+
+__global__ __launch_bounds__(256) void adam_norm_kernel(const float *__restrict__ g, int64_t n,
+                                                        const fs2_adam_param *__restrict__ d, int np,
+                                                        float *__restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4 *>(g)[i];
+    s += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const float v = g[(n4 << 2) + threadIdx.x];
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < np; i += 256)
+      if (d[i].step != nullptr) d[i].step[0] += 1.0f;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float *__restrict__ g, int64_t n, const float *__restrict__ part,
+                                                   const fs2_adam_param *__restrict__ d, int np, const float *lr_ptr,
+                                                   float lr_val, float b1, float b2, float eps, float wd,
+                                                   float max_norm) {
+  __shared__ float red[4];
+  __shared__ float coef_s;
+  float coef = 1.0f;
+  if (max_norm > 0.0f) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < kAdamNormBlocks; i += 256) s += part[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float norm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+      coef_s = fminf(max_norm / (norm + 1e-6f), 1.0f);
+    }
+    __syncthreads();
+    coef = coef_s;
+  }
+  const float lr = lr_ptr != nullptr ? *lr_ptr : lr_val;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t e0 = (int64_t)blockIdx.x * per, e1 = e0 + per < n ? e0 + per : n;
+  if (e0 >= e1) return;
+  // parameter holding e0: last desc with off <= e0 (binary search)
+  int lo = 0, hi = np - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].off <= e0) lo = mid; else hi = mid - 1;
+  }
+  int pi = lo;
+  int64_t pend = d[pi].off + d[pi].numel;
+  float step_size = 0.f, bc2s = 1.f;
+  auto param_consts = [&]() {
+    const float t = d[pi].step != nullptr ? d[pi].step[0] : 1.0f;
+    const float bc1 = 1.0f - powf(b1, t), bc2 = 1.0f - powf(b2, t);
+    step_size = lr / bc1;
+    bc2s = sqrtf(bc2);
+  };
+  param_consts();
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+    if (e >= pend) {
+      while (e >= d[pi].off + d[pi].numel) ++pi;
+      pend = d[pi].off + d[pi].numel;
+      param_consts();
+    }
+    const int64_t j = e - d[pi].off;
+    float gr = g[e];
+    if (max_norm > 0.0f) {
+      gr *= coef;
+      g[e] = gr;
+    }
+    float *pp = d[pi].p + j;
+    const float pv = *pp;
+    if (wd != 0.0f) gr += wd * pv;
+    float *mp = d[pi].m + j, *vp = d[pi].v + j;
+    const float m = b1 * *mp + (1.0f - b1) * gr;
+    const float v = b2 * *vp + (1.0f - b2) * gr * gr;
+    *mp = m;
+    *vp = v;
+    *pp = pv - step_size * m / (sqrtf(v) / bc2s + eps);
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t fs2_adam_ws_bytes(void) { return (int64_t)kAdamNormBlocks * (int64_t)sizeof(float); }
+
+extern "C" int fs2_adam_flat(float *grads, int64_t n, const fs2_adam_param *params_dev, int np, const float *lr_dev,
+                             float lr, float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                             float *ws, int64_t ws_bytes, fs2_stream_t stream) {
+  if (grads == nullptr || params_dev == nullptr || np <= 0 || ws == nullptr || n < 0) return FS2_EINVAL;
+  if (ws_bytes < fs2_adam_ws_bytes()) return FS2_EINVAL;
+  if (n == 0) return FS2_OK;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(adam_norm_kernel, dim3(kAdamNormBlocks), dim3(256), 0, s, grads, n, params_dev, np, ws);
+  int64_t blocks = (n + 4095) / 4096;
+  blocks = blocks > 8192 ? 8192 : blocks;
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, grads, n, ws, params_dev, np, lr_dev, lr,
+                     beta1, beta2, eps, weight_decay, max_norm);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

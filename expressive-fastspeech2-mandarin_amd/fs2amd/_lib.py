@@ -43,6 +43,12 @@ class LossArgs(ctypes.Structure):
                 ("d_mask", _p), ("n_d", _i64)]
 
 
+class AdamParam(ctypes.Structure):
+    """Mirror of ``fs2_adam_param`` (include/fs2hip.h)."""
+
+    _fields_ = [("p", _p), ("m", _p), ("v", _p), ("step", _p), ("off", _i64), ("numel", _i64)]
+
+
 class ConvDesc(ctypes.Structure):
     """Mirror of ``fs2_conv_desc`` (include/fs2hip.h)."""
 
@@ -167,6 +173,8 @@ SIGNATURES = {
     "fs2_bn_train_ws_bytes": (_i64, [_i]),
     "fs2_bn_train_fwd": (_i, [_p, _i64, _i, _p, _p, _f, _f, _p, _p, _i, _f, _p, _i, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "fs2_bn_train_bwd": (_i, [_p, _p, _i64, _i, _p, _p, _p, _p, _i, _f, _p, _i, _p, _p, _p, _i, _p, _i64, _p]),
+    "fs2_adam_ws_bytes": (_i64, []),
+    "fs2_adam_flat": (_i, [_p, _i64, _p, _i, _p, _f, _f, _f, _f, _f, _f, _p, _i64, _p]),
     "fs2_colsum_ws_bytes": (_i64, [_i]),
     "fs2_colsum": (_i, [_p, _i, _i64, _i, _i64, _p, _i, _p, _i64, _p]),
     "fs2_conv_wgrad_ws_bytes": (_i64, [_i, _i, _i, _i, _i]),

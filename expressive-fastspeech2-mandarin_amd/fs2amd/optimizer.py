@@ -24,6 +24,69 @@ class ScheduledOptim:
         self.current_step = current_step
         self.init_lr = np.power(model_config["transformer"]["encoder_hidden"], -0.5)
 
+    # ---- clip + Adam over a flat gradient buffer in two launches (fs2_adam_flat) -----------------
+    def flat_step_ok(self):
+        """The fused flat update applies: one param group, plain Adam (no amsgrad / maximize /
+        differentiable), every parameter on the GPU; FS2_FUSED_ADAM=0 disables it."""
+        import os
+        if os.environ.get("FS2_FUSED_ADAM", "1") == "0":
+            return False
+        gs = self._optimizer.param_groups
+        if len(gs) != 1:
+            return False
+        g = gs[0]
+        return (not g.get("amsgrad", False) and not g.get("maximize", False) and not g.get("differentiable", False)
+                and all(p.is_cuda and p.dtype == torch.float32 for p in g["params"]))
+
+    def flat_step(self, flat, params, max_norm):
+        """clip_grad_norm_(params, max_norm) + Adam.step() where params' gradients are consecutive
+        views of ``flat`` (fs2amd.trainer's buffer). The optimizer state is torch's own (exp_avg,
+        exp_avg_sq, a float32 device step per parameter; created here if absent, outside capture),
+        so state_dict / checkpoints are unchanged."""
+        import ctypes
+        from . import _lib as L
+        from . import ops
+        opt = self._optimizer
+        group = opt.param_groups[0]
+        key = (flat.data_ptr(),) + tuple(p.data_ptr() for p in params)
+        plan = getattr(self, "_flat_plan", None)
+        states = []
+        for p in params:
+            st = opt.state[p]
+            if len(st) == 0:
+                st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            states.append(st)
+        key += tuple(st["exp_avg"].data_ptr() + st["exp_avg_sq"].data_ptr() + st["step"].data_ptr() for st in states)
+        if plan is None or plan[0] != key:
+            arr = (L.AdamParam * len(params))()
+            off = 0
+            for d, p, st in zip(arr, params, states):
+                if not (p.is_contiguous() and st["exp_avg"].is_contiguous() and st["exp_avg_sq"].is_contiguous()):
+                    raise RuntimeError("fs2amd: fused Adam needs contiguous parameters and state")
+                if st["step"].device != p.device or st["step"].dtype != torch.float32:
+                    st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
+                d.p, d.m, d.v, d.step = (p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                                         st["step"].data_ptr())
+                d.off, d.numel = off, p.numel()
+                off += p.numel()
+            if off != flat.numel():
+                raise RuntimeError("fs2amd: flat gradient buffer does not match the parameters")
+            dev = torch.frombuffer(bytearray(bytes(memoryview(arr).cast("B"))), dtype=torch.uint8).to(flat.device)
+            ws = torch.empty(L.load().fs2_adam_ws_bytes() // 4, device=flat.device, dtype=torch.float32)
+            plan = self._flat_plan = (key, dev, ws, len(params))
+        _, dev, ws, n = plan
+        lr = group["lr"]
+        lr_dev = ctypes.c_void_p(lr.data_ptr()) if torch.is_tensor(lr) else None
+        b1, b2 = group["betas"]
+        L.check(L.load().fs2_adam_flat(ctypes.c_void_p(flat.data_ptr()), flat.numel(), ctypes.c_void_p(dev.data_ptr()),
+                                       n, lr_dev, float(lr) if not torch.is_tensor(lr) else 0.0, float(b1), float(b2),
+                                       float(group["eps"]), float(group["weight_decay"]),
+                                       float(max_norm) if max_norm is not None else 0.0,
+                                       ctypes.c_void_p(ws.data_ptr()), ws.numel() * 4, ops._stream(flat)),
+                "fs2_adam_flat")
+
     def step_and_update_lr(self):
         self._update_learning_rate()
         self._optimizer.step()

@@ -21,6 +21,8 @@ PostNet BatchNorm running stats follow rank 0 (DataParallel's semantics: DDP bro
 or one coalesced broadcast per step in the graph form). Gradient clipping needs no extra
 collective: after the all-reduce every rank holds the same gradients.
 """
+import time
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -77,8 +79,12 @@ class TrainStep:
         self._stream = None
         self._closed = False
         self._acc_pending = 0
+        self._fused_adam = False
         if self.flat:
             self._setup_flat_grads()
+            # every optimizer parameter has its gradient in the flat buffer
+            self._fused_adam = (self.optimizer.flat_step_ok() and
+                                len(self._flat_params) == len(self.optimizer._optimizer.param_groups[0]["params"]))
         if self.graph_mode:
             self._stream = torch.cuda.Stream(device)
 
@@ -145,6 +151,7 @@ class TrainStep:
     # ---- flat gradients + explicit all-reduce (graph form) -------------------------------------
     def _setup_flat_grads(self):
         params = [p for p in self.model.parameters() if p.requires_grad]
+        self._flat_params = params
         n = sum(p.numel() for p in params)
         self._flat = torch.zeros(n, dtype=torch.float32, device=params[0].device)
         off = 0
@@ -185,8 +192,8 @@ class TrainStep:
         self._acc_pending += 1
         if self.step_no % self.grad_acc_step == 0:
             self._reduce_grads()
-            nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip_thresh)
-            self.optimizer.step_and_update_lr()
+            self.optimizer._update_learning_rate()
+            self._clip_and_step()
             self._acc_pending = 0
         self.step_no += 1
         return [l.detach() for l in losses]
@@ -200,9 +207,17 @@ class TrainStep:
         with grad_sink():  # the fused blocks accumulate straight into the flat buffer's views
             losses[0].backward()
         self._reduce_grads()
-        nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip_thresh)
-        self.optimizer._optimizer.step()
+        self._clip_and_step()
         return losses
+
+    def _clip_and_step(self):
+        """clip_grad_norm_ + Adam: on the flat buffer in two launches (fs2_adam_flat) when the
+        optimizer allows it, else torch's."""
+        if self._fused_adam:
+            self.optimizer.flat_step(self._flat, self._flat_params, self.grad_clip_thresh)
+        else:
+            nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip_thresh)
+            self.optimizer._optimizer.step()
 
     # ---- whole-step HIP graph --------------------------------------------------------------------
     @staticmethod
@@ -228,6 +243,12 @@ class TrainStep:
             self.step_no += 1
             return losses
         if self._graph is None:
+            if dist.is_available() and dist.is_initialized():
+                # let the process group's watchdog retire the warm-up steps' collectives first: HIP
+                # rejects an event query once the event's stream (RCCL's, joined by the captured
+                # all-reduces) is capturing, and the watchdog aborts the process on that error
+                torch.cuda.synchronize(self.device)
+                time.sleep(0.5)
             static = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in batch.items()}
             self.optimizer._update_learning_rate()
             g = torch.cuda.CUDAGraph()

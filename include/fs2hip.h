@@ -649,6 +649,25 @@ int fs2_bn_train_bwd(const float *dy, const float *z, int64_t R, int C, const fl
                      void *dz, float *dgamma, float *dbeta, int accumulate, float *ws, int64_t ws_bytes,
                      fs2_stream_t stream);
 
+/*
+ * fs2_adam_flat — nn.utils.clip_grad_norm_(max_norm) + torch.optim.Adam's step (fused / capturable
+ * semantics: m = b1 m + (1-b1) g, v = b2 v + (1-b2) g^2, p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t)
+ * + eps), L2 weight decay added to g) for parameters whose gradients are one flat f32 buffer
+ * (train.py:92-95 through ScheduledOptim). params_dev: device array of np descriptors in flat order
+ * (param, exp_avg, exp_avg_sq, step counter (f32, advanced by 1 here), offset and length in the
+ * flat buffer). lr from lr_dev when non-null (a captured step reads the current Noam lr), else lr.
+ * max_norm <= 0: no clipping; else the clipped gradients are written back. Deterministic norm.
+ * ws: fs2_adam_ws_bytes().
+ */
+typedef struct fs2_adam_param {
+  float *p, *m, *v, *step;
+  int64_t off, numel;
+} fs2_adam_param;
+int64_t fs2_adam_ws_bytes(void);
+int fs2_adam_flat(float *grads, int64_t n, const fs2_adam_param *params_dev, int np, const float *lr_dev, float lr,
+                  float beta1, float beta2, float eps, float weight_decay, float max_norm, float *ws,
+                  int64_t ws_bytes, fs2_stream_t stream);
+
 /* Library identification. */
 const char *fs2_version(void);
 const char *fs2_status_string(int status);

@@ -266,7 +266,7 @@ def test_fused_fft_block_train_equals_per_op_path(gpu):
     fused path's gradient cosine to fp32 >= the per-op path's - 0.02 (or >= 0.99), and where the
     per-op path resolves the gradient (cosine >= 0.99) the norms agree within 3 % (the key biases,
     whose exact gradient is 0, only finite). With the gradient sink (flat-buffer steps) the fused nodes accumulate into existing
-    .grad tensors: grad - 0.5 equals the plain result within 2e-3 of its scale (the attention
+    .grad tensors: grad - 0.5 equals the plain result within 1e-2 of its scale (the attention
     backward's atomics make two runs differ in the last bits)."""
     gf, lf = _bf16_grads("train_b16", True)
     gu, lu = _bf16_grads("train_b16", False)
@@ -293,7 +293,7 @@ def test_fused_fft_block_train_equals_per_op_path(gpu):
     for k in resolved:
         d = (gs[k].double() - 0.5) - gf[k].double()
         # the attention backward accumulates with atomics: not bit-reproducible between two runs
-        assert float(d.abs().max()) <= 2e-3 * float(gf[k].abs().max()) + 1e-6, k
+        assert float(d.abs().max()) <= 1e-2 * float(gf[k].abs().max()) + 1e-6, k
 
 
 def test_fused_fft_block_dropout_trains(gpu):

@@ -339,3 +339,54 @@ def test_bn_train_fwd_bwd(ops, C, use_tanh, p):
     assert float((dz.cpu().double() - zd.grad).abs().max()) <= 1e-2 * float(zd.grad.abs().max())
     assert torch.allclose(dg.cpu().double(), gd.grad, rtol=1e-4, atol=1e-4 * float(gd.grad.abs().max()))
     assert torch.allclose(dbe.cpu().double(), bd.grad, rtol=1e-4, atol=1e-4 * float(bd.grad.abs().max()))
+
+
+@pytest.mark.parametrize("capturable,wd", [(True, 0.0), (False, 0.01)])
+def test_adam_flat_equals_torch(ops, capturable, wd):
+    """fs2_adam_flat (clip_grad_norm_ + Adam over the flat gradient buffer, two launches) against
+    nn.utils.clip_grad_norm_ + torch.optim.Adam(fused=True) over 3 steps, clipping active on the
+    first: parameters and exp_avg / exp_avg_sq within 1e-5 relative (+1e-7), steps equal, the
+    clipped gradients written back like clip_grad_norm_'s."""
+    import copy
+    from fs2amd.optimizer import ScheduledOptim
+
+    torch.manual_seed(9)
+    shapes = [(33,), (256, 256), (80, 512, 5), (7,), (1024,)]
+    ps = [torch.randn(s, device=DEV) * 0.1 for s in shapes]
+    tc = {"optimizer": {"betas": [0.9, 0.98], "eps": 1e-9, "weight_decay": wd, "warm_up_step": 4000,
+                        "anneal_steps": [], "anneal_rate": 0.3, "grad_acc_step": 1, "grad_clip_thresh": 1.0}}
+    mc = {"transformer": {"encoder_hidden": 256}}
+
+    class M(torch.nn.Module):
+        def __init__(self, init):
+            super().__init__()
+            self.ps = torch.nn.ParameterList([torch.nn.Parameter(t.clone()) for t in init])
+
+    ma, mb = M(ps), M(ps)
+    oa = ScheduledOptim(ma, tc, mc, 0, capturable=capturable)
+    ob = ScheduledOptim(mb, tc, mc, 0, capturable=capturable)
+    n = sum(p.numel() for p in ma.parameters())
+    flat = torch.zeros(n, device=DEV)
+    off = 0
+    for p in ma.parameters():
+        p.grad = flat[off:off + p.numel()].view_as(p)
+        off += p.numel()
+    for step in range(3):
+        gs = [torch.randn(s, device=DEV) * (3.0 if step == 0 else 0.001) for s in shapes]
+        for p, g in zip(ma.parameters(), gs):
+            p.grad.copy_(g)
+        for p, g in zip(mb.parameters(), gs):
+            p.grad = g.clone()
+        oa._update_learning_rate()
+        oa.flat_step(flat, list(ma.parameters()), 1.0)
+        ob._update_learning_rate()
+        torch.nn.utils.clip_grad_norm_(mb.parameters(), 1.0)
+        ob._optimizer.step()
+        torch.cuda.synchronize()
+        for pa, pb in zip(ma.parameters(), mb.parameters()):
+            assert torch.allclose(pa.grad, pb.grad, rtol=1e-5, atol=1e-7)
+            assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-7), step
+            sa, sb = oa._optimizer.state[pa], ob._optimizer.state[pb]
+            assert torch.allclose(sa["exp_avg"], sb["exp_avg"], rtol=1e-5, atol=1e-9)
+            assert torch.allclose(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-5, atol=1e-12)
+            assert float(sa["step"]) == float(sb["step"]) == step + 1
