@@ -97,11 +97,11 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
   const int r16 = lane & 15, g = lane >> 4;
 
   // buffer row R holds sample t0 + R: inside the utterance?
-  auto inside = [&](int R) { return (unsigned)(t0 + R) < (unsigned)T; };
+  auto inside = [&](int R) __attribute__((always_inline)) { return (unsigned)(t0 + R) < (unsigned)T; };
 
   // ---- DMA of the chain input: CUR <- x, ACT <- lrelu(x) (rows outside [0, T): zeros)
   const rsrc_t xr = make_rsrc(p.x, p.x_bytes), ar = make_rsrc(p.a0, p.x_bytes);
-  auto load_input = [&]() {
+  auto load_input = [&]() __attribute__((always_inline)) {
     constexpr int RPP = 1024 / RB;  // rows per 1 KiB piece
     constexpr int NP = BUF / 1024;
 #pragma unroll
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
       }
     }
   };
-  auto sync = []() {
+  auto sync = []() __attribute__((always_inline)) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
     __builtin_amdgcn_sched_barrier(0);
@@ -126,7 +126,9 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
     __builtin_amdgcn_sched_barrier(0);
   };
   // LDS byte address of (row R, 8-channel group q)
-  auto addr = [&](int buf, int R, int q) { return buf + R * RB + ((q ^ mrf_swz<C>(R)) << 4); };
+  auto addr = [&](int buf, int R, int q) __attribute__((always_inline)) {
+    return buf + R * RB + ((q ^ mrf_swz<C>(R)) << 4);
+  };
 
   f32x4 xs[4][NCB];  // the chains' sum over output rows [64, 320): blocks 4 + w + 4i
 #pragma unroll
@@ -136,8 +138,9 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
 
   // one conv step: output blocks [blo, bhi), kernel K (taps), dilation D, input buffer IN;
   // kind 0: T = lrelu(acc + b) ; 1: CUR = acc + b + CUR, ACT = lrelu(CUR) ; 2: xs += acc + b + CUR
-  auto step = [&](auto KC_, auto KIND_, int K, int D, int IN, const bf16 *wc, const float *bc, int blo, int bhi) {
-    constexpr int kind = decltype(KIND_)::value;
+  // (every lambda is force-inlined: an out-of-line call kept acc / xs on the scratch stack)
+  auto step = [&](int kind, int K, int D, int IN, const bf16 *wc, const float *bc, int blo,
+                  int bhi) __attribute__((always_inline)) {
     const int hk = (K - 1) / 2;
     const rsrc_t wr = make_rsrc(wc, (uint32_t)(K * C * C * 2));
     f32x4 acc[kMrfNBW][NCB];
@@ -148,14 +151,14 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
     const int first = blo + ((w - blo) % 4 + 4) % 4;  // this wave's first block (b = w mod 4)
     const int nks = K * KC;
     bf16x8 wa[2][NCB];
-    auto wload = [&](int s, bf16x8 (&f)[NCB]) {
+    auto wload = [&](int s, bf16x8 (&f)[NCB]) __attribute__((always_inline)) {
 #pragma unroll
       for (int c = 0; c < NCB; ++c)
         f[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                               wr, (uint32_t)lane * 16u, (uint32_t)((s * NCB + c) * 1024), 0));
     };
     // k-step s with its weights in wc (loaded one step ahead into wn)
-    auto kstep = [&](int s, const bf16x8 (&wc)[NCB], bf16x8 (&wn)[NCB]) {
+    auto kstep = [&](int s, const bf16x8 (&wc)[NCB], bf16x8 (&wn)[NCB]) __attribute__((always_inline)) {
       if (s + 1 < nks) {
         wload(s + 1, wn);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCB) : "memory");  // this k-step's weights (the next may fly)
@@ -203,7 +206,7 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
           v[2] += bb.z;
           v[3] += bb.w;
           const int o = R * RB + (((ch >> 3) ^ mrf_swz<C>(R)) << 4) + (ch & 7) * 2;
-          if constexpr (kind == 0) {
+          if (kind == 0) {
             bf16x4 t;
 #pragma unroll
             for (int q = 0; q < 4; ++q) t[q] = (bf16)(in ? lrelu(v[q], 0.1f) : 0.f);
@@ -212,7 +215,7 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
             const bf16x4 xo = *reinterpret_cast<const bf16x4 *>(smem + CUR_OFF + o);
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] += (float)xo[q];
-            if constexpr (kind == 1) {
+            if (kind == 1) {
               bf16x4 nc, na;
 #pragma unroll
               for (int q = 0; q < 4; ++q) {
@@ -232,28 +235,29 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
     __builtin_amdgcn_s_barrier();  // the step's output visible
   };
 
-  const int ks[3] = {3, 7, 11};
-  mrf_static_for<3>([&](auto J) {
-    constexpr int j = decltype(J)::value;
-    const int K = ks[j], hk = (K - 1) / 2;
+  // runtime loops over the 3 chains x 3 dilation pairs x 2 convs: ONE inlined copy of the step code
+  // (18 unrolled copies overflowed the instruction cache)
+#pragma nounroll
+  for (int j = 0; j < 3; ++j) {
+    const int K = 3 + 4 * j, hk = (K - 1) / 2;
     load_input();
     sync();
-    const int dil[3] = {1, 3, 5};
-    // rows each step must produce: [64 - e, 320 + e) with e = 11hk, 10hk, 7hk, 6hk, hk, 0
-    const int e1[3] = {11 * hk, 7 * hk, hk}, e2[3] = {10 * hk, 6 * hk, 0};
-    mrf_static_for<3>([&](auto P) {
-      constexpr int pp = decltype(P)::value;
-      const bf16 *w1 = p.w + mrf_woff<C>(j, pp, 0), *w2 = p.w + mrf_woff<C>(j, pp, 1);
-      const float *b1 = p.bias + (j * 6 + 2 * pp) * C, *b2 = p.bias + (j * 6 + 2 * pp + 1) * C;
-      const int lo1 = (kMrfH - e1[pp]) / 16, hi1 = (kMrfH + kMrfL + e1[pp] + 15) / 16;
-      step(std::integral_constant<int, KC>{}, std::integral_constant<int, 0>{}, K, dil[pp], ACT_OFF, w1, b1, lo1, hi1);
-      const int lo2 = (kMrfH - e2[pp]) / 16, hi2 = (kMrfH + kMrfL + e2[pp] + 15) / 16;
-      if constexpr (pp < 2)
-        step(std::integral_constant<int, KC>{}, std::integral_constant<int, 1>{}, K, 1, T_OFF, w2, b2, lo2, hi2);
-      else
-        step(std::integral_constant<int, KC>{}, std::integral_constant<int, 2>{}, K, 1, T_OFF, w2, b2, lo2, hi2);
-    });
-  });
+#pragma nounroll
+    for (int pp = 0; pp < 3; ++pp) {
+      // rows each step must produce: [64 - e, 320 + e) with e = 11hk, 10hk, 7hk, 6hk, hk, 0
+      const int e1 = pp == 0 ? 11 * hk : (pp == 1 ? 7 * hk : hk);
+      const int e2 = pp == 0 ? 10 * hk : (pp == 1 ? 6 * hk : 0);
+      const int dil = 1 + 2 * pp;
+#pragma nounroll
+      for (int half = 0; half < 2; ++half) {
+        const int e = half == 0 ? e1 : e2;
+        const int lo = (kMrfH - e) / 16, hi = (kMrfH + kMrfL + e + 15) / 16;
+        const int kind = half == 0 ? 0 : (pp < 2 ? 1 : 2);
+        step(kind, K, half == 0 ? dil : 1, half == 0 ? ACT_OFF : T_OFF, p.w + mrf_woff<C>(j, pp, half),
+             p.bias + (j * 6 + 2 * pp + half) * C, lo, hi);
+      }
+    }
+  }
 
   // ---- out = lrelu(xs / 3, slope) over the tile's 256 samples (blocks 4..19, 4 per wave)
 #pragma unroll
