@@ -794,9 +794,11 @@ void wgrad_launch(const WgArgs &a, bool dy_f32, int tiles, hipStream_t s) {
 }
 
 int wgrad_splits(int tiles, int Q) {
-  int S = (512 + tiles - 1) / tiles;
+  // enough workgroups to fill the chip, few enough splits that the partials stay small (each
+  // split adds a full f32 copy of dW to write and re-read)
+  int S = (256 + tiles - 1) / tiles;
   if (S > Q) S = Q;
-  if (S > 32) S = 32;
+  if (S > 8) S = 8;
   return S < 1 ? 1 : S;
 }
 
@@ -903,7 +905,7 @@ __global__ __launch_bounds__(256) void pack_train_kernel(const fs2_pack_desc *__
       const float *s = d.src + ((int64_t)n * d.C + c) * KS;
       for (int k = 0; k < KS; ++k) {
         const float v = s[k];
-        if (d.fwd != nullptr) reinterpret_cast<bf16 *>(d.fwd)[((int64_t)(d.n_off + n) * KS + k) * d.C + c] = (bf16)v;
+        if (d.fwd != nullptr) reinterpret_cast<bf16 *>(d.fwd)[((int64_t)(d.n_off + n) * KS + k) * d.C_tot + c] = (bf16)v;
         t[k][nl][cl] = v;
       }
     }
@@ -935,7 +937,9 @@ extern "C" int fs2_pack_train_plan(fs2_pack_desc *descs, int nd, int *blocks) {
       blk += (d.N + 255) / 256;
       continue;
     }
-    if (d.N <= 0 || d.C <= 0 || d.KS < 1 || d.KS > 9 || d.n_off < 0 || d.n_off + d.N > d.N_tot) return FS2_EINVAL;
+    if (d.C_tot == 0) d.C_tot = d.C;
+    if (d.N <= 0 || d.C <= 0 || d.KS < 1 || d.KS > 9 || d.n_off < 0 || d.n_off + d.N > d.N_tot || d.C_tot < d.C)
+      return FS2_EINVAL;
     d.tiles_c = (d.C + 31) / 32;
     d.blk0 = blk;
     blk += ((d.N + 31) / 32) * d.tiles_c;
@@ -1164,89 +1168,60 @@ __device__ __forceinline__ void bn_row_reduce(float *red, const BnGeom &g, int C
       for (int q = 0; q < 4; ++q) v[q] += red[r * C + g.cg * 4 + q];
 }
 
-// part[blk][c] = (n, mean, M2) of the block's rows
+// part[blk][c][2] = (sum (z - K_c), sum (z - K_c)^2) over the block's rows, K_c = z[0][c]: shifted
+// sums (no E[z^2] - E[z]^2 cancellation for |mean| >> std), added in a fixed order by the finish
 __global__ __launch_bounds__(256) void bn_stats_part_kernel(const float *__restrict__ z, int64_t R, int C, int rpb,
                                                             float *__restrict__ part) {
   extern __shared__ float red[];
   const BnGeom g = bn_geom(C);
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = r0 + rpb < R ? r0 + rpb : R;
-  const float n = (float)(r1 > r0 ? r1 - r0 : 0);
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  if (g.active)
-    for (int64_t r = r0 + g.rsub; r < r1; r += g.RPI) {
-      float v[4];
-      load4(z + r * C + g.cg * 4, v);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) s[q] += v[q];
-    }
-  bn_row_reduce(red, g, C, s);
-  __shared__ float mean_s[1024];
-  if (g.active && g.rsub == 0)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) mean_s[g.cg * 4 + q] = n > 0.f ? s[q] / n : 0.f;
-  __syncthreads();
-  float m[4], m2[4] = {0.f, 0.f, 0.f, 0.f};
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
   if (g.active) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) m[q] = mean_s[g.cg * 4 + q];
+    float K[4];
+    load4(z + g.cg * 4, K);
     for (int64_t r = r0 + g.rsub; r < r1; r += g.RPI) {
       float v[4];
       load4(z + r * C + g.cg * 4, v);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) m2[q] += (v[q] - m[q]) * (v[q] - m[q]);
+      for (int q = 0; q < 4; ++q) {
+        const float d = v[q] - K[q];
+        s1[q] += d;
+        s2[q] += d * d;
+      }
     }
   }
-  bn_row_reduce(red, g, C, m2);
+  bn_row_reduce(red, g, C, s1);
+  bn_row_reduce(red, g, C, s2);
   if (g.active && g.rsub == 0)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float *p = part + ((int64_t)blockIdx.x * C + g.cg * 4 + q) * 3;
-      p[0] = n;
-      p[1] = m[q];
-      p[2] = m2[q];
+      float *p = part + ((int64_t)blockIdx.x * C + g.cg * 4 + q) * 2;
+      p[0] = s1[q];
+      p[1] = s2[q];
     }
 }
 
-__global__ __launch_bounds__(256) void bn_stats_finish_kernel(const float *__restrict__ part, int blocks, int C,
+__global__ __launch_bounds__(256) void bn_stats_finish_kernel(const float *__restrict__ z, int64_t R,
+                                                              const float *__restrict__ part, int blocks, int C,
                                                               float eps, float momentum, float *running_mean,
                                                               float *running_var, float *__restrict__ mean_out,
                                                               float *__restrict__ rstd_out) {
-  // Chan's combination: row group g combines partial blocks g, g+4, ... in order, then the four
-  // group results are combined in order (deterministic)
-  __shared__ double red[3][4][64];
-  const int rg = threadIdx.x >> 6, cl = threadIdx.x & 63;
-  const int c = blockIdx.x * 64 + cl;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  if (c < C)
-    for (int k = rg; k < blocks; k += 4) {
-      const float *p = part + ((int64_t)k * C + c) * 3;
-      const double nb = p[0];
-      if (nb == 0.0) continue;
-      const double nab = n + nb, d = (double)p[1] - mean;
-      mean += d * nb / nab;
-      m2 += (double)p[2] + d * d * n * nb / nab;
-      n = nab;
-    }
-  red[0][rg][cl] = n;
-  red[1][rg][cl] = mean;
-  red[2][rg][cl] = m2;
+  __shared__ float sv[2][64];
+  const int64_t col = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);  // c * 2 + j
+  const float v = parts_col_sum(part, blocks, 2LL * C, col);
+  if (threadIdx.x < 64) sv[col & 1][threadIdx.x >> 1] = v;  // (sum, sum of squares) of channel col / 2
   __syncthreads();
-  if (rg != 0 || c >= C) return;
-  n = red[0][0][cl], mean = red[1][0][cl], m2 = red[2][0][cl];
-  for (int g = 1; g < 4; ++g) {
-    const double nb = red[0][g][cl];
-    if (nb == 0.0) continue;
-    const double nab = n + nb, d = red[1][g][cl] - mean;
-    mean += d * nb / nab;
-    m2 += red[2][g][cl] + d * d * n * nb / nab;
-    n = nab;
-  }
-  const float var = (float)(m2 / n);
-  mean_out[c] = (float)mean;
-  rstd_out[c] = rsqrtf(var + eps);
+  if (threadIdx.x >= 32) return;
+  const int c = blockIdx.x * 32 + threadIdx.x;
+  if (c >= C) return;
+  const double n = (double)R, m1 = (double)sv[0][threadIdx.x] / n;
+  const double var = fmax((double)sv[1][threadIdx.x] / n - m1 * m1, 0.0);
+  const float mean = z[c] + (float)m1;
+  mean_out[c] = mean;
+  rstd_out[c] = rsqrtf((float)var + eps);
   if (running_mean != nullptr) {
-    running_mean[c] = (1.0f - momentum) * running_mean[c] + momentum * (float)mean;
-    running_var[c] = (1.0f - momentum) * running_var[c] + momentum * (float)(m2 / (n > 1.0 ? n - 1.0 : 1.0));
+    running_mean[c] = (1.0f - momentum) * running_mean[c] + momentum * mean;
+    running_var[c] = (1.0f - momentum) * running_var[c] + momentum * (float)(var * n / (n > 1.0 ? n - 1.0 : 1.0));
   }
 }
 
@@ -1424,7 +1399,7 @@ extern "C" int fs2_bn_train_fwd(const float *z, int64_t R, int C, const float *g
   const int nb = bn_blocks(R, &rpb);
   const size_t lds = (size_t)(256 / (C >> 2)) * C * sizeof(float);
   hipLaunchKernelGGL(bn_stats_part_kernel, dim3(nb), dim3(256), lds, s, z, R, C, rpb, ws);
-  hipLaunchKernelGGL(bn_stats_finish_kernel, dim3((C + 63) / 64), dim3(256), 0, s, ws, nb, C, eps, momentum,
+  hipLaunchKernelGGL(bn_stats_finish_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, s, z, R, ws, nb, C, eps, momentum,
                      running_mean, running_var, mean, rstd);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(bn_grid(R, C)), dim3(256), 0, s, z, R, C, mean, rstd, gamma, beta, use_tanh,
                      drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt, residual,

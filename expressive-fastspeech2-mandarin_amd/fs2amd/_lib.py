@@ -31,7 +31,7 @@ class PackDesc(ctypes.Structure):
     """Mirror of ``fs2_pack_desc`` (include/fs2hip.h)."""
 
     _fields_ = [("src", _p), ("fwd", _p), ("tr", _p), ("N", _i), ("C", _i), ("KS", _i), ("n_off", _i),
-                ("N_tot", _i), ("f32_copy", _i), ("tiles_c", _i), ("blk0", _i)]
+                ("N_tot", _i), ("f32_copy", _i), ("C_tot", _i), ("tiles_c", _i), ("blk0", _i)]
 
 
 class LossArgs(ctypes.Structure):

@@ -83,8 +83,12 @@ class TrainStep:
         if self.flat:
             self._setup_flat_grads()
             # every optimizer parameter has its gradient in the flat buffer
+            # (frozen parameters, e.g. the position-encoding tables, never get a gradient: torch's Adam
+            # skips them, and so does the flat update)
+            inflat = {id(p) for p in self._flat_params}
             self._fused_adam = (self.optimizer.flat_step_ok() and
-                                len(self._flat_params) == len(self.optimizer._optimizer.param_groups[0]["params"]))
+                                all(id(p) in inflat or not p.requires_grad
+                                    for p in self.optimizer._optimizer.param_groups[0]["params"]))
         if self.graph_mode:
             self._stream = torch.cuda.Stream(device)
 

@@ -169,6 +169,7 @@ def fft_block(blk, x, mask, lens, p_drop, training, compute):
 
 # ---- the FFT block as one autograd node on the training kernels (train.hip) -------------------------
 _SINK = [False]
+_PACKED = [{}]  # conv module -> (forward image, input-gradient image) refreshed by this step's pack launch
 
 
 class grad_sink:
@@ -215,9 +216,9 @@ class _TrainPack:
     bias concatenated) in persistent buffers, refreshed by ONE fs2_pack_train launch per forward
     (captured with the step). Built outside graph capture; rebuilt if a parameter moved."""
 
-    def __init__(self, blocks, dev):
+    def __init__(self, blocks, dev, extra_convs=()):
         from . import _lib as LL
-        self.key = _pack_key(blocks)
+        self.key = _pack_key(blocks, extra_convs)
         bf = dict(dtype=torch.bfloat16, device=dev)
         descs, self.per_block = [], []
 
@@ -229,6 +230,19 @@ class _TrainPack:
             d.N, d.C, d.KS, d.n_off, d.N_tot, d.f32_copy = N, C, KS, n_off, N_tot or N, f32
             descs.append(d)
 
+        def conv_images(w):
+            """forward [N][KS][cin_pad(C)] + input-gradient [C][KS][cin_pad(N)] images of a conv,
+            zero-initialised (the padding channels stay zero)."""
+            N, C, KS = w.shape
+            cp, npd = ops.cin_pad(C, L.FS2_BF16), ops.cin_pad(N, L.FS2_BF16)
+            fw, tr = torch.zeros(N, KS, cp, **bf), torch.zeros(C, KS, npd, **bf)
+            add(w, fw, tr, N, C, KS, 0, npd)
+            descs[-1].C_tot = cp
+            return fw, tr
+
+        self.extra = {}
+        for conv in extra_convs:
+            self.extra[conv] = conv_images(conv.weight)
         for blk in blocks:
             a, f = blk.slf_attn, blk.pos_ffn
             k1, k2, F_ = f.w_1.kernel_size[0], f.w_2.kernel_size[0], f.w_1.out_channels
@@ -259,19 +273,32 @@ class _TrainPack:
                                          ops._stream(stream_of)), "fs2_pack_train")
 
 
-def _pack_key(blocks):
-    return tuple(p.data_ptr() for b in blocks for p in _block_params(b))
+def _pack_key(blocks, extra_convs=()):
+    return tuple(p.data_ptr() for b in blocks for p in _block_params(b)) + tuple(c.weight.data_ptr()
+                                                                                 for c in extra_convs)
 
 
-def _train_pack(model, blocks, dev):
+def _train_pack(model, blocks, dev, extra_convs=()):
     """The model's _TrainPack (None while capturing before one exists: per-block packing then)."""
     tp = getattr(model, "_fs2_train_pack", None)
-    if tp is not None and tp.key == _pack_key(blocks):
+    if tp is not None and tp.key == _pack_key(blocks, extra_convs):
         return tp
     if torch.cuda.is_current_stream_capturing():
         return None
-    tp = model._fs2_train_pack = _TrainPack(blocks, dev)
+    tp = model._fs2_train_pack = _TrainPack(blocks, dev, extra_convs)
     return tp
+
+
+def _extra_convs(model, compute):
+    """VariancePredictor and PostNet convs whose images join the step's pack launch."""
+    convs = []
+    va = model.variance_adaptor
+    for vp in (va.duration_predictor, va.pitch_predictor, va.energy_predictor):
+        if _vp_fused_ok(vp, compute):
+            convs += [vp.conv_layer.conv1d_1.conv, vp.conv_layer.conv1d_2.conv]
+    if _postnet_fused_ok(model.postnet, compute):
+        convs += [seq[0].conv for seq in model.postnet.convolutions]
+    return convs
 
 
 class FFTBlockFn(torch.autograd.Function):
@@ -356,7 +383,7 @@ class FFTBlockFn(torch.autograd.Function):
             dbs = [torch.empty_like(b) for b in (bq, bk, bv)]
             ops.conv_wgrad(dqkv, xb, 1, 0, parts=(dws, dbs))
             gq = [dws[0], dbs[0], dws[1], dbs[1], dws[2], dbs[2]]
-        dx = ops.conv1d(dqkv.to(torch.bfloat16), wqkvT, None, cin=3 * H * dk, ks=1, pad=0, compute=BF,
+        dx = ops.conv1d(dqkv, wqkvT, None, cin=3 * H * dk, ks=1, pad=0, compute=BF,
                         epilogue=L.EPI_BIAS_RES, out_dtype=L.FS2_F32, residual=dres1)
         if sink:
             grads = gq + [None] * 10
@@ -420,8 +447,10 @@ class PostNetFn(torch.autograd.Function):
             w, b, g, be = params[4 * i:4 * i + 4]
             N, Cin, KS = w.shape
             pad = (KS - 1) // 2
-            z = ops.conv1d(x_bf, ops.pack_conv_weight(w, BF), b.detach(), cin=Cin, ks=KS, pad=pad, compute=BF,
-                           epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+            imgs = _PACKED[0].get(seq[0].conv)
+            wf, wT = imgs if imgs is not None else (ops.pack_conv_weight(w, BF), _packT_any(w))
+            z = ops.conv1d(x_bf, wf, b.detach(), cin=Cin, ks=KS, pad=pad, compute=BF, epilogue=L.EPI_BIAS,
+                           out_dtype=L.FS2_F32)
             last = i == n - 1
             yb, yf, mean, rstd = ops.bn_train_fwd(z, g.detach(), be.detach(), bn.eps, bn.momentum, bn.running_mean,
                                                   bn.running_var, use_tanh=not last, p_drop=p_drop, seed=seed,
@@ -429,7 +458,7 @@ class PostNetFn(torch.autograd.Function):
                                                   want_bf16=not last, want_f32=last)
             if bn.num_batches_tracked is not None:
                 bn.num_batches_tracked.add_(1)
-            saved.append((x_bf, z, mean, rstd, _packT_any(w), pad, KS))
+            saved.append((x_bf, z, mean, rstd, wT, pad, KS))
             x_bf, out = yb, yf
         ctx.saved = saved
         ctx.meta = (p_drop, seed, salt)
@@ -513,19 +542,20 @@ class VPLayerFn(torch.autograd.Function):
         N, Cin, KS = w.shape
         BF = L.FS2_BF16
         xb = x_bf if x_bf is not None else x.to(torch.bfloat16)
-        a = ops.conv1d(xb, ops.pack_conv_weight(w, BF), b.detach(), cin=Cin, ks=KS, pad=pad, compute=BF,
-                       epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+        wf, wT = meta[5] if len(meta) > 5 and meta[5] is not None else (ops.pack_conv_weight(w, BF), _packT_any(w))
+        a = ops.conv1d(xb, wf, b.detach(), cin=Cin, ks=KS, pad=pad, compute=BF, epilogue=L.EPI_BIAS,
+                       out_dtype=L.FS2_F32)
         y, yb, xh, rs = ops.relu_ln_fwd(a, g.detach(), be.detach(), eps, p_drop, seed, salt)
         ctx.save_for_backward(xb, a, xh, rs, w, b, g, be)
         ctx.meta = meta
-        ctx.wT = _packT(w)
+        ctx.wT = wT
         ctx.mark_non_differentiable(yb)
         return y, yb
 
     @staticmethod
     def backward(ctx, dy, _dyb):
         xb, a, xh, rs, w, b, g, be = ctx.saved_tensors
-        pad, p_drop, seed, salt, eps = ctx.meta
+        pad, p_drop, seed, salt, eps = ctx.meta[:5]
         N, Cin, KS = w.shape
         sink = _SINK[0] and all(t.grad is not None for t in (w, b, g, be))
         G = (lambda t: t.grad) if sink else (lambda t: None)
@@ -547,9 +577,10 @@ def _vp_fused(vp, x, mask, training, seed, salt):
     k = c1.kernel_size[0]
     p1 = cl.dropout_1.p if training else 0.0
     p2 = cl.dropout_2.p if training else 0.0
-    h, hb = VPLayerFn.apply(x.contiguous(), None, ((k - 1) // 2, p1, seed, salt, cl.layer_norm_1.eps), c1.weight,
-                            c1.bias, cl.layer_norm_1.weight, cl.layer_norm_1.bias)
-    h, _ = VPLayerFn.apply(h, hb, (1, p2, seed, salt + 1, cl.layer_norm_2.eps), c2.weight, c2.bias,
+    pk = _PACKED[0]
+    h, hb = VPLayerFn.apply(x.contiguous(), None, ((k - 1) // 2, p1, seed, salt, cl.layer_norm_1.eps, pk.get(c1)),
+                            c1.weight, c1.bias, cl.layer_norm_1.weight, cl.layer_norm_1.bias)
+    h, _ = VPLayerFn.apply(h, hb, (1, p2, seed, salt + 1, cl.layer_norm_2.eps, pk.get(c2)), c2.weight, c2.bias,
                            cl.layer_norm_2.weight, cl.layer_norm_2.bias)
     out = F.linear(h, vp.linear_layer.weight, vp.linear_layer.bias).squeeze(-1)
     return out.masked_fill(mask, 0.0)
@@ -631,16 +662,18 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
 
     # encoder (transformer/Models.py:73-100; training never recomputes the PE table)
     fused = all(fused_block_on(b, compute) for b in list(enc.layer_stack) + list(dec.layer_stack))
+    _PACKED[0] = {}
     packs = [None] * (len(enc.layer_stack) + len(dec.layer_stack))
     if fused:
         seed = _train_seed(model, dev)
         if training:
             seed.add_(1)
         if os.environ.get("FS2_TRAIN_PACK", "1") != "0":
-            tp = _train_pack(model, list(enc.layer_stack) + list(dec.layer_stack), dev)
+            tp = _train_pack(model, list(enc.layer_stack) + list(dec.layer_stack), dev, _extra_convs(model, compute))
             if tp is not None:
                 tp.run(texts)
                 packs = tp.per_block
+                _PACKED[0] = tp.extra
     x = _embed(enc.src_word_emb, texts, fused) + enc.position_enc[:, :Lx, :]
     xb = None
     for i, blk in enumerate(enc.layer_stack):

@@ -594,6 +594,7 @@ typedef struct fs2_pack_desc {
   void *fwd;
   void *tr;
   int N, C, KS, n_off, N_tot, f32_copy;
+  int C_tot;         /* row length of the forward image (>= C: channel padding left as is); 0 = C */
   int tiles_c, blk0; /* filled by fs2_pack_train_plan */
 } fs2_pack_desc;
 int fs2_pack_train_plan(fs2_pack_desc *descs, int nd, int *blocks);

@@ -187,9 +187,17 @@ def test_pack_train_images(ops):
 
     torch.manual_seed(5)
     blocks = [_FFTBlock(256, 2, 1024, (9, 1)).to(DEV), _FFTBlock(256, 2, 1024, (9, 3)).to(DEV)]
-    tp = _TrainPack(blocks, torch.device(DEV))
+    extra = [torch.nn.Conv1d(80, 512, 5).to(DEV), torch.nn.Conv1d(512, 80, 5).to(DEV),
+             torch.nn.Conv1d(256, 256, 3).to(DEV)]
+    tp = _TrainPack(blocks, torch.device(DEV), extra)
     tp.run(torch.zeros(1, device=DEV))
     torch.cuda.synchronize()
+    from fs2amd.training import _packT_any
+    for conv in extra:  # VariancePredictor / PostNet convs, channel-padded images (80 channels)
+        fw, tr = tp.extra[conv]
+        ef, et = ops.pack_conv_weight(conv.weight, L.FS2_BF16), _packT_any(conv.weight)
+        assert fw.shape == ef.shape and tr.shape == et.shape
+        assert torch.equal(fw, ef) and torch.equal(tr, et)
     for blk, P in zip(blocks, tp.per_block):
         a, f = blk.slf_attn, blk.pos_ffn
         wqkv = torch.cat([a.w_qs.weight, a.w_ks.weight, a.w_vs.weight], 0).detach()
