@@ -1314,8 +1314,14 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         launch<CT, 2, 4, 2, 9, TIn, 32>(a, s);  // 64 x 128
       return;
     }
-    if (narrow && GLd && ntn == 1 && nKd >= 32 && splitk_env() && a.sk_cnt != nullptr &&
-        (int64_t)((a.M + 127) / 128) >= 64)
+    const int64_t t128 = (int64_t)((a.M + 127) / 128) * ntn;
+    if (GLd && nKd >= 64 && a.N >= 256 && splitk_env() && a.sk_cnt != nullptr && t128 < kTargetWGs && t128 >= 32)
+      // long K at a few thousand rows (training: the FFN w_1 input gradient, K = 9 x 1024; the
+      // PostNet 512 -> 512 convs, K = 2560): 128 x 128 tiles + the split-K tail instead of 32-row
+      // tiles that each stream the whole K (110 -> see DESIGN.md §6)
+      launch_128<CT, TIn>(a, s);
+    else if (narrow && GLd && ntn == 1 && nKd >= 32 && splitk_env() && a.sk_cnt != nullptr &&
+             (int64_t)((a.M + 127) / 128) >= 64)
       // one N tile and a long K (PostNet's last conv: N = 80, K = 2560): 128-row tiles and the
       // split-K tail fill the chip, instead of 32-row tiles that each stream the whole K
       launch_128<CT, TIn>(a, s);
