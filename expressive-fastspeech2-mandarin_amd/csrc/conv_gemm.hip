@@ -1301,19 +1301,6 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         return;
       }
     }
-    // thin GEMMs gathered through a row map (mel_linear: packed decoder rows -> padded [B, T, 80],
-    // K = 256): FS2_MEL_TILE (A/B) picks the row tile
-    static const int mel_tile = [] {
-      const char *e = getenv("FS2_MEL_TILE");
-      return e == nullptr ? 0 : atoi(e);
-    }();
-    if (GLd && mel_tile != 0 && a.a_rowmap != nullptr && ntn == 1 && a.KS == 1) {
-      if (mel_tile == 128)
-        launch_128<CT, TIn>(a, s);
-      else
-        launch<CT, 2, 4, 2, 9, TIn, 32>(a, s);  // 64 x 128
-      return;
-    }
     const int64_t t128 = (int64_t)((a.M + 127) / 128) * ntn;
     if (GLd && nKd >= 64 && a.N >= 256 && splitk_env() && a.sk_cnt != nullptr && t128 < kTargetWGs && t128 >= 32)
       // long K at a few thousand rows (training: the FFN w_1 input gradient, K = 9 x 1024; the
