@@ -40,7 +40,7 @@ template <int CT>
 __global__ __launch_bounds__(256, 2) void attn_kernel(const typename ATraits<CT>::T *__restrict__ qkv, int64_t qs,
                                                       const int64_t *__restrict__ lens, int T, int H, float scale_log2,
                                                       typename ATraits<CT>::T *__restrict__ out, int64_t os,
-                                                      const int32_t *__restrict__ cu) {
+                                                      const int32_t *__restrict__ cu, float *__restrict__ lse) {
   using TE = typename ATraits<CT>::T;
   constexpr int ES = sizeof(TE);
   constexpr int CEp = ATraits<CT>::CEp;
@@ -232,6 +232,9 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const typename ATraits<CT>
     TE *orow = out + (row0 + q) * os + h * DK + (lane & 15);
 #pragma unroll
     for (int ni = 0; ni < DK / 16; ++ni) orow[ni * 16] = (TE)(oacc[ni][j] * inv);
+    // log2-domain log-sum-exp of the scaled scores (the backward's softmax statistics)
+    if (lse != nullptr && (lane & 15) == 0)
+      lse[(row0 + q) * H + h] = l_run[j] > 0.f ? m_run[j] + __log2f(l_run[j]) : INFINITY;
   }
 }
 
@@ -294,7 +297,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
                                                                 uint32_t qkv_bytes, const int64_t *__restrict__ lens,
                                                                 int B, int T, int H, int nqt, float scale_log2,
                                                                 bf16 *__restrict__ out, int64_t os,
-                                                                const int32_t *__restrict__ cu) {
+                                                                const int32_t *__restrict__ cu,
+                                                                float *__restrict__ lse) {
   constexpr int QTW = 16 * NWV;          // queries per workgroup
   static_assert(KTT == 64 || KTT == 32, "keys per tile");
   constexpr int PPW = KTT / 4 / NWV;     // K (and V) 1 KiB pieces per wave per tile
@@ -485,6 +489,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
   const int q = q0 + 16 * w + li;
   if (q < T) {
     const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
+    if (lse != nullptr && g == 0)  // log2-domain log-sum-exp (m_run is in unscaled score units here)
+      lse[((int64_t)seq_base + q) * H + h] = l_run > 0.f ? m_run * scale_log2 + __log2f(l_run) : INFINITY;
     bf16 *orow = out + ((int64_t)seq_base + q) * os + h * DK + 4 * g;
 #pragma unroll
     for (int nd = 0; nd < DK / 16; ++nd) {
@@ -499,7 +505,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
 
 extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
                              int H, int dk, float temperature, void *out, int64_t out_row_stride,
-                             const int32_t *seq_cu, fs2_stream_t stream) {
+                             const int32_t *seq_cu, float *lse, fs2_stream_t stream) {
   if (qkv == nullptr || (key_lens == nullptr && seq_cu == nullptr) || out == nullptr) return FS2_EINVAL;
   if (dk != DK || H <= 0 || B < 0 || T < 0 || !(temperature > 0.f)) return FS2_EINVAL;
   if (qkv_row_stride < 3LL * H * dk || out_row_stride < (int64_t)H * dk) return FS2_EINVAL;
@@ -523,17 +529,17 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
       const int nqt = (T + 127) / 128;
       hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), dim3(nqt * H * B), dim3(512), 0, s,
                          reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
-                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
+                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse);
     } else {
       const int nqt = (T + 63) / 64;
       hipLaunchKernelGGL((attn_bf16_kernel<4, 2>), dim3(nqt * H * B), dim3(256), 0, s,
                          reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
-                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu);
+                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse);
     }
   } else if (dtype == FS2_F32)
     hipLaunchKernelGGL(attn_kernel<FS2_F32>, grid, dim3(256), 0, s, reinterpret_cast<const float *>(qkv),
                        qkv_row_stride, key_lens, T, H, scale_log2, reinterpret_cast<float *>(out), out_row_stride,
-                       seq_cu);
+                       seq_cu, lse);
   else
     return FS2_EUNSUPPORTED;
   FS2_CHECK_LAUNCH();

@@ -90,7 +90,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(const typename BT<C
                                                              const int32_t *__restrict__ cu, int T, int H,
                                                              float scale_log2, float inv_temp,
                                                              float *__restrict__ dqkv, int64_t dqs,
-                                                             float *__restrict__ lse_ws, float *__restrict__ d_ws) {
+                                                             float *__restrict__ lse_ws, float *__restrict__ d_ws,
+                                                             const float *__restrict__ lse_in) {
   using TE = typename BT<CT>::T;
   using Frag = typename BT<CT>::Frag;
   constexpr int ES = sizeof(TE), KE = BT<CT>::KE, CK = 4 * KE, NCH = DK / CK;
@@ -178,14 +179,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(const typename BT<C
   };
 
   const int ntiles = (len + KT - 1) / KT;
-  // ---- pass 1: softmax statistics of the rows 4g+j
+  // ---- pass 1: softmax statistics of the rows 4g+j (skipped when the forward saved them)
   float m[4], l[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     m[j] = -INFINITY;
     l[j] = 0.f;
   }
-  for (int kt = 0; kt < ntiles; ++kt) {
+  for (int kt = 0; kt < (lse_in == nullptr ? ntiles : 0); ++kt) {
     load_tile(kt * KT, false);
     f32x4 s[4];
     scores(kt * KT, s);
@@ -210,6 +211,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(const typename BT<C
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     lse[j] = l[j] > 0.f ? m[j] + __log2f(l[j]) : INFINITY;  // no valid key: P = 0
+    if (lse_in != nullptr) {
+      const int q = q0 + 16 * w + 4 * g + j;
+      lse[j] = q < T ? lse_in[(row0 + q) * H + h] : INFINITY;
+    }
     Dj[j] = Drow[w][4 * g + j];
   }
   // ---- pass 2: dQ
@@ -254,7 +259,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(const typename BT<C
 #pragma unroll
     for (int ni = 0; ni < DK / 16; ++ni) dr[ni * 16] = dq[ni][j] * inv_temp;
     if (li == 0) {
-      lse_ws[(row0 + q) * H + h] = lse[j];
+      if (lse_in == nullptr) lse_ws[(row0 + q) * H + h] = lse[j];
       d_ws[(row0 + q) * H + h] = Dj[j];
     }
   }
@@ -406,16 +411,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkv_kernel(const typename BT<
 template <int CT>
 void launch_bwd(const void *qkv, int64_t qs, const void *o, int64_t os, const float *dout, int64_t ds,
                 const int64_t *lens, const int32_t *cu, int B, int T, int H, float temperature, float *dqkv,
-                int64_t dqs, float *ws, hipStream_t s) {
+                int64_t dqs, float *ws, const float *lse_in, hipStream_t s) {
   using TE = typename BT<CT>::T;
   const float scale_log2 = 1.4426950408889634f / temperature, inv_temp = 1.0f / temperature;
   float *lse_ws = ws, *d_ws = ws + (int64_t)B * T * H;
   dim3 grid((T + 63) / 64, H, B);
   hipLaunchKernelGGL(attn_bwd_dq_kernel<CT>, grid, dim3(256), 0, s, reinterpret_cast<const TE *>(qkv), qs,
                      reinterpret_cast<const TE *>(o), os, dout, ds, lens, cu, T, H, scale_log2, inv_temp, dqkv, dqs,
-                     lse_ws, d_ws);
+                     lse_ws, d_ws, lse_in);
   hipLaunchKernelGGL(attn_bwd_dkv_kernel<CT>, grid, dim3(256), 0, s, reinterpret_cast<const TE *>(qkv), qs, dout, ds,
-                     lens, cu, T, H, scale_log2, inv_temp, dqkv, dqs, lse_ws, d_ws);
+                     lens, cu, T, H, scale_log2, inv_temp, dqkv, dqs, lse_in != nullptr ? lse_in : lse_ws, d_ws);
 }
 
 }  // namespace
@@ -424,7 +429,7 @@ extern "C" int fs2_attention_bwd(const void *qkv, int dtype, int64_t qkv_row_str
                                  int64_t out_row_stride, const float *dout, int64_t dout_row_stride,
                                  const int64_t *key_lens, int B, int T, int H, int dk, float temperature,
                                  float *dqkv, int64_t dqkv_row_stride, const int32_t *seq_cu, float *ws,
-                                 int64_t ws_bytes, fs2_stream_t stream) {
+                                 int64_t ws_bytes, const float *lse, fs2_stream_t stream) {
   if (qkv == nullptr || out == nullptr || dout == nullptr || dqkv == nullptr || ws == nullptr) return FS2_EINVAL;
   if ((key_lens == nullptr) == (seq_cu == nullptr)) return FS2_EINVAL;
   if (B < 0 || T < 0 || H <= 0 || dk != DK || temperature <= 0.f) return FS2_EINVAL;
@@ -439,10 +444,10 @@ extern "C" int fs2_attention_bwd(const void *qkv, int dtype, int64_t qkv_row_str
   hipStream_t s = as_stream(stream);
   if (dtype == FS2_BF16)
     launch_bwd<FS2_BF16>(qkv, qkv_row_stride, out, out_row_stride, dout, dout_row_stride, key_lens, seq_cu, B, T, H,
-                         temperature, dqkv, dqkv_row_stride, ws, s);
+                         temperature, dqkv, dqkv_row_stride, ws, lse, s);
   else if (dtype == FS2_F32)
     launch_bwd<FS2_F32>(qkv, qkv_row_stride, out, out_row_stride, dout, dout_row_stride, key_lens, seq_cu, B, T, H,
-                        temperature, dqkv, dqkv_row_stride, ws, s);
+                        temperature, dqkv, dqkv_row_stride, ws, lse, s);
   else
     return FS2_EUNSUPPORTED;
   FS2_CHECK_LAUNCH();

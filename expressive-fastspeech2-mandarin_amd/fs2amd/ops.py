@@ -607,9 +607,10 @@ def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=No
     return (out, qkv) if next_qkv is not None else out
 
 
-def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None):
+def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None, lse=None):
     """Key-padding-masked multi-head self-attention over a fused [B, T, 3*H*dk] projection
-    (or packed [B*T, 3*H*dk] rows of a SeqLayout: lens unused)."""
+    (or packed [B*T, 3*H*dk] rows of a SeqLayout: lens unused). lse: optional f32 [rows, H] that
+    receives the softmax statistics for :func:`attention_bwd`."""
     _gpu(qkv, lens)
     if layout is not None:
         B, T = layout.B, layout.T
@@ -621,7 +622,8 @@ def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None):
         out = torch.empty(*shape, device=qkv.device, dtype=qkv.dtype)
     L.check(_lib.fs2_attention(_ptr(qkv), _dt(qkv), _rows(qkv, "qkv"), _ptr(lens), B, T, n_head, d_k,
                                float(temperature), _ptr(out), _rows(out, "out"),
-                               _ptr(layout.cu) if layout is not None else None, _stream(qkv)), "fs2_attention")
+                               _ptr(layout.cu) if layout is not None else None, _ptr(lse), _stream(qkv)),
+            "fs2_attention")
     return out
 
 
@@ -650,7 +652,7 @@ def raise_if_bad_ids(device):
             raise IndexError(f"fs2amd: {n} token id(s) outside the embedding table (their encoder rows are NaN)")
 
 
-def attention_bwd(qkv, out, dout, lens, n_head, d_k, temperature, layout=None):
+def attention_bwd(qkv, out, dout, lens, n_head, d_k, temperature, layout=None, lse=None):
     """Gradient of :func:`attention` (fs2_attention_bwd): dqkv f32 with qkv's shape. qkv / out in
     the forward's dtype (the MFMA operand type), dout f32."""
     _gpu(qkv, out, dout, lens)
@@ -665,7 +667,7 @@ def attention_bwd(qkv, out, dout, lens, n_head, d_k, temperature, layout=None):
                                    _rows(dout, "dout"), _ptr(lens) if layout is None else None, B, T, n_head, d_k,
                                    float(temperature), _ptr(dqkv), _rows(dqkv, "dqkv"),
                                    _ptr(layout.cu) if layout is not None else None, _ptr(ws), ws.numel() * 4,
-                                   _stream(qkv)), "fs2_attention_bwd")
+                                   _ptr(lse), _stream(qkv)), "fs2_attention_bwd")
     return dqkv
 
 

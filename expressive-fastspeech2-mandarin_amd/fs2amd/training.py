@@ -329,7 +329,9 @@ class FFTBlockFn(torch.autograd.Function):
                       w2T=_packT(w2))
         qkv = ops.conv1d(xb, pk["qkv"], pk["bqkv"], cin=256, ks=1, pad=0, compute=BF, epilogue=L.EPI_BIAS,
                          out_dtype=BF)
-        att = ops.attention(qkv, lens, H, dk, temp)
+        B_, T_ = x.shape[0], x.shape[1]
+        lse = torch.empty(B_ * T_, H, device=x.device, dtype=torch.float32)
+        att = ops.attention(qkv, lens, H, dk, temp, lse=lse)
         a1 = ops.conv1d(att, pk["fc"], bfc.detach(), cin=256, ks=1, pad=0, compute=BF, epilogue=L.EPI_BIAS,
                         out_dtype=L.FS2_F32)
         h, hb, xh1, rs1 = ops.res_ln_fwd(a1, x.contiguous(), g1.detach(), be1.detach(), a.layer_norm.eps, lens,
@@ -340,7 +342,7 @@ class FFTBlockFn(torch.autograd.Function):
                         epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
         y, yb, xh2, rs2 = ops.res_ln_fwd(a2, h, g2.detach(), be2.detach(), f.layer_norm.eps, lens, p_drop, seed,
                                          salt + 1)
-        ctx.save_for_backward(xb, qkv, att, hb, u, xh1, rs1, xh2, rs2, lens, *params)
+        ctx.save_for_backward(xb, qkv, att, hb, u, xh1, rs1, xh2, rs2, lens, lse, *params)
         ctx.packT = (pk["qkvT"], pk["fcT"], pk["w1T"], pk["w2T"])
         ctx.meta = (H, dk, temp, k1, k2, p_drop, salt, seed)
         ctx.mark_non_differentiable(yb)
@@ -348,7 +350,7 @@ class FFTBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dyb):
-        xb, qkv, att, hb, u, xh1, rs1, xh2, rs2, lens, *params = ctx.saved_tensors
+        xb, qkv, att, hb, u, xh1, rs1, xh2, rs2, lens, lse, *params = ctx.saved_tensors
         (wq, bq, wk, bk, wv, bv, wfc, bfc, g1, be1, w1, b1, w2, b2, g2, be2) = params
         H, dk, temp, k1, k2, p_drop, salt, seed = ctx.meta
         wqkvT, wfcT, w1T, w2T = ctx.packT
@@ -373,7 +375,7 @@ class FFTBlockFn(torch.autograd.Function):
         dwfc, _ = ops.conv_wgrad(da1, att, 1, 0, dw=G(wfc), accumulate=acc)
         datt = ops.conv1d(da1, wfcT, None, cin=256, ks=1, pad=0, compute=BF, epilogue=L.EPI_BIAS,
                           out_dtype=L.FS2_F32)
-        dqkv = ops.attention_bwd(qkv, att, datt, lens, H, dk, temp)
+        dqkv = ops.attention_bwd(qkv, att, datt, lens, H, dk, temp, lse=lse)
         if sink:
             ops.conv_wgrad(dqkv, xb, 1, 0, parts=([wq.grad, wk.grad, wv.grad], [bq.grad, bk.grad, bv.grad]),
                            accumulate=True)

@@ -332,10 +332,12 @@ int64_t fs2_wconv_weight_elems(int KS, int Cin, int N); /* N*KS*Cin */
  * masked_fill then zeroes).  dk must be 128.
  * seq_cu (int32 [B+1], fs2_seq_layout) != NULL: packed rows — sequence b is rows
  * seq_cu[b] .. seq_cu[b+1]-1 of qkv / out (T = capacity bound on its length; key_lens unused).
+ * lse (optional, training): f32 [rows][H], the log2-domain log-sum-exp of each query's scaled
+ * scores (log2(e)/temperature units; +inf without a valid key) for fs2_attention_bwd.
  */
 int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
                   int H, int dk, float temperature, void *out, int64_t out_row_stride, const int32_t *seq_cu,
-                  fs2_stream_t stream);
+                  float *lse, fs2_stream_t stream);
 
 /*
  * fs2_attention_bwd — gradient of fs2_attention (training; autograd of transformer/Modules.py:14-25
@@ -347,11 +349,13 @@ int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int6
  * dqkv: f32 [rows, >= 3*H*dk] (dQ | dK | dV in the Q | K | V columns; fully written for every
  * row < T of every sequence). Layout as fs2_attention: key_lens (padded [B, T] rows) XOR seq_cu
  * (packed rows). ws: f32 workspace of >= 2*B*T*H floats (softmax statistics). dk must be 128.
+ * lse (optional): the forward's saved statistics (fs2_attention's lse); the dQ kernel then skips
+ * its statistics pass.
  */
 int fs2_attention_bwd(const void *qkv, int dtype, int64_t qkv_row_stride, const void *out, int64_t out_row_stride,
                       const float *dout, int64_t dout_row_stride, const int64_t *key_lens, int B, int T, int H,
                       int dk, float temperature, float *dqkv, int64_t dqkv_row_stride, const int32_t *seq_cu,
-                      float *ws, int64_t ws_bytes, fs2_stream_t stream);
+                      float *ws, int64_t ws_bytes, const float *lse, fs2_stream_t stream);
 
 /*
  * fs2_embed_pe — out[b,l,:] = table[tokens[b,l], :] + pe[l, :]   (f32 math)

@@ -122,6 +122,19 @@ def test_attention_backward_matches_autograd(gpu, compute, T, lens):
     assert float((out.double() - ref)[ok].abs().max()) < tol * float(ref[ok].abs().max())
     assert float((gq.double() - rq)[ok].abs().max()) < tol * float(rq[ok].abs().max())
     assert float(gq[~ok].abs().max() if (~ok).any() else 0.0) == 0.0
+    # the forward's saved log-sum-exp (fs2_attention lse) in place of the dQ kernel's statistics
+    # pass: the same gradient within 1e-5 (f32) / 1e-2 (bf16) of its scale
+    from fs2amd import ops
+    qa = src.to(torch.bfloat16) if compute == 1 else src.contiguous()
+    lse = torch.empty(B * T, H, device=DEV)
+    o2 = ops.attention(qa, lt.to(torch.int64), H, dk, dk ** 0.5, lse=lse)
+    g_lse = ops.attention_bwd(qa, o2, do, lt.to(torch.int64), H, dk, dk ** 0.5, lse=lse)
+    g_own = ops.attention_bwd(qa, o2, do, lt.to(torch.int64), H, dk, dk ** 0.5)
+    torch.cuda.synchronize()
+    assert torch.equal(o2.float(), out.detach().to(o2.dtype).float()) or compute == 1
+    tl = 1e-5 if compute == 0 else 1e-2
+    assert float((g_lse - g_own)[ok].abs().max()) <= tl * float(g_own[ok].abs().max())
+    assert float(g_lse[~ok].abs().max() if (~ok).any() else 0.0) == 0.0
 
 
 def _assert_params_close(pa, pb, lr_sum):

@@ -128,7 +128,7 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     assert lib.fs2_wconv(ctypes.byref(wd), None) == _lib.FS2_EINVAL
     assert lib.fs2_wconv_weight_elems(5, 512, 512) == 512 * 5 * 512
 
-    assert lib.fs2_attention(None, 0, 768, None, 1, 1, 2, 128, 11.3, None, 256, None, None) == _lib.FS2_EINVAL
+    assert lib.fs2_attention(None, 0, 768, None, 1, 1, 2, 128, 11.3, None, 256, None, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_lr_durations(None, 0, 1.0, 1, 1, None, None, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_lr_expand(None, 0, None, None, 1, 1, 8, 1, None, None, 0, None, None, None) == _lib.FS2_EINVAL
     assert lib.fs2_vp_norm(None, 512, 1, 2, 256, None, None, 1e-5, None, 1024, None) == _lib.FS2_EINVAL
