@@ -540,7 +540,7 @@ class VPLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, x_bf, meta, w, b, g, be):
-        pad, p_drop, seed, salt, eps = meta
+        pad, p_drop, seed, salt, eps = meta[:5]
         N, Cin, KS = w.shape
         BF = L.FS2_BF16
         xb = x_bf if x_bf is not None else x.to(torch.bfloat16)

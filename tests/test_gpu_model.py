@@ -180,7 +180,17 @@ def test_cfg2_bf16_free_running_flip_rate(model):
     assert r["dur"] <= FLIP_MAX_DUR and r["dur_step"] <= 1.0, r
     assert r["pitch"] <= FLIP_MAX_BUCKET and r["pitch_step"] <= 1 and r["dp"] <= PRED_MAX_ERR, r
     # compounded through flipped pitch embedding rows (see above): measured 44.8 % (rounds 2 and 3)
-    assert r["energy"] <= 0.5, r
+    assert r["energy"] <= 0.47, r
+    # away from the flipped pitch buckets (no flip within the energy predictor's receptive field,
+    # +-2 phonemes: two k=3 convs) the energy buckets behave as in the pinned run below
+    valid = ~f[6]
+    pflip = ((torch.bucketize(f[2], va.pitch_bins) != torch.bucketize(b[2], va.pitch_bins)) & valid).float()
+    near = torch.nn.functional.max_pool1d(pflip[:, None], 5, 1, 2)[:, 0] > 0
+    clean = valid & ~near
+    eflip = (torch.bucketize(f[3], va.energy_bins) != torch.bucketize(b[3], va.energy_bins)) & clean
+    r_clean = int(eflip.sum()) / max(1, int(clean.sum()))
+    print("energy flips away from pitch flips:", r_clean, "of", int(clean.sum()))
+    assert int(clean.sum()) >= 0.3 * r["n"] and r_clean <= FLIP_MAX_BUCKET, (r_clean, int(clean.sum()))
     # the output length follows the rounded durations exactly
     np.testing.assert_array_equal(_np(b[9]), _np(b[5]).sum(1).astype(np.int64))
     # energy on its own: pitch buckets pinned to the fp32 predictions
