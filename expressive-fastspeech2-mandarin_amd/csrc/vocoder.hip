@@ -179,13 +179,41 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
         }
       }
     };
-    wload(0, wa[0]);
-    int s = 0;
-    for (; s + 1 < nks; s += 2) {
-      kstep(s, wa[0], wa[1]);
-      kstep(s + 1, wa[1], wa[0]);
+    if constexpr (C == 32) {
+      // 32 channels: a k-step is only 12 MFMAs per wave, shorter than an L2 round trip, so the
+      // whole conv's weights (<= 11 k-steps x 2 fragments = 88 VGPRs) are loaded up front and the
+      // latency is paid once per conv instead of once per k-step
+      bf16x8 wall[11][NCB];
+#pragma unroll
+      for (int st = 0; st < 11; ++st)
+        if (st < nks) wload(st, wall[st]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int st = 0; st < 11; ++st) {
+        if (st < nks) {
+          const int shift = (st - hk) * D;  // KC == 1: k-step = tap
+#pragma unroll
+          for (int i = 0; i < kMrfNBW; ++i) {
+            const int b = first + 4 * i;
+            if (b < bhi) {
+              const int R = min(max(b * 16 + r16 + shift, 0), kMrfR - 1);
+              const bf16x8 fb = *reinterpret_cast<const bf16x8 *>(smem + addr(IN, R, g));
+#pragma unroll
+              for (int c = 0; c < NCB; ++c)
+                acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wall[st][c], fb, acc[i][c], 0, 0, 0);
+            }
+          }
+        }
+      }
+    } else {
+      wload(0, wa[0]);
+      int s = 0;
+      for (; s + 1 < nks; s += 2) {
+        kstep(s, wa[0], wa[1]);
+        kstep(s + 1, wa[1], wa[0]);
+      }
+      if (s < nks) kstep(s, wa[0], wa[1]);
     }
-    if (s < nks) kstep(s, wa[0], wa[1]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
     __builtin_amdgcn_s_barrier();  // every wave done reading IN (and T may be rewritten)
