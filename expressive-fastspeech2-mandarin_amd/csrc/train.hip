@@ -401,9 +401,9 @@ extern "C" int64_t fs2_res_ln_bwd_ws_bytes(int D) { return (int64_t)kLnBlocks * 
 extern "C" int fs2_res_ln_bwd(const float *dy, const float *xhat, const float *rstd, const float *gamma,
                               const int64_t *lens, int64_t R, int T, int D, float p_drop, const int64_t *seed, int salt,
                               float *dres, void *da, float *dgamma, float *dbeta, float *dbias, int accumulate,
-                              float *ws, int64_t ws_bytes, fs2_stream_t stream) {
+                              int defer, float *ws, int64_t ws_bytes, fs2_stream_t stream) {
   if (dy == nullptr || xhat == nullptr || rstd == nullptr || gamma == nullptr || dres == nullptr || da == nullptr ||
-      dgamma == nullptr || dbeta == nullptr || ws == nullptr)
+      ((dgamma == nullptr || dbeta == nullptr) && !defer) || ws == nullptr)
     return FS2_EINVAL;
   if (D != kD) return FS2_EUNSUPPORTED;
   if (R < 0 || T <= 0 || !(p_drop >= 0.0f && p_drop < 1.0f) || (p_drop > 0.0f && seed == nullptr)) return FS2_EINVAL;
@@ -411,6 +411,10 @@ extern "C" int fs2_res_ln_bwd(const float *dy, const float *xhat, const float *r
   if (ws_bytes < fs2_res_ln_bwd_ws_bytes(D)) return FS2_EINVAL;
   hipStream_t s = as_stream(stream);
   if (R == 0) {
+    if (defer) {
+      (void)hipMemsetAsync(ws, 0, 3 * kD * sizeof(float), s);  // one zero partial block
+      return FS2_OK;
+    }
     if (!accumulate) {
       (void)hipMemsetAsync(dgamma, 0, kD * sizeof(float), s);
       (void)hipMemsetAsync(dbeta, 0, kD * sizeof(float), s);
@@ -424,6 +428,10 @@ extern "C" int fs2_res_ln_bwd(const float *dy, const float *xhat, const float *r
   const int grid = (int)(b64 < kLnBlocks ? b64 : kLnBlocks);
   hipLaunchKernelGGL(res_ln_bwd_kernel, dim3(grid), dim3(256), 0, s, dy, xhat, rstd, gamma, lens, R, T, thr, scale,
                      seed, (uint32_t)salt, dres, reinterpret_cast<bf16 *>(da), ws);
+  if (defer) {
+    FS2_CHECK_LAUNCH();
+    return FS2_OK;
+  }
   hipLaunchKernelGGL(ln_finish_kernel, dim3(3 * kD / 64), dim3(256), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
@@ -447,16 +455,20 @@ extern "C" int fs2_relu_ln_fwd(const float *a, const float *gamma, const float *
 
 extern "C" int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xhat, const float *rstd,
                                const float *gamma, int64_t R, int D, float p_drop, const int64_t *seed, int salt,
-                               void *da, float *dgamma, float *dbeta, float *dbias, int accumulate, float *ws,
-                               int64_t ws_bytes, fs2_stream_t stream) {
+                               void *da, float *dgamma, float *dbeta, float *dbias, int accumulate, int defer,
+                               float *ws, int64_t ws_bytes, fs2_stream_t stream) {
   if (dy == nullptr || a == nullptr || xhat == nullptr || rstd == nullptr || gamma == nullptr || da == nullptr ||
-      dgamma == nullptr || dbeta == nullptr || ws == nullptr)
+      ((dgamma == nullptr || dbeta == nullptr) && !defer) || ws == nullptr)
     return FS2_EINVAL;
   if (D != kD) return FS2_EUNSUPPORTED;
   if (R < 0 || !(p_drop >= 0.0f && p_drop < 1.0f) || (p_drop > 0.0f && seed == nullptr)) return FS2_EINVAL;
   if (ws_bytes < fs2_res_ln_bwd_ws_bytes(D)) return FS2_EINVAL;
   hipStream_t s = as_stream(stream);
   if (R == 0) {
+    if (defer) {
+      (void)hipMemsetAsync(ws, 0, 3 * kD * sizeof(float), s);  // one zero partial block
+      return FS2_OK;
+    }
     if (!accumulate) {
       (void)hipMemsetAsync(dgamma, 0, kD * sizeof(float), s);
       (void)hipMemsetAsync(dbeta, 0, kD * sizeof(float), s);
@@ -469,6 +481,10 @@ extern "C" int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xha
   hipLaunchKernelGGL(relu_ln_bwd_kernel, dim3(grid), dim3(256), 0, s, dy, a, xhat, rstd, gamma, R,
                      drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt,
                      reinterpret_cast<bf16 *>(da), ws);
+  if (defer) {
+    FS2_CHECK_LAUNCH();
+    return FS2_OK;
+  }
   hipLaunchKernelGGL(ln_finish_kernel, dim3(3 * kD / 64), dim3(256), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
@@ -793,30 +809,40 @@ void wgrad_launch(const WgArgs &a, bool dy_f32, int tiles, hipStream_t s) {
     hipLaunchKernelGGL((wgrad_kernel<KS, WN, WCB, false>), dim3(tiles, a.S), dim3(256), 0, s, a);
 }
 
-int wgrad_splits(int tiles, int Q) {
+int wgrad_splits(int tiles, int Q, int KS_) {
   // enough workgroups to fill the chip, few enough splits that the partials stay small (each
   // split adds a full f32 copy of dW to write and re-read)
-  int S = (256 + tiles - 1) / tiles;
+  // KS == 1 (dW of Q|K|V, fc, w_2, mel_linear: <= 1 MB outputs): up to 32 splits for ~512
+  // workgroups; wide-tap convs (FFN w_1: a 9.4 MB dW) at most 8 splits for ~256
+  const int target = KS_ == 1 ? 512 : 256, cap = KS_ == 1 ? 32 : 8;
+  int S = (target + tiles - 1) / tiles;
   if (S > Q) S = Q;
-  if (S > 8) S = 8;
+  if (S > cap) S = cap;
   return S < 1 ? 1 : S;
 }
 
 }  // namespace
 
+extern "C" int fs2_conv_wgrad_splits(int B, int T, int N, int C, int KS) {
+  if (B <= 0 || T <= 0 || N <= 0 || C <= 0 || KS <= 0) return 1;
+  const int WN = KS == 1 ? 2 : 1, WCB = KS == 1 ? 2 : 1;
+  const int tiles = ((N + 64 * WN - 1) / (64 * WN)) * ((C + 64 * WCB - 1) / (64 * WCB));
+  return wgrad_splits(tiles, B * ((T + 31) / 32), KS);
+}
+
 extern "C" int64_t fs2_conv_wgrad_ws_bytes(int B, int T, int N, int C, int KS) {
   if (B <= 0 || T <= 0 || N <= 0 || C <= 0 || KS <= 0) return 0;
   const int WN = KS == 1 ? 2 : 1, WCB = KS == 1 ? 2 : 1;
   const int tiles = ((N + 64 * WN - 1) / (64 * WN)) * ((C + 64 * WCB - 1) / (64 * WCB));
-  const int S = wgrad_splits(tiles, B * ((T + 31) / 32));
+  const int S = wgrad_splits(tiles, B * ((T + 31) / 32), KS);
   return ((int64_t)S * KS * N * C + (int64_t)S * N) * (int64_t)sizeof(float);
 }
 
 extern "C" int fs2_conv_wgrad(const void *dy, int dy_dtype, int64_t dy_row_stride, const void *x,
                               int64_t x_row_stride, int B, int T, int N, int C, int KS, int pad, float *dw,
                               float *db, int accumulate, int split_rows, float *dw1, float *dw2, float *db1,
-                              float *db2, float *ws, int64_t ws_bytes, fs2_stream_t stream) {
-  if (dy == nullptr || x == nullptr || dw == nullptr || ws == nullptr) return FS2_EINVAL;
+                              float *db2, int defer, float *ws, int64_t ws_bytes, fs2_stream_t stream) {
+  if (dy == nullptr || x == nullptr || (dw == nullptr && !defer) || ws == nullptr) return FS2_EINVAL;
   WgOut o;
   o.dw[0] = dw, o.dw[1] = dw1, o.dw[2] = dw2;
   o.db[0] = db, o.db[1] = db1, o.db[2] = db2;
@@ -833,6 +859,10 @@ extern "C" int fs2_conv_wgrad(const void *dy, int dy_dtype, int64_t dy_row_strid
   if (KS != 1 && KS != 3 && KS != 5 && KS != 9) return FS2_EUNSUPPORTED;
   hipStream_t s = as_stream(stream);
   if ((int64_t)B * T == 0) {
+    if (defer) {  // the batch reduction sums zero partials
+      (void)hipMemsetAsync(ws, 0, (size_t)fs2_conv_wgrad_ws_bytes(B > 0 ? B : 1, T > 0 ? T : 1, N, C, KS), s);
+      return FS2_OK;
+    }
     if (!accumulate)
       for (int i = 0; i * o.split < N; ++i) {
         (void)hipMemsetAsync(o.dw[i], 0, (size_t)o.split * C * KS * sizeof(float), s);
@@ -855,7 +885,7 @@ extern "C" int fs2_conv_wgrad(const void *dy, int dy_dtype, int64_t dy_row_strid
   a.CT = (T + 31) / 32;
   a.tiles_c = (C + 64 * WCB - 1) / (64 * WCB);
   const int tiles = ((N + 64 * WN - 1) / (64 * WN)) * a.tiles_c;
-  a.S = wgrad_splits(tiles, B * a.CT);
+  a.S = wgrad_splits(tiles, B * a.CT, KS);
   a.part = ws;
   a.pbias = db != nullptr ? ws + (int64_t)a.S * KS * N * C : nullptr;
   const bool f32 = dy_dtype == FS2_F32;
@@ -864,6 +894,10 @@ extern "C" int fs2_conv_wgrad(const void *dy, int dy_dtype, int64_t dy_row_strid
     case 3: wgrad_launch<3, 1, 1>(a, f32, tiles, s); break;
     case 5: wgrad_launch<5, 1, 1>(a, f32, tiles, s); break;
     default: wgrad_launch<9, 1, 1>(a, f32, tiles, s); break;
+  }
+  if (defer) {  // partials left in ws for fs2_reduce_batch
+    FS2_CHECK_LAUNCH();
+    return FS2_OK;
   }
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(((int64_t)N * C * KS + 63) / 64)), dim3(256), 0, s, ws, a.S,
                      KS, N, C, o, accumulate);
@@ -1553,6 +1587,64 @@ extern "C" int fs2_adam_flat(float *grads, int64_t n, const fs2_adam_param *para
   blocks = blocks > 8192 ? 8192 : blocks;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, grads, n, ws, params_dev, np, lr_dev, lr,
                      beta1, beta2, eps, weight_decay, max_norm);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_ln_bwd_parts(int64_t R) {
+  const int64_t b64 = (R + 3) / 4;
+  return R <= 0 ? 1 : (int)(b64 < kLnBlocks ? b64 : kLnBlocks);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Deferred split-partial reductions of a backward pass in one launch (per <= 32 of them): the
+// weight / bias / LayerNorm-parameter gradients of the fused training nodes are only read by the
+// optimizer, so their finish passes are batched after the backward instead of one small launch
+// each. Same fixed-order sums as the immediate finish kernels (parts_col_sum).
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+__global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
+  int i = 0;
+  for (int j = 1; j < a.n; ++j)
+    if (a.d[j].blk0 <= (int64_t)blockIdx.x) i = j;
+  const fs2_reduce_desc &d = a.d[i];
+  const int64_t col = ((int64_t)blockIdx.x - d.blk0) * 64 + (threadIdx.x & 63);
+  const float v = parts_col_sum(d.part, d.S, d.M, col);
+  if (threadIdx.x >= 64 || col >= d.M) return;
+  float *base;
+  int64_t off;
+  if (d.kind == 0) {
+    const int64_t which = col / d.split;
+    base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
+    off = col - which * d.split;
+  } else {  // weight gradient partials [S][KS][N][C] -> out[n][c][k] (rows split into parameters)
+    const int64_t NC = (int64_t)d.N * d.C;
+    const int k = (int)(col / NC);
+    const int64_t nc = col - (int64_t)k * NC;
+    const int n = (int)(nc / d.C), which = n / d.split;
+    base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
+    off = (nc - (int64_t)which * d.split * d.C) * d.KS + k;
+  }
+  if (base == nullptr) return;  // an output not wanted (e.g. no conv bias behind a LayerNorm)
+  float *dst = base + off;
+  *dst = d.accumulate ? *dst + v : v;
+}
+
+}  // namespace
+
+extern "C" int fs2_reduce_batch_launch(fs2_reduce_batch *a, fs2_stream_t stream) {
+  if (a == nullptr || a->n <= 0 || a->n > FS2_REDUCE_BATCH_MAX) return FS2_EINVAL;
+  int64_t blk = 0;
+  for (int i = 0; i < a->n; ++i) {
+    fs2_reduce_desc &d = a->d[i];
+    if (d.part == nullptr || d.S <= 0 || d.M <= 0 || d.split <= 0 || (d.kind != 0 && d.kind != 1)) return FS2_EINVAL;
+    if (d.kind == 1 && (d.KS <= 0 || d.N <= 0 || d.C <= 0 || (int64_t)d.KS * d.N * d.C != d.M)) return FS2_EINVAL;
+    d.blk0 = blk;
+    blk += (d.M + 63) / 64;
+  }
+  if (blk >= (1LL << 31)) return FS2_EUNSUPPORTED;
+  hipLaunchKernelGGL(reduce_batch_kernel, dim3((unsigned)blk), dim3(256), 0, as_stream(stream), *a);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

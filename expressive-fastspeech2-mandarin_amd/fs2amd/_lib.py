@@ -49,6 +49,22 @@ class AdamParam(ctypes.Structure):
     _fields_ = [("p", _p), ("m", _p), ("v", _p), ("step", _p), ("off", _i64), ("numel", _i64)]
 
 
+class ReduceDesc(ctypes.Structure):
+    """Mirror of ``fs2_reduce_desc`` (include/fs2hip.h)."""
+
+    _fields_ = [("part", _p), ("M", _i64), ("S", _i), ("kind", _i), ("KS", _i), ("N", _i), ("C", _i), ("split", _i),
+                ("accumulate", _i), ("pad_", _i), ("out0", _p), ("out1", _p), ("out2", _p), ("blk0", _i64)]
+
+
+REDUCE_BATCH_MAX = 32
+
+
+class ReduceBatch(ctypes.Structure):
+    """Mirror of ``fs2_reduce_batch`` (include/fs2hip.h)."""
+
+    _fields_ = [("n", _i), ("pad_", _i), ("d", ReduceDesc * REDUCE_BATCH_MAX)]
+
+
 class ConvDesc(ctypes.Structure):
     """Mirror of ``fs2_conv_desc`` (include/fs2hip.h)."""
 
@@ -164,9 +180,9 @@ SIGNATURES = {
     "fs2_res_ln_bwd_ws_bytes": (_i64, [_i]),
     "fs2_pack_train_plan": (_i, [_p, _i, _p]),
     "fs2_pack_train": (_i, [_p, _i, _i, _p]),
-    "fs2_res_ln_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p, _i, _p, _p, _p, _p, _p, _i, _p, _i64, _p]),
+    "fs2_res_ln_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p, _i, _p, _p, _p, _p, _p, _i, _i, _p, _i64, _p]),
     "fs2_relu_ln_fwd": (_i, [_p, _p, _p, _i64, _i, _f, _f, _p, _i, _p, _p, _p, _p, _p]),
-    "fs2_relu_ln_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i, _f, _p, _i, _p, _p, _p, _p, _i, _p, _i64, _p]),
+    "fs2_relu_ln_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i, _f, _p, _i, _p, _p, _p, _p, _i, _i, _p, _i64, _p]),
     "fs2_embedding_bwd": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _p, _i, _p]),
     "fs2_loss_ws_bytes": (_i64, []),
     "fs2_loss_fwd": (_i, [_p, _p, _p, _p, _i64, _p]),
@@ -179,8 +195,11 @@ SIGNATURES = {
     "fs2_colsum_ws_bytes": (_i64, [_i]),
     "fs2_colsum": (_i, [_p, _i, _i64, _i, _i64, _p, _i, _p, _i64, _p]),
     "fs2_conv_wgrad_ws_bytes": (_i64, [_i, _i, _i, _i, _i]),
-    "fs2_conv_wgrad": (_i, [_p, _i, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p, _p, _p, _p, _i64,
-                            _p]),
+    "fs2_conv_wgrad": (_i, [_p, _i, _i64, _p, _i64, _i, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p, _p, _p, _p, _i, _p,
+                            _i64, _p]),
+    "fs2_conv_wgrad_splits": (_i, [_i, _i, _i, _i, _i]),
+    "fs2_ln_bwd_parts": (_i, [_i64]),
+    "fs2_reduce_batch_launch": (_i, [_p, _p]),
     "fs2_length_masks": (_i, [_p, _i, _i, _p, _p]),
     "fs2_length_regulate": (_i, [_p, _i, _p, _i, _f, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p, _p, _p]),
 }

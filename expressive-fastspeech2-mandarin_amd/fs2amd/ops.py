@@ -953,8 +953,33 @@ def res_ln_fwd(a, res, gamma, beta, eps, lens=None, p_drop=0.0, seed=None, salt=
     return y, yb, xhat, rstd
 
 
+def _defer_add(defer, ws, **kw):
+    """Queue one split-partial reduction for :func:`reduce_flush` (ws stays referenced until then)."""
+    d = L.ReduceDesc()
+    d.part = ws.data_ptr()
+    for k, v in kw.items():
+        if k == "outs":
+            for j, t in enumerate(list(v) + [None] * (3 - len(v))):
+                setattr(d, f"out{j}", t.data_ptr() if t is not None else None)
+        else:
+            setattr(d, k, v)
+    defer.append((d, ws))
+
+
+def reduce_flush(defer, like):
+    """Run the queued reductions (fs2_reduce_batch_launch, <= 32 per launch) on ``like``'s stream."""
+    for i in range(0, len(defer), L.REDUCE_BATCH_MAX):
+        chunk = defer[i:i + L.REDUCE_BATCH_MAX]
+        b = L.ReduceBatch()
+        b.n = len(chunk)
+        for j, (d, _) in enumerate(chunk):
+            b.d[j] = d
+        L.check(_lib.fs2_reduce_batch_launch(ctypes.byref(b), _stream(like)), "fs2_reduce_batch_launch")
+    defer.clear()
+
+
 def res_ln_bwd(dy, xhat, rstd, gamma, lens=None, p_drop=0.0, seed=None, salt=0, dgamma=None, dbeta=None, dbias=None,
-               want_dbias=True, accumulate=False):
+               want_dbias=True, accumulate=False, defer=None):
     """Backward of :func:`res_ln_fwd` (fs2_res_ln_bwd): returns (dres f32, da bf16, dgamma, dbeta,
     dbias) — dbias is the bias gradient of the conv that produced a (None unless wanted / given);
     accumulate adds into the given dgamma / dbeta / dbias."""
@@ -971,8 +996,11 @@ def res_ln_bwd(dy, xhat, rstd, gamma, lens=None, p_drop=0.0, seed=None, salt=0, 
     ws = torch.empty(_lib.fs2_res_ln_bwd_ws_bytes(D) // 4, device=xhat.device, dtype=torch.float32)
     L.check(_lib.fs2_res_ln_bwd(_ptr(dy), _ptr(xhat), _ptr(rstd), _ptr(gamma), _ptr(lens), B * T, T, D,
                                 float(p_drop), _ptr(seed), int(salt), _ptr(dres), _ptr(da), _ptr(dgamma), _ptr(dbeta),
-                                _ptr(dbias), 1 if accumulate else 0, _ptr(ws), ws.numel() * 4, _stream(xhat)),
-            "fs2_res_ln_bwd")
+                                _ptr(dbias), 1 if accumulate else 0, 1 if defer is not None else 0, _ptr(ws),
+                                ws.numel() * 4, _stream(xhat)), "fs2_res_ln_bwd")
+    if defer is not None:
+        _defer_add(defer, ws, M=3 * D, S=_lib.fs2_ln_bwd_parts(B * T), kind=0, split=D,
+                   accumulate=1 if accumulate else 0, outs=(dgamma, dbeta, dbias))
     return dres, da, dgamma, dbeta, dbias
 
 
@@ -992,7 +1020,7 @@ def relu_ln_fwd(a, gamma, beta, eps, p_drop=0.0, seed=None, salt=0, want_bf16=Tr
 
 
 def relu_ln_bwd(dy, a, xhat, rstd, gamma, p_drop=0.0, seed=None, salt=0, dgamma=None, dbeta=None, dbias=None,
-                want_dbias=True, accumulate=False):
+                want_dbias=True, accumulate=False, defer=None):
     """Backward of :func:`relu_ln_fwd` (fs2_relu_ln_bwd): (da bf16, dgamma, dbeta, dbias)."""
     _gpu(dy, a, xhat, rstd, gamma, seed)
     dy = dy.contiguous()
@@ -1006,7 +1034,11 @@ def relu_ln_bwd(dy, a, xhat, rstd, gamma, p_drop=0.0, seed=None, salt=0, dgamma=
     ws = torch.empty(_lib.fs2_res_ln_bwd_ws_bytes(256) // 4, device=a.device, dtype=torch.float32)
     L.check(_lib.fs2_relu_ln_bwd(_ptr(dy), _ptr(a), _ptr(xhat), _ptr(rstd), _ptr(gamma), R, 256, float(p_drop),
                                  _ptr(seed), int(salt), _ptr(da), _ptr(dgamma), _ptr(dbeta), _ptr(dbias),
-                                 1 if accumulate else 0, _ptr(ws), ws.numel() * 4, _stream(a)), "fs2_relu_ln_bwd")
+                                 1 if accumulate else 0, 1 if defer is not None else 0, _ptr(ws), ws.numel() * 4,
+                                 _stream(a)), "fs2_relu_ln_bwd")
+    if defer is not None:
+        _defer_add(defer, ws, M=3 * 256, S=_lib.fs2_ln_bwd_parts(R), kind=0, split=256,
+                   accumulate=1 if accumulate else 0, outs=(dgamma, dbeta, dbias))
     return da, dgamma, dbeta, dbias
 
 
@@ -1121,7 +1153,7 @@ def colsum(x, out=None, accumulate=False):
     return out
 
 
-def conv_wgrad(dy, x, ks, pad, dw=None, db=None, want_db=False, accumulate=False, parts=None):
+def conv_wgrad(dy, x, ks, pad, dw=None, db=None, want_db=False, accumulate=False, parts=None, defer=None):
     """Conv1d weight gradient (fs2_conv_wgrad): dy [B, T, N] f32 / bf16, x [B, T, C] bf16 ->
     dw f32 [N, C, ks] (and db f32 [N] when want_db / db given); accumulate adds into dw / db.
     parts = ([dw_0, dw_1(, dw_2)], [db_0, ...] or None): N split into equal row parts written to
@@ -1149,5 +1181,14 @@ def conv_wgrad(dy, x, ks, pad, dw=None, db=None, want_db=False, accumulate=False
     ws = torch.empty(max(1, _lib.fs2_conv_wgrad_ws_bytes(B, T, N, C, ks) // 4), device=dy.device, dtype=torch.float32)
     L.check(_lib.fs2_conv_wgrad(_ptr(dy), _dt(dy), _rows(dy, "dy"), _ptr(x), _rows(x, "x"), B, T, N, C, ks, pad,
                                 _ptr(dw), _ptr(db), 1 if accumulate else 0, split, *[_ptr(t) for t in extra],
-                                _ptr(ws), ws.numel() * 4, _stream(dy)), "fs2_conv_wgrad")
+                                1 if defer is not None else 0, _ptr(ws), ws.numel() * 4, _stream(dy)), "fs2_conv_wgrad")
+    if defer is not None:
+        S = _lib.fs2_conv_wgrad_splits(B, T, N, C, ks)
+        sp = split if split else N
+        dws = (dw, extra[0], extra[1]) if split else (dw,)
+        dbs = (db, extra[2], extra[3]) if split else (db,)
+        acc = 1 if accumulate else 0
+        _defer_add(defer, ws, M=ks * N * C, S=S, kind=1, KS=ks, N=N, C=C, split=sp, accumulate=acc, outs=dws)
+        if db is not None:
+            _defer_add(defer, ws[S * ks * N * C:], M=N, S=S, kind=0, split=sp, accumulate=acc, outs=dbs)
     return dw, db

@@ -169,6 +169,7 @@ def fft_block(blk, x, mask, lens, p_drop, training, compute):
 
 # ---- the FFT block as one autograd node on the training kernels (train.hip) -------------------------
 _SINK = [False]
+_DEFER = [None]  # in a grad_sink: the fused nodes' split-partial gradient reductions, run after backward
 _PACKED = [{}]  # conv module -> (forward image, input-gradient image) refreshed by this step's pack launch
 
 
@@ -181,9 +182,13 @@ class grad_sink:
     def __enter__(self):
         self.prev = _SINK[0]
         _SINK[0] = True
+        _DEFER[0] = []
 
     def __exit__(self, *exc):
         _SINK[0] = self.prev
+        q, _DEFER[0] = _DEFER[0], None
+        if q:  # the deferred gradient finishes, one batched launch per 32 (fs2_reduce_batch_launch)
+            ops.reduce_flush(q, q[0][1])
 
 
 def fused_block_on(blk, compute):
@@ -361,24 +366,25 @@ class FFTBlockFn(torch.autograd.Function):
         pad1, pad2 = (k1 - 1) // 2, (k2 - 1) // 2
         F_ = w1.shape[0]
         # FFN: LN backward, w_2 gradients, relu-masked input gradient, w_1 gradients, + residual
+        q = _DEFER[0] if sink else None
         dres2, da2, dg2, dbe2, db2 = ops.res_ln_bwd(dy, xh2, rs2, g2.detach(), lens, p_drop, seed, salt + 1,
-                                                    dgamma=G(g2), dbeta=G(be2), dbias=G(b2), accumulate=acc)
-        dw2, _ = ops.conv_wgrad(da2, u, k2, pad2, dw=G(w2), accumulate=acc)
+                                                    dgamma=G(g2), dbeta=G(be2), dbias=G(b2), accumulate=acc, defer=q)
+        dw2, _ = ops.conv_wgrad(da2, u, k2, pad2, dw=G(w2), accumulate=acc, defer=q)
         du = ops.conv1d(da2, w2T, None, cin=256, ks=k2, pad=k2 - 1 - pad2, compute=BF, epilogue=L.EPI_RELU_GRAD,
                         out_dtype=BF, residual=u)
-        dw1, db1 = ops.conv_wgrad(du, hb, k1, pad1, dw=G(w1), db=G(b1), want_db=True, accumulate=acc)
+        dw1, db1 = ops.conv_wgrad(du, hb, k1, pad1, dw=G(w1), db=G(b1), want_db=True, accumulate=acc, defer=q)
         dh = ops.conv1d(du, w1T, None, cin=F_, ks=k1, pad=k1 - 1 - pad1, compute=BF, epilogue=L.EPI_BIAS_RES,
                         out_dtype=L.FS2_F32, residual=dres2)
         # attention sub-layer
         dres1, da1, dg1, dbe1, dbfc = ops.res_ln_bwd(dh, xh1, rs1, g1.detach(), lens, p_drop, seed, salt,
-                                                     dgamma=G(g1), dbeta=G(be1), dbias=G(bfc), accumulate=acc)
-        dwfc, _ = ops.conv_wgrad(da1, att, 1, 0, dw=G(wfc), accumulate=acc)
+                                                     dgamma=G(g1), dbeta=G(be1), dbias=G(bfc), accumulate=acc, defer=q)
+        dwfc, _ = ops.conv_wgrad(da1, att, 1, 0, dw=G(wfc), accumulate=acc, defer=q)
         datt = ops.conv1d(da1, wfcT, None, cin=256, ks=1, pad=0, compute=BF, epilogue=L.EPI_BIAS,
                           out_dtype=L.FS2_F32)
         dqkv = ops.attention_bwd(qkv, att, datt, lens, H, dk, temp, lse=lse)
         if sink:
             ops.conv_wgrad(dqkv, xb, 1, 0, parts=([wq.grad, wk.grad, wv.grad], [bq.grad, bk.grad, bv.grad]),
-                           accumulate=True)
+                           accumulate=True, defer=q)
             gq = [None] * 6
         else:
             dws = [torch.empty_like(w) for w in (wq, wk, wv)]
@@ -487,7 +493,7 @@ class PostNetFn(torch.autograd.Function):
                                            dgamma=g.grad if sink else None, dbeta=be.grad if sink else None,
                                            accumulate=sink)
             dw, db = ops.conv_wgrad(dz, x_bf, KS, pad, dw=w.grad if sink else None, db=b.grad if sink else None,
-                                    want_db=True, accumulate=sink)
+                                    want_db=True, accumulate=sink, defer=_DEFER[0] if sink else None)
             if not sink:
                 grads[4 * i:4 * i + 4] = [dw, db, dg, dbe]
             if i > 0:
@@ -561,9 +567,10 @@ class VPLayerFn(torch.autograd.Function):
         N, Cin, KS = w.shape
         sink = _SINK[0] and all(t.grad is not None for t in (w, b, g, be))
         G = (lambda t: t.grad) if sink else (lambda t: None)
+        q = _DEFER[0] if sink else None
         da, dg, dbe, db = ops.relu_ln_bwd(dy, a, xh, rs, g.detach(), p_drop, seed, salt, dgamma=G(g), dbeta=G(be),
-                                          dbias=G(b), accumulate=sink)
-        dw, _ = ops.conv_wgrad(da, xb, KS, pad, dw=G(w), accumulate=sink)
+                                          dbias=G(b), accumulate=sink, defer=q)
+        dw, _ = ops.conv_wgrad(da, xb, KS, pad, dw=G(w), accumulate=sink, defer=q)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = ops.conv1d(da, ctx.wT, None, cin=N, ks=KS, pad=KS - 1 - pad, compute=L.FS2_BF16,

@@ -548,6 +548,8 @@ int64_t fs2_hifigan_mrf_weight_elems(int C);
  *   {1, 3, 5, 9}, N and C multiples of 8. MFMA bf16, f32 accumulation, deterministic.
  *   split_rows > 0: rows [i*split_rows, (i+1)*split_rows) of dw / db go to (dw, dw1, dw2)[i] /
  *   (db, db1, db2)[i] (2 or 3 parts: the separate Q, K, V parameters of one fused projection).
+ *   defer != 0: only the partials are written to ws ([S][KS][N][C] for dW, then [S][N] for db;
+ *   S = fs2_conv_wgrad_splits(...)), for fs2_reduce_batch_launch; dw / db unused.
  */
 int fs2_res_ln_fwd(const float *a, const void *res, int res_dtype, const float *gamma, const float *beta,
                    const int64_t *lens, int64_t R, int T, int D, float eps, float p_drop, const int64_t *seed,
@@ -555,8 +557,8 @@ int fs2_res_ln_fwd(const float *a, const void *res, int res_dtype, const float *
 int64_t fs2_res_ln_bwd_ws_bytes(int D);
 int fs2_res_ln_bwd(const float *dy, const float *xhat, const float *rstd, const float *gamma, const int64_t *lens,
                    int64_t R, int T, int D, float p_drop, const int64_t *seed, int salt, float *dres, void *da,
-                   float *dgamma, float *dbeta, float *dbias, int accumulate, float *ws, int64_t ws_bytes,
-                   fs2_stream_t stream);
+                   float *dgamma, float *dbeta, float *dbias, int accumulate, int defer, float *ws,
+                   int64_t ws_bytes, fs2_stream_t stream);
 /* fs2_relu_ln_fwd / fs2_relu_ln_bwd — one VariancePredictor layer after its conv in train mode,
  *   y = dropout(LayerNorm(relu(a)))  (model/modules.py:218-235; R rows of D = 256), y f32 (+ optional
  *   bf16 copy), saved xhat / rstd; the backward takes a again (relu mask) and gives da bf16 and
@@ -567,7 +569,8 @@ int fs2_relu_ln_fwd(const float *a, const float *gamma, const float *beta, int64
                     fs2_stream_t stream);
 int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xhat, const float *rstd, const float *gamma,
                     int64_t R, int D, float p_drop, const int64_t *seed, int salt, void *da, float *dgamma,
-                    float *dbeta, float *dbias, int accumulate, float *ws, int64_t ws_bytes, fs2_stream_t stream);
+                    float *dbeta, float *dbias, int accumulate, int defer, float *ws, int64_t ws_bytes,
+                    fs2_stream_t stream);
 /* fs2_embedding_bwd — nn.Embedding's weight gradient (transformer/Models.py:82 src_word_emb with
  *   padding_idx, model/modules.py:80-100 pitch / energy tables, fastspeech2.py:101-110 speaker /
  *   emotion tables): out[v][:] (+)= sum over i with tokens[i] == v, in increasing i, of dy[i][:]
@@ -581,7 +584,8 @@ int fs2_colsum(const void *x, int dtype, int64_t R, int N, int64_t row_stride, f
 int64_t fs2_conv_wgrad_ws_bytes(int B, int T, int N, int C, int KS);
 int fs2_conv_wgrad(const void *dy, int dy_dtype, int64_t dy_row_stride, const void *x, int64_t x_row_stride, int B,
                    int T, int N, int C, int KS, int pad, float *dw, float *db, int accumulate, int split_rows,
-                   float *dw1, float *dw2, float *db1, float *db2, float *ws, int64_t ws_bytes, fs2_stream_t stream);
+                   float *dw1, float *dw2, float *db1, float *db2, int defer, float *ws, int64_t ws_bytes,
+                   fs2_stream_t stream);
 
 /*
  * fs2_pack_train_plan / fs2_pack_train — every MFMA weight image of a training step in one launch.
@@ -672,6 +676,31 @@ int64_t fs2_adam_ws_bytes(void);
 int fs2_adam_flat(float *grads, int64_t n, const fs2_adam_param *params_dev, int np, const float *lr_dev, float lr,
                   float beta1, float beta2, float eps, float weight_decay, float max_norm, float *ws,
                   int64_t ws_bytes, fs2_stream_t stream);
+
+/*
+ * fs2_reduce_batch_launch — up to FS2_REDUCE_BATCH_MAX deferred split-partial reductions in one
+ * launch (the fused training nodes' gradient finishes, batched after the backward): per descriptor
+ * out[m] (+)= sum over s < S of part[s * M + m] (fixed order), scattered by kind:
+ *   0: m -> (out0 | out1 | out2)[m / split][m % split] (LayerNorm gamma / beta / bias, Q|K|V biases);
+ *   1: weight-gradient partials m = (k*N + n)*C + c -> out_{n / split}[((n % split)*C + c)*KS + k].
+ * blk0 is filled in. Partials come from fs2_conv_wgrad / fs2_res_ln_bwd / fs2_relu_ln_bwd with
+ * defer != 0 (fs2_conv_wgrad_splits / fs2_ln_bwd_parts give their S).
+ */
+#define FS2_REDUCE_BATCH_MAX 32
+typedef struct fs2_reduce_desc {
+  const float *part;
+  int64_t M;
+  int S, kind, KS, N, C, split, accumulate, pad_;
+  float *out0, *out1, *out2;
+  int64_t blk0;
+} fs2_reduce_desc;
+typedef struct fs2_reduce_batch {
+  int n, pad_;
+  fs2_reduce_desc d[FS2_REDUCE_BATCH_MAX];
+} fs2_reduce_batch;
+int fs2_reduce_batch_launch(fs2_reduce_batch *a, fs2_stream_t stream);
+int fs2_conv_wgrad_splits(int B, int T, int N, int C, int KS);
+int fs2_ln_bwd_parts(int64_t R);
 
 /* Library identification. */
 const char *fs2_version(void);

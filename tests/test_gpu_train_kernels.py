@@ -398,3 +398,36 @@ def test_adam_flat_equals_torch(ops, capturable, wd):
             assert torch.allclose(sa["exp_avg"], sb["exp_avg"], rtol=1e-5, atol=1e-9)
             assert torch.allclose(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-5, atol=1e-12)
             assert float(sa["step"]) == float(sb["step"]) == step + 1
+
+
+def test_deferred_reductions_bit_identical(ops):
+    """defer= (partials only, one fs2_reduce_batch_launch afterwards) gives the same bits as the
+    immediate finishes for fs2_conv_wgrad (Q|K|V parts + biases, a k=9 conv) and fs2_res_ln_bwd."""
+    torch.manual_seed(10)
+    B, T = 3, 70
+    dy = torch.randn(B, T, 768, device=DEV)
+    x = torch.randn(B, T, 256, device=DEV).to(torch.bfloat16)
+    mk = lambda: ([torch.ones(256, 256, device=DEV) for _ in range(3)], [torch.ones(256, device=DEV) for _ in range(3)])
+    p1, p2 = mk(), mk()
+    ops.conv_wgrad(dy, x, 1, 0, parts=p1, accumulate=True)
+    q = []
+    ops.conv_wgrad(dy, x, 1, 0, parts=p2, accumulate=True, defer=q)
+    dy9 = torch.randn(B, T, 1024, device=DEV).to(torch.bfloat16)
+    w9a, b9a = ops.conv_wgrad(dy9, x, 9, 4, want_db=True)
+    w9b, b9b = torch.zeros(1024, 256, 9, device=DEV), torch.zeros(1024, device=DEV)
+    ops.conv_wgrad(dy9, x, 9, 4, dw=w9b, db=b9b, defer=q)
+    a = torch.randn(B, T, 256, device=DEV)
+    lens = torch.tensor([70, 33, 1], device=DEV)
+    g = torch.rand(256, device=DEV) + 0.5
+    y, yb, xh, rs = ops.res_ln_fwd(a, torch.randn_like(a), g, torch.zeros(256, device=DEV), 1e-5, lens)
+    dyl = torch.randn_like(a)
+    _, _, ga, ba, bia = ops.res_ln_bwd(dyl, xh, rs, g, lens)
+    gb, bb, bib = (torch.zeros(256, device=DEV) for _ in range(3))
+    ops.res_ln_bwd(dyl, xh, rs, g, lens, dgamma=gb, dbeta=bb, dbias=bib, defer=q)
+    assert len(q) == 5
+    ops.reduce_flush(q, dy)
+    torch.cuda.synchronize()
+    for t1, t2 in zip(p1[0] + p1[1], p2[0] + p2[1]):
+        assert torch.equal(t1, t2)
+    assert torch.equal(w9a, w9b) and torch.equal(b9a, b9b)
+    assert torch.equal(ga, gb) and torch.equal(ba, bb) and torch.equal(bia, bib)
