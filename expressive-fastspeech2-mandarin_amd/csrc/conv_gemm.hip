@@ -1302,8 +1302,8 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
       }
     }
     const int64_t t128 = (int64_t)((a.M + 127) / 128) * ntn;
-    if (CT == FS2_BF16 && GLd && nKd >= 64 && a.N >= 256 && splitk_env() && a.sk_cnt != nullptr &&
-        t128 < kTargetWGs && t128 >= 32)
+    if (CT == FS2_BF16 && GLd && a.KS * a.Cin_pad >= 2048 && a.N >= 256 && splitk_env() && a.sk_cnt != nullptr &&
+        t128 < kTargetWGs && t128 >= 8)
       // long K at a few thousand rows (training: the FFN w_1 input gradient, K = 9 x 1024; the
       // PostNet 512 -> 512 convs, K = 2560): 128 x 128 tiles + the split-K tail instead of 32-row
       // tiles that each stream the whole K (110 -> see DESIGN.md §6)
