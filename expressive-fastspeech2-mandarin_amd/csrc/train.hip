@@ -814,7 +814,7 @@ int wgrad_splits(int tiles, int Q, int KS_) {
   // split adds a full f32 copy of dW to write and re-read)
   // KS == 1 (dW of Q|K|V, fc, w_2, mel_linear: <= 1 MB outputs): up to 32 splits for ~512
   // workgroups; wide-tap convs (FFN w_1: a 9.4 MB dW) at most 8 splits for ~256
-  const int target = KS_ == 1 ? 512 : 256, cap = KS_ == 1 ? 32 : 8;
+  const int target = KS_ == 1 ? 512 : 256, cap = KS_ == 1 ? 16 : 8;
   int S = (target + tiles - 1) / tiles;
   if (S > Q) S = Q;
   if (S > cap) S = cap;
@@ -1604,31 +1604,46 @@ extern "C" int fs2_ln_bwd_parts(int64_t R) {
 // ---------------------------------------------------------------------------------------------
 namespace {
 
+// one thread = 4 consecutive columns (16-byte partial loads, the S splits summed in order): the
+// partial buffers are large (up to 8 x 9.4 MB for the FFN w_1 gradient) and S small
 __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
   int i = 0;
   for (int j = 1; j < a.n; ++j)
     if (a.d[j].blk0 <= (int64_t)blockIdx.x) i = j;
   const fs2_reduce_desc &d = a.d[i];
-  const int64_t col = ((int64_t)blockIdx.x - d.blk0) * 64 + (threadIdx.x & 63);
-  const float v = parts_col_sum(d.part, d.S, d.M, col);
-  if (threadIdx.x >= 64 || col >= d.M) return;
-  float *base;
-  int64_t off;
-  if (d.kind == 0) {
-    const int64_t which = col / d.split;
-    base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
-    off = col - which * d.split;
-  } else {  // weight gradient partials [S][KS][N][C] -> out[n][c][k] (rows split into parameters)
-    const int64_t NC = (int64_t)d.N * d.C;
-    const int k = (int)(col / NC);
-    const int64_t nc = col - (int64_t)k * NC;
-    const int n = (int)(nc / d.C), which = n / d.split;
-    base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
-    off = (nc - (int64_t)which * d.split * d.C) * d.KS + k;
+  const int64_t col0 = (((int64_t)blockIdx.x - d.blk0) * 256 + threadIdx.x) * 4;
+  if (col0 >= d.M) return;
+  float4 acc = *reinterpret_cast<const float4 *>(d.part + col0);
+#pragma unroll 4
+  for (int k = 1; k < d.S; ++k) {
+    const float4 v = *reinterpret_cast<const float4 *>(d.part + (int64_t)k * d.M + col0);
+    acc.x += v.x;
+    acc.y += v.y;
+    acc.z += v.z;
+    acc.w += v.w;
   }
-  if (base == nullptr) return;  // an output not wanted (e.g. no conv bias behind a LayerNorm)
-  float *dst = base + off;
-  *dst = d.accumulate ? *dst + v : v;
+  const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t col = col0 + q;
+    float *base;
+    int64_t off;
+    if (d.kind == 0) {
+      const int64_t which = col / d.split;
+      base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
+      off = col - which * d.split;
+    } else {  // weight gradient partials [S][KS][N][C] -> out[n][c][k] (rows split into parameters)
+      const int64_t NC = (int64_t)d.N * d.C;
+      const int k = (int)(col / NC);
+      const int64_t nc = col - (int64_t)k * NC;
+      const int n = (int)(nc / d.C), which = n / d.split;
+      base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
+      off = (nc - (int64_t)which * d.split * d.C) * d.KS + k;
+    }
+    if (base == nullptr) continue;  // an output not wanted (e.g. no conv bias behind a LayerNorm)
+    float *dst = base + off;
+    *dst = d.accumulate ? *dst + vals[q] : vals[q];
+  }
 }
 
 }  // namespace
@@ -1638,10 +1653,12 @@ extern "C" int fs2_reduce_batch_launch(fs2_reduce_batch *a, fs2_stream_t stream)
   int64_t blk = 0;
   for (int i = 0; i < a->n; ++i) {
     fs2_reduce_desc &d = a->d[i];
-    if (d.part == nullptr || d.S <= 0 || d.M <= 0 || d.split <= 0 || (d.kind != 0 && d.kind != 1)) return FS2_EINVAL;
+    if (d.part == nullptr || d.S <= 0 || d.M <= 0 || (d.M & 3) || d.split <= 0 || (d.kind != 0 && d.kind != 1) ||
+        (reinterpret_cast<uintptr_t>(d.part) & 15))
+      return FS2_EINVAL;
     if (d.kind == 1 && (d.KS <= 0 || d.N <= 0 || d.C <= 0 || (int64_t)d.KS * d.N * d.C != d.M)) return FS2_EINVAL;
     d.blk0 = blk;
-    blk += (d.M + 63) / 64;
+    blk += (d.M + 1023) / 1024;
   }
   if (blk >= (1LL << 31)) return FS2_EUNSUPPORTED;
   hipLaunchKernelGGL(reduce_batch_kernel, dim3((unsigned)blk), dim3(256), 0, as_stream(stream), *a);

@@ -401,8 +401,10 @@ def test_adam_flat_equals_torch(ops, capturable, wd):
 
 
 def test_deferred_reductions_bit_identical(ops):
-    """defer= (partials only, one fs2_reduce_batch_launch afterwards) gives the same bits as the
-    immediate finishes for fs2_conv_wgrad (Q|K|V parts + biases, a k=9 conv) and fs2_res_ln_bwd."""
+    """defer= (partials only, one fs2_reduce_batch_launch afterwards) equals the immediate finishes
+    for fs2_conv_wgrad (Q|K|V parts + biases, a k=9 conv) and fs2_res_ln_bwd within f32 rounding of
+    the different (but fixed) summation order: 1e-6 of each output's scale; two deferred runs are
+    bit-identical."""
     torch.manual_seed(10)
     B, T = 3, 70
     dy = torch.randn(B, T, 768, device=DEV)
@@ -426,8 +428,12 @@ def test_deferred_reductions_bit_identical(ops):
     ops.res_ln_bwd(dyl, xh, rs, g, lens, dgamma=gb, dbeta=bb, dbias=bib, defer=q)
     assert len(q) == 5
     ops.reduce_flush(q, dy)
+    w9c = torch.zeros_like(w9b)
+    ops.conv_wgrad(dy9, x, 9, 4, dw=w9c, defer=q)
+    ops.reduce_flush(q, dy)
     torch.cuda.synchronize()
+    close = lambda u, v: float((u - v).abs().max()) <= 1e-6 * max(1.0, float(u.abs().max()))
     for t1, t2 in zip(p1[0] + p1[1], p2[0] + p2[1]):
-        assert torch.equal(t1, t2)
-    assert torch.equal(w9a, w9b) and torch.equal(b9a, b9b)
-    assert torch.equal(ga, gb) and torch.equal(ba, bb) and torch.equal(bia, bib)
+        assert close(t1, t2)
+    assert close(w9a, w9b) and close(b9a, b9b) and torch.equal(w9b, w9c)
+    assert close(ga, gb) and close(ba, bb) and close(bia, bib)
