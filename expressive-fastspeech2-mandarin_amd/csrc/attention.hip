@@ -434,27 +434,30 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
       // raw v_exp_f32 (exp2; underflow -> 0, -inf -> 0): libm exp2f's range reduction is dead work here
       const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2);
       l_run *= alpha;
+      // scalar multiplies: packed f32 VALU beside MFMAs costs more issue cycles than two scalar
+      // ops (cdna_hip_programming.md, VALU issue costs); same products, same bits
 #pragma unroll
-      for (int nd = 0; nd < DK / 16; ++nd) oacc[nd] *= alpha;
+      for (int nd = 0; nd < DK / 16; ++nd)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) oacc[nd][q] = __builtin_fmaf(oacc[nd][q], alpha, 0.0f);
     }
     m_run = m_new;
-    // p = exp2(s * c - m * c): the fma on score pairs (v_pk_fma_f32), pair sums (v_pk_add_f32)
+    // p = exp2(s * c - m * c), two running sums (x / y elements, as the packed form summed them)
     const float mc = -m_new * scale_log2;
-    const f32x2 c2 = {scale_log2, scale_log2}, mc2 = {mc, mc};
-    f32x2 sum2 = {0.f, 0.f};
+    float sx = 0.f, sy = 0.f;
     bf16x8 pf[NB / 2];
 #pragma unroll
     for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
-        const f32x2 sv = {sacc[ni][2 * jp], sacc[ni][2 * jp + 1]};
-        const f32x2 e = __builtin_elementwise_fma(sv, c2, mc2);
-        const f32x2 pv = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
-        sum2 += pv;
-        pf[ni >> 1][(ni & 1) * 4 + 2 * jp] = (bf16)pv.x;
-        pf[ni >> 1][(ni & 1) * 4 + 2 * jp + 1] = (bf16)pv.y;
+        const float px = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[ni][2 * jp], scale_log2, mc));
+        const float py = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[ni][2 * jp + 1], scale_log2, mc));
+        sx += px;
+        sy += py;
+        pf[ni >> 1][(ni & 1) * 4 + 2 * jp] = (bf16)px;
+        pf[ni >> 1][(ni & 1) * 4 + 2 * jp + 1] = (bf16)py;
       }
-    l_run += rows_sum(sum2.x + sum2.y);
+    l_run += rows_sum(sx + sy);
 
     // V^T fragments 4 at a time ahead of their MFMAs (one read / wait / MFMA chain per fragment
     // left every MFMA waiting out an LDS round trip)
