@@ -33,7 +33,6 @@ constexpr int kMrfL = 256;              // output samples per workgroup
 constexpr int kMrfH = 64;               // halo rows each side (>= 6 (11 - 1) = 60)
 constexpr int kMrfR = kMrfL + 2 * kMrfH;  // 384 buffer rows
 constexpr int kMrfNB = kMrfR / 16;      // 24 row blocks
-constexpr int kMrfNBW = kMrfNB / 4;     // at most 6 blocks per wave
 constexpr int kMrfLgkm0 = 0xC07F;
 
 struct MrfArgs {
@@ -77,8 +76,12 @@ __host__ __device__ constexpr int mrf_woff(int j, int p, int second) {
   return off + (2 * p + second) * mrf_conv_elems<C>(ks[j]);
 }
 
-template <int C>
-__global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
+// NW waves: 4 for C = 32 (two workgroups per CU fit LDS), 8 for C = 64 (one workgroup per CU:
+// two waves per SIMD hide the LDS / weight latency a single wave exposed)
+template <int C, int NW>
+__global__ __launch_bounds__(64 * NW) void mrf_kernel(MrfArgs p) {
+  constexpr int kMrfNBW = kMrfNB / NW;  // row blocks per wave
+  constexpr int NXS = 16 / NW;          // output row blocks (4..19) per wave
   constexpr int RB = C * 2;          // row bytes
   constexpr int NCB = C / 16;        // channel blocks (MFMA A blocks)
   constexpr int KC = C / 32;         // 32-channel k-steps per tap
@@ -105,8 +108,8 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
     constexpr int RPP = 1024 / RB;  // rows per 1 KiB piece
     constexpr int NP = BUF / 1024;
 #pragma unroll
-    for (int i = 0; i < (NP + 3) / 4; ++i) {
-      const int pc = w + 4 * i;
+    for (int i = 0; i < (NP + NW - 1) / NW; ++i) {
+      const int pc = w + NW * i;
       if (pc < NP) {
         const int R = pc * RPP + lane / (RB / 16), phys = lane % (RB / 16);
         const int logical = phys ^ mrf_swz<C>(R);
@@ -130,9 +133,9 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
     return buf + R * RB + ((q ^ mrf_swz<C>(R)) << 4);
   };
 
-  f32x4 xs[4][NCB];  // the chains' sum over output rows [64, 320): blocks 4 + w + 4i
+  f32x4 xs[NXS][NCB];  // the chains' sum over output rows [64, 320): blocks b = w (mod NW)
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NXS; ++i)
 #pragma unroll
     for (int c = 0; c < NCB; ++c) xs[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -148,7 +151,7 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
     for (int i = 0; i < kMrfNBW; ++i)
 #pragma unroll
       for (int c = 0; c < NCB; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int first = blo + ((w - blo) % 4 + 4) % 4;  // this wave's first block (b = w mod 4)
+    const int first = blo + ((w - blo) % NW + NW) % NW;  // this wave's first block (b = w mod NW)
     const int nks = K * KC;
     bf16x8 wa[2][NCB];
     auto wload = [&](int s, bf16x8 (&f)[NCB]) __attribute__((always_inline)) {
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
       const int shift = (tap - hk) * D;
 #pragma unroll
       for (int i = 0; i < kMrfNBW; ++i) {
-        const int b = first + 4 * i;
+        const int b = first + NW * i;
         if (b < bhi) {  // wave-uniform
           const int R = min(max(b * 16 + r16 + shift, 0), kMrfR - 1);
           const bf16x8 fb = *reinterpret_cast<const bf16x8 *>(smem + addr(IN, R, 4 * kc + g));
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
           const int shift = (st - hk) * D;  // KC == 1: k-step = tap
 #pragma unroll
           for (int i = 0; i < kMrfNBW; ++i) {
-            const int b = first + 4 * i;
+            const int b = first + NW * i;
             if (b < bhi) {
               const int R = min(max(b * 16 + r16 + shift, 0), kMrfR - 1);
               const bf16x8 fb = *reinterpret_cast<const bf16x8 *>(smem + addr(IN, R, g));
@@ -220,7 +223,7 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
     // epilogue: lane holds channels 16c + 4g .. +3 of row 16b + r16
 #pragma unroll
     for (int i = 0; i < kMrfNBW; ++i) {
-      const int b = first + 4 * i;
+      const int b = first + NW * i;
       if (b < bhi) {
         const int R = b * 16 + r16;
         const bool in = inside(R);
@@ -252,8 +255,8 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
               }
               *reinterpret_cast<bf16x4 *>(smem + CUR_OFF + o) = nc;
               *reinterpret_cast<bf16x4 *>(smem + ACT_OFF + o) = na;
-            } else if (i < 4) {
-              xs[i & 3][c] += v;  // the last conv of a chain: blocks 4 + w + 4i (i < 4), rows 64..319
+            } else if (i < NXS) {
+              xs[i % NXS][c] += v;  // the last conv of a chain: its output blocks 4..19, rows 64..319
             }
           }
         }
@@ -287,10 +290,10 @@ __global__ __launch_bounds__(256) void mrf_kernel(MrfArgs p) {
     }
   }
 
-  // ---- out = lrelu(xs / 3, slope) over the tile's 256 samples (blocks 4..19, 4 per wave)
+  // ---- out = lrelu(xs / 3, slope) over the tile's 256 samples (blocks 4..19, NXS per wave)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int b = 4 + w + 4 * i;
+  for (int i = 0; i < NXS; ++i) {
+    const int b = 4 + ((w - 4) % NW + NW) % NW + NW * i;
     const int R = b * 16 + r16, t = t0 + R;
     if (t < T) {
 #pragma unroll
@@ -332,9 +335,9 @@ extern "C" int fs2_hifigan_mrf(const void *x, const void *x_act, const void *w, 
   p.x_bytes = (uint32_t)bytes;
   const dim3 grid((unsigned)p.ntiles, (unsigned)B);
   if (C == 32)
-    hipLaunchKernelGGL(mrf_kernel<32>, grid, dim3(256), 0, as_stream(stream), p);
+    hipLaunchKernelGGL((mrf_kernel<32, 4>), grid, dim3(256), 0, as_stream(stream), p);
   else
-    hipLaunchKernelGGL(mrf_kernel<64>, grid, dim3(256), 0, as_stream(stream), p);
+    hipLaunchKernelGGL((mrf_kernel<64, 8>), grid, dim3(512), 0, as_stream(stream), p);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
