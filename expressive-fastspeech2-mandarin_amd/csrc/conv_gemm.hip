@@ -1301,6 +1301,12 @@ void dispatch(const ConvArgs &a, bool ln, hipStream_t s) {
         return;
       }
     }
+    // thin GEMMs gathered through a row map (mel_linear: packed decoder rows -> padded [B, T, 80],
+    // K = 256): 128-row tiles, so the 80 x 256 weights are read by 4x fewer workgroups
+    if (GLd && a.a_rowmap != nullptr && ntn == 1 && a.KS == 1 && a.M >= 128 * 64) {
+      launch_128<CT, TIn>(a, s);
+      return;
+    }
     const int64_t t128 = (int64_t)((a.M + 127) / 128) * ntn;
     if (CT == FS2_BF16 && GLd && a.KS * a.Cin_pad >= 2048 && a.N >= 256 && splitk_env() && a.sk_cnt != nullptr &&
         t128 < kTargetWGs && t128 >= 8)
