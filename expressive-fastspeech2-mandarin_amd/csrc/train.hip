@@ -1528,7 +1528,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float *__restrict__ g, int64_
     coef = coef_s;
   }
   const float lr = lr_ptr != nullptr ? *lr_ptr : lr_val;
-  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t per = ((n + gridDim.x - 1) / gridDim.x + 3) / 4 * 4;
   const int64_t e0 = (int64_t)blockIdx.x * per, e1 = e0 + per < n ? e0 + per : n;
   if (e0 >= e1) return;
   // parameter holding e0: last desc with off <= e0 (binary search)
@@ -1547,27 +1547,45 @@ __global__ __launch_bounds__(256) void adam_kernel(float *__restrict__ g, int64_
     bc2s = sqrtf(bc2);
   };
   param_consts();
-  for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+  // 4 consecutive elements per thread: a group lies in one parameter (16-byte aligned starts) or
+  // in the zero gap after it; whole groups use 16-byte accesses, a parameter's ragged end scalars
+  auto upd = [&](float gr, float &pv, float &mv, float &vv) __attribute__((always_inline)) {
+    if (wd != 0.0f) gr += wd * pv;
+    mv = b1 * mv + (1.0f - b1) * gr;
+    vv = b2 * vv + (1.0f - b2) * gr * gr;
+    pv = pv - step_size * mv / (sqrtf(vv) / bc2s + eps);
+  };
+  for (int64_t e = e0 + 4 * threadIdx.x; e < e1; e += 1024) {
     if (e >= pend) {
-      while (e >= d[pi].off + d[pi].numel) ++pi;
+      while (e >= d[pi].off + d[pi].numel && pi + 1 < np && e >= d[pi + 1].off) ++pi;
       pend = d[pi].off + d[pi].numel;
       param_consts();
     }
-    const int64_t j = e - d[pi].off;
-    float gr = g[e];
-    if (max_norm > 0.0f) {
-      gr *= coef;
-      g[e] = gr;
+    if (e < d[pi].off || e >= pend) {  // the gap after a parameter (zeros, nothing to update)
+      if (max_norm > 0.0f) *reinterpret_cast<float4 *>(g + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+      continue;
     }
-    float *pp = d[pi].p + j;
-    const float pv = *pp;
-    if (wd != 0.0f) gr += wd * pv;
-    float *mp = d[pi].m + j, *vp = d[pi].v + j;
-    const float m = b1 * *mp + (1.0f - b1) * gr;
-    const float v = b2 * *vp + (1.0f - b2) * gr * gr;
-    *mp = m;
-    *vp = v;
-    *pp = pv - step_size * m / (sqrtf(v) / bc2s + eps);
+    const int64_t j = e - d[pi].off;
+    float4 gv = *reinterpret_cast<const float4 *>(g + e);
+    if (max_norm > 0.0f) {
+      gv.x *= coef, gv.y *= coef, gv.z *= coef, gv.w *= coef;
+      *reinterpret_cast<float4 *>(g + e) = gv;
+    }
+    float *pp = d[pi].p + j, *mp = d[pi].m + j, *vp = d[pi].v + j;
+    if (j + 4 <= d[pi].numel) {
+      float4 pv = *reinterpret_cast<const float4 *>(pp), mv = *reinterpret_cast<const float4 *>(mp),
+             vv = *reinterpret_cast<const float4 *>(vp);
+      upd(gv.x, pv.x, mv.x, vv.x);
+      upd(gv.y, pv.y, mv.y, vv.y);
+      upd(gv.z, pv.z, mv.z, vv.z);
+      upd(gv.w, pv.w, mv.w, vv.w);
+      *reinterpret_cast<float4 *>(pp) = pv;
+      *reinterpret_cast<float4 *>(mp) = mv;
+      *reinterpret_cast<float4 *>(vp) = vv;
+    } else {
+      const float gs[4] = {gv.x, gv.y, gv.z, gv.w};
+      for (int q = 0; q < 4 && j + q < d[pi].numel; ++q) upd(gs[q], pp[q], mp[q], vp[q]);
+    }
   }
 }
 
@@ -1578,7 +1596,9 @@ extern "C" int64_t fs2_adam_ws_bytes(void) { return (int64_t)kAdamNormBlocks * (
 extern "C" int fs2_adam_flat(float *grads, int64_t n, const fs2_adam_param *params_dev, int np, const float *lr_dev,
                              float lr, float beta1, float beta2, float eps, float weight_decay, float max_norm,
                              float *ws, int64_t ws_bytes, fs2_stream_t stream) {
-  if (grads == nullptr || params_dev == nullptr || np <= 0 || ws == nullptr || n < 0) return FS2_EINVAL;
+  if (grads == nullptr || params_dev == nullptr || np <= 0 || ws == nullptr || n < 0 || (n & 3) ||
+      (reinterpret_cast<uintptr_t>(grads) & 15))
+    return FS2_EINVAL;
   if (ws_bytes < fs2_adam_ws_bytes()) return FS2_EINVAL;
   if (n == 0) return FS2_OK;
   hipStream_t s = as_stream(stream);

@@ -39,8 +39,9 @@ class ScheduledOptim:
                 and all(p.is_cuda and p.dtype == torch.float32 for p in g["params"]))
 
     def flat_step(self, flat, params, max_norm):
-        """clip_grad_norm_(params, max_norm) + Adam.step() where params' gradients are consecutive
-        views of ``flat`` (fs2amd.trainer's buffer). The optimizer state is torch's own (exp_avg,
+        """clip_grad_norm_(params, max_norm) + Adam.step() where params' gradients are views of
+        ``flat`` in increasing order, each starting on a 16-byte boundary (fs2amd.trainer's buffer;
+        gap elements between them stay zero). The optimizer state is torch's own (exp_avg,
         exp_avg_sq, a float32 device step per parameter; created here if absent, outside capture),
         so state_dict / checkpoints are unchanged."""
         import ctypes
@@ -61,7 +62,7 @@ class ScheduledOptim:
         key += tuple(st["exp_avg"].data_ptr() + st["exp_avg_sq"].data_ptr() + st["step"].data_ptr() for st in states)
         if plan is None or plan[0] != key:
             arr = (L.AdamParam * len(params))()
-            off = 0
+            base, end = flat.data_ptr(), 0
             for d, p, st in zip(arr, params, states):
                 if not (p.is_contiguous() and st["exp_avg"].is_contiguous() and st["exp_avg_sq"].is_contiguous()):
                     raise RuntimeError("fs2amd: fused Adam needs contiguous parameters and state")
@@ -69,10 +70,14 @@ class ScheduledOptim:
                     st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
                 d.p, d.m, d.v, d.step = (p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
                                          st["step"].data_ptr())
-                d.off, d.numel = off, p.numel()
-                off += p.numel()
-            if off != flat.numel():
-                raise RuntimeError("fs2amd: flat gradient buffer does not match the parameters")
+                g = p.grad
+                if g is None or not g.is_contiguous() or not (base <= g.data_ptr() < base + 4 * flat.numel()):
+                    raise RuntimeError("fs2amd: every parameter's gradient must be a view of the flat buffer")
+                d.off, d.numel = (g.data_ptr() - base) // 4, p.numel()
+                ptrs = (g.data_ptr(), d.p, d.m, d.v)
+                if any(x % 16 for x in ptrs) or d.off < end:
+                    raise RuntimeError("fs2amd: fused Adam needs 16-byte aligned, increasing, disjoint gradient views")
+                end = d.off + d.numel
             dev = torch.frombuffer(bytearray(bytes(memoryview(arr).cast("B"))), dtype=torch.uint8).to(flat.device)
             ws = torch.empty(L.load().fs2_adam_ws_bytes() // 4, device=flat.device, dtype=torch.float32)
             plan = self._flat_plan = (key, dev, ws, len(params))

@@ -156,12 +156,15 @@ class TrainStep:
     def _setup_flat_grads(self):
         params = [p for p in self.model.parameters() if p.requires_grad]
         self._flat_params = params
-        n = sum(p.numel() for p in params)
-        self._flat = torch.zeros(n, dtype=torch.float32, device=params[0].device)
-        off = 0
+        # each gradient starts on a 16-byte boundary (the fused Adam's vector loads); the few gap
+        # elements stay zero (all-reduced and counted in the norm as zeros)
+        offs, n = [], 0
         for p in params:
+            offs.append(n)
+            n += (p.numel() + 3) // 4 * 4
+        self._flat = torch.zeros(n, dtype=torch.float32, device=params[0].device)
+        for p, off in zip(params, offs):
             p.grad = self._flat[off:off + p.numel()].view_as(p)
-            off += p.numel()
         step = max(1, int(self.bucket_mb * (1 << 20) // 4))
         self._buckets = [self._flat[i:i + step] for i in range(0, n, step)]
         self._bn_buffers = [b for name, b in self.model.named_buffers()

@@ -373,12 +373,15 @@ def test_adam_flat_equals_torch(ops, capturable, wd):
     ma, mb = M(ps), M(ps)
     oa = ScheduledOptim(ma, tc, mc, 0, capturable=capturable)
     ob = ScheduledOptim(mb, tc, mc, 0, capturable=capturable)
-    n = sum(p.numel() for p in ma.parameters())
-    flat = torch.zeros(n, device=DEV)
-    off = 0
+    # the trainer's layout: each gradient starts on a 16-byte boundary, zero gaps after the
+    # ragged sizes (33, 7) -- exercises the kernel's vector groups, ragged ends and gaps
+    offs, n = [], 0
     for p in ma.parameters():
+        offs.append(n)
+        n += (p.numel() + 3) // 4 * 4
+    flat = torch.zeros(n, device=DEV)
+    for p, off in zip(ma.parameters(), offs):
         p.grad = flat[off:off + p.numel()].view_as(p)
-        off += p.numel()
     for step in range(3):
         gs = [torch.randn(s, device=DEV) * (3.0 if step == 0 else 0.001) for s in shapes]
         for p, g in zip(ma.parameters(), gs):
@@ -398,6 +401,10 @@ def test_adam_flat_equals_torch(ops, capturable, wd):
             assert torch.allclose(sa["exp_avg"], sb["exp_avg"], rtol=1e-5, atol=1e-9)
             assert torch.allclose(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-5, atol=1e-12)
             assert float(sa["step"]) == float(sb["step"]) == step + 1
+        used = torch.zeros(n, dtype=torch.bool, device=DEV)
+        for p, off in zip(ma.parameters(), offs):
+            used[off:off + p.numel()] = True
+        assert not flat[~used].any()
 
 
 def test_deferred_reductions_bit_identical(ops):

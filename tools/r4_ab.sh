@@ -7,4 +7,6 @@ timeout -k 10 120 python tools/kernel_probe.py attn --time > $O/attn_time.log 2>
 tail -1 $O/attn_time.log
 timeout -k 10 400 python -u -m pytest tests/test_gpu_vocoder.py tests/test_gpu_ops.py tests/test_gpu_train.py tests/test_gpu_graphs.py -k "vocoder or mrf or generator or attention or attn or graph" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1 || { tail -20 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
+timeout -k 10 200 python -u -m pytest tests/test_gpu_train_kernels.py -k adam -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tests_adam.log 2>&1 || { tail -20 $O/tests_adam.log; exit 1; }
+tail -1 $O/tests_adam.log
 bash tools/prof_voc.sh $TAG && bash tools/fwd_trace.sh $TAG
