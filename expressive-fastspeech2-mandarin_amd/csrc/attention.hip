@@ -504,6 +504,221 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_bf16_kernel(const bf16 *__re
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 32 queries per wave on v_mfma_f32_32x32x16_bf16 (the decoder's long sequences). Swapped product
+// S^T = K Q^T: a lane owns ONE query (column lane & 31) and 16 keys of each 32-key block in its
+// registers (rows crow(r, h) = (r & 3) + 8 (r >> 2) + 4 h, h = lane >> 5), so the row max / sum is
+// in-lane plus one permlane32 swap. The exponentiated scores are already the B operand of
+// O^T = V^T P^T (k-step s = registers 8 (s & 1) .. +7 of block s >> 1, keys in crow order), and
+// V^T's A fragments take the same key order from two transposed reads (rows 4h .. 4h+3 and
+// 8+4h .. 8+4h+3 of the 16-key step). Each K / V fragment read from LDS feeds a 32-query MFMA:
+// half the LDS bytes per FLOP of the 16-query form (whose K and V reads alone were 512 KB per
+// 64-key tile per CU at 16 waves). O^T stays in registers: lane = query, so the online-softmax
+// rescale is lane-local. K / V tiles: the same LDS-DMA ring as attn_bf16_kernel, rows swizzled
+// with the 256-byte-row XOR map under which the b128 row reads and the transposed reads of the
+// 32x32x16 operands are both conflict-free (cdna_hip_programming.md, T11 image (b)).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ int kv32_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int kv32_off(int row, int chunk) { return row * 256 + ((chunk ^ kv32_swz(row)) << 4); }
+
+template <int NWV, int NST>
+__global__ __launch_bounds__(64 * NWV, 2) void attn32_kernel(const bf16 *__restrict__ qkv, int64_t qs, uint32_t qkv_bytes,
+                                                             const int64_t *__restrict__ lens, int B, int T, int H, int nqt,
+                                                             float scale_log2, bf16 *__restrict__ out, int64_t os,
+                                                             const int32_t *__restrict__ cu, float *__restrict__ lse) {
+  constexpr int KTT = 64;
+  constexpr int QTW = 32 * NWV;       // queries per workgroup
+  constexpr int PPW = KTT / 4 / NWV;  // K (and V) 1 KiB pieces per wave per tile
+  constexpr int LPS = 2 * PPW;        // LDS-DMA loads per wave per tile
+  constexpr int STG = 2 * KTT * 256;  // K + V bytes of one tile
+  static_assert(PPW >= 1 && KTT % (4 * NWV) == 0, "pieces per wave");
+  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+
+  // XCD-contiguous work order, as attn_bf16_kernel
+  const int nwg = gridDim.x, id = blockIdx.x;
+  const int q8 = nwg >> 3, rem = nwg & 7, xcd = id & 7;
+  const int t = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (id >> 3);
+  const int qt = t % nqt, bh = t / nqt, h = bh % H, b = bh / H;
+  const int q0 = qt * QTW;
+  int len;
+  uint32_t seq_base;
+  if (cu != nullptr) {
+    seq_base = (uint32_t)cu[b];
+    len = cu[b + 1] - cu[b];
+    T = len;
+  } else {
+    const int64_t len64 = lens[b];
+    len = (int)(len64 < 0 ? 0 : (len64 > T ? T : len64));
+    seq_base = (uint32_t)b * (uint32_t)T;
+  }
+  if (q0 >= T) return;
+  const bool active = q0 + 32 * w < T;  // wave-uniform
+
+  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16 *>(qkv), (short)0, (int)qkv_bytes, 0x00020000);
+  const uint32_t row_bytes = (uint32_t)qs * 2u;
+
+  // Q^T fragments (B operand of 32x32x16): query q0 + 32w + r32, head dims 16s + 8hh .. +7
+  const int qrow = q0 + 32 * w + r32;
+  bf16x8 qf[DK / 16];
+#pragma unroll
+  for (int s = 0; s < DK / 16; ++s) {
+    const uint32_t off = qrow < T ? (seq_base + qrow) * row_bytes + (uint32_t)(h * DK + 16 * s + 8 * hh) * 2u : 0x80000000u;
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    qf[s] = *reinterpret_cast<bf16x8 *>(&v);
+  }
+
+  const int prow = lane >> 4, pch = lane & 15;
+  auto dma = [&](int k0, int buf) __attribute__((always_inline)) {
+    char *Kb = smem + buf * STG;
+    char *Vb = Kb + KTT * 256;
+#pragma unroll
+    for (int it = 0; it < PPW; ++it) {
+      const int p = w + NWV * it;
+      const int r = 4 * p + prow;
+      const int lc = pch ^ kv32_swz(r);
+      const int key = k0 + r;
+      const uint32_t base = key < T ? (seq_base + key) * row_bytes + (uint32_t)lc * 16u : 0x80000000u;
+      const uint32_t koff = base == 0x80000000u ? base : base + (uint32_t)((H + h) * DK) * 2u;
+      const uint32_t voff = base == 0x80000000u ? base : base + (uint32_t)((2 * H + h) * DK) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(Kb + p * 1024), 16, koff,
+                                               0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(Vb + p * 1024), 16, voff,
+                                               0, 0, 0);
+    }
+  };
+
+  f32x16 oacc[DK / 32];
+#pragma unroll
+  for (int i = 0; i < DK / 32; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;  // m: raw score units, both lane halves equal; l: this half's keys
+
+  const int ntiles = (len + KTT - 1) / KTT;
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st)
+    if (st < ntiles) dma(st * KTT, st);
+  // transposed V reads: 16-lane group gq = lane >> 4 takes dims 16 (gq & 1) .. +15 of a 32-dim
+  // block and key rows 4 (gq >> 1) + q (+ 8 for the second read); lane 4q + p of the group
+  // addresses row q, dims 4p .. 4p + 3 (chunk 2 (gq & 1) + (p >> 1), byte 8 (p & 1))
+  const int gq = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int vrow = 4 * (gq >> 1) + tq;
+  auto tile = [&](int kt, auto masked_tag) __attribute__((always_inline)) {
+    constexpr bool MASKED = decltype(masked_tag)::value;
+    const int k0 = kt * KTT;
+    const int ahead = ntiles - 1 - kt;
+    if (NST >= 3 && ahead >= NST - 2)
+      attn_vm_wait<LPS * (NST - 2)>();
+    else
+      attn_vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST - 1 < ntiles) dma(k0 + (NST - 1) * KTT, (kt + NST - 1) % NST);
+    if (!active) return;
+    const char *Kb = smem + (kt % NST) * STG;
+    const char *Vb = Kb + KTT * 256;
+
+    // S^T[key][query] for the tile's two 32-key blocks
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < DK / 16; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(Kb + kv32_off(kb * 32 + r32, 2 * s + hh));
+        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kb], 0, 0, 0);
+      }
+    }
+    if constexpr (MASKED) {  // keys >= len -> -inf
+      const int lim = len - k0 - 4 * hh;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kb * 32 + (r & 3) + 8 * (r >> 2) >= lim) sacc[kb][r] = -INFINITY;
+    }
+    float mx = m_run;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) mx = max_nn(max_nn(mx, sacc[kb][r]), sacc[kb][r + 1]);
+    {
+      auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = max_nn(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    const float m_new = mx;  // includes m_run
+    if (__builtin_amdgcn_ballot_w64(m_new != m_run) != 0) {
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2);
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < DK / 32; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[i][r] = __builtin_fmaf(oacc[i][r], alpha, 0.0f);
+    }
+    m_run = m_new;
+    const float mc = -m_new * scale_log2;
+    float sx = 0.f, sy = 0.f;
+    bf16x8 pf[KTT / 16];
+#pragma unroll
+    for (int s = 0; s < KTT / 16; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const float px = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[s >> 1][8 * (s & 1) + j], scale_log2, mc));
+        const float py = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[s >> 1][8 * (s & 1) + j + 1], scale_log2, mc));
+        sx += px;
+        sy += py;
+        pf[s][j] = (bf16)px;
+        pf[s][j + 1] = (bf16)py;
+      }
+    l_run += sx + sy;
+
+    // O^T[d][q] += V^T[d][keys of step s] P^T: 4 dim blocks x 4 key steps
+#pragma unroll
+    for (int s = 0; s < KTT / 16; ++s) {
+      bf16x8 vf[DK / 32];
+#pragma unroll
+      for (int db = 0; db < DK / 32; ++db) {
+        const int ch = 4 * db + 2 * (gq & 1) + (tp >> 1);
+        const char *v0 = Vb + kv32_off(16 * s + vrow, ch) + 8 * (tp & 1);
+        const char *v1 = Vb + kv32_off(16 * s + 8 + vrow, ch) + 8 * (tp & 1);
+        auto lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)v0);
+        auto hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)v1);
+        __builtin_memcpy(&vf[db], &lo, 8);
+        __builtin_memcpy(reinterpret_cast<char *>(&vf[db]) + 8, &hi, 8);
+      }
+#pragma unroll
+      for (int db = 0; db < DK / 32; ++db)
+        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[db], pf[s], oacc[db], 0, 0, 0);
+    }
+  };
+  for (int kt = 0; kt + 1 < ntiles; ++kt) tile(kt, std::false_type{});
+  if (ntiles > 0) tile(ntiles - 1, std::true_type{});
+
+  // the two halves' sums (same m); O^T[d][query r32], d = 32 db + (r & 3) + 8 (r >> 2) + 4 hh
+  {
+    auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
+    l_run = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  if (active && qrow < T) {
+    const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
+    if (lse != nullptr && hh == 0)
+      lse[((int64_t)seq_base + qrow) * H + h] = l_run > 0.f ? m_run * scale_log2 + __log2f(l_run) : INFINITY;
+    bf16 *orow = out + ((int64_t)seq_base + qrow) * os + h * DK + 4 * hh;
+#pragma unroll
+    for (int db = 0; db < DK / 32; ++db)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        bf16x4 o = {(bf16)(oacc[db][4 * r4] * inv), (bf16)(oacc[db][4 * r4 + 1] * inv),
+                    (bf16)(oacc[db][4 * r4 + 2] * inv), (bf16)(oacc[db][4 * r4 + 3] * inv)};
+        *reinterpret_cast<bf16x4 *>(orow + 32 * db + 8 * r4) = o;
+      }
+  }
+}
+
 }  // namespace
 
 extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
@@ -528,7 +743,17 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
     // stages; 4 waves / 2 or 3 stages 34.5 / 49.9 us; the software-pipelined, 32-key-tile and
     // 32-queries-per-wave variants measured 30.5, 31-32 and 27.4 us standalone / bench-neutral and
     // were removed in round 3).
-    if (T > 64) {
+    static const int use32 = [] {
+      const char *e = getenv("FS2_ATTN32");
+      return (e != nullptr && e[0] == '0') ? 0 : 1;
+    }();
+    if (T > 64 && use32) {
+      // 4 waves x 32 queries, two workgroups per CU (2 x 64 KiB of K / V ring)
+      const int nqt = (T + 127) / 128;
+      hipLaunchKernelGGL((attn32_kernel<4, 2>), dim3(nqt * H * B), dim3(256), 0, s,
+                         reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
+                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse);
+    } else if (T > 64) {
       const int nqt = (T + 127) / 128;
       hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), dim3(nqt * H * B), dim3(512), 0, s,
                          reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,

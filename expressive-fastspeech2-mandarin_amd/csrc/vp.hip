@@ -16,6 +16,8 @@
 #include <type_traits>
 #include <utility>
 
+#include <cstdlib>
+
 #include "conv_common.h"
 #include "fs2_common.h"
 
@@ -154,6 +156,8 @@ constexpr int kVpUnits = 2 * kVpKS * 2;   // per wave: 2 convs x 24 k-steps x (h
 constexpr uint32_t kVpWaveBytes = (uint32_t)kVpUnits * kVpUnit;
 constexpr int kVpDepth = 4;               // k-steps in flight (8 units, 128 registers)
 constexpr int kVpLgkm0 = 0xC07F;          // s_waitcnt lgkmcnt(0) as a real wait-count instruction
+constexpr int kVpPrefetchMax = 20;        // warm-up loads per wave (x tile + ring + these < 64 in flight)
+constexpr int kVpScratchOff = 512 + 4 * ((((50 * 544 + 1023) / 1024) + 3) / 4) * 1024;  // = HHI_OFF
 
 struct VpArgs {
   const bf16 *x;
@@ -165,6 +169,7 @@ struct VpArgs {
   float eps;
   int M, L, G, ntiles;
   const int64_t *lens;
+  int prefetch;       // L2 warm-up of the weight stream (FS2_VP_PREFETCH, default on)
   float *pred;        // [G][M]
   int embed_g;
   bf16 *xo;
@@ -197,6 +202,7 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
   constexpr int IDX_OFF = RED_OFF + kVpHR * 4 * 4;      // bucket index per output row
   constexpr int SMEM = IDX_OFF + kVpBM * 4;
   static_assert(SMEM <= 163840, "LDS");
+  static_assert(kVpScratchOff == HHI_OFF && 4 * 1024 <= kVpHR * kVpPitch, "warm-up scratch slot");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -209,7 +215,25 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
     g = xcd >> 2;
     tile = (blockIdx.x >> 3) * 4 + (xcd & 3);
   }
-  if (tile >= p.ntiles) return;
+  const rsrc_t wr = make_rsrc(p.w, p.w_bytes);
+  // ---- L2 warm-up: the workgroups of one XCD march through the same weight stream in lockstep, so
+  // a ring load is one HBM round trip for the whole XCD (≈ 45–70 GB/s per CU measured). Each wave
+  // first pulls a disjoint 1 KiB slice of its predictor's stream (1.5 MB, fits the XCD's 4 MB L2)
+  // by LDS DMA into a scratch slot (HHI, unused until LN1): the XCD fetches the whole stream at once
+  // and the rings then hit L2. Dispatch is round-robin over the XCDs (speed only, like g above).
+  if (p.prefetch) {
+    constexpr int kPieces = (int)(4 * kVpWaveBytes / 1024);
+    const int xcd = blockIdx.x & 7, peers = ((int)gridDim.x - xcd + 7) / 8;
+    const int me = (int)(blockIdx.x >> 3) * 4 + w, nw = peers * 4;
+    const uint32_t gb = (uint32_t)g * 4u * kVpWaveBytes + (uint32_t)lane * 16u;
+    for (int i = 0, pc = me; i < kVpPrefetchMax && pc < kPieces; ++i, pc += nw)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void *)(smem + kVpScratchOff + w * 1024),
+                                               16, gb + (uint32_t)pc * 1024u, 0, 0, 0);
+  }
+  if (tile >= p.ntiles) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA into LDS outlives the workgroup
+    return;
+  }
   const int M = p.M, L = p.L, m0 = tile * kVpBM;
   const int r16 = lane & 15, hi = lane >> 4;
 
@@ -236,7 +260,6 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
 
   // ---- x tile (rows m0 - 2 .. m0 + 47) -> LDS by DMA, lane-linear pieces of 1 KiB
   const rsrc_t xr = make_rsrc(p.x, p.x_bytes);
-  const rsrc_t wr = make_rsrc(p.w, p.w_bytes);
   const uint32_t xrow = (uint32_t)p.xs * 2u;
 #pragma unroll
   for (int i = 0; i < XPW; ++i) {
@@ -630,6 +653,11 @@ extern "C" int fs2_vp_fused(const fs2_vp_fused_desc *d, fs2_stream_t stream) {
   p.bins = d->bins;
   p.nb = d->n_bins - 1;
   p.table = d->table;
+  static const int prefetch = [] {
+    const char *e = getenv("FS2_VP_PREFETCH");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+  }();
+  p.prefetch = prefetch;
   const int nwg = d->G == 2 ? 8 * ((p.ntiles + 3) / 4) : p.ntiles;
   hipLaunchKernelGGL(vp_fused_kernel, dim3(nwg), dim3(256), 0, as_stream(stream), p);
   FS2_CHECK_LAUNCH();

@@ -4,7 +4,8 @@
     python tools/kernel_probe.py conv9 --reps 20
 kernels: ffn (decoder fused FFN, fs2_ffn), ffn_rows / ffn2_rows (decoder FFN fused / two launches on --rows
 packed rows), enc_ffn (encoder FFN fused, --nsplit), conv9 (decoder FFN Conv1d k=9 256->1024), conv1 (FFN k=1 1024->256 + res + LN),
-qkv, attn, lr (LengthRegulator gather + PE), postnet (512->512 k=5 + tanh).
+qkv, attn, lr (LengthRegulator gather + PE), postnet (512->512 k=5 + tanh), vpf / vpf_dp / vpf_en
+(fs2_vp_fused sets). --flush MB writes that much before each launch (cold caches).
 """
 import argparse
 import os
@@ -25,6 +26,7 @@ def main():
     ap.add_argument("--nsplit", type=int, default=None, help="ffn / enc_ffn / ffn_rows: fs2_ffn split-hidden workgroups per tile")
     ap.add_argument("--tile-rows", type=int, default=None, help="ffn / enc_ffn / ffn_rows: fs2_ffn tile rows (112 / 64)")
     ap.add_argument("--rows", type=int, default=11141, help="ffn_rows / ffn2_rows: packed decoder rows (free-running cfg2: 11141)")
+    ap.add_argument("--flush", type=int, default=0, help="MB written before each launch (cold L2 / MALL); --time subtracts it")
     a = ap.parse_args()
     import bench
     from fs2amd import _lib as L, ops
@@ -168,8 +170,28 @@ def main():
         else:
             from fs2amd.runtime import variance_predictor
             fn = lambda: variance_predictor(P.vp["pitch"], xe, le)
+    elif a.kernel in ("vpf", "vpf_dp", "vpf_en"):  # fs2_vp_fused: duration + pitch set, energy set (both: vpf)
+        V = P.vpfused
+        xe = rnd(64, 64, 256)
+        le = b["src_lens"]
+        emb_p = (1, b.get("p_targets"), 1.0, P.bins["pitch"], P.var_table["pitch"])
+        emb_e = (0, b.get("e_targets"), 1.0, P.bins["energy"], P.var_table["energy"])
+
+        def fn():
+            x = xe
+            if a.kernel != "vpf_en":
+                _, x = ops.vp_fused(x, V.dp, le, embed=emb_p)
+            if a.kernel != "vpf_dp":
+                ops.vp_fused(x, V.energy, le, embed=emb_e)
     else:
         raise SystemExit(f"unknown kernel {a.kernel}")
+    flush_buf = torch.empty(a.flush << 18, device=dev, dtype=torch.float32) if a.flush else None
+    if flush_buf is not None:
+        fn0 = fn
+
+        def fn():
+            flush_buf.zero_()
+            fn0()
     if a.time:
         # the reps are captured as one HIP graph and replayed: small launches are host-bound when
         # issued from Python one by one (~15 us of ctypes / allocator work per call)
@@ -191,7 +213,24 @@ def main():
                 gr.replay()
             e1.record(s)
             e1.synchronize()
-        print(f"{a.kernel}: {e0.elapsed_time(e1) * 1e3 / (3 * a.reps):.2f} us/launch (graph)")
+        t = e0.elapsed_time(e1) * 1e3 / (3 * a.reps)
+        if flush_buf is not None:  # the flush alone, to subtract
+            with torch.cuda.stream(s):
+                gf = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gf, stream=s):
+                    for _ in range(a.reps):
+                        flush_buf.zero_()
+                gf.replay()
+                torch.cuda.synchronize(dev)
+                e0.record(s)
+                for _ in range(3):
+                    gf.replay()
+                e1.record(s)
+                e1.synchronize()
+            tf = e0.elapsed_time(e1) * 1e3 / (3 * a.reps)
+            print(f"{a.kernel}: {t - tf:.2f} us/launch (graph, after a {a.flush} MB flush: {t:.2f} - {tf:.2f})")
+            return
+        print(f"{a.kernel}: {t:.2f} us/launch (graph)")
         return
     for _ in range(a.reps):
         fn()
