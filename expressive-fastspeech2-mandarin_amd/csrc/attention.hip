@@ -522,7 +522,7 @@ __device__ __forceinline__ int kv32_swz(int row) { return ((row & 3) << 2) | ((r
 __device__ __forceinline__ int kv32_off(int row, int chunk) { return row * 256 + ((chunk ^ kv32_swz(row)) << 4); }
 
 template <int NWV, int NST>
-__global__ __launch_bounds__(64 * NWV, 2) void attn32_kernel(const bf16 *__restrict__ qkv, int64_t qs, uint32_t qkv_bytes,
+__global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *__restrict__ qkv, int64_t qs, uint32_t qkv_bytes,
                                                              const int64_t *__restrict__ lens, int B, int T, int H, int nqt,
                                                              float scale_log2, bf16 *__restrict__ out, int64_t os,
                                                              const int32_t *__restrict__ cu, float *__restrict__ lse) {
@@ -747,12 +747,27 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
       const char *e = getenv("FS2_ATTN32");
       return (e != nullptr && e[0] == '0') ? 0 : 1;
     }();
-    if (T > 64 && use32) {
+    static const int form32 = [] {  // A/B: 4x2 (default), 8x2, 8x3 = waves x K/V ring stages
+      const char *e = getenv("FS2_ATTN32_FORM");
+      return e == nullptr ? 0 : (e[0] == '8' && e[2] == '3') ? 2 : (e[0] == '8') ? 1 : 0;
+    }();
+    if (T > 64 && use32 && form32 == 0) {
       // 4 waves x 32 queries, two workgroups per CU (2 x 64 KiB of K / V ring)
       const int nqt = (T + 127) / 128;
       hipLaunchKernelGGL((attn32_kernel<4, 2>), dim3(nqt * H * B), dim3(256), 0, s,
                          reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
                          scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse);
+    } else if (T > 64 && use32) {
+      // 8 waves x 32 queries: each K / V tile serves 256 queries (half the K / V traffic per query)
+      const int nqt = (T + 255) / 256;
+      if (form32 == 1)
+        hipLaunchKernelGGL((attn32_kernel<8, 2>), dim3(nqt * H * B), dim3(512), 0, s,
+                           reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
+                           scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse);
+      else
+        hipLaunchKernelGGL((attn32_kernel<8, 3>), dim3(nqt * H * B), dim3(512), 0, s,
+                           reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
+                           scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse);
     } else if (T > 64) {
       const int nqt = (T + 127) / 128;
       hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), dim3(nqt * H * B), dim3(512), 0, s,

@@ -27,6 +27,7 @@
 // MFMAs. GEMM1 needs no barrier at all; two per chunk hand the hidden slice H over. LDS holds the
 // x tile (60 KiB), H (56 KiB) and b1; the LN epilogue reuses it. A fragment whose shifted row
 // leaves its sequence reads a 16-byte zero slot instead (address select, no branch).
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -57,6 +58,7 @@ struct FfnArgs {
   int ntiles;          // row tiles of the launch
   int *cnt;            // [tiles] arrival counters (zero between launches)
   void *part;          // f32 partial Y^T accumulators, part_bytes(MB) per (tile, split)
+  int acquire;         // agent acquire before the partial loads (FS2_FFN_ACQUIRE=1; off: sc1 hand-off)
   uint32_t part_bytes;
   // the NEXT FFT block's Q|K|V projection of y (optional): qkv[m, :] = y[m, :] . wq^T + bq
   const bf16 *wq;      // [nq][256] in fragment order [nq/64][8][4][4][16][8]
@@ -570,7 +572,13 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       const int last = old == S - 1;
       if (last) {
         __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset for the next launch
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // no acquire (an L1 invalidate, ~1.7 us): every byte handed off is stored AND loaded with
+        // 16-byte sc1 buffer ops (L1 bypassed both ways), each storing wave drained vmcnt before the
+        // barrier behind which one lane adds, the last adder is told by its add's return value and
+        // the other waves load behind the barrier it joins, one workgroup per CU -- the measured
+        // sc1 hand-off of MI355X_MICROARCH.md (inter-workgroup visibility, first row).
+        // FS2_FFN_ACQUIRE=1 restores the fence (A/B).
+        if (p.acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
       *flag = last;
     }
@@ -971,6 +979,11 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   int nwg = ntiles;
   p.nsplit = S;
   p.ntiles = ntiles;
+  static const int acquire = [] {
+    const char *e = getenv("FS2_FFN_ACQUIRE");
+    return (e != nullptr && e[0] == '1') ? 1 : 0;
+  }();
+  p.acquire = acquire;
   if (S > 1) {
     if (d->splitk_ws == nullptr || ntiles > 1024 ||
         d->splitk_ws_bytes < 4096 + (int64_t)ntiles * S * kPartBytes || (int64_t)ntiles * S * kPartBytes >= (1LL << 31))

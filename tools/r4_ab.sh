@@ -17,4 +17,9 @@ for pf in 1 0; do for k in vpf_dp vpf_en; do for fl in 0 512; do
   FS2_VP_PREFETCH=$pf timeout -k 10 120 python tools/kernel_probe.py $k --time --reps 10 --flush $fl >> $O/vp_time.log 2>&1 || { tail -5 $O/vp_time.log; exit 1; }
   echo "prefetch=$pf $(tail -1 $O/vp_time.log)"
 done; done; done
+bash tools/ffn_abl.sh $TAG || exit 1
+for v in 0 1 0 1; do
+  FS2_FFN_ACQUIRE=$v timeout -k 10 120 python tools/kernel_probe.py enc_ffn --time >> $O/enc_ffn_time.log 2>&1 || { tail -5 $O/enc_ffn_time.log; exit 1; }
+  echo "ffn_acquire=$v $(tail -1 $O/enc_ffn_time.log)"
+done
 bash tools/prof_voc.sh $TAG && bash tools/fwd_trace.sh $TAG
