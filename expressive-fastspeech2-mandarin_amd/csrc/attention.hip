@@ -521,11 +521,16 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ int kv32_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 __device__ __forceinline__ int kv32_off(int row, int chunk) { return row * 256 + ((chunk ^ kv32_swz(row)) << 4); }
 
+__device__ __forceinline__ rsrc_t make_rsrc_any(const void *p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+
 template <int NWV, int NST>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *__restrict__ qkv, int64_t qs, uint32_t qkv_bytes,
                                                              const int64_t *__restrict__ lens, int B, int T, int H, int nqt,
                                                              float scale_log2, bf16 *__restrict__ out, int64_t os,
-                                                             const int32_t *__restrict__ cu, float *__restrict__ lse) {
+                                                             const int32_t *__restrict__ cu, float *__restrict__ lse,
+                                                             int oflags) {
   constexpr int KTT = 64;
   constexpr int QTW = 32 * NWV;       // queries per workgroup
   constexpr int PPW = KTT / 4 / NWV;  // K (and V) 1 KiB pieces per wave per tile
@@ -703,10 +708,46 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
     auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
     l_run = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
   }
-  if (active && qrow < T) {
-    const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
-    if (lse != nullptr && hh == 0)
-      lse[((int64_t)seq_base + qrow) * H + h] = l_run > 0.f ? m_run * scale_log2 + __log2f(l_run) : INFINITY;
+  const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
+  if (active && qrow < T && lse != nullptr && hh == 0)
+    lse[((int64_t)seq_base + qrow) * H + h] = l_run > 0.f ? m_run * scale_log2 + __log2f(l_run) : INFINITY;
+  const rsrc_t orsrc = make_rsrc_any(out, 0x7fffffffu);  // wave-uniform base, per-lane offsets
+  if (oflags & 2) {
+    // O staged through LDS (the K / V ring is free once every wave has passed this barrier) and
+    // stored as whole 256-byte rows, 16 bytes a lane (a lane's own 8-byte pieces of one row per
+    // store touched 32 rows per instruction: the store tail was issue-bound). Wave w's 32 x 128
+    // tile at w * 8 KiB, 16-byte chunk XOR (row & 15): the column writes 2-way, the row reads
+    // conflict-free.
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    char *ob = smem + w * (32 * 256);
+    if (active) {
+#pragma unroll
+      for (int db = 0; db < DK / 32; ++db)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          bf16x4 o = {(bf16)(oacc[db][4 * r4] * inv), (bf16)(oacc[db][4 * r4 + 1] * inv),
+                      (bf16)(oacc[db][4 * r4 + 2] * inv), (bf16)(oacc[db][4 * r4 + 3] * inv)};
+          *reinterpret_cast<bf16x4 *>(ob + r32 * 256 + (((4 * db + r4) ^ (r32 & 15)) << 4) + 8 * hh) = o;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile written (same-wave reads follow)
+      const int ch = lane & 15;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = (lane >> 4) + 4 * i, q = q0 + 32 * w + row;
+        const uint4 v = *reinterpret_cast<const uint4 *>(ob + row * 256 + ((ch ^ (row & 15)) << 4));
+        if (q < T) {
+          const uint32_t off = (uint32_t)(((int64_t)seq_base + q) * os + h * DK + ch * 8) * 2u;
+          if (oflags & 1)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                                   orsrc, off, 0, 16);
+          else
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                                   orsrc, off, 0, 0);
+        }
+      }
+    }
+  } else if (active && qrow < T) {
     bf16 *orow = out + ((int64_t)seq_base + qrow) * os + h * DK + 4 * hh;
 #pragma unroll
     for (int db = 0; db < DK / 32; ++db)
@@ -714,7 +755,11 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
       for (int r4 = 0; r4 < 4; ++r4) {
         bf16x4 o = {(bf16)(oacc[db][4 * r4] * inv), (bf16)(oacc[db][4 * r4 + 1] * inv),
                     (bf16)(oacc[db][4 * r4 + 2] * inv), (bf16)(oacc[db][4 * r4 + 3] * inv)};
-        *reinterpret_cast<bf16x4 *>(orow + 32 * db + 8 * r4) = o;
+        if (oflags & 1)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, o), orsrc,
+                                                (uint32_t)((orow - out) + 32 * db + 8 * r4) * 2u, 0, 16);
+        else
+          *reinterpret_cast<bf16x4 *>(orow + 32 * db + 8 * r4) = o;
       }
   }
 }
@@ -747,6 +792,12 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
       const char *e = getenv("FS2_ATTN32");
       return (e != nullptr && e[0] == '0') ? 0 : 1;
     }();
+    // output stores: bit 0 write-through (FS2_OUT_SC1=1, A/B), bit 1 rows staged through LDS
+    // (FS2_ATTN_OSTAGE=0 stores a lane's 8-byte pieces directly, A/B)
+    static const int oflags = [] {
+      const char *e = getenv("FS2_OUT_SC1"), *f = getenv("FS2_ATTN_OSTAGE");
+      return ((e != nullptr && e[0] == '1') ? 1 : 0) | ((f != nullptr && f[0] == '0') ? 0 : 2);
+    }();
     static const int form32 = [] {  // A/B: 4x2 (default), 8x2, 8x3 = waves x K/V ring stages
       const char *e = getenv("FS2_ATTN32_FORM");
       return e == nullptr ? 0 : (e[0] == '8' && e[2] == '3') ? 2 : (e[0] == '8') ? 1 : 0;
@@ -756,18 +807,18 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
       const int nqt = (T + 127) / 128;
       hipLaunchKernelGGL((attn32_kernel<4, 2>), dim3(nqt * H * B), dim3(256), 0, s,
                          reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
-                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse);
+                         scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse, oflags);
     } else if (T > 64 && use32) {
       // 8 waves x 32 queries: each K / V tile serves 256 queries (half the K / V traffic per query)
       const int nqt = (T + 255) / 256;
       if (form32 == 1)
         hipLaunchKernelGGL((attn32_kernel<8, 2>), dim3(nqt * H * B), dim3(512), 0, s,
                            reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
-                           scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse);
+                           scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse, oflags);
       else
         hipLaunchKernelGGL((attn32_kernel<8, 3>), dim3(nqt * H * B), dim3(512), 0, s,
                            reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H, nqt,
-                           scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse);
+                           scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse, oflags);
     } else if (T > 64) {
       const int nqt = (T + 127) / 128;
       hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), dim3(nqt * H * B), dim3(512), 0, s,

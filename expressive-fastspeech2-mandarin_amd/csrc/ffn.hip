@@ -59,6 +59,7 @@ struct FfnArgs {
   int *cnt;            // [tiles] arrival counters (zero between launches)
   void *part;          // f32 partial Y^T accumulators, part_bytes(MB) per (tile, split)
   int acquire;         // agent acquire before the partial loads (FS2_FFN_ACQUIRE=1; off: sc1 hand-off)
+  int out_sc1;         // A/B (FS2_OUT_SC1=1): output rows stored write-through (sc1), no dirty L2 lines at kernel end
   uint32_t part_bytes;
   // the NEXT FFT block's Q|K|V projection of y (optional): qkv[m, :] = y[m, :] . wq^T + bq
   const bf16 *wq;      // [nq][256] in fragment order [nq/64][8][4][4][16][8]
@@ -774,9 +775,14 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
 #pragma unroll 2
     for (int i = tid; i < BM * 32; i += 256) {
       const int m = i >> 5, ch = i & 31;
-      if (m0 + m < M)
-        *reinterpret_cast<uint4 *>(ob + (size_t)(m0 + m) * orow + ch * 16) =
-            *reinterpret_cast<const uint4 *>(smem + H_OFF + m * 512 + (xchunk(m, ch) << 4));
+      if (m0 + m < M) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(smem + H_OFF + m * 512 + (xchunk(m, ch) << 4));
+        if (p.out_sc1)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                                 make_rsrc(ob, 0x7fffffffu), (uint32_t)((m0 + m) * orow + ch * 16), 0, 16);
+        else
+          *reinterpret_cast<uint4 *>(ob + (size_t)(m0 + m) * orow + ch * 16) = v;
+      }
     }
     // ---- the next block's Q|K|V projection (transformer/SubLayers.py:39-41 of block i+1) while
     // y is still on chip: GEMM3 Q|K|V^T[n, m] = sum_c Wq[n, c] . y[m, c] in passes of 256 output
@@ -856,9 +862,15 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
 #pragma unroll 2
         for (int i = tid; i < BM * 32; i += 256) {
           const int m = i >> 5, ch = i & 31;
-          if (m0 + m < M)
-            *reinterpret_cast<uint4 *>(qb + (size_t)(m0 + m) * qrow + ps * 512 + ch * 16) =
-                *reinterpret_cast<const uint4 *>(smem + X_OFF + m * SPITCH + ch * 16);
+          if (m0 + m < M) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(smem + X_OFF + m * SPITCH + ch * 16);
+            if (p.out_sc1)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                                     make_rsrc(qb, 0x7fffffffu),
+                                                     (uint32_t)((m0 + m) * qrow + ps * 512 + ch * 16), 0, 16);
+            else
+              *reinterpret_cast<uint4 *>(qb + (size_t)(m0 + m) * qrow + ps * 512 + ch * 16) = v;
+          }
         }
         lbar();  // the staging region is rewritten by the next pass
       }
@@ -984,6 +996,11 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
     return (e != nullptr && e[0] == '1') ? 1 : 0;
   }();
   p.acquire = acquire;
+  static const int out_sc1 = [] {
+    const char *e = getenv("FS2_OUT_SC1");
+    return (e != nullptr && e[0] == '1') ? 1 : 0;
+  }();
+  p.out_sc1 = out_sc1;
   if (S > 1) {
     if (d->splitk_ws == nullptr || ntiles > 1024 ||
         d->splitk_ws_bytes < 4096 + (int64_t)ntiles * S * kPartBytes || (int64_t)ntiles * S * kPartBytes >= (1LL << 31))
