@@ -445,26 +445,14 @@ def timed_steps(model, batch, device, steps, warmup, graph, frames_out=None):
             for _ in range(2):
                 step()
         torch.cuda.current_stream(device).wait_stream(s)
-        # two instances of the captured forward, replayed alternately: HIP serialises a graph
-        # launch behind the previous launch of the SAME executable graph (its kernel arguments are
-        # rewritten), which left the GPU idle for the host's enqueue of every step (~45 us); with two
-        # instances the next step is queued while the current one runs. Each replay is one full
-        # forward over the batch.
-        gs = []
-        for _ in range(2):
-            g = torch.cuda.CUDAGraph()
-            # captured on the warm-up stream: its split-K workspace already exists, so the graph
-            # holds no counter-zeroing memset (ops.splitk_workspace is per stream)
-            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                out = step()
-            g.replay()
-            gs.append(g)
+        g = torch.cuda.CUDAGraph()
+        # captured on the warm-up stream: its split-K workspace already exists, so the graph holds
+        # no counter-zeroing memset (ops.splitk_workspace is per stream)
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+            out = step()
+        g.replay()
         torch.cuda.synchronize(device)
-        it = [0]
-
-        def run():
-            gs[it[0] & 1].replay()
-            it[0] += 1
+        run = g.replay
     if frames_out is not None:
         frames_out.append(int(out[9].sum()))
     parallel.barrier()

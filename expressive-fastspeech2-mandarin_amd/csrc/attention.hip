@@ -792,15 +792,17 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
       const char *e = getenv("FS2_ATTN32");
       return (e != nullptr && e[0] == '0') ? 0 : 1;
     }();
-    // output stores: bit 0 write-through (FS2_OUT_SC1=1, A/B), bit 1 rows staged through LDS
-    // (FS2_ATTN_OSTAGE=0 stores a lane's 8-byte pieces directly, A/B)
+    // output stores: bit 0 write-through (sc1: the lines leave L2; FS2_OUT_SC1=0 plain, A/B), bit 1
+    // rows staged through LDS (FS2_ATTN_OSTAGE=0 stores a lane's 8-byte pieces directly, A/B)
     static const int oflags = [] {
       const char *e = getenv("FS2_OUT_SC1"), *f = getenv("FS2_ATTN_OSTAGE");
-      return ((e != nullptr && e[0] == '1') ? 1 : 0) | ((f != nullptr && f[0] == '0') ? 0 : 2);
+      return ((e != nullptr && e[0] == '0') ? 0 : 1) | ((f != nullptr && f[0] == '0') ? 0 : 2);
     }();
-    static const int form32 = [] {  // A/B: 4x2 (default), 8x2, 8x3 = waves x K/V ring stages
+    // waves x K/V ring stages: 8x2 (default: 24.1 us at the cfg2 decoder shape), 4x2 (25.3),
+    // 8x3 (25.4-26.2); FS2_ATTN32_FORM for A/B
+    static const int form32 = [] {
       const char *e = getenv("FS2_ATTN32_FORM");
-      return e == nullptr ? 0 : (e[0] == '8' && e[2] == '3') ? 2 : (e[0] == '8') ? 1 : 0;
+      return e == nullptr ? 1 : (e[0] == '8' && e[2] == '3') ? 2 : (e[0] == '8') ? 1 : 0;
     }();
     if (T > 64 && use32 && form32 == 0) {
       // 4 waves x 32 queries, two workgroups per CU (2 x 64 KiB of K / V ring)

@@ -59,7 +59,7 @@ struct FfnArgs {
   int *cnt;            // [tiles] arrival counters (zero between launches)
   void *part;          // f32 partial Y^T accumulators, part_bytes(MB) per (tile, split)
   int acquire;         // agent acquire before the partial loads (FS2_FFN_ACQUIRE=1; off: sc1 hand-off)
-  int out_sc1;         // A/B (FS2_OUT_SC1=1): output rows stored write-through (sc1), no dirty L2 lines at kernel end
+  int out_sc1;         // output rows stored write-through (sc1): the lines leave L2 (FS2_OUT_SC1=0: plain, A/B)
   uint32_t part_bytes;
   // the NEXT FFT block's Q|K|V projection of y (optional): qkv[m, :] = y[m, :] . wq^T + bq
   const bf16 *wq;      // [nq][256] in fragment order [nq/64][8][4][4][16][8]
@@ -998,7 +998,7 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   p.acquire = acquire;
   static const int out_sc1 = [] {
     const char *e = getenv("FS2_OUT_SC1");
-    return (e != nullptr && e[0] == '1') ? 1 : 0;
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
   }();
   p.out_sc1 = out_sc1;
   if (S > 1) {

@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
-"""One graph-replayed forward from a rocprofv3 kernel trace: kernels in order, duration, gap to
-the previous kernel's end (us), averaged over the last N forwards (forward = cond_kernel .. next).
+"""Graph-replayed forwards from a rocprofv3 kernel trace of bench.py: kernels in order, duration,
+gap to the previous kernel's end (us), averaged over the timed graph replays.
+
+A forward starts at its two length-mask launches. The bench's trace also holds eager forwards
+(warm-up, and the roofline's HIP-event-timed forwards, whose host-bound launches leave gaps); the
+graph replays are the forwards with (almost) no internal gaps, so those are the ones averaged.
 
     python tools/fwd_gaps.py gpurun_out/trace/t/bench_kernel_trace.csv [--min-gap 1]
 """
@@ -9,11 +13,19 @@ import re
 import sys
 
 
+def forwards(rows):
+    st = [i for i, r in enumerate(rows) if "length_mask" in r["Kernel_Name"] and i + 1 < len(rows)
+          and "length_mask" in rows[i + 1]["Kernel_Name"]]
+    return [rows[a:b] for a, b in zip(st, st[1:])]
+
+
 def main(path, min_gap=0.0):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    st = [i for i, r in enumerate(rows) if "cond_kernel" in r["Kernel_Name"]]
-    segs = [rows[a:b] for a, b in zip(st[-11:-1], st[-10:])]
-    n = len(segs[0])
+    fw = forwards(rows)
+    n = max(set(len(f) for f in fw), key=lambda k: sum(len(f) == k for f in fw))  # the usual launch count
+    inner = lambda f: sum(int(f[i]["Start_Timestamp"]) - int(f[i - 1]["End_Timestamp"]) for i in range(1, len(f))) / 1e3
+    graphed = [f for f in fw if len(f) == n and inner(f) < 5.0]
+    segs = graphed[-8:] if graphed else [f for f in fw if len(f) == n][-8:]
     tot_d = tot_g = 0.0
     for i in range(n):
         d = sum(int(s[i]["End_Timestamp"]) - int(s[i]["Start_Timestamp"]) for s in segs) / len(segs) / 1e3
@@ -24,7 +36,9 @@ def main(path, min_gap=0.0):
         if g >= min_gap:
             name = re.sub(r"^_ZN12_GLOBAL__N_1\d+", "", r["Kernel_Name"])[:40]
             print(f"{i:3d} {name:40s} {int(r['Grid_Size_X']) // int(r['Workgroup_Size_X']):6d} {d:8.1f} gap {g:5.1f}")
-    print(f"kernels {n}: busy {tot_d:.1f} us, gaps {tot_g:.1f} us")
+    walls = [(int(f[-1]["End_Timestamp"]) - int(f[0]["Start_Timestamp"])) / 1e3 for f in segs]
+    print(f"kernels {n}: busy {tot_d:.1f} us, gaps {tot_g:.1f} us; {len(segs)} graph-replayed forwards averaged "
+          f"(wall {min(walls):.1f}..{max(walls):.1f} us)")
 
 
 if __name__ == "__main__":
