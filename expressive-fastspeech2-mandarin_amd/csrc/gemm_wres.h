@@ -15,6 +15,7 @@ struct WresArgs {
   int relu;               // 0: y = acc + bias, 1: relu(acc + bias)
   int out_f32;            // f32 output (16-byte stores) instead of bf16
   uint32_t x_bytes, w_bytes;
+  int out_sc1;            // set by wres_launch: write-through bf16 stores (conv_common.h env_out_sc1)
 };
 
 // true when the launch was taken (shape / dtype covered); the caller falls back otherwise

@@ -11,6 +11,8 @@
 // epilogue stores straight from registers (8-byte bf16x4 per lane, no LDS round trip).
 // Grid: (N / 128) column slices x (CUs / slices) row workers, one workgroup per CU; the slices of
 // one worker are adjacent after the XCD remap, so they share its A rows through one L2.
+#include <cstdlib>
+
 #include "gemm_wres.h"
 
 namespace {
@@ -196,6 +198,11 @@ __global__ __launch_bounds__(512, 1) void gemm_wres_kernel(WresArgs a, int nslic
         if (m < M) {
           if (a.out_f32)
             *reinterpret_cast<float4 *>(reinterpret_cast<float *>(a.out) + o) = make_float4(v[0], v[1], v[2], v[3]);
+          else if (a.out_sc1)
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
+                                   bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]}),
+                __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, 0x7fffffff, 0x00020000), (uint32_t)o * 2u, 0, 16);
           else
             *reinterpret_cast<bf16x4 *>(out + o) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         }
@@ -215,11 +222,17 @@ bool wres_launch(const WresArgs &a, int num_cus, hipStream_t s) {
   if (nslice > num_cus) return false;
   const int workers = num_cus / nslice;
   const dim3 grid(nslice * workers), block(512);
+  WresArgs b = a;
+  static const int out_sc1 = [] {  // as conv_common.h env_out_sc1: FS2_OUT_SC1=0 -> plain stores
+    const char *e = getenv("FS2_OUT_SC1");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+  }();
+  b.out_sc1 = out_sc1;
   switch (a.K / 64) {
-    case 1: hipLaunchKernelGGL(gemm_wres_kernel<1>, grid, block, 0, s, a, nslice, workers); break;
-    case 2: hipLaunchKernelGGL(gemm_wres_kernel<2>, grid, block, 0, s, a, nslice, workers); break;
-    case 3: hipLaunchKernelGGL(gemm_wres_kernel<3>, grid, block, 0, s, a, nslice, workers); break;
-    default: hipLaunchKernelGGL(gemm_wres_kernel<4>, grid, block, 0, s, a, nslice, workers); break;
+    case 1: hipLaunchKernelGGL(gemm_wres_kernel<1>, grid, block, 0, s, b, nslice, workers); break;
+    case 2: hipLaunchKernelGGL(gemm_wres_kernel<2>, grid, block, 0, s, b, nslice, workers); break;
+    case 3: hipLaunchKernelGGL(gemm_wres_kernel<3>, grid, block, 0, s, b, nslice, workers); break;
+    default: hipLaunchKernelGGL(gemm_wres_kernel<4>, grid, block, 0, s, b, nslice, workers); break;
   }
   return true;
 }

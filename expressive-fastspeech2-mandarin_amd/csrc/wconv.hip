@@ -38,6 +38,7 @@ struct WconvArgs {
   uint32_t x_bytes, w_bytes;
   const int2 *row_pos;     // packed rows: {frame, length} per row (NULL: padded [B, T] rows)
   const int32_t *rows_dev; // packed rows: the active row count (device)
+  int out_sc1;             // write-through output rows (conv_common.h store16_out)
 };
 
 // position and length of row m's sequence: packed rows from row_pos, padded rows t = m mod T
@@ -269,8 +270,8 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
   for (int i = tid; i < BM * CPR; i += NT) {
     const int m = i / CPR, ch = i - m * CPR;
     if (m0 + m < M)
-      *reinterpret_cast<uint4 *>(ob + (size_t)(m0 + m) * orow + ch * 16) =
-          *reinterpret_cast<const uint4 *>(smem + X_OFF + m * OPITCH + ch * 16);
+      store16_out(ob, (uint32_t)(m0 + m) * orow + (uint32_t)ch * 16u,
+                  *reinterpret_cast<const uint4 *>(smem + X_OFF + m * OPITCH + ch * 16), p.out_sc1);
   }
 }
 
@@ -293,6 +294,7 @@ struct PnHeadArgs {
   uint32_t x_bytes, w1_bytes, w2_bytes;
   const int2 *row_pos;
   const int32_t *rows_dev;
+  int out_sc1;
 };
 
 __global__ __launch_bounds__(512, 1) void pn_head_kernel(PnHeadArgs p) {
@@ -518,8 +520,8 @@ __global__ __launch_bounds__(512, 1) void pn_head_kernel(PnHeadArgs p) {
   for (int i = tid; i < BM * CPR; i += NT) {
     const int m = i / CPR, ch = i - m * CPR;
     if (m0 + m < M)
-      *reinterpret_cast<uint4 *>(ob + (size_t)(m0 + m) * orow + ch * 16) =
-          *reinterpret_cast<const uint4 *>(smem + Y_OFF + m * OPITCH + ch * 16);
+      store16_out(ob, (uint32_t)(m0 + m) * orow + (uint32_t)ch * 16u,
+                  *reinterpret_cast<const uint4 *>(smem + Y_OFF + m * OPITCH + ch * 16), p.out_sc1);
   }
 }
 
@@ -761,6 +763,7 @@ extern "C" int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream) {
   p.row_pos = row_pos;
   p.rows_dev = d->rows_dev;
   p.M = (int)Mg;
+  p.out_sc1 = env_out_sc1();
   const int nwg = (int)((Mg + 111) / 112);
 #ifndef WCONV_WQ
 #define WCONV_WQ 1  // 8 waves x 64 columns (2 quads per wave: 224 accumulators + the ring spill; analysis only)
@@ -785,6 +788,7 @@ extern "C" int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream) {
     q.w2_bytes = (uint32_t)(fs2_wconv_weight_elems(d->KS, 512, 512) * 2);
     q.row_pos = row_pos;
     q.rows_dev = d->rows_dev;
+    q.out_sc1 = env_out_sc1();
     hipLaunchKernelGGL(pn_head_kernel, dim3(nwg), dim3(512), 0, as_stream(stream), q);
   } else if (d->Cin == 80)
     hipLaunchKernelGGL((wconv_kernel<5, 80, 1>), dim3(nwg), dim3(512), 0, as_stream(stream), p);
