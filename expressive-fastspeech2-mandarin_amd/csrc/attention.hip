@@ -798,14 +798,14 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
       const char *e = getenv("FS2_OUT_SC1"), *f = getenv("FS2_ATTN_OSTAGE");
       return ((e != nullptr && e[0] == '0') ? 0 : 1) | ((f != nullptr && f[0] == '0') ? 0 : 2);
     }();
-    // waves x K/V ring stages: 8x2 for long sequences (T >= 384: 24.1 us at the cfg2 decoder shape
-    // vs 25.3 for 4x2, 25.4-26.2 for 8x3), 4x2 below (a 256-query tile would leave most sequences
-    // one workgroup per head and half the chip idle); FS2_ATTN32_FORM forces one (A/B)
-    static const int form_env = [] {
+    // waves x K/V ring stages: 4x2. 8x2 (FS2_ATTN32_FORM=8x2) is 1.2 us faster at the cfg2 decoder
+    // shape (24.1 vs 25.3 us) but with a long max length over short sequences (free-running cfg2:
+    // T 960, mean 174 frames) its 256-query tiles leave most (utterance, head) pairs ONE workgroup
+    // and the forward ~0.1 ms slower; the host knows only T here. 8x3: 25.4-26.2 us.
+    static const int form32 = [] {
       const char *e = getenv("FS2_ATTN32_FORM");
-      return e == nullptr ? -1 : (e[0] == '8' && e[2] == '3') ? 2 : (e[0] == '8') ? 1 : 0;
+      return e == nullptr ? 0 : (e[0] == '8' && e[2] == '3') ? 2 : (e[0] == '8') ? 1 : 0;
     }();
-    const int form32 = form_env >= 0 ? form_env : (T >= 384 ? 1 : 0);
     if (T > 64 && use32 && form32 == 0) {
       // 4 waves x 32 queries, two workgroups per CU (2 x 64 KiB of K / V ring)
       const int nqt = (T + 127) / 128;
