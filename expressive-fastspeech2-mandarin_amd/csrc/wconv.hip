@@ -549,35 +549,28 @@ struct PnTailArgs {
   const int32_t *rows_dev;
 };
 
-// NWT = 4: 4 waves x (2 row blocks x 5 column blocks). NWT = 8 (FS2_PN_TAIL8): the same tile with
-// two waves per SIMD -- wave w and w + 4 share row blocks 2 (w & 3), +1 and split the 5 column
-// blocks 3 + 2, so one wave's LDS / barrier latency hides behind the other's MFMAs (the B fragments
-// are read twice; only waves 0-3 issue the weight DMA, the others' vmcnt waits are no-ops).
-template <int NWT>
-__global__ __launch_bounds__(64 * NWT, 1) void pn_tail_kernel(PnTailArgs p) {
-  constexpr int KS = 5, CIN = 512, NB = 5, NCOL = 80, BM = 112, NST = 3, KPS = 2, NT = 64 * NWT;
+__global__ __launch_bounds__(256, 1) void pn_tail_kernel(PnTailArgs p) {
+  constexpr int KS = 5, CIN = 512, NB = 5, NCOL = 80, BM = 112, NST = 3, KPS = 2;
   constexpr int XR = BM + KS - 1;
   constexpr int XPITCH = CIN * 2 + 32;
   constexpr int XPIECES = (XR * XPITCH + 1023) / 1024;
-  constexpr int XPW = (XPIECES + NWT - 1) / NWT;
+  constexpr int XPW = (XPIECES + 3) / 4;
   constexpr int NKS = CIN / 32, NU = KS * NKS;  // 16 k-steps per tap, 80 in all
   constexpr int NS = NU / KPS;                  // ring stages of 2 k-steps
-  constexpr int PPS = 12;                       // 10 weight pieces + 2 dummies: waves 0-3 issue 3
+  constexpr int PPS = 12;                       // 10 weight pieces + 2 dummies: every wave issues 3
   constexpr int STG = PPS * 1024;
   constexpr int ZBYTES = NKS * 64;
   constexpr int X_OFF = ZBYTES;
-  constexpr int W_OFF = X_OFF + NWT * XPW * 1024;
+  constexpr int W_OFF = X_OFF + 4 * XPW * 1024;
   constexpr int B_OFF = W_OFF + NST * STG;
   constexpr int SMEM = B_OFF + NCOL * 4;
   constexpr int OPITCH = NCOL * 4 + 16;         // f32 staging (in the x region)
-  constexpr int NBW = NWT == 4 ? NB : 3;        // column blocks per wave (waves >= 4: the other 2)
-  static_assert(BM * OPITCH <= NWT * XPW * 1024, "staging fits the x region");
+  static_assert(BM * OPITCH <= 4 * XPW * 1024, "staging fits the x region");
   static_assert(SMEM <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w & 3;                          // row-block pair 2 wr, 2 wr + 1
   const int M = p.rows_dev != nullptr ? min(*p.rows_dev, p.M) : p.M, T = p.T, pad = p.pad;
   const int m0 = blockIdx.x * BM;
   if (m0 >= M) return;
@@ -585,7 +578,7 @@ __global__ __launch_bounds__(64 * NWT, 1) void pn_tail_kernel(PnTailArgs p) {
   int vm[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int rb = 2 * wr + j;
+    const int rb = 2 * w + j;
     const int m = m0 + rb * 16 + hrow0;
     int v = 0;
     if (rb * 16 < BM && m < M) {
@@ -596,15 +589,15 @@ __global__ __launch_bounds__(64 * NWT, 1) void pn_tail_kernel(PnTailArgs p) {
     }
     vm[j] = v;
   }
-  for (int i = tid; i < ZBYTES / 16; i += NT) *reinterpret_cast<float4 *>(smem + 16 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = tid; i < ZBYTES / 16; i += 256) *reinterpret_cast<float4 *>(smem + 16 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
   if (tid < NCOL / 4)
     *reinterpret_cast<float4 *>(smem + B_OFF + 16 * tid) = reinterpret_cast<const float4 *>(p.bias)[tid];
 
-  const rsrc_t xr = make_rsrc(p.x, p.x_bytes), wrs = make_rsrc(p.w, p.w_bytes);
+  const rsrc_t xr = make_rsrc(p.x, p.x_bytes), wr = make_rsrc(p.w, p.w_bytes);
   const uint32_t xrow = (uint32_t)p.xs * 2u;
 #pragma unroll
   for (int i = 0; i < XPW; ++i) {
-    const int pc = w + NWT * i;
+    const int pc = w + 4 * i;
     const int o = pc * 1024 + lane * 16;
     const int r = o / XPITCH, within = o - r * XPITCH;
     const int gm = m0 - pad + r;
@@ -612,59 +605,46 @@ __global__ __launch_bounds__(64 * NWT, 1) void pn_tail_kernel(PnTailArgs p) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)(smem + X_OFF + pc * 1024),
                                              16, ok ? (uint32_t)gm * xrow + (uint32_t)within : kOOB, 0, 0, 0);
   }
-  // stage s (k-steps 2s, 2s + 1) -> ring slot s % NST: wave w < 4 DMAs pieces w, w + 4, w + 8
-  // (pieces 10, 11: dummies, zeros)
-  auto wdma = [&](int st_idx) __attribute__((always_inline)) {
-    if (w >= 4) return;
+  // stage s (k-steps 2s, 2s + 1) -> ring slot s % NST: wave w DMAs pieces w, w + 4, w + 8 (pieces
+  // 10, 11: dummies, zeros)
+  auto wdma = [&](int st_idx) {
     char *st = smem + W_OFF + (st_idx % NST) * STG;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int pc = w + 4 * j;
       const uint32_t off = pc < KPS * NB ? (uint32_t)(st_idx * KPS * NB + pc) * 1024u + (uint32_t)lane * 16u : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (__attribute__((address_space(3))) void *)(st + pc * 1024), 16, off,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void *)(st + pc * 1024), 16, off,
                                                0, 0, 0);
     }
   };
 #pragma unroll
   for (int st = 0; st < NST - 1; ++st) wdma(st);
 
-  f32x4 acc[NBW][2];
+  f32x4 acc[NB][2];
 #pragma unroll
-  for (int b = 0; b < NBW; ++b) acc[b][0] = acc[b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // stage s: k-steps u = 2s + q (tap = u / 16): every fragment read first, then the MFMAs; columns
-  // blocks B0 .. B0 + NC - 1
-  auto stage = [&](int st_idx, auto B0T, auto NCT) __attribute__((always_inline)) {
-    constexpr int B0 = decltype(B0T)::value, NC = decltype(NCT)::value;
+  for (int b = 0; b < NB; ++b) acc[b][0] = acc[b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // stage s: k-steps u = 2s + q (tap = u / 16): every fragment read first, then the 20 MFMAs
+  auto stage = [&](int st_idx) {
     const char *st = smem + W_OFF + (st_idx % NST) * STG;
-    bf16x8 fa[KPS][NC], fb[KPS][2];
+    bf16x8 fa[KPS][NB], fb[KPS][2];
 #pragma unroll
     for (int q = 0; q < KPS; ++q) {
       const int u = st_idx * KPS + q, tap = u >> 4, ks = u & 15;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int ad = (X_OFF + ((2 * wr + j) * 16 + hrow0 + tap) * XPITCH + hi * 16) & __builtin_amdgcn_sbfe(vm[j], tap, 1);
+        const int ad = (X_OFF + ((2 * w + j) * 16 + hrow0 + tap) * XPITCH + hi * 16) & __builtin_amdgcn_sbfe(vm[j], tap, 1);
         fb[q][j] = *reinterpret_cast<const bf16x8 *>(smem + ad + ks * 64);
       }
 #pragma unroll
-      for (int b = 0; b < NC; ++b) fa[q][b] = *reinterpret_cast<const bf16x8 *>(st + (q * NB + B0 + b) * 1024 + lane * 16);
+      for (int b = 0; b < NB; ++b) fa[q][b] = *reinterpret_cast<const bf16x8 *>(st + (q * NB + b) * 1024 + lane * 16);
     }
 #pragma unroll
     for (int q = 0; q < KPS; ++q)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int b = 0; b < NC; ++b)
+        for (int b = 0; b < NB; ++b)
           acc[b][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q][b], fb[q][j], acc[b][j], 0, 0, 0);
-  };
-  auto run_stage = [&](int st_idx) __attribute__((always_inline)) {
-    if constexpr (NWT == 4) {
-      stage(st_idx, std::integral_constant<int, 0>{}, std::integral_constant<int, NB>{});
-    } else {
-      if (w < 4)
-        stage(st_idx, std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{});
-      else
-        stage(st_idx, std::integral_constant<int, 3>{}, std::integral_constant<int, 2>{});
-    }
   };
   // the x tile (issued first) and stage 0 landed; stage 1 may stay in flight
   asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
@@ -685,31 +665,28 @@ __global__ __launch_bounds__(64 * NWT, 1) void pn_tail_kernel(PnTailArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     if (st + NST - 1 < NS) wdma(st + NST - 1);
-    run_stage(st);
+    stage(st);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   __syncthreads();  // every wave is done with the x tile: it becomes the f32 staging tile
-  const int bw0 = (NWT == 8 && w >= 4) ? 3 : 0, nbw = (NWT == 8) ? (w >= 4 ? 2 : 3) : NB;
 #pragma unroll
-  for (int b = 0; b < NBW; ++b) {
-    if (b < nbw) {
-      const int n = (bw0 + b) * 16 + 4 * hi;
-      const float4 bb = *reinterpret_cast<const float4 *>(smem + B_OFF + 4 * n);
+  for (int b = 0; b < NB; ++b) {
+    const int n = b * 16 + 4 * hi;
+    const float4 bb = *reinterpret_cast<const float4 *>(smem + B_OFF + 4 * n);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = (2 * wr + j) * 16 + hrow0;
-        if (r < BM) {
-          const f32x4 v = acc[b][j];
-          *reinterpret_cast<float4 *>(smem + X_OFF + r * OPITCH + n * 4) =
-              make_float4(v[0] + bb.x, v[1] + bb.y, v[2] + bb.z, v[3] + bb.w);
-        }
+    for (int j = 0; j < 2; ++j) {
+      const int r = (2 * w + j) * 16 + hrow0;
+      if (r < BM) {
+        const f32x4 v = acc[b][j];
+        *reinterpret_cast<float4 *>(smem + X_OFF + r * OPITCH + n * 4) =
+            make_float4(v[0] + bb.x, v[1] + bb.y, v[2] + bb.z, v[3] + bb.w);
       }
     }
   }
   __syncthreads();
   constexpr int CPR = NCOL * 4 / 16;  // 20 16-byte chunks per row
-  for (int i = tid; i < BM * CPR; i += NT) {
+  for (int i = tid; i < BM * CPR; i += 256) {
     const int m = i / CPR, ch = i - m * CPR;
     if (m0 + m < M) {
       const float4 a = *reinterpret_cast<const float4 *>(smem + X_OFF + m * OPITCH + ch * 16);
@@ -766,14 +743,7 @@ extern "C" int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream) {
     q.row_pos = row_pos;
     q.rows_dev = d->rows_dev;
     q.M = (int)Mg;
-    static const int tail8 = [] {
-      const char *e = getenv("FS2_PN_TAIL8");
-      return (e != nullptr && e[0] == '1') ? 1 : 0;
-    }();
-    if (tail8)
-      hipLaunchKernelGGL(pn_tail_kernel<8>, dim3((unsigned)((Mg + 111) / 112)), dim3(512), 0, as_stream(stream), q);
-    else
-      hipLaunchKernelGGL(pn_tail_kernel<4>, dim3((unsigned)((Mg + 111) / 112)), dim3(256), 0, as_stream(stream), q);
+    hipLaunchKernelGGL(pn_tail_kernel, dim3((unsigned)((Mg + 111) / 112)), dim3(256), 0, as_stream(stream), q);
     FS2_CHECK_LAUNCH();
     return FS2_OK;
   }
