@@ -157,6 +157,7 @@ constexpr uint32_t kVpWaveBytes = (uint32_t)kVpUnits * kVpUnit;
 constexpr int kVpDepth = 4;               // k-steps in flight (8 units, 128 registers)
 constexpr int kVpLgkm0 = 0xC07F;          // s_waitcnt lgkmcnt(0) as a real wait-count instruction
 constexpr int kVpPrefetchMax = 20;        // warm-up loads per wave (x tile + ring + these < 64 in flight)
+constexpr int kVpScratchOff = 512 + 4 * ((((50 * 544 + 1023) / 1024) + 3) / 4) * 1024;  // = HHI_OFF
 
 struct VpArgs {
   const bf16 *x;
@@ -189,23 +190,19 @@ __device__ __forceinline__ void vp_static_for(Fn &&f) {
   vp_static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// NB2 = output row blocks per tile (2: 32 rows, the default; 4: 64 rows, FS2_VP_TILE=64 -- half the
-// workgroups, each weight stream serving twice the rows); conv1 runs on NB2 + 1 blocks (the halo)
-template <int NB2>
 __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
-  constexpr int NB1 = NB2 + 1, BMt = 16 * NB2, HRt = 16 * NB1, XRt = HRt + 2;
-  constexpr int XPIECES = (XRt * kVpPitch + 1023) / 1024;
+  constexpr int XPIECES = (kVpXR * kVpPitch + 1023) / 1024;
   constexpr int XPW = (XPIECES + 3) / 4;
   constexpr int ZERO_OFF = 0;  // 512 zero bytes: a masked tap's fragment address lands here
   constexpr int X_OFF = 512;
   constexpr int HHI_OFF = X_OFF + 4 * XPW * 1024;
-  constexpr int HLO_OFF = HHI_OFF + HRt * kVpPitch;
-  constexpr int VEC_OFF = HLO_OFF + HRt * kVpPitch;  // b1, g1, be1, b2, g2, be2, lin_w
+  constexpr int HLO_OFF = HHI_OFF + kVpHR * kVpPitch;
+  constexpr int VEC_OFF = HLO_OFF + kVpHR * kVpPitch;  // b1, g1, be1, b2, g2, be2, lin_w
   constexpr int RED_OFF = VEC_OFF + 7 * kVpC * 4;       // row statistics [48 rows][4 waves]
-  constexpr int IDX_OFF = RED_OFF + HRt * 4 * 4;      // bucket index per output row
-  constexpr int SMEM = IDX_OFF + BMt * 4;
+  constexpr int IDX_OFF = RED_OFF + kVpHR * 4 * 4;      // bucket index per output row
+  constexpr int SMEM = IDX_OFF + kVpBM * 4;
   static_assert(SMEM <= 163840, "LDS");
-  static_assert(4 * 1024 <= HRt * kVpPitch, "warm-up scratch slot (HHI, unused until LN1)");
+  static_assert(kVpScratchOff == HHI_OFF && 4 * 1024 <= kVpHR * kVpPitch, "warm-up scratch slot");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -230,14 +227,14 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
     const int me = (int)(blockIdx.x >> 3) * 4 + w, nw = peers * 4;
     const uint32_t gb = (uint32_t)g * 4u * kVpWaveBytes + (uint32_t)lane * 16u;
     for (int i = 0, pc = me; i < kVpPrefetchMax && pc < kPieces; ++i, pc += nw)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void *)(smem + HHI_OFF + w * 1024),
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void *)(smem + kVpScratchOff + w * 1024),
                                                16, gb + (uint32_t)pc * 1024u, 0, 0, 0);
   }
   if (tile >= p.ntiles) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA into LDS outlives the workgroup
     return;
   }
-  const int M = p.M, L = p.L, m0 = tile * BMt;
+  const int M = p.M, L = p.L, m0 = tile * kVpBM;
   const int r16 = lane & 15, hi = lane >> 4;
 
   // ---- tap masks: bit t set when row + t - 1 lies in the row's own utterance
@@ -250,11 +247,11 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
     }
     return v;
   };
-  int vm1[NB1], vm2[NB2];
+  int vm1[3], vm2[2];
 #pragma unroll
-  for (int nb = 0; nb < NB1; ++nb) vm1[nb] = taps(m0 - 1 + nb * 16 + r16);
+  for (int nb = 0; nb < 3; ++nb) vm1[nb] = taps(m0 - 1 + nb * 16 + r16);
 #pragma unroll
-  for (int nb = 0; nb < NB2; ++nb) vm2[nb] = taps(m0 + nb * 16 + r16);
+  for (int nb = 0; nb < 2; ++nb) vm2[nb] = taps(m0 + nb * 16 + r16);
 
   const float *vec = p.vec + (size_t)g * 7 * kVpC;
   for (int i = tid; i < 7 * kVpC / 4; i += 256)
@@ -270,7 +267,7 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
     const int o = pc * 1024 + lane * 16;
     const int r = o / kVpPitch, within = o - r * kVpPitch;
     const int gm = m0 - 2 + r;
-    const bool ok = r < XRt && within < 512 && gm >= 0 && gm < M;
+    const bool ok = r < kVpXR && within < 512 && gm >= 0 && gm < M;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)(smem + X_OFF + pc * 1024),
                                              16, ok ? (uint32_t)gm * xrow + (uint32_t)within : kOOB, 0, 0, 0);
   }
@@ -302,38 +299,38 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * kVpDepth) : "memory");  // the x tile (older than the ring)
   bar();
 
-  f32x4 acc1[4][NB1], acc2[4][NB2];
+  f32x4 acc1[4][3], acc2[4][2];
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb) {
 #pragma unroll
-    for (int nb = 0; nb < NB1; ++nb) acc1[jb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nb = 0; nb < 3; ++nb) acc1[jb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int nb = 0; nb < NB2; ++nb) acc2[jb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nb = 0; nb < 2; ++nb) acc2[jb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
   // ---- conv1: B fragments from the x tile (row r16 + 16 nb + tap, channels 32 ks + 8 hi)
-  auto bases1 = [&](int tap, int (&ad)[NB1]) {
+  auto bases1 = [&](int tap, int (&ad)[3]) {
     const int base = X_OFF + (r16 + tap) * kVpPitch + hi * 16;
 #pragma unroll
-    for (int nb = 0; nb < NB1; ++nb) ad[nb] = (base + nb * 16 * kVpPitch) & __builtin_amdgcn_sbfe(vm1[nb], tap, 1);
+    for (int nb = 0; nb < 3; ++nb) ad[nb] = (base + nb * 16 * kVpPitch) & __builtin_amdgcn_sbfe(vm1[nb], tap, 1);
   };
-  auto rd1 = [&](const int (&ad)[NB1], auto KSI, bf16x8 (&f)[NB1]) {
+  auto rd1 = [&](const int (&ad)[3], auto KSI, bf16x8 (&f)[3]) {
     constexpr int off = decltype(KSI)::value * 64;
 #pragma unroll
-    for (int nb = 0; nb < NB1; ++nb) f[nb] = *reinterpret_cast<const bf16x8 *>(smem + ad[nb] + off);
+    for (int nb = 0; nb < 3; ++nb) f[nb] = *reinterpret_cast<const bf16x8 *>(smem + ad[nb] + off);
   };
-  auto mma1 = [&](auto S, const bf16x8 (&f)[NB1]) {
+  auto mma1 = [&](auto S, const bf16x8 (&f)[3]) {
     constexpr int s = decltype(S)::value;
 #pragma unroll
     for (int e = 0; e < 2; ++e)
 #pragma unroll
-      for (int nb = 0; nb < NB1; ++nb)
+      for (int nb = 0; nb < 3; ++nb)
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb)
           acc1[jb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[s][e][jb], f[nb], acc1[jb][nb], 0, 0, 0);
   };
-  bf16x8 fa0[NB1], fa1[NB1];
-  int bc[NB1], bn[NB1];
+  bf16x8 fa0[3], fa1[3];
+  int bc[3], bn[3];
   bases1(0, bc);
   rd1(bc, std::integral_constant<int, 0>{}, fa0);
 #pragma nounroll
@@ -356,7 +353,7 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
       load_at(std::integral_constant<int, s>{}, tap * 8 + ks + kVpDepth);
     });
 #pragma unroll
-    for (int nb = 0; nb < NB1; ++nb) bc[nb] = bn[nb];
+    for (int nb = 0; nb < 3; ++nb) bc[nb] = bn[nb];
   }
 
   // ---- row statistics over the 256 channels: a lane holds 16 of them (4 blocks x 4) for rows
@@ -387,9 +384,9 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
 
   // ---- LN1 -> h as bf16 hi / lo planes (fs2_vp_norm's arithmetic), rows 0..47 of the H tile
   {
-    float part[NB1], mean[NB1], var[NB1];
+    float part[3], mean[3], var[3];
 #pragma unroll
-    for (int nb = 0; nb < NB1; ++nb) {
+    for (int nb = 0; nb < 3; ++nb) {
       float sum = 0.f;
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
@@ -398,15 +395,15 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
         v[0] = fmaxf(v[0] + b.x, 0.f);
         v[1] = fmaxf(v[1] + b.y, 0.f);
         v[2] = fmaxf(v[2] + b.z, 0.f);
-        v[NB1] = fmaxf(v[NB1] + b.w, 0.f);
+        v[3] = fmaxf(v[3] + b.w, 0.f);
         acc1[jb][nb] = v;
-        sum += (v[0] + v[1]) + (v[2] + v[NB1]);
+        sum += (v[0] + v[1]) + (v[2] + v[3]);
       }
       part[nb] = sum;
     }
-    row_reduce(std::integral_constant<int, NB1>{}, part, mean);
+    row_reduce(std::integral_constant<int, 3>{}, part, mean);
 #pragma unroll
-    for (int nb = 0; nb < NB1; ++nb) {
+    for (int nb = 0; nb < 3; ++nb) {
       mean[nb] *= inv_n;
       float ss = 0.f;
 #pragma unroll
@@ -415,15 +412,15 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
         d[0] -= mean[nb];
         d[1] -= mean[nb];
         d[2] -= mean[nb];
-        d[NB1] -= mean[nb];
+        d[3] -= mean[nb];
         acc1[jb][nb] = d;
-        ss += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[NB1] * d[NB1]);
+        ss += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
       }
       part[nb] = ss;
     }
-    row_reduce(std::integral_constant<int, NB1>{}, part, var);
+    row_reduce(std::integral_constant<int, 3>{}, part, var);
 #pragma unroll
-    for (int nb = 0; nb < NB1; ++nb) {
+    for (int nb = 0; nb < 3; ++nb) {
       const float rstd = 1.0f / sqrtf(var[nb] * inv_n + p.eps);
       const int row = nb * 16 + r16;
 #pragma unroll
@@ -432,7 +429,7 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
         const float4 ga = vec4(1, ch), be = vec4(2, ch);
         const f32x4 d = acc1[jb][nb];
         const float h[4] = {d[0] * rstd * ga.x + be.x, d[1] * rstd * ga.y + be.y, d[2] * rstd * ga.z + be.z,
-                            d[NB1] * rstd * ga.w + be.w};
+                            d[3] * rstd * ga.w + be.w};
         bf16x4 oh, ol;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -447,44 +444,44 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
   bar();  // the H planes are visible
 
   // ---- conv2: output row j = r16 + 16 nb reads h rows j + tap (h row i <-> global m0 - 1 + i)
-  auto bases2 = [&](int tap, int (&ah)[NB2], int (&al)[NB2]) {
+  auto bases2 = [&](int tap, int (&ah)[2], int (&al)[2]) {
     const int rel = (r16 + tap) * kVpPitch + hi * 16;
 #pragma unroll
-    for (int nb = 0; nb < NB2; ++nb) {
+    for (int nb = 0; nb < 2; ++nb) {
       const int keep = __builtin_amdgcn_sbfe(vm2[nb], tap, 1);
       ah[nb] = (HHI_OFF + rel + nb * 16 * kVpPitch) & keep;
       al[nb] = (HLO_OFF + rel + nb * 16 * kVpPitch) & keep;
     }
   };
-  auto rd2 = [&](const int (&ah)[NB2], const int (&al)[NB2], auto KSI, bf16x8 (&fh)[NB2], bf16x8 (&fl)[NB2]) {
+  auto rd2 = [&](const int (&ah)[2], const int (&al)[2], auto KSI, bf16x8 (&fh)[2], bf16x8 (&fl)[2]) {
     constexpr int off = decltype(KSI)::value * 64;
 #pragma unroll
-    for (int nb = 0; nb < NB2; ++nb) {
+    for (int nb = 0; nb < 2; ++nb) {
       fh[nb] = *reinterpret_cast<const bf16x8 *>(smem + ah[nb] + off);
       fl[nb] = *reinterpret_cast<const bf16x8 *>(smem + al[nb] + off);
     }
   };
-  auto mma2 = [&](auto S, const bf16x8 (&fh)[NB2], const bf16x8 (&fl)[NB2]) {
+  auto mma2 = [&](auto S, const bf16x8 (&fh)[2], const bf16x8 (&fl)[2]) {
     constexpr int s = decltype(S)::value;
 #pragma unroll
-    for (int nb = 0; nb < NB2; ++nb)
+    for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
         acc2[jb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[s][0][jb], fh[nb], acc2[jb][nb], 0, 0, 0);
 #pragma unroll
-    for (int nb = 0; nb < NB2; ++nb)
+    for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
         acc2[jb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[s][1][jb], fh[nb], acc2[jb][nb], 0, 0, 0);
 #pragma unroll
-    for (int nb = 0; nb < NB2; ++nb)
+    for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
         acc2[jb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[s][0][jb], fl[nb], acc2[jb][nb], 0, 0, 0);
   };
   {
-    bf16x8 fh0[NB2], fl0[NB2], fh1[NB2], fl1[NB2];
-    int ahc[NB2], alc[NB2], ahn[NB2], aln[NB2];
+    bf16x8 fh0[2], fl0[2], fh1[2], fl1[2];
+    int ahc[2], alc[2], ahn[2], aln[2];
     bases2(0, ahc, alc);
     rd2(ahc, alc, std::integral_constant<int, 0>{}, fh0, fl0);
 #pragma nounroll
@@ -507,7 +504,7 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
         load_at(std::integral_constant<int, s>{}, kVpKS + tap * 8 + ks + kVpDepth);
       });
 #pragma unroll
-      for (int nb = 0; nb < NB2; ++nb) {
+      for (int nb = 0; nb < 2; ++nb) {
         ahc[nb] = ahn[nb];
         alc[nb] = aln[nb];
       }
@@ -516,11 +513,11 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the past-the-end reloads
 
   // ---- LN2, Linear(256 -> 1), mask (fs2_vp_head's arithmetic)
-  float dot[NB2];
+  float dot[2];
   {
-    float part[NB2], mean[NB2], var[NB2];
+    float part[2], mean[2], var[2];
 #pragma unroll
-    for (int nb = 0; nb < NB2; ++nb) {
+    for (int nb = 0; nb < 2; ++nb) {
       float sum = 0.f;
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
@@ -529,15 +526,15 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
         v[0] = fmaxf(v[0] + b.x, 0.f);
         v[1] = fmaxf(v[1] + b.y, 0.f);
         v[2] = fmaxf(v[2] + b.z, 0.f);
-        v[NB1] = fmaxf(v[NB1] + b.w, 0.f);
+        v[3] = fmaxf(v[3] + b.w, 0.f);
         acc2[jb][nb] = v;
-        sum += (v[0] + v[1]) + (v[2] + v[NB1]);
+        sum += (v[0] + v[1]) + (v[2] + v[3]);
       }
       part[nb] = sum;
     }
-    row_reduce(std::integral_constant<int, NB2>{}, part, mean);
+    row_reduce(std::integral_constant<int, 2>{}, part, mean);
 #pragma unroll
-    for (int nb = 0; nb < NB2; ++nb) {
+    for (int nb = 0; nb < 2; ++nb) {
       mean[nb] *= inv_n;
       float ss = 0.f;
 #pragma unroll
@@ -546,15 +543,15 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
         d[0] -= mean[nb];
         d[1] -= mean[nb];
         d[2] -= mean[nb];
-        d[NB1] -= mean[nb];
+        d[3] -= mean[nb];
         acc2[jb][nb] = d;
-        ss += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[NB1] * d[NB1]);
+        ss += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
       }
       part[nb] = ss;
     }
-    row_reduce(std::integral_constant<int, NB2>{}, part, var);
+    row_reduce(std::integral_constant<int, 2>{}, part, var);
 #pragma unroll
-    for (int nb = 0; nb < NB2; ++nb) {
+    for (int nb = 0; nb < 2; ++nb) {
       const float rstd = 1.0f / sqrtf(var[nb] * inv_n + p.eps);
       float sd = 0.f;
 #pragma unroll
@@ -563,18 +560,18 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
         const float4 ga = vec4(4, ch), be = vec4(5, ch), lw = vec4(6, ch);
         const f32x4 d = acc2[jb][nb];
         sd += (d[0] * rstd * ga.x + be.x) * lw.x + (d[1] * rstd * ga.y + be.y) * lw.y +
-              (d[2] * rstd * ga.z + be.z) * lw.z + (d[NB1] * rstd * ga.w + be.w) * lw.w;
+              (d[2] * rstd * ga.z + be.z) * lw.z + (d[3] * rstd * ga.w + be.w) * lw.w;
       }
       part[nb] = sd;
     }
-    row_reduce(std::integral_constant<int, NB2>{}, part, dot);
+    row_reduce(std::integral_constant<int, 2>{}, part, dot);
   }
   const bool embed = g == p.embed_g;
   int *idx = reinterpret_cast<int *>(smem + IDX_OFF);
   if (w == 0 && hi == 0) {
     const float lb = p.lin_b[g];
 #pragma unroll
-    for (int nb = 0; nb < NB2; ++nb) {
+    for (int nb = 0; nb < 2; ++nb) {
       const int j = nb * 16 + r16, gm = m0 + j;
       if (gm < M) {
         const int b = gm / L, t = gm - b * L;
@@ -602,7 +599,7 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
   char *ob = reinterpret_cast<char *>(p.xo);
   const uint32_t orow = (uint32_t)p.xos * 2u;
 #pragma unroll
-  for (int i = tid; i < BMt * 32; i += 256) {
+  for (int i = tid; i < kVpBM * 32; i += 256) {
     const int j = i >> 5, ch = i & 31;
     if (m0 + j < M) {
       float a[8], e[8];
@@ -645,12 +642,7 @@ extern "C" int fs2_vp_fused(const fs2_vp_fused_desc *d, fs2_stream_t stream) {
   p.M = (int)M64;
   p.L = d->L;
   p.G = d->G;
-  static const int tile64 = [] {
-    const char *e = getenv("FS2_VP_TILE");
-    return (e != nullptr && e[0] == '6') ? 1 : 0;
-  }();
-  const int bm = tile64 ? 64 : kVpBM;
-  p.ntiles = (int)((M64 + bm - 1) / bm);
+  p.ntiles = (int)((M64 + kVpBM - 1) / kVpBM);
   p.lens = d->lens;
   p.pred = d->pred;
   p.embed_g = d->embed_group;
@@ -667,10 +659,7 @@ extern "C" int fs2_vp_fused(const fs2_vp_fused_desc *d, fs2_stream_t stream) {
   }();
   p.prefetch = prefetch;
   const int nwg = d->G == 2 ? 8 * ((p.ntiles + 3) / 4) : p.ntiles;
-  if (tile64)
-    hipLaunchKernelGGL(vp_fused_kernel<4>, dim3(nwg), dim3(256), 0, as_stream(stream), p);
-  else
-    hipLaunchKernelGGL(vp_fused_kernel<2>, dim3(nwg), dim3(256), 0, as_stream(stream), p);
+  hipLaunchKernelGGL(vp_fused_kernel, dim3(nwg), dim3(256), 0, as_stream(stream), p);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
