@@ -156,7 +156,8 @@ constexpr int kVpUnits = 2 * kVpKS * 2;   // per wave: 2 convs x 24 k-steps x (h
 constexpr uint32_t kVpWaveBytes = (uint32_t)kVpUnits * kVpUnit;
 constexpr int kVpDepth = 4;               // k-steps in flight (8 units, 128 registers)
 constexpr int kVpLgkm0 = 0xC07F;          // s_waitcnt lgkmcnt(0) as a real wait-count instruction
-constexpr int kVpPrefetchMax = 20;        // warm-up loads per wave (x tile + ring + these < 64 in flight)
+constexpr int kVpPrefetchMax = 24;        // warm-up loads per wave (x tile + ring + these <= 63 in flight):
+                                          // the energy set's 16 workgroups per XCD cover the whole stream
 constexpr int kVpScratchOff = 512 + 4 * ((((50 * 544 + 1023) / 1024) + 3) / 4) * 1024;  // = HHI_OFF
 
 struct VpArgs {
@@ -202,6 +203,7 @@ __global__ __launch_bounds__(256, 1) void vp_fused_kernel(VpArgs p) {
   constexpr int IDX_OFF = RED_OFF + kVpHR * 4 * 4;      // bucket index per output row
   constexpr int SMEM = IDX_OFF + kVpBM * 4;
   static_assert(SMEM <= 163840, "LDS");
+  static_assert(kVpPrefetchMax + XPW + 8 * kVpDepth <= 63, "vmcnt holds at most 63 outstanding loads");
   static_assert(kVpScratchOff == HHI_OFF && 4 * 1024 <= kVpHR * kVpPitch, "warm-up scratch slot");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
