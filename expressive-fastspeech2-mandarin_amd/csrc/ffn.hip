@@ -60,6 +60,7 @@ struct FfnArgs {
   void *part;          // f32 partial Y^T accumulators, part_bytes(MB) per (tile, split)
   int acquire;         // agent acquire before the partial loads (FS2_FFN_ACQUIRE=1; off: sc1 hand-off)
   int out_sc1;         // output rows stored write-through (sc1): the lines leave L2 (FS2_OUT_SC1=0: plain, A/B)
+  int prefetch;        // split-hidden form: L2 warm-up of the split's weights (FS2_FFN_PREFETCH)
   uint32_t part_bytes;
   // the NEXT FFT block's Q|K|V projection of y (optional): qkv[m, :] = y[m, :] . wq^T + bq
   const bf16 *wq;      // [nq][256] in fragment order [nq/64][8][4][4][16][8]
@@ -138,7 +139,8 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   constexpr int NU = NK1 + NK2;
   constexpr int DEPTH = kDepth;
   static_assert(NK1 % DEPTH == 0 && NK2 % DEPTH == 0, "static register-ring slots");
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + (FFN_TRACE ? 256 : 0)];
+  constexpr int SCR_OFF = SMEM + (FFN_TRACE ? 256 : 0);  // L2 warm-up scratch (1 KiB per wave), !PRE only
+  __shared__ __attribute__((aligned(16))) char smem[SCR_OFF + (PRE ? 0 : 4096)];
 
   const ConvArgs &a = p.e;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -217,6 +219,30 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     }
   };
   if constexpr (!PRE) {
+    // ---- split-hidden form: L2 warm-up (as vp.hip). An XCD's workgroups run ONE split (the
+    // split-major order above) and stream its ~1.3 MB of weights in lockstep, 16 MFMAs per 4 KiB
+    // unit at 64-row tiles: too little work to cover an XCD-wide first-touch miss with a 4-unit ring.
+    // Each wave first pulls disjoint 1 KiB slices of the split's GEMM1 block and its four GEMM2
+    // column ranges into a scratch slot (waited for with the x tile), so the rings then hit L2.
+    if (S > 1 && p.prefetch) {
+      const int nch = cend - c0;
+      const int p1 = nch * 4 * NK1 * 4, p2q = nch * NK2 * 4;  // 1 KiB pieces: GEMM1 block, one GEMM2 range
+      const uint32_t g1 = (uint32_t)(c0 * 4 * NK1) * (uint32_t)kUnit;
+      constexpr uint32_t W2B = (uint32_t)(F * KS * kD * 2);
+      const int per_xcd = (int)(gridDim.x >> 3);
+      const int me = (int)(blockIdx.x >> 3) * 4 + w, nw = per_xcd * 4;
+      for (int i = 0, pc = me; i < 16 && pc < p1 + 4 * p2q; ++i, pc += nw) {
+        uint32_t off;
+        if (pc < p1) {
+          off = g1 + (uint32_t)pc * 1024u;
+        } else {
+          const int j = pc - p1, ww = j / p2q, r = j - ww * p2q;
+          off = W2B + (uint32_t)(ww * (F / 32) + c0 * NK2) * (uint32_t)kUnit + (uint32_t)r * 1024u;
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void *)(smem + SCR_OFF + w * 1024),
+                                                 16, off + (uint32_t)lane * 16u, 0, 0, 0);
+      }
+    }
     // ---- x tile (rows m0 - pad .. m0 + BM + KS - 2, all 256 channels) -> LDS, once
     tile_dma(a.x, a.x_bytes, a.xs, X_OFF);
   } else {
@@ -1001,6 +1027,11 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
     return (e != nullptr && e[0] == '0') ? 0 : 1;
   }();
   p.out_sc1 = out_sc1;
+  static const int ffn_prefetch = [] {
+    const char *e = getenv("FS2_FFN_PREFETCH");
+    return (e != nullptr && e[0] == '1') ? 1 : 0;
+  }();
+  p.prefetch = ffn_prefetch;
   if (S > 1) {
     if (d->splitk_ws == nullptr || ntiles > 1024 ||
         d->splitk_ws_bytes < 4096 + (int64_t)ntiles * S * kPartBytes || (int64_t)ntiles * S * kPartBytes >= (1LL << 31))
