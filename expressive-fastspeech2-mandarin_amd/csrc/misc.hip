@@ -53,19 +53,6 @@ __global__ __launch_bounds__(256) void cond_kernel(const int64_t *speakers, cons
   extern __shared__ float sm[];
   const int tid = threadIdx.x;
   const int n0 = blockIdx.x * 64, b0 = blockIdx.y * kCondU;
-  const int nl = tid & 63, kq = tid >> 6, n = n0 + nl;
-  // the weight quarter this thread reads does not depend on the ids: issued first (dc <= 256: at
-  // most 16 float4 per thread), so its latency overlaps the id -> table gathers below instead of
-  // following them
-  const int dc = d_emo + d_aro + d_val;
-  const bool pre = emo_table != nullptr && (dc & 15) == 0 && dc <= 256 && n < D;
-  float4 wpre[16];
-  if (pre) {
-    const float *wr = lin_w + (int64_t)n * dc + kq * (dc >> 2);
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (4 * j < (dc >> 2)) wpre[j] = *reinterpret_cast<const float4 *>(wr + 4 * j);
-  }
   if (spk_table != nullptr) {
     for (int i = tid; i < kCondU * 64; i += 256) {
       const int b = b0 + (i >> 6), n = n0 + (i & 63);
@@ -73,6 +60,7 @@ __global__ __launch_bounds__(256) void cond_kernel(const int64_t *speakers, cons
     }
   }
   if (emo_table == nullptr) return;
+  const int dc = d_emo + d_aro + d_val;
   float *cat = sm;                   // [kCondU][dc]
   float *red = sm + kCondU * dc;     // [kCondU][4][64]
   for (int i = tid; i < kCondU * dc; i += 256) {
@@ -89,24 +77,11 @@ __global__ __launch_bounds__(256) void cond_kernel(const int64_t *speakers, cons
     cat[i] = x;
   }
   __syncthreads();
+  const int nl = tid & 63, kq = tid >> 6, n = n0 + nl;
   float acc[kCondU];
 #pragma unroll
   for (int u = 0; u < kCondU; ++u) acc[u] = 0.f;
-  if (pre) {
-    const int k0 = kq * (dc >> 2);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      if (4 * j < (dc >> 2)) {
-        const float4 wv = wpre[j];
-        const int k = k0 + 4 * j;
-#pragma unroll
-        for (int u = 0; u < kCondU; ++u) {
-          const float4 c = *reinterpret_cast<const float4 *>(cat + u * dc + k);
-          acc[u] = fmaf(wv.x, c.x, fmaf(wv.y, c.y, fmaf(wv.z, c.z, fmaf(wv.w, c.w, acc[u]))));
-        }
-      }
-    }
-  } else if (n < D) {
+  if (n < D) {
     const float *wr = lin_w + (int64_t)n * dc;
     if ((dc & 15) == 0) {
       const int kper = dc >> 2, k0 = kq * kper;
