@@ -16,9 +16,11 @@ trace through it with ``fullgraph=True`` instead of breaking the graph at a ctyp
 * ``fs2::ffn(x, w_packed, b1, b2, ln_gamma, ln_beta, ln_eps, lens, ks, pad) -> y`` — the FFT block's
   ``PositionwiseFeedForward`` + residual + LayerNorm + padding mask (transformer/SubLayers.py:85-93,
   transformer/Layers.py:28) as one fs2_ffn launch (inference; weights from ops.pack_ffn_weights).
+* ``fs2::conv1d(x, w_packed, bias, cin, ks, pad, compute, epilogue, out_dtype) -> y`` — fs2_conv1d
+  with a plain (bias / activation) epilogue.
 
-Importing this module registers the ops (``import fs2amd.library``); ``fs2amd`` imports it lazily so
-the C library is not loaded before first use.
+Importing this module (``import fs2amd.library``, or the ``model`` drop-in package) registers the ops;
+the C library itself is loaded at the first launch.
 """
 from typing import Optional, Tuple
 
@@ -89,4 +91,24 @@ def _ffn_fake(x, w_packed, b1, b2, ln_gamma, ln_beta, ln_eps, lens, ks, pad):
     return torch.empty_like(x)
 
 
-OPS = ("length_regulate", "attention", "attention_bwd", "ffn")
+@torch.library.custom_op("fs2::conv1d", mutates_args=())
+def conv1d(x: Tensor, w_packed: Tensor, bias: Optional[Tensor], cin: int, ks: int, pad: int, compute: int,
+           epilogue: int, out_dtype: int) -> Tensor:
+    """fs2_conv1d with a plain epilogue (bias / bias + ReLU / bias + tanh / bias + leaky ReLU):
+    ``nn.Conv1d`` / ``nn.Linear`` over [B, T, C] rows (the VariancePredictor / PostNet / mel_linear
+    convolutions, model/modules.py:253-296, transformer/Layers.py:33-137, model/fastspeech2.py:134);
+    w_packed from ops.pack_conv_weight (N = w_packed.shape[0] output channels)."""
+    from . import _lib as L
+    if epilogue not in (L.EPI_BIAS, L.EPI_BIAS_RELU, L.EPI_BIAS_TANH, L.EPI_BIAS_LRELU):
+        raise ValueError("fs2::conv1d: plain epilogues only (residual / LayerNorm forms go through fs2amd.ops)")
+    return ops.conv1d(x, w_packed, bias, cin=cin, ks=ks, pad=pad, compute=compute, epilogue=epilogue,
+                      out_dtype=out_dtype)
+
+
+@conv1d.register_fake
+def _conv1d_fake(x, w_packed, bias, cin, ks, pad, compute, epilogue, out_dtype):
+    B, T, _ = x.shape
+    return x.new_empty(B, T, w_packed.shape[0], dtype=ops.torch_dtype(out_dtype))
+
+
+OPS = ("length_regulate", "attention", "attention_bwd", "ffn", "conv1d")

@@ -82,6 +82,25 @@ def test_ffn_op_equals_direct_launch(gpu):
     assert torch.equal(a, b)
 
 
+def test_conv1d_op_equals_direct_launch(gpu):
+    ops, L = gpu
+    g = torch.Generator(device=DEV).manual_seed(5)
+    w = torch.randn(256, 256, 3, device=DEV, generator=g) / 28.0
+    b = 0.1 * torch.randn(256, device=DEV, generator=g)
+    wp = ops.pack_conv_weight(w, L.FS2_BF16)
+    x = torch.randn(3, 41, 256, device=DEV, generator=g).to(torch.bfloat16)
+    a = torch.ops.fs2.conv1d(x, wp, b, 256, 3, 1, L.FS2_BF16, L.EPI_BIAS_RELU, L.FS2_BF16)
+    r = ops.conv1d(x, wp, b, cin=256, ks=3, pad=1, compute=L.FS2_BF16, epilogue=L.EPI_BIAS_RELU,
+                   out_dtype=L.FS2_BF16)
+    ref = torch.relu(torch.nn.functional.conv1d(x.float().transpose(1, 2), w.to(torch.bfloat16).float(), b,
+                                                padding=1)).transpose(1, 2)
+    torch.cuda.synchronize()
+    assert torch.equal(a, r) and a.shape == (3, 41, 256)
+    assert (a.float() - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+    with pytest.raises(ValueError):
+        torch.ops.fs2.conv1d(x, wp, b, 256, 3, 1, L.FS2_BF16, L.EPI_RES_LN, L.FS2_BF16)
+
+
 def test_compile_fullgraph(gpu):
     """LengthRegulator -> attention over the expanded frames, traced whole (no graph break at the
     ctypes launches) and equal to the eager ops."""

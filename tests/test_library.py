@@ -42,6 +42,10 @@ def test_fake_shapes(lib):
                               torch.empty(256, device="cuda"), torch.empty(256, device="cuda"),
                               torch.empty(256, device="cuda"), 1e-5, lens, 9, 4)
         assert f.shape == x.shape and f.dtype == x.dtype
+        from fs2amd import _lib as L
+        c = torch.ops.fs2.conv1d(x, torch.empty(80, 256, device="cuda", dtype=torch.bfloat16), None, 256, 1, 0,
+                                 L.FS2_BF16, L.EPI_BIAS, L.FS2_F32)
+        assert c.shape == (3, 11, 80) and c.dtype == torch.float32
 
 
 def test_cpu_tensors_refused(lib):
