@@ -112,32 +112,109 @@ def build_model(device, dtype):
     return model, pc, mc
 
 
-def time_kernel_in_forward(model, batch, n_fwd=6):
-    """Mean duration of the decoder FFN launches inside real (eager) forwards: HIP events recorded
-    around each launch on its stream (fs2amd.runtime.TIMERS entries (start, end, tag)). Returns
-    {tag: (mean seconds, launches)}: "ffn" the plain fused FFN (the last decoder block), "ffn+qkv"
-    the launches that also project the next block's Q|K|V (blocks 1..5), "conv9" the unfused
-    conv-k9 op."""
+_SLEEP_CYCLES_PER_MS = []
+
+
+def _gpu_busy(ms):
+    """Keep the launch stream busy for about `ms` (torch.cuda._sleep, calibrated once with HIP
+    events) so that the host enqueues a whole eager forward before the GPU reaches it: HIP events
+    around each launch then time the kernel, not the host's launch latency."""
+    if not _SLEEP_CYCLES_PER_MS:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(1000)
+        e0.record()
+        torch.cuda._sleep(2_000_000)
+        e1.record()
+        e1.synchronize()
+        _SLEEP_CYCLES_PER_MS.append(2_000_000 / max(e0.elapsed_time(e1), 1e-3))
+    torch.cuda._sleep(int(ms * _SLEEP_CYCLES_PER_MS[0]))
+
+
+def forward_timers(model, batch, n_fwd=6):
+    """HIP events around every launch of interest (fs2amd.runtime.TIMERS: (start, end, tag) in
+    launch order) over n_fwd eager forwards, each forward queued behind ~20 ms of GPU work so that
+    the timings are kernel durations. Returns [(tag, seconds)] per forward."""
     from fs2amd import runtime
 
     # one utterance group: the timed launches have the chip to themselves (with stream groups,
     # concurrent launches share the CUs and per-launch durations stop being kernel speed)
     prev = os.environ.get("FS2_STREAMS")
     os.environ["FS2_STREAMS"] = "1"
-    runtime.TIMERS = []
-    with torch.no_grad():
-        for _ in range(n_fwd):
+    per_fwd = []
+    try:
+        with torch.no_grad():
             model(**batch)
-    torch.cuda.synchronize()
+            for _ in range(n_fwd):
+                runtime.TIMERS = []
+                _gpu_busy(20.0)
+                model(**batch)
+                per_fwd.append(runtime.TIMERS)
+                runtime.TIMERS = None
+        torch.cuda.synchronize()
+    finally:
+        runtime.TIMERS = None
+        if prev is None:
+            del os.environ["FS2_STREAMS"]
+        else:
+            os.environ["FS2_STREAMS"] = prev
+    return [[(tag, a.elapsed_time(b) / 1e3) for a, b, tag in tms] for tms in per_fwd]
+
+
+def time_kernel_in_forward(model, batch, n_fwd=6, fwd=None):
+    """Mean duration per tag of the timed launches inside real (eager) forwards (forward_timers).
+    Returns {tag: (mean seconds, launches)}: decoder FFN tags "fc+ffn" (the last decoder block),
+    "fc+ffn+qkv" (blocks 1..5, which also project the next block's Q|K|V), "ffn", "ffn+qkv",
+    "ffn8", "conv9"; the other launches "<stack>:<op>"."""
+    fwd = forward_timers(model, batch, n_fwd) if fwd is None else fwd
     by = {}
-    for a, b, tag in runtime.TIMERS:
-        by.setdefault(tag, []).append(a.elapsed_time(b) / 1e3)
-    runtime.TIMERS = None
-    if prev is None:
-        del os.environ["FS2_STREAMS"]
-    else:
-        os.environ["FS2_STREAMS"] = prev
+    for tms in fwd:
+        for tag, t in tms:
+            by.setdefault(tag, []).append(t)
     return {k: (sum(v) / len(v), len(v)) for k, v in by.items()}
+
+
+GEMM_OPS = {"qkv", "fc", "ffn", "ffn+qkv", "fc+ffn", "fc+ffn+qkv", "conv9", "conv1", "ffn8"}
+FFT_GEMM_FLOPS_PER_TOKEN = 2 * (256 * 768 + 256 * 256 + 256 * 9 * 1024 + 1024 * 256)  # 5,767,168 (SURVEY §8d)
+
+
+def forward_breakdown(fwd, batch_cpu, peak_tflops):
+    """Per-forward sums of the timed launches (us), and the two north-star fractions:
+    * fft_gemm — every FFT-block GEMM launch of the forward (Q|K|V, fc + LN, the FFN pair, fused
+      or not): SURVEY §8d's 5,767,168 FLOP per valid token per layer (QKV + out proj + conv-k9 +
+      conv-k1) over the encoder's valid phonemes x 4 layers and the decoder's valid frames x 6,
+      divided by the summed durations of those launches, against the dense MFMA peak;
+    * lr — the LengthRegulator launch (fs2_lr_fused: scan + packed layout + gather + PE): bytes it
+      must move (x read once, durations, the packed frames written, the layout) over its duration,
+      against 8 TB/s."""
+    n = len(fwd)
+    tot = {}
+    for tms in fwd:
+        for tag, t in tms:
+            tot[tag] = tot.get(tag, 0.0) + t / n
+    op = lambda tag: tag.split(":", 1)[-1]
+    gemm_s = sum(t for tag, t in tot.items() if op(tag) in GEMM_OPS and not tag.startswith("va:"))
+    n_gemm = sum(1 for tag, _ in fwd[0] if op(tag) in GEMM_OPS and not tag.startswith("va:"))
+    enc_tok = int(batch_cpu["src_lens"].sum())
+    frames = int(batch_cpu["mel_lens"].sum()) if batch_cpu.get("mel_lens") is not None else None
+    B, Lp = batch_cpu["texts"].shape
+    out = {"us_per_forward": {k: round(v * 1e6, 2) for k, v in sorted(tot.items(), key=lambda kv: -kv[1])},
+           "forwards_timed": n,
+           "timing": "HIP events around each launch on its stream in eager forwards queued behind ~20 ms of GPU "
+                     "work (torch.cuda._sleep), so the events bracket the kernel, not the host's launch latency"}
+    if frames is not None and gemm_s > 0:
+        fl = float(FFT_GEMM_FLOPS_PER_TOKEN) * (4 * enc_tok + 6 * frames)
+        out["fft_gemm"] = {"flops_per_forward": fl, "us_per_forward": round(gemm_s * 1e6, 2), "launches": n_gemm,
+                           "achieved": round(fl / gemm_s / 1e12, 2), "peak": peak_tflops, "unit": "TFLOP/s",
+                           "frac": round(fl / gemm_s / 1e12 / peak_tflops, 4)}
+    lr = tot.get("va:lr")
+    if lr and frames is not None:
+        T = int(batch_cpu["max_mel_len"])
+        byt = B * Lp * 256 * 2.0 + B * Lp * 8.0 + frames * 256 * 2.0 + B * T * 4.0 + frames * 8.0 + (B + 1) * 4.0
+        out["lr"] = {"bytes": byt, "us": round(lr * 1e6, 2), "achieved": round(byt / lr / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(byt / lr / 1e9 / HBM_PEAK_GBS, 4),
+                     "bytes_note": "bf16 x read once + int64 durations + packed bf16 frames written + rowmap "
+                                   "(B*T int32) + row_pos (frames x 8 B) + cu"}
+    return out
 
 
 def ffn_fused(model, batch, device):
@@ -495,8 +572,15 @@ def extra_workloads(model, args, rank, device):
     record("free_running_cfg2_eager", synth_batch(args.batch, args.phonemes, seed=1 + rank, teacher=False), False,
            "durations predicted + rounded (modules.py:131-137), one D2H read of max(mel_len), eager launches")
     res["free_running_cfg2"] = synth_graphs_workload(model, args, rank, device, steps)
-    record("cfg4_b256", synth_batch(256, 16, 160, seed=1 + rank), True,
-           "B=256 x U{16..160} phonemes, teacher-forced durations U{2..10}")
+    b4 = synth_batch(256, 16, 160, seed=1 + rank)
+    record("cfg4_b256", b4, True, "B=256 x U{16..160} phonemes, teacher-forced durations U{2..10}")
+    # the LengthRegulator stress shape (152 MB bf16): its launch inside eager cfg4
+    # forwards, and the FFT-block GEMM fraction at B=256
+    brk4 = forward_breakdown(forward_timers(model, to_device(b4, device), n_fwd=3), b4,
+                             {"bf16": BF16_PEAK_TFLOPS, "fp8": FP8_PEAK_TFLOPS}.get(prec, F32_PEAK_TFLOPS))
+    for k in ("lr", "fft_gemm"):
+        if k in brk4:
+            res["cfg4_b256"][k] = brk4[k]
     if prec == "bf16":
         cal = synth_batch(args.batch, args.phonemes, seed=1000 + rank)
         model.set_precision("fp8")
@@ -521,34 +605,56 @@ def extra_workloads(model, args, rank, device):
     return res
 
 
-def synth_graphs_workload(model, args, rank, device, steps):
-    """The synthesis path (free-running cfg2: predicted durations, no max_mel_len) through
-    fs2amd.graphs.SynthGraphs: stage-1 graph, the one host read of max(mel_len), stage-2 graph
-    (captured on the first call for this T_out; warm-up). Each timed step is a whole synthesis
-    call including its host read, as a serving loop runs it."""
+def synth_graphs_workload(model, args, rank, device, steps, n_batches=8):
+    """The synthesis path (free-running cfg2: predicted durations, no max_mel_len) as a serving
+    loop runs it: ``n_batches`` DISTINCT seeded batches of 64 x 64 phonemes called in rotation, each
+    timed call a whole synthesis call including its one host read. Through
+    fs2amd.graphs.SynthGraphs (stage-1 graph, the host read, the decoder graph of the T bucket, the
+    eager T_out-shaped tail) and, for comparison, the eager forward on the same rotation. One
+    warm-up pass over the batches captures what it needs; the captures of the timed calls are
+    counted (a serving loop must not recapture per batch)."""
     from fs2amd import parallel
     from fs2amd.data import synth_batch, to_device
     from fs2amd.graphs import SynthGraphs
 
-    b = to_device(synth_batch(args.batch, args.phonemes, seed=1 + rank, teacher=False), device)
+    bs = [to_device(synth_batch(args.batch, args.phonemes, seed=1 + rank + 1000 * i, teacher=False), device)
+          for i in range(n_batches)]
     synth = SynthGraphs(model)
-    for _ in range(2):
-        out = synth(**b)
-    torch.cuda.synchronize(device)
-    frames = int(out[9].sum())
-    parallel.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        synth(**b)
-    torch.cuda.synchronize(device)
-    parallel.barrier()
-    el, fr = parallel.aggregate(time.perf_counter() - t0, frames, device)
-    return {"value": round(fr * steps / el, 1), "unit": "mel-frames/s", "ms_per_step": round(el / steps * 1e3, 4),
-            "steps": steps, "frames_per_step": fr, "hip_graph": True, "dtype": model.precision,
-            "graphs_captured": synth.captures,
-            "note": "durations predicted + rounded (modules.py:131-137); fs2amd.graphs.SynthGraphs: stage-1 graph, "
-                    "ONE device->host read (max(mel_len) + bad-id count), stage-2 graph keyed by T_out"}
+    res = {}
+    for name, fn in (("graphs", lambda b: synth(**b)), ("eager", lambda b: model(**b))):
+        frames, t_out = [], []
+        with torch.no_grad():
+            for b in bs:
+                out = fn(b)
+                frames.append(int(out[9].sum()))
+                t_out.append(int(out[0].shape[1]))
+        torch.cuda.synchronize(device)
+        cap0 = synth.captures
+        parallel.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            for i in range(steps):
+                fn(bs[i % n_batches])
+        torch.cuda.synchronize(device)
+        parallel.barrier()
+        fr = sum(frames[i % n_batches] for i in range(steps))
+        el, fr = parallel.aggregate(time.perf_counter() - t0, fr, device)
+        res[name] = {"value": round(fr / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
+                     "frames_per_step_mean": round(fr / steps, 1), "T_out": t_out,
+                     **({"graphs_captured_warmup": cap0, "graphs_captured_timed": synth.captures - cap0}
+                        if name == "graphs" else {})}
+    synth.close()
+    g = res["graphs"]
+    return {"value": g["value"], "unit": "mel-frames/s", "ms_per_step": g["ms_per_step"], "steps": steps,
+            "distinct_batches": n_batches, "frames_per_step_mean": g["frames_per_step_mean"], "T_out": g["T_out"],
+            "hip_graph": True, "dtype": model.precision,
+            "graphs_captured_warmup": g["graphs_captured_warmup"], "graphs_captured_timed": g["graphs_captured_timed"],
+            "eager": {k: res["eager"][k] for k in ("value", "ms_per_step")},
+            "note": "durations predicted + rounded (modules.py:131-137); 8 distinct seeded batches in rotation; "
+                    "fs2amd.graphs.SynthGraphs: stage-1 graph, ONE device->host read (max / sum of mel_len + "
+                    "bad-id count), the decoder graph of the 64-frame T bucket, the T_out-shaped mel_linear / "
+                    "PostNet tail issued eagerly behind it; 'eager': the eager forward on the same rotation"}
 
 
 def vocoder_workload(model, args, rank, device, steps):
@@ -660,7 +766,8 @@ def main():
     elapsed, tot_frames = parallel.aggregate(elapsed, frames, device)
     extra = extra_workloads(model, args, rank, device) if args.extra else {}
 
-    timed = time_kernel_in_forward(model, batch)
+    fwd_t = forward_timers(model, batch)
+    timed = time_kernel_in_forward(model, batch, fwd=fwd_t)
     eager_s, n_launch = timed.get("fc+ffn", timed.get("ffn", timed.get("conv9", (float("nan"), 0))))
     standalone_s, kernel_flops = time_dominant_kernel(model, batch_cpu, device, args.kernel_reps)
     table = None
@@ -730,6 +837,12 @@ def main():
                      "traffic_note": "2*FETCH_SIZE + WRITE_SIZE per launch (rocprofv3 PMC, profiles/"
                                      + ("ffn_traffic.json)" if fused else "conv9_traffic.json)")},
     }
+    brk = forward_breakdown(fwd_t, batch_cpu, peak)
+    if "fft_gemm" in brk:
+        rec["fft_gemm_frac"] = brk["fft_gemm"]["frac"]
+    if "lr" in brk:
+        rec["lr_hbm_frac"] = brk["lr"]["frac"]
+    rec["forward_breakdown"] = brk
     if table is not None:
         rec["decoder_ops"] = table
     if rank == 0 and world == 1 and args.cpu_baseline:

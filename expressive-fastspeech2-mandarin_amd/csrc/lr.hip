@@ -191,6 +191,36 @@ void launch_expand(const void *x, const int32_t *cum, const int64_t *mel_len, in
   launch_expand_v<TX, TO, 32, true>(x, cum, mel_len, B, L, D, T_out, pe, out, index_map, out_cu, s);
 }
 
+// LengthRegulator backward (training, model/modules.py:161-194 through autograd): the gather's
+// gradient is, per phoneme i of utterance b, the sum of dy over its contiguous frame range
+// [cum[i-1], cum[i]) clipped to the T output frames (frames past T -- the max_len / decoder crop --
+// carry no gradient). A segmented sum in frame order: deterministic, no atomics (torch's gather
+// backward is a scatter-add with float atomics). 8 phonemes per workgroup, D/8 lanes per phoneme,
+// 8 f32 columns per lane; dy [B, T, D] and dx [B, L, D] f32, contiguous.
+__global__ __launch_bounds__(256) void lr_bwd_kernel(const float *__restrict__ dy, const int32_t *__restrict__ cum,
+                                                     int L, int D, int T, float *__restrict__ dx) {
+  constexpr int PH = 8;
+  const int b = blockIdx.y, i0 = blockIdx.x * PH;
+  const int vpr = D >> 3;
+  const int32_t *c = cum + (int64_t)b * L;
+  const float *db = dy + (int64_t)b * T * D;
+  for (int e = threadIdx.x; e < PH * vpr; e += 256) {
+    const int i = i0 + e / vpr;
+    if (i >= L) break;
+    const int col = (e - (i - i0) * vpr) << 3;
+    const int t0 = i == 0 ? 0 : min(c[i - 1], T);
+    const int t1 = min(c[i], T);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int t = t0; t < t1; ++t) {
+      float v[8];
+      load8(db + (int64_t)t * D + col, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += v[q];
+    }
+    store8(dx + ((int64_t)b * L + i) * D + col, acc);
+  }
+}
+
 // The whole LengthRegulator stage in ONE launch (round 4): each workgroup (32 frames of one
 // utterance) (1) re-derives the utterance's cumulative frame counts in LDS -- from the durations
 // (scan) or from a cum row computed before the free-running host read --, (2) the decoder's packed
@@ -560,6 +590,17 @@ extern "C" int fs2_length_regulate(const void *x, int x_dtype, const void *dur, 
   int rc = fs2_lr_durations(dur, dur_kind, d_control, B, L, cum, mel_len, d_rounded, stream);
   if (rc != FS2_OK) return rc;
   return fs2_lr_expand(x, x_dtype, cum, mel_len, B, L, D, T_out, pe, out, out_dtype, index_map, nullptr, stream);
+}
+
+extern "C" int fs2_lr_backward(const float *dy, const int32_t *cum, int B, int L, int D, int T, float *dx,
+                               fs2_stream_t stream) {
+  if (dy == nullptr || cum == nullptr || dx == nullptr || B < 0 || L < 0 || T < 0 || D <= 0 || (D & 7) || D > 2048)
+    return FS2_EINVAL;
+  if (B == 0 || L == 0) return FS2_OK;
+  hipLaunchKernelGGL(lr_bwd_kernel, dim3((unsigned)((L + 7) / 8), (unsigned)B), dim3(256), 0, as_stream(stream), dy,
+                     cum, L, D, T, dx);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
 }
 
 extern "C" int fs2_len_stats(const int64_t *lens, int B, const int32_t *bad_counter, int32_t *meta, fs2_stream_t stream) {

@@ -118,10 +118,11 @@ __global__ __launch_bounds__(256) void cond_kernel(const int64_t *speakers, cons
 // 32 lanes per row (inside one wave, so the read of pred[m] by every lane precedes lane 0's
 // write-back), 8 channels per lane per step.                   (model/modules.py:80-100)
 template <typename TX>
-__global__ __launch_bounds__(256) void variance_embed_kernel(TX *__restrict__ x, float *__restrict__ pred,
+__global__ __launch_bounds__(256) void variance_embed_kernel(const TX *x, TX *out, const float *pred, float *pred_out,
                                                              const float *__restrict__ target, float control,
                                                              const float *__restrict__ bins, int nb,
-                                                             const float *__restrict__ table, int M, int D) {
+                                                             const float *__restrict__ table, int M, int D,
+                                                             int64_t *__restrict__ idx_out) {
   const int m = blockIdx.x * 8 + (threadIdx.x >> 5);
   const int sub = threadIdx.x & 31;
   if (m >= M) return;
@@ -137,16 +138,18 @@ __global__ __launch_bounds__(256) void variance_embed_kernel(TX *__restrict__ x,
     const int mid = (lo + hi) >> 1;
     if (bins[mid] < v) lo = mid + 1; else hi = mid;
   }
-  if (target == nullptr && sub == 0) pred[m] = v;
+  if (target == nullptr && pred_out != nullptr && sub == 0) pred_out[m] = v;
+  if (idx_out != nullptr && sub == 0) idx_out[m] = lo;
   const float *trow = table + (int64_t)lo * D;
-  TX *xrow = x + (int64_t)m * D;
+  const TX *xrow = x + (int64_t)m * D;
+  TX *orow = out + (int64_t)m * D;
   for (int col = sub * 8; col < D; col += 256) {
     float a[8], t[8];
     load8(xrow + col, a);
     load8(trow + col, t);
 #pragma unroll
     for (int q = 0; q < 8; ++q) a[q] += t[q];
-    store8(xrow + col, a);
+    store8(orow + col, a);
   }
 }
 
@@ -242,27 +245,50 @@ extern "C" int fs2_cond_vectors(const int64_t *speakers, const float *speaker_ta
   return FS2_OK;
 }
 
-extern "C" int fs2_variance_embed(void *x, int x_dtype, float *pred, const float *target, float control,
-                                  const float *bins, int n_bins, const float *table, int M, int D,
-                                  fs2_stream_t stream) {
-  if (x == nullptr || pred == nullptr || bins == nullptr || table == nullptr) return FS2_EINVAL;
+static int variance_embed_launch(const void *x, int x_dtype, void *out, const float *pred, float *pred_out,
+                                 const float *target, float control, const float *bins, int n_bins,
+                                 const float *table, int M, int D, int64_t *idx_out, fs2_stream_t stream) {
+  if (x == nullptr || out == nullptr || (pred == nullptr && target == nullptr) || bins == nullptr || table == nullptr)
+    return FS2_EINVAL;
   if (M < 0 || D <= 0 || (D & 7) || n_bins < 2) return FS2_EINVAL;
   if (M == 0) return FS2_OK;
   dim3 grid((M + 7) / 8);
   hipStream_t s = as_stream(stream);
   if (x_dtype == FS2_F32)
-    hipLaunchKernelGGL(variance_embed_kernel<float>, grid, dim3(256), 0, s, reinterpret_cast<float *>(x), pred, target,
-                       control, bins, n_bins - 1, table, M, D);
+    hipLaunchKernelGGL(variance_embed_kernel<float>, grid, dim3(256), 0, s, reinterpret_cast<const float *>(x),
+                       reinterpret_cast<float *>(out), pred, pred_out, target, control, bins, n_bins - 1, table, M, D,
+                       idx_out);
   else if (x_dtype == FS2_BF16)
-    hipLaunchKernelGGL(variance_embed_kernel<bf16>, grid, dim3(256), 0, s, reinterpret_cast<bf16 *>(x), pred, target,
-                       control, bins, n_bins - 1, table, M, D);
+    hipLaunchKernelGGL(variance_embed_kernel<bf16>, grid, dim3(256), 0, s, reinterpret_cast<const bf16 *>(x),
+                       reinterpret_cast<bf16 *>(out), pred, pred_out, target, control, bins, n_bins - 1, table, M, D,
+                       idx_out);
   else
     return FS2_EUNSUPPORTED;
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
 
+extern "C" int fs2_variance_embed(void *x, int x_dtype, float *pred, const float *target, float control,
+                                  const float *bins, int n_bins, const float *table, int M, int D,
+                                  fs2_stream_t stream) {
+  if (pred == nullptr) return FS2_EINVAL;
+  return variance_embed_launch(x, x_dtype, x, pred, pred, target, control, bins, n_bins, table, M, D, nullptr, stream);
+}
+
+extern "C" int fs2_variance_embed_ex(const void *x, int x_dtype, const float *value, const float *bins, int n_bins,
+                                     const float *table, int M, int D, void *out, int64_t *idx_out,
+                                     fs2_stream_t stream) {
+  if (value == nullptr) return FS2_EINVAL;
+  return variance_embed_launch(x, x_dtype, out, nullptr, nullptr, value, 1.0f, bins, n_bins, table, M, D, idx_out,
+                               stream);
+}
+
 extern "C" const char *fs2_version(void) { return "fs2hip 0.1.0 (gfx950)"; }
+
+#ifndef FS2_BUILD_ID
+#define FS2_BUILD_ID "unset"
+#endif
+extern "C" const char *fs2_build_id(void) { return FS2_BUILD_ID; }
 
 extern "C" const char *fs2_status_string(int status) {
   switch (status) {

@@ -145,6 +145,7 @@ class VpFusedDesc(ctypes.Structure):
 # name -> (restype, argtypes)
 SIGNATURES = {
     "fs2_version": (ctypes.c_char_p, []),
+    "fs2_build_id": (ctypes.c_char_p, []),
     "fs2_status_string": (ctypes.c_char_p, [_i]),
     "fs2_conv_cin_pad": (_i, [_i, _i]),
     "fs2_conv1d": (_i, [ctypes.POINTER(ConvDesc), _p]),
@@ -161,6 +162,8 @@ SIGNATURES = {
     "fs2_cond_vectors": (_i, [_p, _p, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p, _i, _i, _p, _p,
                               _p]),
     "fs2_variance_embed": (_i, [_p, _i, _p, _p, _f, _p, _i, _p, _i, _i, _p]),
+    "fs2_variance_embed_ex": (_i, [_p, _i, _p, _p, _i, _p, _i, _i, _p, _p, _p]),
+    "fs2_lr_backward": (_i, [_p, _p, _i, _i, _i, _i, _p, _p]),
     "fs2_lr_durations": (_i, [_p, _i, _f, _i, _i, _p, _p, _p, _p]),
     "fs2_lr_expand": (_i, [_p, _i, _p, _p, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p]),
     "fs2_pack_rows": (_i, [_p, _i, _p, _p, _i, _p, _p, _i64, _p]),
@@ -214,6 +217,26 @@ def header_symbols(header_path):
 
 
 _LIB = None
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "fs2hip.h")
+
+
+def source_build_id(csrc=CSRC, header=HEADER):
+    """sha256 (first 16 hex digits) of csrc/*.hip, csrc/*.h and include/fs2hip.h, in name order:
+    the id __graft_entry__.build_hip embeds as fs2_build_id(). None when the sources are absent."""
+    import hashlib
+
+    if not os.path.isdir(csrc) or not os.path.exists(header):
+        return None
+    h = hashlib.sha256()
+    for name in sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h"))):
+        h.update(name.encode())
+        with open(os.path.join(csrc, name), "rb") as f:
+            h.update(f.read())
+    with open(header, "rb") as f:
+        h.update(b"fs2hip.h")
+        h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def lib_path():
@@ -240,6 +263,14 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # provenance: the default in-tree library must have been built from the sources beside it
+    # (FS2_LIB overrides are A/B builds of other trees and are not checked)
+    if "FS2_LIB" not in os.environ:
+        want = source_build_id()
+        got = lib.fs2_build_id().decode()
+        if want is not None and got != want:
+            raise RuntimeError(f"fs2amd: {path} was built from other sources (fs2_build_id {got}, sources "
+                               f"{want}); rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
     _LIB = lib
     return lib
 

@@ -10,9 +10,17 @@ has run, so the path has one device->host read (runtime.host_meta) and cannot be
   variance adaptor and the LengthRegulator scan (duration rounding, cumulative frames, mel_len),
   plus the int32 meta vector [max(mel_len), sum(mel_len), out-of-vocabulary count];
 * the host reads the meta vector (one sync), raises IndexError on bad ids;
-* stage 2 (keyed by stage 1's key, T_out and the PostNet form; an LRU of ``max_stage2``
-  graphs): the LengthRegulator gather + PE, the decoder, mel_linear, the PostNet (valid-region
-  form when the batch is mostly padding, runtime._postnet) and the mel mask.
+* stage 2 (keyed by stage 1's key, the T bucket and the decoder's row bucket; an LRU of
+  ``max_stage2`` graphs): the LengthRegulator gather + PE and the decoder on packed rows
+  (runtime.decode_packed), captured for T_b = T_out rounded up to a multiple of ``t_step``: the
+  packed rows and their layout do not depend on T beyond T >= max(mel_len) (the padded-row map
+  and the grids' early-exiting tails do), so one graph serves every batch of the bucket and a
+  stream of distinct batches stops recapturing;
+* the T_out-shaped tail, issued eagerly behind the stage-2 replay (the host enqueues it while
+  the GPU runs the decoder): the packed layout over T_out, mel_linear into [B, T_out, n_mel], the
+  PostNet (valid-region form when the batch is mostly padding, runtime._postnet) and the mel mask.
+  Where the packed path does not apply (frame-level variance, a kernel-3 w_2) stage 2 is the whole
+  of runtime._stage2, keyed by the exact T_out.
 
 Each entry keeps the weight pack it was captured against (model.packed): when the weights change the
 pack is rebuilt, and the stale graphs are dropped and recaptured on the next call. Each call
@@ -31,10 +39,11 @@ from . import runtime as R
 
 
 class SynthGraphs:
-    def __init__(self, model, max_stage2=8, max_stage1=4):
+    def __init__(self, model, max_stage2=16, max_stage1=4, t_step=64):
         self.model = model
         self.max_stage2 = max_stage2
         self.max_stage1 = max_stage1
+        self.t_step = t_step
         self._g1 = OrderedDict()
         self._g2 = OrderedDict()
         self.captures = 0
@@ -123,16 +132,29 @@ class SynthGraphs:
         R.HOST_READS[0] += 1
         T_out, sum_len = R.check_meta(e1.meta_host, dev)
         pn_valid = R.postnet_valid_rows(B, T_out, sum_len)
-        # the decoder's packed launches are sized from the bucketed row count (runtime._stage2)
-        key2 = key1 + (T_out, pn_valid, ops.rows_bucket(sum_len, B * T_out))
+        st = e1.st
+        packed = R.packed_stage2_ok(P, st, st.x)
+        if packed:
+            # the decoder graph per T bucket (T <= the stored PE table: no per-length recompute)
+            T_b = -(-T_out // self.t_step) * self.t_step
+            if T_b > P.dec_pe.shape[0]:
+                T_b = T_out
+            # the decoder's packed launches are sized from the bucketed row count (runtime.decode_packed)
+            key2 = key1 + ("dec", T_b, ops.rows_bucket(sum_len, B * T_b))
+        else:
+            key2 = key1 + (T_out, pn_valid, ops.rows_bucket(sum_len, B * T_out))
         e2 = self._g2.get(key2)
         if e2 is not None and e2.e1 is not e1:  # captured on another (dropped) stage-1 entry's buffers
             del self._g2[key2]
             e2 = None
         if e2 is None:
-            def body():
-                mel, post, st = R._stage2(P, e1.g, e1.st, T_out, T_out, controls[0], pn_valid, sum_len)
-                return mel, post, R._mask(st.mel_len, T_out)
+            if packed:
+                def body():
+                    return R.decode_packed(P, st, st.x, st.mel_len, T_b, sum_len)
+            else:
+                def body():
+                    mel, post, st2 = R._stage2(P, e1.g, st, T_out, T_out, controls[0], pn_valid, sum_len)
+                    return mel, post, R._mask(st2.mel_len, T_out)
             graph, outs = self._capture(body)
             e2 = self._g2[key2] = SimpleNamespace(graph=graph, outs=outs, e1=e1)
             while len(self._g2) > self.max_stage2:
@@ -140,12 +162,21 @@ class SynthGraphs:
         else:
             self._g2.move_to_end(key2)
         e2.graph.replay()
-        st = e1.st
         # fresh output tensors (the graphs' buffers are overwritten by the next call), copied in one
         # multi-tensor launch instead of one copy each
-        srcs = [e2.outs[0], e2.outs[1], st.p_pred, st.e_pred, st.log_d, st.d_rounded, e1.src_masks, e2.outs[2],
-                st.mel_len]
+        srcs = [st.p_pred, st.e_pred, st.log_d, st.d_rounded, e1.src_masks, st.mel_len]
+        if not packed:
+            srcs += list(e2.outs)
         outs = [torch.empty_like(t) for t in srcs]
         torch._foreach_copy_(outs, srcs)
-        mel, post, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, mel_len = outs
+        p_pred, e_pred, log_d, d_rounded, src_masks, mel_len = outs[:6]
+        if packed:
+            # the T_out-shaped tail, eager (fresh outputs): the decoder rows of the replay are read
+            # before the next call's replay overwrites them (same stream)
+            x_dec, lay_b = e2.outs
+            lay = ops.SeqLayout(mel_len, T_out)
+            mel, post = R.mel_postnet(P, x_dec, lay, mel_len, pn_valid, sum_len)
+            mel_masks = R._mask(mel_len, T_out)
+        else:
+            mel, post, mel_masks = outs[6:]
         return (mel, post, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens.to(dev), mel_len)

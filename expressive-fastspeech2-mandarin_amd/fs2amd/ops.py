@@ -234,7 +234,10 @@ def conv1d(x, w_packed, bias, *, cin, ks, pad, compute, epilogue, out_dtype=None
     if layout is not None or src_layout is not None:
         lay = layout if layout is not None else src_layout
         B, T = lay.B, lay.T
-        assert x.dim() == 2 and x.shape[0] == lay.capacity, (tuple(x.shape), lay.capacity)
+        # a src_layout's packed rows may sit in a larger buffer (the decoder of a longer T bucket,
+        # fs2amd.graphs.SynthGraphs): only its first cu[B] <= capacity rows are read
+        assert x.dim() == 2 and (x.shape[0] == lay.capacity or (layout is None and x.shape[0] >= lay.capacity)), \
+            (tuple(x.shape), lay.capacity)
     else:
         B, T, _ = x.shape
     N = w_packed.shape[0] if n is None else n
@@ -607,6 +610,17 @@ def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=No
     return (out, qkv) if next_qkv is not None else out
 
 
+def _check_attention_args(qkv, lens, B, n_head, d_k, layout):
+    """The kernels read int64 key lengths, B of them, and a fused Q|K|V row of 3*H*dk values: a
+    mismatch would read the wrong lengths or past the buffers, so it raises here."""
+    if qkv.shape[-1] != 3 * n_head * d_k:
+        raise ValueError(f"attention: qkv has {qkv.shape[-1]} columns, expected 3*n_head*d_k = {3 * n_head * d_k}")
+    if layout is None:
+        if lens is None or lens.dtype != torch.int64 or lens.dim() != 1 or lens.numel() != B:
+            raise ValueError(f"attention: lens must be an int64 vector of the B = {B} key lengths, got "
+                             f"{None if lens is None else (lens.dtype, tuple(lens.shape))}")
+
+
 def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None, lse=None):
     """Key-padding-masked multi-head self-attention over a fused [B, T, 3*H*dk] projection
     (or packed [B*T, 3*H*dk] rows of a SeqLayout: lens unused). lse: optional f32 [rows, H] that
@@ -618,6 +632,7 @@ def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None, lse=No
     else:
         B, T, _ = qkv.shape
         shape = (B, T, n_head * d_k)
+    _check_attention_args(qkv, lens, B, n_head, d_k, layout)
     if out is None:
         out = torch.empty(*shape, device=qkv.device, dtype=qkv.dtype)
     L.check(_lib.fs2_attention(_ptr(qkv), _dt(qkv), _rows(qkv, "qkv"), _ptr(lens), B, T, n_head, d_k,
@@ -661,6 +676,7 @@ def attention_bwd(qkv, out, dout, lens, n_head, d_k, temperature, layout=None, l
         B, T = layout.B, layout.T
     else:
         B, T, _ = qkv.shape
+    _check_attention_args(qkv, lens, B, n_head, d_k, layout)
     dqkv = torch.empty(qkv.shape, device=qkv.device, dtype=torch.float32)
     ws = torch.empty(2 * B * T * n_head, device=qkv.device, dtype=torch.float32)
     L.check(_lib.fs2_attention_bwd(_ptr(qkv), _dt(qkv), _rows(qkv, "qkv"), _ptr(out), _rows(out, "out"), _ptr(dout),
@@ -888,6 +904,38 @@ def lr_expand(x, cum, mel_len, T_out, pe=None, out_dtype=None, index_map=False, 
                                _ptr(im), _ptr(out_layout.cu) if out_layout is not None else None, _stream(x)),
             "fs2_lr_expand")
     return (out, im) if index_map else out
+
+
+def lr_backward(dy, cum, n_phonemes):
+    """fs2_lr_backward: gradient of the LengthRegulator gather, dy f32 [B, T, D] -> dx f32
+    [B, n_phonemes, D] (per phoneme the sum of dy over its frames [cum[i-1], cum[i]) below T, in
+    frame order: deterministic)."""
+    _gpu(dy, cum)
+    dy = dy.float().contiguous()
+    B, T, D = dy.shape
+    if tuple(cum.shape) != (B, n_phonemes) or cum.dtype != torch.int32:
+        raise ValueError(f"lr_backward: cum must be int32 [{B}, {n_phonemes}], got {cum.dtype} {tuple(cum.shape)}")
+    dx = torch.empty(B, n_phonemes, D, device=dy.device, dtype=torch.float32)
+    L.check(_lib.fs2_lr_backward(_ptr(dy), _ptr(cum.contiguous()), B, int(n_phonemes), D, T, _ptr(dx), _stream(dy)),
+            "fs2_lr_backward")
+    return dx
+
+
+def variance_embed_ex(x, value, bins, table):
+    """fs2_variance_embed_ex (training form, out of place): idx = bucketize(value, bins) (int64,
+    torch.bucketize's right=False), out = x + table[idx]. Returns (out, idx)."""
+    _gpu(x, value, bins, table)
+    x = x.contiguous()
+    value = value.detach().float().contiguous()
+    M = value.numel()
+    D = x.shape[-1]
+    if x.numel() != M * D:
+        raise ValueError(f"variance_embed_ex: x {tuple(x.shape)} vs {M} values")
+    out = torch.empty_like(x)
+    idx = torch.empty(value.shape, device=x.device, dtype=torch.int64)
+    L.check(_lib.fs2_variance_embed_ex(_ptr(x), _dt(x), _ptr(value), _ptr(bins), bins.numel() + 1, _ptr(table), M, D,
+                                       _ptr(out), _ptr(idx), _stream(x)), "fs2_variance_embed_ex")
+    return out, idx
 
 
 def lr_fused(x, lens, T_out, pe=None, out_dtype=None, dur=None, logpred=False, d_control=1.0, cum=None, mel_len=None):

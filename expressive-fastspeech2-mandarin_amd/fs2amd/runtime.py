@@ -52,9 +52,39 @@ def _pe(P, which, n):
     return getattr(P, key)
 
 
-# Optional measurement hook: when a list, the decoder's FFN conv-k9 launches are bracketed by
-# HIP events on the launch stream (bench.py's live roofline timing of the dominant kernel).
+# Optional measurement hook: when a list, the forward's launches are bracketed by HIP events on
+# the launch stream, (start, end, tag) appended in launch order (bench.py's live roofline timing:
+# the decoder's fused FFN, every FFT-block GEMM launch, attention, the LengthRegulator). Decoder
+# FFN tags: "fc+ffn[+qkv]" / "ffn[+qkv]" / "ffn8" / "conv9"; the other launches "<stack>:<op>" with
+# stack "enc" / "dec" / "va" and op "qkv", "attn", "fc", "ffn", "conv1", "lr", "mel", "postnet".
 TIMERS = None
+_STACK = ["enc"]
+
+
+class _Timed:
+    """Context manager recording HIP events around the launches inside it when TIMERS is a list."""
+
+    __slots__ = ("tag", "e0")
+
+    def __init__(self, tag):
+        self.tag = tag
+
+    def __enter__(self):
+        if TIMERS is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if TIMERS is not None and exc[0] is None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            TIMERS.append((self.e0, e1, self.tag))
+        return False
+
+
+def _tm(op):
+    return _Timed(f"{_STACK[0]}:{op}")
 # fp8 calibration hook (FastSpeech2.calibrate_fp8): when a dict, every FFT block records
 # (max|h|, max|f|) of its FFN inputs over the valid rows, keyed by the layer's key.
 CALIB = None
@@ -89,93 +119,81 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
     if qkv is not None:
         pass
     elif q is not None and q.wqkv is not None and x8 is not None:
-        qkv = ops.conv1d(x8, q.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=L.FS2_FP8, epilogue=L.EPI_BIAS,
-                         out_dtype=dt, col_scale=q.cs_qkv, layout=layout)
+        with _tm("qkv"):
+            qkv = ops.conv1d(x8, q.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=L.FS2_FP8, epilogue=L.EPI_BIAS,
+                             out_dtype=dt, col_scale=q.cs_qkv, layout=layout)
     else:
-        qkv = ops.conv1d(x, lp.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_BIAS,
-                         out_dtype=dt, layout=layout)
-    att = ops.attention(qkv, lens, H, dk, float(np.power(dk, 0.5)), layout=layout)
+        with _tm("qkv"):
+            qkv = ops.conv1d(x, lp.wqkv, lp.bqkv, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_BIAS,
+                             out_dtype=dt, layout=layout)
+    with _tm("attn"):
+        att = ops.attention(qkv, lens, H, dk, float(np.power(dk, 0.5)), layout=layout)
     # cfg5: the fc+LN epilogue also writes the fp8 copy of h the e4m3 k=9 conv reads (one launch)
     h8 = None
     if q is None and getattr(lp, "wfcf", None) is not None and CALIB is None and ffn_pre_on() and \
             ffn_fused_ok(P, lp, x, layout) and ops.ffn_pre_ok(x, layout, lp.b1.numel(), lp.k1):
         # fc + residual + LN (SubLayers.py:54-55) in the fused FFN's prologue: no h round trip,
         # one launch less per block (the decoder's packed 112-row launches)
-        if timed and TIMERS is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
         fuse_qkv = nxt is not None and getattr(nxt, "wqf", None) is not None and \
             (nxt.fp8 is None or nxt.fp8.wqkv is None) and qkv_fused_on()
-        r = ops.ffn(x, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, layout=layout,
-                    next_qkv=(nxt.wqf, nxt.bqkv) if fuse_qkv else None, pre=(att, lp.wfcf, lp.bfc, lp.ln1))
+        tag = "fc+ffn+qkv" if fuse_qkv else "fc+ffn"
+        with _Timed(tag if timed else f"{_STACK[0]}:{tag}"):
+            r = ops.ffn(x, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, layout=layout,
+                        next_qkv=(nxt.wqf, nxt.bqkv) if fuse_qkv else None, pre=(att, lp.wfcf, lp.bfc, lp.ln1))
         y, qn = r if fuse_qkv else (r, None)
-        if timed and TIMERS is not None:
-            e1.record()
-            TIMERS.append((e0, e1, "fc+ffn+qkv" if fuse_qkv else "fc+ffn"))
         return y, None, qn
     if q is not None:
         h8 = (layout.empty(d_model, torch.float8_e4m3fn) if layout is not None
               else torch.empty(*x.shape[:-1], d_model, device=x.device, dtype=torch.float8_e4m3fn))
-    h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
-                   residual=x, ln=lp.ln1, lens=lens, layout=layout, out2=h8,
-                   out2_scale=1.0 / q.s_h if q is not None else 1.0)
+    with _tm("fc"):
+        h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN,
+                       out_dtype=dt, residual=x, ln=lp.ln1, lens=lens, layout=layout, out2=h8,
+                       out2_scale=1.0 / q.s_h if q is not None else 1.0)
     if q is not None and layout is not None and getattr(q, "w12_8", None) is not None and ffn8_on() \
             and CALIB is None and lp.k1 == 9 and lp.p1 == 4:
         # cfg5: the whole FFN as ONE e4m3 launch (fs2_ffn8: hidden quantised on chip, never in HBM)
-        if timed and TIMERS is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
         y8 = _fp8_like(x, layout, d_model) if next_s is not None else None
-        y = ops.ffn8(h8, h, q.w12_8, q.cs1, lp.b1, 1.0 / q.s_f, q.cs2, lp.b2, ln=lp.ln2, layout=layout, out8=y8,
-                     out8_scale=1.0 / next_s if next_s is not None else 1.0)
-        if timed and TIMERS is not None:
-            e1.record()
-            TIMERS.append((e0, e1, "ffn8"))
+        with _Timed("ffn8" if timed else f"{_STACK[0]}:ffn8"):
+            y = ops.ffn8(h8, h, q.w12_8, q.cs1, lp.b1, 1.0 / q.s_f, q.cs2, lp.b2, ln=lp.ln2, layout=layout, out8=y8,
+                         out8_scale=1.0 / next_s if next_s is not None else 1.0)
         return y, y8, None
     if q is not None:
         # cfg5: the FFN pair on e4m3 MFMA; the k=9 epilogue writes relu(.) directly as fp8 for w_2
-        if timed and TIMERS is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        f8 = ops.conv1d(h8, q.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=L.FS2_FP8,
-                        epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_FP8, out_scale=1.0 / q.s_f, col_scale=q.cs1,
-                        layout=layout)
-        if timed and TIMERS is not None:
-            e1.record()
-            TIMERS.append((e0, e1, "conv9"))
+        with _Timed("conv9" if timed else f"{_STACK[0]}:conv9"):
+            f8 = ops.conv1d(h8, q.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=L.FS2_FP8,
+                            epilogue=L.EPI_BIAS_RELU, out_dtype=L.FS2_FP8, out_scale=1.0 / q.s_f, col_scale=q.cs1,
+                            layout=layout)
         y8 = _fp8_like(x, layout, d_model) if next_s is not None else None
-        y = ops.conv1d(f8, q.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=L.FS2_FP8,
-                       epilogue=L.EPI_RES_LN, out_dtype=dt, residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1,
-                       addvec2=addvec2, layout=layout, col_scale=q.cs2, out2=y8,
-                       out2_scale=1.0 / next_s if next_s is not None else 1.0)
+        with _tm("conv1"):
+            y = ops.conv1d(f8, q.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=L.FS2_FP8,
+                           epilogue=L.EPI_RES_LN, out_dtype=dt, residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1,
+                           addvec2=addvec2, layout=layout, col_scale=q.cs2, out2=y8,
+                           out2_scale=1.0 / next_s if next_s is not None else 1.0)
         return y, y8, None
-    if timed and TIMERS is not None:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
     if ffn_fused_ok(P, lp, h, layout) and CALIB is None:
         # the whole FFN (conv-k9 + ReLU + conv-k1 + residual + LN + mask) as one launch: the
         # [rows, 1024] hidden stays on chip
         fuse_qkv = nxt is not None and getattr(nxt, "wqf", None) is not None and \
             (nxt.fp8 is None or nxt.fp8.wqkv is None) and qkv_fused_on()
-        r = ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, lens=lens, addvec1=addvec1,
-                    addvec2=addvec2, layout=layout, next_qkv=(nxt.wqf, nxt.bqkv) if fuse_qkv else None)
+        tag = "ffn+qkv" if fuse_qkv else "ffn"
+        with _Timed(tag if timed else f"{_STACK[0]}:{tag}"):
+            r = ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, lens=lens, addvec1=addvec1,
+                        addvec2=addvec2, layout=layout, next_qkv=(nxt.wqf, nxt.bqkv) if fuse_qkv else None)
         y, qn = r if fuse_qkv else (r, None)
-        if timed and TIMERS is not None:
-            e1.record()
-            TIMERS.append((e0, e1, "ffn+qkv" if fuse_qkv else "ffn"))
         return y, None, qn
-    f = ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=c, epilogue=L.EPI_BIAS_RELU, out_dtype=dt,
-                   layout=layout)
-    if timed and TIMERS is not None:
-        e1.record()
-        TIMERS.append((e0, e1, "conv9"))
+    with _Timed("conv9" if timed else f"{_STACK[0]}:conv9"):
+        f = ops.conv1d(h, lp.w1, lp.b1, cin=lp.c1, ks=lp.k1, pad=lp.p1, compute=c, epilogue=L.EPI_BIAS_RELU,
+                       out_dtype=dt, layout=layout)
     if CALIB is not None and lp.key is not None:
         rows = int(layout.cu[-1]) if layout is not None else None
         hv, fv = (h[:rows], f[:rows]) if rows is not None else (h, f)
         CALIB[lp.key]["h"] = float(hv.float().abs().max()) if hv.numel() else 0.0
         CALIB[lp.key]["f"] = float(fv.float().abs().max()) if fv.numel() else 0.0
-    return ops.conv1d(f, lp.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=c, epilogue=L.EPI_RES_LN, out_dtype=dt,
-                      residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2, layout=layout), None, None
+    with _tm("conv1"):
+        y = ops.conv1d(f, lp.w2, lp.b2, cin=lp.c2, ks=lp.k2, pad=lp.p2, compute=c, epilogue=L.EPI_RES_LN,
+                       out_dtype=dt, residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2,
+                       layout=layout)
+    return y, None, None
 
 
 FFN_FUSED_MIN_ROWS = 16384
@@ -224,6 +242,7 @@ def ffn_fused_ok(P, lp, h, layout):
 
 def _stack(P, layers, x, lens, layout=None, timed=False, addvecs=(None, None)):
     """FFT-block stack; in fp8 mode each block hands the next one an fp8 copy of its output."""
+    _STACK[0] = "dec" if timed else "enc"
     x8 = qkv = None
     n = len(layers)
     for i, lp in enumerate(layers):
@@ -387,11 +406,12 @@ def _stage1(P, va, g, p_control, d_control, defer_lr=False):
         # duration + pitch as ONE launch (each a whole predictor per 32-row tile; the pitch group
         # writes x + pitch embedding to a new buffer), then energy on it (modules.py:110-126)
         V = P.vpfused
-        dp, x = ops.vp_fused(x, V.dp, g.lens_src, embed=(1, g.p_targets, p_control, P.bins["pitch"],
-                                                           P.var_table["pitch"]))
-        st.log_d, st.p_pred = dp[0], dp[1]
-        en, x = ops.vp_fused(x, V.energy, g.lens_src, embed=(0, g.e_targets, p_control, P.bins["energy"],
-                                                             P.var_table["energy"]))  # p_control: :124-125
+        with _Timed("va:vp"):
+            dp, x = ops.vp_fused(x, V.dp, g.lens_src, embed=(1, g.p_targets, p_control, P.bins["pitch"],
+                                                               P.var_table["pitch"]))
+            st.log_d, st.p_pred = dp[0], dp[1]
+            en, x = ops.vp_fused(x, V.energy, g.lens_src, embed=(0, g.e_targets, p_control, P.bins["energy"],
+                                                                 P.var_table["energy"]))  # p_control: :124-125
         st.e_pred = en[0]
         st.x = x
     elif P.vpcols is not None and st.phoneme_p and st.phoneme_e and vp_columns_on():
@@ -448,27 +468,9 @@ def _stage2(P, g, st, T_out, T_dec, p_control, postnet_valid=False, rows_hint=No
     if not frame_level and T_dec == T_out and packed_decoder_ok(P):
         # packed decoder: only the dec_lens frames of each utterance are computed
         # (cfg2: 24.9k of 27.5k rows, cfg4: 135k of 249k); mel_linear scatters back to [B, T, n_mel]
-        if lr_fused_ok(x):
-            # scan (teacher-forced) + packed layout + gather (+ PE) in one launch
-            if st.cum is None:
-                x, lay, st.cum, st.mel_len, _ = ops.lr_fused(x, dec_lens, T_out, pe=_pe(P, "dec", T_out),
-                                                             out_dtype=P.act_dtype, dur=st.dur_pending)
-            else:
-                x, lay = ops.lr_fused(x, dec_lens, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype,
-                                      cum=st.cum, mel_len=st.mel_len)
-        else:
-            _ensure_lr(st)
-            lay = ops.SeqLayout(dec_lens, T_dec)
-            x = ops.lr_expand(x, st.cum, st.mel_len, T_out, pe=_pe(P, "dec", T_out), out_dtype=P.act_dtype,
-                              out_layout=lay)
-        # active rows when known on the host (free-running), rounded up (ops.rows_bucket) so that
-        # a captured stage-2 graph serves every batch of the bucket
-        lay.rows_hint = None if rows_hint is None else ops.rows_bucket(rows_hint, lay.capacity)
-        x = _stack(P, P.dec_layers, x, None, layout=lay, timed=True)
-        mel_bf = _mel_copy(P, x, (lay.B, lay.T))
-        mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
-                         out_dtype=L.FS2_F32, src_layout=lay, out2=mel_bf)
-        return mel, _postnet(P, mel, mel_bf, dec_lens if postnet_valid else None, rows_hint), st
+        x, lay = decode_packed(P, st, x, dec_lens, T_out, rows_hint)
+        mel, pn = mel_postnet(P, x, lay, dec_lens, postnet_valid, rows_hint)
+        return mel, pn, st
     # LR gather with the decoder's position encoding fused (frame-level variance needs the bare
     # expanded x first, so the PE add moves to a second pass in that configuration)
     _ensure_lr(st)
@@ -491,6 +493,50 @@ def _stage2(P, g, st, T_out, T_dec, p_control, postnet_valid=False, rows_hint=No
     mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
                      out_dtype=L.FS2_F32, out2=mel_bf)
     return mel, _postnet(P, mel, mel_bf, dec_lens if postnet_valid else None, rows_hint), st
+
+
+def decode_packed(P, st, x, dec_lens, T_lay, rows_hint=None):
+    """LengthRegulator gather (+ PE) into the packed layout of dec_lens over T_lay frames and the
+    decoder stack on those rows. The result does not depend on T_lay beyond T_lay >= max(dec_lens)
+    (the packed rows, cu and row_pos are those of the valid frames; only the padded-row maps and
+    the grids' early-exiting tails grow with it): fs2amd.graphs.SynthGraphs captures this part per
+    T bucket. Returns (packed x [B*T_lay, d_model], layout)."""
+    if lr_fused_ok(x):
+        # scan (teacher-forced) + packed layout + gather (+ PE) in one launch
+        with _Timed("va:lr"):
+            if st.cum is None:
+                x, lay, st.cum, st.mel_len, _ = ops.lr_fused(x, dec_lens, T_lay, pe=_pe(P, "dec", T_lay),
+                                                             out_dtype=P.act_dtype, dur=st.dur_pending)
+            else:
+                x, lay = ops.lr_fused(x, dec_lens, T_lay, pe=_pe(P, "dec", T_lay), out_dtype=P.act_dtype,
+                                      cum=st.cum, mel_len=st.mel_len)
+    else:
+        _ensure_lr(st)
+        lay = ops.SeqLayout(dec_lens, T_lay)
+        x = ops.lr_expand(x, st.cum, st.mel_len, T_lay, pe=_pe(P, "dec", T_lay), out_dtype=P.act_dtype,
+                          out_layout=lay)
+    # active rows when known on the host (free-running), rounded up (ops.rows_bucket) so that
+    # a captured stage-2 graph serves every batch of the bucket
+    lay.rows_hint = None if rows_hint is None else ops.rows_bucket(rows_hint, lay.capacity)
+    return _stack(P, P.dec_layers, x, None, layout=lay, timed=True), lay
+
+
+def mel_postnet(P, x, lay, dec_lens, postnet_valid=False, rows_hint=None):
+    """mel_linear from the packed decoder rows into the padded [B, lay.T, n_mel] contract (padded
+    frames get the bias, as the reference's masked decoder output gives) and the PostNet +
+    residual with the reference's padded semantics over lay.T frames."""
+    mel_bf = _mel_copy(P, x, (lay.B, lay.T))
+    with _Timed("dec:mel"):
+        mel = ops.conv1d(x, P.mel_w, P.mel_b, cin=P.d_model, ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
+                         out_dtype=L.FS2_F32, src_layout=lay, out2=mel_bf)
+    with _Timed("dec:postnet"):
+        pn = _postnet(P, mel, mel_bf, dec_lens if postnet_valid else None, rows_hint)
+    return mel, pn
+
+
+def packed_stage2_ok(P, st, x):
+    """The packed decoder path of _stage2 applies (phoneme-level variance, kernel-1 w_2, lr_fused)."""
+    return st.phoneme_p and st.phoneme_e and packed_decoder_ok(P) and lr_fused_ok(x)
 
 
 def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, max_src_len, mels, mel_lens,

@@ -79,6 +79,7 @@ class TrainStep:
         self._stream = None
         self._closed = False
         self._acc_pending = 0
+        self._calls = 0  # steps this TrainStep ran (warm-up counts these, not the resumed step number)
         self._fused_adam = False
         if self.flat:
             self._setup_flat_grads()
@@ -242,7 +243,11 @@ class TrainStep:
         return out
 
     def _graphed(self, batch):
-        if self.step_no <= self.warmup or (self._graph is not None and self._sig(batch) != self._graph[0]):
+        # warm-up by the calls of THIS TrainStep (at least one eager step, whatever `warmup` says): a
+        # step resumed from a checkpoint (current_step > warmup) still runs the lazy one-time setup
+        # (fused-Adam plan, dropout seed: synchronous host copies, illegal inside a capture) eagerly
+        self._calls += 1
+        if self._calls <= max(1, self.warmup) or (self._graph is not None and self._sig(batch) != self._graph[0]):
             # eager step body (same flat buffer, zeroed inside): detached losses, so no autograd
             # graph of a warm-up step outlives it into the capture
             self.optimizer._update_learning_rate()

@@ -14,7 +14,9 @@ Where the arithmetic runs:
   * self-attention: :class:`AttentionFn` — forward ``fs2_attention``, backward
     ``fs2_attention_bwd`` (flash-style dQ and dK/dV kernels, no T x T tensor);
   * LengthRegulator: the duration scan and source-index map on ``fs2_lr_durations`` /
-    ``fs2_lr_expand``, the differentiable gather (and its scatter-add gradient) in torch;
+    ``fs2_lr_expand`` (+ the decoder PE), its gradient a deterministic segmented sum
+    (``fs2_lr_backward``, LengthRegulatorFn); bucketize + pitch / energy embedding on
+    ``fs2_variance_embed_ex`` with the table gradient on ``fs2_embedding_bwd`` (VarianceEmbedFn);
   * LayerNorm, dropout, BatchNorm, embeddings, losses: torch on the device.
 Parity: tests/test_gpu_train.py against the reference's own gradients (train_grads.npz).
 """
@@ -617,29 +619,70 @@ def variance_predictor(vp, x, mask, training, compute, seed=None, salt=0):
     return out.masked_fill(mask, 0.0)
 
 
+class VarianceEmbedFn(torch.autograd.Function):
+    """x + Embedding(bucketize(value, bins)) (model/modules.py:80-100, x + emb :117-126) as one
+    fs2_variance_embed_ex launch; backward: dx = dy, the table's gradient on fs2_embedding_bwd over
+    the saved bucket indices (deterministic; gradient sink as EmbeddingFn). value carries no
+    gradient (bucketize is piecewise constant)."""
+
+    @staticmethod
+    def forward(ctx, x, value, bins, weight):
+        out, idx = ops.variance_embed_ex(x.detach(), value, bins, weight.detach())
+        ctx.save_for_backward(idx, weight)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        idx, weight = ctx.saved_tensors
+        gw = None
+        if ctx.needs_input_grad[3]:
+            if _SINK[0] and weight.grad is not None:
+                ops.embedding_bwd(idx, dy, weight.shape[0], None, out=weight.grad, accumulate=True)
+            else:
+                gw = ops.embedding_bwd(idx, dy, weight.shape[0], None)
+        return dy, None, None, gw
+
+
 def _variance_embed(va, kind, x, target, mask, control, training, compute, seed=None, salt=0):
-    """model/modules.py:80-100,117-126 (energy is scaled by p_control in the reference)."""
+    """model/modules.py:80-100,117-126 (energy is scaled by p_control in the reference): the
+    prediction, and x + the embedding of its bucket (fs2_variance_embed_ex, VarianceEmbedFn)."""
     pred = variance_predictor(getattr(va, f"{kind}_predictor"), x, mask, training, compute, seed, salt)
     bins = getattr(va, f"{kind}_bins")
     table = getattr(va, f"{kind}_embedding")
-    fused = seed is not None
-    if target is not None:
-        emb = _embed(table, torch.bucketize(target, bins), fused)
-    else:
+    if target is None:
         pred = pred * control
-        emb = _embed(table, torch.bucketize(pred, bins), fused)
-    return pred, emb
+    value = target if target is not None else pred
+    return pred, VarianceEmbedFn.apply(x.contiguous(), value.detach(), bins, table.weight)
 
 
-def _length_regulate(x, dur, max_len):
-    """LengthRegulator (model/modules.py:161-194): HIP scan + source-index map, torch gather."""
+class LengthRegulatorFn(torch.autograd.Function):
+    """LengthRegulator gather (model/modules.py:161-194 + pad, utils/tools.py:360-378) over T
+    output frames, optionally + the decoder's position encoding (transformer/Models.py:158-160)
+    in the same pass (fs2_lr_expand); backward: fs2_lr_backward, a deterministic per-phoneme
+    segmented sum over its frames (no scatter-add atomics)."""
+
+    @staticmethod
+    def forward(ctx, x, cum, mel_len, T, pe):
+        out = ops.lr_expand(x.detach().float(), cum, mel_len, T, pe=pe, out_dtype=L.FS2_F32)
+        ctx.save_for_backward(cum)
+        ctx.n, ctx.dtype = x.shape[1], x.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        (cum,) = ctx.saved_tensors
+        return ops.lr_backward(dy, cum, ctx.n).to(ctx.dtype), None, None, None, None
+
+
+def _length_regulate(x, dur, max_len, crop=None, pe=None):
+    """LengthRegulator (model/modules.py:161-194) on HIP: the duration scan, then the gather over
+    T = max_len (or max(mel_len): one host read) frames, cropped to ``crop`` frames (the training
+    decoder's max_seq_len, transformer/Models.py:154-162) and with ``pe`` [>= T, D] added when
+    given. Returns (x [B, T', D] f32, mel_len, T) with T the uncropped length."""
     cum, mel_len, _ = ops.lr_durations(dur if dur.dtype in (torch.int64, torch.float32) else dur.to(torch.int64))
     T = int(max_len) if max_len else int(mel_len.max().item())
-    im = ops.lr_expand(x.detach(), cum, mel_len, T, map_only=True)
-    B, Lx, D = x.shape
-    xz = torch.cat([x, x.new_zeros(B, 1, D)], 1)
-    idx = torch.where(im < 0, torch.full_like(im, Lx), im).long()
-    return torch.gather(xz, 1, idx.unsqueeze(-1).expand(-1, -1, D)), mel_len
+    Tc = T if crop is None else min(T, int(crop))
+    return LengthRegulatorFn.apply(x.contiguous(), cum, mel_len, Tc, pe), mel_len, T
 
 
 def _mask(lengths, width):
@@ -703,31 +746,33 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
     log_d = variance_predictor(va.duration_predictor, x, src_masks, training, compute, vseed, 1000)
     p_pred = e_pred = None
     if va.pitch_feature_level == "phoneme_level":
-        p_pred, emb = _variance_embed(va, "pitch", x, p_targets, src_masks, p_control, training, compute, vseed, 1002)
-        x = x + emb
+        p_pred, x = _variance_embed(va, "pitch", x, p_targets, src_masks, p_control, training, compute, vseed, 1002)
     if va.energy_feature_level == "phoneme_level":
-        e_pred, emb = _variance_embed(va, "energy", x, e_targets, src_masks, p_control, training, compute, vseed,
+        e_pred, x = _variance_embed(va, "energy", x, e_targets, src_masks, p_control, training, compute, vseed,
                                       1004)
-        x = x + emb
+    # phoneme-level variance (this config): the decoder crop and its position encoding join the
+    # LengthRegulator's gather (one pass); frame-level variance needs the bare expanded x first
+    phoneme_level = va.pitch_feature_level != "frame_level" and va.energy_feature_level != "frame_level"
+    crop = dec.max_seq_len if phoneme_level else None
+    pe = dec.position_enc[0].detach().contiguous() if phoneme_level else None
     if d_targets is not None:
-        x, mel_len = _length_regulate(x, d_targets, max_mel_len)
+        x, mel_len, T_lr = _length_regulate(x, d_targets, max_mel_len, crop, pe)
         d_rounded = d_targets
     else:
         d_rounded = torch.clamp(torch.round(torch.exp(log_d) - 1) * d_control, min=0)
-        x, mel_len = _length_regulate(x, d_rounded, None)
-        mel_masks = _mask(mel_len, int(mel_len.max().item()))
+        x, mel_len, T_lr = _length_regulate(x, d_rounded, None, crop, pe)
+        mel_masks = _mask(mel_len, T_lr)
     if va.pitch_feature_level == "frame_level":
-        p_pred, emb = _variance_embed(va, "pitch", x, p_targets, mel_masks, p_control, training, compute, vseed,
+        p_pred, x = _variance_embed(va, "pitch", x, p_targets, mel_masks, p_control, training, compute, vseed,
                                       1002)
-        x = x + emb
     if va.energy_feature_level == "frame_level":
-        e_pred, emb = _variance_embed(va, "energy", x, e_targets, mel_masks, p_control, training, compute, vseed,
+        e_pred, x = _variance_embed(va, "energy", x, e_targets, mel_masks, p_control, training, compute, vseed,
                                       1004)
-        x = x + emb
 
     # decoder (transformer/Models.py:139-171, training: crop to max_seq_len)
     T = min(x.shape[1], dec.max_seq_len)
-    x = x[:, :T] + dec.position_enc[:, :T, :]
+    if not phoneme_level:
+        x = x[:, :T] + dec.position_enc[:, :T, :]
     mel_masks = mel_masks[:, :T]
     dec_lens = torch.clamp((~mel_masks).sum(1), max=T)
     xb = None

@@ -388,6 +388,15 @@ int fs2_cond_vectors(const int64_t *speakers, const float *speaker_table, int n_
  */
 int fs2_variance_embed(void *x, int x_dtype, float *pred, const float *target, float control, const float *bins,
                        int n_bins, const float *table, int M, int D, fs2_stream_t stream);
+/*
+ * fs2_variance_embed_ex — the same bucketize + embedding add, out of place, for training
+ *   (model/modules.py:80-100 + VarianceAdaptor.forward :117-126 under autograd):
+ *   idx_out[m] = #{bins[i] < value[m]};  out[m, :] = x[m, :] + table[idx_out[m], :]
+ * value f32 [M] (the target, or the prediction already scaled by the control); idx_out int64 [M]
+ * (optional: the embedding backward's indices, fs2_embedding_bwd).
+ */
+int fs2_variance_embed_ex(const void *x, int x_dtype, const float *value, const float *bins, int n_bins,
+                          const float *table, int M, int D, void *out, int64_t *idx_out, fs2_stream_t stream);
 
 /*
  * VariancePredictor, column-split form (model/modules.py:197-250; VarianceAdaptor.forward
@@ -702,8 +711,20 @@ int fs2_reduce_batch_launch(fs2_reduce_batch *a, fs2_stream_t stream);
 int fs2_conv_wgrad_splits(int B, int T, int N, int C, int KS);
 int fs2_ln_bwd_parts(int64_t R);
 
-/* Library identification. */
+/*
+ * fs2_lr_backward — gradient of the LengthRegulator gather (training; model/modules.py:161-194 +
+ *   the decoder crop transformer/Models.py:154-162): dx[b, i, :] = sum over t in
+ *   [cum[b, i-1], cum[b, i]) with t < T of dy[b, t, :] (cum from fs2_lr_durations, int32 [B, L]; dy
+ *   f32 [B, T, D], dx f32 [B, L, D], contiguous). Frames summed in order: deterministic, no atomics.
+ */
+int fs2_lr_backward(const float *dy, const int32_t *cum, int B, int L, int D, int T, float *dx, fs2_stream_t stream);
+
+/* Library identification. fs2_build_id: sha256 (hex, first 16 digits) of the sources the library
+ * was compiled from (csrc/*.hip, csrc/*.h, include/fs2hip.h, in name order), embedded by the build
+ * (__graft_entry__.build_hip); fs2amd._lib.load() refuses a library whose id differs from the
+ * sources beside it. */
 const char *fs2_version(void);
+const char *fs2_build_id(void);
 const char *fs2_status_string(int status);
 
 /*

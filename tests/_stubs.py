@@ -55,17 +55,54 @@ def lr_durations(dur, logpred=False, d_control=1.0):
     return torch.cumsum(f, 1).int(), f.sum(1), None
 
 
-def lr_expand(x, cum, mel_len, T, pe=None, out_dtype=None, index_map=False, out_layout=None, map_only=False):
+def _index_map(cum, mel_len, T):
     t = torch.arange(T)[None, :, None]
     src = (cum[:, None, :].long() <= t).sum(-1)
-    im = torch.where(t[..., 0] < mel_len[:, None], src, torch.full_like(src, -1)).int()
+    return torch.where(t[..., 0] < mel_len[:, None], src, torch.full_like(src, -1)).int()
+
+
+def lr_expand(x, cum, mel_len, T, pe=None, out_dtype=None, index_map=False, out_layout=None, map_only=False):
+    im = _index_map(cum, mel_len, T)
     if map_only:
         return im
-    return torch.zeros(x.shape[0], T, x.shape[2]), im
+    B, L, D = x.shape
+    xz = torch.cat([x.float(), x.new_zeros(B, 1, D, dtype=torch.float32)], 1)
+    idx = torch.where(im < 0, torch.full_like(im, L), im).long()
+    out = torch.gather(xz, 1, idx.unsqueeze(-1).expand(-1, -1, D))
+    if pe is not None:
+        out = out + pe[:T]
+    return (out, im) if index_map else out
+
+
+def lr_backward(dy, cum, n):
+    B, T, D = dy.shape
+    im = _index_map(cum, cum[:, -1].long() if cum.shape[1] else torch.zeros(B, dtype=torch.long), T).long()
+    dx = torch.zeros(B, n + 1, D)
+    return dx.scatter_add_(1, torch.where(im < 0, n, im).unsqueeze(-1).expand(-1, -1, D), dy.float())[:, :n]
+
+
+def variance_embed_ex(x, value, bins, table):
+    idx = torch.bucketize(value.float(), bins)
+    return x + table[idx], idx
+
+
+def embedding_bwd(tokens, dy, V, padding_idx=None, out=None, accumulate=False):
+    D = dy.shape[-1]
+    g = torch.zeros(V, D).index_add_(0, tokens.reshape(-1).long(), dy.reshape(-1, D).float())
+    if padding_idx is not None:
+        g[padding_idx] = 0
+    if out is None:
+        return g
+    if accumulate:
+        out.add_(g)
+    else:
+        out.copy_(g)
+    return out
 
 
 def install_training_stubs(setattr_fn):
-    """Zero-filling kernels, CPU LR scan / masks, device check off, for fs2amd.training."""
+    """Zero-filling kernels, CPU LR scan / gather / its gradient, bucketize + embedding, masks,
+    device check off, for fs2amd.training."""
     from fs2amd import _lib, ops, training
 
     lib = ZeroingLib(_lib.load())
@@ -76,4 +113,7 @@ def install_training_stubs(setattr_fn):
     setattr_fn(training, "_mask", lambda l, w: torch.arange(int(w))[None, :] >= l[:, None])
     setattr_fn(ops, "lr_durations", lr_durations)
     setattr_fn(ops, "lr_expand", lr_expand)
+    setattr_fn(ops, "lr_backward", lr_backward)
+    setattr_fn(ops, "variance_embed_ex", variance_embed_ex)
+    setattr_fn(ops, "embedding_bwd", embedding_bwd)
     return lib

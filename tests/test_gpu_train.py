@@ -199,6 +199,119 @@ def test_graphed_train_step_equals_eager(gpu):
     _assert_params_close(pg, pe, _lr_sum(tc, 8))
 
 
+def test_graphed_train_step_bf16_resumed(gpu):
+    """The bf16 fused training path (FFTBlockFn / VPLayerFn / PostNetFn / EmbeddingFn, the pack
+    launch, the in-graph seed advance, the deferred finishes flushed inside the capture, fused Adam
+    on the sink-filled flat buffer) through TrainStep, captured, against the same step body run
+    eagerly (flat_grads=True), dropout off. Both resume at step 100 (> warmup): the graph must still
+    be captured after this TrainStep's own warm-up calls, not on its first call. Tolerances (bf16,
+    same kernels, non-deterministic f32 atomics only in the torch LR gather backward): losses rtol
+    1e-3; parameters as _assert_params_close with rtol 1e-3 and at most 0.05 % of the elements
+    differing by up to 2x the summed learning rates."""
+    from fs2amd import config as C
+    from fs2amd.data import synth_batch, to_device
+    from fs2amd.model import FastSpeech2
+    from fs2amd.trainer import TrainStep
+
+    pc, mc, _ = configs()
+    tc = C.ESD_TRAIN_CONFIG
+    runs = []
+    for graph in (False, True):
+        m = FastSpeech2(pc, mc)
+        m.load_state_dict(oracle_state_dict())
+        m = m.to(DEV).set_precision("bf16")
+        m.train_dropout = False
+        st = TrainStep(m, pc, mc, tc, device=torch.device(DEV), graph=graph, flat_grads=True, warmup=2,
+                       current_step=100)
+        base = synth_batch(8, 16, 40, seed=50, with_mels=True, pe_targets=True)
+        kept = []
+        for i in range(6):
+            b = dict(base, mels=base["mels"] * (1 + 0.1 * i), p_targets=base["p_targets"] + 0.05 * i)
+            kept.append(st(to_device(b, DEV))[0])
+        torch.cuda.synchronize()
+        runs.append(([float(l) for l in kept], {k: p.detach().clone() for k, p in m.named_parameters()}, st))
+    (le, pe, ste), (lg, pg, stg) = runs
+    assert stg._graph is not None, "the graph was never captured"
+    assert stg._calls == 6 and stg.step_no == 107
+    ste.close()
+    stg.close()
+    np.testing.assert_allclose(lg, le, rtol=1e-3)
+    o = tc["optimizer"]
+    lr_sum = sum(256 ** -0.5 * min(s ** -0.5, o["warm_up_step"] ** -1.5 * s) for s in range(101, 107))
+    nbad = total = 0
+    worst = 0.0
+    for k in pe:
+        bad = ~torch.isclose(pg[k], pe[k], rtol=1e-3, atol=1e-6)
+        nbad += int(bad.sum())
+        total += bad.numel()
+        if bad.any():
+            worst = max(worst, float((pg[k] - pe[k]).abs()[bad].max()))
+    assert nbad <= 5e-4 * total and worst <= 2 * lr_sum, (nbad, total, worst, lr_sum)
+
+
+def test_bf16_train_gradients_deterministic(gpu):
+    """Two identical bf16 forward + backward passes of the fused training path (dropout on, same
+    seed) give bit-identical gradients for every parameter: no float atomics anywhere in the step
+    (the LengthRegulator backward is a segmented sum, embeddings / weight gradients are ordered
+    sums, split-K partials are summed in a fixed order)."""
+    from fs2amd.data import loss_inputs, synth_batch, to_device
+    from fs2amd.loss import FastSpeech2Loss
+    from fs2amd.model import FastSpeech2
+
+    pc, mc, _ = configs()
+    m = FastSpeech2(pc, mc)
+    m.load_state_dict(oracle_state_dict())
+    m = m.to(DEV).train().set_precision("bf16")
+    a = to_device(synth_batch(16, 16, 64, seed=7, with_mels=True, pe_targets=True), DEV)
+    grads = []
+    for _ in range(2):
+        m._fs2_train_seed = torch.tensor([12345], dtype=torch.int64, device=DEV)
+        m.zero_grad(set_to_none=True)
+        out = m(**a)
+        FastSpeech2Loss(pc, mc)(loss_inputs(a), out)[0].backward()
+        torch.cuda.synchronize()
+        grads.append({k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 200
+    diff = [k for k in grads[0] if not torch.equal(grads[0][k], grads[1][k])]
+    assert not diff, diff[:10]
+
+
+def test_graph_train_step_grad_accumulation(gpu):
+    """grad_acc_step = 2 (train.py:89-97) through TrainStep(graph=True) — the flat-buffer
+    accumulation path (eager launches, the buffer zeroed every second call) — against the plain
+    eager step (per-parameter .grad accumulation, torch clip + Adam), fp32, dropout off: losses
+    rtol 1e-5, parameters as the graphed fp32 test."""
+    import copy
+
+    from fs2amd import config as C
+    from fs2amd.data import synth_batch, to_device
+    from fs2amd.model import FastSpeech2
+    from fs2amd.trainer import TrainStep
+
+    pc, mc, _ = configs()
+    tc = copy.deepcopy(C.ESD_TRAIN_CONFIG)
+    tc["optimizer"]["grad_acc_step"] = 2
+    runs = []
+    for graph in (False, True):
+        m = FastSpeech2(pc, mc)
+        m.load_state_dict(oracle_state_dict())
+        m = m.to(DEV).set_precision("fp32")
+        m.train_dropout = False
+        st = TrainStep(m, pc, mc, tc, device=torch.device(DEV), graph=graph, warmup=1)
+        base = synth_batch(4, 8, 20, seed=60, with_mels=True, pe_targets=True)
+        kept = []
+        for i in range(6):
+            b = dict(base, mels=base["mels"] * (1 + 0.1 * i))
+            kept.append(float(st(to_device(b, DEV))[0]))
+        torch.cuda.synchronize()
+        runs.append((kept, {k: p.detach().clone() for k, p in m.named_parameters()}, st))
+    (le, pe, ste), (lg, pg, stg) = runs
+    ste.close()
+    stg.close()
+    np.testing.assert_allclose(lg, le, rtol=1e-5)
+    _assert_params_close(pg, pe, _lr_sum(tc, 3))
+
+
 def test_ddp_step_over_rccl_equals_plain(gpu, tmp_path):
     """The data-parallel training path (train.py:52-53 DataParallel -> one process per GPU, DDP over
     RCCL): a single-rank "nccl" process group wraps TrainStep in DistributedDataParallel, so every

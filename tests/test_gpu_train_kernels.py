@@ -262,6 +262,50 @@ def test_embedding_bwd(ops, V, D, n, pad):
     assert float((o1.cpu().double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
 
 
+@pytest.mark.parametrize("B,L,T_cut", [(4, 23, None), (3, 64, 150), (2, 300, None)])
+def test_lr_backward_segmented_sum(ops, B, L, T_cut):
+    """fs2_lr_backward (the LengthRegulator gather's gradient, model/modules.py:161-194 under
+    autograd) against float64 autograd of the reference's expand / cat / pad: zero and long
+    durations, padded phonemes, a crop below max(mel_len) (T_cut: frames past it carry no
+    gradient); 1e-6 of the gradient scale, and bit-identical across calls (no atomics)."""
+    torch.manual_seed(B * L)
+    lens = torch.randint(1, L + 1, (B,))
+    lens[0] = L
+    dur = torch.randint(0, 12, (B, L)) * (torch.arange(L)[None] < lens[:, None])
+    dur[0, 1] = 40
+    cum, mel_len, _ = ops.lr_durations(dur.to(DEV))
+    T = int(mel_len.max()) if T_cut is None else T_cut
+    dy = torch.randn(B, T, 256)
+    x = torch.randn(B, L, 256, dtype=torch.float64, requires_grad=True)
+    rows = []
+    for b in range(B):
+        r = torch.cat([x[b, i].expand(int(dur[b, i]), -1) for i in range(L)], 0)
+        rows.append(F.pad(r, (0, 0, 0, max(0, T - r.shape[0])))[:T])
+    ref, = torch.autograd.grad(torch.stack(rows), x, dy.double())
+    g1 = ops.lr_backward(dy.to(DEV), cum, L)
+    g2 = ops.lr_backward(dy.to(DEV), cum, L)
+    torch.cuda.synchronize()
+    assert torch.equal(g1, g2)
+    assert float((g1.cpu().double() - ref).abs().max()) <= 1e-6 * float(ref.abs().max())
+
+
+def test_variance_embed_ex_equals_torch(ops):
+    """fs2_variance_embed_ex: bucket indices equal torch.bucketize (right=False) exactly, incl.
+    values on a boundary and outside the range; out = x + table[idx] exact in f32."""
+    torch.manual_seed(3)
+    bins = torch.linspace(-2.0, 8.0, 255)
+    table = torch.randn(256, 256)
+    M = 2000
+    v = torch.randn(M) * 4 + 3
+    v[:10] = bins[:10]  # exactly on boundaries
+    v[10:20] = torch.tensor([-1e9, 1e9, -2.0, 8.0, 8.5, -2.5, 0.0, 3.0, float(bins[100]), float(bins[254])])
+    x = torch.randn(M, 256)
+    out, idx = ops.variance_embed_ex(x.to(DEV), v.to(DEV), bins.to(DEV), table.to(DEV))
+    ref_idx = torch.bucketize(v, bins)
+    assert torch.equal(idx.cpu(), ref_idx)
+    assert torch.equal(out.cpu(), x + table[ref_idx])
+
+
 @pytest.mark.parametrize("frame_level", [False, True])
 def test_loss_fused_equals_torch(ops, frame_level, monkeypatch):
     """FastSpeech2Loss on fs2_loss_fwd / _bwd against its torch statement (FS2_LOSS_FUSED=0): the six

@@ -18,11 +18,13 @@ def test_library_exports_every_header_symbol():
 
     lib = _lib.load()
     declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
-    assert len(declared) == len(_lib.SIGNATURES) == 54
+    assert len(declared) == len(_lib.SIGNATURES) == 57
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
     assert b"gfx950" in lib.fs2_version()
+    # provenance: the loaded library was compiled from exactly these sources
+    assert lib.fs2_build_id().decode() == _lib.source_build_id()
     assert lib.fs2_status_string(1) == b"invalid argument"
     assert lib.fs2_conv_cin_pad(80, _lib.FS2_BF16) == 128 and lib.fs2_conv_cin_pad(80, _lib.FS2_F32) == 96
 

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Free-running cfg2 synthesis (SynthGraphs) repeated, for rocprofv3 kernel traces: the bench's
-free_running_cfg2 leg alone. --eager: the eager forward instead."""
+free_running_cfg2 leg alone, over 8 distinct seeded batches in rotation (as the bench).
+--eager: the eager forward instead."""
 import os
 import sys
 import time
@@ -18,18 +19,20 @@ def main():
 
     dev = torch.device("cuda:0")
     model, _, _ = bench.build_model(dev, "bf16")
-    b = to_device(synth_batch(64, 64, seed=1, teacher=False), dev)
-    run = (lambda: model(**b)) if "--eager" in sys.argv else SynthGraphs(model)
-    fn = (lambda: run()) if "--eager" in sys.argv else (lambda: run(**b))
+    bs = [to_device(synth_batch(64, 64, seed=1 + 1000 * i, teacher=False), dev) for i in range(8)]
+    synth = SynthGraphs(model)
+    fn = (lambda b: model(**b)) if "--eager" in sys.argv else (lambda b: synth(**b))
     with torch.no_grad():
-        for _ in range(3):
-            out = fn()
+        frames = [int(fn(b)[9].sum()) for b in bs]
         torch.cuda.synchronize()
+        cap = synth.captures
         t0 = time.perf_counter()
-        for _ in range(10):
-            out = fn()
+        for i in range(16):
+            out = fn(bs[i % 8])
         torch.cuda.synchronize()
-    print(f"{(time.perf_counter() - t0) / 10 * 1e3:.3f} ms per call, T_out {out[0].shape[1]}, frames {int(out[9].sum())}")
+    dt = (time.perf_counter() - t0) / 16
+    print(f"{dt * 1e3:.3f} ms per call, {sum(frames) / 8 / dt / 1e6:.2f} M frames/s, frames {frames}, "
+          f"captures {cap} + {synth.captures - cap} timed")
 
 
 if __name__ == "__main__":

@@ -6,22 +6,27 @@ A forward starts at its two length-mask launches. The bench's trace also holds e
 (warm-up, and the roofline's HIP-event-timed forwards, whose host-bound launches leave gaps); the
 graph replays are the forwards with (almost) no internal gaps, so those are the ones averaged.
 
-    python tools/fwd_gaps.py gpurun_out/trace/t/bench_kernel_trace.csv [--min-gap 1]
+    python tools/fwd_gaps.py gpurun_out/trace/t/bench_kernel_trace.csv [--min-gap 1] [--start embed_pe]
 """
 import csv
 import re
 import sys
 
 
-def forwards(rows):
-    st = [i for i, r in enumerate(rows) if "length_mask" in r["Kernel_Name"] and i + 1 < len(rows)
-          and "length_mask" in rows[i + 1]["Kernel_Name"]]
+def forwards(rows, start=None):
+    """Cut the trace into calls: at each `start` kernel (name substring) when given, else at the two
+    length-mask launches a teacher-forced forward begins with."""
+    if start:
+        st = [i for i, r in enumerate(rows) if start in r["Kernel_Name"]]
+    else:
+        st = [i for i, r in enumerate(rows) if "length_mask" in r["Kernel_Name"] and i + 1 < len(rows)
+              and "length_mask" in rows[i + 1]["Kernel_Name"]]
     return [rows[a:b] for a, b in zip(st, st[1:])]
 
 
-def main(path, min_gap=0.0):
+def main(path, min_gap=0.0, start=None):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    fw = forwards(rows)
+    fw = forwards(rows, start)
     n = max(set(len(f) for f in fw), key=lambda k: sum(len(f) == k for f in fw))  # the usual launch count
     inner = lambda f: sum(int(f[i]["Start_Timestamp"]) - int(f[i - 1]["End_Timestamp"]) for i in range(1, len(f))) / 1e3
     graphed = [f for f in fw if len(f) == n and inner(f) < 5.0]
@@ -43,4 +48,4 @@ def main(path, min_gap=0.0):
 
 if __name__ == "__main__":
     mg = float(sys.argv[sys.argv.index("--min-gap") + 1]) if "--min-gap" in sys.argv else -1e9
-    main(sys.argv[1], mg)
+    main(sys.argv[1], mg, sys.argv[sys.argv.index("--start") + 1] if "--start" in sys.argv else None)

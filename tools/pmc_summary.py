@@ -25,6 +25,9 @@ g = m.get("GRBM_GUI_ACTIVE")
 if g:
     print("--- derived")
     if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
-        print(f"MFMA busy / (GRBM*256 CUs... see guide)  {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (g * 256 * 4):.3f} (per-SIMD, /4)")
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (kernel cycles = GRBM / 8); the MFMA busy
+        # cycles are summed over all 1,024 SIMDs (MI355X_MICROARCH.md, PMC units)
+        print(f"MFMA busy per SIMD = busy / (1024 x GRBM/8)  {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * g / 8):.3f}")
+        print(f"kernel cycles (GRBM/8)                      {g / 8:.0f}")
     if "SQ_WAIT_ANY" in m and "SQ_BUSY_CYCLES" in m:
         print(f"WAIT_ANY / WAVE-cycles-ish          {m['SQ_WAIT_ANY'] / max(1, m.get('SQ_WAVE_CYCLES', m['SQ_BUSY_CYCLES'])):.3f}")
