@@ -160,6 +160,100 @@ def forward_timers(model, batch, n_fwd=6):
     return [[(tag, a.elapsed_time(b) / 1e3) for a, b, tag in tms] for tms in per_fwd]
 
 
+class ExternalEvents:
+    """HIP timing events recorded with hipEventRecordWithFlags(..., hipEventRecordExternal): inside
+    a stream capture each record becomes an event node of the graph (a plain hipEventRecord there
+    only orders the capture), so launches can be timed inside graph replays. Events come from a
+    pool created before the capture; read with hipEventElapsedTime after a replay."""
+
+    def __init__(self):
+        import ctypes
+
+        self.ct = ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so.7")  # the HIP runtime torch already mapped
+        self.hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        self.hip.hipEventRecordWithFlags.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+        self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+        self.hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self.pool, self.used = [], 0
+
+    def reserve(self, n):
+        while len(self.pool) < n:
+            ev = self.ct.c_void_p()
+            if self.hip.hipEventCreateWithFlags(self.ct.byref(ev), 0) != 0:
+                raise RuntimeError("hipEventCreateWithFlags failed")
+            self.pool.append(ev)
+
+    def record(self):
+        if self.used >= len(self.pool):
+            raise RuntimeError("ExternalEvents: pool exhausted (reserve more before the capture)")
+        ev = self.pool[self.used]
+        self.used += 1
+        st = torch.cuda.current_stream().cuda_stream
+        if self.hip.hipEventRecordWithFlags(ev, self.ct.c_void_p(st), 1) != 0:  # hipEventRecordExternal
+            raise RuntimeError("hipEventRecordWithFlags failed")
+        return ev
+
+    def elapsed_s(self, a, b):
+        ms = self.ct.c_float()
+        if self.hip.hipEventElapsedTime(self.ct.byref(ms), a, b) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value / 1e3
+
+    def close(self):
+        for ev in self.pool:
+            self.hip.hipEventDestroy(ev)
+        self.pool = []
+
+
+def forward_timers_graph(model, batch, n_replay=8):
+    """The forward captured ONCE as a HIP graph with an external event node before and after every
+    launch of interest (runtime.TIMERS / TIMER_RECORD), replayed n_replay times; returns [(tag,
+    seconds)] per replay. Each pair brackets the kernel plus the event node's packet processing
+    (~1-2 us), with no host in the loop: the graph-replay form of forward_timers."""
+    from fs2amd import runtime
+
+    dev = batch["texts"].device
+    prev = os.environ.get("FS2_STREAMS")
+    os.environ["FS2_STREAMS"] = "1"
+    ev = ExternalEvents()
+    ev.reserve(512)
+    per = []
+    g = None
+    try:
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s), torch.no_grad():
+            for _ in range(2):
+                model(**batch)
+            torch.cuda.synchronize(dev)
+            runtime.TIMER_RECORD = ev.record
+            runtime.TIMERS = []
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                model(**batch)
+            tms = runtime.TIMERS
+            runtime.TIMERS = None
+            runtime.TIMER_RECORD = None
+            g.replay()
+            torch.cuda.synchronize(dev)
+            for _ in range(n_replay):
+                g.replay()
+                s.synchronize()
+                per.append([(tag, ev.elapsed_s(a, b)) for a, b, tag in tms])
+    finally:
+        runtime.TIMERS = None
+        runtime.TIMER_RECORD = None
+        if prev is None:
+            del os.environ["FS2_STREAMS"]
+        else:
+            os.environ["FS2_STREAMS"] = prev
+        del g
+        torch.cuda.synchronize(dev)
+        ev.close()
+    return per
+
+
 def time_kernel_in_forward(model, batch, n_fwd=6, fwd=None):
     """Mean duration per tag of the timed launches inside real (eager) forwards (forward_timers).
     Returns {tag: (mean seconds, launches)}: decoder FFN tags "fc+ffn" (the last decoder block),
@@ -436,8 +530,9 @@ def cpu_baseline(batch_cpu, pc, mc, budget_s=20.0):
                       f"first {int(sub['texts'].shape[0])} utterances ({sub_frames} frames) on 1 thread, {dt1:.1f} s"}
 
 
-def load_traffic(dtype="bf16", fused=False):
-    name = "ffn_traffic.json" if fused else ("conv9_traffic.json" if dtype == "bf16" else f"conv9_{dtype}_traffic.json")
+def load_traffic(dtype="bf16", fused=False, pre=False):
+    name = ("ffn_pre_traffic.json" if pre else "ffn_traffic.json") if fused else \
+        ("conv9_traffic.json" if dtype == "bf16" else f"conv9_{dtype}_traffic.json")
     path = os.path.join(REPO, "profiles", name)
     if os.path.exists(path):
         with open(path) as f:
@@ -576,18 +671,35 @@ def extra_workloads(model, args, rank, device):
     record("cfg4_b256", b4, True, "B=256 x U{16..160} phonemes, teacher-forced durations U{2..10}")
     # the LengthRegulator stress shape (152 MB bf16): its launch inside eager cfg4
     # forwards, and the FFT-block GEMM fraction at B=256
-    brk4 = forward_breakdown(forward_timers(model, to_device(b4, device), n_fwd=3), b4,
-                             {"bf16": BF16_PEAK_TFLOPS, "fp8": FP8_PEAK_TFLOPS}.get(prec, F32_PEAK_TFLOPS))
+    pk4 = {"bf16": BF16_PEAK_TFLOPS, "fp8": FP8_PEAK_TFLOPS}.get(prec, F32_PEAK_TFLOPS)
+    try:
+        brk4 = forward_breakdown(forward_timers_graph(model, to_device(b4, device), n_replay=4), b4, pk4)
+    except Exception as e:  # noqa: BLE001
+        print(f"bench: cfg4 in-graph event timing failed: {e!r}", file=sys.stderr, flush=True)
+        brk4 = forward_breakdown(forward_timers(model, to_device(b4, device), n_fwd=3), b4, pk4)
     for k in ("lr", "fft_gemm"):
         if k in brk4:
             res["cfg4_b256"][k] = brk4[k]
     if prec == "bf16":
         cal = synth_batch(args.batch, args.phonemes, seed=1000 + rank)
-        model.set_precision("fp8")
-        model.calibrate_fp8(**to_device(cal, device))
         b5 = synth_batch(args.batch, args.phonemes, seed=1 + rank)
-        record("cfg5_fp8", b5, True,
-               "cfg2 with e4m3 FFN + Q|K|V GEMMs (static calibrated scales); tolerance vs bf16 in tests/test_gpu_fp8.py")
+        # cfg5's tolerance against bf16 on the benched batch: teacher-forced durations, pitch / energy
+        # pinned to the bf16 predictions (no bucket can flip), valid frames (tests/test_gpu_fp8.py)
+        with torch.no_grad():
+            bd = to_device(b5, device)
+            r16 = model(**bd)
+            pinned = dict(bd, p_targets=r16[2].clone(), e_targets=r16[3].clone())
+            r16 = model(**pinned)
+            model.set_precision("fp8")
+            model.calibrate_fp8(**to_device(cal, device))
+            r8 = model(**pinned)
+            valid = (torch.arange(r16[1].shape[1], device=device)[None, :] < r16[9][:, None])[..., None]
+            err = (r8[1].float() - r16[1].float()).abs().masked_select(valid)
+            tol = {"postnet_max_abs": round(float(err.max()), 5), "postnet_mean_abs": round(float(err.mean()), 6),
+                   "reference": "bf16 forward, same batch, pitch / energy pinned to its predictions, valid frames",
+                   "asserted": "tests/test_gpu_fp8.py::test_fp8_model_vs_bf16_reported"}
+        record("cfg5_fp8", b5, True, "cfg2 with e4m3 FFN + Q|K|V GEMMs (static calibrated scales)")
+        res["cfg5_fp8"]["tol_vs_bf16"] = tol
         # the fused e4m3 FFN (fs2_ffn8) against the dense fp8 peak: HIP events around its launches in
         # eager forwards (all 6 decoder blocks)
         t8 = time_kernel_in_forward(model, to_device(b5, device))
@@ -824,7 +936,7 @@ def main():
                                                  + ("conv_gemm_8p_kernel whole rounds + conv_gemm_kernel rows left"
                                                     if args.dtype == "bf16" else "conv_gemm_kernel")),
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": load_traffic(args.dtype, fused),
+                     "frac": round(achieved / peak, 4), "traffic": load_traffic(args.dtype, fused, pre),
                      "kernel_ms": round(kernel_s * 1e3, 4), "timing": timing,
                      "op_calls_timed": n_launch,
                      "kernel_ms_standalone_random": round(standalone_s * 1e3, 4),
@@ -835,14 +947,30 @@ def main():
                          "achieved": round((kernel_flops + 2.0 * frames * 256 * 768) / timed[qtag][0] / 1e12, 2)}}
                         if qtag in timed else {}),
                      "traffic_note": "2*FETCH_SIZE + WRITE_SIZE per launch (rocprofv3 PMC, profiles/"
-                                     + ("ffn_traffic.json)" if fused else "conv9_traffic.json)")},
+                                     + ("ffn_pre_traffic.json: this launch inside eager cfg2 forwards, round 5)"
+                                        if pre else "ffn_traffic.json)" if fused else "conv9_traffic.json)")},
     }
-    brk = forward_breakdown(fwd_t, batch_cpu, peak)
+    # the north-star fractions from the graph-replayed forward (event nodes around every launch);
+    # the eager-event form beside it for comparison
+    brk = None
+    if args.graph:
+        try:
+            brk = forward_breakdown(forward_timers_graph(model, batch), batch_cpu, peak)
+            brk["timing"] = ("HIP events recorded as graph nodes (hipEventRecordWithFlags, hipEventRecordExternal) "
+                             "around each launch of the forward captured once and replayed 8 times; each pair "
+                             "brackets the kernel plus the event packet's processing")
+        except Exception as e:  # noqa: BLE001  (diagnostics: never lose the headline line)
+            print(f"bench: in-graph event timing failed: {e!r}", file=sys.stderr, flush=True)
+    eager_brk = forward_breakdown(fwd_t, batch_cpu, peak)
+    if brk is None:
+        brk = eager_brk
     if "fft_gemm" in brk:
         rec["fft_gemm_frac"] = brk["fft_gemm"]["frac"]
     if "lr" in brk:
         rec["lr_hbm_frac"] = brk["lr"]["frac"]
     rec["forward_breakdown"] = brk
+    if brk is not eager_brk:
+        rec["forward_breakdown_eager"] = {k: eager_brk[k] for k in ("fft_gemm", "lr") if k in eager_brk}
     if table is not None:
         rec["decoder_ops"] = table
     if rank == 0 and world == 1 and args.cpu_baseline:

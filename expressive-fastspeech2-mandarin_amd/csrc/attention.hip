@@ -575,23 +575,31 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
     qf[s] = *reinterpret_cast<bf16x8 *>(&v);
   }
 
+  // K / V tile DMA: piece p = w + NWV it is key rows 4p .. 4p + 3 (lane: row 4p + (lane >> 4), 16-byte
+  // chunk lane & 15 under the row swizzle). The per-lane part of each piece's source offset is
+  // fixed (dbase); a tile adds k0 rows through the scalar offset, and a key past the sequence gets
+  // an out-of-range offset (the buffer load returns zeros: V rows of masked keys must be finite)
   const int prow = lane >> 4, pch = lane & 15;
+  uint32_t dbase[PPW];
+#pragma unroll
+  for (int it = 0; it < PPW; ++it) {
+    const int r = 4 * (w + NWV * it) + prow;
+    dbase[it] = (seq_base + (uint32_t)r) * row_bytes + (uint32_t)(pch ^ kv32_swz(r)) * 16u + (uint32_t)((H + h) * DK) * 2u;
+  }
+  const uint32_t v_minus_k = (uint32_t)(H * DK) * 2u;  // V columns sit H * DK after K's
   auto dma = [&](int k0, int buf) __attribute__((always_inline)) {
     char *Kb = smem + buf * STG;
     char *Vb = Kb + KTT * 256;
+    const int lim = T - k0;
+    const uint32_t so = (uint32_t)k0 * row_bytes;
 #pragma unroll
     for (int it = 0; it < PPW; ++it) {
       const int p = w + NWV * it;
-      const int r = 4 * p + prow;
-      const int lc = pch ^ kv32_swz(r);
-      const int key = k0 + r;
-      const uint32_t base = key < T ? (seq_base + key) * row_bytes + (uint32_t)lc * 16u : 0x80000000u;
-      const uint32_t koff = base == 0x80000000u ? base : base + (uint32_t)((H + h) * DK) * 2u;
-      const uint32_t voff = base == 0x80000000u ? base : base + (uint32_t)((2 * H + h) * DK) * 2u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(Kb + p * 1024), 16, koff,
-                                               0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(Vb + p * 1024), 16, voff,
-                                               0, 0, 0);
+      const uint32_t vo = 4 * p + prow < lim ? dbase[it] : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(Kb + p * 1024), 16, vo, so,
+                                               0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(Vb + p * 1024), 16, vo,
+                                               so + v_minus_k, 0, 0);
     }
   };
 
@@ -611,7 +619,27 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
   // addresses row q, dims 4p .. 4p + 3 (chunk 2 (gq & 1) + (p >> 1), byte 8 (p & 1))
   const int gq = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
   const int vrow = 4 * (gq >> 1) + tq;
-  auto tile = [&](int kt, auto masked_tag) __attribute__((always_inline)) {
+  // per-lane LDS offsets of every fragment read, computed once: the row swizzle depends on row & 15
+  // only, so a K read is koff[s] + 8 KiB kb and a V read voff[db][half] + 4 KiB s, and with the
+  // ring slot a template constant each read is one VGPR + an immediate offset (the per-read
+  // address arithmetic was 46 of the ~270 VALU per tile and wave)
+  int koff[DK / 16], voff[DK / 32][2];
+#pragma unroll
+  for (int s = 0; s < DK / 16; ++s) koff[s] = r32 * 256 + (((2 * s + hh) ^ kv32_swz(r32)) << 4);
+#pragma unroll
+  for (int db = 0; db < DK / 32; ++db) {
+    const int ch = 4 * db + 2 * (gq & 1) + (tp >> 1);
+    voff[db][0] = kv32_off(vrow, ch) + 8 * (tp & 1);
+    voff[db][1] = kv32_off(8 + vrow, ch) + 8 * (tp & 1);
+  }
+  // online softmax with a lazy running max (FlashAttention-4's threshold): the running reference
+  // m_run moves (and O / l are rescaled) only when some lane's tile maximum exceeds it by more than
+  // 2^kLazy in the exponentiated domain; otherwise p = exp2((s - m_run) * scale) stays <= 2^kLazy,
+  // well inside bf16 / f32 range. The result is the same softmax (O / l and lse are taken against
+  // the same reference); the 64-element O rescale no longer runs on nearly every tile.
+  constexpr float kLazy = 8.0f;
+  auto tile = [&](int kt, auto slot_tag, auto masked_tag) __attribute__((always_inline)) {
+    constexpr int SLOT = decltype(slot_tag)::value;
     constexpr bool MASKED = decltype(masked_tag)::value;
     const int k0 = kt * KTT;
     const int ahead = ntiles - 1 - kt;
@@ -623,20 +651,29 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
     __builtin_amdgcn_s_barrier();
     if (kt + NST - 1 < ntiles) dma(k0 + (NST - 1) * KTT, (kt + NST - 1) % NST);
     if (!active) return;
-    const char *Kb = smem + (kt % NST) * STG;
+    const char *Kb = smem + SLOT * STG;
     const char *Vb = Kb + KTT * 256;
 
-    // S^T[key][query] for the tile's two 32-key blocks
+    // S^T[key][query] for the tile's two 32-key blocks, interleaved: the K fragments of step s + 1
+    // are read while the two MFMAs of step s run (64 cycles of matrix work cover each read)
     f32x16 sacc[2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
+    bf16x8 kf[2][2];
 #pragma unroll
-      for (int s = 0; s < DK / 16; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(Kb + kv32_off(kb * 32 + r32, 2 * s + hh));
-        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kb], 0, 0, 0);
+    for (int kb = 0; kb < 2; ++kb) kf[0][kb] = *reinterpret_cast<const bf16x8 *>(Kb + kb * 32 * 256 + koff[0]);
+#pragma unroll
+    for (int s = 0; s < DK / 16; ++s) {
+      if (s + 1 < DK / 16) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          kf[(s + 1) & 1][kb] = *reinterpret_cast<const bf16x8 *>(Kb + kb * 32 * 256 + koff[s + 1]);
       }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s & 1][kb], qf[s], sacc[kb], 0, 0, 0);
     }
     if constexpr (MASKED) {  // keys >= len -> -inf
       const int lim = len - k0 - 4 * hh;
@@ -655,17 +692,17 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
       auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
       mx = max_nn(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
     }
-    const float m_new = mx;  // includes m_run
-    if (__builtin_amdgcn_ballot_w64(m_new != m_run) != 0) {
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2);
+    // first tile: m_run = -inf, so the difference is +inf and every lane takes its maximum
+    if (__builtin_amdgcn_ballot_w64((mx - m_run) * scale_log2 > kLazy) != 0) {
+      const float alpha = __builtin_amdgcn_exp2f((m_run - mx) * scale_log2);
       l_run *= alpha;
 #pragma unroll
       for (int i = 0; i < DK / 32; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) oacc[i][r] = __builtin_fmaf(oacc[i][r], alpha, 0.0f);
+      m_run = mx;
     }
-    m_run = m_new;
-    const float mc = -m_new * scale_log2;
+    const float mc = -m_run * scale_log2;
     float sx = 0.f, sy = 0.f;
     bf16x8 pf[KTT / 16];
 #pragma unroll
@@ -687,9 +724,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
       bf16x8 vf[DK / 32];
 #pragma unroll
       for (int db = 0; db < DK / 32; ++db) {
-        const int ch = 4 * db + 2 * (gq & 1) + (tp >> 1);
-        const char *v0 = Vb + kv32_off(16 * s + vrow, ch) + 8 * (tp & 1);
-        const char *v1 = Vb + kv32_off(16 * s + 8 + vrow, ch) + 8 * (tp & 1);
+        const char *v0 = Vb + s * 16 * 256 + voff[db][0];
+        const char *v1 = Vb + s * 16 * 256 + voff[db][1];
         auto lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)v0);
         auto hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)v1);
         __builtin_memcpy(&vf[db], &lo, 8);
@@ -700,8 +736,35 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
         oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[db], pf[s], oacc[db], 0, 0, 0);
     }
   };
-  for (int kt = 0; kt + 1 < ntiles; ++kt) tile(kt, std::false_type{});
-  if (ntiles > 0) tile(ntiles - 1, std::true_type{});
+  // the ring slot of tile kt is kt % NST: the loop walks NST tiles per iteration with constant
+  // slots; the last (masked) tile dispatches on its slot
+  static_assert(NST == 2 || NST == 3, "ring stages");
+  using F = std::false_type;
+  using Tr = std::true_type;
+  int kt = 0;
+  for (; kt + NST < ntiles; kt += NST) {
+    tile(kt, std::integral_constant<int, 0>{}, F{});
+    tile(kt + 1, std::integral_constant<int, 1>{}, F{});
+    if constexpr (NST == 3) tile(kt + 2, std::integral_constant<int, 2 % NST>{}, F{});
+  }
+  for (; kt + 1 < ntiles; ++kt) {
+    const int sl = kt % NST;
+    if (sl == 0)
+      tile(kt, std::integral_constant<int, 0>{}, F{});
+    else if (NST == 2 || sl == 1)
+      tile(kt, std::integral_constant<int, 1>{}, F{});
+    else
+      tile(kt, std::integral_constant<int, 2 % NST>{}, F{});
+  }
+  if (ntiles > 0) {
+    const int sl = kt % NST;
+    if (sl == 0)
+      tile(kt, std::integral_constant<int, 0>{}, Tr{});
+    else if (NST == 2 || sl == 1)
+      tile(kt, std::integral_constant<int, 1>{}, Tr{});
+    else
+      tile(kt, std::integral_constant<int, 2 % NST>{}, Tr{});
+  }
 
   // the two halves' sums (same m); O^T[d][query r32], d = 32 db + (r & 3) + 8 (r >> 2) + 4 hh
   {

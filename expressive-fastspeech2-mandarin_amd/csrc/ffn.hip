@@ -456,6 +456,18 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  // trace builds: 32 stamp slots per workgroup -- past the split-K partials in the workspace for the
+  // split form (probe-sized workspace), else output row a.M - 1 - block (the packed capacity tail)
+  auto trace_dump = [&](int last) {
+    if (FFN_TRACE) {
+      uint64_t *o = S > 1 ? reinterpret_cast<uint64_t *>(static_cast<char *>(p.part) + p.part_bytes + 256u * blockIdx.x)
+                          : reinterpret_cast<uint64_t *>(static_cast<char *>(a.out) + (size_t)(a.M - 1 - blockIdx.x) * a.os * 2);
+      for (int i = 0; i < 21; ++i) o[i] = *reinterpret_cast<const uint64_t *>(smem + SMEM + 8 * i);
+      o[29] = (uint64_t)split;
+      o[30] = (uint64_t)last;
+      o[31] = (uint64_t)21;
+    }
+  };
   stamp(0);
 
   // chunk c's hidden slice: H[m][j] = bf16(relu(acc1 + b1)); lane holds 4 consecutive j of row m
@@ -532,11 +544,11 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     // chunk's hidden columns starting at this wave's own block (units 2w, 2w + 1: its own writes,
     // no barrier); the barrier that makes the other waves' blocks visible comes after that first
     // unit, so it absorbs the skew between the waves' write_h instead of stalling on it.
-    stamp(2 + 2 * c);
+    stamp(2 + 2 * (c - c0));
     bar();
     write_h(c);
     __builtin_amdgcn_s_waitcnt(kLgkm0);
-    stamp(3 + 2 * c);
+    stamp(3 + 2 * (c - c0));
     read_h(2 * w, f0);
     const uint32_t next1 = c + 1 < cend ? base1(c + 1) : 0u;  // past the last unit: harmless reloads
     static_for<NK2>([&](auto Q) {
@@ -611,6 +623,10 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    stamp(19);
+    if (FFN_TRACE && !*flag) {  // trace builds: the stamps of a split that hands off and exits
+      if (tid == 0) trace_dump(0);
+    }
     if (!*flag) return;
     __syncthreads();  // flag read by every wave before the epilogue reuses the slot
     // sum in split order into the dead H^T accumulators. MB = 4: every other split's partial is
@@ -670,6 +686,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) acc2[nb][mb] = acc1[nb][mb];
+    stamp(20);
   }
   {
     float *red = reinterpret_cast<float *>(smem + RED_OFF);
@@ -907,11 +924,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   if (FFN_TRACE) {
     stamp(3 + 2 * NCH);
     __syncthreads();
-    if (tid == 0) {  // trace build: the stamps go to output row a.M - 1 - block (packed capacity tail)
-      uint64_t *o = reinterpret_cast<uint64_t *>(static_cast<char *>(a.out) + (size_t)(a.M - 1 - blockIdx.x) * a.os * 2);
-      for (int i = 0; i < 19; ++i) o[i] = *reinterpret_cast<const uint64_t *>(smem + SMEM + 8 * i);
-      o[31] = (uint64_t)19;
-    }
+    if (tid == 0) trace_dump(1);
   }
 }
 
@@ -1034,7 +1047,8 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   p.prefetch = ffn_prefetch;
   if (S > 1) {
     if (d->splitk_ws == nullptr || ntiles > 1024 ||
-        d->splitk_ws_bytes < 4096 + (int64_t)ntiles * S * kPartBytes || (int64_t)ntiles * S * kPartBytes >= (1LL << 31))
+        d->splitk_ws_bytes < 4096 + (int64_t)ntiles * S * kPartBytes + (FFN_TRACE ? 256LL * (ntiles * S + 8) : 0) ||
+        (int64_t)ntiles * S * kPartBytes >= (1LL << 31))
       return FS2_EINVAL;
     p.cnt = static_cast<int *>(d->splitk_ws);
     p.part = static_cast<char *>(d->splitk_ws) + 4096;

@@ -13,6 +13,7 @@
 // zero. An optional f32 position-encoding row is added on the way out (Decoder input,
 // transformer/Models.py:158-160) so the expanded tensor is written to HBM exactly once.
 #include <cstdlib>
+#include <type_traits>
 
 #include "fs2_common.h"
 
@@ -248,9 +249,9 @@ struct LrFusedArgs {
   int32_t *rowmap;
 };
 
-template <typename TX, typename TO, bool HAS_PE>
+template <typename TX, typename TO, bool HAS_PE, int ROWS>
 __global__ __launch_bounds__(256) void lr_fused_kernel(LrFusedArgs a) {
-  constexpr int ROWS = 32, UNR = ROWS / 8;
+  constexpr int UNR = ROWS / 8 < 8 ? ROWS / 8 : 8;  // 16-byte pieces in flight per thread
   const int b = blockIdx.y, t0 = blockIdx.x * ROWS;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int L = a.L, T = a.T, D = a.D;
@@ -653,15 +654,32 @@ extern "C" int fs2_lr_fused(const void *x, int x_dtype, const void *dur, int dur
   a.cu = cu;
   a.row_pos = reinterpret_cast<int2 *>(row_pos);
   a.rowmap = rowmap;
-  const dim3 grid((unsigned)((T_out + 31) / 32), (unsigned)B);
+  // frames per workgroup (FS2_LR_ROWS = 32 / 64 / 128, A/B): every workgroup re-derives its
+  // utterance's scan and packed offset, so more frames per workgroup amortise that prologue
+  static const int rows_env = [] {
+    const char *e = getenv("FS2_LR_ROWS");
+    const int v = e != nullptr ? atoi(e) : 32;
+    return (v == 64 || v == 128) ? v : 32;
+  }();
+  const int R = rows_env;
+  const dim3 grid((unsigned)((T_out + R - 1) / R), (unsigned)B);
   hipStream_t s = as_stream(stream);
   auto go = [&](auto TXv, auto TOv) {
     using TX = decltype(TXv);
     using TO = decltype(TOv);
-    if (pe != nullptr)
-      hipLaunchKernelGGL((lr_fused_kernel<TX, TO, true>), grid, dim3(256), 0, s, a);
+    auto launch = [&](auto RC) {
+      constexpr int RR = decltype(RC)::value;
+      if (pe != nullptr)
+        hipLaunchKernelGGL((lr_fused_kernel<TX, TO, true, RR>), grid, dim3(256), 0, s, a);
+      else
+        hipLaunchKernelGGL((lr_fused_kernel<TX, TO, false, RR>), grid, dim3(256), 0, s, a);
+    };
+    if (R == 128)
+      launch(std::integral_constant<int, 128>{});
+    else if (R == 64)
+      launch(std::integral_constant<int, 64>{});
     else
-      hipLaunchKernelGGL((lr_fused_kernel<TX, TO, false>), grid, dim3(256), 0, s, a);
+      launch(std::integral_constant<int, 32>{});
   };
   if (x_dtype == FS2_BF16 && out_dtype == FS2_BF16)
     go(bf16{}, bf16{});

@@ -55,6 +55,12 @@ class SynthGraphs:
         for k in [k for k in self._g2 if k[:len(key1)] == key1]:
             del self._g2[k]
 
+    def _side_stream(self, dev):
+        s = getattr(self, "_side", None)
+        if s is None or s.device != dev:
+            s = self._side = torch.cuda.Stream(dev)
+        return s
+
     def close(self):
         """Release every captured graph (and the memory pools they hold)."""
         torch.cuda.synchronize()
@@ -161,22 +167,35 @@ class SynthGraphs:
                 self._g2.popitem(last=False)
         else:
             self._g2.move_to_end(key2)
-        e2.graph.replay()
-        # fresh output tensors (the graphs' buffers are overwritten by the next call), copied in one
-        # multi-tensor launch instead of one copy each
+        cur = torch.cuda.current_stream(dev)
         srcs = [st.p_pred, st.e_pred, st.log_d, st.d_rounded, e1.src_masks, st.mel_len]
-        if not packed:
+        if packed:
+            # fresh copies of stage 1's outputs (its buffers are overwritten by the next call's
+            # replay) on a side stream, concurrent with the decoder graph: stage 1 has completed
+            # (the host read above), and the caller's stream waits for the copies before anything
+            # later on it (the returned tensors' users, the next call's stage-1 replay)
+            side = self._side_stream(dev)
+            with torch.cuda.stream(side):
+                outs = [torch.empty_like(t) for t in srcs]
+                torch._foreach_copy_(outs, srcs)
+            e2.graph.replay()
+        else:
+            e2.graph.replay()
             srcs += list(e2.outs)
-        outs = [torch.empty_like(t) for t in srcs]
-        torch._foreach_copy_(outs, srcs)
+            outs = [torch.empty_like(t) for t in srcs]
+            torch._foreach_copy_(outs, srcs)  # fresh outputs, one multi-tensor launch
         p_pred, e_pred, log_d, d_rounded, src_masks, mel_len = outs[:6]
         if packed:
             # the T_out-shaped tail, eager (fresh outputs): the decoder rows of the replay are read
             # before the next call's replay overwrites them (same stream)
             x_dec, lay_b = e2.outs
-            lay = ops.SeqLayout(mel_len, T_out)
-            mel, post = R.mel_postnet(P, x_dec, lay, mel_len, pn_valid, sum_len)
-            mel_masks = R._mask(mel_len, T_out)
+            lens = st.mel_len  # stage 1's buffer: read here, before the next call's replay
+            lay = ops.SeqLayout(lens, T_out)
+            mel, post = R.mel_postnet(P, x_dec, lay, lens, pn_valid, sum_len)
+            mel_masks = R._mask(lens, T_out)
+            cur.wait_stream(side)
+            for t in outs:
+                t.record_stream(cur)
         else:
             mel, post, mel_masks = outs[6:]
         return (mel, post, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens.to(dev), mel_len)

@@ -58,7 +58,19 @@ def _pe(P, which, n):
 # FFN tags: "fc+ffn[+qkv]" / "ffn[+qkv]" / "ffn8" / "conv9"; the other launches "<stack>:<op>" with
 # stack "enc" / "dec" / "va" and op "qkv", "attn", "fc", "ffn", "conv1", "lr", "mel", "postnet".
 TIMERS = None
+# optional event recorder for TIMERS (callable() -> event handle recorded on the current stream):
+# bench.py installs hipEventRecordWithFlags(..., hipEventRecordExternal), which a stream capture
+# turns into event nodes of the graph, so the launches are timed inside graph replays
+TIMER_RECORD = None
 _STACK = ["enc"]
+
+
+def _record_event():
+    if TIMER_RECORD is not None:
+        return TIMER_RECORD()
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
 
 
 class _Timed:
@@ -71,15 +83,12 @@ class _Timed:
 
     def __enter__(self):
         if TIMERS is not None:
-            self.e0 = torch.cuda.Event(enable_timing=True)
-            self.e0.record()
+            self.e0 = _record_event()
         return self
 
     def __exit__(self, *exc):
         if TIMERS is not None and exc[0] is None:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            TIMERS.append((self.e0, e1, self.tag))
+            TIMERS.append((self.e0, _record_event(), self.tag))
         return False
 
 

@@ -720,7 +720,7 @@ int fs2_ln_bwd_parts(int64_t R);
 int fs2_lr_backward(const float *dy, const int32_t *cum, int B, int L, int D, int T, float *dx, fs2_stream_t stream);
 
 /* Library identification. fs2_build_id: sha256 (hex, first 16 digits) of the sources the library
- * was compiled from (csrc/*.hip, csrc/*.h, include/fs2hip.h, in name order), embedded by the build
+ * was compiled from (the .hip and .h files of csrc and include/fs2hip.h, in name order), embedded by the build
  * (__graft_entry__.build_hip); fs2amd._lib.load() refuses a library whose id differs from the
  * sources beside it. */
 const char *fs2_version(void);

@@ -237,17 +237,30 @@ def test_cfg4_variable_length_fp32_checksums(model):
     ok = np.isclose((post * valid).sum((1, 2)).numpy(), z["ck_post_valid_sum"], rtol=0, atol=1.0)
     ok &= np.isclose((post.abs() * valid).sum((1, 2)).numpy(), z["ck_post_valid_abs"], rtol=2e-5, atol=0)
     ok &= np.isclose(post.sum((1, 2)).numpy(), z["ck_post_all_sum"], rtol=0, atol=2.0)
-    # fp32 summation order differs from the reference's: a pitch / energy prediction within
-    # ~1e-7 of a bucket edge can land in the neighbouring bucket (the utterance then differs by
-    # one embedding row). Allowed only where a prediction is that close to an edge, <= 2 of 256.
+    # fp32 summation order differs from the reference's: a pitch / energy prediction that sits on a
+    # bucket edge can land in the neighbouring bucket (the utterance then differs by one embedding
+    # row). Allowed, <= 2 of 256, only where that is what happened: the utterance has a phoneme
+    # whose bucket differs between this run and the reference, and there the two predictions agree
+    # within FLIP_EPS (so the reference value lies within FLIP_EPS of the edge between them).
+    # Energy flips count only in an utterance without a pitch flip (a flipped pitch row changes
+    # the energy predictor's input).
+    FLIP_EPS = 4e-6
     bad = np.flatnonzero(~ok)
     assert len(bad) <= 2, bad
     va = model.variance_adaptor
     src_valid = ~z["out_src_masks"]
+    pbins, ebins = va.pitch_bins.cpu().numpy(), va.energy_bins.cpu().numpy()
     for b in bad:
-        dp = np.abs(z["out_p_pred"][b][src_valid[b]][:, None] - va.pitch_bins.cpu().numpy()[None, :]).min()
-        de = np.abs(z["out_e_pred"][b][src_valid[b]][:, None] - va.energy_bins.cpu().numpy()[None, :]).min()
-        assert min(dp, de) < 1e-4, (b, dp, de)
+        v = src_valid[b]
+        gp, rp = _np(got[2])[b][v], z["out_p_pred"][b][v]
+        ge, re = _np(got[3])[b][v], z["out_e_pred"][b][v]
+        fp = np.searchsorted(pbins, gp, side="left") != np.searchsorted(pbins, rp, side="left")
+        fe = np.searchsorted(ebins, ge, side="left") != np.searchsorted(ebins, re, side="left")
+        d = np.abs(gp - rp)[fp] if fp.any() else np.abs(ge - re)[fe]
+        print(f"cfg4 fp32 flip: utterance {b}: pitch flips {int(fp.sum())}, energy flips {int(fe.sum())}, "
+              f"|d pred| at the flips {d.tolist()}")
+        assert fp.any() or fe.any(), (b, "checksum mismatch without a bucket flip")
+        assert float(d.max()) <= FLIP_EPS, (b, d.tolist())
     np.testing.assert_allclose(_np(got[2]), z["out_p_pred"], atol=5e-4)
     keep = np.setdiff1d(np.arange(len(ok)), bad)  # energy sees the flipped pitch embedding
     np.testing.assert_allclose(_np(got[3])[keep], z["out_e_pred"][keep], atol=5e-4)

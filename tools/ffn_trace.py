@@ -64,5 +64,58 @@ def main():
         print(f"{lab:28s} mean {float(d.mean()):9.0f}  max {float(d.max()):9.0f} cycles")
 
 
+def main_enc(nsplit=4, tile_rows=64, with_qkv=True):
+    """The encoder's split-hidden FFN (64 x 64 padded rows, the forward's launch form): per-workgroup
+    phase stamps from the split-K workspace (past the partials), every split included."""
+    import bench
+    from fs2amd import ops
+    from fs2amd.data import synth_batch, to_device
+
+    dev = torch.device("cuda:0")
+    model, _, _ = bench.build_model(dev, "bf16")
+    b = to_device(synth_batch(64, 64, seed=1), dev)
+    P = model.packed(dev)
+    el, nx = P.enc_layers[0], P.enc_layers[1]
+    x = torch.randn(64, 64, 256, generator=torch.Generator().manual_seed(0)).to(dev, torch.bfloat16)
+    kw = dict(ks=9, pad=4, ln=el.ln2, lens=b["src_lens"], nsplit=nsplit, tile_rows=tile_rows)
+    if with_qkv:
+        kw["next_qkv"] = (nx.wqf, nx.bqkv)
+    for _ in range(3):
+        ops.ffn(x, el.w12, el.b1, el.b2, **kw)
+    torch.cuda.synchronize()
+    ws = ops.splitk_workspace(dev)
+    MB = tile_rows // 16
+    ntiles = 4096 // tile_rows
+    part = ntiles * nsplit * 4 * 4 * MB * 64 * 16
+    nwg = (ntiles * nsplit + 7) & ~7
+    st = ws[4096 + part: 4096 + part + 256 * nwg].view(torch.int64).reshape(nwg, 32).cpu()
+    ok = st[:, 31] == 21
+    st = st[ok].double()
+    last = st[:, 30] == 1
+    t0 = st[:, 0].min()
+    lab = {1: "prologue (x tile)", 2: "gemm1", 3: "write_h", 10: "gemm2 (+ drain start)", 19: "partials stored + counter",
+           20: "partial sums loaded (last)", 18: "LN epilogue to staging (last)", 13: "stores + Q|K|V (last)"}
+    print(f"workgroups traced {int(ok.sum())}, last arrivers {int(last.sum())}; start skew "
+          f"{float((st[:, 0] - t0).max()):.0f} cycles")
+
+    def seg(rows, a, b_):
+        d = rows[:, b_] - rows[:, a]
+        return float(d.mean()), float(d.max())
+    for a, b_, name in ((0, 1, "prologue: x tile, first units"), (1, 2, "gemm1 (1 chunk)"), (2, 3, "write_h"),
+                        (3, 10, "gemm2"), (10, 19, "partial store + counter")):
+        m, mx = seg(st, a, b_)
+        print(f"{name:32s} mean {m:9.0f} max {mx:9.0f} cycles")
+    L = st[last]
+    for a, b_, name in ((19, 20, "last: partial loads + sum"), (20, 18, "last: LN epilogue"),
+                        (18, 13, "last: stores + next Q|K|V"), (0, 13, "last: total")):
+        m, mx = seg(L, a, b_)
+        print(f"{name:32s} mean {m:9.0f} max {mx:9.0f} cycles")
+    end_all = float((L[:, 13] - t0).max())
+    print(f"kernel span (first start -> last end) {end_all:.0f} cycles")
+
+
 if __name__ == "__main__":
-    main()
+    if "--enc" in sys.argv:
+        main_enc(with_qkv="--no-qkv" not in sys.argv)
+    else:
+        main()

@@ -111,6 +111,12 @@ def main():
         x4 = torch.randn(256, b4["texts"].shape[1], 256, generator=g).to(dev, dt)
         cum4, ml4, _ = ops.lr_durations(b4["d_targets"])
         fn = lambda: ops.lr_expand(x4, cum4, ml4, int(b4["max_mel_len"]), pe=P.dec_pe, out_dtype=P.act_dtype)
+    elif a.kernel in ("lr_fused", "lr_fused4"):  # the forward's one-launch LR (scan + layout + gather + PE)
+        bb = b if a.kernel == "lr_fused" else to_device(synth_batch(256, 16, 160, seed=1), dev)
+        Bq, Lq = bb["texts"].shape
+        xq = torch.randn(Bq, Lq, 256, generator=g).to(dev, dt)
+        Tq = int(bb["max_mel_len"])
+        fn = lambda: ops.lr_fused(xq, bb["mel_lens"], Tq, pe=P.dec_pe, out_dtype=P.act_dtype, dur=bb["d_targets"])
     elif a.kernel == "postnet":
         y = rnd(B, T, 512)
         pl = P.postnet[1]
