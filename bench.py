@@ -190,14 +190,18 @@ class ExternalEvents:
         ev = self.pool[self.used]
         self.used += 1
         st = torch.cuda.current_stream().cuda_stream
-        if self.hip.hipEventRecordWithFlags(ev, self.ct.c_void_p(st), 1) != 0:  # hipEventRecordExternal
-            raise RuntimeError("hipEventRecordWithFlags failed")
+        rc = self.hip.hipEventRecordWithFlags(ev, self.ct.c_void_p(st), 1)  # hipEventRecordExternal
+        if rc != 0:
+            self.hip.hipGetLastError()  # clear the sticky error: later launches check it
+            raise RuntimeError(f"hipEventRecordWithFlags failed: hipError {rc}")
         return ev
 
     def elapsed_s(self, a, b):
         ms = self.ct.c_float()
-        if self.hip.hipEventElapsedTime(self.ct.byref(ms), a, b) != 0:
-            raise RuntimeError("hipEventElapsedTime failed")
+        rc = self.hip.hipEventElapsedTime(self.ct.byref(ms), a, b)
+        if rc != 0:
+            self.hip.hipGetLastError()
+            raise RuntimeError(f"hipEventElapsedTime failed: hipError {rc}")
         return ms.value / 1e3
 
     def close(self):

@@ -167,6 +167,9 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   // ---- tap validity of this lane's activation rows: bit tap of vmask[mb] is set when the row
   // shifted by tap - pad stays inside its sequence (sequence position / length)
   int vmask[MB];
+  // padded rows with lengths: bit mb set when this lane's row of block mb is padding (t >= lens[b]),
+  // read here, beside the x tile DMA, rather than in the LN epilogue's dependent chain
+  int padmask = 0;
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + mb * 16 + (lane & 15);
@@ -179,6 +182,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       } else {
         tpos = m % T;
         tlen = T;
+        if (a.lens != nullptr && (int64_t)tpos >= a.lens[m / T]) padmask |= 1 << mb;
       }
     }
     int v = 0;
@@ -353,6 +357,16 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       for (int mb = 0; mb < 4; ++mb) {
         const int r = 64 * ps + 16 * mb + hr;
         const float rstd = 1.0f / sqrtf(var[mb] * (1.0f / kD) + p.eps1);
+        // padded rows (t >= lens[b], the encoder's [B, L] form): h = masked_fill(LN1(.), 0)
+        // (transformer/Layers.py:25-26), the zeros the FFN's conv taps read past a sequence's end
+        float keep = 1.0f;
+        if (a.lens != nullptr) {
+          const int gm = m0 - pad + r;
+          if (gm >= 0 && gm < M) {
+            const int bb = gm / T;
+            keep = (int64_t)(gm - bb * T) < a.lens[bb] ? 1.0f : 0.0f;
+          }
+        }
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) {
           const int n = w * 64 + jb * 16 + 4 * hq;
@@ -360,10 +374,10 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
           const float4 be = *reinterpret_cast<const float4 *>(p.be1 + n);
           const f32x4 d = a0[jb][mb];
           bf16x4 o;
-          o[0] = (bf16)(d[0] * rstd * g.x + be.x);
-          o[1] = (bf16)(d[1] * rstd * g.y + be.y);
-          o[2] = (bf16)(d[2] * rstd * g.z + be.z);
-          o[3] = (bf16)(d[3] * rstd * g.w + be.w);
+          o[0] = (bf16)((d[0] * rstd * g.x + be.x) * keep);
+          o[1] = (bf16)((d[1] * rstd * g.y + be.y) * keep);
+          o[2] = (bf16)((d[2] * rstd * g.z + be.z) * keep);
+          o[3] = (bf16)((d[3] * rstd * g.w + be.w) * keep);
           if (r < XROWS) *reinterpret_cast<bf16x4 *>(smem + X_OFF + r * XPITCH + n * 2) = o;
         }
       }
@@ -776,9 +790,8 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
         bool masked = false;
         int bb = 0;
         if constexpr (padded) {
-          const int gm = m0 + m;
-          bb = gm / T;
-          masked = a.lens != nullptr && (int64_t)(gm - bb * T) >= a.lens[bb];
+          bb = (m0 + m) / T;
+          masked = (padmask >> mb) & 1;
         }
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) {
@@ -1009,7 +1022,11 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
     if (d->pre_w == nullptr || d->pre_b == nullptr || d->pre_gamma == nullptr || d->pre_beta == nullptr ||
         d->pre_att_row_stride < kD || (d->pre_att_row_stride & 7) || d->pre_att == d->out)
       return FS2_EINVAL;
-    if (d->rows_dev == nullptr || S != 1 || d->tile_rows == 64 || d->KS != 9 || d->F != 1024) return FS2_EUNSUPPORTED;
+    // packed 112-row unsplit launches (the decoder) or padded [B, T] rows with lengths, 64-row tiles
+    // in the split-hidden form (the encoder)
+    const bool dec_form = d->rows_dev != nullptr && S == 1 && d->tile_rows != 64;
+    const bool enc_form = d->rows_dev == nullptr && d->tile_rows == 64;
+    if (!(dec_form || enc_form) || d->KS != 9 || d->F != 1024) return FS2_EUNSUPPORTED;
     const int64_t ab = M64 * d->pre_att_row_stride * 2;
     if (ab >= (1LL << 31)) return FS2_EUNSUPPORTED;
     p.att = reinterpret_cast<const bf16 *>(d->pre_att);
@@ -1069,7 +1086,9 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   using I3 = std::integral_constant<int, 3>;
   using C4 = std::integral_constant<int, 4>;
   using C2 = std::integral_constant<int, 2>;
-  if (pre)
+  if (pre && MB == 4)
+    hipLaunchKernelGGL((ffn_fused_kernel<9, 4, 4, true>), dim3(nwg), dim3(256), 0, s, p);
+  else if (pre)
     hipLaunchKernelGGL((ffn_fused_kernel<9, 4, 7, true>), dim3(nwg), dim3(256), 0, s, p);
   else if (d->KS == 9 && nch == 4)
     go(I9{}, C4{});

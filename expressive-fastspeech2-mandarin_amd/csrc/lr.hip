@@ -247,6 +247,7 @@ struct LrFusedArgs {
   int32_t *cu;
   int2 *row_pos;
   int32_t *rowmap;
+  int store;  // bf16 frame stores: 0 non-temporal, 1 plain, 2 write-through (sc1); FS2_LR_STORE (A/B)
 };
 
 template <typename TX, typename TO, bool HAS_PE, int ROWS>
@@ -373,7 +374,15 @@ __global__ __launch_bounds__(256) void lr_fused_kernel(LrFusedArgs a) {
           bf16x8 o;
 #pragma unroll
           for (int q = 0; q < 8; ++q) o[q] = (bf16)v[u][q];
-          __builtin_nontemporal_store(o, reinterpret_cast<bf16x8 *>(ob + (int64_t)e * 8));
+          bf16x8 *dst = reinterpret_cast<bf16x8 *>(ob + (int64_t)e * 8);
+          if (a.store == 0)
+            __builtin_nontemporal_store(o, dst);
+          else if (a.store == 1)
+            *dst = o;
+          else
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o),
+                                                   __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 16, 0x00020000), 0u,
+                                                   0, 16);
         } else {
           store8(ob + (int64_t)e * 8, v[u]);
         }
@@ -654,6 +663,11 @@ extern "C" int fs2_lr_fused(const void *x, int x_dtype, const void *dur, int dur
   a.cu = cu;
   a.row_pos = reinterpret_cast<int2 *>(row_pos);
   a.rowmap = rowmap;
+  static const int store_env = [] {
+    const char *e = getenv("FS2_LR_STORE");
+    return e == nullptr ? 0 : (e[0] == 'p' ? 1 : e[0] == 's' ? 2 : 0);
+  }();
+  a.store = store_env;
   // frames per workgroup (FS2_LR_ROWS = 32 / 64 / 128, A/B): every workgroup re-derives its
   // utterance's scan and packed offset, so more frames per workgroup amortise that prologue
   static const int rows_env = [] {

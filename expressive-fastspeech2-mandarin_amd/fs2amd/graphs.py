@@ -38,6 +38,16 @@ from . import ops
 from . import runtime as R
 
 
+def _spin_until_landed(meta_host, budget_s=0.05):
+    """Poll the pinned meta vector until its first entry leaves -1 (the device->host copy landed),
+    for at most budget_s (the caller's stream synchronize covers the rest)."""
+    import time
+
+    t_end = time.perf_counter() + budget_s
+    while int(meta_host[0]) == -1 and time.perf_counter() < t_end:
+        pass
+
+
 class SynthGraphs:
     def __init__(self, model, max_stage2=16, max_stage1=4, t_step=64):
         self.model = model
@@ -132,8 +142,13 @@ class SynthGraphs:
         ks = [k for k, v in x.items() if v is not None]
         torch._foreach_copy_([e1.static[k] for k in ks], [x[k] for k in ks], non_blocking=True)  # one launch
         e1.graph.replay()
-        # the one host read
+        # the one host read: the copy lands in pinned memory whose first entry (max mel_len >= 0)
+        # the host set to -1; spinning on it returns as soon as the bytes land (a blocking stream
+        # synchronize parks the thread and the wake-up cost ~30-60 us per call); the synchronize
+        # after it then returns at once and orders the rest of the copy
+        e1.meta_host[0] = -1
         e1.meta_host.copy_(e1.meta, non_blocking=True)
+        _spin_until_landed(e1.meta_host)
         torch.cuda.current_stream(dev).synchronize()
         R.HOST_READS[0] += 1
         T_out, sum_len = R.check_meta(e1.meta_host, dev)
@@ -170,15 +185,16 @@ class SynthGraphs:
         cur = torch.cuda.current_stream(dev)
         srcs = [st.p_pred, st.e_pred, st.log_d, st.d_rounded, e1.src_masks, st.mel_len]
         if packed:
-            # fresh copies of stage 1's outputs (its buffers are overwritten by the next call's
-            # replay) on a side stream, concurrent with the decoder graph: stage 1 has completed
-            # (the host read above), and the caller's stream waits for the copies before anything
-            # later on it (the returned tensors' users, the next call's stage-1 replay)
+            # the decoder graph first (the GPU has been idle since the read), then fresh copies of
+            # stage 1's outputs (its buffers are overwritten by the next call's replay) on a side
+            # stream, concurrent with the decoder: stage 1 has completed (the host read above), and
+            # the caller's stream waits for the copies before anything later on it (the returned
+            # tensors' users, the next call's stage-1 replay)
+            e2.graph.replay()
             side = self._side_stream(dev)
             with torch.cuda.stream(side):
                 outs = [torch.empty_like(t) for t in srcs]
                 torch._foreach_copy_(outs, srcs)
-            e2.graph.replay()
         else:
             e2.graph.replay()
             srcs += list(e2.outs)

@@ -533,9 +533,18 @@ def ffn_launch_rows(x, layout):
 
 
 def ffn_pre_ok(x, layout, F, ks):
-    """fs2_ffn's fc + residual + LN prologue (pre_att) covers packed 112-row, unsplit launches of the
-    k = 9, F = 1024 FFN (the decoder's)."""
-    return layout is not None and ks == 9 and F == 1024 and ffn_form(ffn_launch_rows(x, layout), F) == (112, 1)
+    """fs2_ffn's fc + residual + LN prologue (pre_att) covers the k = 9, F = 1024 FFN as packed
+    112-row unsplit launches (the decoder's) and, opt-in (FS2_FFN_PRE_ENC=1), as padded [B, T]
+    launches on 64-row tiles (the encoder's split-hidden form; padded rows are masked in the
+    prologue). Off by default: every split of a tile recomputes the prologue, and the encoder
+    launch grew by more than the fc launch it replaces (51-53 vs 41.6 + 10.4 us per block in
+    eager forwards, profiles/r5f)."""
+    if ks != 9 or F != 1024:
+        return False
+    form = ffn_form(ffn_launch_rows(x, layout), F)
+    if layout is not None:
+        return form == (112, 1)
+    return form[0] == 64 and os.environ.get("FS2_FFN_PRE_ENC", "0") == "1"
 
 
 def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=None, layout=None, out=None,

@@ -142,13 +142,15 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
     if q is None and getattr(lp, "wfcf", None) is not None and CALIB is None and ffn_pre_on() and \
             ffn_fused_ok(P, lp, x, layout) and ops.ffn_pre_ok(x, layout, lp.b1.numel(), lp.k1):
         # fc + residual + LN (SubLayers.py:54-55) in the fused FFN's prologue: no h round trip,
-        # one launch less per block (the decoder's packed 112-row launches)
+        # one launch less per block (the decoder's packed 112-row launches; the encoder's padded
+        # split-hidden launches, each split recomputing its tile's h)
         fuse_qkv = nxt is not None and getattr(nxt, "wqf", None) is not None and \
-            (nxt.fp8 is None or nxt.fp8.wqkv is None) and qkv_fused_on()
+            (nxt.fp8 is None or nxt.fp8.wqkv is None) and qkv_fused_on() and qkv_epilogue_ok(x, layout, lp)
         tag = "fc+ffn+qkv" if fuse_qkv else "fc+ffn"
         with _Timed(tag if timed else f"{_STACK[0]}:{tag}"):
-            r = ops.ffn(x, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, layout=layout,
-                        next_qkv=(nxt.wqf, nxt.bqkv) if fuse_qkv else None, pre=(att, lp.wfcf, lp.bfc, lp.ln1))
+            r = ops.ffn(x, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, lens=lens, addvec1=addvec1,
+                        addvec2=addvec2, layout=layout, next_qkv=(nxt.wqf, nxt.bqkv) if fuse_qkv else None,
+                        pre=(att, lp.wfcf, lp.bfc, lp.ln1))
         y, qn = r if fuse_qkv else (r, None)
         return y, None, qn
     if q is not None:
@@ -183,7 +185,7 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
         # the whole FFN (conv-k9 + ReLU + conv-k1 + residual + LN + mask) as one launch: the
         # [rows, 1024] hidden stays on chip
         fuse_qkv = nxt is not None and getattr(nxt, "wqf", None) is not None and \
-            (nxt.fp8 is None or nxt.fp8.wqkv is None) and qkv_fused_on()
+            (nxt.fp8 is None or nxt.fp8.wqkv is None) and qkv_fused_on() and qkv_epilogue_ok(h, layout, lp)
         tag = "ffn+qkv" if fuse_qkv else "ffn"
         with _Timed(tag if timed else f"{_STACK[0]}:{tag}"):
             r = ops.ffn(h, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, lens=lens, addvec1=addvec1,
@@ -223,6 +225,17 @@ def qkv_fused_on():
     """The next block's Q|K|V projection in the fused FFN's epilogue (fs2_ffn wqkv). FS2_QKV_FUSED=0:
     separate Q|K|V launches (A/B)."""
     return os.environ.get("FS2_QKV_FUSED", "1") != "0"
+
+
+def qkv_epilogue_ok(x, layout, lp):
+    """The Q|K|V epilogue only for unsplit FFN launches (the decoder's). In the split-hidden form
+    (the encoder's 64-row tiles x 4 splits) only the last-arriving split of a tile runs the
+    epilogue, so the projection ran on a quarter of the CUs, streaming all 393 KB of Q|K|V weights
+    per tile: 21.8k of the launch's 79.7k cycles (profiles/r5e/enc_ffn_trace.txt), where the
+    weight-resident projection over all CUs takes ~8 us. FS2_QKV_FUSED=2 keeps it everywhere (A/B)."""
+    if os.environ.get("FS2_QKV_FUSED", "1") == "2":
+        return True
+    return ops.ffn_form(ops.ffn_launch_rows(x, layout), lp.b1.numel())[1] == 1
 
 
 def ffn_fused_ok(P, lp, h, layout):
@@ -662,12 +675,29 @@ def check_meta(meta, dev):
     return int(meta[0]), int(meta[1])
 
 
+_META_HOST = {}
+
+
 def host_meta(mel_len, dev):
     """The free-running path's ONE device->host read: max(mel_len), sum(mel_len) and the
-    out-of-vocabulary counter in one copy."""
-    meta = meta_vector(mel_len, dev).cpu()
+    out-of-vocabulary counter in one copy, into pinned memory the host polls (a blocking
+    synchronize parks the thread: a wake-up of tens of us per call)."""
+    from .graphs import _spin_until_landed
+
+    meta = meta_vector(mel_len, dev)
+    if meta.device.type != "cuda":  # host-side dry runs (tests/test_host.py)
+        HOST_READS[0] += 1
+        return check_meta(meta.cpu(), dev)
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)  # per stream: reentrant across threads
+    host = _META_HOST.get(key)
+    if host is None or host.shape != meta.shape:
+        host = _META_HOST[key] = torch.empty(meta.shape, dtype=meta.dtype, pin_memory=True)
+    host[0] = -1
+    host.copy_(meta, non_blocking=True)
+    _spin_until_landed(host)
+    torch.cuda.current_stream(dev).synchronize()
     HOST_READS[0] += 1
-    return check_meta(meta, dev)
+    return check_meta(host.clone(), dev)
 
 
 def postnet_valid_rows(B, T, sum_len):

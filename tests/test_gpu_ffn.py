@@ -318,3 +318,47 @@ def test_ffn_pre_fc_ln_prologue(gpu, B, T, seed):
     assert torch.equal(one_q[:R], one[:R])
     qref = (one[:R].double() @ wq.to(torch.bfloat16).double().t() + bq.double())
     assert float((qkv[:R].double() - qref).abs().max()) <= 0.05 * max(1.0, float(qref.abs().max()))
+
+
+@pytest.mark.parametrize("B,T,nsplit,seed", [(64, 64, 4, 41), (8, 37, 4, 42), (5, 50, 2, 43)])
+def test_ffn_pre_padded_split_form(gpu, B, T, nsplit, seed):
+    """The encoder's form of the fc + residual + LN prologue: padded [B, T] rows with lengths, 64-row
+    tiles in the split-hidden form (every split recomputes its tile's h; padded rows of h are zeroed
+    as masked_fill does, Layers.py:25-26), the speaker / emotion vectors in the LN epilogue and the
+    next block's Q|K|V. Against the two launches it replaces (fc + LN + mask on fs2_conv1d, then
+    fs2_ffn on the same form): the h rounding can move by one bf16 ulp with the summation order,
+    which moves the output by a fraction of the LN scale, so valid rows within 0.05 absolute (max)
+    and 1e-3 (mean), at most 0.5 % of the elements beyond 2 ulps of the output; padded rows (zeros
+    + the speaker / emotion vectors) exactly."""
+    ops, L = gpu
+    W = _weights(ops, L, seed=seed)
+    g = torch.Generator(device=DEV).manual_seed(seed + 7)
+    lens = torch.randint(T // 2, T + 1, (B,), device=DEV, generator=g)
+    lens[0] = T
+    if B > 2:
+        lens[1], lens[2] = 1, T - 1
+    x = _x(B, T, lens, seed + 1)
+    att = torch.randn(B, T, 256, device=DEV, generator=g).to(torch.bfloat16)
+    wfc = torch.randn(256, 256, device=DEV, generator=g) / 16
+    bfc = 0.1 * torch.randn(256, device=DEV, generator=g)
+    ln1 = (1 + 0.1 * torch.randn(256, device=DEV, generator=g), 0.1 * torch.randn(256, device=DEV, generator=g), 1e-5)
+    av1 = torch.randn(B, 256, device=DEV, generator=g)
+    av2 = torch.randn(B, 256, device=DEV, generator=g)
+    wq = torch.randn(768, 256, device=DEV, generator=g) / 16
+    bq = 0.1 * torch.randn(768, device=DEV, generator=g)
+    kw = dict(ks=9, pad=4, ln=W["ln"], lens=lens, addvec1=av1, addvec2=av2, nsplit=nsplit, tile_rows=64,
+              next_qkv=(ops.pack_frag_rows(wq), bq))
+    h2 = ops.conv1d(att, ops.pack_conv_weight(wfc, L.FS2_BF16), bfc, cin=256, ks=1, pad=0, compute=L.FS2_BF16,
+                    epilogue=L.EPI_RES_LN, out_dtype=L.FS2_BF16, residual=x, ln=ln1, lens=lens)
+    two, q2 = ops.ffn(h2, W["w12"], W["b1"], W["b2"], **kw)
+    one, q1 = ops.ffn(x, W["w12"], W["b1"], W["b2"], pre=(att, ops.pack_frag_rows(wfc), bfc, ln1), **kw)
+    torch.cuda.synchronize()
+    valid = torch.arange(T, device=DEV)[None, :] < lens[:, None]
+    d = (one.float() - two.float()).abs()[valid]
+    ulp = two.float().abs().clamp(min=2 ** -8)[valid] * 2 ** -7
+    far = float((d > 2 * ulp).float().mean())
+    print(f"pre padded split: max {float(d.max()):.4f} mean {float(d.mean()):.2e} beyond 2 ulps {far:.2e}")
+    assert float(d.max()) <= 0.05 and float(d.mean()) <= 1e-3 and far <= 5e-3, (float(d.max()), float(d.mean()), far)
+    assert torch.equal(one[~valid], two[~valid])
+    dq = (q1.float() - q2.float()).abs()
+    assert float(dq.max()) <= 0.05 * max(1.0, float(q2.float().abs().max())), float(dq.max())

@@ -98,10 +98,10 @@ def test_fp8_output_and_ln_fp8_copy(gpu):
 
 def test_fp8_model_vs_bf16_reported(gpu):
     """cfg5 at the bench shape: fp8 FFN GEMMs vs the bf16 path, teacher-forced durations and
-    pitch/energy pinned to the bf16 predictions (no bucket flips). Reported numbers (printed);
-    the bound asserted is a sanity bound, not a parity claim: mean |d postnet| <= 0.1,
-    max <= 1.0 (postnet values are O(1); e4m3 keeps 3 mantissa bits, 2^-4 relative per element;
-    round 1 measured mean 0.050, max 0.33)."""
+    pitch/energy pinned to the bf16 predictions (no bucket flips). Measured on the fused e4m3
+    launch (fs2_ffn8, round 5, profiles/r5f and the bench line's extra.cfg5_fp8.tol_vs_bf16):
+    postnet mean |d| 0.064, max 0.445 (postnet values are O(1); e4m3 keeps 3 mantissa bits,
+    2^-4 relative per element). Asserted: mean <= 0.1 (1.6x), max <= 0.9 (2x)."""
     from _common import configs
     from fs2amd.data import synth_batch, to_device
     from fs2amd.model import FastSpeech2
@@ -125,7 +125,7 @@ def test_fp8_model_vs_bf16_reported(gpu):
     mel_err = (got[0] - ref[0]).abs().masked_select(valid)
     print(f"\nfp8 vs bf16 (cfg2, pinned): postnet max {float(err.max()):.4f} mean {float(err.mean()):.5f}; "
           f"mel max {float(mel_err.max()):.4f} mean {float(mel_err.mean()):.5f}")
-    assert float(err.mean()) <= 0.1 and float(err.max()) <= 1.0
+    assert float(err.mean()) <= 0.1 and float(err.max()) <= 0.9
     assert torch.equal(got[9], ref[9])
 
 

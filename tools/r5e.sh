@@ -3,7 +3,7 @@
 # FFN phase trace (abl/libfs2hip_trace.so, -DFFN_TRACE=1), attention probe timing, then the bench
 # line and the free-running trace (tools/checkpoint.sh without the full suite / PMC).
 O=gpurun_out/r5e; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_graphs.py tests/test_gpu_model.py tests/test_gpu_fp8.py tests/test_gpu_ops.py tests/test_gpu_packed.py tests/test_gpu_train.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider > $O/first.log 2>&1 || { tail -30 $O/first.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_ffn.py tests/test_gpu_graphs.py tests/test_gpu_model.py tests/test_gpu_fp8.py tests/test_gpu_ops.py tests/test_gpu_packed.py tests/test_gpu_train.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider > $O/first.log 2>&1 || { tail -30 $O/first.log; exit 1; }
 tail -2 $O/first.log
 timeout -k 10 120 python tools/kernel_probe.py attn --time > $O/attn_time.log 2>&1 || { tail -20 $O/attn_time.log; exit 1; }
 tail -1 $O/attn_time.log
