@@ -131,7 +131,8 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   constexpr int ATT_OFF = H_OFF;
   constexpr int RED0_OFF = ATT_OFF + 4 * XP_PER_WAVE * 1024;
   constexpr int SMEM0 = RED_OFF + BM * 16;
-  constexpr int SMEM = PRE && RED0_OFF + 64 * 16 > SMEM0 ? RED0_OFF + 64 * 16 : SMEM0;
+  constexpr int VEC0_OFF = RED0_OFF + 64 * 16;   // PRE: bfc, gamma1, beta1 (3 x 256 f32)
+  constexpr int SMEM = PRE && VEC0_OFF + 3 * kD * 4 > SMEM0 ? VEC0_OFF + 3 * kD * 4 : SMEM0;
   static_assert(SMEM <= 163840, "LDS");
   static_assert(BM * 528 <= 4 * XP_PER_WAVE * 1024, "Q|K|V staging fits in the x region");
   constexpr int NK1 = KS * (kD / 32);  // GEMM1 units per chunk (tap-major, 8 k-steps per tap)
@@ -143,6 +144,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[SCR_OFF + (PRE ? 0 : 4096)];
 
   const ConvArgs &a = p.e;
+  const uint64_t t_entry = FFN_TRACE ? __builtin_readcyclecounter() : 0;  // trace builds: kernel entry
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // weight-row quarter (64 rows)
   const int M = a.rows_dev != nullptr ? min(*a.rows_dev, a.M) : a.M;
@@ -222,6 +224,33 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
           ok ? (uint32_t)gm * srow + (uint32_t)within : kOOB, 0, 0, 0);
     }
   };
+  // ---- weight units: register ring of DEPTH units. Every load site is static (its unit is known
+  // from its position in the unrolled code), so the stream needs no branch: a branch there splits
+  // the MFMA sequence and hipcc then copies the accumulators between blocks.
+  constexpr uint32_t W2_BASE = (uint32_t)(F * KS * kD * 2);
+  const uint32_t lane_off = (uint32_t)lane * 16u;
+  auto base1 = [&](int c) { return (uint32_t)((c * 4 + w) * NK1) * (uint32_t)kUnit; };
+  auto base2 = [&](int c) { return W2_BASE + (uint32_t)(w * (F / 32) + c * NK2) * (uint32_t)kUnit; };
+  bf16x8 pa[DEPTH][4];
+  auto load_at = [&](auto S, uint32_t so) {
+    constexpr int s = decltype(S)::value;
+    if (FFN_ABLATE & 2) return;
+    // pinned after the MFMAs that read the slot's previous unit: a load hoisted above them keeps
+    // both units live, and the register allocator then rotates the whole ring through copies
+    // (each copy waiting for its load) at the loop back-edge
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(wr, lane_off + jb * 1024, (FFN_ABLATE & 8) ? 0u : so, 0);
+      pa[s][jb] = __builtin_bit_cast(bf16x8, v);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto ring_start = [&]() {
+    static_for<DEPTH>([&](auto I) { load_at(I, base1(c0) + (uint32_t)(decltype(I)::value * kUnit)); });
+  };
+  // the first DEPTH units follow the x tile DMA (PRE: the prologue), so that the counted wait below
+  // (all but the ring's 4 * DEPTH youngest loads) covers the tile
   if constexpr (!PRE) {
     // ---- split-hidden form: L2 warm-up (as vp.hip). An XCD's workgroups run ONE split (the
     // split-major order above) and stream its ~1.3 MB of weights in lockstep, 16 MFMAs per 4 KiB
@@ -249,13 +278,17 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     }
     // ---- x tile (rows m0 - pad .. m0 + BM + KS - 2, all 256 channels) -> LDS, once
     tile_dma(a.x, a.x_bytes, a.xs, X_OFF);
+    ring_start();
   } else {
     // ---- prologue GEMM0 (SubLayers.py:54-55 + Layers.py:25: fc + residual + LayerNorm): the FFN
     // input h of the tile's XROWS rows (halo included: the taps of GEMM1 read them), written as
     // the x tile. fc^T[n, m] = sum_d Wfc[n, d] att[m, d]: the 8 weight k-steps of this wave's 64
     // output channels stay in registers for both row passes (4 blocks = 64 rows each); the att
     // tile is DMA'd to LDS at the x pitch; residual rows from global; LN statistics via LDS.
+    // both tiles by LDS-DMA at once: att at ATT_OFF, the block input x (the residual) at X_OFF,
+    // where each lane overwrites its own elements with h (nothing else reads x in the prologue)
     tile_dma(p.att, p.att_bytes, p.as, ATT_OFF);
+    tile_dma(a.x, a.x_bytes, a.xs, X_OFF);
     const rsrc_t fr = make_rsrc(p.wfc, (uint32_t)(kD * kD * 2));
     const uint32_t lane_o = (uint32_t)lane * 16u;
     bf16x8 wf[8][4];
@@ -265,12 +298,16 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       for (int jb = 0; jb < 4; ++jb)
         wf[ks][jb] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                                     fr, lane_o + (uint32_t)(jb * 1024), (uint32_t)((w * 8 + ks) * kUnit), 0));
+    // bfc / gamma1 / beta1 -> LDS (read per row block below; registers are the scarce resource here)
+    const int hr = lane & 15, hq = lane >> 4;
+    if (tid < 3 * kD / 4) {
+      const float *src = tid < kD / 4 ? p.bfc : tid < kD / 2 ? p.g1 : p.be1;
+      *reinterpret_cast<float4 *>(smem + VEC0_OFF + 16 * tid) = reinterpret_cast<const float4 *>(src)[tid % (kD / 4)];
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
     float *red0 = reinterpret_cast<float *>(smem + RED0_OFF);
-    const int hr = lane & 15, hq = lane >> 4;
-    const bf16 *xres = reinterpret_cast<const bf16 *>(a.x);
     static_for<(XROWS + 63) / 64>([&](auto PS) {
       constexpr int ps = decltype(PS)::value;
       f32x4 a0[4][4];
@@ -302,9 +339,9 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) {
           const int n = w * 64 + jb * 16 + 4 * hq;
-          const float4 bb = *reinterpret_cast<const float4 *>(p.bfc + n);
+          const float4 bb = *reinterpret_cast<const float4 *>(smem + VEC0_OFF + 4 * n);
           bf16x4 xv = {(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
-          if (ok) xv = *reinterpret_cast<const bf16x4 *>(xres + (int64_t)gm * a.xs + n);
+          if (ok) xv = *reinterpret_cast<const bf16x4 *>(smem + X_OFF + r * XPITCH + n * 2);
           f32x4 v = a0[jb][mb];
           v[0] = v[0] + bb.x + (float)xv[0];
           v[1] = v[1] + bb.y + (float)xv[1];
@@ -370,8 +407,8 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) {
           const int n = w * 64 + jb * 16 + 4 * hq;
-          const float4 g = *reinterpret_cast<const float4 *>(p.g1 + n);
-          const float4 be = *reinterpret_cast<const float4 *>(p.be1 + n);
+          const float4 g = *reinterpret_cast<const float4 *>(smem + VEC0_OFF + 4 * (kD + n));
+          const float4 be = *reinterpret_cast<const float4 *>(smem + VEC0_OFF + 4 * (2 * kD + n));
           const f32x4 d = a0[jb][mb];
           bf16x4 o;
           o[0] = (bf16)((d[0] * rstd * g.x + be.x) * keep);
@@ -385,31 +422,9 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();  // every wave past its att reads: the vectors overwrite the region
     load_vectors();
+    ring_start();
   }
 
-  // ---- weight units: register ring of DEPTH units. Every load site is static (its unit is known
-  // from its position in the unrolled code), so the stream needs no branch: a branch there splits
-  // the MFMA sequence and hipcc then copies the accumulators between blocks.
-  constexpr uint32_t W2_BASE = (uint32_t)(F * KS * kD * 2);
-  const uint32_t lane_off = (uint32_t)lane * 16u;
-  auto base1 = [&](int c) { return (uint32_t)((c * 4 + w) * NK1) * (uint32_t)kUnit; };
-  auto base2 = [&](int c) { return W2_BASE + (uint32_t)(w * (F / 32) + c * NK2) * (uint32_t)kUnit; };
-  bf16x8 pa[DEPTH][4];
-  auto load_at = [&](auto S, uint32_t so) {
-    constexpr int s = decltype(S)::value;
-    if (FFN_ABLATE & 2) return;
-    // pinned after the MFMAs that read the slot's previous unit: a load hoisted above them keeps
-    // both units live, and the register allocator then rotates the whole ring through copies
-    // (each copy waiting for its load) at the loop back-edge
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int jb = 0; jb < 4; ++jb) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b128(wr, lane_off + jb * 1024, (FFN_ABLATE & 8) ? 0u : so, 0);
-      pa[s][jb] = __builtin_bit_cast(bf16x8, v);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  static_for<DEPTH>([&](auto I) { load_at(I, base1(c0) + (uint32_t)(decltype(I)::value * kUnit)); });
 
   // ---- B fragments
   const int hrow0 = lane & 15;  // activation row (tile-relative) of block 0
@@ -477,6 +492,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       uint64_t *o = S > 1 ? reinterpret_cast<uint64_t *>(static_cast<char *>(p.part) + p.part_bytes + 256u * blockIdx.x)
                           : reinterpret_cast<uint64_t *>(static_cast<char *>(a.out) + (size_t)(a.M - 1 - blockIdx.x) * a.os * 2);
       for (int i = 0; i < 21; ++i) o[i] = *reinterpret_cast<const uint64_t *>(smem + SMEM + 8 * i);
+      o[28] = t_entry;
       o[29] = (uint64_t)split;
       o[30] = (uint64_t)last;
       o[31] = (uint64_t)21;

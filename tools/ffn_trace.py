@@ -114,8 +114,52 @@ def main_enc(nsplit=4, tile_rows=64, with_qkv=True):
     print(f"kernel span (first start -> last end) {end_all:.0f} cycles")
 
 
+def main_dec_pre():
+    """The decoder's in-forward launch: fc + residual + LN prologue, the FFN, the LN epilogue and
+    the next block's Q|K|V (packed 112-row tiles, one per CU)."""
+    import bench
+    from fs2amd import ops
+    from fs2amd.data import synth_batch, to_device
+
+    dev = torch.device("cuda:0")
+    model, _, _ = bench.build_model(dev, "bf16")
+    bc = synth_batch(64, 64, seed=1)
+    b = to_device(bc, dev)
+    P = model.packed(dev)
+    B, T = 64, int(bc["max_mel_len"])
+    lp, nx = P.dec_layers[0], P.dec_layers[1]
+    lay = ops.SeqLayout(b["mel_lens"], T)
+    gen = torch.Generator().manual_seed(0)
+    x = torch.randn(B * T, 256, generator=gen).to(dev, torch.bfloat16)
+    att = torch.randn(B * T, 256, generator=gen).to(dev, torch.bfloat16)
+    out = torch.empty_like(x)
+    kw = dict(ks=9, pad=4, ln=lp.ln2, layout=lay, out=out, pre=(att, lp.wfcf, lp.bfc, lp.ln1))
+    if "--no-qkv" not in sys.argv:
+        kw["next_qkv"] = (nx.wqf, nx.bqkv)
+    for _ in range(3):
+        ops.ffn(x, lp.w12, lp.b1, lp.b2, **kw)
+    torch.cuda.synchronize()
+    R = int(lay.cu[-1])
+    nwg = (R + 111) // 112
+    assert B * T - nwg >= R, "no spare capacity rows for the stamps"
+    st = out.view(torch.int64).reshape(B * T, -1)[B * T - nwg:].flip(0)[:, :32].cpu()
+    ok = st[:, 31] == 21
+    t = st[ok].double()
+    print(f"workgroups traced {int(ok.sum())}")
+    t[:, 27] = t[:, 28]  # kernel entry (slot 28) as column 27 for the table below
+    segs = [(27, 0, "entry -> PRE prologue done"), (0, 1, "x tile landed / first units"), (1, 2, "c0 gemm1"), (2, 3, "c0 write_h"),
+            (3, 4, "c0 gemm2 + c1 gemm1"), (4, 5, "c1 write_h"), (5, 6, "c1 gemm2 + c2 gemm1"), (6, 7, "c2 write_h"),
+            (7, 8, "c2 gemm2 + c3 gemm1"), (8, 9, "c3 write_h"), (9, 10, "c3 gemm2"), (10, 12, "drain + barrier"),
+            (12, 18, "LN epilogue to staging"), (18, 13, "stores + next Q|K|V"), (27, 13, "total")]
+    for a, b_, name in segs:
+        d = t[:, b_] - t[:, a]
+        print(f"{name:36s} mean {float(d.mean()):9.0f} max {float(d.max()):9.0f} cycles")
+
+
 if __name__ == "__main__":
-    if "--enc" in sys.argv:
+    if "--dec-pre" in sys.argv:
+        main_dec_pre()
+    elif "--enc" in sys.argv:
         main_enc(with_qkv="--no-qkv" not in sys.argv)
     else:
         main()
