@@ -271,7 +271,7 @@ def time_kernel_in_forward(model, batch, n_fwd=6, fwd=None):
     return {k: (sum(v) / len(v), len(v)) for k, v in by.items()}
 
 
-GEMM_OPS = {"qkv", "fc", "ffn", "ffn+qkv", "fc+ffn", "fc+ffn+qkv", "conv9", "conv1", "ffn8"}
+GEMM_OPS = {"qkv", "qkv0", "fc", "ffn", "ffn+qkv", "fc+ffn", "fc+ffn+qkv", "conv9", "conv1", "ffn8"}
 FFT_GEMM_FLOPS_PER_TOKEN = 2 * (256 * 768 + 256 * 256 + 256 * 9 * 1024 + 1024 * 256)  # 5,767,168
 
 
@@ -301,6 +301,10 @@ def forward_breakdown(fwd, batch_cpu, peak_tflops):
                      "work (torch.cuda._sleep), so the events bracket the kernel, not the host's launch latency"}
     if frames is not None and gemm_s > 0:
         fl = float(FFT_GEMM_FLOPS_PER_TOKEN) * (4 * enc_tok + 6 * frames)
+        if "dec:qkv0" in tot:
+            # the decoder's first Q|K|V runs on the phoneme rows (fs2_lr_fused_proj adds the PE term
+            # while it gathers): count the FLOPs that GEMM performs, not the frame-level ones
+            fl += 2.0 * 256 * 768 * (enc_tok - frames)
         out["fft_gemm"] = {"flops_per_forward": fl, "us_per_forward": round(gemm_s * 1e6, 2), "launches": n_gemm,
                            "achieved": round(fl / gemm_s / 1e12, 2), "peak": peak_tflops, "unit": "TFLOP/s",
                            "frac": round(fl / gemm_s / 1e12 / peak_tflops, 4)}
@@ -308,10 +312,15 @@ def forward_breakdown(fwd, batch_cpu, peak_tflops):
     if lr and frames is not None:
         T = int(batch_cpu["max_mel_len"])
         byt = B * Lp * 256 * 2.0 + B * Lp * 8.0 + frames * 256 * 2.0 + B * T * 4.0 + frames * 8.0 + (B + 1) * 4.0
+        proj = "dec:qkv0" in tot
+        if proj:  # fs2_lr_fused_proj: f32 phoneme projection + f32 PE table read once, bf16 Q|K|V written
+            byt += B * Lp * 768 * 4.0 + T * 768 * 4.0 + frames * 768 * 2.0
         out["lr"] = {"bytes": byt, "us": round(lr * 1e6, 2), "achieved": round(byt / lr / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(byt / lr / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_note": "bf16 x read once + int64 durations + packed bf16 frames written + rowmap "
-                                   "(B*T int32) + row_pos (frames x 8 B) + cu"}
+                                   "(B*T int32) + row_pos (frames x 8 B) + cu" +
+                                   (" + f32 [B*L, 768] phoneme Q|K|V and f32 [T, 768] PE table read once + packed "
+                                    "bf16 Q|K|V frames written" if proj else "")}
     return out
 
 

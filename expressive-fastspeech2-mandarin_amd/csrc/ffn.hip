@@ -103,6 +103,8 @@ __device__ __forceinline__ void static_for(Fn &&f) {
 // lgkmcnt(0) as a real s_waitcnt the compiler's wait-count pass sees: gfx9 simm16 = vmcnt 63
 // (bits 3:0 and 15:14), expcnt 7, lgkmcnt 0
 constexpr int kLgkm0 = 0xC07F;
+// s_waitcnt immediate waiting for vmcnt <= n only (gfx9 encoding: vmcnt [3:0] + [15:14])
+constexpr int vm_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
 
 // MB = 16-row activation blocks per tile: 7 (112 rows: the full-chip decoder launches) or 4 (64 rows:
 // the split-hidden form of small launches, whose 4 splits x 64-row tiles fill the chip)
@@ -137,7 +139,6 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   static_assert(BM * 528 <= 4 * XP_PER_WAVE * 1024, "Q|K|V staging fits in the x region");
   constexpr int NK1 = KS * (kD / 32);  // GEMM1 units per chunk (tap-major, 8 k-steps per tap)
   constexpr int NK2 = kChunk / 32;     // GEMM2 units per chunk
-  constexpr int NU = NK1 + NK2;
   constexpr int DEPTH = kDepth;
   static_assert(NK1 % DEPTH == 0 && NK2 % DEPTH == 0, "static register-ring slots");
   constexpr int SCR_OFF = SMEM + (FFN_TRACE ? 256 : 0);  // L2 warm-up scratch (1 KiB per wave), !PRE only
@@ -172,48 +173,74 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   // padded rows with lengths: bit mb set when this lane's row of block mb is padding (t >= lens[b]),
   // read here, beside the x tile DMA, rather than in the LN epilogue's dependent chain
   int padmask = 0;
+  // every block's row_pos / lens entry is loaded before any is used (clamped row, no branch), so
+  // the MB loads overlap: a per-block load + wait chain cost ~15k cycles at kernel start
+  int2 rq[MB];
+  int64_t rl[MB];
+  if (a.row_pos != nullptr) {  // (uniform branches around whole loops: no wait between the loads)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) rq[mb] = a.row_pos[min(m0 + mb * 16 + (lane & 15), M - 1)];
+  } else {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int m = min(m0 + mb * 16 + (lane & 15), M - 1);
+      rq[mb] = make_int2(m % T, T);
+    }
+    if (a.lens != nullptr) {
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) rl[mb] = a.lens[min(m0 + mb * 16 + (lane & 15), M - 1) / T];
+    } else {
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) rl[mb] = T;
+    }
+  }
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + mb * 16 + (lane & 15);
     int tpos = 0, tlen = 0;  // rows past M: never valid (not stored)
     if (m < M) {
-      if (a.row_pos != nullptr) {
-        const int2 q = a.row_pos[m];
-        tpos = q.x;
-        tlen = q.y;
-      } else {
-        tpos = m % T;
-        tlen = T;
-        if (a.lens != nullptr && (int64_t)tpos >= a.lens[m / T]) padmask |= 1 << mb;
-      }
+      tpos = rq[mb].x;
+      tlen = rq[mb].y;
+      if (a.row_pos == nullptr && (int64_t)tpos >= rl[mb]) padmask |= 1 << mb;
     }
     int v = 0;
 #pragma unroll
     for (int tap = 0; tap < KS; ++tap) v |= ((unsigned)(tpos + tap - pad) < (unsigned)tlen ? 1 : 0) << tap;
     vmask[mb] = v;
   }
+  // 1 KiB of an f32 vector straight into LDS (LDS-DMA: no register round trip, so no wait here;
+  // the vmcnt waits that cover the tiles cover these older loads too)
+  auto vec_dma = [&](const float *src, int piece, char *dst) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(src, (uint32_t)(piece + 1) * 1024u),
+                                             (__attribute__((address_space(3))) void *)dst, 16,
+                                             (uint32_t)piece * 1024u + (uint32_t)lane * 16u, 0, 0, 0);
+  };
   auto load_vectors = [&]() {
-    // b1 -> LDS; the LN epilogue's vectors, read once here instead of after the K loop
-    for (int i = tid; i < F / 4; i += 256)
-      *reinterpret_cast<float4 *>(smem + B1_OFF + 16 * i) = reinterpret_cast<const float4 *>(p.b1)[i];
-    if (tid < 3 * kD / 4) {
-      const float *src = tid < kD / 4 ? a.bias : tid < kD / 2 ? a.gamma : a.beta;
-      *reinterpret_cast<float4 *>(smem + EP_OFF + 16 * tid) =
-          reinterpret_cast<const float4 *>(src)[tid % (kD / 4)];
-    }
+    // b1 -> LDS (F / 256 pieces over the waves); the LN epilogue's b2 / gamma / beta (waves 0-2)
+    for (int pc = w; pc < F / 256; pc += 4) vec_dma(p.b1, pc, smem + B1_OFF + pc * 1024);
+    if (w < 3) vec_dma(w == 0 ? a.bias : w == 1 ? a.gamma : a.beta, 0, smem + EP_OFF + w * 1024);
   };
   if constexpr (!PRE) load_vectors();
   if (tid < 32) *reinterpret_cast<float4 *>(smem + ZERO_OFF + 16 * tid) = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) asm volatile("" ::"v"(vmask[mb]));
 
+  // trace builds: wave 0 stamps the shader clock into an LDS slot past the kernel's own LDS
+  auto stamp = [&](int i) {
+    if (FFN_TRACE) {
+      __builtin_amdgcn_sched_barrier(0);
+      const uint64_t t = __builtin_readcyclecounter();
+      if (tid == 0) *reinterpret_cast<uint64_t *>(smem + SMEM + 8 * i) = t;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   const rsrc_t wr = make_rsrc(p.w, p.w_bytes);
   // lane-linear 1 KiB LDS-DMA pieces of a [XROWS x 512 B] row tile at the 544-byte pitch
-  auto tile_dma = [&](const void *src, uint32_t bytes, int64_t stride, int off) {
+  auto tile_dma_range = [&](const void *src, uint32_t bytes, int64_t stride, int off, int i0, int i1) {
     const rsrc_t sr = make_rsrc(src, bytes);
     const uint32_t srow = (uint32_t)stride * 2u;
 #pragma unroll
-    for (int i = 0; i < XP_PER_WAVE; ++i) {
+    for (int i = i0; i < i1; ++i) {
       const int pc = w + 4 * i;
       const int o = pc * 1024 + lane * 16;  // lane-linear LDS image: row o / XPITCH, byte o % XPITCH
       const int r = o / XPITCH, within = o - r * XPITCH;
@@ -223,6 +250,9 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
           sr, (__attribute__((address_space(3))) void *)(smem + off + pc * 1024), 16,
           ok ? (uint32_t)gm * srow + (uint32_t)within : kOOB, 0, 0, 0);
     }
+  };
+  auto tile_dma = [&](const void *src, uint32_t bytes, int64_t stride, int off) {
+    tile_dma_range(src, bytes, stride, off, 0, XP_PER_WAVE);
   };
   // ---- weight units: register ring of DEPTH units. Every load site is static (its unit is known
   // from its position in the unrolled code), so the stream needs no branch: a branch there splits
@@ -287,8 +317,11 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     // tile is DMA'd to LDS at the x pitch; residual rows from global; LN statistics via LDS.
     // both tiles by LDS-DMA at once: att at ATT_OFF, the block input x (the residual) at X_OFF,
     // where each lane overwrites its own elements with h (nothing else reads x in the prologue)
-    tile_dma(p.att, p.att_bytes, p.as, ATT_OFF);
-    tile_dma(a.x, a.x_bytes, a.xs, X_OFF);
+    // issue order: the LN vectors (oldest: their LDS store waits only for them), the fc weights,
+    // then both tiles' first PRE_SPLIT pieces per wave (rows 0 .. ~67: row pass 0), then the rest --
+    // pass 0 starts when its rows have landed while the second half still streams in
+    const int hr = lane & 15, hq = lane >> 4;
+    if (w < 3) vec_dma(w == 0 ? p.bfc : w == 1 ? p.g1 : p.be1, 0, smem + VEC0_OFF + w * 1024);
     const rsrc_t fr = make_rsrc(p.wfc, (uint32_t)(kD * kD * 2));
     const uint32_t lane_o = (uint32_t)lane * 16u;
     bf16x8 wf[8][4];
@@ -298,18 +331,26 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
       for (int jb = 0; jb < 4; ++jb)
         wf[ks][jb] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                                     fr, lane_o + (uint32_t)(jb * 1024), (uint32_t)((w * 8 + ks) * kUnit), 0));
-    // bfc / gamma1 / beta1 -> LDS (read per row block below; registers are the scarce resource here)
-    const int hr = lane & 15, hq = lane >> 4;
-    if (tid < 3 * kD / 4) {
-      const float *src = tid < kD / 4 ? p.bfc : tid < kD / 2 ? p.g1 : p.be1;
-      *reinterpret_cast<float4 *>(smem + VEC0_OFF + 16 * tid) = reinterpret_cast<const float4 *>(src)[tid % (kD / 4)];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // pieces w + 4 i, i < PRE_SPLIT, of both tiles: LDS bytes < 4 PRE_SPLIT KiB, i.e. rows < 64 + halo
+    constexpr int PRE_SPLIT = (64 * XPITCH + 1023) / 1024 / 4 + 1;
+    static_assert(4 * PRE_SPLIT * 1024 >= 64 * XPITCH && PRE_SPLIT <= XP_PER_WAVE, "row pass 0 pieces");
+    tile_dma_range(p.att, p.att_bytes, p.as, ATT_OFF, 0, PRE_SPLIT);
+    tile_dma_range(a.x, a.x_bytes, a.xs, X_OFF, 0, PRE_SPLIT);
+    tile_dma_range(p.att, p.att_bytes, p.as, ATT_OFF, PRE_SPLIT, XP_PER_WAVE);
+    tile_dma_range(a.x, a.x_bytes, a.xs, X_OFF, PRE_SPLIT, XP_PER_WAVE);
+    stamp(21);
+    // everything but the second-half pieces (2 (XP_PER_WAVE - PRE_SPLIT) per wave, the youngest)
+    __builtin_amdgcn_s_waitcnt(vm_imm(2 * (XP_PER_WAVE - PRE_SPLIT)));
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
+    stamp(22);
     float *red0 = reinterpret_cast<float *>(smem + RED0_OFF);
     static_for<(XROWS + 63) / 64>([&](auto PS) {
       constexpr int ps = decltype(PS)::value;
+      if constexpr (ps == 1) {  // the second half of both tiles
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
       f32x4 a0[4][4];
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
@@ -418,6 +459,7 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
           if (r < XROWS) *reinterpret_cast<bf16x4 *>(smem + X_OFF + r * XPITCH + n * 2) = o;
         }
       }
+      stamp(23 + ps);
     });
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();  // every wave past its att reads: the vectors overwrite the region
@@ -476,26 +518,17 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  // trace builds: wave 0 stamps the shader clock into an LDS slot past the kernel's own LDS
-  auto stamp = [&](int i) {
-    if (FFN_TRACE) {
-      __builtin_amdgcn_sched_barrier(0);
-      const uint64_t t = __builtin_readcyclecounter();
-      if (tid == 0) *reinterpret_cast<uint64_t *>(smem + SMEM + 8 * i) = t;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
   // trace builds: 32 stamp slots per workgroup -- past the split-K partials in the workspace for the
   // split form (probe-sized workspace), else output row a.M - 1 - block (the packed capacity tail)
   auto trace_dump = [&](int last) {
     if (FFN_TRACE) {
       uint64_t *o = S > 1 ? reinterpret_cast<uint64_t *>(static_cast<char *>(p.part) + p.part_bytes + 256u * blockIdx.x)
                           : reinterpret_cast<uint64_t *>(static_cast<char *>(a.out) + (size_t)(a.M - 1 - blockIdx.x) * a.os * 2);
-      for (int i = 0; i < 21; ++i) o[i] = *reinterpret_cast<const uint64_t *>(smem + SMEM + 8 * i);
+      for (int i = 0; i < 25; ++i) o[i] = *reinterpret_cast<const uint64_t *>(smem + SMEM + 8 * i);
       o[28] = t_entry;
       o[29] = (uint64_t)split;
       o[30] = (uint64_t)last;
-      o[31] = (uint64_t)21;
+      o[31] = (uint64_t)25;
     }
   };
   stamp(0);

@@ -248,6 +248,12 @@ struct LrFusedArgs {
   int2 *row_pos;
   int32_t *rowmap;
   int store;  // bf16 frame stores: 0 non-temporal, 1 plain, 2 write-through (sc1); FS2_LR_STORE (A/B)
+  // optional projection of the gathered frames (fs2_lr_fused_proj): proj_out[row] =
+  // bf16(proj_src[b, src] + proj_pe[t]) over NP columns -- the decoder's first Q|K|V by linearity
+  const float *proj_src;
+  const float *proj_pe;
+  int NP;
+  bf16 *proj_out;
 };
 
 template <typename TX, typename TO, bool HAS_PE, int ROWS>
@@ -343,48 +349,100 @@ __global__ __launch_bounds__(256) void lr_fused_kernel(LrFusedArgs a) {
   const int vpr = D >> 3, total = rows * vpr;
   const TX *xb = reinterpret_cast<const TX *>(a.x) + (int64_t)b * L * D;
   TO *ob = reinterpret_cast<TO *>(a.out) + ((int64_t)cu_b + t0) * D;
-  for (int base = tid; base < total; base += 256 * UNR) {
-    float v[UNR][8];
+  // x (+ PE) gathered by all threads, then (with the projection) the Q|K|V rows by waves 0-2
+  const bool proj = a.proj_out != nullptr;
+  auto gather = [&](auto UC, int me, int nthr) {
+    constexpr int U = decltype(UC)::value;
+    for (int base = me; base < total; base += nthr * U) {
+      float v[U][8];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int e = base + u * 256;
-      const int r = e / vpr;
-      const int col = (e - r * vpr) << 3;
-      const int sidx = e < total ? src[r] : -1;
-      if (sidx >= 0) {
-        load8(xb + (int64_t)sidx * D + col, v[u]);
-      } else {
+      for (int u = 0; u < U; ++u) {
+        const int e = base + u * nthr;
+        const int r = e / vpr;
+        const int col = (e - r * vpr) << 3;
+        const int sidx = e < total ? src[r] : -1;
+        if (sidx >= 0) {
+          load8(xb + (int64_t)sidx * D + col, v[u]);
+        } else {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[u][q] = 0.0f;
+          for (int q = 0; q < 8; ++q) v[u][q] = 0.0f;
+        }
+        if constexpr (HAS_PE) {
+          if (e < total) {
+            float pv[8];
+            load8(a.pe + (int64_t)(t0 + r) * D + col, pv);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[u][q] += pv[q];
+          }
+        }
       }
-      if constexpr (HAS_PE) {
-        if (e < total) {
-          float pv[8];
-          load8(a.pe + (int64_t)(t0 + r) * D + col, pv);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[u][q] += pv[q];
+      for (int u = 0; u < U; ++u) {
+        const int e = base + u * nthr;
+        if (e < total) {
+          if constexpr (sizeof(TO) == 2) {
+            bf16x8 o;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o[q] = (bf16)v[u][q];
+            bf16x8 *dst = reinterpret_cast<bf16x8 *>(ob + (int64_t)e * 8);
+            if (a.store == 0)
+              __builtin_nontemporal_store(o, dst);
+            else if (a.store == 1)
+              *dst = o;
+            else
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o),
+                                                     __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 16, 0x00020000), 0u,
+                                                     0, 16);
+          } else {
+            store8(ob + (int64_t)e * 8, v[u]);
+          }
         }
       }
     }
+  };
+  gather(std::integral_constant<int, UNR>{}, tid, 256);
+  // (5) the projection: (x[src] + pe[t]) W + b = (x W)[src] + (pe W + b)[t], both f32, one bf16
+  // rounding at the end. Waves 0-2: thread t owns 8 columns (t % 96) of every other row (t / 96)
+  // and walks 8 of its rows per round with all 32 loads in flight (the table rows from L2, shared
+  // by the B utterances; the phoneme rows mostly from L1, one phoneme serving ~7 consecutive
+  // frames); 16-byte stores. Graph-timed alone at cfg2 (r5p): 24.2 us against 10.9 without the
+  // projection -- the 38 MB of Q|K|V rows at ~5.8 TB/s, ~90 MB of L2 reads, ~4 us of loop.
+  if (proj && wv < 3) {
+    constexpr int RB = 8;
+    const int NP = a.NP, cg = NP >> 3;  // 8-column groups per row (96 at NP = 768)
+    const float *tb = a.proj_pe + (int64_t)t0 * NP;
+    const float *sb = a.proj_src + (int64_t)b * L * NP;
+    bf16 *pb = a.proj_out + ((int64_t)cu_b + t0) * NP;
+    const int lanes = 192 / cg * cg;  // threads in use: whole rows of column groups
+    if (tid < lanes) {
+      const int c = (tid % cg) * 8, r1 = tid / cg, rs = lanes / cg;
+      for (int r0 = r1; r0 < rows; r0 += RB * rs) {
+        float4 tv[RB][2], sv[RB][2];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int e = base + u * 256;
-      if (e < total) {
-        if constexpr (sizeof(TO) == 2) {
-          bf16x8 o;
+        for (int u = 0; u < RB; ++u) {
+          const int r = min(r0 + u * rs, rows - 1);
+          const int sidx = src[r];
+          const float *tp = tb + (int64_t)r * NP + c;
+          tv[u][0] = *reinterpret_cast<const float4 *>(tp);
+          tv[u][1] = *reinterpret_cast<const float4 *>(tp + 4);
+          if (sidx >= 0) {
+            const float *sp = sb + (int64_t)sidx * NP + c;
+            sv[u][0] = *reinterpret_cast<const float4 *>(sp);
+            sv[u][1] = *reinterpret_cast<const float4 *>(sp + 4);
+          } else {
+            sv[u][0] = sv[u][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
 #pragma unroll
-          for (int q = 0; q < 8; ++q) o[q] = (bf16)v[u][q];
-          bf16x8 *dst = reinterpret_cast<bf16x8 *>(ob + (int64_t)e * 8);
-          if (a.store == 0)
-            __builtin_nontemporal_store(o, dst);
-          else if (a.store == 1)
-            *dst = o;
-          else
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o),
-                                                   __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 16, 0x00020000), 0u,
-                                                   0, 16);
-        } else {
-          store8(ob + (int64_t)e * 8, v[u]);
+        for (int u = 0; u < RB; ++u) {
+          const int r = r0 + u * rs;
+          if (r < rows) {
+            const bf16x8 o{(bf16)(tv[u][0].x + sv[u][0].x), (bf16)(tv[u][0].y + sv[u][0].y),
+                           (bf16)(tv[u][0].z + sv[u][0].z), (bf16)(tv[u][0].w + sv[u][0].w),
+                           (bf16)(tv[u][1].x + sv[u][1].x), (bf16)(tv[u][1].y + sv[u][1].y),
+                           (bf16)(tv[u][1].z + sv[u][1].z), (bf16)(tv[u][1].w + sv[u][1].w)};
+            __builtin_nontemporal_store(o, reinterpret_cast<bf16x8 *>(pb + (int64_t)r * NP + c));
+          }
         }
       }
     }
@@ -625,6 +683,19 @@ extern "C" int fs2_lr_fused(const void *x, int x_dtype, const void *dur, int dur
                             const float *pe, const int64_t *layout_lens, int32_t *cu, int32_t *row_pos,
                             int32_t *rowmap, void *out, int out_dtype, int32_t *cum, int64_t *mel_len,
                             float *d_rounded, fs2_stream_t stream) {
+  return fs2_lr_fused_proj(x, x_dtype, dur, dur_kind, d_control, cum_in, mel_len_in, B, L, D, T_out, pe, layout_lens,
+                           cu, row_pos, rowmap, out, out_dtype, cum, mel_len, d_rounded, nullptr, nullptr, 0, nullptr,
+                           stream);
+}
+
+extern "C" int fs2_lr_fused_proj(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control,
+                                 const int32_t *cum_in, const int64_t *mel_len_in, int B, int L, int D, int T_out,
+                                 const float *pe, const int64_t *layout_lens, int32_t *cu, int32_t *row_pos,
+                                 int32_t *rowmap, void *out, int out_dtype, int32_t *cum, int64_t *mel_len,
+                                 float *d_rounded, const float *proj_src, const float *proj_pe, int NP,
+                                 void *proj_out, fs2_stream_t stream) {
+  if (proj_out != nullptr && (proj_src == nullptr || proj_pe == nullptr || NP < 8 || NP > 1536 || (NP & 7) != 0))
+    return FS2_EINVAL;
   if (x == nullptr || out == nullptr || layout_lens == nullptr || cu == nullptr) return FS2_EINVAL;
   if (B < 0 || L <= 0 || D <= 0 || (D & 7) != 0 || T_out < 0 || B > kSeqMaxB || L > kLdsCum) return FS2_EINVAL;
   if ((int64_t)B * T_out > 0x7fffff00LL) return FS2_EINVAL;
@@ -668,6 +739,10 @@ extern "C" int fs2_lr_fused(const void *x, int x_dtype, const void *dur, int dur
     return e == nullptr ? 0 : (e[0] == 'p' ? 1 : e[0] == 's' ? 2 : 0);
   }();
   a.store = store_env;
+  a.proj_src = proj_src;
+  a.proj_pe = proj_pe;
+  a.NP = NP;
+  a.proj_out = reinterpret_cast<bf16 *>(proj_out);
   // frames per workgroup (FS2_LR_ROWS = 32 / 64 / 128, A/B): every workgroup re-derives its
   // utterance's scan and packed offset, so more frames per workgroup amortise that prologue
   static const int rows_env = [] {

@@ -947,11 +947,14 @@ def variance_embed_ex(x, value, bins, table):
     return out, idx
 
 
-def lr_fused(x, lens, T_out, pe=None, out_dtype=None, dur=None, logpred=False, d_control=1.0, cum=None, mel_len=None):
+def lr_fused(x, lens, T_out, pe=None, out_dtype=None, dur=None, logpred=False, d_control=1.0, cum=None, mel_len=None,
+             proj=None):
     """fs2_lr_fused: LengthRegulator gather (+ PE) into the packed decoder rows of the layout of
     ``lens`` over T_out, the layout built by the same launch. Durations scanned here (``dur``:
     returns (out, layout, cum, mel_len, d_rounded)) or from fs2_lr_durations (``cum``, ``mel_len``:
-    returns (out, layout))."""
+    returns (out, layout)). ``proj`` = (proj_src f32 [B*Lx, NP], proj_pe f32 [>= T_out, NP])
+    (fs2_lr_fused_proj): the packed bf16 rows bf16(proj_src[src] + proj_pe[t]) come back as one
+    more trailing result."""
     _gpu(x, lens, pe, dur, cum, mel_len)
     x = x.contiguous()
     B, Lx, D = x.shape
@@ -960,20 +963,34 @@ def lr_fused(x, lens, T_out, pe=None, out_dtype=None, dur=None, logpred=False, d
     lens = lens.to(torch.int64).contiguous()
     lay = SeqLayout.deferred(B, T_out, dev)
     out = lay.empty(D, torch_dtype(od))
+    psrc = ppe = pout = None
+    NP = 0
+    if proj is not None:
+        psrc, ppe = proj
+        _gpu(psrc, ppe)
+        NP = psrc.shape[-1]
+        assert psrc.dtype == torch.float32 and ppe.dtype == torch.float32 and psrc.is_contiguous() \
+            and ppe.is_contiguous() and psrc.numel() == B * Lx * NP and ppe.dim() == 2 and ppe.shape[1] == NP \
+            and ppe.shape[0] >= T_out and NP % 8 == 0 and 8 <= NP <= 1536, (tuple(psrc.shape), tuple(ppe.shape), B, Lx, T_out)
+        pout = lay.empty(NP, torch.bfloat16)
     if dur is not None:
         dur = dur.contiguous()
         cum = torch.empty(B, Lx, device=dev, dtype=torch.int32)
         mel_len = torch.empty(B, device=dev, dtype=torch.int64)
         d_rounded = torch.empty(B, Lx, device=dev, dtype=torch.float32) if logpred else None
-        L.check(_lib.fs2_lr_fused(_ptr(x), _dt(x), _ptr(dur), _dur_kind(dur, logpred), float(d_control), None, None,
-                                  B, Lx, D, int(T_out), _ptr(pe), _ptr(lens), _ptr(lay.cu), _ptr(lay.row_pos),
-                                  _ptr(lay.rowmap), _ptr(out), od, _ptr(cum), _ptr(mel_len), _ptr(d_rounded),
-                                  _stream(x)), "fs2_lr_fused")
-        return out, lay, cum, mel_len, d_rounded
-    L.check(_lib.fs2_lr_fused(_ptr(x), _dt(x), None, 0, 1.0, _ptr(cum), _ptr(mel_len), B, Lx, D, int(T_out), _ptr(pe),
-                              _ptr(lens), _ptr(lay.cu), _ptr(lay.row_pos), _ptr(lay.rowmap), _ptr(out), od, None,
-                              None, None, _stream(x)), "fs2_lr_fused")
-    return out, lay
+        L.check(_lib.fs2_lr_fused_proj(_ptr(x), _dt(x), _ptr(dur), _dur_kind(dur, logpred), float(d_control), None,
+                                       None, B, Lx, D, int(T_out), _ptr(pe), _ptr(lens), _ptr(lay.cu),
+                                       _ptr(lay.row_pos), _ptr(lay.rowmap), _ptr(out), od, _ptr(cum), _ptr(mel_len),
+                                       _ptr(d_rounded), _ptr(psrc), _ptr(ppe), NP, _ptr(pout), _stream(x)),
+                "fs2_lr_fused_proj")
+        res = (out, lay, cum, mel_len, d_rounded)
+    else:
+        L.check(_lib.fs2_lr_fused_proj(_ptr(x), _dt(x), None, 0, 1.0, _ptr(cum), _ptr(mel_len), B, Lx, D, int(T_out),
+                                       _ptr(pe), _ptr(lens), _ptr(lay.cu), _ptr(lay.row_pos), _ptr(lay.rowmap),
+                                       _ptr(out), od, None, None, None, _ptr(psrc), _ptr(ppe), NP, _ptr(pout),
+                                       _stream(x)), "fs2_lr_fused_proj")
+        res = (out, lay)
+    return res + (pout,) if proj is not None else res
 
 
 def length_regulate(x, duration, max_len=None, return_index_map=False):

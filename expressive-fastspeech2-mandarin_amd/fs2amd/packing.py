@@ -66,6 +66,26 @@ def _fft_layer(layer, device, compute, key=None, fp8_scales=None):
     )
 
 
+def qkv_pe_rows(pe, a, compute):
+    """pe W^T + b of a block's concatenated Q|K|V projection, f64-accumulated, f32 [rows, 768]; W
+    rounded to bf16 first in bf16 compute (the weights the fs2_conv1d projection multiplies)."""
+    w = torch.cat([a.w_qs.weight, a.w_ks.weight, a.w_vs.weight], 0).detach().to(pe.device)
+    b = torch.cat([a.w_qs.bias, a.w_ks.bias, a.w_vs.bias], 0).detach().to(pe.device)
+    if compute == L.FS2_BF16:
+        w = w.to(torch.bfloat16)
+    return (pe.double() @ w.double().t() + b.double()).float().contiguous()
+
+
+def _qkv_pe_table(pe, layers, device, compute):
+    """The decoder's first Q|K|V projection of the position encoding (runtime.decode_packed: the
+    LengthRegulator launch then projects the frames by linearity, fs2_lr_fused_proj) and the
+    attention module it came from (runtime._qkv_pe: longer tables on demand)."""
+    if len(layers) == 0 or compute != L.FS2_BF16:
+        return None
+    a = layers[0].slf_attn
+    return SimpleNamespace(table=qkv_pe_rows(pe, a, compute), attn=a, compute=compute)
+
+
 def _ffn_pair(f, device, compute):
     """w_1 | w_2 in the fs2_ffn layout (bf16 FFNs of the shapes the fused kernel covers), else None."""
     ks, F, D = f.w_1.kernel_size[0], f.w_1.out_channels, f.w_1.in_channels
@@ -185,6 +205,7 @@ def pack_model(model, device, precision, vp_precision="fp32", fp8_scales=None):
     P.dec_pe = _f32(model.decoder.position_enc[0], device)
     P.enc_layers = [_fft_layer(l, device, big, ("enc", i), sc) for i, l in enumerate(model.encoder.layer_stack)]
     P.dec_layers = [_fft_layer(l, device, big, ("dec", i), sc) for i, l in enumerate(model.decoder.layer_stack)]
+    P.dec_qkv_pe = _qkv_pe_table(P.dec_pe, model.decoder.layer_stack, device, big)
     P.vp = {k: _vp(getattr(va, f"{k}_predictor"), device, vpc, vsplit) for k in ("duration", "pitch", "energy")}
     # bf16x3 VariancePredictors in their column-split form (duration + pitch side by side, energy)
     P.vpcols = None

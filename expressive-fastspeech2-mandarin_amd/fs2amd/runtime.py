@@ -52,6 +52,30 @@ def _pe(P, which, n):
     return getattr(P, key)
 
 
+def _qkv_pe(P, n):
+    """pe W^T + b of the decoder's first Q|K|V over >= n positions (packing.qkv_pe_rows), grown with
+    the PE table for sequences past max_seq_len."""
+    q = P.dec_qkv_pe
+    if n <= q.table.shape[0]:
+        return q.table
+    key = f"_qkv_pe_{n}"
+    if not hasattr(P, key):
+        from .packing import qkv_pe_rows
+        setattr(P, key, qkv_pe_rows(_pe(P, "dec", n)[:n], q.attn, q.compute))
+    return getattr(P, key)
+
+
+def lr_proj_ok(P, x):
+    """The decoder's first Q|K|V projection folded into the LengthRegulator launch (bf16 packed
+    decoder): the projection runs on the B*L phoneme rows (one fs2_conv1d, f32 out) and
+    fs2_lr_fused_proj adds the per-position table while it gathers, instead of a GEMM over the
+    ~7x more frames. FS2_LR_PROJ=0: the frame-level Q|K|V launch (A/B)."""
+    if os.environ.get("FS2_LR_PROJ", "1") == "0" or getattr(P, "dec_qkv_pe", None) is None or CALIB is not None:
+        return False
+    lp = P.dec_layers[0]
+    return x.dtype == torch.bfloat16 and (lp.fp8 is None or lp.fp8.wqkv is None) and lp.n_head * lp.d_k == x.shape[-1]
+
+
 # Optional measurement hook: when a list, the forward's launches are bracketed by HIP events on
 # the launch stream, (start, end, tag) appended in launch order (bench.py's live roofline timing:
 # the decoder's fused FFN, every FFT-block GEMM launch, attention, the LengthRegulator). Decoder
@@ -262,10 +286,12 @@ def ffn_fused_ok(P, lp, h, layout):
     return -(-rows // tr) * ns >= FFN_SPLIT_MIN_WG
 
 
-def _stack(P, layers, x, lens, layout=None, timed=False, addvecs=(None, None)):
-    """FFT-block stack; in fp8 mode each block hands the next one an fp8 copy of its output."""
+def _stack(P, layers, x, lens, layout=None, timed=False, addvecs=(None, None), qkv0=None):
+    """FFT-block stack; in fp8 mode each block hands the next one an fp8 copy of its output.
+    qkv0: the first block's Q|K|V projection, already computed (fs2_lr_fused_proj)."""
     _STACK[0] = "dec" if timed else "enc"
-    x8 = qkv = None
+    x8 = None
+    qkv = qkv0
     n = len(layers)
     for i, lp in enumerate(layers):
         nxt = layers[i + 1] if i + 1 < n else None
@@ -523,15 +549,26 @@ def decode_packed(P, st, x, dec_lens, T_lay, rows_hint=None):
     (the packed rows, cu and row_pos are those of the valid frames; only the padded-row maps and
     the grids' early-exiting tails grow with it): fs2amd.graphs.SynthGraphs captures this part per
     T bucket. Returns (packed x [B*T_lay, d_model], layout)."""
+    qkv0 = None
     if lr_fused_ok(x):
-        # scan (teacher-forced) + packed layout + gather (+ PE) in one launch
+        proj = None
+        if lr_proj_ok(P, x):
+            lp = P.dec_layers[0]
+            with _Timed("dec:qkv0"):  # x W^T on the phoneme rows (Models.py:145-152 input, linearity)
+                xw = ops.conv1d(x, lp.wqkv, None, cin=x.shape[-1], ks=1, pad=0, compute=P.compute,
+                                epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+            proj = (xw.view(-1, xw.shape[-1]), _qkv_pe(P, T_lay))
+        # scan (teacher-forced) + packed layout + gather (+ PE) (+ the first Q|K|V) in one launch
         with _Timed("va:lr"):
             if st.cum is None:
-                x, lay, st.cum, st.mel_len, _ = ops.lr_fused(x, dec_lens, T_lay, pe=_pe(P, "dec", T_lay),
-                                                             out_dtype=P.act_dtype, dur=st.dur_pending)
+                r = ops.lr_fused(x, dec_lens, T_lay, pe=_pe(P, "dec", T_lay), out_dtype=P.act_dtype,
+                                 dur=st.dur_pending, proj=proj)
+                x, lay, st.cum, st.mel_len = r[:4]
             else:
-                x, lay = ops.lr_fused(x, dec_lens, T_lay, pe=_pe(P, "dec", T_lay), out_dtype=P.act_dtype,
-                                      cum=st.cum, mel_len=st.mel_len)
+                r = ops.lr_fused(x, dec_lens, T_lay, pe=_pe(P, "dec", T_lay), out_dtype=P.act_dtype,
+                                 cum=st.cum, mel_len=st.mel_len, proj=proj)
+                x, lay = r[:2]
+            qkv0 = r[-1] if proj is not None else None
     else:
         _ensure_lr(st)
         lay = ops.SeqLayout(dec_lens, T_lay)
@@ -540,7 +577,7 @@ def decode_packed(P, st, x, dec_lens, T_lay, rows_hint=None):
     # active rows when known on the host (free-running), rounded up (ops.rows_bucket) so that
     # a captured stage-2 graph serves every batch of the bucket
     lay.rows_hint = None if rows_hint is None else ops.rows_bucket(rows_hint, lay.capacity)
-    return _stack(P, P.dec_layers, x, None, layout=lay, timed=True), lay
+    return _stack(P, P.dec_layers, x, None, layout=lay, timed=True, qkv0=qkv0), lay
 
 
 def mel_postnet(P, x, lay, dec_lens, postnet_valid=False, rows_hint=None):

@@ -502,6 +502,21 @@ int fs2_lr_fused(const void *x, int x_dtype, const void *dur, int dur_kind, floa
                  const int64_t *layout_lens, int32_t *cu, int32_t *row_pos, int32_t *rowmap, void *out,
                  int out_dtype, int32_t *cum, int64_t *mel_len, float *d_rounded, fs2_stream_t stream);
 
+/*
+ * fs2_lr_fused_proj — fs2_lr_fused plus the decoder's first Q|K|V projection of the gathered frames
+ * by linearity (SubLayers.py:39-41 on the LengthRegulator output, Models.py:145-152's PE added):
+ * (x[b, src] + pe[t]) W^T + b = (x W^T)[b, src] + (pe W^T + b)[t], so
+ * proj_out[cu[b] + t, :NP] = bf16(proj_src[b * L + src(b,t), :] + proj_pe[t, :]) (proj_src row
+ * omitted for t >= mel_len[b]). proj_src: f32 [B * L, NP], the phoneme rows' projection (one
+ * fs2_conv1d over B*L rows instead of the frames); proj_pe: f32 [>= T_out, NP] = pe W^T + b, a
+ * per-weight table. NP % 8 == 0, NP <= 1536. With proj_out == NULL this is fs2_lr_fused.
+ */
+int fs2_lr_fused_proj(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control,
+                      const int32_t *cum_in, const int64_t *mel_len_in, int B, int L, int D, int T_out,
+                      const float *pe, const int64_t *layout_lens, int32_t *cu, int32_t *row_pos, int32_t *rowmap,
+                      void *out, int out_dtype, int32_t *cum, int64_t *mel_len, float *d_rounded,
+                      const float *proj_src, const float *proj_pe, int NP, void *proj_out, fs2_stream_t stream);
+
 /* Convenience: both launches with a caller-known T_out (the teacher-forced / max_mel_len path). */
 int fs2_length_regulate(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control, int B, int L,
                         int D, int T_out, const float *pe, void *out, int out_dtype, int32_t *cum, int64_t *mel_len,

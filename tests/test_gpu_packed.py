@@ -237,8 +237,11 @@ torch.save(outs, sys.argv[1])
     # default (packed decoder, 2 utterance-group streams) vs padded decoder vs one stream
     for tag, packed, streams in (("default", "1", "2"), ("padded", "0", "2"), ("one_stream", "1", "1")):
         path = f"/tmp/fs2_packed_{tag}_{os.getpid()}.pt"
+        # FS2_LR_PROJ=0: the packed decoder's first Q|K|V by linearity (fs2_lr_fused_proj) rounds
+        # once instead of twice, so it is not bit-identical to the padded GEMM; test_lr_fused_proj
+        # and the oracle-level model tests cover it
         env = dict(os.environ, FS2_PACKED_DECODER=packed, FS2_STREAMS=streams, REPO=repo, FS2_CONV_SPLITK="0",
-                   FS2_CONV_PHASED="0")
+                   FS2_CONV_PHASED="0", FS2_LR_PROJ="0")
         r = subprocess.run([sys.executable, "-c", code, path], env=env, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-3000:]
         res[tag] = torch.load(path, weights_only=True)
@@ -302,3 +305,54 @@ def test_lr_fused_equals_three_launches(gpu, mode):
         R = int(lay.cu[-1])
         assert torch.equal(lay2.row_pos[:R], lay.row_pos[:R])
         assert torch.equal(got[:R], ref[:R]), (B, Lx, mode)
+
+
+@pytest.mark.parametrize("mode", ["i64", "cum"])
+def test_lr_fused_proj(gpu, mode):
+    """fs2_lr_fused_proj (runtime.decode_packed's first decoder Q|K|V by linearity): frames, layout
+    and scan outputs bit-identical to fs2_lr_fused; the projected rows against an f64 torch
+    reference of bf16((x[src] + pe[t]) W^T + b) (the frame-level projection the reference's
+    decoder computes, SubLayers.py:39-41 on Models.py:145-152's input) within one bf16 rounding of
+    the f32 sum: |got - ref| <= 2^-8 |ref| + 2e-5. Rows t >= mel_len (x = 0) get pe W^T + b only."""
+    ops, L = gpu
+    g = torch.Generator(device=DEV).manual_seed(33)
+    for B, Lx in ((7, 70), (3, 160), (1, 1)):
+        D, NP = 256, 768
+        d = torch.randint(-1, 9, (B, Lx), device=DEV, generator=g)
+        if B > 1:
+            d[1] = 0
+        x = torch.randn(B, Lx, D, device=DEV, generator=g).to(torch.bfloat16)
+        cum, mel_len, _ = ops.lr_durations(d)
+        T = max(int(mel_len.max()) + 3, 1)
+        dec = mel_len.clone()
+        dec[0] += 2
+        if B > 2:
+            dec[2] = T + 7
+        pe = torch.randn(T, D, device=DEV, generator=g)
+        W = torch.randn(NP, D, device=DEV, generator=g) / 16
+        bias = torch.randn(NP, device=DEV, generator=g) * 0.1
+        wp = ops.pack_conv_weight(W, L.FS2_BF16)
+        xw = ops.conv1d(x, wp, None, cin=D, ks=1, pad=0, compute=L.FS2_BF16, epilogue=L.EPI_BIAS,
+                        out_dtype=L.FS2_F32)
+        Wd = W.to(torch.bfloat16).double()
+        tab = (pe.double() @ Wd.t() + bias.double()).float().contiguous()
+        proj = (xw.view(-1, NP), tab)
+        if mode == "cum":
+            ref_x, ref_lay = ops.lr_fused(x, dec, T, pe=pe, out_dtype=L.FS2_BF16, cum=cum, mel_len=mel_len)
+            got_x, lay, q = ops.lr_fused(x, dec, T, pe=pe, out_dtype=L.FS2_BF16, cum=cum, mel_len=mel_len, proj=proj)
+        else:
+            ref_x, ref_lay, _, _, _ = ops.lr_fused(x, dec, T, pe=pe, out_dtype=L.FS2_BF16, dur=d)
+            got_x, lay, cum2, ml2, _, q = ops.lr_fused(x, dec, T, pe=pe, out_dtype=L.FS2_BF16, dur=d, proj=proj)
+            assert torch.equal(cum2, cum) and torch.equal(ml2, mel_len)
+        torch.cuda.synchronize()
+        R = int(lay.cu[-1])
+        assert torch.equal(lay.cu, ref_lay.cu) and torch.equal(lay.rowmap, ref_lay.rowmap)
+        assert torch.equal(got_x[:R], ref_x[:R])
+        # f64 reference of the frame-level projection
+        xe = ops.lr_expand(x.double().float(), cum, mel_len, T, pe=None, out_dtype=L.FS2_F32)  # [B, T, D] f32 exact
+        ref = (xe.double() + pe.double()[None]) @ Wd.t() + bias.double()
+        valid = (torch.arange(T, device=DEV)[None, :] < dec.clamp(0, T)[:, None]).reshape(-1)
+        ref = ref.reshape(-1, NP)[valid]
+        err = (q[:R].double() - ref).abs()
+        bound = ref.abs() * 2.0 ** -8 + 2e-5
+        assert bool((err <= bound).all()), (B, Lx, mode, float((err - bound).max()))

@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
     lib = _lib.load()
     declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
-    assert len(declared) == len(_lib.SIGNATURES) == 57
+    assert len(declared) == len(_lib.SIGNATURES) == 58
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
@@ -324,7 +324,7 @@ def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher, streams):
     assert n_conv == k * (10 * 4 + 6 + 1 + 5), rec.calls
     assert rec.calls.count("fs2_attention") == k * 10
     # the packed decoder's layout: built by the one-launch LengthRegulator (fs2_lr_fused)
-    assert ("fs2_lr_fused" in rec.calls) == (packed == "1")
+    assert any(c.startswith("fs2_lr_fused") for c in rec.calls) == (packed == "1")
     assert ("fs2_lr_expand" in rec.calls) == (packed == "0")
 
 

@@ -89,7 +89,7 @@ def main_enc(nsplit=4, tile_rows=64, with_qkv=True):
     part = ntiles * nsplit * 4 * 4 * MB * 64 * 16
     nwg = (ntiles * nsplit + 7) & ~7
     st = ws[4096 + part: 4096 + part + 256 * nwg].view(torch.int64).reshape(nwg, 32).cpu()
-    ok = st[:, 31] == 21
+    ok = st[:, 31] >= 21
     st = st[ok].double()
     last = st[:, 30] == 1
     t0 = st[:, 0].min()
@@ -143,10 +143,16 @@ def main_dec_pre():
     nwg = (R + 111) // 112
     assert B * T - nwg >= R, "no spare capacity rows for the stamps"
     st = out.view(torch.int64).reshape(B * T, -1)[B * T - nwg:].flip(0)[:, :32].cpu()
-    ok = st[:, 31] == 21
+    ok = st[:, 31] >= 21
     t = st[ok].double()
     print(f"workgroups traced {int(ok.sum())}")
     t[:, 27] = t[:, 28]  # kernel entry (slot 28) as column 27 for the table below
+    if int(st[0, 31]) >= 25:  # PRE sub-stamps: 21 loads issued, 22 landed, 23 / 24 row passes
+        for a, b_, name in ((27, 21, "  PRE: row masks, loads issued"), (21, 22, "  PRE: tiles + fc weights landed"),
+                            (22, 23, "  PRE: pass 0 (GEMM0 + LN, 64 rows)"), (23, 24, "  PRE: pass 1"),
+                            (24, 0, "  PRE: vectors + ring start")):
+            d = t[:, b_] - t[:, a]
+            print(f"{name:36s} mean {float(d.mean()):9.0f} max {float(d.max()):9.0f} cycles")
     segs = [(27, 0, "entry -> PRE prologue done"), (0, 1, "x tile landed / first units"), (1, 2, "c0 gemm1"), (2, 3, "c0 write_h"),
             (3, 4, "c0 gemm2 + c1 gemm1"), (4, 5, "c1 write_h"), (5, 6, "c1 gemm2 + c2 gemm1"), (6, 7, "c2 write_h"),
             (7, 8, "c2 gemm2 + c3 gemm1"), (8, 9, "c3 write_h"), (9, 10, "c3 gemm2"), (10, 12, "drain + barrier"),

@@ -4,7 +4,8 @@
     python tools/kernel_probe.py conv9 --reps 20
 kernels: ffn (decoder fused FFN, fs2_ffn), ffn_rows / ffn2_rows (decoder FFN fused / two launches on --rows
 packed rows), enc_ffn (encoder FFN fused, --nsplit), conv9 (decoder FFN Conv1d k=9 256->1024), conv1 (FFN k=1 1024->256 + res + LN),
-qkv, attn, lr (LengthRegulator gather + PE), postnet (512->512 k=5 + tanh), vpf / vpf_dp / vpf_en
+qkv, attn, lr (LengthRegulator gather + PE), lr_fused / lr_proj (the forward's LR launch without / with
+the first Q|K|V), postnet (512->512 k=5 + tanh), vpf / vpf_dp / vpf_en
 (fs2_vp_fused sets). --flush MB writes that much before each launch (cold caches).
 """
 import argparse
@@ -117,6 +118,14 @@ def main():
         xq = torch.randn(Bq, Lq, 256, generator=g).to(dev, dt)
         Tq = int(bb["max_mel_len"])
         fn = lambda: ops.lr_fused(xq, bb["mel_lens"], Tq, pe=P.dec_pe, out_dtype=P.act_dtype, dur=bb["d_targets"])
+    elif a.kernel == "lr_proj":  # lr_fused + the decoder's first Q|K|V by linearity (fs2_lr_fused_proj)
+        from fs2amd.runtime import _qkv_pe
+        Lq = b["texts"].shape[1]
+        xq = torch.randn(B, Lq, 256, generator=g).to(dev, dt)
+        xw = torch.randn(B * Lq, 768, generator=g).to(dev)
+        tab = _qkv_pe(P, T)
+        fn = lambda: ops.lr_fused(xq, b["mel_lens"], T, pe=P.dec_pe, out_dtype=P.act_dtype, dur=b["d_targets"],
+                                  proj=(xw, tab))
     elif a.kernel == "postnet":
         y = rnd(B, T, 512)
         pl = P.postnet[1]
