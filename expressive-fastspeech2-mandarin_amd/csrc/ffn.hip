@@ -370,17 +370,17 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
           for (int jb = 0; jb < 4; ++jb)
             a0[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][jb], fb[mb], a0[jb][mb], 0, 0, 0);
       }
-      // + bfc + residual; row statistics over the 4 waves' 64 columns each
-      float part[4], mean[4], var[4];
+      // + bfc + residual; row statistics over the 4 waves' 64 columns each (jb outer: each LDS
+      // vector read once per pass; per row the same summation order as row-major)
+      float part[4] = {0.f, 0.f, 0.f, 0.f}, mean[4], var[4];
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb) {
-        const int r = 64 * ps + 16 * mb + hr, gm = m0 - pad + r;
-        const bool ok = r < XROWS && gm >= 0 && gm < M;
-        float sum = 0.f;
+      for (int jb = 0; jb < 4; ++jb) {
+        const int n = w * 64 + jb * 16 + 4 * hq;
+        const float4 bb = *reinterpret_cast<const float4 *>(smem + VEC0_OFF + 4 * n);
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb) {
-          const int n = w * 64 + jb * 16 + 4 * hq;
-          const float4 bb = *reinterpret_cast<const float4 *>(smem + VEC0_OFF + 4 * n);
+        for (int mb = 0; mb < 4; ++mb) {
+          const int r = 64 * ps + 16 * mb + hr, gm = m0 - pad + r;
+          const bool ok = r < XROWS && gm >= 0 && gm < M;
           bf16x4 xv = {(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
           if (ok) xv = *reinterpret_cast<const bf16x4 *>(smem + X_OFF + r * XPITCH + n * 2);
           f32x4 v = a0[jb][mb];
@@ -389,9 +389,8 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
           v[2] = v[2] + bb.z + (float)xv[2];
           v[3] = v[3] + bb.w + (float)xv[3];
           a0[jb][mb] = v;
-          sum += (v[0] + v[1]) + (v[2] + v[3]);
+          part[mb] += (v[0] + v[1]) + (v[2] + v[3]);
         }
-        part[mb] = sum;
       }
       auto reduce4 = [&](float (&pv)[4], float (&tot)[4]) {
         float t[4];
@@ -431,31 +430,35 @@ __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
         part[mb] = ss;
       }
       reduce4(part, var);
+      float rstd[4], keep[4] = {1.f, 1.f, 1.f, 1.f};
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb) {
-        const int r = 64 * ps + 16 * mb + hr;
-        const float rstd = 1.0f / sqrtf(var[mb] * (1.0f / kD) + p.eps1);
-        // padded rows (t >= lens[b], the encoder's [B, L] form): h = masked_fill(LN1(.), 0)
-        // (transformer/Layers.py:25-26), the zeros the FFN's conv taps read past a sequence's end
-        float keep = 1.0f;
-        if (a.lens != nullptr) {
-          const int gm = m0 - pad + r;
+      for (int mb = 0; mb < 4; ++mb) rstd[mb] = 1.0f / sqrtf(var[mb] * (1.0f / kD) + p.eps1);
+      // padded rows (t >= lens[b], the encoder's [B, L] form): h = masked_fill(LN1(.), 0)
+      // (transformer/Layers.py:25-26), the zeros the FFN's conv taps read past a sequence's end
+      if (a.lens != nullptr) {
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          const int gm = m0 - pad + 64 * ps + 16 * mb + hr;
           if (gm >= 0 && gm < M) {
             const int bb = gm / T;
-            keep = (int64_t)(gm - bb * T) < a.lens[bb] ? 1.0f : 0.0f;
+            keep[mb] = (int64_t)(gm - bb * T) < a.lens[bb] ? 1.0f : 0.0f;
           }
         }
+      }
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb) {
-          const int n = w * 64 + jb * 16 + 4 * hq;
-          const float4 g = *reinterpret_cast<const float4 *>(smem + VEC0_OFF + 4 * (kD + n));
-          const float4 be = *reinterpret_cast<const float4 *>(smem + VEC0_OFF + 4 * (2 * kD + n));
+      for (int jb = 0; jb < 4; ++jb) {
+        const int n = w * 64 + jb * 16 + 4 * hq;
+        const float4 g = *reinterpret_cast<const float4 *>(smem + VEC0_OFF + 4 * (kD + n));
+        const float4 be = *reinterpret_cast<const float4 *>(smem + VEC0_OFF + 4 * (2 * kD + n));
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          const int r = 64 * ps + 16 * mb + hr;
           const f32x4 d = a0[jb][mb];
           bf16x4 o;
-          o[0] = (bf16)((d[0] * rstd * g.x + be.x) * keep);
-          o[1] = (bf16)((d[1] * rstd * g.y + be.y) * keep);
-          o[2] = (bf16)((d[2] * rstd * g.z + be.z) * keep);
-          o[3] = (bf16)((d[3] * rstd * g.w + be.w) * keep);
+          o[0] = (bf16)((d[0] * rstd[mb] * g.x + be.x) * keep[mb]);
+          o[1] = (bf16)((d[1] * rstd[mb] * g.y + be.y) * keep[mb]);
+          o[2] = (bf16)((d[2] * rstd[mb] * g.z + be.z) * keep[mb]);
+          o[3] = (bf16)((d[3] * rstd[mb] * g.w + be.w) * keep[mb]);
           if (r < XROWS) *reinterpret_cast<bf16x4 *>(smem + X_OFF + r * XPITCH + n * 2) = o;
         }
       }

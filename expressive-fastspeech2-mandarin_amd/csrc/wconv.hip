@@ -39,6 +39,15 @@ struct WconvArgs {
   const int2 *row_pos;     // packed rows: {frame, length} per row (NULL: padded [B, T] rows)
   const int32_t *rows_dev; // packed rows: the active row count (device)
   int out_sc1;             // write-through output rows (conv_common.h store16_out)
+  // TAIL (the PostNet's last two convs in one launch): the 512 -> 80 conv + residual on this
+  // conv's output tile; w2 in pn_tail's k-step-major order, f32 out2 = conv + bias2 + res
+  const bf16 *w2;
+  const float *bias2;
+  const float *res;
+  int64_t rs;
+  float *out2;
+  int64_t os2;
+  uint32_t w2_bytes;
 };
 
 // position and length of row m's sequence: packed rows from row_pos, padded rows t = m mod T
@@ -73,12 +82,166 @@ __device__ __forceinline__ float tanh_fast(float x) {
   return fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + e), 1.0f);
 }
 
+// The fused PostNet tail (wconv_kernel<5, 512, 1, true>): this conv's 112 output rows (y, + bias,
+// tanh) go to LDS at the x-tile pitch and feed the 512 -> 80 conv + residual (transformer/Layers.py
+// :129-137, fastspeech2.py:136) on the workgroup's TB = 108 middle rows -- pn_tail_kernel's k-step
+// order (so the result is bit-identical to the two launches) without the 28 MB y round trip or
+// its launch. LDS bandwidth bounds this part (every wave reads the k-step's 5 KiB of weight
+// fragments), so 4 waves, one per SIMD, own 2 row blocks x the 5 column blocks each (27 KiB of
+// fragment reads per k-step instead of 42 with one row block per wave); the other 4 waves DMA
+// the weight ring (2 k-steps x 5 KiB per stage, 3 stages).
+#ifndef WCONV_TAIL_ABLATE
+#define WCONV_TAIL_ABLATE 0  // analysis builds only: 1 skips the tail MFMA loop, 2 the whole tail (timing)
+#endif
+template <int X_OFF, int XPITCH, int BIAS_OFF, int W_OFF, int B_OFF>
+__device__ __forceinline__ void tail_epilogue(const WconvArgs &p, const f32x4 (&acc)[4][7], char *smem, int m0, int M,
+                                              int T, int w, int lane) {
+  constexpr int MB = 7, KS = 5, NB = 5, KPS = 2, NST = 3, STG = KPS * NB * 1024, NKS = 16, NS = KS * NKS / KPS;
+  constexpr int TB = 16 * MB - (KS - 1);
+  const int hrow0 = lane & 15, hi = lane >> 4;
+  if (WCONV_TAIL_ABLATE & 2) return;
+  const rsrc_t w2r = make_rsrc(p.w2, p.w2_bytes);
+  // waves 4..7 DMA a stage's 10 pieces: 3, 3, 2, 2
+  const int dw = w - 4, npc = dw < 2 ? 3 : 2;
+  auto wdma = [&](int st_idx) {
+    if (dw >= 0) {
+      char *st = smem + W_OFF + (st_idx % NST) * STG;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int pc = dw + 4 * j;
+        if (j < npc)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(w2r, (__attribute__((address_space(3))) void *)(st + pc * 1024), 16,
+                                                   (uint32_t)(st_idx * KPS * NB + pc) * 1024u + (uint32_t)lane * 16u, 0,
+                                                   0, 0);
+      }
+    }
+  };
+  auto wait_stages = [&](bool one_in_flight) {  // this wave's pieces of the older stages landed
+    if (!one_in_flight)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (npc == 3)
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  };
+  wdma(0);
+  wdma(1);
+  if (w == 3 && lane < 20)
+    *reinterpret_cast<float4 *>(smem + B_OFF + 16 * lane) = reinterpret_cast<const float4 *>(p.bias2)[lane];
+  // y = bf16(tanh(acc + b)) at the x pitch: row r of the tile is row m0 + r
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const int n = w * 64 + nb * 16 + 4 * hi;
+    const float4 bb = *reinterpret_cast<const float4 *>(smem + BIAS_OFF + 4 * n);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const f32x4 v = acc[nb][mb];
+      bf16x4 o;
+      o[0] = (bf16)tanh_fast(v[0] + bb.x);
+      o[1] = (bf16)tanh_fast(v[1] + bb.y);
+      o[2] = (bf16)tanh_fast(v[2] + bb.z);
+      o[3] = (bf16)tanh_fast(v[3] + bb.w);
+      *reinterpret_cast<bf16x4 *>(smem + X_OFF + (hrow0 + mb * 16) * XPITCH + n * 2) = o;
+    }
+  }
+  // waves 0..3: tail rows i = 32 w + 16 j + hrow0 (j = 0, 1; i < TB), row g = m0 + 2 + i; tap t
+  // reads tile row i + t
+  int vt[2] = {0, 0}, ri[2], gi[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    ri[j] = 32 * w + 16 * j + hrow0;
+    gi[j] = m0 + (KS - 1) / 2 + ri[j];
+    if (w < 4 && ri[j] < TB && gi[j] < M) {
+      int tpos, tlen;
+      seq_pos(p.row_pos, gi[j], T, tpos, tlen);
+#pragma unroll
+      for (int tap = 0; tap < KS; ++tap) vt[j] |= ((unsigned)(tpos + tap - 2) < (unsigned)tlen ? 1 : 0) << tap;
+    }
+  }
+  f32x4 at[NB][2];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) at[b][0] = at[b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // software-pipelined: stage st + 1's fragments are read (after its barrier) before stage st's
+  // 20 MFMAs issue, so the LDS latency hides under them; the ring is 3 stages deep (DMA two ahead)
+  struct Frags {
+    bf16x8 fa[KPS][NB], fb[KPS][2];
+  };
+  auto read_stage = [&](int st, Frags &f) {
+    const char *sp = smem + W_OFF + (st % NST) * STG;
+#pragma unroll
+    for (int q = 0; q < KPS; ++q) {
+      const int u = st * KPS + q, tap = u >> 4, ks = u & 15;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ad = (X_OFF + (ri[j] + tap) * XPITCH + hi * 16) & __builtin_amdgcn_sbfe(vt[j], tap, 1);
+        f.fb[q][j] = *reinterpret_cast<const bf16x8 *>(smem + ad + ks * 64);
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b) f.fa[q][b] = *reinterpret_cast<const bf16x8 *>(sp + (q * NB + b) * 1024 + lane * 16);
+    }
+  };
+  auto mma_stage = [&](const Frags &f) {
+#pragma unroll
+    for (int q = 0; q < KPS; ++q)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) at[b][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.fa[q][b], f.fb[q][j], at[b][j], 0, 0, 0);
+  };
+  wdma(2);
+  asm volatile("" ::: "memory");
+  // stage 0 landed (stages 1 and 2 may stay in flight)
+  if (npc == 3)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(kLgkm0);
+  __syncthreads();  // y rows, tail bias, stage 0 visible
+  Frags F0, F1;
+  if (w < 4) read_stage(0, F0);
+  auto step = [&](int st, Frags &cur, Frags &nxt) {
+    if (st + 1 < NS) {
+      wait_stages(st + 2 < NS);  // stage st + 1 landed (st + 2 may stay in flight)
+      __builtin_amdgcn_s_waitcnt(kLgkm0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();  // ... visible; every wave's reads of stage st's slot are done
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + NST < NS) wdma(st + NST);  // into stage st's slot
+      if (w < 4) read_stage(st + 1, nxt);
+    }
+    if (w < 4) mma_stage(cur);
+  };
+#pragma nounroll
+  for (int st = 0; st < NS; st += 2) {
+    step(st, F0, F1);
+    step(st + 1, F1, F0);
+  }
+  // + bias2 + residual, f32 rows (lane: row g, columns 16 b + 4 hi .. + 3)
+  if (w < 4) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (ri[j] < TB && gi[j] < M) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const int n = b * 16 + 4 * hi;
+          const float4 bb = *reinterpret_cast<const float4 *>(smem + B_OFF + 4 * n);
+          const float4 r = *reinterpret_cast<const float4 *>(p.res + (size_t)gi[j] * p.rs + n);
+          const f32x4 v = at[b][j];
+          *reinterpret_cast<float4 *>(p.out2 + (size_t)gi[j] * p.os2 + n) =
+              make_float4((v[0] + bb.x) + r.x, (v[1] + bb.y) + r.y, (v[2] + bb.z) + r.z, (v[3] + bb.w) + r.w);
+        }
+      }
+    }
+  }
+}
+
 // CIN % 32 != 0 (the PostNet's first conv, 80 -> 512): the K dimension is (tap, channel) flattened,
 // k = tap * CIN + c, in 32-wide steps ("flat" units); a lane group's 8 consecutive k stay inside one
 // tap (CIN % 8 == 0), so each lane addresses its own (row + tap, channel) per unit.
-template <int KS, int CIN, int WQ>
+template <int KS, int CIN, int WQ, bool TAIL = false>
 __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
   constexpr bool FLAT = CIN % 32 != 0;
+  static_assert(!TAIL || (KS == 5 && CIN == 512 && WQ == 1), "the fused tail: the PostNet's 512 -> 512 -> 80");
   static_assert(CIN % 8 == 0, "8-channel lane groups");
   // WQ: 64-column quads per wave (1: 8 waves, two per SIMD; 2: 4 waves, 128 columns each)
   constexpr int MB = 7, BM = 16 * MB, NWV = 8 / WQ, NT = 64 * NWV, NCOL = 512, JB = 4 * WQ;
@@ -93,7 +256,11 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
   // the x region doubles as the output staging area (sized for the larger of the two)
   constexpr int XREG = NWV * XP_PER_WAVE * 1024 > BM * OPITCH ? NWV * XP_PER_WAVE * 1024 : BM * OPITCH;
   constexpr int BIAS_OFF = X_OFF + XREG;
-  constexpr int SMEM = BIAS_OFF + NCOL * 4;
+  // TAIL: the 512 -> 80 conv's weight ring (NST stages of 2 k-steps x 5 fragment blocks) + bias
+  constexpr int T_NB = 5, T_KPS = 2, T_NST = 3, T_STG = T_KPS * T_NB * 1024;
+  constexpr int T_W_OFF = BIAS_OFF + NCOL * 4;
+  constexpr int T_B_OFF = T_W_OFF + T_NST * T_STG;
+  constexpr int SMEM = TAIL ? T_B_OFF + 80 * 4 : BIAS_OFF + NCOL * 4;
   static_assert(SMEM <= 163840, "LDS");
   constexpr int DEPTH = WQ == 1 ? 4 : 2;
   static_assert(FLAT || NKS % DEPTH == 0, "static ring slots");
@@ -102,8 +269,11 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = p.rows_dev != nullptr ? min(*p.rows_dev, p.M) : p.M, T = p.T, pad = p.pad;
-  const int m0 = blockIdx.x * BM;
-  if (m0 >= M) return;
+  // TAIL: a workgroup's 112 rows of this conv's output feed TB = 108 rows of the tail conv (its
+  // taps reach 2 rows either side), so workgroups step by 108 and start 2 rows early
+  constexpr int TB = TAIL ? BM - (KS - 1) : BM;
+  if ((int)blockIdx.x * TB >= M) return;
+  const int m0 = (int)blockIdx.x * TB - (TAIL ? (KS - 1) / 2 : 0);
   const int hrow0 = lane & 15, hi = lane >> 4;
 
   // tap validity (padded rows: position t mod T in a sequence of T frames; packed: row_pos)
@@ -112,7 +282,7 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
   for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + mb * 16 + hrow0;
     int tpos = 0, tlen = 0;
-    if (m < M) seq_pos(p.row_pos, m, T, tpos, tlen);
+    if (m >= 0 && m < M) seq_pos(p.row_pos, m, T, tpos, tlen);
     int v = 0;
 #pragma unroll
     for (int tap = 0; tap < KS; ++tap) v |= ((unsigned)(tpos + tap - pad) < (unsigned)tlen ? 1 : 0) << tap;
@@ -247,6 +417,10 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_waitcnt(kLgkm0);
   __syncthreads();
+  if constexpr (TAIL) {
+    tail_epilogue<X_OFF, XPITCH, BIAS_OFF, T_W_OFF, T_B_OFF>(p, acc, smem, m0, M, T, w, lane);
+    return;
+  } else {
 #pragma unroll
   for (int nb = 0; nb < JB; ++nb) {
     const int n = w * 64 * WQ + nb * 16 + 4 * hi;
@@ -272,6 +446,7 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
     if (m0 + m < M)
       store16_out(ob, (uint32_t)(m0 + m) * orow + (uint32_t)ch * 16u,
                   *reinterpret_cast<const uint4 *>(smem + X_OFF + m * OPITCH + ch * 16), p.out_sc1);
+  }
   }
 }
 
@@ -704,8 +879,9 @@ extern "C" int64_t fs2_wconv_weight_elems(int KS, int Cin, int N) { return (int6
 extern "C" int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream) {
   if (d == nullptr || d->x == nullptr || d->w == nullptr || d->bias == nullptr || d->out == nullptr)
     return FS2_EINVAL;
+  const bool fused_tail = d->w2 != nullptr && d->Cin == 512;  // out: the f32 [B*T, 80] tail output
   if (d->B < 0 || d->T < 0 || d->pad < 0 || d->x_row_stride < d->Cin || (d->x_row_stride & 7) ||
-      d->out_row_stride < d->N || (d->out_row_stride & 7))
+      (!fused_tail && (d->out_row_stride < d->N || (d->out_row_stride & 7))))
     return FS2_EINVAL;
   const bool tail = d->epilogue == FS2_EPI_BIAS_RES;  // the last conv: N = 80, + residual, f32 out
   if (tail) {
@@ -768,7 +944,22 @@ extern "C" int fs2_wconv(const fs2_wconv_desc *d, fs2_stream_t stream) {
 #ifndef WCONV_WQ
 #define WCONV_WQ 1  // 8 waves x 64 columns (2 quads per wave: 224 accumulators + the ring spill; analysis only)
 #endif
-  if (d->w2 != nullptr) {
+  if (fused_tail) {
+    // the PostNet's last two layers fused (512 -> 512 tanh, then 512 -> 80 + residual, f32 out)
+    if (d->bias2 == nullptr || d->residual == nullptr || d->pad != 2 || d->res_row_stride < 80 ||
+        (d->res_row_stride & 3) || d->out_row_stride < 80 || (d->out_row_stride & 3))
+      return FS2_EINVAL;
+    p.w2 = reinterpret_cast<const bf16 *>(d->w2);
+    p.bias2 = d->bias2;
+    p.res = d->residual;
+    p.rs = d->res_row_stride;
+    p.out2 = reinterpret_cast<float *>(d->out);
+    p.os2 = d->out_row_stride;
+    p.out = nullptr;
+    p.w2_bytes = (uint32_t)(fs2_wconv_weight_elems(5, 512, 80) * 2);
+    hipLaunchKernelGGL((wconv_kernel<5, 512, 1, true>), dim3((unsigned)((Mg + 107) / 108)), dim3(512), 0,
+                       as_stream(stream), p);
+  } else if (d->w2 != nullptr) {
     // the PostNet's first two layers fused (80 -> 512 -> 512, both tanh)
     if (d->Cin != 80 || d->bias2 == nullptr || d->pad != 2) return FS2_EUNSUPPORTED;
     PnHeadArgs q;

@@ -440,11 +440,14 @@ def hifigan_mrf(x, x_act, w_packed, bias, out_slope, out=None):
     return out
 
 
-def wconv(x, w_packed, bias, *, ks, pad, out=None, second=None, layout=None):
+def wconv(x, w_packed, bias, *, ks, pad, out=None, second=None, layout=None, tail=None):
     """PostNet Conv1d(512, 512, k=5) + folded BatchNorm + tanh on padded bf16 rows [B, T, 512]
     (fs2_wconv; w_packed from :func:`pack_wconv_weight`). second = (w2_packed, bias2): the next
-    512 -> 512 conv applied in the same launch (the PostNet's layers 0 and 1, Cin = 80). layout:
-    packed rows [B*T, C] (ops.SeqLayout; the valid-region PostNet)."""
+    512 -> 512 conv applied in the same launch (the PostNet's layers 0 and 1, Cin = 80). tail =
+    (w_tail from :func:`pack_wconv_tail`, bias_tail, residual f32): the PostNet's last conv +
+    residual on this conv's output in the same launch (layers 3 and 4, Cin = 512): returns the f32
+    [.., 80] PostNet output instead. layout: packed rows [B*T, C] (ops.SeqLayout; the valid-region
+    PostNet)."""
     _gpu(x, w_packed, bias)
     if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
         raise TypeError("fs2amd.wconv: bf16 activations and weights only")
@@ -454,6 +457,24 @@ def wconv(x, w_packed, bias, *, ks, pad, out=None, second=None, layout=None):
     if second is not None:
         _gpu(*second)
         assert second[0].numel() == _lib.fs2_wconv_weight_elems(ks, N, N) and second[1].numel() == N
+    if tail is not None:
+        wt, bt, res = tail
+        _gpu(wt, bt, res)
+        assert second is None and cin == 512 and N == 512 and bt.numel() == 80 and res.dtype == torch.float32
+        assert wt.dtype == torch.bfloat16 and wt.numel() == _lib.fs2_wconv_weight_elems(ks, 512, 80)
+        assert tuple(res.shape) == (*rs, 80), (tuple(res.shape), rs)
+        if out is None:
+            out = torch.empty(*rs, 80, device=x.device, dtype=torch.float32)
+        d = L.WconvDesc()
+        _wconv_layout(d, layout)
+        d.x, d.x_row_stride = x.data_ptr(), _rows(x, "x")
+        d.w, d.bias = w_packed.data_ptr(), bias.data_ptr()
+        d.B, d.T, d.Cin, d.N, d.KS, d.pad, d.epilogue = B, T, cin, N, ks, pad, L.EPI_BIAS_TANH
+        d.out, d.out_row_stride = out.data_ptr(), _rows(out, "out")
+        d.w2, d.bias2 = wt.data_ptr(), bt.data_ptr()
+        d.residual, d.res_row_stride = res.data_ptr(), _rows(res, "residual")
+        L.check(_lib.fs2_wconv(ctypes.byref(d), _stream(x)), "fs2_wconv")
+        return out
     if out is None:
         out = torch.empty(*rs, N, device=x.device, dtype=torch.bfloat16)
     d = L.WconvDesc()

@@ -770,6 +770,11 @@ def pn_head_on():
     return os.environ.get("FS2_PN_HEAD", "1") != "0"
 
 
+def pn_tail_fused_on():
+    """FS2_PN_TAIL_FUSED=0: the PostNet's last conv + residual as its own fs2_wconv launch (A/B)."""
+    return os.environ.get("FS2_PN_TAIL_FUSED", "1") != "0"
+
+
 def postnet_valid_region_on():
     return os.environ.get("FS2_POSTNET_VALID", "1") != "0"
 
@@ -822,9 +827,17 @@ def _postnet_convs(P, y, res, layout=None):
         l0, l1 = P.postnet[0], P.postnet[1]
         y = ops.wconv(y, l0.wfr, l0.b, ks=l0.k, pad=l0.p, second=(l1.wfr, l1.b), layout=layout)
         first = 2
+    last = P.postnet[-1]
     for i, lp in enumerate(P.postnet):
         if i < first:
             continue
+        if i == n_pn - 2 and n_pn > 2 and getattr(lp, "wfr", None) is not None and lp.cin == 512 and lp.k == 5 \
+                and lp.p == 2 and getattr(last, "wtail", None) is not None and wconv_on() and pn_tail_fused_on() \
+                and y.dtype == torch.bfloat16 and res.dtype == torch.float32:
+            # layers 3 and 4 (512 -> 512 tanh, 512 -> 80 + residual) in one launch: the 512-channel
+            # output stays on chip
+            return ops.wconv(y, lp.wfr, lp.b, ks=lp.k, pad=lp.p, layout=layout,
+                             tail=(last.wtail, last.b, res.contiguous()))
         if i < n_pn - 1 and getattr(lp, "wfr", None) is not None and wconv_on() and y.dtype == torch.bfloat16:
             # 512 -> 512 convs: the weight-streamed kernel (fs2_wconv)
             y = ops.wconv(y, lp.wfr, lp.b, ks=lp.k, pad=lp.p, layout=layout)

@@ -305,6 +305,10 @@ typedef struct fs2_wconv_desc {
      conv(x; w) + bias); w2) + bias2). w2: fs2_wconv_weight_elems(5, 512, 512) elements, NULL = off */
   const void *w2;
   const float *bias2;
+  /* w2 with Cin = 512 (N = 512, KS = 5, pad 2, tanh): the PostNet's last two layers in one launch
+     (transformer/Layers.py:92-137 layers 3 and 4 + fastspeech2.py:136): out is then f32 [B*T, >= 80]
+     = conv(tanh(conv(x; w) + bias); w2) + bias2 + residual, w2 / bias2 / residual as the
+     FS2_EPI_BIAS_RES form below; the 512-channel intermediate never leaves the chip */
   /* epilogue FS2_EPI_BIAS_RES (the PostNet's last conv + the residual, fastspeech2.py:136): Cin = 512,
      N = 80, KS = 5, pad 2; out f32 [B*T, >= 80] = conv(x; w) + bias + residual (f32 [B*T, >= 80]);
      w in the k-step-major order [K/32][N/16][4][16][8], element (s, b, h, r, e) = W[16b + r][32s + 8h + e] */

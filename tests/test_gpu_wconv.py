@@ -144,3 +144,43 @@ def test_postnet_valid_region_equals_padded(gpu, prec):
         valid = R._postnet(P, mel, mel_bf, lens, int(lens.sum()))
     torch.cuda.synchronize()
     assert torch.equal(valid, full), float((valid - full).abs().max())
+
+
+@pytest.mark.parametrize("B,T,seed,packed", [(64, 430, 31, False), (3, 37, 32, False), (1, 1, 33, False),
+                                             (5, 113, 34, False), (2, 3, 35, False), (9, 250, 36, True),
+                                             (4, 61, 37, True)])
+def test_pn_tail_fused_equals_two_launches(gpu, B, T, seed, packed):
+    """The PostNet's layers 3 and 4 in one launch (fs2_wconv with a Cin = 512 w2: the 512 -> 512
+    tanh output kept on chip, the 512 -> 80 conv + residual on each workgroup's 108 middle rows)
+    equal fs2_wconv + the N = 80 tail launch BIT-EXACTLY: the same bf16 intermediate rows (per-row
+    arithmetic independent of the 108-row tiling) and pn_tail's k-step order; ragged T, a lone row,
+    T below the halo, padded rows and packed rows (lengths 0 / 1 / T included)."""
+    ops, L = gpu
+    x, w, s, b = _case(ops, L, B, T, seed, 512)
+    g = torch.Generator(device=DEV).manual_seed(seed + 500)
+    wt = torch.randn(80, 512, 5, device=DEV, generator=g) / (512 * 5) ** 0.5
+    sc = 1 + 0.1 * torch.randn(80, device=DEV, generator=g)
+    bt = 0.1 * torch.randn(80, device=DEV, generator=g)
+    res = torch.randn(B, T, 80, device=DEV, generator=g)
+    p, pt = ops.pack_wconv_weight(w, scale=s), ops.pack_wconv_tail(wt, scale=sc)
+    lay = None
+    if packed:
+        lens = torch.randint(0, T + 1, (B,), generator=torch.Generator().manual_seed(seed)).to(DEV)
+        lens[0], lens[-1] = T, 0
+        if B > 2:
+            lens[1] = 1
+        lay = ops.SeqLayout(lens, T)
+        rm = lay.rowmap.long()
+        ok = rm >= 0
+        xp = x.new_zeros(lay.capacity, 512)
+        xp[rm[ok]] = x.reshape(-1, 512)[ok]
+        rp = res.new_zeros(lay.capacity, 80)
+        rp[rm[ok]] = res.reshape(-1, 80)[ok]
+        x, res = xp, rp
+    two = ops.wconv_tail(ops.wconv(x, p, b, ks=5, pad=2, layout=lay), pt, bt, res, layout=lay)
+    one = ops.wconv(x, p, b, ks=5, pad=2, layout=lay, tail=(pt, bt, res))
+    torch.cuda.synchronize()
+    if lay is not None:
+        R = int(lay.cu[-1])
+        one, two = one[:R], two[:R]
+    assert torch.equal(one, two), float((one - two).abs().max())

@@ -135,6 +135,14 @@ def main():
         y = rnd(B, T, 512)
         pl = P.postnet[1]
         fn = lambda: ops.wconv(y, pl.wfr, pl.b, ks=5, pad=2)
+    elif a.kernel in ("pn_tail_fused", "pn_tail"):  # PostNet layers 3 + 4 in one launch / the N = 80 tail alone
+        y = rnd(B, T, 512)
+        pl, pt = P.postnet[3], P.postnet[4]
+        res = torch.randn(B, T, 80, generator=g).to(dev)
+        if a.kernel == "pn_tail":
+            fn = lambda: ops.wconv_tail(y, pt.wtail, pt.b, res)
+        else:
+            fn = lambda: ops.wconv(y, pl.wfr, pl.b, ks=5, pad=2, tail=(pt.wtail, pt.b, res))
     elif a.kernel in ("postnet_first", "postnet_first_bf", "postnet_last"):
         # PostNet 80->512 (f32 mel in, or its bf16 copy) / 512->80 + residual
         mel = torch.randn(B, T, 80, generator=g).to(dev)
