@@ -278,11 +278,24 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
 
   // tap validity (padded rows: position t mod T in a sequence of T frames; packed: row_pos)
   int vmask[MB];
+  int2 rq[MB];  // packed rows: every block's row_pos entry loaded before any is used (one wait)
+  if (p.row_pos != nullptr) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) rq[mb] = p.row_pos[min(max(m0 + mb * 16 + hrow0, 0), M - 1)];
+  }
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + mb * 16 + hrow0;
     int tpos = 0, tlen = 0;
-    if (m >= 0 && m < M) seq_pos(p.row_pos, m, T, tpos, tlen);
+    if (m >= 0 && m < M) {
+      if (p.row_pos != nullptr) {
+        tpos = rq[mb].x;
+        tlen = rq[mb].y;
+      } else {
+        tpos = m % T;
+        tlen = T;
+      }
+    }
     int v = 0;
 #pragma unroll
     for (int tap = 0; tap < KS; ++tap) v |= ((unsigned)(tpos + tap - pad) < (unsigned)tlen ? 1 : 0) << tap;
@@ -290,8 +303,11 @@ __global__ __launch_bounds__(512 / WQ, 1) void wconv_kernel(WconvArgs p) {
   }
   for (int i = tid; i < ZBYTES / 16; i += NT)
     *reinterpret_cast<float4 *>(smem + 16 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (tid < NCOL / 4)
-    *reinterpret_cast<float4 *>(smem + BIAS_OFF + 16 * tid) = reinterpret_cast<const float4 *>(p.bias)[tid];
+  // bias -> LDS by LDS-DMA (1 KiB pieces, waves 0..1): no load-to-store wait before the x tile DMA
+  if (w < NCOL / 256)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(p.bias, NCOL * 4),
+                                             (__attribute__((address_space(3))) void *)(smem + BIAS_OFF + w * 1024), 16,
+                                             (uint32_t)(w * 1024 + lane * 16), 0, 0, 0);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) asm volatile("" ::"v"(vmask[mb]));
 
@@ -511,10 +527,11 @@ __global__ __launch_bounds__(512, 1) void pn_head_kernel(PnHeadArgs p) {
     return v;
   };
   for (int i = tid; i < ZBYTES / 16; i += NT) *reinterpret_cast<float4 *>(smem + 16 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (tid < NCOL / 4) {
-    *reinterpret_cast<float4 *>(smem + B1_OFF + 16 * tid) = reinterpret_cast<const float4 *>(p.b1)[tid];
-    *reinterpret_cast<float4 *>(smem + B2_OFF + 16 * tid) = reinterpret_cast<const float4 *>(p.b2)[tid];
-  }
+  // b1 | b2 -> LDS by LDS-DMA (waves 0..3, one 1 KiB piece each; B2_OFF = B1_OFF + 2 KiB)
+  if (w < 4)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(w < 2 ? p.b1 : p.b2, NCOL * 4),
+                                             (__attribute__((address_space(3))) void *)(smem + B1_OFF + w * 1024), 16,
+                                             (uint32_t)((w & 1) * 1024 + lane * 16), 0, 0, 0);
 
   // mel tile -> LDS (lane-linear 1 KiB pieces at the padded pitch)
   const rsrc_t xr = make_rsrc(p.x, p.x_bytes);
