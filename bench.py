@@ -271,7 +271,7 @@ def time_kernel_in_forward(model, batch, n_fwd=6, fwd=None):
     return {k: (sum(v) / len(v), len(v)) for k, v in by.items()}
 
 
-GEMM_OPS = {"qkv", "qkv0", "fc", "ffn", "ffn+qkv", "fc+ffn", "fc+ffn+qkv", "conv9", "conv1", "ffn8"}
+GEMM_OPS = {"qkv", "qkv0", "qkv+attn+fc", "fc", "ffn", "ffn+qkv", "fc+ffn", "fc+ffn+qkv", "conv9", "conv1", "ffn8"}
 FFT_GEMM_FLOPS_PER_TOKEN = 2 * (256 * 768 + 256 * 256 + 256 * 9 * 1024 + 1024 * 256)  # 5,767,168
 
 

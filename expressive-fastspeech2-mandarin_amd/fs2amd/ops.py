@@ -672,6 +672,25 @@ def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None, lse=No
     return out
 
 
+def enc_attn_block(x, lens, wqkv_frag, bqkv, wfc_frag, bfc, ln, n_head, d_k, temperature, out=None):
+    """fs2_enc_attn_block: the encoder FFT block's attention sub-layer (Q|K|V projection, masked
+    2-head attention, fc + residual + LayerNorm, padded rows zeroed) in one launch, bf16
+    [B, L <= 64, 256] -> bf16 [B, L, 256]. Weights in fragment order (:func:`pack_frag_rows`)."""
+    _gpu(x, lens, wqkv_frag, bqkv, wfc_frag, bfc)
+    B, Lx, D = x.shape
+    assert x.dtype == torch.bfloat16 and x.is_contiguous() and D == n_head * d_k, (x.dtype, tuple(x.shape))
+    assert lens.dtype == torch.int64 and lens.numel() == B, (lens.dtype, lens.numel(), B)
+    assert wqkv_frag.dtype == torch.bfloat16 and wqkv_frag.numel() == 3 * D * D and bqkv.numel() == 3 * D
+    assert wfc_frag.dtype == torch.bfloat16 and wfc_frag.numel() == D * D and bfc.numel() == D
+    g, b, eps = ln
+    if out is None:
+        out = torch.empty_like(x)
+    L.check(_lib.fs2_enc_attn_block(_ptr(x), _ptr(lens), B, Lx, _ptr(wqkv_frag), _ptr(bqkv), _ptr(wfc_frag),
+                                    _ptr(bfc), _ptr(g), _ptr(b), float(eps), n_head, d_k, float(temperature),
+                                    _ptr(out), _stream(x)), "fs2_enc_attn_block")
+    return out
+
+
 _bad_ids = {}
 
 

@@ -149,6 +149,11 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
         rows = int(layout.cu[-1]) if layout is not None else None
         xv = x[:rows] if rows is not None else x
         CALIB.setdefault(lp.key, {})["x"] = float(xv.float().abs().max()) if xv.numel() else 0.0
+    if qkv is None and layout is None and lens is not None and enc_block_ok(P, lp, x):
+        # Q|K|V + attention + fc + residual + LN + row mask as one launch per utterance (L <= 64)
+        with _tm("qkv+attn+fc"):
+            h = ops.enc_attn_block(x, lens, lp.wqf, lp.bqkv, lp.wfcf, lp.bfc, lp.ln1, H, dk, float(np.power(dk, 0.5)))
+        return _ffn_tail(P, lp, x, h, lens, addvec1, addvec2, timed, layout, q, next_s, nxt)
     if qkv is not None:
         pass
     elif q is not None and q.wqkv is not None and x8 is not None:
@@ -184,6 +189,15 @@ def fft_block(P, lp, x, lens, addvec1=None, addvec2=None, timed=False, layout=No
         h = ops.conv1d(att, lp.wfc, lp.bfc, cin=d_model, ks=1, pad=0, compute=c, epilogue=L.EPI_RES_LN,
                        out_dtype=dt, residual=x, ln=lp.ln1, lens=lens, layout=layout, out2=h8,
                        out2_scale=1.0 / q.s_h if q is not None else 1.0)
+    return _ffn_tail(P, lp, x, h, lens, addvec1, addvec2, timed, layout, q, next_s, nxt, h8=h8)
+
+
+def _ffn_tail(P, lp, x, h, lens, addvec1, addvec2, timed, layout, q, next_s, nxt, h8=None):
+    """The FFT block after its attention sub-layer: the PositionwiseFeedForward on h (fused or two
+    launches, fp8 forms) -> (out, out8|None, next block's qkv|None)."""
+    c = P.compute
+    dt = P.act_dtype
+    d_model = lp.n_head * lp.d_k
     if q is not None and layout is not None and getattr(q, "w12_8", None) is not None and ffn8_on() \
             and CALIB is None and lp.k1 == 9 and lp.p1 == 4:
         # cfg5: the whole FFN as ONE e4m3 launch (fs2_ffn8: hidden quantised on chip, never in HBM)
@@ -249,6 +263,20 @@ def qkv_fused_on():
     """The next block's Q|K|V projection in the fused FFN's epilogue (fs2_ffn wqkv). FS2_QKV_FUSED=0:
     separate Q|K|V launches (A/B)."""
     return os.environ.get("FS2_QKV_FUSED", "1") != "0"
+
+
+def enc_block_on():
+    """FS2_ENC_BLOCK=0: the encoder's attention sub-layer as three launches (A/B)."""
+    return os.environ.get("FS2_ENC_BLOCK", "1") != "0"
+
+
+def enc_block_ok(P, lp, x):
+    """fs2_enc_attn_block applies: bf16 padded [B, L <= 64, 256] rows, 2 x 128-dim heads, the
+    fragment-ordered Q|K|V / fc weights, a bf16 layer (not cfg5's fp8 ones), no calibration pass."""
+    return (enc_block_on() and P.compute == L.FS2_BF16 and x.dtype == torch.bfloat16 and x.dim() == 3
+            and x.shape[1] <= 64 and x.shape[2] == 256 and lp.n_head == 2 and lp.d_k == 128 and CALIB is None
+            and getattr(lp, "wqf", None) is not None and getattr(lp, "wfcf", None) is not None
+            and lp.fp8 is None)  # fp8 layers: their FFN reads the fp8 copy of h the fc epilogue writes
 
 
 def qkv_epilogue_ok(x, layout, lp):

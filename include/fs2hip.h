@@ -344,6 +344,21 @@ int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int6
                   float *lse, fs2_stream_t stream);
 
 /*
+ * fs2_enc_attn_block — the encoder FFT block's attention sub-layer as ONE launch (bf16): Q|K|V
+ * projection (transformer/SubLayers.py:39-41), 2-head attention with the key-padding mask
+ * (Modules.py:14-25), output projection + residual + LayerNorm (SubLayers.py:54-55) and the
+ * padded-row mask (Layers.py:25): out[b, t] = t < lens[b] ? LN(fc(attn(x))[b, t] + x[b, t]) : 0.
+ * Replaces fs2_conv1d (Q|K|V) + fs2_attention + fs2_conv1d (EPI_RES_LN) for short sequences: one
+ * workgroup per utterance, Q|K|V and the attention output kept in LDS.
+ * x / out: bf16 [B, L, 256] (out != x); lens int64 [B]; wqkv / wfc: the [768, 256] / [256, 256]
+ * weights in MFMA fragment order ([N/64][K/32][4][4][16][8] bf16, fs2amd.ops.pack_frag_rows);
+ * bqkv f32 [768], bfc / gamma / beta f32 [256]. H = 2, dk = 128, L <= 64 (else FS2_EUNSUPPORTED).
+ */
+int fs2_enc_attn_block(const void *x, const int64_t *lens, int B, int L, const void *wqkv, const float *bqkv,
+                       const void *wfc, const float *bfc, const float *gamma, const float *beta, float eps, int H,
+                       int dk, float temperature, void *out, fs2_stream_t stream);
+
+/*
  * fs2_attention_bwd — gradient of fs2_attention (training; autograd of transformer/Modules.py:14-25
  * and the head split/merge of SubLayers.py:36-52) without any T x T tensor: two flash-style
  * kernels (dQ per 64-query block with the softmax statistics rebuilt from Q and K; dK / dV per

@@ -1,0 +1,94 @@
+"""fs2_enc_attn_block — the encoder FFT block's attention sub-layer in one launch
+(transformer/SubLayers.py:29-57 + Modules.py:14-25 + Layers.py:25), bf16.
+
+* against the three launches it replaces (fs2_conv1d Q|K|V, fs2_attention, fs2_conv1d fc +
+  residual + LayerNorm with the row mask) on the same operands: Q|K|V and the attention output
+  round identically (same MFMA k order, attn_bf16_kernel's per-wave arithmetic), only the
+  LayerNorm statistics are summed in another order -> within 2 bf16 ulps;
+* against a float64 statement of the sub-layer on the same bf16 weights: bf16 tolerance;
+* padded rows (t >= len) exactly zero; lengths 0, 1, L; L = 64, 37, 1.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from fs2amd import ops, _lib as L
+
+    return ops, L
+
+
+def _weights(g, D=256):
+    wqkv = torch.randn(3 * D, D, device=DEV, generator=g) / D ** 0.5
+    bqkv = 0.1 * torch.randn(3 * D, device=DEV, generator=g)
+    wfc = torch.randn(D, D, device=DEV, generator=g) / D ** 0.5
+    bfc = 0.1 * torch.randn(D, device=DEV, generator=g)
+    gam = 1 + 0.1 * torch.randn(D, device=DEV, generator=g)
+    bet = 0.1 * torch.randn(D, device=DEV, generator=g)
+    return wqkv, bqkv, wfc, bfc, gam, bet
+
+
+def _ref64(x, lens, wqkv, bqkv, wfc, bfc, gam, bet, eps=1e-5, H=2, dk=128):
+    """float64 statement of the sub-layer on the bf16-rounded weights / input."""
+    xd = x.double()
+    B, L, D = x.shape
+    qkv = xd @ wqkv.to(torch.bfloat16).double().t() + bqkv.double()
+    q, k, v = qkv.split(D, -1)
+    heads = lambda t: t.view(B, L, H, dk).transpose(1, 2)
+    s = heads(q) @ heads(k).transpose(-1, -2) / dk ** 0.5
+    keymask = torch.arange(L, device=DEV)[None, :] >= lens[:, None]
+    s = s.masked_fill(keymask[:, None, None, :], float("-inf"))
+    a = torch.softmax(s, -1).nan_to_num(0.0)
+    o = (a @ heads(v)).transpose(1, 2).reshape(B, L, D)
+    y = o @ wfc.to(torch.bfloat16).double().t() + bfc.double() + xd
+    y = torch.nn.functional.layer_norm(y, (D,), gam.double(), bet.double(), eps)
+    return y.masked_fill(keymask[..., None], 0.0)
+
+
+@pytest.mark.parametrize("B,L,seed", [(64, 64, 1), (5, 37, 2), (3, 1, 3), (7, 64, 4)])
+def test_enc_attn_block_matches_three_launches_and_float64(gpu, B, L, seed):
+    ops, Lb = gpu
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    wqkv, bqkv, wfc, bfc, gam, bet = _weights(g)
+    x = torch.randn(B, L, 256, device=DEV, generator=g).to(torch.bfloat16)
+    lens = torch.randint(0, L + 1, (B,), generator=torch.Generator().manual_seed(seed)).to(DEV)
+    lens[0] = L
+    if B > 2:
+        lens[1], lens[2] = 0, 1
+    ln = (gam, bet, 1e-5)
+    got = ops.enc_attn_block(x, lens, ops.pack_frag_rows(wqkv), bqkv, ops.pack_frag_rows(wfc), bfc, ln, 2, 128,
+                             128 ** 0.5)
+    qkv = ops.conv1d(x, ops.pack_conv_weight(wqkv, Lb.FS2_BF16), bqkv, cin=256, ks=1, pad=0, compute=Lb.FS2_BF16,
+                     epilogue=Lb.EPI_BIAS, out_dtype=Lb.FS2_BF16)
+    att = ops.attention(qkv, lens, 2, 128, 128 ** 0.5)
+    three = ops.conv1d(att, ops.pack_conv_weight(wfc, Lb.FS2_BF16), bfc, cin=256, ks=1, pad=0, compute=Lb.FS2_BF16,
+                       epilogue=Lb.EPI_RES_LN, out_dtype=Lb.FS2_BF16, residual=x, ln=ln, lens=lens)
+    torch.cuda.synchronize()
+    pad = torch.arange(L, device=DEV)[None, :] >= lens[:, None]
+    assert bool((got[pad] == 0).all()), "padded rows must be zero"
+    d = (got.float() - three.float()).abs()
+    ulp = three.float().abs().clamp(min=2 ** -6) * 2 ** -7
+    assert bool((d <= 2 * ulp).all()), float((d - 2 * ulp).max())
+    ref = _ref64(x, lens, wqkv, bqkv, wfc, bfc, gam, bet)
+    err = (got.double() - ref).abs()
+    assert float(err.max()) <= 0.06 and float(err.mean()) <= 4e-3, (float(err.max()), float(err.mean()))
+
+
+def test_enc_attn_block_rejects(gpu):
+    ops, Lb = gpu
+    g = torch.Generator(device=DEV).manual_seed(9)
+    wqkv, bqkv, wfc, bfc, gam, bet = _weights(g)
+    x = torch.randn(2, 65, 256, device=DEV, generator=g).to(torch.bfloat16)
+    lens = torch.tensor([65, 3], device=DEV)
+    with pytest.raises(RuntimeError):  # L > 64: the three-launch path covers it
+        ops.enc_attn_block(x, lens, ops.pack_frag_rows(wqkv), bqkv, ops.pack_frag_rows(wfc), bfc, (gam, bet, 1e-5), 2,
+                           128, 128 ** 0.5)
+    with pytest.raises(AssertionError):
+        ops.enc_attn_block(x.float(), lens, ops.pack_frag_rows(wqkv), bqkv, ops.pack_frag_rows(wfc), bfc,
+                           (gam, bet, 1e-5), 2, 128, 128 ** 0.5)
