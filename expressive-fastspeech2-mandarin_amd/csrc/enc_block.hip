@@ -59,6 +59,16 @@ struct EncBlockArgs {
   const float *bfc, *gamma, *beta;
   float eps, scale_log2;
   bf16 *out;           // [B, L, 256]
+  // EMBED (the first encoder block): x = bf16(emb[tokens] + pe) built in LDS (fs2_embed_pe's
+  // arithmetic: out-of-vocabulary ids give NaN rows and count in *bad), and the forward's masks
+  // get_mask_from_lengths(lens, L) / (mel_lens, T_mel) written beside it (NULL: not wanted)
+  const int64_t *tokens;
+  const float *emb, *pe;
+  int vocab, T_mel;
+  int32_t *bad;
+  uint8_t *src_mask;
+  const int64_t *mel_lens;
+  uint8_t *mel_mask;
 };
 
 // LDS image (bytes)
@@ -74,6 +84,7 @@ constexpr int SMEM = VEC_OFF + (NQKV + 3 * D) * 4;
 static_assert(2 * LMAX * QP >= LMAX * XP, "o fits the Q region");
 static_assert(SMEM <= 163840, "LDS");
 
+template <bool EMBED>
 __global__ __launch_bounds__(NT, 1) void enc_attn_block_kernel(EncBlockArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -85,14 +96,16 @@ __global__ __launch_bounds__(NT, 1) void enc_attn_block_kernel(EncBlockArgs p) {
   const uint32_t xrow0 = (uint32_t)b * (uint32_t)L;
 
   // ---- x tile (rows >= L: zeros) and the four vectors by LDS-DMA; Q|K|V weight ring start
-  const rsrc_t xr = rsrc(p.x, (uint32_t)p.B * (uint32_t)L * D * 2u);
   static_assert(LMAX * XP % 1024 == 0, "whole 1 KiB pieces");
-  for (int pc = w; pc < LMAX * XP / 1024; pc += 8) {
-    const int o = pc * 1024 + lane * 16, r = o / XP, within = o - r * XP;
-    const bool ok = r < L && within < D * 2;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)(smem + X_OFF + pc * 1024), 16,
-                                             ok ? (xrow0 + r) * (uint32_t)(D * 2) + (uint32_t)within : 0x80000000u, 0,
-                                             0, 0);
+  if constexpr (!EMBED) {
+    const rsrc_t xr = rsrc(p.x, (uint32_t)p.B * (uint32_t)L * D * 2u);
+    for (int pc = w; pc < LMAX * XP / 1024; pc += 8) {
+      const int o = pc * 1024 + lane * 16, r = o / XP, within = o - r * XP;
+      const bool ok = r < L && within < D * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)(smem + X_OFF + pc * 1024),
+                                               16, ok ? (xrow0 + r) * (uint32_t)(D * 2) + (uint32_t)within : 0x80000000u,
+                                               0, 0, 0);
+    }
   }
   {  // 6 KiB of vectors = 6 pieces: bqkv (3), bfc, gamma, beta
     if (w < 6) {
@@ -123,6 +136,38 @@ __global__ __launch_bounds__(NT, 1) void enc_attn_block_kernel(EncBlockArgs p) {
   };
 #pragma unroll
   for (int ks = 0; ks < RING; ++ks) wload(ks, ring[ks]);
+  if constexpr (EMBED) {
+    // x rows (transformer/Models.py:82-91): row r, 8-channel chunk c per item, 4 items a thread
+    for (int i = tid; i < LMAX * (D / 8); i += NT) {
+      const int r = i >> 5, c = (i & 31) * 8;
+      bf16x8 o;
+      if (r < L) {
+        const int64_t tok = p.tokens[xrow0 + r];
+        if (tok < 0 || tok >= p.vocab) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] = (bf16)__builtin_nanf("");
+          if (p.bad != nullptr && c == 0) atomicAdd(p.bad, 1);
+        } else {
+          float v[8], e[8];
+          load8(p.emb + tok * D + c, v);
+          load8(p.pe + (int64_t)r * D + c, e);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] = (bf16)(v[q] + e[q]);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = (bf16)0.f;
+      }
+      *reinterpret_cast<bf16x8 *>(smem + X_OFF + r * XP + c * 2) = o;
+    }
+    // get_mask_from_lengths (utils/tools.py:152-160): True = padding
+    if (p.src_mask != nullptr)
+      for (int t = tid; t < L; t += NT) p.src_mask[(int64_t)b * L + t] = (int64_t)t >= len64 ? 1 : 0;
+    if (p.mel_mask != nullptr) {
+      const int64_t ml = p.mel_lens[b];
+      for (int t = tid; t < p.T_mel; t += NT) p.mel_mask[(int64_t)b * p.T_mel + t] = (int64_t)t >= ml ? 1 : 0;
+    }
+  }
   // x tile, vectors and k-step 0 landed (k-steps 1..3, the youngest 3 x NB1 loads, may stay in
   // flight: waiting for the whole ring made every CU pull ~230 KB before its first MFMA)
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 1) * NB1) : "memory");
@@ -368,18 +413,22 @@ __global__ __launch_bounds__(NT, 1) void enc_attn_block_kernel(EncBlockArgs p) {
 
 }  // namespace
 
-extern "C" int fs2_enc_attn_block(const void *x, const int64_t *lens, int B, int L, const void *wqkv, const float *bqkv,
-                                  const void *wfc, const float *bfc, const float *gamma, const float *beta, float eps,
-                                  int H, int dk, float temperature, void *out, fs2_stream_t stream) {
-  if (x == nullptr || lens == nullptr || wqkv == nullptr || bqkv == nullptr || wfc == nullptr || bfc == nullptr ||
-      gamma == nullptr || beta == nullptr || out == nullptr || !(temperature > 0.f))
+static int enc_block_launch(const void *x, const int64_t *tokens, const float *emb, int vocab, const float *pe,
+                            int32_t *bad_ids, const int64_t *lens, int B, int L, const void *wqkv, const float *bqkv,
+                            const void *wfc, const float *bfc, const float *gamma, const float *beta, float eps, int H,
+                            int dk, float temperature, void *out, uint8_t *src_mask, const int64_t *mel_lens, int T_mel,
+                            uint8_t *mel_mask, fs2_stream_t stream) {
+  const bool embed = tokens != nullptr;
+  if ((!embed && x == nullptr) || (embed && (emb == nullptr || pe == nullptr || vocab <= 0)) || lens == nullptr ||
+      wqkv == nullptr || bqkv == nullptr || wfc == nullptr || bfc == nullptr || gamma == nullptr || beta == nullptr ||
+      out == nullptr || !(temperature > 0.f))
     return FS2_EINVAL;
-  if (B < 0 || L < 0) return FS2_EINVAL;
+  if (B < 0 || L < 0 || (mel_mask != nullptr && (mel_lens == nullptr || T_mel < 0))) return FS2_EINVAL;
   if (H != 2 || dk != DK || L > LMAX) return FS2_EUNSUPPORTED;
   if (x == out) return FS2_EINVAL;
   if (B == 0 || L == 0) return FS2_OK;
   if ((int64_t)B * L * D * 2 >= (1LL << 31)) return FS2_EUNSUPPORTED;
-  EncBlockArgs a;
+  EncBlockArgs a{};
   a.x = reinterpret_cast<const bf16 *>(x);
   a.lens = lens;
   a.B = B;
@@ -393,7 +442,37 @@ extern "C" int fs2_enc_attn_block(const void *x, const int64_t *lens, int B, int
   a.eps = eps;
   a.scale_log2 = 1.4426950408889634f / temperature;
   a.out = reinterpret_cast<bf16 *>(out);
-  hipLaunchKernelGGL(enc_attn_block_kernel, dim3((unsigned)B), dim3(NT), 0, as_stream(stream), a);
+  a.tokens = tokens;
+  a.emb = emb;
+  a.pe = pe;
+  a.vocab = vocab;
+  a.bad = bad_ids;
+  a.src_mask = src_mask;
+  a.mel_lens = mel_lens;
+  a.T_mel = T_mel;
+  a.mel_mask = mel_mask;
+  if (embed)
+    hipLaunchKernelGGL(enc_attn_block_kernel<true>, dim3((unsigned)B), dim3(NT), 0, as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(enc_attn_block_kernel<false>, dim3((unsigned)B), dim3(NT), 0, as_stream(stream), a);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
+}
+
+extern "C" int fs2_enc_attn_block(const void *x, const int64_t *lens, int B, int L, const void *wqkv, const float *bqkv,
+                                  const void *wfc, const float *bfc, const float *gamma, const float *beta, float eps,
+                                  int H, int dk, float temperature, void *out, fs2_stream_t stream) {
+  return enc_block_launch(x, nullptr, nullptr, 0, nullptr, nullptr, lens, B, L, wqkv, bqkv, wfc, bfc, gamma, beta, eps, H,
+                          dk, temperature, out, nullptr, nullptr, 0, nullptr, stream);
+}
+
+extern "C" int fs2_enc_embed_attn_block(const int64_t *tokens, const float *emb, int vocab, const float *pe,
+                                        int32_t *bad_ids, const int64_t *lens, int B, int L, const void *wqkv,
+                                        const float *bqkv, const void *wfc, const float *bfc, const float *gamma,
+                                        const float *beta, float eps, int H, int dk, float temperature, void *out,
+                                        uint8_t *src_mask, const int64_t *mel_lens, int T_mel, uint8_t *mel_mask,
+                                        fs2_stream_t stream) {
+  if (tokens == nullptr) return FS2_EINVAL;
+  return enc_block_launch(nullptr, tokens, emb, vocab, pe, bad_ids, lens, B, L, wqkv, bqkv, wfc, bfc, gamma, beta, eps,
+                          H, dk, temperature, out, src_mask, mel_lens, T_mel, mel_mask, stream);
 }

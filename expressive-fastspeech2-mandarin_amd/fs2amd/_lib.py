@@ -178,6 +178,8 @@ SIGNATURES = {
     "fs2_vp_fused_weight_elems": (ctypes.c_int64, [_i]),
     "fs2_lr_fused": (_i, [_p, _i, _p, _i, _f, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "fs2_enc_attn_block": (_i, [_p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _f, _i, _i, _f, _p, _p]),
+    "fs2_enc_embed_attn_block": (_i, [_p, _p, _i, _p, _p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _f, _i, _i, _f, _p, _p, _p,
+                                      _i, _p, _p]),
     "fs2_lr_fused_proj": (_i, [_p, _i, _p, _i, _f, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p,
                                _p, _p, _i, _p, _p]),
     "fs2_hifigan_mrf": (_i, [_p, _p, _p, _p, _i, _i, _i, _f, _p, _p]),

@@ -672,10 +672,40 @@ def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None, lse=No
     return out
 
 
-def enc_attn_block(x, lens, wqkv_frag, bqkv, wfc_frag, bfc, ln, n_head, d_k, temperature, out=None):
+def enc_attn_block(x, lens, wqkv_frag, bqkv, wfc_frag, bfc, ln, n_head, d_k, temperature, out=None, embed=None,
+                   masks=None):
     """fs2_enc_attn_block: the encoder FFT block's attention sub-layer (Q|K|V projection, masked
     2-head attention, fc + residual + LayerNorm, padded rows zeroed) in one launch, bf16
-    [B, L <= 64, 256] -> bf16 [B, L, 256]. Weights in fragment order (:func:`pack_frag_rows`)."""
+    [B, L <= 64, 256] -> bf16 [B, L, 256]. Weights in fragment order (:func:`pack_frag_rows`).
+    embed = (tokens int64 [B, L], table f32 [vocab, 256], pe f32 [>= L, 256]) instead of x
+    (fs2_enc_embed_attn_block: the first block builds its input as fs2_embed_pe would); masks =
+    (src_mask bool [B, L], mel_lens | None, mel_mask bool [B, T_mel] | None) filled as
+    fs2_length_masks by that launch."""
+    if embed is not None:
+        tokens, table, pe = embed
+        _gpu(tokens, table, pe, lens, wqkv_frag, bqkv, wfc_frag, bfc)
+        B, Lx = tokens.shape
+        D = table.shape[1]
+        assert tokens.dtype == torch.int64 and tokens.is_contiguous() and table.dtype == torch.float32 \
+            and pe.dtype == torch.float32 and pe.shape[0] >= Lx and D == n_head * d_k
+        assert lens.dtype == torch.int64 and lens.numel() == B, (lens.dtype, lens.numel(), B)
+        g, b, eps = ln
+        if out is None:
+            out = torch.empty(B, Lx, D, device=tokens.device, dtype=torch.bfloat16)
+        src_mask = mel_lens = mel_mask = None
+        T_mel = 0
+        if masks is not None:
+            src_mask, mel_lens, mel_mask = masks
+            assert src_mask.dtype == torch.bool and tuple(src_mask.shape) == (B, Lx)
+            if mel_mask is not None:
+                assert mel_mask.dtype == torch.bool and mel_mask.shape[0] == B and mel_lens.dtype == torch.int64
+                T_mel = mel_mask.shape[1]
+        L.check(_lib.fs2_enc_embed_attn_block(
+            _ptr(tokens), _ptr(table), table.shape[0], _ptr(pe), _ptr(bad_id_counter(tokens.device)), _ptr(lens), B, Lx,
+            _ptr(wqkv_frag), _ptr(bqkv), _ptr(wfc_frag), _ptr(bfc), _ptr(g), _ptr(b), float(eps), n_head, d_k,
+            float(temperature), _ptr(out), _ptr(src_mask), _ptr(mel_lens), T_mel, _ptr(mel_mask), _stream(tokens)),
+            "fs2_enc_embed_attn_block")
+        return out
     _gpu(x, lens, wqkv_frag, bqkv, wfc_frag, bfc)
     B, Lx, D = x.shape
     assert x.dtype == torch.bfloat16 and x.is_contiguous() and D == n_head * d_k, (x.dtype, tuple(x.shape))

@@ -279,6 +279,18 @@ def enc_block_ok(P, lp, x):
             and lp.fp8 is None)  # fp8 layers: their FFN reads the fp8 copy of h the fc epilogue writes
 
 
+def embed_block_ok(P, Lx):
+    """The first encoder block's launch also builds the encoder input (embedding + PE) and writes
+    the forward's masks (fs2_enc_embed_attn_block). FS2_ENC_EMBED=0: fs2_embed_pe and the two
+    fs2_length_masks launches (A/B)."""
+    if os.environ.get("FS2_ENC_EMBED", "1") == "0" or not P.enc_layers or P.act_dtype != L.FS2_BF16:
+        return False
+    lp = P.enc_layers[0]
+    return (enc_block_on() and P.compute == L.FS2_BF16 and 0 < Lx <= 64 and P.enc_emb.shape[1] == 256
+            and lp.n_head == 2 and lp.d_k == 128 and CALIB is None and getattr(lp, "wqf", None) is not None
+            and getattr(lp, "wfcf", None) is not None and lp.fp8 is None)
+
+
 def qkv_epilogue_ok(x, layout, lp):
     """The Q|K|V epilogue only for unsplit FFN launches (the decoder's). In the split-hidden form
     (the encoder's 64-row tiles x 4 splits) only the last-arriving split of a tile runs the
@@ -461,7 +473,9 @@ def _stage1(P, va, g, p_control, d_control, defer_lr=False):
     """Encoder (+ conditioning), variance predictors, duration scan for one utterance group.
     defer_lr (teacher-forced durations, decoder length known): the duration scan is left to the
     one-launch LengthRegulator of stage 2 (fs2_lr_fused)."""
-    x = ops.embed_pe(g.texts, P.enc_emb, _pe(P, "enc", g.Lx), P.act_dtype)
+    fold = getattr(g, "mask_out", None) is not None
+    if not fold:
+        x = ops.embed_pe(g.texts, P.enc_emb, _pe(P, "enc", g.Lx), P.act_dtype)
     spk_vec = emo_vec = None
     if P.spk_table is not None or P.emo_table is not None:
         spk_vec, emo_vec = ops.cond_vectors(
@@ -470,7 +484,21 @@ def _stage1(P, va, g, p_control, d_control, defer_lr=False):
             getattr(P, "aro_table", None), getattr(P, "val_table", None), getattr(P, "emo_w", None),
             getattr(P, "emo_b", None), P.d_model)
     n_enc = len(P.enc_layers)
-    x = _stack(P, P.enc_layers, x, g.lens_src, addvecs=(spk_vec, emo_vec))
+    if fold:
+        # block 0's attention sub-layer with the embedding + PE and the masks in the same launch
+        _STACK[0] = "enc"
+        lp = P.enc_layers[0]
+        with _tm("qkv+attn+fc"):
+            h = ops.enc_attn_block(None, g.lens_src, lp.wqf, lp.bqkv, lp.wfcf, lp.bfc, lp.ln1, lp.n_head, lp.d_k,
+                                   float(np.power(lp.d_k, 0.5)), embed=(g.texts, P.enc_emb, _pe(P, "enc", g.Lx)),
+                                   masks=g.mask_out)
+        last = n_enc == 1
+        x, _, _ = _ffn_tail(P, lp, h, h, g.lens_src, spk_vec if last else None, emo_vec if last else None, False, None,
+                            None, None, P.enc_layers[1] if n_enc > 1 else None)
+        if n_enc > 1:
+            x = _stack(P, P.enc_layers[1:], x, g.lens_src, addvecs=(spk_vec, emo_vec))
+    else:
+        x = _stack(P, P.enc_layers, x, g.lens_src, addvecs=(spk_vec, emo_vec))
     if n_enc == 0 and (spk_vec is not None or emo_vec is not None):
         raise NotImplementedError("encoder_layer = 0")
 
@@ -641,19 +669,26 @@ def run_forward(model, speakers, emotions, arousals, valences, texts, src_lens, 
     if texts.shape[1] != Lx:
         raise RuntimeError(f"texts has {texts.shape[1]} positions but max_src_len is {Lx}")
     src_lens = src_lens.to(dev)
-    src_masks = _mask(src_lens, Lx)
-    mel_masks = _mask(mel_lens, max_mel_len if max_mel_len is not None else int(mel_lens.max().item())) \
-        if mel_lens is not None else None
+    n = _streams_for(B)
+    mel_w = None if mel_lens is None else (max_mel_len if max_mel_len is not None else int(mel_lens.max().item()))
+    mask_out = None
+    if n == 1 and embed_block_ok(P, Lx):
+        # the first encoder block's launch builds its input and writes both masks (fs2_enc_embed_attn_block)
+        src_masks = torch.empty(B, Lx, device=dev, dtype=torch.bool)
+        mel_masks = None if mel_lens is None else torch.empty(B, int(mel_w), device=dev, dtype=torch.bool)
+        mask_out = (src_masks, None if mel_lens is None else mel_lens.to(dev).to(torch.int64).contiguous(), mel_masks)
+    else:
+        src_masks = _mask(src_lens, Lx)
+        mel_masks = _mask(mel_lens, mel_w) if mel_lens is not None else None
     full = SimpleNamespace(
         speakers=ids(speakers), emotions=ids(emotions), arousals=ids(arousals), valences=ids(valences),
         texts=ids(texts), lens_src=src_lens.to(torch.int64).contiguous(), Lx=Lx,
         p_targets=f32(p_targets), e_targets=f32(e_targets),
         d_targets=None if d_targets is None else d_targets.to(dev),
-        mel_lens=None if mel_lens is None else mel_lens.to(dev).to(torch.int64).contiguous())
+        mel_lens=None if mel_lens is None else mel_lens.to(dev).to(torch.int64).contiguous(), mask_out=mask_out)
 
     # utterance groups (contiguous ranges of b; same padded L / T as the whole batch, so every
     # group's outputs are bit-identical to the one-group run)
-    n = _streams_for(B)
     bounds = [(B * i // n, B * (i + 1) // n) for i in range(n)]
 
     def part(b0, b1):

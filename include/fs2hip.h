@@ -357,6 +357,19 @@ int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int6
 int fs2_enc_attn_block(const void *x, const int64_t *lens, int B, int L, const void *wqkv, const float *bqkv,
                        const void *wfc, const float *bfc, const float *gamma, const float *beta, float eps, int H,
                        int dk, float temperature, void *out, fs2_stream_t stream);
+/*
+ * fs2_enc_embed_attn_block — the FIRST encoder block's attention sub-layer with the encoder input
+ * built in the same launch (replaces fs2_embed_pe + fs2_length_masks x 2 + fs2_enc_attn_block):
+ * x[b, t] = bf16(emb[tokens[b, t]] + pe[t]) exactly as fs2_embed_pe (an id outside [0, vocab):
+ * NaN row, *bad_ids += 1), never written to HBM; src_mask[b, t] = t >= lens[b] (bool [B, L]) and,
+ * when mel_mask != NULL, mel_mask[b, t] = t >= mel_lens[b] (bool [B, T_mel]) as fs2_length_masks.
+ * Other arguments and limits as fs2_enc_attn_block.
+ */
+int fs2_enc_embed_attn_block(const int64_t *tokens, const float *emb, int vocab, const float *pe, int32_t *bad_ids,
+                             const int64_t *lens, int B, int L, const void *wqkv, const float *bqkv, const void *wfc,
+                             const float *bfc, const float *gamma, const float *beta, float eps, int H, int dk,
+                             float temperature, void *out, uint8_t *src_mask, const int64_t *mel_lens, int T_mel,
+                             uint8_t *mel_mask, fs2_stream_t stream);
 
 /*
  * fs2_attention_bwd — gradient of fs2_attention (training; autograd of transformer/Modules.py:14-25

@@ -92,3 +92,41 @@ def test_enc_attn_block_rejects(gpu):
     with pytest.raises(AssertionError):
         ops.enc_attn_block(x.float(), lens, ops.pack_frag_rows(wqkv), bqkv, ops.pack_frag_rows(wfc), bfc,
                            (gam, bet, 1e-5), 2, 128, 128 ** 0.5)
+
+
+@pytest.mark.parametrize("B,L,seed", [(64, 64, 5), (5, 37, 6), (3, 1, 7)])
+def test_enc_embed_attn_block_equals_embed_then_block(gpu, B, L, seed):
+    """fs2_enc_embed_attn_block (the first encoder block builds x = bf16(emb[tok] + pe) itself and
+    writes both masks) equals fs2_embed_pe + fs2_enc_attn_block BIT-EXACTLY, the masks equal
+    fs2_length_masks, and an out-of-vocabulary id gives a NaN input row and counts once."""
+    ops, Lb = gpu
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    wqkv, bqkv, wfc, bfc, gam, bet = _weights(g)
+    vocab = 50
+    table = torch.randn(vocab, 256, device=DEV, generator=g)
+    pe = torch.randn(L + 3, 256, device=DEV, generator=g)
+    tok = torch.randint(0, vocab, (B, L), device=DEV, generator=g)
+    lens = torch.randint(0, L + 1, (B,), generator=torch.Generator().manual_seed(seed)).to(DEV)
+    lens[0] = L
+    mel_lens = torch.randint(-2, 90, (B,), generator=torch.Generator().manual_seed(seed + 1)).to(DEV)
+    ln = (gam, bet, 1e-5)
+    wq, wf = ops.pack_frag_rows(wqkv), ops.pack_frag_rows(wfc)
+    x = ops.embed_pe(tok, table, pe, Lb.FS2_BF16)
+    two = ops.enc_attn_block(x, lens, wq, bqkv, wf, bfc, ln, 2, 128, 128 ** 0.5)
+    sm = torch.empty(B, L, device=DEV, dtype=torch.bool)
+    mm = torch.empty(B, 77, device=DEV, dtype=torch.bool)
+    one = ops.enc_attn_block(None, lens, wq, bqkv, wf, bfc, ln, 2, 128, 128 ** 0.5, embed=(tok, table, pe),
+                             masks=(sm, mel_lens, mm))
+    torch.cuda.synchronize()
+    assert torch.equal(one, two), float((one.float() - two.float()).abs().max())
+    assert torch.equal(sm, ops.length_mask(lens, L)) and torch.equal(mm, ops.length_mask(mel_lens, 77))
+    if B > 1 and L > 1:
+        bad = ops.bad_id_counter(torch.device(DEV))
+        before = int(bad.item())
+        tok[1, 0] = vocab + 3
+        lens[1] = L
+        out = ops.enc_attn_block(None, lens, wq, bqkv, wf, bfc, ln, 2, 128, 128 ** 0.5, embed=(tok, table, pe))
+        torch.cuda.synchronize()
+        assert int(bad.item()) == before + 1
+        assert bool(torch.isnan(out[1].float()).any()) and not bool(torch.isnan(out[0].float()).any())
+        bad.zero_()

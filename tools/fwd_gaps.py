@@ -2,7 +2,8 @@
 """Graph-replayed forwards from a rocprofv3 kernel trace of bench.py: kernels in order, duration,
 gap to the previous kernel's end (us), averaged over the timed graph replays.
 
-A forward starts at its two length-mask launches. The bench's trace also holds eager forwards
+A forward starts at its two length-mask launches (or, with the masks written by the first encoder
+block, at the conditioning launch / that block). The bench's trace also holds eager forwards
 (warm-up, and the roofline's HIP-event-timed forwards, whose host-bound launches leave gaps); the
 graph replays are the forwards with (almost) no internal gaps, so those are the ones averaged.
 
@@ -21,6 +22,11 @@ def forwards(rows, start=None):
     else:
         st = [i for i, r in enumerate(rows) if "length_mask" in r["Kernel_Name"] and i + 1 < len(rows)
               and "length_mask" in rows[i + 1]["Kernel_Name"]]
+        # round 5: the first encoder block writes the masks (fs2_enc_embed_attn_block); a forward
+        # then starts at the conditioning launch, or at that block when there is none
+        for marker in ("cond_kernel", "enc_attn_block_kernelILb1"):
+            if len(st) < 2:
+                st = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
     return [rows[a:b] for a, b in zip(st, st[1:])]
 
 
