@@ -2,6 +2,7 @@
 // per-utterance speaker/emotion conditioning vectors, and the pitch/energy bucketize +
 // embedding add of the VarianceAdaptor.
 #include "fs2_common.h"
+#include "cond.h"
 
 namespace {
 
@@ -34,85 +35,9 @@ __global__ __launch_bounds__(256) void embed_pe_kernel(const int64_t *__restrict
   store8(out + row * D + col, v);
 }
 
-__device__ __forceinline__ int64_t clampi(int64_t v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); }
-
-// The per-utterance conditioning vectors                           (model/fastspeech2.py:101-110)
-// Workgroup (channel block of 64, utterance block of kCondU): the speaker rows are copied; the
-// emotion Linear splits each channel's dot product over the 4 waves (a quarter of k each, 16-byte
-// weight loads), every weight read serving kCondU utterances, then sums the 4 partials in LDS.
-// (One workgroup per utterance re-read the whole 256 KB weight 64 times: 13.5 us at cfg2.)
-constexpr int kCondU = 8;
-
-__global__ __launch_bounds__(256) void cond_kernel(const int64_t *speakers, const float *spk_table, int n_spk,
-                                                   const int64_t *emotions, const float *emo_table, int n_emo,
-                                                   int d_emo, const int64_t *arousals, const float *aro_table,
-                                                   int n_aro, int d_aro, const int64_t *valences,
-                                                   const float *val_table, int n_val, int d_val,
-                                                   const float *lin_w, const float *lin_b, int B, int D,
-                                                   float *spk_out, float *emo_out) {
+__global__ __launch_bounds__(256) void cond_kernel(CondArgs a) {
   extern __shared__ float sm[];
-  const int tid = threadIdx.x;
-  const int n0 = blockIdx.x * 64, b0 = blockIdx.y * kCondU;
-  if (spk_table != nullptr) {
-    for (int i = tid; i < kCondU * 64; i += 256) {
-      const int b = b0 + (i >> 6), n = n0 + (i & 63);
-      if (b < B && n < D) spk_out[(int64_t)b * D + n] = spk_table[clampi(speakers[b], n_spk) * D + n];
-    }
-  }
-  if (emo_table == nullptr) return;
-  const int dc = d_emo + d_aro + d_val;
-  float *cat = sm;                   // [kCondU][dc]
-  float *red = sm + kCondU * dc;     // [kCondU][4][64]
-  for (int i = tid; i < kCondU * dc; i += 256) {
-    const int u = i / dc, k = i - u * dc, b = b0 + u;
-    float x = 0.f;
-    if (b < B) {
-      if (k < d_emo)
-        x = emo_table[clampi(emotions[b], n_emo) * d_emo + k];
-      else if (k < d_emo + d_aro)
-        x = aro_table[clampi(arousals[b], n_aro) * d_aro + (k - d_emo)];
-      else
-        x = val_table[clampi(valences[b], n_val) * d_val + (k - d_emo - d_aro)];
-    }
-    cat[i] = x;
-  }
-  __syncthreads();
-  const int nl = tid & 63, kq = tid >> 6, n = n0 + nl;
-  float acc[kCondU];
-#pragma unroll
-  for (int u = 0; u < kCondU; ++u) acc[u] = 0.f;
-  if (n < D) {
-    const float *wr = lin_w + (int64_t)n * dc;
-    if ((dc & 15) == 0) {
-      const int kper = dc >> 2, k0 = kq * kper;
-#pragma unroll 16
-      for (int k = k0; k < k0 + kper; k += 4) {
-        const float4 wv = *reinterpret_cast<const float4 *>(wr + k);
-#pragma unroll
-        for (int u = 0; u < kCondU; ++u) {
-          const float4 c = *reinterpret_cast<const float4 *>(cat + u * dc + k);
-          acc[u] = fmaf(wv.x, c.x, fmaf(wv.y, c.y, fmaf(wv.z, c.z, fmaf(wv.w, c.w, acc[u]))));
-        }
-      }
-    } else {
-      const int kper = (dc + 3) >> 2, k0 = kq * kper, k1 = min(dc, k0 + kper);
-      for (int k = k0; k < k1; ++k) {
-        const float wv = wr[k];
-#pragma unroll
-        for (int u = 0; u < kCondU; ++u) acc[u] = fmaf(wv, cat[u * dc + k], acc[u]);
-      }
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kCondU; ++u) red[(u * 4 + kq) * 64 + nl] = acc[u];
-  __syncthreads();
-  for (int i = tid; i < kCondU * 64; i += 256) {
-    const int u = i >> 6, c = i & 63, b = b0 + u, nn = n0 + c;
-    if (b < B && nn < D) {
-      const float *r = red + u * 256 + c;
-      emo_out[(int64_t)b * D + nn] = fmaxf(((r[0] + r[64]) + (r[128] + r[192])) + lin_b[nn], 0.f);
-    }
-  }
+  cond_tile(a, blockIdx.x, blockIdx.y, threadIdx.x, sm);
 }
 
 // 32 lanes per row (inside one wave, so the read of pred[m] by every lane precedes lane 0's
@@ -238,9 +163,10 @@ extern "C" int fs2_cond_vectors(const int64_t *speakers, const float *speaker_ta
   const int dc = emo_table != nullptr ? d_emo + d_aro + d_val : 0;
   const size_t smem = (size_t)kCondU * (dc + 256) * sizeof(float);
   if (smem > 65536) return FS2_EUNSUPPORTED;
+  CondArgs a{speakers, speaker_table, n_speaker, emotions, emo_table, n_emo, d_emo, arousals, aro_table, n_aro, d_aro,
+             valences, val_table, n_val, d_val, lin_w, lin_b, B, D, spk_out, emo_out};
   hipLaunchKernelGGL(cond_kernel, dim3((unsigned)((D + 63) / 64), (unsigned)((B + kCondU - 1) / kCondU)), dim3(256), smem,
-                     as_stream(stream), speakers, speaker_table, n_speaker, emotions, emo_table, n_emo, d_emo, arousals,
-                     aro_table, n_aro, d_aro, valences, val_table, n_val, d_val, lin_w, lin_b, B, D, spk_out, emo_out);
+                     as_stream(stream), a);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

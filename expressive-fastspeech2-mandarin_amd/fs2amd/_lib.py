@@ -112,6 +112,17 @@ class WconvDesc(ctypes.Structure):
     ]
 
 
+class CondDesc(ctypes.Structure):
+    """Mirror of ``fs2_cond_desc`` (include/fs2hip.h)."""
+
+    _fields_ = [
+        ("speakers", _p), ("speaker_table", _p), ("n_speaker", _i), ("emotions", _p), ("emo_table", _p),
+        ("n_emo", _i), ("d_emo", _i), ("arousals", _p), ("aro_table", _p), ("n_aro", _i), ("d_aro", _i),
+        ("valences", _p), ("val_table", _p), ("n_val", _i), ("d_val", _i), ("lin_w", _p), ("lin_b", _p),
+        ("spk_out", _p), ("emo_out", _p),
+    ]
+
+
 class FfnDesc(ctypes.Structure):
     """Mirror of ``fs2_ffn_desc`` (include/fs2hip.h)."""
 
@@ -177,9 +188,9 @@ SIGNATURES = {
     "fs2_vp_fused": (_i, [ctypes.POINTER(VpFusedDesc), _p]),
     "fs2_vp_fused_weight_elems": (ctypes.c_int64, [_i]),
     "fs2_lr_fused": (_i, [_p, _i, _p, _i, _f, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
-    "fs2_enc_attn_block": (_i, [_p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _f, _i, _i, _f, _p, _p]),
+    "fs2_enc_attn_block": (_i, [_p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _f, _i, _i, _f, _p, _p, _i64, _p]),
     "fs2_enc_embed_attn_block": (_i, [_p, _p, _i, _p, _p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _f, _i, _i, _f, _p, _p, _p,
-                                      _i, _p, _p]),
+                                      _i, _p, _p, _p, _i64, _p]),
     "fs2_lr_fused_proj": (_i, [_p, _i, _p, _i, _f, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p,
                                _p, _p, _i, _p, _p]),
     "fs2_hifigan_mrf": (_i, [_p, _p, _p, _p, _i, _i, _i, _f, _p, _p]),

@@ -673,14 +673,16 @@ def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None, lse=No
 
 
 def enc_attn_block(x, lens, wqkv_frag, bqkv, wfc_frag, bfc, ln, n_head, d_k, temperature, out=None, embed=None,
-                   masks=None):
+                   masks=None, cond=None):
     """fs2_enc_attn_block: the encoder FFT block's attention sub-layer (Q|K|V projection, masked
     2-head attention, fc + residual + LayerNorm, padded rows zeroed) in one launch, bf16
     [B, L <= 64, 256] -> bf16 [B, L, 256]. Weights in fragment order (:func:`pack_frag_rows`).
     embed = (tokens int64 [B, L], table f32 [vocab, 256], pe f32 [>= L, 256]) instead of x
     (fs2_enc_embed_attn_block: the first block builds its input as fs2_embed_pe would); masks =
     (src_mask bool [B, L], mel_lens | None, mel_mask bool [B, T_mel] | None) filled as
-    fs2_length_masks by that launch."""
+    fs2_length_masks by that launch. cond (with embed) = the arguments of :func:`cond_vectors`
+    (speakers, spk_table, emotions, arousals, valences, emo_table, aro_table, val_table, lin_w,
+    lin_b): extra workgroups of the same launch compute them; returns (out, spk_vec, emo_vec)."""
     if embed is not None:
         tokens, table, pe = embed
         _gpu(tokens, table, pe, lens, wqkv_frag, bqkv, wfc_frag, bfc)
@@ -700,12 +702,32 @@ def enc_attn_block(x, lens, wqkv_frag, bqkv, wfc_frag, bfc, ln, n_head, d_k, tem
             if mel_mask is not None:
                 assert mel_mask.dtype == torch.bool and mel_mask.shape[0] == B and mel_lens.dtype == torch.int64
                 T_mel = mel_mask.shape[1]
+        cd = None
+        spk_out = emo_out = None
+        if cond is not None:
+            speakers, spk_table, emotions, arousals, valences, emo_table, aro_table, val_table, lin_w, lin_b = cond
+            _gpu(speakers, spk_table, emotions, arousals, valences, emo_table, aro_table, val_table, lin_w, lin_b)
+            cd = L.CondDesc()
+            if spk_table is not None:
+                spk_out = torch.empty(B, D, device=tokens.device)
+                cd.speakers, cd.speaker_table, cd.n_speaker = _ptr(speakers), _ptr(spk_table), spk_table.shape[0]
+                cd.spk_out = _ptr(spk_out)
+            if emo_table is not None:
+                emo_out = torch.empty(B, D, device=tokens.device)
+                cd.emotions, cd.emo_table, cd.n_emo, cd.d_emo = _ptr(emotions), _ptr(emo_table), emo_table.shape[0], \
+                    emo_table.shape[1]
+                cd.arousals, cd.aro_table, cd.n_aro, cd.d_aro = _ptr(arousals), _ptr(aro_table), aro_table.shape[0], \
+                    aro_table.shape[1]
+                cd.valences, cd.val_table, cd.n_val, cd.d_val = _ptr(valences), _ptr(val_table), val_table.shape[0], \
+                    val_table.shape[1]
+                cd.lin_w, cd.lin_b, cd.emo_out = _ptr(lin_w), _ptr(lin_b), _ptr(emo_out)
         L.check(_lib.fs2_enc_embed_attn_block(
             _ptr(tokens), _ptr(table), table.shape[0], _ptr(pe), _ptr(bad_id_counter(tokens.device)), _ptr(lens), B, Lx,
             _ptr(wqkv_frag), _ptr(bqkv), _ptr(wfc_frag), _ptr(bfc), _ptr(g), _ptr(b), float(eps), n_head, d_k,
-            float(temperature), _ptr(out), _ptr(src_mask), _ptr(mel_lens), T_mel, _ptr(mel_mask), _stream(tokens)),
+            float(temperature), _ptr(out), _ptr(src_mask), _ptr(mel_lens), T_mel, _ptr(mel_mask),
+            ctypes.byref(cd) if cd is not None else None, *_enc_ws(tokens.device), _stream(tokens)),
             "fs2_enc_embed_attn_block")
-        return out
+        return (out, spk_out, emo_out) if cond is not None else out
     _gpu(x, lens, wqkv_frag, bqkv, wfc_frag, bfc)
     B, Lx, D = x.shape
     assert x.dtype == torch.bfloat16 and x.is_contiguous() and D == n_head * d_k, (x.dtype, tuple(x.shape))
@@ -717,8 +739,19 @@ def enc_attn_block(x, lens, wqkv_frag, bqkv, wfc_frag, bfc, ln, n_head, d_k, tem
         out = torch.empty_like(x)
     L.check(_lib.fs2_enc_attn_block(_ptr(x), _ptr(lens), B, Lx, _ptr(wqkv_frag), _ptr(bqkv), _ptr(wfc_frag),
                                     _ptr(bfc), _ptr(g), _ptr(b), float(eps), n_head, d_k, float(temperature),
-                                    _ptr(out), _stream(x)), "fs2_enc_attn_block")
+                                    _ptr(out), *_enc_ws(x.device), _stream(x)), "fs2_enc_attn_block")
     return out
+
+
+def _enc_ws(device):
+    """(pointer, bytes) of the split-K workspace for fs2_enc_attn_block's head-split form
+    (FS2_ENC_HALF=1, A/B: measured no faster than one workgroup per utterance, profiles/r5y), or
+    (None, 0): one workgroup per utterance (the default). FS2_ENC_TRACE=1 (trace builds): the
+    workspace carries the phase stamps."""
+    if os.environ.get("FS2_ENC_HALF", "0") != "1" and os.environ.get("FS2_ENC_TRACE", "0") != "1":
+        return None, 0
+    ws = splitk_workspace(device)
+    return (None, 0) if ws is None else (ws.data_ptr(), ws.numel())
 
 
 _bad_ids = {}

@@ -477,7 +477,8 @@ def _stage1(P, va, g, p_control, d_control, defer_lr=False):
     if not fold:
         x = ops.embed_pe(g.texts, P.enc_emb, _pe(P, "enc", g.Lx), P.act_dtype)
     spk_vec = emo_vec = None
-    if P.spk_table is not None or P.emo_table is not None:
+    has_cond = P.spk_table is not None or P.emo_table is not None
+    if has_cond and not fold:
         spk_vec, emo_vec = ops.cond_vectors(
             g.speakers if P.spk_table is not None else None, P.spk_table,
             g.emotions if P.emo_table is not None else None, g.arousals, g.valences, P.emo_table,
@@ -488,10 +489,17 @@ def _stage1(P, va, g, p_control, d_control, defer_lr=False):
         # block 0's attention sub-layer with the embedding + PE and the masks in the same launch
         _STACK[0] = "enc"
         lp = P.enc_layers[0]
+        cond = None
+        if has_cond:  # the conditioning vectors on extra workgroups of the same launch
+            cond = (g.speakers if P.spk_table is not None else None, P.spk_table,
+                    g.emotions if P.emo_table is not None else None, g.arousals, g.valences, P.emo_table,
+                    getattr(P, "aro_table", None), getattr(P, "val_table", None), getattr(P, "emo_w", None),
+                    getattr(P, "emo_b", None))
         with _tm("qkv+attn+fc"):
-            h = ops.enc_attn_block(None, g.lens_src, lp.wqf, lp.bqkv, lp.wfcf, lp.bfc, lp.ln1, lp.n_head, lp.d_k,
+            r = ops.enc_attn_block(None, g.lens_src, lp.wqf, lp.bqkv, lp.wfcf, lp.bfc, lp.ln1, lp.n_head, lp.d_k,
                                    float(np.power(lp.d_k, 0.5)), embed=(g.texts, P.enc_emb, _pe(P, "enc", g.Lx)),
-                                   masks=g.mask_out)
+                                   masks=g.mask_out, cond=cond)
+        h, spk_vec, emo_vec = r if cond is not None else (r, None, None)
         last = n_enc == 1
         x, _, _ = _ffn_tail(P, lp, h, h, g.lens_src, spk_vec if last else None, emo_vec if last else None, False, None,
                             None, None, P.enc_layers[1] if n_enc > 1 else None)

@@ -353,11 +353,16 @@ class FFTBlockFn(torch.autograd.Function):
         ctx.packT = (pk["qkvT"], pk["fcT"], pk["w1T"], pk["w2T"])
         ctx.meta = (H, dk, temp, k1, k2, p_drop, salt, seed)
         ctx.mark_non_differentiable(yb)
+        # the bf16 copy never gets a gradient: without this autograd zero-fills one of its size
+        # per block per step (a FillFunc launch each)
+        ctx.set_materialize_grads(False)
         return y, yb
 
     @staticmethod
     def backward(ctx, dy, _dyb):
         xb, qkv, att, hb, u, xh1, rs1, xh2, rs2, lens, lse, *params = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros(xb.shape, device=xb.device, dtype=torch.float32)
         (wq, bq, wk, bk, wv, bv, wfc, bfc, g1, be1, w1, b1, w2, b2, g2, be2) = params
         H, dk, temp, k1, k2, p_drop, salt, seed = ctx.meta
         wqkvT, wfcT, w1T, w2T = ctx.packT
@@ -560,11 +565,14 @@ class VPLayerFn(torch.autograd.Function):
         ctx.meta = meta
         ctx.wT = wT
         ctx.mark_non_differentiable(yb)
+        ctx.set_materialize_grads(False)  # (as FFTBlockFn: no zero-filled gradient for yb)
         return y, yb
 
     @staticmethod
     def backward(ctx, dy, _dyb):
         xb, a, xh, rs, w, b, g, be = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros(xh.shape, device=xh.device, dtype=torch.float32)
         pad, p_drop, seed, salt, eps = ctx.meta[:5]
         N, Cin, KS = w.shape
         sink = _SINK[0] and all(t.grad is not None for t in (w, b, g, be))

@@ -353,10 +353,13 @@ int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int6
  * x / out: bf16 [B, L, 256] (out != x); lens int64 [B]; wqkv / wfc: the [768, 256] / [256, 256]
  * weights in MFMA fragment order ([N/64][K/32][4][4][16][8] bf16, fs2amd.ops.pack_frag_rows);
  * bqkv f32 [768], bfc / gamma / beta f32 [256]. H = 2, dk = 128, L <= 64 (else FS2_EUNSUPPORTED).
+ * ws (optional, the fs2_conv_desc split-K workspace: 4 KiB of zeroed int32 counters, then
+ * >= B * 128 KiB): two workgroups per utterance, one per head, meeting through a write-through
+ * hand-off of their f32 fc halves (the counters are left zero); NULL: one workgroup per utterance.
  */
 int fs2_enc_attn_block(const void *x, const int64_t *lens, int B, int L, const void *wqkv, const float *bqkv,
                        const void *wfc, const float *bfc, const float *gamma, const float *beta, float eps, int H,
-                       int dk, float temperature, void *out, fs2_stream_t stream);
+                       int dk, float temperature, void *out, void *ws, int64_t ws_bytes, fs2_stream_t stream);
 /*
  * fs2_enc_embed_attn_block — the FIRST encoder block's attention sub-layer with the encoder input
  * built in the same launch (replaces fs2_embed_pe + fs2_length_masks x 2 + fs2_enc_attn_block):
@@ -365,11 +368,31 @@ int fs2_enc_attn_block(const void *x, const int64_t *lens, int B, int L, const v
  * when mel_mask != NULL, mel_mask[b, t] = t >= mel_lens[b] (bool [B, T_mel]) as fs2_length_masks.
  * Other arguments and limits as fs2_enc_attn_block.
  */
+typedef struct fs2_cond_desc {  /* the arguments of fs2_cond_vectors (below), B and D implied */
+  const int64_t *speakers;
+  const float *speaker_table;
+  int n_speaker;
+  const int64_t *emotions;
+  const float *emo_table;
+  int n_emo, d_emo;
+  const int64_t *arousals;
+  const float *aro_table;
+  int n_aro, d_aro;
+  const int64_t *valences;
+  const float *val_table;
+  int n_val, d_val;
+  const float *lin_w, *lin_b;
+  float *spk_out, *emo_out;
+} fs2_cond_desc;
+
+/* cond != NULL: fs2_cond_vectors' outputs computed by extra workgroups of the same launch (they run
+   on the CUs the B utterance workgroups leave idle); d_emo + d_aro + d_val <= 4096 */
 int fs2_enc_embed_attn_block(const int64_t *tokens, const float *emb, int vocab, const float *pe, int32_t *bad_ids,
                              const int64_t *lens, int B, int L, const void *wqkv, const float *bqkv, const void *wfc,
                              const float *bfc, const float *gamma, const float *beta, float eps, int H, int dk,
                              float temperature, void *out, uint8_t *src_mask, const int64_t *mel_lens, int T_mel,
-                             uint8_t *mel_mask, fs2_stream_t stream);
+                             uint8_t *mel_mask, const fs2_cond_desc *cond, void *ws, int64_t ws_bytes,
+                             fs2_stream_t stream);
 
 /*
  * fs2_attention_bwd — gradient of fs2_attention (training; autograd of transformer/Modules.py:14-25

@@ -130,3 +130,59 @@ def test_enc_embed_attn_block_equals_embed_then_block(gpu, B, L, seed):
         assert int(bad.item()) == before + 1
         assert bool(torch.isnan(out[1].float()).any()) and not bool(torch.isnan(out[0].float()).any())
         bad.zero_()
+
+
+@pytest.mark.parametrize("B,L,seed", [(64, 64, 11), (13, 37, 12), (3, 1, 13)])
+def test_enc_attn_block_head_split_equals_one_workgroup(gpu, B, L, seed, monkeypatch):
+    """The head-split form (two workgroups per utterance, f32 fc halves summed head 0 + head 1 by
+    the last arriver through the split-K workspace) against the one-workgroup form: the same
+    Q|K|V, attention and o; the fc sum regrouped (k 0..127 + k 128..255 instead of one chain) ->
+    within 2 bf16 ulps; run twice (the arrival counters must be left zero); B not a multiple of 8."""
+    ops, Lb = gpu
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    wqkv, bqkv, wfc, bfc, gam, bet = _weights(g)
+    x = torch.randn(B, L, 256, device=DEV, generator=g).to(torch.bfloat16)
+    lens = torch.randint(0, L + 1, (B,), generator=torch.Generator().manual_seed(seed)).to(DEV)
+    lens[0] = L
+    ln = (gam, bet, 1e-5)
+    wq, wf = ops.pack_frag_rows(wqkv), ops.pack_frag_rows(wfc)
+    monkeypatch.setenv("FS2_ENC_HALF", "0")
+    one = ops.enc_attn_block(x, lens, wq, bqkv, wf, bfc, ln, 2, 128, 128 ** 0.5)
+    monkeypatch.setenv("FS2_ENC_HALF", "1")
+    two = ops.enc_attn_block(x, lens, wq, bqkv, wf, bfc, ln, 2, 128, 128 ** 0.5)
+    again = ops.enc_attn_block(x, lens, wq, bqkv, wf, bfc, ln, 2, 128, 128 ** 0.5)
+    torch.cuda.synchronize()
+    assert torch.equal(two, again)
+    assert int(ops.splitk_workspace(torch.device(DEV))[:4096].view(torch.int32)[:B].abs().sum()) == 0
+    d = (two.float() - one.float()).abs()
+    ulp = one.float().abs().clamp(min=2 ** -6) * 2 ** -7
+    assert bool((d <= 2 * ulp).all()), float((d - 2 * ulp).max())
+
+
+def test_enc_embed_block_conditioning_tiles_equal_cond_vectors(gpu):
+    """The conditioning vectors computed by extra workgroups of the first encoder block's launch
+    (cond.h tiles on otherwise idle CUs) equal fs2_cond_vectors BIT-EXACTLY (the same tile code),
+    ids clamped as there; the block output is unchanged by them."""
+    ops, Lb = gpu
+    g = torch.Generator(device=DEV).manual_seed(21)
+    B, L = 13, 40
+    wqkv, bqkv, wfc, bfc, gam, bet = _weights(g)
+    table = torch.randn(30, 256, device=DEV, generator=g)
+    pe = torch.randn(L, 256, device=DEV, generator=g)
+    tok = torch.randint(0, 30, (B, L), device=DEV, generator=g)
+    lens = torch.randint(1, L + 1, (B,), generator=torch.Generator().manual_seed(3)).to(DEV)
+    spk_t = torch.randn(10, 256, device=DEV, generator=g)
+    emo_t, aro_t, val_t = (torch.randn(n, d, device=DEV, generator=g) for n, d in ((5, 128), (7, 64), (7, 64)))
+    lin_w = torch.randn(256, 256, device=DEV, generator=g) / 16
+    lin_b = torch.randn(256, device=DEV, generator=g)
+    ids = lambda n, hi: torch.randint(-1, hi + 1, (n,), device=DEV, generator=g)
+    spk, emo, aro, val = ids(B, 10), ids(B, 5), ids(B, 7), ids(B, 7)
+    ln = (gam, bet, 1e-5)
+    wq, wf = ops.pack_frag_rows(wqkv), ops.pack_frag_rows(wfc)
+    out, sv, ev = ops.enc_attn_block(None, lens, wq, bqkv, wf, bfc, ln, 2, 128, 128 ** 0.5, embed=(tok, table, pe),
+                                     cond=(spk, spk_t, emo, aro, val, emo_t, aro_t, val_t, lin_w, lin_b))
+    plain = ops.enc_attn_block(None, lens, wq, bqkv, wf, bfc, ln, 2, 128, 128 ** 0.5, embed=(tok, table, pe))
+    rs, re = ops.cond_vectors(spk, spk_t, emo, aro, val, emo_t, aro_t, val_t, lin_w, lin_b, 256)
+    torch.cuda.synchronize()
+    assert torch.equal(sv, rs) and torch.equal(ev, re)
+    assert torch.equal(out, plain)
