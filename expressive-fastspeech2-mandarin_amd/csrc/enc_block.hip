@@ -111,7 +111,7 @@ __device__ __attribute__((noinline)) void cond_role(const CondArgs &a, int bx, i
   cond_tile(a, bx, by, tid, sm);
 }
 
-template <bool EMBED>
+template <bool EMBED, bool COND = false>
 __global__ __launch_bounds__(NT, 1) void enc_attn_block_kernel(EncBlockArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   uint64_t tst[10];
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(NT, 1) void enc_attn_block_kernel(EncBlockArgs p) {
   };
   stamp();
   const int tid = threadIdx.x, lane = tid & 63;
-  if constexpr (EMBED) {
+  if constexpr (COND) {
     if ((int)blockIdx.x >= p.B) {  // a conditioning-vector tile on an otherwise idle CU
       const int c = (int)blockIdx.x - p.B;
       cond_role(p.cond, c % p.ncx, c / p.ncx, tid, reinterpret_cast<float *>(smem));
@@ -904,8 +904,11 @@ static int enc_block_launch(const void *x, const int64_t *tokens, const float *e
     hipLaunchKernelGGL(enc_attn_half_kernel<true>, dim3(nhalf), dim3(NT), 0, as_stream(stream), a);
   else if (half)
     hipLaunchKernelGGL(enc_attn_half_kernel<false>, dim3(nhalf), dim3(NT), 0, as_stream(stream), a);
+  else if (embed && a.ncond > 0)
+    hipLaunchKernelGGL((enc_attn_block_kernel<true, true>), dim3((unsigned)(B + a.ncond)), dim3(NT), 0,
+                       as_stream(stream), a);
   else if (embed)
-    hipLaunchKernelGGL(enc_attn_block_kernel<true>, dim3((unsigned)(B + a.ncond)), dim3(NT), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(enc_attn_block_kernel<true>, dim3((unsigned)B), dim3(NT), 0, as_stream(stream), a);
   else
     hipLaunchKernelGGL(enc_attn_block_kernel<false>, dim3((unsigned)B), dim3(NT), 0, as_stream(stream), a);
   FS2_CHECK_LAUNCH();

@@ -478,7 +478,10 @@ def _stage1(P, va, g, p_control, d_control, defer_lr=False):
         x = ops.embed_pe(g.texts, P.enc_emb, _pe(P, "enc", g.Lx), P.act_dtype)
     spk_vec = emo_vec = None
     has_cond = P.spk_table is not None or P.emo_table is not None
-    if has_cond and not fold:
+    # FS2_ENC_COND=1: the conditioning tiles on extra workgroups of the first block's launch (A/B:
+    # 32.4 us for that launch against 16.8 + 9.2 for the block and fs2_cond_vectors, profiles/r5ck)
+    cond_fold = fold and os.environ.get("FS2_ENC_COND", "0") == "1"
+    if has_cond and not cond_fold:
         spk_vec, emo_vec = ops.cond_vectors(
             g.speakers if P.spk_table is not None else None, P.spk_table,
             g.emotions if P.emo_table is not None else None, g.arousals, g.valences, P.emo_table,
@@ -490,7 +493,7 @@ def _stage1(P, va, g, p_control, d_control, defer_lr=False):
         _STACK[0] = "enc"
         lp = P.enc_layers[0]
         cond = None
-        if has_cond:  # the conditioning vectors on extra workgroups of the same launch
+        if has_cond and cond_fold:  # the conditioning vectors on extra workgroups of the same launch
             cond = (g.speakers if P.spk_table is not None else None, P.spk_table,
                     g.emotions if P.emo_table is not None else None, g.arousals, g.valences, P.emo_table,
                     getattr(P, "aro_table", None), getattr(P, "val_table", None), getattr(P, "emo_w", None),
@@ -499,7 +502,10 @@ def _stage1(P, va, g, p_control, d_control, defer_lr=False):
             r = ops.enc_attn_block(None, g.lens_src, lp.wqf, lp.bqkv, lp.wfcf, lp.bfc, lp.ln1, lp.n_head, lp.d_k,
                                    float(np.power(lp.d_k, 0.5)), embed=(g.texts, P.enc_emb, _pe(P, "enc", g.Lx)),
                                    masks=g.mask_out, cond=cond)
-        h, spk_vec, emo_vec = r if cond is not None else (r, None, None)
+        if cond is not None:
+            h, spk_vec, emo_vec = r
+        else:
+            h = r
         last = n_enc == 1
         x, _, _ = _ffn_tail(P, lp, h, h, g.lens_src, spk_vec if last else None, emo_vec if last else None, False, None,
                             None, None, P.enc_layers[1] if n_enc > 1 else None)

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Per-launch PMC table of a whole forward from tools/pmc_cmd.sh passes over tools/fwd_probe.py.
 
-Dispatches are ordered by id and cut into forwards at their two leading length-mask launches
-(as tools/fwd_gaps.py); counters are averaged per launch position over the forwards of the most
+Dispatches are ordered by id and cut into forwards at their two leading length-mask launches (or
+the conditioning launch / the first encoder block, as tools/fwd_gaps.py); counters are averaged per launch position over the forwards of the most
 common launch count. Units and corrections (MI355X_MICROARCH.md):
 * FETCH_SIZE / WRITE_SIZE are KiB; FETCH_SIZE is doubled (gfx950 reports half the bytes of a
   16 B/lane streaming read). hbm_MB = 2 * FETCH + WRITE.
@@ -42,6 +42,11 @@ def dispatches(d):
 
 def forwards(seq):
     st = [i for i in range(len(seq) - 1) if "length_mask" in seq[i]["name"] and "length_mask" in seq[i + 1]["name"]]
+    # round 5: the first encoder block writes the masks; a forward starts at the conditioning
+    # launch, or at that block when there is none (as tools/fwd_gaps.py)
+    for marker in ("cond_kernel", "enc_attn_block_kernel<true>", "enc_attn_block_kernelILb1"):
+        if len(st) < 2:
+            st = [i for i in range(len(seq)) if marker in seq[i]["name"]]
     return [seq[a:b] for a, b in zip(st, st[1:] + [len(seq)])]
 
 
