@@ -308,6 +308,213 @@ __global__ __launch_bounds__(64 * NW) void mrf_kernel(MrfArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// One ResBlock1 dilation pair at C = 128 (the 64x stage: 128 channels, T * 64 samples) in ONE
+// launch (hifigan/models.py:34-45):
+//
+//   y = conv_k,1(lrelu(conv_k,d(lrelu(x)) + b1, 0.1)) + b2 + x (+ xs)
+//   out = y, or lrelu(y * out_scale, out_slope) for the stage's last pair
+//
+// The whole-stage MRF form above needs three [384 x C] buffers (288 KiB at C = 128); as two conv
+// launches per pair every intermediate made an HBM round trip (conv1 wrote t, conv2 read t and x
+// and wrote x and lrelu(x): 2.7 GB per pair at cfg2, 12.4 ms of a 29.4 ms vocoder call). Here a
+// workgroup owns L = 256 samples of one utterance:
+// * A: lrelu(x) over [t0 - hk (D + 1), t0 + L + hk (D + 1)) by LDS-DMA + an in-place leaky_relu
+//   (each lane converts the 16-byte chunks its own DMA wrote, after its own vmcnt wait);
+// * T: lrelu(conv1 + b1) over [t0 - hk, t0 + L + hk) (17 row blocks), zeros outside [0, T);
+// * conv2 over T, + b2 + x (registers, loaded at the start) (+ xs), staged in T's rows and stored
+//   as whole 256-byte rows.
+// 8 waves (two per SIMD), wave w owns output channels 16w .. 16w + 15 of both convs and every row
+// block: its weight fragment of a k-step (1 KiB, fragment order of pack_wconv_tail) comes from
+// L2 three k-steps ahead; the activations are the B operand from LDS. Rows are 256 B with the
+// 16-byte chunk rotated by 2 * row (phys = (c + 2 r) & 15): the ds_read_b128 lane groups
+// {0-3,12-15,20-27}, ... hit 16 distinct slots for every row shift (the bank behaviour of a
+// 288-byte pitch, without its padding), and a 1 KiB LDS-DMA piece stays 4 whole rows.
+constexpr int kPrL = 256;   // output samples per workgroup
+constexpr int kPrC = 128;   // channels
+constexpr int kPrNW = 8;    // waves
+constexpr int kPrNBT = 17;  // conv1 output row blocks (>= (L + 2 hk) / 16 for k <= 11)
+
+struct PairArgs {
+  const bf16 *x;        // [B, T, 128] pair input (residual; conv1 reads lrelu(x))
+  const bf16 *w1, *w2;  // pack_wconv_tail fragment order, [k * 4 k-steps][8 blocks][64][8]
+  const float *b1, *b2; // [128]
+  const bf16 *xs;       // optional running sum (may alias out)
+  bf16 *out;            // [B, T, 128]
+  int T, D;             // samples per utterance, conv1 dilation
+  float out_scale, out_slope;
+  int out_act;          // 0: out = y; 1: out = lrelu(y * out_scale, out_slope)
+  uint32_t x_bytes;
+};
+
+__device__ __forceinline__ int pr_phys(int r, int c) { return (c + 2 * r) & 15; }
+
+template <int K>
+__global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
+  constexpr int HK = (K - 1) / 2;
+  // A rows: L + 2 hk (D + 1) <= L + 12 hk (D <= 5), + 16 rows that conv1's unused output rows
+  // (T rows >= L + 2 hk) read past the end (stale data there reaches only those rows)
+  constexpr int RA_MAX = kPrL + 12 * HK + 16;
+  constexpr int A_OFF = 0, T_OFF = RA_MAX * 256;
+  constexpr int SMEM = T_OFF + kPrNBT * 16 * 256;
+  static_assert(SMEM <= 163840, "LDS");
+  static_assert(kPrL + 2 * HK <= kPrNBT * 16, "conv1 rows");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g = lane >> 4;
+  const int T = p.T, D = p.D;
+  const int t0 = blockIdx.x * kPrL;
+  const int64_t ubase = (int64_t)blockIdx.y * T;
+  const int HA = HK * (D + 1);         // A halo
+  const int RA = kPrL + 2 * HA;        // A rows of this launch (multiple of 4)
+  const int a0 = t0 - HA;              // sample of A row 0
+  const rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+
+  // ---- A <- x over [a0, a0 + RA) by LDS-DMA (rows outside [0, T) read as zeros)
+  const int npc = RA / 4;  // 1 KiB pieces
+  for (int pc = w; pc < npc; pc += kPrNW) {
+    const int R = 4 * pc + (lane >> 4), ph = lane & 15;
+    const int c = (ph - 2 * R) & 15, s = a0 + R;
+    const uint32_t off = (unsigned)s < (unsigned)T ? (uint32_t)((ubase + s) * 256 + c * 16) : kOOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)(smem + A_OFF + pc * 1024),
+                                             16, off, 0, 0, 0);
+  }
+  // the residual x of this wave's conv2 output (rows t0 + 16b + r16, channels 16w + 4g .. +3)
+  bf16x4 res[16];
+#pragma unroll
+  for (int b = 0; b < 16; ++b) {
+    const int s = t0 + 16 * b + r16;
+    const uint32_t off = s < T ? (uint32_t)((ubase + s) * 256 + (16 * w + 4 * g) * 2) : kOOB;
+    res[b] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // lrelu in place over this wave's own pieces
+  for (int pc = w; pc < npc; pc += kPrNW) {
+    bf16x8 *q = reinterpret_cast<bf16x8 *>(smem + A_OFF + pc * 1024 + lane * 16);
+    bf16x8 v = *q;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (bf16)lrelu((float)v[i], 0.1f);
+    *q = v;
+  }
+  __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
+  __builtin_amdgcn_s_barrier();
+
+  // ---- one conv: NB output row blocks from IN, k-step s = tap * 4 + kc, weights wp (block w),
+  // B row of output row r and tap: r + tap * dil (IN row; conv1 reads A rows up to 16 * 17 - 1 +
+  // 2 hk D <= RA_MAX - 1, conv2 T rows up to 255 + 2 hk < 272)
+  auto conv = [&](auto nb_tag, const bf16 *wp, int IN, int dil, f32x4 (&acc)[decltype(nb_tag)::value])
+      __attribute__((always_inline)) {
+    constexpr int NB = decltype(nb_tag)::value;
+    const rsrc_t wr = make_rsrc(wp, (uint32_t)(K * kPrC * kPrC * 2));
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 wf[4];
+    auto wload = [&](int s, bf16x8 &f) __attribute__((always_inline)) {
+      f = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wr, (uint32_t)lane * 16u,
+                                                                           (uint32_t)((s * 8 + w) * 1024), 0));
+    };
+    wload(0, wf[0]);
+    wload(1, wf[1]);
+    wload(2, wf[2]);
+#pragma nounroll
+    for (int tap = 0; tap < K; ++tap) {
+      const int sh = tap * dil;
+#pragma unroll
+      for (int kc = 0; kc < 4; ++kc) {
+        const int s = tap * 4 + kc;
+        if (s + 3 < 4 * K) {
+          wload(s + 3, wf[(kc + 3) & 3]);
+          asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        // row 16 b + r16 + sh: the rotation (c + 2 row) & 15 does not depend on b, so every block's
+        // read is one base + an immediate 4 KiB * b
+        const int R0 = r16 + sh;
+        const char *base = smem + IN + R0 * 256 + pr_phys(R0, 4 * kc + g) * 16;
+        bf16x8 fb[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) fb[b] = *reinterpret_cast<const bf16x8 *>(base + b * 4096);
+        // all reads issued before the first MFMA (interleaved read -> wait -> MFMA pairs exposed
+        // the LDS latency on every MFMA)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kc], fb[b], acc[b], 0, 0, 0);
+      }
+    }
+  };
+
+  const int ch = 16 * w + 4 * g;  // this lane's 4 output channels
+  {
+    f32x4 acc[kPrNBT];
+    conv(std::integral_constant<int, kPrNBT>{}, p.w1, A_OFF, D, acc);
+    const float4 bb = *reinterpret_cast<const float4 *>(p.b1 + ch);
+    // T row r = sample t0 - HK + r
+#pragma unroll
+    for (int b = 0; b < kPrNBT; ++b) {
+      const int R = 16 * b + r16, s = t0 - HK + R;
+      // zero padding of conv2's input as a multiply (a select here became a branch per element;
+      // rows that see stale LDS are never read)
+      const float m = (unsigned)s < (unsigned)T ? 1.f : 0.f;
+      bf16x4 t;
+      t[0] = (bf16)(lrelu(acc[b][0] + bb.x, 0.1f) * m);
+      t[1] = (bf16)(lrelu(acc[b][1] + bb.y, 0.1f) * m);
+      t[2] = (bf16)(lrelu(acc[b][2] + bb.z, 0.1f) * m);
+      t[3] = (bf16)(lrelu(acc[b][3] + bb.w, 0.1f) * m);
+      *reinterpret_cast<bf16x4 *>(smem + T_OFF + R * 256 + pr_phys(R, ch >> 3) * 16 + (ch & 7) * 2) = t;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
+  __builtin_amdgcn_s_barrier();
+
+  f32x4 acc[16];
+  conv(std::integral_constant<int, 16>{}, p.w2, T_OFF, 1, acc);
+  // the running sum (first in the load queue after conv2's last weight wait)
+  bf16x4 xs[16];
+  if (p.xs != nullptr) {
+    const rsrc_t sr = make_rsrc(p.xs, p.x_bytes);
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int s = t0 + 16 * b + r16;
+      const uint32_t off = s < T ? (uint32_t)((ubase + s) * 256 + ch * 2) : kOOB;
+      xs[b] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(sr, off, 0, 0));
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
+  __builtin_amdgcn_s_barrier();  // every wave done reading T: its rows 0 .. 255 become the output stage
+  {
+    const float4 bb = *reinterpret_cast<const float4 *>(p.b2 + ch);
+    const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int R = 16 * b + r16;
+      bf16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = acc[b][i] + bv[i] + (float)res[b][i];
+        if (p.xs != nullptr) v += (float)xs[b][i];
+        o[i] = (bf16)(p.out_act ? lrelu(v * p.out_scale, p.out_slope) : v);
+      }
+      *reinterpret_cast<bf16x4 *>(smem + T_OFF + R * 256 + pr_phys(R, ch >> 3) * 16 + (ch & 7) * 2) = o;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
+  __builtin_amdgcn_s_barrier();
+  // whole 256-byte rows, 16 bytes a lane
+  const rsrc_t orr = make_rsrc(p.out, p.x_bytes);
+#pragma unroll
+  for (int i = 0; i < kPrL * 16 / (64 * kPrNW); ++i) {
+    const int q = i * 64 * kPrNW + tid, R = q >> 4, c = q & 15, s = t0 + R;
+    const uint4 v = *reinterpret_cast<const uint4 *>(smem + T_OFF + R * 256 + pr_phys(R, c) * 16);
+    if (s < T)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), orr,
+                                             (uint32_t)((ubase + s) * 256 + c * 16), 0, 0);
+  }
+}
+
 }  // namespace
 
 extern "C" int64_t fs2_hifigan_mrf_weight_elems(int C) {
@@ -338,6 +545,41 @@ extern "C" int fs2_hifigan_mrf(const void *x, const void *x_act, const void *w, 
     hipLaunchKernelGGL((mrf_kernel<32, 4>), grid, dim3(256), 0, as_stream(stream), p);
   else
     hipLaunchKernelGGL((mrf_kernel<64, 8>), grid, dim3(512), 0, as_stream(stream), p);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_hifigan_pair(const void *x, const void *w1, const float *b1, const void *w2, const float *b2, int B,
+                                int T, int C, int ks, int dilation, const void *xs, float out_scale, float out_slope,
+                                int out_act, void *out, fs2_stream_t stream) {
+  if (x == nullptr || w1 == nullptr || b1 == nullptr || w2 == nullptr || b2 == nullptr || out == nullptr || B < 0 || T < 0)
+    return FS2_EINVAL;
+  if (C != kPrC || !(ks == 3 || ks == 7 || ks == 11) || dilation < 1 || dilation > 5) return FS2_EUNSUPPORTED;
+  if (out == x) return FS2_EINVAL;  // other tiles re-read the input's halo rows
+  if (B == 0 || T == 0) return FS2_OK;
+  const int64_t bytes = (int64_t)B * T * C * 2;
+  if (bytes >= (1LL << 31)) return FS2_EUNSUPPORTED;
+  PairArgs p;
+  p.x = reinterpret_cast<const bf16 *>(x);
+  p.w1 = reinterpret_cast<const bf16 *>(w1);
+  p.w2 = reinterpret_cast<const bf16 *>(w2);
+  p.b1 = b1;
+  p.b2 = b2;
+  p.xs = reinterpret_cast<const bf16 *>(xs);
+  p.out = reinterpret_cast<bf16 *>(out);
+  p.T = T;
+  p.D = dilation;
+  p.out_scale = out_scale;
+  p.out_slope = out_slope;
+  p.out_act = out_act ? 1 : 0;
+  p.x_bytes = (uint32_t)bytes;
+  const dim3 grid((unsigned)((T + kPrL - 1) / kPrL), (unsigned)B);
+  if (ks == 3)
+    hipLaunchKernelGGL(pair_kernel<3>, grid, dim3(64 * kPrNW), 0, as_stream(stream), p);
+  else if (ks == 7)
+    hipLaunchKernelGGL(pair_kernel<7>, grid, dim3(64 * kPrNW), 0, as_stream(stream), p);
+  else
+    hipLaunchKernelGGL(pair_kernel<11>, grid, dim3(64 * kPrNW), 0, as_stream(stream), p);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

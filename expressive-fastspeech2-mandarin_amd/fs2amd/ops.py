@@ -440,6 +440,24 @@ def hifigan_mrf(x, x_act, w_packed, bias, out_slope, out=None):
     return out
 
 
+def hifigan_pair(x, w1, b1, w2, b2, ks, dilation, *, xs=None, out_scale=1.0, out_slope=0.1, out_act=False, out=None):
+    """fs2_hifigan_pair: one ResBlock1 dilation pair at C = 128 in one launch,
+    y = conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2 + x (+ xs); returns y, or lrelu(y * out_scale,
+    out_slope) with out_act. x / xs bf16 [B, T, 128]; w1 / w2 from :func:`pack_wconv_tail`."""
+    _gpu(x, w1, b1, w2, b2)
+    B, T, C = x.shape
+    assert x.dtype == torch.bfloat16 and x.is_contiguous()
+    assert w1.numel() == ks * C * C and w2.numel() == ks * C * C and b1.numel() == C and b2.numel() == C
+    if xs is not None:
+        assert xs.shape == x.shape and xs.dtype == torch.bfloat16 and xs.is_contiguous()
+    if out is None:
+        out = torch.empty_like(x)
+    L.check(_lib.fs2_hifigan_pair(_ptr(x), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), B, T, C, int(ks), int(dilation),
+                                  None if xs is None else _ptr(xs), float(out_scale), float(out_slope),
+                                  1 if out_act else 0, _ptr(out), _stream(x)), "fs2_hifigan_pair")
+    return out
+
+
 def wconv(x, w_packed, bias, *, ks, pad, out=None, second=None, layout=None, tail=None):
     """PostNet Conv1d(512, 512, k=5) + folded BatchNorm + tanh on padded bf16 rows [B, T, 512]
     (fs2_wconv; w_packed from :func:`pack_wconv_weight`). second = (w2_packed, bias2): the next

@@ -180,11 +180,19 @@ class Generator(nn.Module):
             P["rb"].append([(conv(c1), conv(c2)) for c1, c2 in zip(rb.convs1, rb.convs2)])
         # the narrow stages' multi-receptive-field blocks as one fused launch each (fs2_hifigan_mrf)
         P["mrf"] = {}
+        # the 128-channel stage: one fused launch per ResBlock1 dilation pair (fs2_hifigan_pair)
+        P["pair"] = {}
         if c == L.FS2_BF16 and list(self.h.resblock_kernel_sizes) == [3, 7, 11] and \
                 all(list(d) == [1, 3, 5] for d in self.h.resblock_dilation_sizes) and str(self.h.resblock) == "1":
             nk = self.num_kernels
             for i in range(self.num_upsamples):
                 ch = self.h.upsample_initial_channel // (2 ** (i + 1))
+                if ch == 128:
+                    P["pair"][i] = [[(ops.pack_wconv_tail(_weight(c1).float().to(dev)), c1.bias.detach().float().to(dev),
+                                      ops.pack_wconv_tail(_weight(c2).float().to(dev)), c2.bias.detach().float().to(dev),
+                                      c1.kernel_size[0], c1.dilation[0])
+                                     for c1, c2 in zip(rb.convs1, rb.convs2)]
+                                    for rb in self.resblocks[i * nk:(i + 1) * nk]]
                 if ch not in (32, 64):
                     continue
                 ws, bs = [], []
@@ -203,6 +211,28 @@ class Generator(nn.Module):
         P["post"] = {"w": ops.pack_conv_weight(w4, c), "b": b4, "cin": wp.shape[1], "ks": wp.shape[2], "pad": 3}
         self._packs[key] = (fp, P)
         return P
+
+    def _pair_stage(self, chains, xu, out_slope):
+        """A 128-channel stage's multi-receptive-field block as 9 fs2_hifigan_pair launches:
+        chain j's pairs 0 and 1 ping-pong between two buffers, its last pair adds into the running
+        sum xs (in place), and the last chain's emits leaky_relu(xs / num_kernels, out_slope)."""
+        from . import ops
+
+        nk = len(chains)
+        xa, xb, xs, nxt = (torch.empty_like(xu) for _ in range(4))
+        for j, pairs in enumerate(chains):
+            xp = xu
+            for pi, (w1, b1, w2, b2, k, d) in enumerate(pairs):
+                if pi < len(pairs) - 1:
+                    xn = xa if xp is not xa else xb
+                    ops.hifigan_pair(xp, w1, b1, w2, b2, k, d, out=xn)
+                    xp = xn
+                elif j < nk - 1:
+                    ops.hifigan_pair(xp, w1, b1, w2, b2, k, d, xs=xs if j > 0 else None, out=xs)
+                else:
+                    ops.hifigan_pair(xp, w1, b1, w2, b2, k, d, xs=xs, out_scale=1.0 / nk, out_slope=out_slope,
+                                     out_act=True, out=nxt)
+        return nxt
 
     # ---- forward ---------------------------------------------------------------------------------
     def forward(self, x):
@@ -232,10 +262,16 @@ class Generator(nn.Module):
             T2 = T * up["u"]
             C = up["cout"]
             xu = torch.empty(B, T2, C, device=mel.device, dtype=dt)      # ups output (residual of pair 0)
+            last_stage = i == len(P["ups"]) - 1
+            if i in P["pair"] and os.environ.get("FS2_VOC_PAIR", "1") != "0":
+                # one launch per dilation pair (leaky_relu of the pair input applied on chip)
+                run(h, up, L.EPI_BIAS, xu, T)
+                T = T2
+                h = self._pair_stage(P["pair"][i], xu, 0.01 if last_stage else LRELU_SLOPE)
+                continue
             a0 = torch.empty_like(xu)                                    # leaky_relu(xu): convs1 input of pair 0
             run(h, up, L.EPI_BIAS, xu, T, out2=a0.view(B, T, -1), out2_act=True, out2_slope=LRELU_SLOPE)
             T = T2
-            last_stage = i == len(P["ups"]) - 1
             if i in P["mrf"] and os.environ.get("FS2_VOC_MRF", "1") != "0":
                 # the stage's 18 ResBlock convs, their average and the next leaky_relu in one launch
                 wm, bm = P["mrf"][i]

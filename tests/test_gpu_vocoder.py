@@ -175,3 +175,67 @@ def test_hifigan_mrf_fused_stage(gen, C, T):
     err = (out.double().cpu() - ref).abs()
     scale = float(ref.abs().max())
     assert float(err.max()) <= 3e-2 * scale and float(err.mean()) <= 2e-3 * scale, (float(err.max()), float(err.mean()), scale)
+
+
+@pytest.mark.parametrize("T,k,d,mode", [(1000, 11, 5, "plain"), (300, 7, 3, "xs"), (77, 3, 1, "last"),
+                                        (513, 11, 1, "last"), (256, 3, 5, "plain"), (40, 7, 5, "xs")])
+def test_hifigan_pair_matches_f64(T, k, d, mode):
+    """fs2_hifigan_pair (one ResBlock1 dilation pair at C = 128: lrelu, dilated conv, lrelu, conv,
+    residual, optionally + the running sum and the stage's closing leaky_relu, one launch; 256-sample
+    tiles, the dilated conv's halo on chip) against a float64 statement of hifigan/models.py:34-45 on
+    the same bf16 input and bf16-rounded weights, with the kernel's bf16 rounding points (lrelu(x)
+    and the first conv's output stored as bf16): max |err| <= 2e-2 of the output scale, mean <=
+    2e-3. Tile and utterance edges included (T not a multiple of 256, T < 256, dilation halo
+    larger than the sequence)."""
+    from fs2amd import ops
+
+    g = torch.Generator().manual_seed(T + 10 * k + d)
+    B, C = 3, 128
+    w1, w2 = (torch.randn(C, C, k, generator=g) / (C * k) ** 0.5 for _ in range(2))
+    b1, b2 = (0.05 * torch.randn(C, generator=g) for _ in range(2))
+    x = (0.5 * torch.randn(B, T, C, generator=g)).to(torch.bfloat16)
+    xs = (0.5 * torch.randn(B, T, C, generator=g)).to(torch.bfloat16)
+    kw = {}
+    if mode != "plain":
+        kw["xs"] = xs.to(DEV)
+    if mode == "last":
+        kw.update(out_scale=1.0 / 3, out_slope=0.01, out_act=True)
+    out = ops.hifigan_pair(x.to(DEV), ops.pack_wconv_tail(w1.to(DEV)), b1.to(DEV), ops.pack_wconv_tail(w2.to(DEV)),
+                           b2.to(DEV), k, d, **kw)
+    torch.cuda.synchronize()
+
+    def conv(z, w, b, dd):
+        return F.conv1d(z.transpose(1, 2), w.to(torch.bfloat16).double(), b.double(), dilation=dd,
+                        padding=(k * dd - dd) // 2).transpose(1, 2)
+
+    bf = lambda t: t.to(torch.bfloat16).double()
+    a = bf(F.leaky_relu(x.double(), 0.1))
+    t = bf(F.leaky_relu(conv(a, w1, b1, d), 0.1))
+    y = conv(t, w2, b2, 1) + x.double()
+    if mode != "plain":
+        y = y + xs.double()
+    ref = F.leaky_relu(y / 3, 0.01) if mode == "last" else y
+    err = (out.double().cpu() - ref).abs()
+    scale = float(ref.abs().max())
+    assert float(err.max()) <= 2e-2 * scale and float(err.mean()) <= 2e-3 * scale, (float(err.max()), float(err.mean()), scale)
+
+
+def test_hifigan_pair_stage_matches_per_conv_path(gen):
+    """The 128-channel stage on fs2_hifigan_pair (9 launches) against the same stage on the
+    per-conv fs2_conv1d path (FS2_VOC_PAIR=0, 18 launches): same waveform within bf16 noise."""
+    from fs2amd import _lib as L
+
+    g = torch.Generator().manual_seed(5)
+    mel = (torch.randn(2, 80, 57, generator=g) - 4.0).to(DEV)
+    gen.set_precision("bf16")
+    try:
+        assert list(gen.packed(torch.device(DEV))["pair"]) == [1]  # the 128-channel stage
+        with torch.no_grad():
+            y1 = gen(mel).float().cpu()
+            os.environ["FS2_VOC_PAIR"] = "0"
+            y0 = gen(mel).float().cpu()
+    finally:
+        os.environ.pop("FS2_VOC_PAIR", None)
+        gen.set_precision("fp32")
+    snr = _snr_db(y0.numpy(), y1.numpy())
+    assert snr >= 30.0, snr

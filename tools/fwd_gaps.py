@@ -24,7 +24,7 @@ def forwards(rows, start=None):
               and "length_mask" in rows[i + 1]["Kernel_Name"]]
         # round 5: the first encoder block writes the masks (fs2_enc_embed_attn_block); a forward
         # then starts at the conditioning launch, or at that block when there is none
-        for marker in ("cond_kernel", "enc_attn_block_kernel<true>", "enc_attn_block_kernelILb1"):
+        for marker in ("cond_kernel", "enc_attn_block_kernel<true", "enc_attn_block_kernelILb1"):
             if len(st) < 2:
                 st = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
     return [rows[a:b] for a, b in zip(st, st[1:])]

@@ -44,7 +44,7 @@ def forwards(seq):
     st = [i for i in range(len(seq) - 1) if "length_mask" in seq[i]["name"] and "length_mask" in seq[i + 1]["name"]]
     # round 5: the first encoder block writes the masks; a forward starts at the conditioning
     # launch, or at that block when there is none (as tools/fwd_gaps.py)
-    for marker in ("cond_kernel", "enc_attn_block_kernel<true>", "enc_attn_block_kernelILb1"):
+    for marker in ("cond_kernel", "enc_attn_block_kernel<true", "enc_attn_block_kernelILb1"):
         if len(st) < 2:
             st = [i for i in range(len(seq)) if marker in seq[i]["name"]]
     return [seq[a:b] for a, b in zip(st, st[1:] + [len(seq)])]
