@@ -1074,9 +1074,9 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
     if (d->pre_w == nullptr || d->pre_b == nullptr || d->pre_gamma == nullptr || d->pre_beta == nullptr ||
         d->pre_att_row_stride < kD || (d->pre_att_row_stride & 7) || d->pre_att == d->out)
       return FS2_EINVAL;
-    // packed 112-row unsplit launches (the decoder) or padded [B, T] rows with lengths, 64-row tiles
-    // in the split-hidden form (the encoder)
-    const bool dec_form = d->rows_dev != nullptr && S == 1 && d->tile_rows != 64;
+    // packed unsplit launches on 112- or 64-row tiles (the decoder; 64 rows when free-running) or
+    // padded [B, T] rows with lengths, 64-row tiles in the split-hidden form (the encoder)
+    const bool dec_form = d->rows_dev != nullptr && S == 1;
     const bool enc_form = d->rows_dev == nullptr && d->tile_rows == 64;
     if (!(dec_form || enc_form) || d->KS != 9 || d->F != 1024) return FS2_EUNSUPPORTED;
     const int64_t ab = M64 * d->pre_att_row_stride * 2;

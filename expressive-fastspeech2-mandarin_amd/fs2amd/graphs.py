@@ -88,9 +88,17 @@ class SynthGraphs:
         p_c, e_c, d_c = controls
         g = SimpleNamespace(speakers=s["speakers"], emotions=s["emotions"], arousals=s["arousals"],
                             valences=s["valences"], texts=s["texts"], lens_src=s["src_lens"], Lx=Lx,
-                            p_targets=s["p_targets"], e_targets=s["e_targets"], d_targets=None, mel_lens=None)
+                            p_targets=s["p_targets"], e_targets=s["e_targets"], d_targets=None, mel_lens=None,
+                            mask_out=None)
+        src_masks = None
+        if R.embed_block_ok(P, Lx):
+            # the first encoder block's launch builds its input and writes the source mask
+            src_masks = torch.empty(s["texts"].shape[0], Lx, device=s["texts"].device, dtype=torch.bool)
+            g.mask_out = (src_masks, None, None)
         st = R._stage1(P, va, g, p_c, d_c)
-        return g, st, R._mask(s["src_lens"], Lx), R.meta_vector(st.mel_len, s["texts"].device)
+        if src_masks is None:
+            src_masks = R._mask(s["src_lens"], Lx)
+        return g, st, src_masks, R.meta_vector(st.mel_len, s["texts"].device)
 
     def _capture(self, fn):
         """Warm fn up on a side stream (allocates per-stream workspaces outside the capture), then

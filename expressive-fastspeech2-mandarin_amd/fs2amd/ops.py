@@ -573,7 +573,7 @@ def ffn_launch_rows(x, layout):
 
 def ffn_pre_ok(x, layout, F, ks):
     """fs2_ffn's fc + residual + LN prologue (pre_att) covers the k = 9, F = 1024 FFN as packed
-    112-row unsplit launches (the decoder's) and, opt-in (FS2_FFN_PRE_ENC=1), as padded [B, T]
+    112- or 64-row unsplit launches (the decoder's) and, opt-in (FS2_FFN_PRE_ENC=1), as padded [B, T]
     launches on 64-row tiles (the encoder's split-hidden form; padded rows are masked in the
     prologue). Off by default: every split of a tile recomputes the prologue, and the encoder
     launch grew by more than the fc launch it replaces (51-53 vs 41.6 + 10.4 us per block in
@@ -582,7 +582,9 @@ def ffn_pre_ok(x, layout, F, ks):
         return False
     form = ffn_form(ffn_launch_rows(x, layout), F)
     if layout is not None:
-        return form == (112, 1)
+        # packed unsplit launches: 112-row tiles (teacher-forced cfg2) or 64-row tiles (a
+        # free-running decoder of ~11k rows); FS2_FFN_PRE64=0 keeps the fc launch for the latter
+        return form == (112, 1) or (form == (64, 1) and os.environ.get("FS2_FFN_PRE64", "1") != "0")
     return form[0] == 64 and os.environ.get("FS2_FFN_PRE_ENC", "0") == "1"
 
 

@@ -268,15 +268,17 @@ def test_ffn_next_qkv_epilogue(gpu, tile_rows, nsplit, packed):
     assert float(err.mean()) <= 1e-3 * scale, (float(err.mean()), scale)
 
 
-@pytest.mark.parametrize("B,T,seed", [(64, 430, 31), (8, 130, 32), (3, 37, 33)])
-def test_ffn_pre_fc_ln_prologue(gpu, B, T, seed):
+@pytest.mark.parametrize("B,T,seed,tile", [(64, 430, 31, 112), (8, 130, 32, 112), (3, 37, 33, 112),
+                                          (64, 430, 34, 64), (8, 130, 35, 64), (3, 37, 36, 64)])
+def test_ffn_pre_fc_ln_prologue(gpu, B, T, seed, tile):
     """fs2_ffn with pre_att: the FFT block's attention output projection + residual + LayerNorm
     (SubLayers.py:54-55) computed in the fused FFN's prologue for each tile and its 4+4 halo rows,
     then the FFN (packed rows; ragged lengths incl. 0 and 1). Against a float64 statement of the
     whole sequence (h rounded to bf16 where the two-launch path stores it) within the FFN's bf16
     tolerance, and against the two launches (fc + LN on fs2_conv1d, then fs2_ffn) within 2 bf16 ulps
     (the h rounding can move by one ulp with the summation order). Also with the next block's
-    Q|K|V in the epilogue."""
+    Q|K|V in the epilogue. Both packed unsplit tile forms: 112 rows (teacher-forced decoder) and
+    64 rows (free-running decoder)."""
     ops, L = gpu
     W = _weights(ops, L, seed=seed)
     g = torch.Generator(device=DEV).manual_seed(seed + 7)
@@ -294,13 +296,14 @@ def test_ffn_pre_fc_ln_prologue(gpu, B, T, seed):
     with ops.splitk_enabled(False):  # the 112-row unsplit form the prologue covers
         h2 = ops.conv1d(pk(att), ops.pack_conv_weight(wfc, L.FS2_BF16), bfc, cin=256, ks=1, pad=0, compute=L.FS2_BF16,
                         epilogue=L.EPI_RES_LN, out_dtype=L.FS2_BF16, residual=pk(x), ln=ln1, layout=lay)
-        two = ops.ffn(h2, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay)
+        tf = dict(tile_rows=tile, nsplit=1)
+        two = ops.ffn(h2, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay, **tf)
         one = ops.ffn(pk(x), W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay,
-                      pre=(pk(att), ops.pack_frag_rows(wfc), bfc, ln1))
+                      pre=(pk(att), ops.pack_frag_rows(wfc), bfc, ln1), **tf)
         wq = torch.randn(768, 256, device=DEV, generator=g) / 16
         bq = 0.1 * torch.randn(768, device=DEV, generator=g)
         one_q, qkv = ops.ffn(pk(x), W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay,
-                             pre=(pk(att), ops.pack_frag_rows(wfc), bfc, ln1), next_qkv=(ops.pack_frag_rows(wq), bq))
+                             pre=(pk(att), ops.pack_frag_rows(wfc), bfc, ln1), next_qkv=(ops.pack_frag_rows(wq), bq), **tf)
     torch.cuda.synchronize()
     R = int(lay.cu[-1])
     # float64 reference on the padded rows
