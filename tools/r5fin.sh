@@ -8,6 +8,8 @@ timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > $O/smoke.
 tail -2 $O/smoke.log
 timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
 tail -1 $O/bench.log | cut -c1-300
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --extra 0 > $O/bench_driver.log 2>&1 || { tail -30 $O/bench_driver.log; exit 1; }
+tail -1 $O/bench_driver.log | cut -c1-200
 timeout -k 10 200 python tools/free_probe.py > $O/free.log 2>&1 || { tail -20 $O/free.log; exit 1; }
 grep -v amdgpu.ids $O/free.log | tail -1
 timeout -k 10 200 python tools/free_probe.py --eager > $O/free_eager.log 2>&1 || { tail -20 $O/free_eager.log; exit 1; }
