@@ -381,13 +381,22 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)(smem + A_OFF + pc * 1024),
                                              16, off, 0, 0, 0);
   }
-  // the residual x of this wave's conv2 output (rows t0 + 16b + r16, channels 16w + 4g .. +3)
-  bf16x4 res[16];
+  // wave w: output channels 32 cp .. 32 cp + 31 (cp = w & 3: two 16-channel MFMA blocks) of row
+  // half rh = w >> 2 (conv1 blocks 9 rh .. 9 rh + 8, conv2 blocks 8 rh .. 8 rh + 7): every B
+  // fragment read from LDS feeds two MFMAs (one wave per 16 channels over all rows read 136 KiB
+  // of LDS per k-step per CU, as many LDS cycles as MFMA cycles)
+  const int cp = w & 3, rh = w >> 2;
+  // the residual x of this wave's conv2 output (rows t0 + 16 (8 rh + b) + r16, channels
+  // 32 cp + 16 j + 4 g .. +3)
+  bf16x4 res[2][8];
 #pragma unroll
-  for (int b = 0; b < 16; ++b) {
-    const int s = t0 + 16 * b + r16;
-    const uint32_t off = s < T ? (uint32_t)((ubase + s) * 256 + (16 * w + 4 * g) * 2) : kOOB;
-    res[b] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
+  for (int b = 0; b < 8; ++b) {
+    const int s = t0 + 16 * (8 * rh + b) + r16;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t off = s < T ? (uint32_t)((ubase + s) * 256 + (32 * cp + 16 * j + 4 * g) * 2) : kOOB;
+      res[j][b] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // lrelu in place over this wave's own pieces
@@ -401,19 +410,24 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
   __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
   __builtin_amdgcn_s_barrier();
 
-  // ---- one conv: NB output row blocks from IN, k-step s = tap * 4 + kc, weights wp (block w),
-  // B row of output row r and tap: r + tap * dil (IN row; conv1 reads A rows up to 16 * 17 - 1 +
-  // 2 hk D <= RA_MAX - 1, conv2 T rows up to 255 + 2 hk < 272)
-  auto conv = [&](auto nb_tag, const bf16 *wp, int IN, int dil, f32x4 (&acc)[decltype(nb_tag)::value])
-      __attribute__((always_inline)) {
+  // ---- one conv: NB row blocks from block b0 of IN, k-step s = tap * 4 + kc, weights wp (blocks
+  // 2 cp, 2 cp + 1), B row of output row r and tap: r + tap * dil (IN row; conv1 reads A rows up
+  // to 16 * 18 - 1 + 2 hk D < SMEM / 256 (the second half's 9th block, past the 17, is computed
+  // and dropped: a branch there splits the MFMA stream), conv2 T rows up to 255 + 2 hk < 272)
+  auto conv = [&](auto nb_tag, const bf16 *wp, int IN, int b0, int dil,
+                  f32x4 (&acc)[2][decltype(nb_tag)::value]) __attribute__((always_inline)) {
     constexpr int NB = decltype(nb_tag)::value;
     const rsrc_t wr = make_rsrc(wp, (uint32_t)(K * kPrC * kPrC * 2));
 #pragma unroll
-    for (int b = 0; b < NB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 wf[4];
-    auto wload = [&](int s, bf16x8 &f) __attribute__((always_inline)) {
-      f = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wr, (uint32_t)lane * 16u,
-                                                                           (uint32_t)((s * 8 + w) * 1024), 0));
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) acc[j][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 wf[4][2];
+    auto wload = [&](int s, bf16x8 (&f)[2]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        f[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                              wr, (uint32_t)lane * 16u, (uint32_t)((s * 8 + 2 * cp + j) * 1024), 0));
     };
     wload(0, wf[0]);
     wload(1, wf[1]);
@@ -426,13 +440,13 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
         const int s = tap * 4 + kc;
         if (s + 3 < 4 * K) {
           wload(s + 3, wf[(kc + 3) & 3]);
-          asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        // row 16 b + r16 + sh: the rotation (c + 2 row) & 15 does not depend on b, so every block's
-        // read is one base + an immediate 4 KiB * b
-        const int R0 = r16 + sh;
+        // row 16 (b0 + b) + r16 + sh: the rotation (c + 2 row) & 15 does not depend on b, so every
+        // block's read is one base + an immediate 4 KiB * b
+        const int R0 = 16 * b0 + r16 + sh;
         const char *base = smem + IN + R0 * 256 + pr_phys(R0, 4 * kc + g) * 16;
         bf16x8 fb[NB];
 #pragma unroll
@@ -441,61 +455,76 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
         // the LDS latency on every MFMA)
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kc], fb[b], acc[b], 0, 0, 0);
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[j][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kc][j], fb[b], acc[j][b], 0, 0, 0);
       }
     }
   };
 
-  const int ch = 16 * w + 4 * g;  // this lane's 4 output channels
   {
-    f32x4 acc[kPrNBT];
-    conv(std::integral_constant<int, kPrNBT>{}, p.w1, A_OFF, D, acc);
-    const float4 bb = *reinterpret_cast<const float4 *>(p.b1 + ch);
-    // T row r = sample t0 - HK + r
+    constexpr int NB1 = (kPrNBT + 1) / 2;  // 9
+    f32x4 acc[2][NB1];
+    conv(std::integral_constant<int, NB1>{}, p.w1, A_OFF, NB1 * rh, D, acc);
 #pragma unroll
-    for (int b = 0; b < kPrNBT; ++b) {
-      const int R = 16 * b + r16, s = t0 - HK + R;
-      // zero padding of conv2's input as a multiply (a select here became a branch per element;
-      // rows that see stale LDS are never read)
-      const float m = (unsigned)s < (unsigned)T ? 1.f : 0.f;
-      bf16x4 t;
-      t[0] = (bf16)(lrelu(acc[b][0] + bb.x, 0.1f) * m);
-      t[1] = (bf16)(lrelu(acc[b][1] + bb.y, 0.1f) * m);
-      t[2] = (bf16)(lrelu(acc[b][2] + bb.z, 0.1f) * m);
-      t[3] = (bf16)(lrelu(acc[b][3] + bb.w, 0.1f) * m);
-      *reinterpret_cast<bf16x4 *>(smem + T_OFF + R * 256 + pr_phys(R, ch >> 3) * 16 + (ch & 7) * 2) = t;
+    for (int j = 0; j < 2; ++j) {
+      const int ch = 32 * cp + 16 * j + 4 * g;
+      const float4 bb = *reinterpret_cast<const float4 *>(p.b1 + ch);
+      // T row r = sample t0 - HK + r
+#pragma unroll
+      for (int b = 0; b < NB1; ++b) {
+        const int blk = NB1 * rh + b;
+        if (blk < kPrNBT) {  // wave-uniform
+          const int R = 16 * blk + r16, s = t0 - HK + R;
+          // zero padding of conv2's input as a multiply (a select here became a branch per
+          // element; rows that see stale LDS are never read)
+          const float m = (unsigned)s < (unsigned)T ? 1.f : 0.f;
+          bf16x4 t;
+          t[0] = (bf16)(lrelu(acc[j][b][0] + bb.x, 0.1f) * m);
+          t[1] = (bf16)(lrelu(acc[j][b][1] + bb.y, 0.1f) * m);
+          t[2] = (bf16)(lrelu(acc[j][b][2] + bb.z, 0.1f) * m);
+          t[3] = (bf16)(lrelu(acc[j][b][3] + bb.w, 0.1f) * m);
+          *reinterpret_cast<bf16x4 *>(smem + T_OFF + R * 256 + pr_phys(R, ch >> 3) * 16 + (ch & 7) * 2) = t;
+        }
+      }
     }
   }
   __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
   __builtin_amdgcn_s_barrier();
 
-  f32x4 acc[16];
-  conv(std::integral_constant<int, 16>{}, p.w2, T_OFF, 1, acc);
+  f32x4 acc[2][8];
+  conv(std::integral_constant<int, 8>{}, p.w2, T_OFF, 8 * rh, 1, acc);
   // the running sum (first in the load queue after conv2's last weight wait)
-  bf16x4 xs[16];
+  bf16x4 xs[2][8];
   if (p.xs != nullptr) {
     const rsrc_t sr = make_rsrc(p.xs, p.x_bytes);
 #pragma unroll
-    for (int b = 0; b < 16; ++b) {
-      const int s = t0 + 16 * b + r16;
-      const uint32_t off = s < T ? (uint32_t)((ubase + s) * 256 + ch * 2) : kOOB;
-      xs[b] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(sr, off, 0, 0));
+    for (int b = 0; b < 8; ++b) {
+      const int s = t0 + 16 * (8 * rh + b) + r16;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t off = s < T ? (uint32_t)((ubase + s) * 256 + (32 * cp + 16 * j + 4 * g) * 2) : kOOB;
+        xs[j][b] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(sr, off, 0, 0));
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
   __builtin_amdgcn_s_barrier();  // every wave done reading T: its rows 0 .. 255 become the output stage
-  {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ch = 32 * cp + 16 * j + 4 * g;
     const float4 bb = *reinterpret_cast<const float4 *>(p.b2 + ch);
     const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-    for (int b = 0; b < 16; ++b) {
-      const int R = 16 * b + r16;
+    for (int b = 0; b < 8; ++b) {
+      const int R = 16 * (8 * rh + b) + r16;
       bf16x4 o;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v = acc[b][i] + bv[i] + (float)res[b][i];
-        if (p.xs != nullptr) v += (float)xs[b][i];
+        float v = acc[j][b][i] + bv[i] + (float)res[j][b][i];
+        if (p.xs != nullptr) v += (float)xs[j][b][i];
         o[i] = (bf16)(p.out_act ? lrelu(v * p.out_scale, p.out_slope) : v);
       }
       *reinterpret_cast<bf16x4 *>(smem + T_OFF + R * 256 + pr_phys(R, ch >> 3) * 16 + (ch & 7) * 2) = o;
