@@ -38,13 +38,14 @@ from . import ops
 from . import runtime as R
 
 
-def _spin_until_landed(meta_host, budget_s=0.05):
-    """Poll the pinned meta vector until its first entry leaves -1 (the device->host copy landed),
-    for at most budget_s (the caller's stream synchronize covers the rest)."""
+def _spin_until_landed(meta_np, budget_s=0.05):
+    """Poll the pinned meta vector (a numpy view of it: an element read is ~0.1 us where a tensor
+    index + int() is several) until its first entry leaves -1 (the device->host copy landed), for
+    at most budget_s (the caller's stream synchronize covers the rest)."""
     import time
 
     t_end = time.perf_counter() + budget_s
-    while int(meta_host[0]) == -1 and time.perf_counter() < t_end:
+    while meta_np[0] == -1 and time.perf_counter() < t_end:
         pass
 
 
@@ -96,6 +97,10 @@ class SynthGraphs:
             src_masks = torch.empty(s["texts"].shape[0], Lx, device=s["texts"].device, dtype=torch.bool)
             g.mask_out = (src_masks, None, None)
         st = R._stage1(P, va, g, p_c, d_c)
+        if R.packed_stage2_ok(P, st, st.x) and R.lr_proj_ok(P, st.x):
+            # the decoder's first Q|K|V on the phoneme rows does not depend on T: it runs here,
+            # under the host read, instead of opening stage 2
+            st.xw = R.phoneme_qkv0(P, st.x)
         if src_masks is None:
             src_masks = R._mask(s["src_lens"], Lx)
         return g, st, src_masks, R.meta_vector(st.mel_len, s["texts"].device)
@@ -142,7 +147,7 @@ class SynthGraphs:
             graph, (g, st, src_masks, meta) = self._capture(lambda: self._stage1_body(P, va, static, Lx, controls))
             meta_host = torch.empty(meta.shape, dtype=meta.dtype, pin_memory=True)
             e1 = self._g1[key1] = SimpleNamespace(graph=graph, static=static, g=g, st=st, src_masks=src_masks,
-                                                  meta=meta, meta_host=meta_host, P=P)
+                                                  meta=meta, meta_host=meta_host, meta_np=meta_host.numpy(), P=P)
             while len(self._g1) > self.max_stage1:
                 self._drop_stage1(next(iter(self._g1)))
         else:
@@ -154,12 +159,12 @@ class SynthGraphs:
         # the host set to -1; spinning on it returns as soon as the bytes land (a blocking stream
         # synchronize parks the thread and the wake-up cost ~30-60 us per call); the synchronize
         # after it then returns at once and orders the rest of the copy
-        e1.meta_host[0] = -1
+        e1.meta_np[0] = -1
         e1.meta_host.copy_(e1.meta, non_blocking=True)
-        _spin_until_landed(e1.meta_host)
+        _spin_until_landed(e1.meta_np)
         torch.cuda.current_stream(dev).synchronize()
         R.HOST_READS[0] += 1
-        T_out, sum_len = R.check_meta(e1.meta_host, dev)
+        T_out, sum_len = R.check_meta(e1.meta_np, dev)
         pn_valid = R.postnet_valid_rows(B, T_out, sum_len)
         st = e1.st
         packed = R.packed_stage2_ok(P, st, st.x)
@@ -177,15 +182,26 @@ class SynthGraphs:
             del self._g2[key2]
             e2 = None
         if e2 is None:
-            if packed:
+            graph_b = None
+            if packed and R.split_stage2_ok(P):
+                # two graphs: the LR launch + the first decoder block, then the other blocks. The
+                # first replays (its outputs are the second's inputs: the second's warm-up run
+                # reads them), then the second is captured
+                graph, (x1, lay1, qkv1) = self._capture(lambda: R.decode_packed_head(P, st, st.x, st.mel_len, T_b,
+                                                                                   sum_len))
+                graph.replay()
+                graph_b, x_dec = self._capture(lambda: R.decode_packed_rest(P, x1, lay1, qkv1))
+                outs = (x_dec, lay1)
+            elif packed:
                 def body():
                     return R.decode_packed(P, st, st.x, st.mel_len, T_b, sum_len)
+                graph, outs = self._capture(body)
             else:
                 def body():
                     mel, post, st2 = R._stage2(P, e1.g, st, T_out, T_out, controls[0], pn_valid, sum_len)
                     return mel, post, R._mask(st2.mel_len, T_out)
-            graph, outs = self._capture(body)
-            e2 = self._g2[key2] = SimpleNamespace(graph=graph, outs=outs, e1=e1)
+                graph, outs = self._capture(body)
+            e2 = self._g2[key2] = SimpleNamespace(graph=graph, graph_b=graph_b, outs=outs, e1=e1)
             while len(self._g2) > self.max_stage2:
                 self._g2.popitem(last=False)
         else:
@@ -199,6 +215,8 @@ class SynthGraphs:
             # the caller's stream waits for the copies before anything later on it (the returned
             # tensors' users, the next call's stage-1 replay)
             e2.graph.replay()
+            if e2.graph_b is not None:
+                e2.graph_b.replay()
             side = self._side_stream(dev)
             with torch.cuda.stream(side):
                 outs = [torch.empty_like(t) for t in srcs]

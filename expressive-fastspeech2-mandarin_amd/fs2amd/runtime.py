@@ -326,20 +326,24 @@ def ffn_fused_ok(P, lp, h, layout):
     return -(-rows // tr) * ns >= FFN_SPLIT_MIN_WG
 
 
-def _stack(P, layers, x, lens, layout=None, timed=False, addvecs=(None, None), qkv0=None):
+def _stack(P, layers, x, lens, layout=None, timed=False, addvecs=(None, None), qkv0=None, tail_next=None):
     """FFT-block stack; in fp8 mode each block hands the next one an fp8 copy of its output.
-    qkv0: the first block's Q|K|V projection, already computed (fs2_lr_fused_proj)."""
+    qkv0: the first block's Q|K|V projection, already computed (fs2_lr_fused_proj). tail_next: the
+    block after the last one: its Q|K|V comes from the last block's fused epilogue and (x, qkv) is
+    returned (SynthGraphs' split stage 2)."""
     _STACK[0] = "dec" if timed else "enc"
     x8 = None
     qkv = qkv0
     n = len(layers)
+    if tail_next is not None and tail_next.fp8 is not None:
+        raise NotImplementedError("_stack: tail_next with fp8 layers")
     for i, lp in enumerate(layers):
-        nxt = layers[i + 1] if i + 1 < n else None
+        nxt = layers[i + 1] if i + 1 < n else tail_next
         next_s = nxt.fp8.s_x if (nxt is not None and nxt.fp8 is not None and nxt.fp8.wqkv is not None) else None
         last = i == n - 1
         x, x8, qkv = fft_block(P, lp, x, lens, addvecs[0] if last else None, addvecs[1] if last else None,
                                timed=timed, layout=layout, x8=x8, next_s=next_s, qkv=qkv, nxt=nxt)
-    return x
+    return (x, qkv) if tail_next is not None else x
 
 
 def packed_decoder_ok(P):
@@ -619,14 +623,33 @@ def decode_packed(P, st, x, dec_lens, T_lay, rows_hint=None):
     (the packed rows, cu and row_pos are those of the valid frames; only the padded-row maps and
     the grids' early-exiting tails grow with it): fs2amd.graphs.SynthGraphs captures this part per
     T bucket. Returns (packed x [B*T_lay, d_model], layout)."""
+    x, lay, qkv0 = _lr_packed(P, st, x, dec_lens, T_lay, rows_hint)
+    return _stack(P, P.dec_layers, x, None, layout=lay, timed=True, qkv0=qkv0), lay
+
+
+def decode_packed_head(P, st, x, dec_lens, T_lay, rows_hint=None):
+    """decode_packed's LengthRegulator launch and first decoder block, whose fused epilogue also
+    projects the second block's Q|K|V: returns (x1, layout, qkv1). With :func:`decode_packed_rest`
+    the same launches in the same order (SynthGraphs captures the two as separate graphs: the
+    small first one starts the GPU sooner after the host read)."""
+    x, lay, qkv0 = _lr_packed(P, st, x, dec_lens, T_lay, rows_hint)
+    x1, qkv1 = _stack(P, P.dec_layers[:1], x, None, layout=lay, timed=True, qkv0=qkv0, tail_next=P.dec_layers[1])
+    return x1, lay, qkv1
+
+
+def decode_packed_rest(P, x1, lay, qkv1):
+    return _stack(P, P.dec_layers[1:], x1, None, layout=lay, timed=True, qkv0=qkv1)
+
+
+def _lr_packed(P, st, x, dec_lens, T_lay, rows_hint=None):
+    """The LengthRegulator part of decode_packed: (packed x, layout, first block's Q|K|V or None)."""
     qkv0 = None
     if lr_fused_ok(x):
         proj = None
         if lr_proj_ok(P, x):
-            lp = P.dec_layers[0]
-            with _Timed("dec:qkv0"):  # x W^T on the phoneme rows (Models.py:145-152 input, linearity)
-                xw = ops.conv1d(x, lp.wqkv, None, cin=x.shape[-1], ks=1, pad=0, compute=P.compute,
-                                epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+            xw = getattr(st, "xw", None)  # SynthGraphs: already run at the end of stage 1
+            if xw is None:
+                xw = phoneme_qkv0(P, x)
             proj = (xw.view(-1, xw.shape[-1]), _qkv_pe(P, T_lay))
         # scan (teacher-forced) + packed layout + gather (+ PE) (+ the first Q|K|V) in one launch
         with _Timed("va:lr"):
@@ -647,7 +670,25 @@ def decode_packed(P, st, x, dec_lens, T_lay, rows_hint=None):
     # active rows when known on the host (free-running), rounded up (ops.rows_bucket) so that
     # a captured stage-2 graph serves every batch of the bucket
     lay.rows_hint = None if rows_hint is None else ops.rows_bucket(rows_hint, lay.capacity)
-    return _stack(P, P.dec_layers, x, None, layout=lay, timed=True, qkv0=qkv0), lay
+    return x, lay, qkv0
+
+
+def phoneme_qkv0(P, x):
+    """x W^T of the decoder's first Q|K|V on the phoneme rows (Models.py:145-152 input; the LR
+    launch adds the per-position pe W^T + b by linearity), f32."""
+    lp = P.dec_layers[0]
+    with _Timed("dec:qkv0"):
+        return ops.conv1d(x, lp.wqkv, None, cin=x.shape[-1], ks=1, pad=0, compute=P.compute, epilogue=L.EPI_BIAS,
+                          out_dtype=L.FS2_F32)
+
+
+def split_stage2_ok(P):
+    """SynthGraphs' stage 2 as two graphs (the first block, then the rest), opt-in
+    (FS2_SYNTH_SPLIT=1): measured 1.351 ms per free-running call against 1.299 ms as one graph
+    (profiles/r5s1) -- the gap after the host read is not the graph's size, and the second
+    launch adds its own."""
+    return (os.environ.get("FS2_SYNTH_SPLIT", "0") == "1" and len(P.dec_layers) >= 2
+            and all(lp.fp8 is None for lp in P.dec_layers))
 
 
 def mel_postnet(P, x, lay, dec_lens, postnet_valid=False, rows_hint=None):
@@ -803,15 +844,17 @@ def host_meta(mel_len, dev):
         HOST_READS[0] += 1
         return check_meta(meta.cpu(), dev)
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)  # per stream: reentrant across threads
-    host = _META_HOST.get(key)
-    if host is None or host.shape != meta.shape:
-        host = _META_HOST[key] = torch.empty(meta.shape, dtype=meta.dtype, pin_memory=True)
-    host[0] = -1
+    ent = _META_HOST.get(key)
+    if ent is None or ent[0].shape != meta.shape:
+        host = torch.empty(meta.shape, dtype=meta.dtype, pin_memory=True)
+        ent = _META_HOST[key] = (host, host.numpy())  # numpy view: cheap element reads while polling
+    host, host_np = ent
+    host_np[0] = -1
     host.copy_(meta, non_blocking=True)
-    _spin_until_landed(host)
+    _spin_until_landed(host_np)
     torch.cuda.current_stream(dev).synchronize()
     HOST_READS[0] += 1
-    return check_meta(host.clone(), dev)
+    return check_meta(host_np.copy(), dev)
 
 
 def postnet_valid_rows(B, T, sum_len):

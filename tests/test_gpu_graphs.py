@@ -132,7 +132,8 @@ def test_weight_change_recaptures_both_stages(model, prec):
             n = synth.captures
             w.mul_(1.25)  # decoder-only change: T_out and the stage-2 key stay the same
             _same(synth(**b), model(**b))
-            assert synth.captures == n + 2, (synth.captures, n)
+            # every graph of the first call recaptured (stage 1 + stage 2's one or two graphs)
+            assert synth.captures == 2 * n, (synth.captures, n)
     finally:
         with torch.no_grad():
             w.copy_(saved)
