@@ -330,71 +330,90 @@ __global__ __launch_bounds__(64 * NW) void mrf_kernel(MrfArgs p) {
 // 16-byte chunk rotated by 2 * row (phys = (c + 2 r) & 15): the ds_read_b128 lane groups
 // {0-3,12-15,20-27}, ... hit 16 distinct slots for every row shift (the bank behaviour of a
 // 288-byte pitch, without its padding), and a 1 KiB LDS-DMA piece stays 4 whole rows.
-constexpr int kPrL = 256;   // output samples per workgroup
-constexpr int kPrC = 128;   // channels
-constexpr int kPrNW = 8;    // waves
-constexpr int kPrNBT = 17;  // conv1 output row blocks (>= (L + 2 hk) / 16 for k <= 11)
+constexpr int kPrNW = 8;  // waves
+
+// per channel count: C = 128 (256-sample tiles, 256-byte rows, chunk rotated by 2 r) or C = 64
+// (512-sample tiles, 128-byte rows, chunk rotated by r: the same ds_read_b128 lane-group check,
+// two rows per 256-byte bank row)
+template <int C>
+struct PairCfg {
+  static constexpr int L = C == 128 ? 256 : 512;  // output samples per workgroup
+  static constexpr int RB = 2 * C;                // row bytes
+  static constexpr int NCK = C / 8;               // 16-byte chunks per row
+  static constexpr int NBT = L / 16 + 1;          // conv1 output row blocks (>= (L + 2 hk) / 16, k <= 11)
+  static constexpr int NCP = C / 32;              // channel pairs (two 16-channel MFMA blocks each)
+  static constexpr int NRG = kPrNW / NCP;         // row groups
+  static constexpr int NB1 = (NBT + NRG - 1) / NRG;  // conv1 blocks per wave (the last group's extras dropped)
+  static constexpr int NB2 = L / 16 / NRG;        // conv2 blocks per wave
+  static constexpr int KC = C / 32;               // k-steps per tap
+  __device__ static __forceinline__ int phys(int r, int c) {
+    return C == 128 ? (c + 2 * r) & 15 : (c + r) & 7;
+  }
+};
 
 struct PairArgs {
-  const bf16 *x;        // [B, T, 128] pair input (residual; conv1 reads lrelu(x))
-  const bf16 *w1, *w2;  // pack_wconv_tail fragment order, [k * 4 k-steps][8 blocks][64][8]
-  const float *b1, *b2; // [128]
+  const bf16 *x;        // [B, T, C] pair input (residual; conv1 reads lrelu(x))
+  const bf16 *w1, *w2;  // pack_wconv_tail fragment order, [k * C/32 k-steps][C/16 blocks][64][8]
+  const float *b1, *b2; // [C]
   const bf16 *xs;       // optional running sum (may alias out)
-  bf16 *out;            // [B, T, 128]
+  bf16 *out;            // [B, T, C]
   int T, D;             // samples per utterance, conv1 dilation
   float out_scale, out_slope;
   int out_act;          // 0: out = y; 1: out = lrelu(y * out_scale, out_slope)
   uint32_t x_bytes;
 };
 
-__device__ __forceinline__ int pr_phys(int r, int c) { return (c + 2 * r) & 15; }
-
-template <int K>
+template <int C, int K>
 __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
+  using Q = PairCfg<C>;
+  constexpr int L = Q::L, RB = Q::RB, NCK = Q::NCK, NBT = Q::NBT, NB1 = Q::NB1, NB2 = Q::NB2, KC = Q::KC;
   constexpr int HK = (K - 1) / 2;
-  // A rows: L + 2 hk (D + 1) <= L + 12 hk (D <= 5), + 16 rows that conv1's unused output rows
-  // (T rows >= L + 2 hk) read past the end (stale data there reaches only those rows)
-  constexpr int RA_MAX = kPrL + 12 * HK + 16;
-  constexpr int A_OFF = 0, T_OFF = RA_MAX * 256;
-  constexpr int SMEM = T_OFF + kPrNBT * 16 * 256;
+  // A rows: L + 2 hk (D + 1) <= L + 12 hk (D <= 5), rounded to whole 1 KiB pieces, + the rows the
+  // dropped conv1 blocks and the unused output rows (>= L + 2 hk) read past them (stale data there
+  // reaches only those rows)
+  constexpr int RPP = 1024 / RB;  // rows per DMA piece
+  constexpr int RA_MAX = L + 12 * HK + RPP + 16 * (NB1 * Q::NRG - NBT) + 16;
+  constexpr int A_OFF = 0, T_OFF = RA_MAX * RB;
+  constexpr int SMEM = T_OFF + NBT * 16 * RB;
   static_assert(SMEM <= 163840, "LDS");
-  static_assert(kPrL + 2 * HK <= kPrNBT * 16, "conv1 rows");
+  static_assert(L + 2 * HK <= NBT * 16, "conv1 rows");
+  static_assert(16 * NB2 * Q::NRG == L, "conv2 rows");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, g = lane >> 4;
   const int T = p.T, D = p.D;
-  const int t0 = blockIdx.x * kPrL;
+  const int t0 = blockIdx.x * L;
   const int64_t ubase = (int64_t)blockIdx.y * T;
   const int HA = HK * (D + 1);         // A halo
-  const int RA = kPrL + 2 * HA;        // A rows of this launch (multiple of 4)
+  const int RA = L + 2 * HA;           // A rows of this launch
   const int a0 = t0 - HA;              // sample of A row 0
   const rsrc_t xr = make_rsrc(p.x, p.x_bytes);
 
-  // ---- A <- x over [a0, a0 + RA) by LDS-DMA (rows outside [0, T) read as zeros)
-  const int npc = RA / 4;  // 1 KiB pieces
+  // ---- A <- x over [a0, a0 + RA) (whole pieces) by LDS-DMA (rows outside [0, T) read as zeros)
+  const int npc = (RA + RPP - 1) / RPP;  // 1 KiB pieces
   for (int pc = w; pc < npc; pc += kPrNW) {
-    const int R = 4 * pc + (lane >> 4), ph = lane & 15;
-    const int c = (ph - 2 * R) & 15, s = a0 + R;
-    const uint32_t off = (unsigned)s < (unsigned)T ? (uint32_t)((ubase + s) * 256 + c * 16) : kOOB;
+    const int R = RPP * pc + lane / NCK, ph = lane % NCK;
+    const int c = C == 128 ? (ph - 2 * R) & 15 : (ph - R) & 7, s = a0 + R;
+    const uint32_t off = (unsigned)s < (unsigned)T ? (uint32_t)((ubase + s) * RB + c * 16) : kOOB;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void *)(smem + A_OFF + pc * 1024),
                                              16, off, 0, 0, 0);
   }
-  // wave w: output channels 32 cp .. 32 cp + 31 (cp = w & 3: two 16-channel MFMA blocks) of row
-  // half rh = w >> 2 (conv1 blocks 9 rh .. 9 rh + 8, conv2 blocks 8 rh .. 8 rh + 7): every B
-  // fragment read from LDS feeds two MFMAs (one wave per 16 channels over all rows read 136 KiB
-  // of LDS per k-step per CU, as many LDS cycles as MFMA cycles)
-  const int cp = w & 3, rh = w >> 2;
-  // the residual x of this wave's conv2 output (rows t0 + 16 (8 rh + b) + r16, channels
+  // wave w: output channels 32 cp .. 32 cp + 31 (two 16-channel MFMA blocks) of row group rg:
+  // conv1 blocks NB1 rg .. +NB1-1, conv2 blocks NB2 rg .. +NB2-1. Every B fragment read from LDS
+  // feeds two MFMAs (one wave per 16 channels over every row block read as many LDS cycles per
+  // k-step as the MFMAs took)
+  const int cp = w % Q::NCP, rg = w / Q::NCP;
+  // the residual x of this wave's conv2 output (rows t0 + 16 (NB2 rg + b) + r16, channels
   // 32 cp + 16 j + 4 g .. +3)
-  bf16x4 res[2][8];
+  bf16x4 res[2][NB2];
 #pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    const int s = t0 + 16 * (8 * rh + b) + r16;
+  for (int b = 0; b < NB2; ++b) {
+    const int s = t0 + 16 * (NB2 * rg + b) + r16;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const uint32_t off = s < T ? (uint32_t)((ubase + s) * 256 + (32 * cp + 16 * j + 4 * g) * 2) : kOOB;
+      const uint32_t off = s < T ? (uint32_t)((ubase + s) * RB + (32 * cp + 16 * j + 4 * g) * 2) : kOOB;
       res[j][b] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
     }
   }
@@ -410,14 +429,15 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
   __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
   __builtin_amdgcn_s_barrier();
 
-  // ---- one conv: NB row blocks from block b0 of IN, k-step s = tap * 4 + kc, weights wp (blocks
-  // 2 cp, 2 cp + 1), B row of output row r and tap: r + tap * dil (IN row; conv1 reads A rows up
-  // to 16 * 18 - 1 + 2 hk D < SMEM / 256 (the second half's 9th block, past the 17, is computed
-  // and dropped: a branch there splits the MFMA stream), conv2 T rows up to 255 + 2 hk < 272)
+  // ---- one conv: NB row blocks from block b0 of IN, k-step s = tap * KC + kc, weights wp (blocks
+  // 2 cp, 2 cp + 1), B row of output row r and tap: r + tap * dil (IN row; inside the A / T
+  // regions by RA_MAX / NBT). A 4-slot register ring of weight pairs, loads 3 k-steps ahead: at
+  // KC = 2 the tap loop walks tap pairs so every slot stays a constant.
   auto conv = [&](auto nb_tag, const bf16 *wp, int IN, int b0, int dil,
                   f32x4 (&acc)[2][decltype(nb_tag)::value]) __attribute__((always_inline)) {
     constexpr int NB = decltype(nb_tag)::value;
-    const rsrc_t wr = make_rsrc(wp, (uint32_t)(K * kPrC * kPrC * 2));
+    constexpr int NKS = K * KC;
+    const rsrc_t wr = make_rsrc(wp, (uint32_t)(K * C * C * 2));
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -427,46 +447,65 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         f[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                              wr, (uint32_t)lane * 16u, (uint32_t)((s * 8 + 2 * cp + j) * 1024), 0));
+                                              wr, (uint32_t)lane * 16u, (uint32_t)((s * (C / 16) + 2 * cp + j) * 1024), 0));
     };
+    // k-step s (ring slot SL = s & 3) of tap `tap`, channel step kc
+    auto kstep = [&](auto sl_tag, int s, int tap, int kc) __attribute__((always_inline)) {
+      constexpr int SL = decltype(sl_tag)::value;
+      if (s + 3 < NKS) {
+        wload(s + 3, wf[(SL + 3) & 3]);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      // row 16 (b0 + b) + r16 + sh: the chunk rotation does not depend on b (16 rows shift it by
+      // a multiple of the row's chunk count), so every block's read is one base + an immediate
+      const int R0 = 16 * b0 + r16 + tap * dil;
+      const char *base = smem + IN + R0 * RB + Q::phys(R0, 4 * kc + g) * 16;
+      bf16x8 fb[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) fb[b] = *reinterpret_cast<const bf16x8 *>(base + b * 16 * RB);
+      // all reads issued before the first MFMA (interleaved read -> wait -> MFMA pairs exposed
+      // the LDS latency on every MFMA)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[j][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[SL][j], fb[b], acc[j][b], 0, 0, 0);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
     wload(0, wf[0]);
     wload(1, wf[1]);
     wload(2, wf[2]);
+    if constexpr (KC == 4) {
 #pragma nounroll
-    for (int tap = 0; tap < K; ++tap) {
-      const int sh = tap * dil;
-#pragma unroll
-      for (int kc = 0; kc < 4; ++kc) {
-        const int s = tap * 4 + kc;
-        if (s + 3 < 4 * K) {
-          wload(s + 3, wf[(kc + 3) & 3]);
-          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        // row 16 (b0 + b) + r16 + sh: the rotation (c + 2 row) & 15 does not depend on b, so every
-        // block's read is one base + an immediate 4 KiB * b
-        const int R0 = 16 * b0 + r16 + sh;
-        const char *base = smem + IN + R0 * 256 + pr_phys(R0, 4 * kc + g) * 16;
-        bf16x8 fb[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) fb[b] = *reinterpret_cast<const bf16x8 *>(base + b * 4096);
-        // all reads issued before the first MFMA (interleaved read -> wait -> MFMA pairs exposed
-        // the LDS latency on every MFMA)
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[j][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kc][j], fb[b], acc[j][b], 0, 0, 0);
+      for (int tap = 0; tap < K; ++tap) {
+        kstep(I0{}, 4 * tap, tap, 0);
+        kstep(I1{}, 4 * tap + 1, tap, 1);
+        kstep(I2{}, 4 * tap + 2, tap, 2);
+        kstep(I3{}, 4 * tap + 3, tap, 3);
       }
+    } else {
+      static_assert(KC == 2 && (K & 1), "tap pairs + one tap");
+#pragma nounroll
+      for (int tap = 0; tap + 1 < K; tap += 2) {
+        kstep(I0{}, 2 * tap, tap, 0);
+        kstep(I1{}, 2 * tap + 1, tap, 1);
+        kstep(I2{}, 2 * tap + 2, tap + 1, 0);
+        kstep(I3{}, 2 * tap + 3, tap + 1, 1);
+      }
+      kstep(I0{}, 2 * (K - 1), K - 1, 0);
+      kstep(I1{}, 2 * (K - 1) + 1, K - 1, 1);
     }
   };
 
   {
-    constexpr int NB1 = (kPrNBT + 1) / 2;  // 9
     f32x4 acc[2][NB1];
-    conv(std::integral_constant<int, NB1>{}, p.w1, A_OFF, NB1 * rh, D, acc);
+    conv(std::integral_constant<int, NB1>{}, p.w1, A_OFF, NB1 * rg, D, acc);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int ch = 32 * cp + 16 * j + 4 * g;
@@ -474,8 +513,8 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
       // T row r = sample t0 - HK + r
 #pragma unroll
       for (int b = 0; b < NB1; ++b) {
-        const int blk = NB1 * rh + b;
-        if (blk < kPrNBT) {  // wave-uniform
+        const int blk = NB1 * rg + b;
+        if (blk < NBT) {  // wave-uniform
           const int R = 16 * blk + r16, s = t0 - HK + R;
           // zero padding of conv2's input as a multiply (a select here became a branch per
           // element; rows that see stale LDS are never read)
@@ -485,7 +524,7 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
           t[1] = (bf16)(lrelu(acc[j][b][1] + bb.y, 0.1f) * m);
           t[2] = (bf16)(lrelu(acc[j][b][2] + bb.z, 0.1f) * m);
           t[3] = (bf16)(lrelu(acc[j][b][3] + bb.w, 0.1f) * m);
-          *reinterpret_cast<bf16x4 *>(smem + T_OFF + R * 256 + pr_phys(R, ch >> 3) * 16 + (ch & 7) * 2) = t;
+          *reinterpret_cast<bf16x4 *>(smem + T_OFF + R * RB + Q::phys(R, ch >> 3) * 16 + (ch & 7) * 2) = t;
         }
       }
     }
@@ -493,33 +532,33 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
   __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
   __builtin_amdgcn_s_barrier();
 
-  f32x4 acc[2][8];
-  conv(std::integral_constant<int, 8>{}, p.w2, T_OFF, 8 * rh, 1, acc);
+  f32x4 acc[2][NB2];
+  conv(std::integral_constant<int, NB2>{}, p.w2, T_OFF, NB2 * rg, 1, acc);
   // the running sum (first in the load queue after conv2's last weight wait)
-  bf16x4 xs[2][8];
+  bf16x4 xs[2][NB2];
   if (p.xs != nullptr) {
     const rsrc_t sr = make_rsrc(p.xs, p.x_bytes);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const int s = t0 + 16 * (8 * rh + b) + r16;
+    for (int b = 0; b < NB2; ++b) {
+      const int s = t0 + 16 * (NB2 * rg + b) + r16;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const uint32_t off = s < T ? (uint32_t)((ubase + s) * 256 + (32 * cp + 16 * j + 4 * g) * 2) : kOOB;
+        const uint32_t off = s < T ? (uint32_t)((ubase + s) * RB + (32 * cp + 16 * j + 4 * g) * 2) : kOOB;
         xs[j][b] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(sr, off, 0, 0));
       }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
-  __builtin_amdgcn_s_barrier();  // every wave done reading T: its rows 0 .. 255 become the output stage
+  __builtin_amdgcn_s_barrier();  // every wave done reading T: its rows 0 .. L - 1 become the output stage
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int ch = 32 * cp + 16 * j + 4 * g;
     const float4 bb = *reinterpret_cast<const float4 *>(p.b2 + ch);
     const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const int R = 16 * (8 * rh + b) + r16;
+    for (int b = 0; b < NB2; ++b) {
+      const int R = 16 * (NB2 * rg + b) + r16;
       bf16x4 o;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -527,20 +566,20 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
         if (p.xs != nullptr) v += (float)xs[j][b][i];
         o[i] = (bf16)(p.out_act ? lrelu(v * p.out_scale, p.out_slope) : v);
       }
-      *reinterpret_cast<bf16x4 *>(smem + T_OFF + R * 256 + pr_phys(R, ch >> 3) * 16 + (ch & 7) * 2) = o;
+      *reinterpret_cast<bf16x4 *>(smem + T_OFF + R * RB + Q::phys(R, ch >> 3) * 16 + (ch & 7) * 2) = o;
     }
   }
   __builtin_amdgcn_s_waitcnt(kMrfLgkm0);
   __builtin_amdgcn_s_barrier();
-  // whole 256-byte rows, 16 bytes a lane
+  // whole rows, 16 bytes a lane
   const rsrc_t orr = make_rsrc(p.out, p.x_bytes);
 #pragma unroll
-  for (int i = 0; i < kPrL * 16 / (64 * kPrNW); ++i) {
-    const int q = i * 64 * kPrNW + tid, R = q >> 4, c = q & 15, s = t0 + R;
-    const uint4 v = *reinterpret_cast<const uint4 *>(smem + T_OFF + R * 256 + pr_phys(R, c) * 16);
+  for (int i = 0; i < L * NCK / (64 * kPrNW); ++i) {
+    const int q = i * 64 * kPrNW + tid, R = q / NCK, c = q % NCK, s = t0 + R;
+    const uint4 v = *reinterpret_cast<const uint4 *>(smem + T_OFF + R * RB + Q::phys(R, c) * 16);
     if (s < T)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), orr,
-                                             (uint32_t)((ubase + s) * 256 + c * 16), 0, 0);
+                                             (uint32_t)((ubase + s) * RB + c * 16), 0, 0);
   }
 }
 
@@ -583,7 +622,8 @@ extern "C" int fs2_hifigan_pair(const void *x, const void *w1, const float *b1, 
                                 int out_act, void *out, fs2_stream_t stream) {
   if (x == nullptr || w1 == nullptr || b1 == nullptr || w2 == nullptr || b2 == nullptr || out == nullptr || B < 0 || T < 0)
     return FS2_EINVAL;
-  if (C != kPrC || !(ks == 3 || ks == 7 || ks == 11) || dilation < 1 || dilation > 5) return FS2_EUNSUPPORTED;
+  if (!(C == 128 || C == 64) || !(ks == 3 || ks == 7 || ks == 11) || dilation < 1 || dilation > 5)
+    return FS2_EUNSUPPORTED;
   if (out == x) return FS2_EINVAL;  // other tiles re-read the input's halo rows
   if (B == 0 || T == 0) return FS2_OK;
   const int64_t bytes = (int64_t)B * T * C * 2;
@@ -602,13 +642,20 @@ extern "C" int fs2_hifigan_pair(const void *x, const void *w1, const float *b1, 
   p.out_slope = out_slope;
   p.out_act = out_act ? 1 : 0;
   p.x_bytes = (uint32_t)bytes;
-  const dim3 grid((unsigned)((T + kPrL - 1) / kPrL), (unsigned)B);
-  if (ks == 3)
-    hipLaunchKernelGGL(pair_kernel<3>, grid, dim3(64 * kPrNW), 0, as_stream(stream), p);
-  else if (ks == 7)
-    hipLaunchKernelGGL(pair_kernel<7>, grid, dim3(64 * kPrNW), 0, as_stream(stream), p);
+  auto go = [&](auto CC) {
+    constexpr int CV = decltype(CC)::value;
+    const dim3 grid((unsigned)((T + PairCfg<CV>::L - 1) / PairCfg<CV>::L), (unsigned)B);
+    if (ks == 3)
+      hipLaunchKernelGGL((pair_kernel<CV, 3>), grid, dim3(64 * kPrNW), 0, as_stream(stream), p);
+    else if (ks == 7)
+      hipLaunchKernelGGL((pair_kernel<CV, 7>), grid, dim3(64 * kPrNW), 0, as_stream(stream), p);
+    else
+      hipLaunchKernelGGL((pair_kernel<CV, 11>), grid, dim3(64 * kPrNW), 0, as_stream(stream), p);
+  };
+  if (C == 128)
+    go(std::integral_constant<int, 128>{});
   else
-    hipLaunchKernelGGL(pair_kernel<11>, grid, dim3(64 * kPrNW), 0, as_stream(stream), p);
+    go(std::integral_constant<int, 64>{});
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

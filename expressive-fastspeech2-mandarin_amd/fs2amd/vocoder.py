@@ -178,16 +178,18 @@ class Generator(nn.Module):
                              "u": u, "cout": w.shape[0] // u})
         for rb in self.resblocks:
             P["rb"].append([(conv(c1), conv(c2)) for c1, c2 in zip(rb.convs1, rb.convs2)])
-        # the narrow stages' multi-receptive-field blocks as one fused launch each (fs2_hifigan_mrf)
+        # the narrow stages' multi-receptive-field blocks as one fused launch each (fs2_hifigan_mrf;
+        # the 32-channel stage, and the 64-channel one with FS2_VOC_PAIR64=0)
         P["mrf"] = {}
-        # the 128-channel stage: one fused launch per ResBlock1 dilation pair (fs2_hifigan_pair)
+        # the 128- and 64-channel stages: one fused launch per ResBlock1 dilation pair
+        # (fs2_hifigan_pair; 64 channels: 5.6 vs 7.3 ms for the stage as one MRF launch)
         P["pair"] = {}
         if c == L.FS2_BF16 and list(self.h.resblock_kernel_sizes) == [3, 7, 11] and \
                 all(list(d) == [1, 3, 5] for d in self.h.resblock_dilation_sizes) and str(self.h.resblock) == "1":
             nk = self.num_kernels
             for i in range(self.num_upsamples):
                 ch = self.h.upsample_initial_channel // (2 ** (i + 1))
-                if ch == 128:
+                if ch in (128, 64):
                     P["pair"][i] = [[(ops.pack_wconv_tail(_weight(c1).float().to(dev)), c1.bias.detach().float().to(dev),
                                       ops.pack_wconv_tail(_weight(c2).float().to(dev)), c2.bias.detach().float().to(dev),
                                       c1.kernel_size[0], c1.dilation[0])
@@ -263,7 +265,8 @@ class Generator(nn.Module):
             C = up["cout"]
             xu = torch.empty(B, T2, C, device=mel.device, dtype=dt)      # ups output (residual of pair 0)
             last_stage = i == len(P["ups"]) - 1
-            if i in P["pair"] and os.environ.get("FS2_VOC_PAIR", "1") != "0":
+            if i in P["pair"] and os.environ.get("FS2_VOC_PAIR", "1") != "0" and \
+                    (C == 128 or os.environ.get("FS2_VOC_PAIR64", "1") != "0"):
                 # one launch per dilation pair (leaky_relu of the pair input applied on chip)
                 run(h, up, L.EPI_BIAS, xu, T)
                 T = T2

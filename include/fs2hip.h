@@ -611,15 +611,15 @@ int fs2_hifigan_mrf(const void *x, const void *x_act, const void *w, const float
 int64_t fs2_hifigan_mrf_weight_elems(int C);
 
 /*
- * fs2_hifigan_pair — one ResBlock1 dilation pair at C = 128 (the second upsampling stage,
- * hifigan/models.py:34-45) in ONE launch:
+ * fs2_hifigan_pair — one ResBlock1 dilation pair at C = 128 or 64 (the second / third upsampling
+ * stage, hifigan/models.py:34-45) in ONE launch:
  *   y = conv2(lrelu(conv1_d(lrelu(x, 0.1)) + b1, 0.1)) + b2 + x (+ xs)
  *   out = y (out_act = 0) or lrelu(y * out_scale, out_slope) (out_act = 1: the stage's last pair,
  *   out_scale = 1 / num_kernels)
- * x bf16 [B, T, 128] (must not alias out); xs optional bf16 [B, T, 128] (the running
+ * x bf16 [B, T, C] (must not alias out); xs optional bf16 [B, T, C] (the running
  * multi-receptive-field sum; may alias out); ks in {3, 7, 11}, dilation 1..5 (conv1; conv2 has
- * dilation 1); w1 / w2 each ks * 128 * 128 bf16 in the fs2_hifigan_mrf per-conv layout
- * [ks * 4 k-steps][8 blocks][4 h][16 r][8 e]; b1 / b2 f32 [128]. Per-utterance zero padding at
+ * dilation 1); w1 / w2 each ks * C * C bf16 in the fs2_hifigan_mrf per-conv layout
+ * [ks * C/32 k-steps][C/16 blocks][4 h][16 r][8 e]; b1 / b2 f32 [C]. Per-utterance zero padding at
  * [0, T) for both convs. Replaces the pair's two fs2_conv1d launches and their t / lrelu(x)
  * round trips through HBM.
  */

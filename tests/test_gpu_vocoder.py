@@ -177,20 +177,22 @@ def test_hifigan_mrf_fused_stage(gen, C, T):
     assert float(err.max()) <= 3e-2 * scale and float(err.mean()) <= 2e-3 * scale, (float(err.max()), float(err.mean()), scale)
 
 
-@pytest.mark.parametrize("T,k,d,mode", [(1000, 11, 5, "plain"), (300, 7, 3, "xs"), (77, 3, 1, "last"),
-                                        (513, 11, 1, "last"), (256, 3, 5, "plain"), (40, 7, 5, "xs")])
-def test_hifigan_pair_matches_f64(T, k, d, mode):
-    """fs2_hifigan_pair (one ResBlock1 dilation pair at C = 128: lrelu, dilated conv, lrelu, conv,
-    residual, optionally + the running sum and the stage's closing leaky_relu, one launch; 256-sample
-    tiles, the dilated conv's halo on chip) against a float64 statement of hifigan/models.py:34-45 on
+@pytest.mark.parametrize("C,T,k,d,mode", [(128, 1000, 11, 5, "plain"), (128, 300, 7, 3, "xs"), (128, 77, 3, 1, "last"),
+                                          (128, 513, 11, 1, "last"), (128, 256, 3, 5, "plain"), (128, 40, 7, 5, "xs"),
+                                          (64, 1500, 11, 5, "xs"), (64, 600, 7, 3, "last"), (64, 512, 3, 1, "plain"),
+                                          (64, 90, 11, 5, "plain")])
+def test_hifigan_pair_matches_f64(C, T, k, d, mode):
+    """fs2_hifigan_pair (one ResBlock1 dilation pair at C = 128 / 64: lrelu, dilated conv, lrelu,
+    conv, residual, optionally + the running sum and the stage's closing leaky_relu, one launch;
+    256- / 512-sample tiles, the dilated conv's halo on chip) against a float64 statement of hifigan/models.py:34-45 on
     the same bf16 input and bf16-rounded weights, with the kernel's bf16 rounding points (lrelu(x)
     and the first conv's output stored as bf16): max |err| <= 2e-2 of the output scale, mean <=
     2e-3. Tile and utterance edges included (T not a multiple of 256, T < 256, dilation halo
     larger than the sequence)."""
     from fs2amd import ops
 
-    g = torch.Generator().manual_seed(T + 10 * k + d)
-    B, C = 3, 128
+    g = torch.Generator().manual_seed(T + 10 * k + d + C)
+    B = 3
     w1, w2 = (torch.randn(C, C, k, generator=g) / (C * k) ** 0.5 for _ in range(2))
     b1, b2 = (0.05 * torch.randn(C, generator=g) for _ in range(2))
     x = (0.5 * torch.randn(B, T, C, generator=g)).to(torch.bfloat16)
@@ -220,6 +222,25 @@ def test_hifigan_pair_matches_f64(T, k, d, mode):
     assert float(err.max()) <= 2e-2 * scale and float(err.mean()) <= 2e-3 * scale, (float(err.max()), float(err.mean()), scale)
 
 
+def test_hifigan_pair64_stage_matches_mrf(gen):
+    """The 64-channel stage on fs2_hifigan_pair (9 pair launches, the default) against the same
+    stage as one fs2_hifigan_mrf launch (FS2_VOC_PAIR64=0): same waveform within bf16 noise."""
+    g = torch.Generator().manual_seed(6)
+    mel = (torch.randn(2, 80, 41, generator=g) - 4.0).to(DEV)
+    gen.set_precision("bf16")
+    try:
+        assert 2 in gen.packed(torch.device(DEV))["pair"]  # the 64-channel stage
+        with torch.no_grad():
+            y1 = gen(mel).float().cpu()
+            os.environ["FS2_VOC_PAIR64"] = "0"
+            y0 = gen(mel).float().cpu()
+    finally:
+        os.environ.pop("FS2_VOC_PAIR64", None)
+        gen.set_precision("fp32")
+    snr = _snr_db(y0.numpy(), y1.numpy())
+    assert snr >= 30.0, snr
+
+
 def test_hifigan_pair_stage_matches_per_conv_path(gen):
     """The 128-channel stage on fs2_hifigan_pair (9 launches) against the same stage on the
     per-conv fs2_conv1d path (FS2_VOC_PAIR=0, 18 launches): same waveform within bf16 noise."""
@@ -229,7 +250,7 @@ def test_hifigan_pair_stage_matches_per_conv_path(gen):
     mel = (torch.randn(2, 80, 57, generator=g) - 4.0).to(DEV)
     gen.set_precision("bf16")
     try:
-        assert list(gen.packed(torch.device(DEV))["pair"]) == [1]  # the 128-channel stage
+        assert 1 in gen.packed(torch.device(DEV))["pair"]  # the 128-channel stage
         with torch.no_grad():
             y1 = gen(mel).float().cpu()
             os.environ["FS2_VOC_PAIR"] = "0"
