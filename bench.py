@@ -160,104 +160,6 @@ def forward_timers(model, batch, n_fwd=6):
     return [[(tag, a.elapsed_time(b) / 1e3) for a, b, tag in tms] for tms in per_fwd]
 
 
-class ExternalEvents:
-    """HIP timing events recorded with hipEventRecordWithFlags(..., hipEventRecordExternal): inside
-    a stream capture each record becomes an event node of the graph (a plain hipEventRecord there
-    only orders the capture), so launches can be timed inside graph replays. Events come from a
-    pool created before the capture; read with hipEventElapsedTime after a replay."""
-
-    def __init__(self):
-        import ctypes
-
-        self.ct = ctypes
-        self.hip = ctypes.CDLL("libamdhip64.so.7")  # the HIP runtime torch already mapped
-        self.hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
-        self.hip.hipEventRecordWithFlags.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
-        self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
-        self.hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
-        self.pool, self.used = [], 0
-
-    def reserve(self, n):
-        while len(self.pool) < n:
-            ev = self.ct.c_void_p()
-            if self.hip.hipEventCreateWithFlags(self.ct.byref(ev), 0) != 0:
-                raise RuntimeError("hipEventCreateWithFlags failed")
-            self.pool.append(ev)
-
-    def record(self):
-        if self.used >= len(self.pool):
-            raise RuntimeError("ExternalEvents: pool exhausted (reserve more before the capture)")
-        ev = self.pool[self.used]
-        self.used += 1
-        st = torch.cuda.current_stream().cuda_stream
-        rc = self.hip.hipEventRecordWithFlags(ev, self.ct.c_void_p(st), 1)  # hipEventRecordExternal
-        if rc != 0:
-            self.hip.hipGetLastError()  # clear the sticky error: later launches check it
-            raise RuntimeError(f"hipEventRecordWithFlags failed: hipError {rc}")
-        return ev
-
-    def elapsed_s(self, a, b):
-        ms = self.ct.c_float()
-        rc = self.hip.hipEventElapsedTime(self.ct.byref(ms), a, b)
-        if rc != 0:
-            self.hip.hipGetLastError()
-            raise RuntimeError(f"hipEventElapsedTime failed: hipError {rc}")
-        return ms.value / 1e3
-
-    def close(self):
-        for ev in self.pool:
-            self.hip.hipEventDestroy(ev)
-        self.pool = []
-
-
-def forward_timers_graph(model, batch, n_replay=8):
-    """The forward captured ONCE as a HIP graph with an external event node before and after every
-    launch of interest (runtime.TIMERS / TIMER_RECORD), replayed n_replay times; returns [(tag,
-    seconds)] per replay. Each pair brackets the kernel plus the event node's packet processing
-    (~1-2 us), with no host in the loop: the graph-replay form of forward_timers."""
-    from fs2amd import runtime
-
-    dev = batch["texts"].device
-    prev = os.environ.get("FS2_STREAMS")
-    os.environ["FS2_STREAMS"] = "1"
-    ev = ExternalEvents()
-    ev.reserve(512)
-    per = []
-    g = None
-    try:
-        s = torch.cuda.Stream(dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s), torch.no_grad():
-            for _ in range(2):
-                model(**batch)
-            torch.cuda.synchronize(dev)
-            runtime.TIMER_RECORD = ev.record
-            runtime.TIMERS = []
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                model(**batch)
-            tms = runtime.TIMERS
-            runtime.TIMERS = None
-            runtime.TIMER_RECORD = None
-            g.replay()
-            torch.cuda.synchronize(dev)
-            for _ in range(n_replay):
-                g.replay()
-                s.synchronize()
-                per.append([(tag, ev.elapsed_s(a, b)) for a, b, tag in tms])
-    finally:
-        runtime.TIMERS = None
-        runtime.TIMER_RECORD = None
-        if prev is None:
-            del os.environ["FS2_STREAMS"]
-        else:
-            os.environ["FS2_STREAMS"] = prev
-        del g
-        torch.cuda.synchronize(dev)
-        ev.close()
-    return per
-
-
 def time_kernel_in_forward(model, batch, n_fwd=6, fwd=None):
     """Mean duration per tag of the timed launches inside real (eager) forwards (forward_timers).
     Returns {tag: (mean seconds, launches)}: decoder FFN tags "fc+ffn" (the last decoder block),
@@ -281,9 +183,10 @@ def forward_breakdown(fwd, batch_cpu, peak_tflops):
       or not): SURVEY §8d's 5,767,168 FLOP per valid token per layer (QKV + out proj + conv-k9 +
       conv-k1) over the encoder's valid phonemes x 4 layers and the decoder's valid frames x 6,
       divided by the summed durations of those launches, against the dense MFMA peak;
-    * lr — the LengthRegulator launch (fs2_lr_fused: scan + packed layout + gather + PE): bytes it
-      must move (x read once, durations, the packed frames written, the layout) over its duration,
-      against 8 TB/s."""
+    * lr_fused — the forward's LengthRegulator launch (fs2_lr_fused[_proj]: scan + packed layout +
+      gather + PE, and the first decoder Q|K|V by linearity): bytes it must move (x read once,
+      durations, the packed frames written, the layout, the projection's operands) over its
+      duration, against 8 TB/s. SURVEY §8d's LR quantity itself is lr_gather_table()."""
     n = len(fwd)
     tot = {}
     for tms in fwd:
@@ -309,13 +212,13 @@ def forward_breakdown(fwd, batch_cpu, peak_tflops):
                            "achieved": round(fl / gemm_s / 1e12, 2), "peak": peak_tflops, "unit": "TFLOP/s",
                            "frac": round(fl / gemm_s / 1e12 / peak_tflops, 4)}
     lr = tot.get("va:lr")
-    if lr and frames is not None:
+    if lr and frames is not None:  # the forward's LR launch (with the projection when it carries it)
         T = int(batch_cpu["max_mel_len"])
         byt = B * Lp * 256 * 2.0 + B * Lp * 8.0 + frames * 256 * 2.0 + B * T * 4.0 + frames * 8.0 + (B + 1) * 4.0
         proj = "dec:qkv0" in tot
         if proj:  # fs2_lr_fused_proj: f32 phoneme projection + f32 PE table read once, bf16 Q|K|V written
             byt += B * Lp * 768 * 4.0 + T * 768 * 4.0 + frames * 768 * 2.0
-        out["lr"] = {"bytes": byt, "us": round(lr * 1e6, 2), "achieved": round(byt / lr / 1e9, 1),
+        out["lr_fused"] = {"bytes": byt, "us": round(lr * 1e6, 2), "achieved": round(byt / lr / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(byt / lr / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_note": "bf16 x read once + int64 durations + packed bf16 frames written + rowmap "
                                    "(B*T int32) + row_pos (frames x 8 B) + cu" +
@@ -501,6 +404,44 @@ def decoder_op_table(model, batch_cpu, device, reps):
     return out
 
 
+def lr_gather_table(model, batch_cpu, device, reps):
+    """SURVEY §8d's LengthRegulator at the batch's shape, each form timed as `reps` back-to-back
+    launches in one HIP graph, random bf16 phoneme rows, the batch's teacher-forced durations:
+      padded  fs2_length_regulate, the reference's LengthRegulator.forward + pad contract
+              (modules.py:161-194, tools.py:360-378) in one launch: bytes = B*L*D*2 (x read once) +
+              B*L*8 (durations) + B*T*D*2 (frames written, zero padding included) + B*8 (mel_len) --
+              §8d's formula (cfg2 16.22 MB, cfg4 152.24 MB); its frac is lr_hbm_frac on the line;
+      packed  fs2_lr_fused, the forward's form without the Q|K|V projection: scan + packed layout +
+              gather + decoder PE into the valid frames only: x + durations + F*D*2 + mel_len + the
+              layout (rowmap B*T*4, row_pos F*8, cu) + the f32 PE rows read once (T*D*4)."""
+    from fs2amd import ops
+    from fs2amd.data import to_device
+
+    P = model.packed(device)
+    b = to_device(batch_cpu, device)
+    B, Lp = (int(v) for v in batch_cpu["texts"].shape)
+    T = int(batch_cpu["max_mel_len"])
+    F = int(batch_cpu["mel_lens"].sum())
+    D = 256
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(B, Lp, D, generator=g).to(device, torch.bfloat16)
+    dur = b["d_targets"]
+    forms = {
+        "padded": (lambda: ops.length_regulate(x, dur, T),
+                   B * Lp * D * 2.0 + B * Lp * 8.0 + B * T * D * 2.0 + B * 8.0),
+        "packed": (lambda: ops.lr_fused(x, b["mel_lens"], T, pe=P.dec_pe, out_dtype=P.act_dtype, dur=dur),
+                   B * Lp * D * 2.0 + B * Lp * 8.0 + F * D * 2.0 + B * 8.0 + B * T * 4.0 + F * 8.0 + (B + 1) * 4.0
+                   + T * D * 4.0),
+    }
+    out = {}
+    for name, (fn, byt) in forms.items():
+        t = _graph_mean_s(fn, device, reps)
+        out[name] = {"us": round(t * 1e6, 2), "bytes": byt, "achieved": round(byt / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(byt / t / 1e9 / HBM_PEAK_GBS, 4)}
+    out["shape"] = {"B": B, "L": Lp, "T": T, "frames": F}
+    return out
+
+
 def cpu_baseline(batch_cpu, pc, mc, budget_s=20.0):
     """The oracle (reference restatement, fp32 PyTorch CPU, bit-exact to the reference's goldens)
     on the SAME 64-utterance batch the GPU headline runs, repeated for about budget_s seconds."""
@@ -553,10 +494,11 @@ def load_traffic(dtype="bf16", fused=False, pre=False):
     return None
 
 
-def main_train(args, rank, world, device):
+def train_workload(args, rank, world, device, steps, warmup, ddp=False):
     """cfg3: one train.py step per iteration (forward, FastSpeech2Loss, backward, RCCL gradient
     all-reduce, clip, ScheduledOptim) on B=16 utterances per GPU, lengths U{16..64}, mel / pitch
-    / energy targets N(0,1). value = mel frames of all ranks per second."""
+    / energy targets N(0,1), timed as the headline is (barrier + device sync on both sides, max over
+    ranks). value = mel frames of all ranks per second. Returns the record (fields of a bench line)."""
     from fs2amd import config as C
     from fs2amd import parallel
     from fs2amd.data import synth_batch, to_device
@@ -568,46 +510,55 @@ def main_train(args, rank, world, device):
     batch_cpu = synth_batch(B, 16, 64, seed=1 + rank, with_mels=True, pe_targets=True)
     batch = to_device(batch_cpu, device)
     frames = int(batch_cpu["mel_lens"].sum())
-    if args.ddp and world == 1 and not torch.distributed.is_initialized():
+    if ddp and world == 1 and not torch.distributed.is_initialized():
         # a single-rank RCCL group, so the step's all-reduce path runs (and is timed) on one GPU
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
         torch.distributed.init_process_group("nccl", init_method="env://", rank=0, world_size=1)
     step = TrainStep(model, pc, mc, tc, device=device, world_size=world, graph=bool(args.graph),
-                     ddp=bool(args.ddp) or world > 1)
-    for _ in range(max(1, args.warmup)):
-        step(batch)
-    torch.cuda.synchronize(device)
-    parallel.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        losses = step(batch)
-    torch.cuda.synchronize(device)
-    parallel.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed, tot_frames = parallel.aggregate(elapsed, frames, device)
-    rec = {
-        "metric": "train mel-frames/sec (cfg3 train.py step, batch 16/GPU, DDP over RCCL)",
-        "value": round(tot_frames * args.steps / elapsed, 1), "unit": "mel-frames/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-        "data": "synthetic (pinyin ids U{64..107}, lengths U{16..64}, durations U{2..10}, mel/pitch/energy "
-                "targets N(0,1); counter-generated random-init weights)",
-        "config": {"workload": "cfg3: FastSpeech2 train step, ESD-Chinese-Singing-MFA model.yaml",
-                   "global_batch": B * world,
-                   "parallelism": (f"dp{world} (flat fp32 gradient buffer all-reduced over RCCL in 32 MB slices "
-                                   "inside the step's HIP graph)" if step.graph_mode and step.reduce else
-                                   f"dp{world} (DDP over RCCL, 32 MB buckets)" if step.reduce else
-                                   "dp1 (one GPU, no collective)"),
-                   "hip_graph": step.graph_mode},
-        "loss": round(float(losses[0]), 5),
-    }
+                     ddp=ddp or world > 1)
+    try:
+        for _ in range(max(1, warmup)):
+            step(batch)
+        torch.cuda.synchronize(device)
+        parallel.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            losses = step(batch)
+        torch.cuda.synchronize(device)
+        parallel.barrier()
+        elapsed = time.perf_counter() - t0
+        elapsed, tot_frames = parallel.aggregate(elapsed, frames, device)
+        return {
+            "metric": "train mel-frames/sec (cfg3 train.py step, batch 16/GPU, DDP over RCCL)",
+            "value": round(tot_frames * steps / elapsed, 1), "unit": "mel-frames/s", "n_gpus": world,
+            "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (pinyin ids U{64..107}, lengths U{16..64}, durations U{2..10}, mel/pitch/energy "
+                    "targets N(0,1); counter-generated random-init weights)",
+            "config": {"workload": "cfg3: FastSpeech2 train step, ESD-Chinese-Singing-MFA model.yaml",
+                       "global_batch": B * world, "frames_per_gpu_batch": frames,
+                       "parallelism": (f"dp{world} (flat fp32 gradient buffer all-reduced over RCCL in 32 MB "
+                                       "slices inside the step's HIP graph)" if step.graph_mode and step.reduce else
+                                       f"dp{world} (DDP over RCCL, 32 MB buckets)" if step.reduce else
+                                       "dp1 (one GPU, no collective)"),
+                       "hip_graph": step.graph_mode},
+            "loss": round(float(losses[0]), 5),
+        }
+    finally:
+        # the graph holds the captured RCCL all-reduces: release it (device drained) before the
+        # communicator is destroyed
+        step.close()
+
+
+def main_train(args, rank, world, device):
+    """``--mode train``: the cfg3 step (train_workload) as the bench line."""
+    from fs2amd import parallel
+
+    rec = train_workload(args, rank, world, device, args.steps, args.warmup, ddp=bool(args.ddp))
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    # the graph holds the captured RCCL all-reduces: release it (device drained) before the
-    # communicator is destroyed
-    step.close()
     parallel.shutdown()
 
 
@@ -685,14 +636,13 @@ def extra_workloads(model, args, rank, device):
     # the LengthRegulator stress shape (152 MB bf16): its launch inside eager cfg4
     # forwards, and the FFT-block GEMM fraction at B=256
     pk4 = {"bf16": BF16_PEAK_TFLOPS, "fp8": FP8_PEAK_TFLOPS}.get(prec, F32_PEAK_TFLOPS)
-    try:
-        brk4 = forward_breakdown(forward_timers_graph(model, to_device(b4, device), n_replay=4), b4, pk4)
-    except Exception as e:  # noqa: BLE001
-        print(f"bench: cfg4 in-graph event timing failed: {e!r}", file=sys.stderr, flush=True)
-        brk4 = forward_breakdown(forward_timers(model, to_device(b4, device), n_fwd=3), b4, pk4)
-    for k in ("lr", "fft_gemm"):
+    brk4 = forward_breakdown(forward_timers(model, to_device(b4, device), n_fwd=3), b4, pk4)
+    for k in ("lr_fused", "fft_gemm"):
         if k in brk4:
             res["cfg4_b256"][k] = brk4[k]
+    if prec == "bf16":
+        # SURVEY §8d's LengthRegulator quantity at the stress shape (152 MB bf16)
+        res["cfg4_b256"]["lr"] = lr_gather_table(model, b4, device, args.kernel_reps)
     if prec == "bf16":
         cal = synth_batch(args.batch, args.phonemes, seed=1000 + rank)
         b5 = synth_batch(args.batch, args.phonemes, seed=1 + rank)
@@ -727,6 +677,17 @@ def extra_workloads(model, args, rank, device):
         model.set_precision(prec)
     if args.vocoder:
         res["vocoder_cfg2"] = vocoder_workload(model, args, rank, device, steps)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and prec in ("bf16", "fp32"):
+        # cfg3 on the driver's record: one graphed TrainStep at B=16 (the --mode train line's step);
+        # one GPU only (at N > 1 this line stays the inference bench: the in-graph RCCL all-reduce
+        # is exercised by `bench.py --mode train`, not inside the scaling runs)
+        tr = train_workload(SimpleNamespace(dtype=prec, graph=1), rank, world, device, max(20, steps), 5)
+        res["train_cfg3"] = {k: tr[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "loss")}
+        res["train_cfg3"].update(frames_per_step=tr["config"]["frames_per_gpu_batch"],
+                                 hip_graph=tr["config"]["hip_graph"], parallelism=tr["config"]["parallelism"],
+                                 note="cfg3 train.py step (forward, FastSpeech2Loss, backward, clip_grad_norm_, "
+                                      "ScheduledOptim Adam) on B=16 x U{16..64} phonemes, one HIP graph per step")
     return res
 
 
@@ -963,27 +924,19 @@ def main():
                                      + ("ffn_pre_traffic.json: this launch inside eager cfg2 forwards, round 5)"
                                         if pre else "ffn_traffic.json)" if fused else "conv9_traffic.json)")},
     }
-    # the north-star fractions from the graph-replayed forward (event nodes around every launch);
-    # the eager-event form beside it for comparison
-    brk = None
-    if args.graph:
-        try:
-            brk = forward_breakdown(forward_timers_graph(model, batch), batch_cpu, peak)
-            brk["timing"] = ("HIP events recorded as graph nodes (hipEventRecordWithFlags, hipEventRecordExternal) "
-                             "around each launch of the forward captured once and replayed 8 times; each pair "
-                             "brackets the kernel plus the event packet's processing")
-        except Exception as e:  # noqa: BLE001  (diagnostics: never lose the headline line)
-            print(f"bench: in-graph event timing failed: {e!r}", file=sys.stderr, flush=True)
-    eager_brk = forward_breakdown(fwd_t, batch_cpu, peak)
-    if brk is None:
-        brk = eager_brk
+    # the north-star fractions: HIP events around every launch of eager forwards (queued behind GPU
+    # work, so they bracket kernels); graph-replayed kernel times are 2-5 % shorter (rocprof traces)
+    brk = forward_breakdown(fwd_t, batch_cpu, peak)
     if "fft_gemm" in brk:
         rec["fft_gemm_frac"] = brk["fft_gemm"]["frac"]
-    if "lr" in brk:
-        rec["lr_hbm_frac"] = brk["lr"]["frac"]
+    if args.dtype == "bf16":
+        # SURVEY §8d's LengthRegulator: scan + gather (+ decoder PE) alone, bytes = x read once +
+        # durations + frames written + mel_len; the forward's launch, which also projects the first
+        # decoder Q|K|V, is forward_breakdown.lr_fused
+        lrt = lr_gather_table(model, batch_cpu, device, args.kernel_reps)
+        rec["lr_hbm_frac"] = lrt["packed"]["frac"]
+        rec["lr"] = lrt
     rec["forward_breakdown"] = brk
-    if brk is not eager_brk:
-        rec["forward_breakdown_eager"] = {k: eager_brk[k] for k in ("fft_gemm", "lr") if k in eager_brk}
     if table is not None:
         rec["decoder_ops"] = table
     if rank == 0 and world == 1 and args.cpu_baseline:

@@ -732,7 +732,8 @@ __global__ __launch_bounds__(NT, 1) void enc_attn_half_kernel(EncBlockArgs p) {
   bar();
   int *flag = reinterpret_cast<int *>(smem + RED_OFF);
   if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(p.cnt + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // acq_rel: the partner's sc1 partial stores are ordered before its add, ours after
+    const int old = __hip_atomic_fetch_add(p.cnt + b, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == 1;
     if (last) __hip_atomic_store(p.cnt + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset for the next launch
     *flag = last;

@@ -254,6 +254,10 @@ struct LrFusedArgs {
   const float *proj_pe;
   int NP;
   bf16 *proj_out;
+  // padded output (fs2_length_regulate, the reference's [B, T, D] contract, utils/tools.py:360-378):
+  // row b*T + t for every t < T, zeros past min(mel_len, T); no packed layout is written
+  int padded;
+  int32_t *index_map;  // optional [B, T] source phoneme per frame (-1 past the expanded length)
 };
 
 template <typename TX, typename TO, bool HAS_PE, int ROWS>
@@ -268,6 +272,14 @@ __global__ __launch_bounds__(256) void lr_fused_kernel(LrFusedArgs a) {
   __shared__ int32_t wcu[4];
   __shared__ int64_t s_ml;
   const bool first = blockIdx.x == 0;
+  auto clen = [&](int j) {
+    const int64_t l = a.lens[j];
+    return (int32_t)(l < 0 ? 0 : (l > T ? T : l));
+  };
+  // the packed offset's loads are issued first, so their latency overlaps the scan's
+  int32_t part = 0;
+  if (!a.padded)
+    for (int j = tid; j < b; j += 256) part += clen(j);
 
   // (2) cumulative frames of utterance b
   if (a.dur != nullptr) {
@@ -303,20 +315,14 @@ __global__ __launch_bounds__(256) void lr_fused_kernel(LrFusedArgs a) {
     if (tid == 0) s_ml = a.mel_len_in[b];
   }
 
-  // (1) packed offset of utterance b and its clamped length
-  auto clen = [&](int j) {
-    const int64_t l = a.lens[j];
-    return (int32_t)(l < 0 ? 0 : (l > T ? T : l));
-  };
-  int32_t part = 0;
-  for (int j = tid; j < b; j += 256) part += clen(j);
+  // (1) packed offset of utterance b and its clamped length (padded: row b*T, all T rows written)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
   if (lane == 0) wcu[wv] = part;
   __syncthreads();
-  const int32_t cu_b = (wcu[0] + wcu[1]) + (wcu[2] + wcu[3]);
-  const int32_t len_b = clen(b);
-  if (first && tid == 0) {
+  const int32_t cu_b = a.padded ? b * T : (wcu[0] + wcu[1]) + (wcu[2] + wcu[3]);
+  const int32_t len_b = a.padded ? T : clen(b);
+  if (first && tid == 0 && !a.padded) {
     a.cu[b] = cu_b;
     if (b == a.B - 1) a.cu[a.B] = cu_b + len_b;
   }
@@ -336,7 +342,8 @@ __global__ __launch_bounds__(256) void lr_fused_kernel(LrFusedArgs a) {
       sidx = lo;
     }
     src[tid] = sidx;
-    if (t < T) {
+    if (a.index_map != nullptr && t < T) a.index_map[(int64_t)b * T + t] = sidx;
+    if (t < T && !a.padded) {
       if (a.rowmap != nullptr) a.rowmap[(int64_t)b * T + t] = t < len_b ? cu_b + t : -1;
       if (a.row_pos != nullptr && t < len_b) a.row_pos[cu_b + t] = make_int2(t, len_b);
     }
@@ -652,12 +659,42 @@ extern "C" int fs2_lr_expand(const void *x, int x_dtype, const int32_t *cum, con
   return FS2_OK;
 }
 
+static int lr_fused_launch(const LrFusedArgs &a, int x_dtype, int out_dtype, hipStream_t s);
+
+// The reference's LengthRegulator.forward + pad (modules.py:161-194, tools.py:360-378) in ONE launch:
+// duration scan, gather (+ PE) into the padded [B, T_out, D] output, zeros past min(mel_len, T_out).
+// (Round 1-5: fs2_lr_durations + fs2_lr_expand, two dependent launches.)
 extern "C" int fs2_length_regulate(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control, int B,
                                    int L, int D, int T_out, const float *pe, void *out, int out_dtype, int32_t *cum,
                                    int64_t *mel_len, float *d_rounded, int32_t *index_map, fs2_stream_t stream) {
-  int rc = fs2_lr_durations(dur, dur_kind, d_control, B, L, cum, mel_len, d_rounded, stream);
-  if (rc != FS2_OK) return rc;
-  return fs2_lr_expand(x, x_dtype, cum, mel_len, B, L, D, T_out, pe, out, out_dtype, index_map, nullptr, stream);
+  if (x == nullptr || dur == nullptr || cum == nullptr || mel_len == nullptr) return FS2_EINVAL;
+  if (dur_kind < FS2_DUR_I64 || dur_kind > FS2_DUR_LOGPRED) return FS2_EINVAL;
+  if (dur_kind == FS2_DUR_LOGPRED && d_rounded == nullptr) return FS2_EINVAL;
+  if (out == nullptr && index_map == nullptr) return FS2_EINVAL;
+  if (B < 0 || L <= 0 || D <= 0 || (D & 7) != 0 || T_out < 0 || (int64_t)B * T_out > 0x7fffff00LL) return FS2_EINVAL;
+  if (B == 0) return FS2_OK;
+  if (T_out == 0 || L > kLdsCum || out == nullptr) {  // long phoneme rows / map only: the two-launch form
+    const int rc = fs2_lr_durations(dur, dur_kind, d_control, B, L, cum, mel_len, d_rounded, stream);
+    if (rc != FS2_OK || T_out == 0) return rc;
+    return fs2_lr_expand(x, x_dtype, cum, mel_len, B, L, D, T_out, pe, out, out_dtype, index_map, nullptr, stream);
+  }
+  LrFusedArgs a{};
+  a.x = x;
+  a.dur = dur;
+  a.dur_kind = dur_kind;
+  a.d_control = d_control;
+  a.B = B;
+  a.L = L;
+  a.D = D;
+  a.T = T_out;
+  a.pe = pe;
+  a.out = out;
+  a.cum = cum;
+  a.mel_len = mel_len;
+  a.d_rounded = d_rounded;
+  a.padded = 1;
+  a.index_map = index_map;
+  return lr_fused_launch(a, x_dtype, out_dtype, as_stream(stream));
 }
 
 extern "C" int fs2_lr_backward(const float *dy, const int32_t *cum, int B, int L, int D, int T, float *dx,
@@ -743,6 +780,11 @@ extern "C" int fs2_lr_fused_proj(const void *x, int x_dtype, const void *dur, in
   a.proj_pe = proj_pe;
   a.NP = NP;
   a.proj_out = reinterpret_cast<bf16 *>(proj_out);
+  return lr_fused_launch(a, x_dtype, out_dtype, as_stream(stream));
+}
+
+static int lr_fused_launch(const LrFusedArgs &a, int x_dtype, int out_dtype, hipStream_t s) {
+  const int T_out = a.T, B = a.B;
   // frames per workgroup (FS2_LR_ROWS = 32 / 64 / 128, A/B): every workgroup re-derives its
   // utterance's scan and packed offset, so more frames per workgroup amortise that prologue
   static const int rows_env = [] {
@@ -752,13 +794,12 @@ extern "C" int fs2_lr_fused_proj(const void *x, int x_dtype, const void *dur, in
   }();
   const int R = rows_env;
   const dim3 grid((unsigned)((T_out + R - 1) / R), (unsigned)B);
-  hipStream_t s = as_stream(stream);
   auto go = [&](auto TXv, auto TOv) {
     using TX = decltype(TXv);
     using TO = decltype(TOv);
     auto launch = [&](auto RC) {
       constexpr int RR = decltype(RC)::value;
-      if (pe != nullptr)
+      if (a.pe != nullptr)
         hipLaunchKernelGGL((lr_fused_kernel<TX, TO, true, RR>), grid, dim3(256), 0, s, a);
       else
         hipLaunchKernelGGL((lr_fused_kernel<TX, TO, false, RR>), grid, dim3(256), 0, s, a);

@@ -583,7 +583,89 @@ __global__ __launch_bounds__(64 * kPrNW) void pair_kernel(PairArgs p) {
   }
 }
 
+// conv_post + tanh (hifigan/models.py:145, 159-162): y[b, t] = tanh(bias + sum_{k<7, c<32}
+// w[c][k] x[b, t + k - 3, c]) over the leaky_relu'd last-stage output x bf16 [B, T, 32], y f32 [B, T].
+// One output channel: as an MFMA conv (N padded to 4 on 128-row tiles) it took 816 us for the 7 M
+// samples of a cfg2 batch, ~7x the time to read its 450 MB input once. Here it is a streaming
+// kernel: a workgroup stages 512 + 6 rows of its utterance in LDS (80-byte pitch: the 2-row-strided
+// 16-byte reads of one lane group fall in distinct bank slots), each lane computes two consecutive
+// samples from 8 rows with v_dot2c_f32_bf16 (bf16 pairs, f32 accumulation: the same operand
+// precision as the bf16 MFMA path) against the 112 weight pairs held in registers.
+constexpr int kPostL = 512;    // output samples per workgroup (2 per lane)
+constexpr int kPostPitch = 80;  // LDS bytes per staged row (64 + 16)
+constexpr int kPostRows = kPostL + 6;
+
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(256) void post_kernel(const bf16 *__restrict__ x, const uint32_t *__restrict__ w, float bias,
+                                                   int T, float *__restrict__ out) {
+  __shared__ __attribute__((aligned(16))) unsigned char sx[kPostRows * kPostPitch];
+  const int b = blockIdx.y, t0 = blockIdx.x * kPostL, tid = threadIdx.x;
+  const bf16 *xb = x + (int64_t)b * T * 32;
+  // stage rows t0 - 3 .. t0 + 514 (4 16-byte chunks each); rows outside [0, T) are the conv's zero padding
+  constexpr int kChunks = kPostRows * 4, kPer = (kChunks + 255) / 256;
+  uint4 v[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int e = tid + i * 256, r = e >> 2, t = t0 - 3 + r;
+    v[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (e < kChunks && t >= 0 && t < T) v[i] = *reinterpret_cast<const uint4 *>(xb + (int64_t)t * 32 + (e & 3) * 8);
+  }
+  uint32_t wr[7][16];  // weight pairs (tap k, channels 2j, 2j + 1)
+#pragma unroll
+  for (int k = 0; k < 7; ++k)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) wr[k][j] = w[k * 16 + j];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int e = tid + i * 256;
+    if (e < kChunks) *reinterpret_cast<uint4 *>(sx + (e >> 2) * kPostPitch + (e & 3) * 16) = v[i];
+  }
+  __syncthreads();
+  // samples s0, s0 + 1 read rows s0 .. s0 + 7 (staged row r = sample + tap)
+  const int s0 = 2 * tid;
+  float acc0 = 0.0f, acc1 = 0.0f;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    uint32_t h[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(sx + (s0 + r) * kPostPitch + c * 16);
+      h[4 * c] = q.x;
+      h[4 * c + 1] = q.y;
+      h[4 * c + 2] = q.z;
+      h[4 * c + 3] = q.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const bf16x2 hv = __builtin_bit_cast(bf16x2, h[j]);
+      if (r < 7) acc0 = __builtin_amdgcn_fdot2_f32_bf16(hv, __builtin_bit_cast(bf16x2, wr[r][j]), acc0, false);
+      if (r >= 1) acc1 = __builtin_amdgcn_fdot2_f32_bf16(hv, __builtin_bit_cast(bf16x2, wr[r - 1][j]), acc1, false);
+    }
+  }
+  const int t = t0 + s0;
+  float *ob = out + (int64_t)b * T;
+  if (t + 1 < T) {
+    *reinterpret_cast<float2 *>(ob + t) = make_float2(tanhf(acc0 + bias), tanhf(acc1 + bias));
+  } else if (t < T) {
+    ob[t] = tanhf(acc0 + bias);
+  }
+}
+
 }  // namespace
+
+extern "C" int fs2_hifigan_post(const void *x, const void *w, float bias, int B, int T, int C, int ks, void *out,
+                                fs2_stream_t stream) {
+  if (x == nullptr || w == nullptr || out == nullptr || B < 0 || T < 0) return FS2_EINVAL;
+  if (C != 32 || ks != 7) return FS2_EUNSUPPORTED;
+  if ((T & 1) != 0) return FS2_EUNSUPPORTED;  // float2 stores: T = frames * hop is even
+  if (B == 0 || T == 0) return FS2_OK;
+  const dim3 grid((unsigned)((T + kPostL - 1) / kPostL), (unsigned)B);
+  hipLaunchKernelGGL(post_kernel, grid, dim3(256), 0, as_stream(stream), reinterpret_cast<const bf16 *>(x),
+                     reinterpret_cast<const uint32_t *>(w), bias, T, reinterpret_cast<float *>(out));
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
 
 extern "C" int64_t fs2_hifigan_mrf_weight_elems(int C) {
   return C == 32 ? mrf_woff<32>(3, 0, 0) : C == 64 ? mrf_woff<64>(3, 0, 0) : C == 128 ? mrf_woff<128>(3, 0, 0) : -1;

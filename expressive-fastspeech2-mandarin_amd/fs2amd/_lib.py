@@ -196,6 +196,7 @@ SIGNATURES = {
     "fs2_hifigan_mrf": (_i, [_p, _p, _p, _p, _i, _i, _i, _f, _p, _p]),
     "fs2_hifigan_mrf_weight_elems": (ctypes.c_int64, [_i]),
     "fs2_hifigan_pair": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _f, _f, _i, _p, _p]),
+    "fs2_hifigan_post": (_i, [_p, _p, _f, _i, _i, _i, _i, _p, _p]),
     "fs2_res_ln_fwd": (_i, [_p, _p, _i, _p, _p, _p, _i64, _i, _i, _f, _f, _p, _i, _p, _p, _p, _p, _p]),
     "fs2_res_ln_bwd_ws_bytes": (_i64, [_i]),
     "fs2_pack_train_plan": (_i, [_p, _i, _p]),

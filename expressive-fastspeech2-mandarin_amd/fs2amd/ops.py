@@ -440,10 +440,27 @@ def hifigan_mrf(x, x_act, w_packed, bias, out_slope, out=None):
     return out
 
 
+def hifigan_post(x, w, bias, out=None):
+    """fs2_hifigan_post: conv_post (32 -> 1, k = 7, pad 3) + tanh (hifigan/models.py:145,159-162) on
+    x bf16 [B, T, 32] -> f32 [B, T]. w: bf16 [7, 32] (conv_post.weight[0].T); bias: python float."""
+    _gpu(x, w)
+    B, T, C = x.shape
+    ks = w.shape[0]
+    assert x.dtype == torch.bfloat16 and x.is_contiguous() and w.dtype == torch.bfloat16 and w.is_contiguous()
+    assert w.shape == (ks, C), (tuple(w.shape), C)
+    if out is None:
+        out = torch.empty(B, T, device=x.device, dtype=torch.float32)
+    assert out.dtype == torch.float32 and out.is_contiguous() and out.shape == (B, T)
+    L.check(_lib.fs2_hifigan_post(_ptr(x), _ptr(w), float(bias), B, T, C, ks, _ptr(out), _stream(x)),
+            "fs2_hifigan_post")
+    return out
+
+
 def hifigan_pair(x, w1, b1, w2, b2, ks, dilation, *, xs=None, out_scale=1.0, out_slope=0.1, out_act=False, out=None):
-    """fs2_hifigan_pair: one ResBlock1 dilation pair at C = 128 in one launch,
-    y = conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2 + x (+ xs); returns y, or lrelu(y * out_scale,
-    out_slope) with out_act. x / xs bf16 [B, T, 128]; w1 / w2 from :func:`pack_wconv_tail`."""
+    """fs2_hifigan_pair: one ResBlock1 dilation pair at C in {128, 64} in one launch (256-sample
+    tiles at C = 128, 512-sample tiles at C = 64), y = conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2 + x
+    (+ xs); returns y, or lrelu(y * out_scale, out_slope) with out_act. x / xs bf16 [B, T, C];
+    w1 / w2 from :func:`pack_wconv_tail`."""
     _gpu(x, w1, b1, w2, b2)
     B, T, C = x.shape
     assert x.dtype == torch.bfloat16 and x.is_contiguous()
@@ -1121,12 +1138,23 @@ def length_regulate(x, duration, max_len=None, return_index_map=False):
     (model/modules.py:192-194): returns (output [B, T, D], mel_len int64 [B]).
 
     T = max_len when given (and non-zero, like utils/tools.py:361), else max(mel_len) — the
-    one device->host read this path needs."""
-    cum, mel_len, _ = lr_durations(duration)
+    one device->host read this path needs. With max_len the whole op is ONE fs2_length_regulate
+    launch (scan + gather + zero padding)."""
     if max_len:
+        _gpu(x, duration)
+        x, duration = x.contiguous(), duration.contiguous()
+        B, Lx, D = x.shape
         T_out = int(max_len)
-    else:
-        T_out = int(mel_len.max().item()) if mel_len.numel() else 0
+        cum = torch.empty(B, Lx, device=x.device, dtype=torch.int32)
+        mel_len = torch.empty(B, device=x.device, dtype=torch.int64)
+        out = torch.empty(B, T_out, D, device=x.device, dtype=x.dtype)
+        im = torch.empty(B, T_out, device=x.device, dtype=torch.int32) if return_index_map else None
+        L.check(_lib.fs2_length_regulate(_ptr(x), _dt(x), _ptr(duration), _dur_kind(duration, False), 1.0, B, Lx, D,
+                                         T_out, None, _ptr(out), _dt(x), _ptr(cum), _ptr(mel_len), None, _ptr(im),
+                                         _stream(x)), "fs2_length_regulate")
+        return (out, mel_len, im) if return_index_map else (out, mel_len)
+    cum, mel_len, _ = lr_durations(duration)
+    T_out = int(mel_len.max().item()) if mel_len.numel() else 0
     res = lr_expand(x, cum, mel_len, T_out, index_map=return_index_map)
     if return_index_map:
         return res[0], mel_len, res[1]

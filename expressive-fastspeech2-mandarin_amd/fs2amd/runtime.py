@@ -82,16 +82,10 @@ def lr_proj_ok(P, x):
 # FFN tags: "fc+ffn[+qkv]" / "ffn[+qkv]" / "ffn8" / "conv9"; the other launches "<stack>:<op>" with
 # stack "enc" / "dec" / "va" and op "qkv", "attn", "fc", "ffn", "conv1", "lr", "mel", "postnet".
 TIMERS = None
-# optional event recorder for TIMERS (callable() -> event handle recorded on the current stream):
-# bench.py installs hipEventRecordWithFlags(..., hipEventRecordExternal), which a stream capture
-# turns into event nodes of the graph, so the launches are timed inside graph replays
-TIMER_RECORD = None
 _STACK = ["enc"]
 
 
 def _record_event():
-    if TIMER_RECORD is not None:
-        return TIMER_RECORD()
     e = torch.cuda.Event(enable_timing=True)
     e.record()
     return e
@@ -511,10 +505,15 @@ def _stage1(P, va, g, p_control, d_control, defer_lr=False):
         else:
             h = r
         last = n_enc == 1
-        x, _, _ = _ffn_tail(P, lp, h, h, g.lens_src, spk_vec if last else None, emo_vec if last else None, False, None,
-                            None, None, P.enc_layers[1] if n_enc > 1 else None)
+        # a Q|K|V the FFN epilogue computes for block 1 is handed on (as the non-fold _stack does);
+        # when block 1 runs the one-launch attention sub-layer, which projects its own, none is asked for
+        nxt = P.enc_layers[1] if n_enc > 1 else None
+        if nxt is not None and enc_block_ok(P, nxt, h):
+            nxt = None
+        x, _, qn = _ffn_tail(P, lp, h, h, g.lens_src, spk_vec if last else None, emo_vec if last else None, False,
+                             None, None, None, nxt)
         if n_enc > 1:
-            x = _stack(P, P.enc_layers[1:], x, g.lens_src, addvecs=(spk_vec, emo_vec))
+            x = _stack(P, P.enc_layers[1:], x, g.lens_src, addvecs=(spk_vec, emo_vec), qkv0=qn)
     else:
         x = _stack(P, P.enc_layers, x, g.lens_src, addvecs=(spk_vec, emo_vec))
     if n_enc == 0 and (spk_vec is not None or emo_vec is not None):
@@ -952,7 +951,8 @@ def _postnet_convs(P, y, res, layout=None):
         if i < first:
             continue
         if i == n_pn - 2 and n_pn > 2 and getattr(lp, "wfr", None) is not None and lp.cin == 512 and lp.k == 5 \
-                and lp.p == 2 and getattr(last, "wtail", None) is not None and wconv_on() and pn_tail_fused_on() \
+                and lp.p == 2 and getattr(last, "wtail", None) is not None and last.cin == 512 and last.k == 5 \
+                and last.p == 2 and wconv_on() and pn_tail_fused_on() \
                 and y.dtype == torch.bfloat16 and res.dtype == torch.float32:
             # layers 3 and 4 (512 -> 512 tanh, 512 -> 80 + residual) in one launch: the 512-channel
             # output stays on chip

@@ -211,11 +211,15 @@ class Generator(nn.Module):
         b4 = torch.zeros(4, device=dev)
         b4[:1] = self.conv_post.bias.detach().float()
         P["post"] = {"w": ops.pack_conv_weight(w4, c), "b": b4, "cin": wp.shape[1], "ks": wp.shape[2], "pad": 3}
+        if c == L.FS2_BF16 and wp.shape[1] == 32 and wp.shape[2] == 7:
+            # the streaming one-channel kernel (fs2_hifigan_post): bf16 weights tap-major [7, 32]
+            P["post1"] = (wp[0].t().contiguous().to(torch.bfloat16), float(self.conv_post.bias.detach()[0]))
         self._packs[key] = (fp, P)
         return P
 
     def _pair_stage(self, chains, xu, out_slope):
-        """A 128-channel stage's multi-receptive-field block as 9 fs2_hifigan_pair launches:
+        """A 128- or 64-channel stage's multi-receptive-field block as 9 fs2_hifigan_pair launches
+        (256-sample tiles at C = 128, 512-sample tiles at C = 64):
         chain j's pairs 0 and 1 ping-pong between two buffers, its last pair adds into the running
         sum xs (in place), and the last chain's emits leaky_relu(xs / num_kernels, out_slope)."""
         from . import ops
@@ -300,6 +304,9 @@ class Generator(nn.Module):
                                       out2_slope=0.01 if last_stage else LRELU_SLOPE)
                         run(tt, c2, L.EPI_RES_SUM, xs, T, **kw)
             h = nxt
+        if "post1" in P and h.dtype == torch.bfloat16 and T % 2 == 0 and os.environ.get("FS2_VOC_POST", "1") != "0":
+            # conv_post + tanh as a streaming one-channel kernel (FS2_VOC_POST=0: the MFMA conv, A/B)
+            return ops.hifigan_post(h.view(B, T, -1), *P["post1"])
         wav = torch.empty(B, T, 4, device=mel.device, dtype=torch.float32)
         run(h, P["post"], L.EPI_BIAS_TANH, wav, T, out_dtype=L.FS2_F32)
         return wav[..., 0]

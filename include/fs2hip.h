@@ -572,7 +572,11 @@ int fs2_lr_fused_proj(const void *x, int x_dtype, const void *dur, int dur_kind,
                       void *out, int out_dtype, int32_t *cum, int64_t *mel_len, float *d_rounded,
                       const float *proj_src, const float *proj_pe, int NP, void *proj_out, fs2_stream_t stream);
 
-/* Convenience: both launches with a caller-known T_out (the teacher-forced / max_mel_len path). */
+/* The reference's LengthRegulator.forward + pad (model/modules.py:161-194, utils/tools.py:360-378)
+ * with a caller-known T_out (the teacher-forced / max_mel_len path) in ONE launch: duration scan
+ * (cum, mel_len, d_rounded as fs2_lr_durations), gather (+ PE) into the padded [B, T_out, D] out,
+ * zeros past min(mel_len, T_out), optional int32 [B, T_out] source map (-1 past the length). out
+ * may be NULL with index_map given (map only; two launches then, as for L > 2048 phonemes). */
 int fs2_length_regulate(const void *x, int x_dtype, const void *dur, int dur_kind, float d_control, int B, int L,
                         int D, int T_out, const float *pe, void *out, int out_dtype, int32_t *cum, int64_t *mel_len,
                         float *d_rounded, int32_t *index_map, fs2_stream_t stream);
@@ -626,6 +630,16 @@ int64_t fs2_hifigan_mrf_weight_elems(int C);
 int fs2_hifigan_pair(const void *x, const void *w1, const float *b1, const void *w2, const float *b2, int B, int T,
                      int C, int ks, int dilation, const void *xs, float out_scale, float out_slope, int out_act,
                      void *out, fs2_stream_t stream);
+
+/*
+ * fs2_hifigan_post — the generator's conv_post + tanh (hifigan/models.py:145, 159-162):
+ *   out[b, t] = tanh(bias + sum_{k<ks, c<C} w[k][c] x[b, t + k - ks/2, c])
+ * x bf16 [B, T, C] (the leaky_relu'd last-stage output), out f32 [B, T] (the waveform), w bf16
+ * [ks][C] (tap-major: the reference's conv_post.weight[0].T), per-utterance zero padding. C = 32,
+ * ks = 7, T even. A streaming one-channel kernel (replaces an MFMA conv with N padded to 4).
+ */
+int fs2_hifigan_post(const void *x, const void *w, float bias, int B, int T, int C, int ks, void *out,
+                     fs2_stream_t stream);
 
 /*
  * Training-step kernels (train.py step; training.py's FFTBlockFn / Conv1dFn backward):

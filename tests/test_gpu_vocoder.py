@@ -260,3 +260,44 @@ def test_hifigan_pair_stage_matches_per_conv_path(gen):
         gen.set_precision("fp32")
     snr = _snr_db(y0.numpy(), y1.numpy())
     assert snr >= 30.0, snr
+
+
+@pytest.mark.parametrize("B,T", [(3, 1024), (2, 600), (1, 514), (4, 6), (2, 130050)])
+def test_hifigan_post_matches_f64(B, T):
+    """fs2_hifigan_post (conv_post 32 -> 1, k = 7, pad 3, + tanh; hifigan/models.py:145,159-162) as
+    the streaming one-channel kernel against a float64 statement on the same bf16 input and the
+    bf16-rounded weights (the kernel's operand precision: v_dot2c_f32_bf16, f32 accumulation of 224
+    products): max |err| <= 2e-5. Tile edges (T not a multiple of 512, T < 512, the 3-sample halo
+    at both utterance ends) and the cfg2-sized per-utterance length (130,050 samples) included."""
+    from fs2amd import ops
+
+    g = torch.Generator().manual_seed(T + B)
+    w = torch.randn(1, 32, 7, generator=g) / (32 * 7) ** 0.5
+    bias = float(0.1 * torch.randn(1, generator=g))
+    x = (0.7 * torch.randn(B, T, 32, generator=g)).to(torch.bfloat16)
+    wt = w[0].t().contiguous().to(torch.bfloat16)
+    out = ops.hifigan_post(x.to(DEV), wt.to(DEV), bias)
+    torch.cuda.synchronize()
+    ref = torch.tanh(F.conv1d(x.double().transpose(1, 2), wt.double().t()[None], torch.tensor([bias], dtype=torch.float64),
+                              padding=3))[:, 0]
+    err = (out.cpu().double() - ref).abs()
+    assert out.shape == (B, T) and float(err.max()) <= 2e-5, float(err.max())
+
+
+def test_vocoder_post_kernel_equals_mfma_path(gen, golden):
+    """The bf16 generator with conv_post on fs2_hifigan_post equals the same generator with the
+    MFMA conv_post (FS2_VOC_POST=0) within the two summation orders' f32 rounding (the stages
+    before conv_post are the same launches, so their outputs are bit-identical)."""
+    mel = torch.from_numpy(golden["mini2__mel"]).to(DEV)  # [B, n_mels, T]
+    gen.set_precision("bf16")
+    x = mel.transpose(1, 2).contiguous()
+    with torch.no_grad():
+        a = gen.forward_btc(x).clone()
+        os.environ["FS2_VOC_POST"] = "0"
+        try:
+            b = gen.forward_btc(x).clone()
+        finally:
+            del os.environ["FS2_VOC_POST"]
+    torch.cuda.synchronize()
+    gen.set_precision("fp32")
+    assert a.shape == b.shape and float((a - b).abs().max()) <= 1e-4, float((a - b).abs().max())
