@@ -161,6 +161,7 @@ SIGNATURES = {
     "fs2_conv_cin_pad": (_i, [_i, _i]),
     "fs2_conv1d": (_i, [ctypes.POINTER(ConvDesc), _p]),
     "fs2_ffn": (_i, [ctypes.POINTER(FfnDesc), _p]),
+    "fs2_ffn_wide": (_i, [ctypes.POINTER(FfnDesc), _p, ctypes.c_int64, _p]),
     "fs2_ffn_weight_elems": (ctypes.c_int64, [_i, _i]),
     "fs2_ffn8": (_i, [ctypes.POINTER(Ffn8Desc), _p]),
     "fs2_ffn8_weight_bytes": (ctypes.c_int64, [_i, _i]),

@@ -677,6 +677,63 @@ def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=No
     return (out, qkv) if next_qkv is not None else out
 
 
+WIDE_MAX_ROWS = 16384  # fs2_ffn_wide below this many rows (the fused 112-row tiles fill the chip above it)
+
+
+def ffn_wide_ok(rows, F, ks):
+    """fs2_ffn_wide's shapes: F in {512, 1024}, kernel 9 or 3, rows within its workspace (the
+    f32 pre-norm rows: 1 KiB per row in the split-K workspace) and below WIDE_MAX_ROWS.
+    FS2_FFN_WIDE=0 keeps the fused split-hidden launch (A/B)."""
+    return (os.environ.get("FS2_FFN_WIDE", "1") != "0" and _splitk_on[0] and F in (512, 1024) and ks in (3, 9)
+            and 0 < rows <= WIDE_MAX_ROWS and 4096 + rows * 1024 <= SPLITK_WS_BYTES)
+
+
+def ffn_wide(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=None, layout=None, out=None):
+    """fs2_ffn_wide: the FFN of :func:`ffn` (same weights, masks, addvecs, padded or packed rows) as
+    two wide-tile launches for small row counts: the [rows, F] hidden goes through a bf16 buffer
+    (8 MB at the cfg2 encoder's 4k rows, L2 / MALL resident) and the LayerNorm is finished by the
+    last of 4 column-quarter workgroups per 64-row tile."""
+    _gpu(x, w_packed, b1, b2, lens, addvec1, addvec2)
+    if x.dtype != torch.bfloat16 or w_packed.dtype != torch.bfloat16:
+        raise TypeError("fs2amd.ffn_wide: bf16 activations and weights only")
+    if layout is not None:
+        B, T = layout.B, layout.T
+        assert x.dim() == 2 and x.shape[0] == layout.capacity, (tuple(x.shape), layout.capacity)
+    else:
+        B, T, _ = x.shape
+    D = x.shape[-1]
+    F = b1.numel()
+    assert w_packed.is_contiguous() and w_packed.numel() == _lib.fs2_ffn_weight_elems(ks, F), tuple(w_packed.shape)
+    d = L.FfnDesc()
+    d.x, d.x_row_stride = x.data_ptr(), _rows(x, "x")
+    d.w, d.b1, d.b2 = w_packed.data_ptr(), b1.data_ptr(), b2.data_ptr()
+    d.B, d.T, d.D, d.F, d.KS, d.pad = B, T, D, F, ks, pad
+    g, b, eps = ln
+    d.ln_gamma, d.ln_beta, d.ln_eps = g.data_ptr(), b.data_ptr(), float(eps)
+    if lens is not None:
+        assert lens.dtype == torch.int64 and lens.numel() == B
+        d.lens = lens.data_ptr()
+    if addvec1 is not None:
+        d.addvec1 = addvec1.data_ptr()
+    if addvec2 is not None:
+        d.addvec2 = addvec2.data_ptr()
+    if layout is not None:
+        d.rows_dev, d.row_pos = layout.rows_dev, layout.row_pos.data_ptr()
+    if out is None:
+        out = torch.empty_like(x)
+    d.out, d.out_row_stride = out.data_ptr(), _rows(out, "out")
+    rows = ffn_launch_rows(x, layout)
+    if layout is not None and rows < layout.capacity:
+        d.rows_max = int(rows)
+    ws = splitk_workspace(x.device)
+    if ws is None or not ffn_wide_ok(rows, F, ks):
+        raise RuntimeError(f"fs2amd.ffn_wide: {rows} rows / F {F} / k {ks} not covered (ops.ffn_wide_ok)")
+    d.splitk_ws, d.splitk_ws_bytes = ws.data_ptr(), ws.numel()
+    hidden = torch.empty(rows, F, device=x.device, dtype=torch.bfloat16)
+    L.check(_lib.fs2_ffn_wide(ctypes.byref(d), hidden.data_ptr(), hidden.numel() * 2, _stream(x)), "fs2_ffn_wide")
+    return out
+
+
 def _check_attention_args(qkv, lens, B, n_head, d_k, layout):
     """The kernels read int64 key lengths, B of them, and a fused Q|K|V row of 3*H*dk values: a
     mismatch would read the wrong lengths or past the buffers, so it raises here."""

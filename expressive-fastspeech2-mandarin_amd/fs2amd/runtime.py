@@ -213,6 +213,13 @@ def _ffn_tail(P, lp, x, h, lens, addvec1, addvec2, timed, layout, q, next_s, nxt
                            addvec2=addvec2, layout=layout, col_scale=q.cs2, out2=y8,
                            out2_scale=1.0 / next_s if next_s is not None else 1.0)
         return y, y8, None
+    if ffn_wide_ok(P, lp, h, layout) and CALIB is None:
+        # small row counts (the encoder's 4k phoneme rows): conv-k9 on 256-row x 64-column tiles
+        # with the x tile LDS-resident, then the k=1 conv + LN (fs2_ffn_wide: two launches)
+        with _Timed("ffn" if timed else f"{_STACK[0]}:ffn"):
+            y = ops.ffn_wide(h, lp.w12, lp.b1, lp.b2, ks=lp.k1, pad=lp.p1, ln=lp.ln2, lens=lens, addvec1=addvec1,
+                             addvec2=addvec2, layout=layout)
+        return y, None, None
     if ffn_fused_ok(P, lp, h, layout) and CALIB is None:
         # the whole FFN (conv-k9 + ReLU + conv-k1 + residual + LN + mask) as one launch: the
         # [rows, 1024] hidden stays on chip
@@ -237,6 +244,17 @@ def _ffn_tail(P, lp, x, h, lens, addvec1, addvec2, timed, layout, q, next_s, nxt
                        out_dtype=dt, residual=h, ln=lp.ln2, lens=lens, addvec1=addvec1, addvec2=addvec2,
                        layout=layout)
     return y, None, None
+
+
+def ffn_wide_ok(P, lp, h, layout):
+    """fs2_ffn_wide for the padded encoder stack's FFN (no fused Q|K|V epilogue or fc prologue is
+    asked there: the next block's one-launch attention sub-layer projects its own Q|K|V) when
+    the rows are few (ops.ffn_wide_ok: the cfg2 encoder's 4,096; cfg4's 41k keep the fused
+    112-row launch). Packed decoder launches keep fs2_ffn (its fc prologue and Q|K|V epilogue)."""
+    if layout is not None or P.compute != L.FS2_BF16 or h.dtype != torch.bfloat16 or getattr(lp, "w12", None) is None:
+        return False
+    return (h.dim() == 3 and h.shape[-1] == 256 and lp.k2 == 1 and lp.p1 == (lp.k1 - 1) // 2
+            and ops.ffn_wide_ok(h.shape[0] * h.shape[1], lp.b1.numel(), lp.k1))
 
 
 FFN_FUSED_MIN_ROWS = 16384

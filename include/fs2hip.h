@@ -242,6 +242,18 @@ int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream);
 int64_t fs2_ffn_weight_elems(int KS, int F); /* F*KS*256 + 256*F */
 
 /*
+ * fs2_ffn_wide — the same PositionwiseFeedForward + residual + LayerNorm + mask (+ addvecs) as
+ * fs2_ffn (transformer/SubLayers.py:85-93, Layers.py:27-30), for small row counts (the encoder's
+ * B x L_max phoneme rows), as two wide-tile launches: H = relu(conv_k(x) + b1) into `hidden`
+ * (bf16 [rows, F], >= rows * F * 2 bytes; rows = B * T, or rows_max for packed launches) on
+ * 256-row x 64-column tiles that keep the x tile in LDS for every tap, then the k = 1 conv on
+ * 64 x 64 tiles with the LayerNorm finished by the last of each row tile's 4 column quarters (f32
+ * pre-norm rows and arrival counters in d->splitk_ws: 4096 + rows * 1024 bytes, rows <= 65536).
+ * Same descriptor as fs2_ffn; tile_rows / nsplit are ignored, wqkv and pre_att must be NULL.
+ */
+int fs2_ffn_wide(const fs2_ffn_desc *d, void *hidden, int64_t hidden_bytes, fs2_stream_t stream);
+
+/*
  * fs2_ffn8 — the fused PositionwiseFeedForward + residual + LayerNorm on e4m3 MFMA (cfg5; the fp8
  * form of fs2_ffn, v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales). Quantisation points
  * and scales of the two-launch fp8 path (fs2_conv1d, FS2_FP8):

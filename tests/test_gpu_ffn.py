@@ -365,3 +365,63 @@ def test_ffn_pre_padded_split_form(gpu, B, T, nsplit, seed):
     assert torch.equal(one[~valid], two[~valid])
     dq = (q1.float() - q2.float()).abs()
     assert float(dq.max()) <= 0.05 * max(1.0, float(q2.float().abs().max())), float(dq.max())
+
+
+# ---- fs2_ffn_wide (the small-row-count form: conv-k9 on 256-row x 64-column tiles into a bf16 hidden,
+# then the k=1 conv + LN finished by the last of 4 column quarters)
+@pytest.mark.parametrize("B,T,seed,F,ks", [(64, 64, 51, 1024, 9), (8, 130, 52, 1024, 9), (3, 37, 53, 1024, 9),
+                                          (5, 50, 54, 512, 3), (1, 300, 55, 1024, 9)])
+def test_ffn_wide_matches_float64_and_fused(gpu, B, T, seed, F, ks):
+    """fs2_ffn_wide against the float64 statement (bf16 tolerance, as the fused launch) and against
+    the unsplit fused launch, which accumulates both GEMMs in the same k order: the hidden and the
+    pre-norm sums are the same f32 values, only the LayerNorm row statistics are summed in another
+    order -- at most 1 bf16 ulp of |y| <~ 4 (1.6e-2) on a few elements. Ragged lengths (0 / 1 /
+    shorter than the taps' reach), rows past the last 256-row tile, repeated launches identical."""
+    ops, L = gpu
+    W = _weights(ops, L, F=F, ks=ks, seed=seed)
+    rng = np.random.default_rng(seed)
+    lens_l = rng.integers(0, T + 1, B).tolist()
+    lens_l[0] = T
+    if B > 2:
+        lens_l[1], lens_l[2] = 1, 3
+    lens = torch.tensor(lens_l, dtype=torch.int64, device=DEV)
+    x = _x(B, T, lens, seed)
+    pad = (ks - 1) // 2
+    got = ops.ffn_wide(x, W["w12"], W["b1"], W["b2"], ks=ks, pad=pad, ln=W["ln"], lens=lens)
+    again = ops.ffn_wide(x, W["w12"], W["b1"], W["b2"], ks=ks, pad=pad, ln=W["ln"], lens=lens)
+    fused = ops.ffn(x, W["w12"], W["b1"], W["b2"], ks=ks, pad=pad, ln=W["ln"], lens=lens, tile_rows=112, nsplit=1)
+    torch.cuda.synchronize()
+    assert torch.equal(got, again)
+    ref = _ref(x, lens, W)
+    err = (got.double() - ref).abs()
+    assert float(err.max()) <= 3e-2 and float(err.mean()) <= 2e-3, (float(err.max()), float(err.mean()))
+    d = (got.float() - fused.float()).abs()
+    assert float(d.max()) <= 1.6e-2 and float((d > 0).float().mean()) <= 0.01, (float(d.max()), float((d > 0).float().mean()))
+
+
+def test_ffn_wide_addvecs_packed_and_form_rule(gpu):
+    """fs2_ffn_wide with speaker / emotion vectors (added after the mask, every row), on packed rows
+    of a SeqLayout (rows_dev, row positions: packed == padded bit-identical, as fs2_ffn), and the
+    runtime picks it for the cfg2 encoder's 4,096 rows only (cfg4's 41k keep the fused launch)."""
+    ops, L = gpu
+    from fs2amd import runtime
+
+    W = _weights(ops, L, seed=61)
+    B, T = 6, 70
+    lens = torch.tensor([70, 0, 1, 33, 69, 12], dtype=torch.int64, device=DEV)
+    x = _x(B, T, lens, 61)
+    g = torch.Generator(device=DEV).manual_seed(62)
+    v1, v2 = (torch.randn(B, 256, device=DEV, generator=g) for _ in range(2))
+    got = ops.ffn_wide(x, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], lens=lens, addvec1=v1, addvec2=v2)
+    ref = _ref(x, lens, W, (v1, v2))
+    assert float((got.double() - ref).abs().max()) <= 3e-2
+    lay = ops.SeqLayout(lens, T)
+    xp = _pack(lay, x)
+    gp = ops.ffn_wide(xp, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], layout=lay)
+    gd = ops.ffn_wide(x, W["w12"], W["b1"], W["b2"], ks=9, pad=4, ln=W["ln"], lens=lens)
+    torch.cuda.synchronize()
+    rm = lay.rowmap.long()
+    ok = rm >= 0
+    R = int(lay.cu[-1])
+    assert torch.equal(gp[:R], gd.reshape(-1, 256)[ok])
+    assert ops.ffn_wide_ok(64 * 64, 1024, 9) and not ops.ffn_wide_ok(256 * 160, 1024, 9)

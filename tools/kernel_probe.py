@@ -2,7 +2,8 @@
 """Launch ONE hot-path kernel repeatedly at the bench's cfg2 shapes (for rocprofv3 PMC passes).
 
     python tools/kernel_probe.py conv9 --reps 20
-kernels: ffn (decoder fused FFN, fs2_ffn), ffn_rows / ffn2_rows (decoder FFN fused / two launches on --rows
+kernels: ffn (decoder fused FFN, fs2_ffn), enc_ffn_wide / ffn_wide_rows (fs2_ffn_wide at the encoder shape /
+on --rows packed decoder rows), ffn_rows / ffn2_rows (decoder FFN fused / two launches on --rows
 packed rows), enc_ffn (encoder FFN fused, --nsplit), conv9 (decoder FFN Conv1d k=9 256->1024), conv1 (FFN k=1 1024->256 + res + LN),
 qkv, attn, lr (LengthRegulator gather + PE), lr_fused / lr_proj (the forward's LR launch without / with
 the first Q|K|V), postnet (512->512 k=5 + tanh), vpf / vpf_dp / vpf_en
@@ -83,6 +84,18 @@ def main():
         xe = rnd(64, 64, 256)
         fn = lambda: ops.ffn(xe, el.w12, el.b1, el.b2, ks=9, pad=4, ln=el.ln2, lens=b["src_lens"], nsplit=a.nsplit,
                               tile_rows=a.tile_rows)
+    elif a.kernel == "enc_ffn_wide":  # encoder FFN as fs2_ffn_wide (two wide-tile launches)
+        el = P.enc_layers[0]
+        xe = rnd(64, 64, 256)
+        fn = lambda: ops.ffn_wide(xe, el.w12, el.b1, el.b2, ks=9, pad=4, ln=el.ln2, lens=b["src_lens"])
+    elif a.kernel == "ffn_wide_rows":  # decoder FFN as fs2_ffn_wide on --rows packed rows
+        l3 = torch.full((64,), a.rows // 64, dtype=torch.int64)
+        l3[: a.rows - int(l3.sum())] += 1
+        lay3 = ops.SeqLayout(l3.to(dev), 959)
+        lay3.rows_hint = a.rows
+        h3 = rnd(lay3.capacity, 256)
+        out3 = torch.empty_like(h3)
+        fn = lambda: ops.ffn_wide(h3, lp.w12, lp.b1, lp.b2, ks=9, pad=4, ln=lp.ln2, layout=lay3, out=out3)
     elif a.kernel == "mel":  # mel_linear: packed decoder rows -> padded [B, T, 80] f32 + the bf16 copy
         h = rnd(B * T, 256)
         mel_bf = torch.empty(B, T, 80, device=dev, dtype=torch.bfloat16)

@@ -3,7 +3,8 @@
 # the chain stops at the first failure (no GPU step after a fault / abort / timeout).
 #   bash tools/run.sh TAG STEP [STEP ...]
 # steps:
-#   tests[=PYTEST_TARGETS]  pytest -m gpu (default: the whole tests/ dir; e.g. tests=tests/test_gpu_ops.py)
+#   tests[=PYTEST_TARGETS]  pytest -m gpu (default: the whole tests/ dir; comma-separated targets, e.g.
+#                           tests=tests/test_gpu_ops.py,tests/test_gpu_ffn.py)
 #   smoke                   __graft_entry__.smoke()
 #   bench                   the default bench line (50 / 20, all extra keys)
 #   driver                  the driver's protocol: --gpus 1 --steps 20 --warmup 5
@@ -21,7 +22,7 @@ fail() { tail -${2:-30} $1; exit 1; }
 for st in "$@"; do
   case $st in
     tests|tests=*)
-      T=${st#tests}; T=${T#=}; T=${T:-tests}
+      T=${st#tests}; T=${T#=}; T=${T:-tests}; T=${T//,/ }
       timeout -k 10 900 python -u -m pytest $T -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
         > $O/tests.log 2>&1 || fail $O/tests.log 40
       tail -2 $O/tests.log ;;
