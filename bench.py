@@ -643,6 +643,7 @@ def extra_workloads(model, args, rank, device):
     if prec == "bf16":
         # SURVEY §8d's LengthRegulator quantity at the stress shape (152 MB bf16)
         res["cfg4_b256"]["lr"] = lr_gather_table(model, b4, device, args.kernel_reps)
+        res["cfg4_b256"]["lr_hbm_frac"] = res["cfg4_b256"]["lr"]["padded"]["frac"]
     if prec == "bf16":
         cal = synth_batch(args.batch, args.phonemes, seed=1000 + rank)
         b5 = synth_batch(args.batch, args.phonemes, seed=1 + rank)
@@ -934,7 +935,7 @@ def main():
         # durations + frames written + mel_len; the forward's launch, which also projects the first
         # decoder Q|K|V, is forward_breakdown.lr_fused
         lrt = lr_gather_table(model, batch_cpu, device, args.kernel_reps)
-        rec["lr_hbm_frac"] = lrt["packed"]["frac"]
+        rec["lr_hbm_frac"] = lrt["padded"]["frac"]
         rec["lr"] = lrt
     rec["forward_breakdown"] = brk
     if table is not None:

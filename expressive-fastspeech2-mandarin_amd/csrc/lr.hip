@@ -661,6 +661,123 @@ extern "C" int fs2_lr_expand(const void *x, int x_dtype, const int32_t *cum, con
 
 static int lr_fused_launch(const LrFusedArgs &a, int x_dtype, int out_dtype, hipStream_t s);
 
+// fs2_length_regulate's kernel: the padded contract alone, sized for HBM streaming. Each workgroup
+// owns FR frames of one utterance and re-derives the utterance's scan (L <= 1024 durations: <= 4 per
+// thread, cached in registers), but where lr_fused_kernel binary-searches every frame's source in an
+// LDS cum row (log2 L dependent LDS reads), each phoneme here PAINTS its frame range
+// [cum[i-1], cum[i]) clipped to the workgroup's frames into src[] -- one pass, no dependent chain;
+// the first i with cum[i] > t is exactly the phoneme whose range holds t. Then the FR x D gather
+// (+ PE) with 8 x 16-byte pieces in flight per thread and non-temporal stores. No projection or packed
+// layout code is compiled in: the lean register file keeps ~4 workgroups per CU resident, so one
+// workgroup's scan runs under the others' streams (lr_fused_kernel in the padded mode carried the
+// projection's registers: 44 us at cfg4, 0.42 of HBM).
+template <typename TX, typename TO, bool HAS_PE, int FR>
+__global__ __launch_bounds__(256) void lr_pad_kernel(LrFusedArgs a) {
+  constexpr int PER = 4;  // durations per thread (L <= 1024)
+  constexpr int U = 8;    // 16-byte pieces in flight per thread
+  const int b = blockIdx.y, t0 = blockIdx.x * FR;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int L = a.L, T = a.T, D = a.D;
+  __shared__ int src[FR];
+  __shared__ int64_t wtot[4];
+  const bool first = blockIdx.x == 0;
+  if (tid < FR) src[tid] = -1;
+  const int per = (L + 255) >> 8;
+  const int i0 = min(tid * per, L), i1 = min(i0 + per, L);
+  const int64_t base = (int64_t)b * L;
+  int64_t fr[PER];
+  int64_t local = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    fr[k] = i0 + k < i1 ? frames_of(a.dur, a.dur_kind, a.d_control, base + i0 + k, first ? a.d_rounded : nullptr) : 0;
+    local += fr[k];
+  }
+  int64_t incl = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wtot[wv] = incl;
+  __syncthreads();
+  int64_t run = incl - local;
+  for (int w = 0; w < wv; ++w) run += wtot[w];
+  const int64_t f0 = t0, f1 = min(t0 + FR, T);
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (i0 + k < i1) {
+      const int64_t s = run;
+      run += fr[k];
+      if (first) a.cum[base + i0 + k] = (int32_t)(run < 0x7fffffff ? run : 0x7fffffff);
+      const int lo = (int)(s > f0 ? s : f0), hi = (int)(run < f1 ? run : f1);
+      for (int t = lo; t < hi; ++t) src[t - t0] = i0 + k;
+    }
+  }
+  if (first && tid == 0) a.mel_len[b] = (wtot[0] + wtot[1]) + (wtot[2] + wtot[3]);
+  __syncthreads();
+  if (a.index_map != nullptr && tid < FR && t0 + tid < T) a.index_map[(int64_t)b * T + t0 + tid] = src[tid];
+
+  const int rows = min(FR, T - t0);
+  const int vpr = D >> 3, total = rows * vpr;
+  const TX *xb = reinterpret_cast<const TX *>(a.x) + base * D;
+  TO *ob = reinterpret_cast<TO *>(a.out) + ((int64_t)b * T + t0) * D;
+  for (int e0 = tid; e0 < total; e0 += 256 * U) {
+    float v[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * 256;
+      const int r = e / vpr, col = (e - r * vpr) << 3;
+      const int s = e < total ? src[r] : -1;
+      if (s >= 0) {
+        load8(xb + (int64_t)s * D + col, v[u]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[u][q] = 0.0f;
+      }
+      if constexpr (HAS_PE) {
+        if (e < total) {
+          float pv[8];
+          load8(a.pe + (int64_t)(t0 + r) * D + col, pv);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[u][q] += pv[q];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * 256;
+      if (e < total) {
+        if constexpr (sizeof(TO) == 2) {
+          bf16x8 o;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] = (bf16)v[u][q];
+          __builtin_nontemporal_store(o, reinterpret_cast<bf16x8 *>(ob + (int64_t)e * 8));
+        } else {
+          store8(ob + (int64_t)e * 8, v[u]);
+        }
+      }
+    }
+  }
+}
+
+template <typename TX, typename TO>
+static void lr_pad_launch(const LrFusedArgs &a, int fr, hipStream_t s) {
+  const dim3 grid((unsigned)((a.T + fr - 1) / fr), (unsigned)a.B);
+  auto go = [&](auto FRC) {
+    constexpr int F = decltype(FRC)::value;
+    if (a.pe != nullptr)
+      hipLaunchKernelGGL((lr_pad_kernel<TX, TO, true, F>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((lr_pad_kernel<TX, TO, false, F>), grid, dim3(256), 0, s, a);
+  };
+  if (fr == 256)
+    go(std::integral_constant<int, 256>{});
+  else if (fr == 128)
+    go(std::integral_constant<int, 128>{});
+  else
+    go(std::integral_constant<int, 64>{});
+}
+
 // The reference's LengthRegulator.forward + pad (modules.py:161-194, tools.py:360-378) in ONE launch:
 // duration scan, gather (+ PE) into the padded [B, T_out, D] output, zeros past min(mel_len, T_out).
 // (Round 1-5: fs2_lr_durations + fs2_lr_expand, two dependent launches.)
@@ -694,7 +811,28 @@ extern "C" int fs2_length_regulate(const void *x, int x_dtype, const void *dur, 
   a.d_rounded = d_rounded;
   a.padded = 1;
   a.index_map = index_map;
-  return lr_fused_launch(a, x_dtype, out_dtype, as_stream(stream));
+  if (L > 1024) return lr_fused_launch(a, x_dtype, out_dtype, as_stream(stream));
+  // frames per workgroup: 128 once that still gives >= 2 workgroups per CU (cfg4: 2,048 of 64 KB),
+  // else 64 (cfg2: 448 of 32 KB); FS2_LR_PAD_FR = 64 / 128 / 256 for A/B
+  static const int fr_env = [] {
+    const char *e = getenv("FS2_LR_PAD_FR");
+    const int v = e != nullptr ? atoi(e) : 0;
+    return (v == 64 || v == 128 || v == 256) ? v : 0;
+  }();
+  const int fr = fr_env != 0 ? fr_env : (int64_t)B * ((T_out + 127) / 128) >= 512 ? 128 : 64;
+  hipStream_t s = as_stream(stream);
+  if (x_dtype == FS2_BF16 && out_dtype == FS2_BF16)
+    lr_pad_launch<bf16, bf16>(a, fr, s);
+  else if (x_dtype == FS2_F32 && out_dtype == FS2_F32)
+    lr_pad_launch<float, float>(a, fr, s);
+  else if (x_dtype == FS2_F32 && out_dtype == FS2_BF16)
+    lr_pad_launch<float, bf16>(a, fr, s);
+  else if (x_dtype == FS2_BF16 && out_dtype == FS2_F32)
+    lr_pad_launch<bf16, float>(a, fr, s);
+  else
+    return FS2_EUNSUPPORTED;
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
 }
 
 extern "C" int fs2_lr_backward(const float *dy, const int32_t *cum, int B, int L, int D, int T, float *dx,

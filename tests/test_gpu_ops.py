@@ -250,6 +250,28 @@ def test_length_regulate_cfg4_index_map_and_values(ops, golden_dir, dtype):
     assert torch.equal(out.cpu(), ref)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("crop", [0, 37])
+def test_length_regulate_one_launch_cfg4(ops, golden_dir, dtype, crop):
+    """fs2_length_regulate's one launch (lr_pad_kernel: per-workgroup scan, phoneme ranges painted
+    into the frame map, 128 frames per workgroup at this size) at the LR stress shape: index map,
+    mel_len and the padded values bit-exact against the reference capture, also with max_len
+    cropping the output below max(mel_len) (mel_len stays the uncropped total, modules.py:180)."""
+    z = np.load(os.path.join(golden_dir, "cfg4_lr_index.npz"))
+    d = torch.from_numpy(z["d"].astype(np.int64))
+    T = int(z["max_mel_len"]) - crop
+    B, Lx = d.shape
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(B, Lx, 256, generator=g).to(dtype)
+    out, mel_len, im = ops.length_regulate(x.to(DEV), d.to(DEV), T, return_index_map=True)
+    torch.cuda.synchronize()
+    imt = torch.from_numpy(z["index_map"].astype(np.int64))[:, :T]
+    np.testing.assert_array_equal(im.cpu().numpy(), imt.numpy().astype(np.int32))
+    np.testing.assert_array_equal(mel_len.cpu().numpy(), z["mel_len"])
+    ref = torch.where((imt >= 0)[..., None], x[torch.arange(B)[:, None], imt.clamp(min=0)], torch.zeros((), dtype=dtype))
+    assert torch.equal(out.cpu(), ref)
+
+
 def test_length_regulate_logpred_rounding(ops):
     """duration = clamp(round(exp(logd) - 1) * d_control, min=0) with half-to-even rounding."""
     from oracle import fs2_oracle as O

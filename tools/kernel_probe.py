@@ -5,7 +5,7 @@
 kernels: ffn (decoder fused FFN, fs2_ffn), enc_ffn_wide / ffn_wide_rows (fs2_ffn_wide at the encoder shape /
 on --rows packed decoder rows), ffn_rows / ffn2_rows (decoder FFN fused / two launches on --rows
 packed rows), enc_ffn (encoder FFN fused, --nsplit), conv9 (decoder FFN Conv1d k=9 256->1024), conv1 (FFN k=1 1024->256 + res + LN),
-qkv, attn, lr (LengthRegulator gather + PE), lr_fused / lr_proj (the forward's LR launch without / with
+qkv, attn, lr (LengthRegulator gather + PE), lr_pad / lr_pad4 (fs2_length_regulate at cfg2 / cfg4), lr_fused / lr_proj (the forward's LR launch without / with
 the first Q|K|V), postnet (512->512 k=5 + tanh), vpf / vpf_dp / vpf_en
 (fs2_vp_fused sets). --flush MB writes that much before each launch (cold caches).
 """
@@ -125,6 +125,11 @@ def main():
         x4 = torch.randn(256, b4["texts"].shape[1], 256, generator=g).to(dev, dt)
         cum4, ml4, _ = ops.lr_durations(b4["d_targets"])
         fn = lambda: ops.lr_expand(x4, cum4, ml4, int(b4["max_mel_len"]), pe=P.dec_pe, out_dtype=P.act_dtype)
+    elif a.kernel in ("lr_pad", "lr_pad4"):  # fs2_length_regulate: the padded contract in one launch
+        bb = b if a.kernel == "lr_pad" else to_device(synth_batch(256, 16, 160, seed=1), dev)
+        xq = torch.randn(*bb["texts"].shape, 256, generator=g).to(dev, dt)
+        Tq = int(bb["max_mel_len"])
+        fn = lambda: ops.length_regulate(xq, bb["d_targets"], Tq)
     elif a.kernel in ("lr_fused", "lr_fused4"):  # the forward's one-launch LR (scan + layout + gather + PE)
         bb = b if a.kernel == "lr_fused" else to_device(synth_batch(256, 16, 160, seed=1), dev)
         Bq, Lq = bb["texts"].shape
