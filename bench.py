@@ -729,7 +729,8 @@ def synth_graphs_workload(model, args, rank, device, steps, n_batches=8):
         el, fr = parallel.aggregate(time.perf_counter() - t0, fr, device)
         res[name] = {"value": round(fr / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
                      "frames_per_step_mean": round(fr / steps, 1), "T_out": t_out,
-                     **({"graphs_captured_warmup": cap0, "graphs_captured_timed": synth.captures - cap0}
+                     **({"graphs_captured_warmup": cap0, "graphs_captured_timed": synth.captures - cap0,
+                         "speculation_hits": synth.spec_hits, "speculation_misses": synth.spec_misses}
                         if name == "graphs" else {})}
     synth.close()
     g = res["graphs"]
@@ -737,11 +738,14 @@ def synth_graphs_workload(model, args, rank, device, steps, n_batches=8):
             "distinct_batches": n_batches, "frames_per_step_mean": g["frames_per_step_mean"], "T_out": g["T_out"],
             "hip_graph": True, "dtype": model.precision,
             "graphs_captured_warmup": g["graphs_captured_warmup"], "graphs_captured_timed": g["graphs_captured_timed"],
+            "speculation": {"hits": g["speculation_hits"], "misses": g["speculation_misses"]},
             "eager": {k: res["eager"][k] for k in ("value", "ms_per_step")},
             "note": "durations predicted + rounded (modules.py:131-137); 8 distinct seeded batches in rotation; "
                     "fs2amd.graphs.SynthGraphs: stage-1 graph, ONE device->host read (max / sum of mel_len + "
-                    "bad-id count), the decoder graph of the 64-frame T bucket, the T_out-shaped mel_linear / "
-                    "PostNet tail issued eagerly behind it; 'eager': the eager forward on the same rotation"}
+                    "bad-id count) with the decoder graph of the recent calls' buckets replayed speculatively "
+                    "under it (kept when the call fits them with the same launch forms), the T_out-shaped "
+                    "mel_linear / PostNet tail issued eagerly behind it; 'eager': the eager forward on the "
+                    "same rotation"}
 
 
 def vocoder_workload(model, args, rank, device, steps):

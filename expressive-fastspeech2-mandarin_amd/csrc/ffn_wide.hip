@@ -36,6 +36,10 @@
 #include "conv_common.h"
 #include "fs2_common.h"
 
+#ifndef WIDE_TRACE
+#define WIDE_TRACE 0  // analysis builds only: thread 0's shader clock at each phase into the workspace tail
+#endif
+
 namespace {
 
 constexpr int kWD = 256;          // d_model
@@ -72,21 +76,58 @@ struct WideArgs {
   bf16 *out;
   int64_t os;
   int nslices, ntiles;   // launch 1: hidden slices (F / 64) and 256-row tiles; launch 2: 64-row tiles
+  uint64_t *trace;       // WIDE_TRACE builds: 512 workgroups x 8 stamps per launch, else null
+};
+
+// WIDE_TRACE: stamps of thread 0 (s_memtime) at the phase boundaries, written at the end
+struct Stamps {
+  uint64_t t[8];
+  int n = 0;
+  __device__ __forceinline__ void at() {
+    if (WIDE_TRACE) {
+      __builtin_amdgcn_sched_barrier(0);
+      t[n++] = __builtin_readcyclecounter();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __device__ __forceinline__ void put(uint64_t *tr, int slot) {
+    if (WIDE_TRACE && tr != nullptr && threadIdx.x == 0 && slot < 512) {
+      for (int i = 0; i < n; ++i) tr[slot * 8 + i] = t[i];
+      tr[slot * 8 + 7] = (uint64_t)n;
+    }
+  }
 };
 
 // ---------------------------------------------------------------------------------------------------
 // launch 1: H = relu(conv_k(x) + b1) on 256-row x 64-column tiles
+//
+// The x tile (256 + KS - 1 rows x 256 channels) is STREAMED through LDS channel chunk by channel chunk
+// and the k loop runs chunk-major (for each 32-channel chunk c, the KS taps): a 3-slot ring of chunks
+// (chunk c + 2 is DMA'd into the slot chunk c - 1 left), so the first MFMAs wait for 1/8 of the tile
+// and the workgroup needs 52 KB of LDS instead of 140 -- two workgroups per CU, one's prologue and
+// H stores under the other's MFMAs (the whole-tile form's prologue took ~8-10k of ~36k cycles).
+// Slot image: a 64-byte zero pad (the masked tap rows' fragment source) + 272 rows x 64 bytes; the
+// 16-byte slot of channel group hi in row R is hi ^ (2 * bit 2 of R), which keeps every ds_read_b128
+// lane group on 16 distinct slots for ANY row shift (the taps). The fragment addresses of all (tap,
+// row block) pairs are computed once (invalid taps -> the zero pad); the ring slot is the
+// instruction's immediate offset.
 template <int KS>
-__global__ __launch_bounds__(256, 1) void ffn_hidden_kernel(WideArgs p) {
-  constexpr int BM = 256, XROWS = BM + KS - 1, XPITCH = 544;
-  constexpr int XPIECES = (XROWS * XPITCH + 1023) / 1024, XP_PER_WAVE = (XPIECES + 3) / 4;
-  constexpr int X_OFF = 512;  // [0, 512): zeros, the masked tap rows' fragment source
-  constexpr int SMEM = X_OFF + 4 * XP_PER_WAVE * 1024;
-  static_assert(SMEM <= 163840, "LDS");
-  static_assert(BM * 144 <= 4 * XP_PER_WAVE * 1024, "H staging fits in the x region");
-  constexpr int NK = KS * (kWD / 32);  // k-steps (tap-major, 8 per tap)
-  constexpr int DEPTH = 8;             // weight k-steps in flight per wave (one tap ahead)
+__global__ __launch_bounds__(256, 2) void ffn_hidden_kernel(WideArgs p) {
+  constexpr int BM = 256, XROWS = BM + KS - 1;
+  constexpr int NPC = (XROWS + 15) / 16;  // DMA pieces (16 rows x 64 B) per chunk
+  constexpr int CH = 64 + NPC * 1024;     // chunk region: zero pad + rows
+  constexpr int NCH = kWD / 32;           // channel chunks (k-steps per tap)
+  constexpr int PPW = (NPC + 3) / 4;      // pieces per wave per chunk (the last piece issued by every wave)
+  constexpr int NSLOT = 3;                // chunk ring
+  constexpr int SMEM = NSLOT * CH;
+  static_assert(2 * SMEM <= 163840, "two workgroups per CU");
+  static_assert(BM * 144 <= SMEM, "H staging fits in the ring");
+  static_assert((NSLOT - 1) * CH < 65536, "slot offsets fit the ds_read immediate");
+  constexpr int NK = KS * NCH;  // k-steps; weight unit of (tap t, chunk c) = t * NCH + c (ops.pack_ffn_weights)
+  constexpr int MB = 8;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  Stamps st;
+  st.at();
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -101,29 +142,11 @@ __global__ __launch_bounds__(256, 1) void ffn_hidden_kernel(WideArgs p) {
   if (m0 >= M) return;
   const int pad = p.pad, T = p.T;
 
-  // the zero region first: a ds_write behind the tile's LDS-DMA would wait for all of it
-  if (tid < 32) *reinterpret_cast<float4 *>(smem + 16 * tid) = make_float4(0.f, 0.f, 0.f, 0.f);
-  // x tile (rows m0 - pad .. m0 + BM + KS - 2) -> LDS by LDS-DMA, lane-linear 1 KiB pieces
-  {
-    const rsrc_t sr = make_rsrc(p.x, p.x_bytes);
-    const uint32_t srow = (uint32_t)p.xs * 2u;
-#pragma unroll
-    for (int i = 0; i < XP_PER_WAVE; ++i) {
-      const int pc = w + 4 * i;
-      const int o = pc * 1024 + lane * 16;
-      const int r = o / XPITCH, within = o - r * XPITCH;
-      const int gm = m0 - pad + r;
-      const bool ok = r < XROWS && within < 512 && gm >= 0 && gm < M;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(sr, (__attribute__((address_space(3))) void *)(smem + X_OFF + pc * 1024),
-                                               16, ok ? (uint32_t)gm * srow + (uint32_t)within : kOOB, 0, 0, 0);
-    }
-  }
-
-  // row positions of this lane's 8 row blocks and b1 of its 8 hidden columns: loads issued here,
-  // used after the weight ring starts (one wait covers them with the x tile)
-  constexpr int MB = 8;
-  // (padded rows: position m % T of a length-T sequence, computed first; packed rows: loaded over
-  // them -- ALU writes after the loads into the same registers would wait for the loads)
+  // the zero pads first: a ds_write behind the tile's LDS-DMA would wait for all of it
+  if (tid < NSLOT * 4) *reinterpret_cast<float4 *>(smem + (tid >> 2) * CH + (tid & 3) * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+  // row positions of this lane's 8 row blocks and b1 of its 8 hidden columns, issued before the tile
+  // (the chunk-0 wait covers them). Padded rows: position m % T of a length-T sequence; packed rows:
+  // loaded over them (ALU writes after the loads into the same registers would wait for the loads)
   int2 rq[MB];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
@@ -137,51 +160,110 @@ __global__ __launch_bounds__(256, 1) void ffn_hidden_kernel(WideArgs p) {
   const int hcol0 = slice * 64 + hh * 32 + 4 * (lane >> 4);
   const float4 bb0 = *reinterpret_cast<const float4 *>(p.b1 + hcol0);
   const float4 bb1 = *reinterpret_cast<const float4 *>(p.b1 + hcol0 + 16);
+  // chunk c of the x tile into ring slot c % 3: wave w issues pieces w, w + 4, ... and the last one
+  // (every wave writes its identical bytes), PPW per chunk, so every wave's count is the same
+  const rsrc_t sr = make_rsrc(p.x, p.x_bytes);
+  const uint32_t srow = (uint32_t)p.xs * 2u;
+  auto dma_chunk = [&](auto CI) {
+    constexpr int c = decltype(CI)::value;
+    const int ps = lane & 3;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int pc = min(w + 4 * i, NPC - 1);
+      const int R = pc * 16 + (lane >> 2);
+      const int hl = ps ^ ((R >> 1) & 2);
+      const int gm = m0 - pad + R;
+      const bool ok = R < XROWS && gm >= 0 && gm < M;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          sr, (__attribute__((address_space(3))) void *)(smem + (c % NSLOT) * CH + 64 + pc * 1024), 16,
+          ok ? (uint32_t)gm * srow + (uint32_t)(c * 64 + hl * 16) : kOOB, 0, 0, 0);
+    }
+  };
+  dma_chunk(std::integral_constant<int, 0>{});
+  dma_chunk(std::integral_constant<int, 1>{});
 
-  // weight ring: unit k of this slice at (slice * NK + k) * 4 KiB; this wave's two 1 KiB fragments
+  // weight ring: RD k-steps ahead (k-step kk = c * KS + t reads ring slot kk % RD; the loop is fully
+  // unrolled, so every slot index is static)
+  constexpr int RD = 6;
   const rsrc_t wr = make_rsrc(p.w, p.w_bytes);
   const uint32_t wbase = (uint32_t)(slice * NK) * (uint32_t)kWUnit + (uint32_t)(hh * 2048 + lane * 16);
-  bf16x8 pa[DEPTH][2];
-  auto load_at = [&](auto S, int k) {
-    constexpr int s = decltype(S)::value;
+  bf16x8 pa[RD][2];
+  auto load_at = [&](auto KI) {  // k-step kk's fragments into slot kk % RD
+    constexpr int kk = decltype(KI)::value, c = kk / KS, t = kk % KS;
     __builtin_amdgcn_sched_barrier(0);
-    const uint32_t o = wbase + (uint32_t)min(k, NK - 1) * (uint32_t)kWUnit;
-    pa[s][0] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wr, o, 0, 0));
-    pa[s][1] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wr, o + 1024, 0, 0));
+    const uint32_t o = wbase + (uint32_t)(t * NCH + c) * (uint32_t)kWUnit;
+    pa[kk % RD][0] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wr, o, 0, 0));
+    pa[kk % RD][1] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wr, o + 1024, 0, 0));
     __builtin_amdgcn_sched_barrier(0);
   };
-  wfor<DEPTH>([&](auto I) { load_at(I, decltype(I)::value); });
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DEPTH) : "memory");  // x tile, rows, b1 (older than the ring)
-  // tap validity per row block: bit tap set when row + tap - pad stays inside its sequence
-  int vmask[MB];
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
-    int v = 0;
-#pragma unroll
-    for (int tap = 0; tap < KS; ++tap) v |= ((unsigned)(rq[mb].x + tap - pad) < (unsigned)rq[mb].y ? 1 : 0) << tap;
-    vmask[mb] = v;
-  }
-  __builtin_amdgcn_s_waitcnt(kWLgkm0);
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
+  wfor<RD>([&](auto I) { load_at(I); });
+  // ring refills (2 loads each) issued by k-steps [a, b]: k-step kk refills iff kk + RD < NK
+  auto refills = [](int a, int b) constexpr {
+    int n = 0;
+    for (int kk = a; kk <= b; ++kk) n += kk + RD < NK ? 2 : 0;
+    return n;
+  };
 
-  const int hrow0 = rh * 128 + (lane & 15), hi = lane >> 4;
-  auto bases = [&](int tap, int (&ad)[MB]) {
-    const int base = X_OFF + (hrow0 + tap) * XPITCH + hi * 16;
+  // fragment addresses: (tap t, row block mb) -> LDS row R = rh*128 + 16 mb + r16 + t of slot 0, or
+  // the zero pad when row + t - pad leaves the sequence (the rows' positions are needed: wait for
+  // them); two 16-bit addresses per register (row blocks 2i, 2i + 1)
+  const int r16 = lane & 15, hi = lane >> 4;
+  uint32_t adp[KS][MB / 2];
+  {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW + 2 * RD) : "memory");  // rows + b1 (older than the tile)
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) ad[mb] = (base + mb * 16 * XPITCH) & __builtin_amdgcn_sbfe(vmask[mb], tap, 1);
-  };
-  auto issue = [&](const int (&ad)[MB], auto KSI, bf16x8 (&f)[MB]) {
-    constexpr int off = decltype(KSI)::value * 64;
+    for (int t = 0; t < KS; ++t) {
+      const int R0 = rh * 128 + r16 + t;
+      const int sl = (hi ^ ((R0 >> 1) & 2)) * 16;  // bit 2 of R is the same for every row block (16 mb)
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) f[mb] = *reinterpret_cast<const bf16x8 *>(smem + ad[mb] + off);
+      for (int i = 0; i < MB / 2; ++i) {
+        uint32_t a2[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int mb = 2 * i + j;
+          const bool ok = (unsigned)(rq[mb].x + t - pad) < (unsigned)rq[mb].y;
+          a2[j] = ok ? (uint32_t)(64 + (R0 + 16 * mb) * 64 + sl) : 0u;
+        }
+        adp[t][i] = a2[0] | (a2[1] << 16);
+      }
+    }
+  }
+  static_assert(CH < 65536, "16-bit fragment addresses");
+  // chunk c landed (this wave's pieces, then everyone's): vector-memory ops this wave issued after
+  // chunk c's last piece -- chunk 0: chunk 1's pieces + the ring prologue; chunk 1: the ring prologue
+  // + chunk 0's refills before its last k-step; chunk c >= 2 (issued inside the last k-step of chunk
+  // c - 2, behind the barrier): that k-step's refill + chunk c - 1's refills before its last k-step
+  auto wait_chunk = [&](auto CI) {
+    constexpr int c = decltype(CI)::value;
+    constexpr int n = c == 0 ? PPW + 2 * RD
+                             : c == 1 ? 2 * RD + refills(0, KS - 2)
+                                      : refills((c - 2) * KS + KS - 1, (c - 1) * KS + KS - 2);
+    static_assert(n <= 63, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory");
+    __builtin_amdgcn_s_waitcnt(kWLgkm0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
   };
+  wait_chunk(std::integral_constant<int, 0>{});
+  st.at();
+
   f32x4 acc[2][MB];
 #pragma unroll
   for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) acc[jb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](auto CI, auto TI, bf16x8 (&f)[MB]) {
+    constexpr int c = decltype(CI)::value, t = decltype(TI)::value, off = (c % NSLOT) * CH;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      // volatile: unpacked per use (hipcc would otherwise keep all 72 unpacked addresses live across
+      // the unrolled chunks and spill)
+      uint32_t a;
+      asm volatile("v_bfe_u32 %0, %1, %2, 16" : "=v"(a) : "v"(adp[t][mb >> 1]), "n"((mb & 1) * 16));
+      f[mb] = *reinterpret_cast<const bf16x8 *>(smem + a + off);
+    }
+  };
   auto mma = [&](const bf16x8 (&fa)[2], const bf16x8 (&fb)[MB]) {
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
@@ -190,38 +272,42 @@ __global__ __launch_bounds__(256, 1) void ffn_hidden_kernel(WideArgs p) {
         acc[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[jb], fb[mb], acc[jb][mb], 0, 0, 0);
   };
   bf16x8 f0[MB], f1[MB];
-  int bc[MB], bn[MB];
-  bases(0, bc);
-  issue(bc, std::integral_constant<int, 0>{}, f0);
-#pragma nounroll
-  for (int tap = 0; tap < KS; ++tap) {
-    bases(tap + 1, bn);  // tap KS: every row masked (the zero region): harmless reads
-    wfor<8>([&](auto KSI) {
-      constexpr int ks = decltype(KSI)::value;
-      if constexpr (ks + 1 < 8) {
-        if constexpr (ks & 1)
-          issue(bc, std::integral_constant<int, ks + 1>{}, f0);
+  issue(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, f0);
+  wfor<NCH>([&](auto CI) {
+    constexpr int c = decltype(CI)::value;
+    wfor<KS>([&](auto TI) {
+      constexpr int t = decltype(TI)::value;
+      constexpr int kk = c * KS + t;  // k-step index: f0 / f1 alternate
+      // next k-step's fragments first (one k-step of LDS latency hidden under this one's MFMAs)
+      if constexpr (t + 1 < KS) {
+        if constexpr (kk & 1)
+          issue(CI, std::integral_constant<int, t + 1>{}, f0);
         else
-          issue(bc, std::integral_constant<int, ks + 1>{}, f1);
-      } else {
-        issue(bn, std::integral_constant<int, 0>{}, f0);
+          issue(CI, std::integral_constant<int, t + 1>{}, f1);
+      } else if constexpr (c + 1 < NCH) {
+        wait_chunk(std::integral_constant<int, c + 1>{});
+        // every wave is past chunk c - 1: its slot takes chunk c + 2
+        if constexpr (c + 2 < NCH) dma_chunk(std::integral_constant<int, c + 2>{});
+        if constexpr (kk & 1)
+          issue(std::integral_constant<int, c + 1>{}, std::integral_constant<int, 0>{}, f0);
+        else
+          issue(std::integral_constant<int, c + 1>{}, std::integral_constant<int, 0>{}, f1);
       }
-      if constexpr (ks & 1)
-        mma(pa[ks], f1);
+      if constexpr (kk & 1)
+        mma(pa[kk % RD], f1);
       else
-        mma(pa[ks], f0);
-      load_at(std::integral_constant<int, ks>{}, (tap + 1) * 8 + ks);  // past the end: unit NK - 1 again
+        mma(pa[kk % RD], f0);
+      if constexpr (kk + RD < NK) load_at(std::integral_constant<int, kk + RD>{});
     });
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) bc[mb] = bn[mb];
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  });
   __builtin_amdgcn_s_waitcnt(kWLgkm0);
   __builtin_amdgcn_s_barrier();  // every wave done with the x tile: stage H over it
+  st.at();
 
   // H = bf16(relu(acc + b1)): lane holds hidden columns 4 hi .. +3 of block jb, row hrow0 + 16 mb;
   // staged at a 144-byte row pitch, then whole 128-byte row segments out (8 x 16 B per row)
   constexpr int HP = 144;
+  const int hrow0 = rh * 128 + r16;
 #pragma unroll
   for (int jb = 0; jb < 2; ++jb) {
     const float4 bb = jb == 0 ? bb0 : bb1;
@@ -233,7 +319,7 @@ __global__ __launch_bounds__(256, 1) void ffn_hidden_kernel(WideArgs p) {
       o[1] = (bf16)fmaxf(v[1] + bb.y, 0.f);
       o[2] = (bf16)fmaxf(v[2] + bb.z, 0.f);
       o[3] = (bf16)fmaxf(v[3] + bb.w, 0.f);
-      *reinterpret_cast<bf16x4 *>(smem + X_OFF + (hrow0 + 16 * mb) * HP + (hh * 32 + jb * 16 + 4 * hi) * 2) = o;
+      *reinterpret_cast<bf16x4 *>(smem + (hrow0 + 16 * mb) * HP + (hh * 32 + jb * 16 + 4 * hi) * 2) = o;
     }
   }
   __builtin_amdgcn_s_waitcnt(kWLgkm0);
@@ -245,7 +331,12 @@ __global__ __launch_bounds__(256, 1) void ffn_hidden_kernel(WideArgs p) {
     const int e = tid + 256 * i, r = e >> 3, c = e & 7;
     if (m0 + r < M)
       *reinterpret_cast<uint4 *>(hb + (uint32_t)(m0 + r) * hrow + (uint32_t)(slice * 128 + c * 16)) =
-          *reinterpret_cast<const uint4 *>(smem + X_OFF + r * HP + c * 16);
+          *reinterpret_cast<const uint4 *>(smem + r * HP + c * 16);
+  }
+  if (WIDE_TRACE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st.at();
+    st.put(p.trace, L);
   }
 }
 
@@ -257,7 +348,12 @@ __global__ __launch_bounds__(256, 1) void ffn_out_kernel(WideArgs p) {
   constexpr int NK = F / 32;       // k-steps of 32 hidden columns
   constexpr int KW = NK / 4;       // per wave
   constexpr int RED = 4 * 16 * 64 * 16;  // 4 waves' partial tiles in LDS: [wave][jb * 4 + mb][lane] f32x4
-  __shared__ __attribute__((aligned(16))) char smem[RED + 16];
+  constexpr int VEC = RED;               // gamma | beta (f32, by LDS-DMA at kernel start)
+  constexpr int OP = kWD * 2 + 16;       // LayerNorm output staging pitch (over the partials)
+  static_assert(64 * OP <= RED, "staging fits");
+  __shared__ __attribute__((aligned(16))) char smem[RED + 2048 + 16];
+  Stamps st;
+  st.at();
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -270,6 +366,11 @@ __global__ __launch_bounds__(256, 1) void ffn_out_kernel(WideArgs p) {
   if (m0 >= M) return;
   const int T = p.T;
   const int hi = lane >> 4, r16 = lane & 15;
+  // the LayerNorm vectors into LDS first (only the last arriver reads them, after its vmcnt(0))
+  if (w < 2)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(w == 0 ? p.gamma : p.beta, 1024),
+                                             (__attribute__((address_space(3))) void *)(smem + VEC + w * 1024), 16,
+                                             (uint32_t)lane * 16u, 0, 0, 0);
 
   // every operand of this wave's K quarter at once: KW k-steps x (4 w2 fragments + 4 H fragments)
   const rsrc_t wr = make_rsrc(p.w, p.w_bytes);
@@ -291,9 +392,27 @@ __global__ __launch_bounds__(256, 1) void ffn_out_kernel(WideArgs p) {
                       hr, m < M ? (uint32_t)m * hrow + (uint32_t)((w * KW + k) * 64 + hi * 16) : kOOB, 0, 0));
     }
   }
+  // + b2 + residual operands of this lane (row m0 + 16 w + r16, columns 64 q + 16 jb + 4 hi .. + 3),
+  // loaded with the rest: a load issued after the first z store would wait for that store
+  const int m = m0 + 16 * w + r16;
+  const bool mok = m < M;
+  const rsrc_t xr = make_rsrc(p.x, p.x_bytes);
+  const rsrc_t zr = make_rsrc(p.z, p.z_bytes);
+  float4 b2v[4];
+  uint2 xv[4];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) {
+    const int n = 64 * q + 16 * jb + 4 * hi;
+    b2v[jb] = *reinterpret_cast<const float4 *>(p.b2 + n);
+    xv[jb] = bload8(xr, mok ? (uint32_t)m * (uint32_t)p.xs * 2u + (uint32_t)n * 2u : kOOB);
+  }
   // all loads stay ahead of the MFMAs (left alone, hipcc interleaves them to save registers and
   // every k-step then waits for its own memory round trip)
   __builtin_amdgcn_sched_barrier(0);
+  if (WIDE_TRACE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st.at();
+  }
   f32x4 acc[4][4];
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb)
@@ -312,7 +431,9 @@ __global__ __launch_bounds__(256, 1) void ffn_out_kernel(WideArgs p) {
   for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) red[(w * 16 + jb * 4 + mb) * 64 + lane] = acc[jb][mb];
-  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(kWLgkm0);
+  __builtin_amdgcn_s_barrier();
+  st.at();
   f32x4 zv[4];
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb) {
@@ -321,29 +442,23 @@ __global__ __launch_bounds__(256, 1) void ffn_out_kernel(WideArgs p) {
     for (int ww = 1; ww < 4; ++ww) s += red[(ww * 16 + jb * 4 + w) * 64 + lane];
     zv[jb] = s;
   }
-  // + b2 + residual; lane: row m0 + 16 w + r16, columns 64 q + 16 jb + 4 hi .. + 3
-  const int m = m0 + 16 * w + r16;
-  const bool mok = m < M;
-  const rsrc_t xr = make_rsrc(p.x, p.x_bytes);
-  const rsrc_t zr = make_rsrc(p.z, p.z_bytes);
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb) {
     const int n = 64 * q + 16 * jb + 4 * hi;
-    const float4 b2 = *reinterpret_cast<const float4 *>(p.b2 + n);
-    const uint2 xv = bload8(xr, mok ? (uint32_t)m * (uint32_t)p.xs * 2u + (uint32_t)n * 2u : kOOB);
-    const bf16x4 x4 = __builtin_bit_cast(bf16x4, xv);
+    const bf16x4 x4 = __builtin_bit_cast(bf16x4, xv[jb]);
     f32x4 v = zv[jb];
-    v[0] = v[0] + b2.x + (float)x4[0];
-    v[1] = v[1] + b2.y + (float)x4[1];
-    v[2] = v[2] + b2.z + (float)x4[2];
-    v[3] = v[3] + b2.w + (float)x4[3];
+    v[0] = v[0] + b2v[jb].x + (float)x4[0];
+    v[1] = v[1] + b2v[jb].y + (float)x4[1];
+    v[2] = v[2] + b2v[jb].z + (float)x4[2];
+    v[3] = v[3] + b2v[jb].w + (float)x4[3];
     // write-through (sc1): the last-arriving quarter reads it with sc1 loads from another CU
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), zr,
                                            mok ? ((uint32_t)m * kWD + (uint32_t)n) * 4u : kOOB, 0, 16);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int *flag = reinterpret_cast<int *>(smem + RED);
+  st.at();
+  int *flag = reinterpret_cast<int *>(smem + RED + 2048);
   if (tid == 0) {
     // relaxed add + sc1 stores / loads of every handed-off byte, each storing wave drained before the
     // barrier ahead of this add, one workgroup per CU: ffn.hip's split-hidden hand-off
@@ -353,59 +468,86 @@ __global__ __launch_bounds__(256, 1) void ffn_out_kernel(WideArgs p) {
     *flag = last;
   }
   __syncthreads();
-  if (!*flag) return;
+  st.at();
+  if (!*flag) {
+    st.put(p.trace, L);
+    return;
+  }
 
   // LayerNorm of the tile's rows over all 256 columns: wave w takes rows 16 w + r16; lane (r16, hi)
-  // holds columns 16 i + 4 hi .. + 3, i = 0..15 (64 values); row sums over the 4 lanes of a row
-  f32x4 v[16];
+  // holds columns 16 i + 4 hi .. + 3, i = 0..15 (64 values); row sums over the 4 lanes of a row.
+  // The bf16 rows are staged in LDS (over the partials) and leave as whole 512-byte rows.
+  if (mok) {
+    f32x4 v[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-    v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                         zr, mok ? ((uint32_t)m * kWD + (uint32_t)(16 * i + 4 * hi)) * 4u : kOOB, 0, 16));
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
-  s += __shfl_xor(s, 16, 64);
-  s += __shfl_xor(s, 32, 64);
-  const float mean = s * (1.0f / 256.0f);
-  float ss = 0.f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    v[i] -= mean;
-    ss += (v[i][0] * v[i][0] + v[i][1] * v[i][1]) + (v[i][2] * v[i][2] + v[i][3] * v[i][3]);
-  }
-  ss += __shfl_xor(ss, 16, 64);
-  ss += __shfl_xor(ss, 32, 64);
-  const float rstd = 1.0f / sqrtf(ss * (1.0f / 256.0f) + p.eps);
-  bool masked = false;
-  int bb = 0;
-  if (p.row_pos == nullptr && mok) {
-    bb = m / T;
-    masked = p.lens != nullptr && (int64_t)(m - bb * T) >= p.lens[bb];
-  }
-  if (!mok) return;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int n = 16 * i + 4 * hi;
-    const float4 g = *reinterpret_cast<const float4 *>(p.gamma + n);
-    const float4 be = *reinterpret_cast<const float4 *>(p.beta + n);
-    float y[4] = {v[i][0] * rstd * g.x + be.x, v[i][1] * rstd * g.y + be.y, v[i][2] * rstd * g.z + be.z,
-                  v[i][3] * rstd * g.w + be.w};
-    if (masked) y[0] = y[1] = y[2] = y[3] = 0.f;
-    if (p.av1 != nullptr) {
-      const float4 a1 = *reinterpret_cast<const float4 *>(p.av1 + (int64_t)bb * kWD + n);
-      y[0] += a1.x; y[1] += a1.y; y[2] += a1.z; y[3] += a1.w;
+    for (int i = 0; i < 16; ++i)
+      v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           zr, ((uint32_t)m * kWD + (uint32_t)(16 * i + 4 * hi)) * 4u, 0, 16));
+    bool masked = false;
+    int bb = 0;
+    if (p.row_pos == nullptr) {
+      bb = m / T;
+      masked = p.lens != nullptr && (int64_t)(m - bb * T) >= p.lens[bb];
     }
-    if (p.av2 != nullptr) {
-      const float4 a2 = *reinterpret_cast<const float4 *>(p.av2 + (int64_t)bb * kWD + n);
-      y[0] += a2.x; y[1] += a2.y; y[2] += a2.z; y[3] += a2.w;
+    float4 a1[16], a2[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int n = 16 * i + 4 * hi;
+      a1[i] = p.av1 != nullptr ? *reinterpret_cast<const float4 *>(p.av1 + (int64_t)bb * kWD + n) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    bf16x4 o;
-    o[0] = (bf16)y[0];
-    o[1] = (bf16)y[1];
-    o[2] = (bf16)y[2];
-    o[3] = (bf16)y[3];
-    *reinterpret_cast<bf16x4 *>(p.out + (int64_t)m * p.os + n) = o;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mean = s * (1.0f / 256.0f);
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      v[i] -= mean;
+      ss += (v[i][0] * v[i][0] + v[i][1] * v[i][1]) + (v[i][2] * v[i][2] + v[i][3] * v[i][3]);
+    }
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    const float rstd = 1.0f / sqrtf(ss * (1.0f / 256.0f) + p.eps);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int n = 16 * i + 4 * hi;
+      a2[i] = p.av2 != nullptr ? *reinterpret_cast<const float4 *>(p.av2 + (int64_t)bb * kWD + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float *vg = reinterpret_cast<const float *>(smem + VEC), *vb = vg + kWD;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int n = 16 * i + 4 * hi;
+      const float4 g = *reinterpret_cast<const float4 *>(vg + n);
+      const float4 be = *reinterpret_cast<const float4 *>(vb + n);
+      float y[4] = {v[i][0] * rstd * g.x + be.x, v[i][1] * rstd * g.y + be.y, v[i][2] * rstd * g.z + be.z,
+                    v[i][3] * rstd * g.w + be.w};
+      if (masked) y[0] = y[1] = y[2] = y[3] = 0.f;
+      // addvecs after the mask, every row
+      if (p.av1 != nullptr) {
+        y[0] += a1[i].x; y[1] += a1[i].y; y[2] += a1[i].z; y[3] += a1[i].w;
+      }
+      if (p.av2 != nullptr) {
+        y[0] += a2[i].x; y[1] += a2[i].y; y[2] += a2[i].z; y[3] += a2[i].w;
+      }
+      const bf16x4 o = {(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3]};
+      *reinterpret_cast<bf16x4 *>(smem + (16 * w + r16) * OP + n * 2) = o;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(kWLgkm0);
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = tid + 256 * i, r = e >> 5, c = e & 31;
+    if (m0 + r < M)
+      *reinterpret_cast<uint4 *>(p.out + (int64_t)(m0 + r) * p.os + c * 8) =
+          *reinterpret_cast<const uint4 *>(smem + r * OP + c * 16);
+  }
+  if (WIDE_TRACE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st.at();
+    st.put(p.trace, L);
   }
 }
 
@@ -465,18 +607,27 @@ extern "C" int fs2_ffn_wide(const fs2_ffn_desc *d, void *hidden, int64_t hidden_
   p.z_bytes = (uint32_t)zb;
   p.out = static_cast<bf16 *>(d->out);
   p.os = d->out_row_stride;
+  if (WIDE_TRACE)
+    p.trace = reinterpret_cast<uint64_t *>(static_cast<char *>(d->splitk_ws) + d->splitk_ws_bytes - 65536);
   hipStream_t s = as_stream(stream);
   // launch 1: hidden slices x 256-row tiles, grid padded to whole XCD rounds
   p.nslices = d->F / 64;
   p.ntiles = (int)((Mg + 255) / 256);
   const int n1 = (p.nslices * p.ntiles + 7) & ~7;
+  // launch 1 fits twice per CU (LDS, registers): two co-resident workgroups overlap one's prologue
+  // and H stores with the other's MFMAs (free-running decoder rows: 656 workgroups); with at most one
+  // workgroup per CU to launch, extra dynamic LDS keeps it at one per CU
+  constexpr int kCUs = 256;
+  // (static LDS 52 KB; + 32 KB is past half of the CU's 160 KB)
+  const size_t solo = 32 * 1024;
   if (d->KS == 9)
-    hipLaunchKernelGGL((ffn_hidden_kernel<9>), dim3(n1), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((ffn_hidden_kernel<9>), dim3(n1), dim3(256), n1 <= kCUs ? solo : 0, s, p);
   else
-    hipLaunchKernelGGL((ffn_hidden_kernel<3>), dim3(n1), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((ffn_hidden_kernel<3>), dim3(n1), dim3(256), n1 <= kCUs ? solo : 0, s, p);
   FS2_CHECK_LAUNCH();
   // launch 2: 64-row tiles x 4 column quarters
   p.ntiles = ntiles64;
+  if (WIDE_TRACE) p.trace += 4096;
   const int n2 = (ntiles64 * 4 + 7) & ~7;
   if (d->F == 1024)
     hipLaunchKernelGGL((ffn_out_kernel<1024>), dim3(n2), dim3(256), 0, s, p);

@@ -261,6 +261,17 @@ FFN_FUSED_MIN_ROWS = 16384
 FFN_SPLIT_MIN_WG = 128
 
 
+def decoder_forms(P, rows):
+    """The decoder launch choices a host-known active row count makes (packed stage 2 with
+    ``rows_hint`` = rows): whether the FFN is the fused launch and its (tile rows, split) form --
+    the only arithmetic the row bucket changes (grids and early exits aside). Two row buckets with
+    equal forms give bit-identical decoder outputs (graphs.SynthGraphs' speculation relies on it)."""
+    F = P.dec_layers[0].b1.numel() if P.dec_layers else 0
+    tr, ns = ops.ffn_form(rows, F) if F else (0, 0)
+    fused = os.environ.get("FS2_FFN_FUSED", "1") == "2" or rows >= FFN_FUSED_MIN_ROWS or -(-rows // tr) * ns >= FFN_SPLIT_MIN_WG
+    return (fused, tr, ns)
+
+
 def ffn8_on():
     """FS2_FFN8=0: the cfg5 FFN as the two e4m3 fs2_conv1d launches (A/B)."""
     return os.environ.get("FS2_FFN8", "1") != "0"

@@ -373,10 +373,12 @@ def test_ffn_pre_padded_split_form(gpu, B, T, nsplit, seed):
                                           (5, 50, 54, 512, 3), (1, 300, 55, 1024, 9)])
 def test_ffn_wide_matches_float64_and_fused(gpu, B, T, seed, F, ks):
     """fs2_ffn_wide against the float64 statement (bf16 tolerance, as the fused launch) and against
-    the unsplit fused launch, which accumulates both GEMMs in the same k order: the hidden and the
-    pre-norm sums are the same f32 values, only the LayerNorm row statistics are summed in another
-    order -- at most 1 bf16 ulp of |y| <~ 4 (1.6e-2) on a few elements. Ragged lengths (0 / 1 /
-    shorter than the taps' reach), rows past the last 256-row tile, repeated launches identical."""
+    the unsplit fused launch. The wide form's conv-k loop runs channel-chunk-major (the x tile streams
+    into LDS chunk by chunk) where the fused kernel runs tap-major, so the f32 hidden sums round
+    differently: a hidden value can land one bf16 ulp apart, and the LayerNorm row statistics are
+    summed in another order -- measured within 2 bf16 ulps of |y| <~ 4 on a few percent of the
+    elements. Ragged lengths (0 / 1 / shorter than the taps' reach), rows past the last 256-row tile,
+    repeated launches identical."""
     ops, L = gpu
     W = _weights(ops, L, F=F, ks=ks, seed=seed)
     rng = np.random.default_rng(seed)
@@ -396,7 +398,7 @@ def test_ffn_wide_matches_float64_and_fused(gpu, B, T, seed, F, ks):
     err = (got.double() - ref).abs()
     assert float(err.max()) <= 3e-2 and float(err.mean()) <= 2e-3, (float(err.max()), float(err.mean()))
     d = (got.float() - fused.float()).abs()
-    assert float(d.max()) <= 1.6e-2 and float((d > 0).float().mean()) <= 0.01, (float(d.max()), float((d > 0).float().mean()))
+    assert float(d.max()) <= 3.2e-2 and float((d > 0).float().mean()) <= 0.05, (float(d.max()), float((d > 0).float().mean()))
 
 
 def test_ffn_wide_addvecs_packed_and_form_rule(gpu):

@@ -32,7 +32,7 @@ def main():
         torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / 16
     print(f"{dt * 1e3:.3f} ms per call, {sum(frames) / 8 / dt / 1e6:.2f} M frames/s, frames {frames}, "
-          f"captures {cap} + {synth.captures - cap} timed")
+          f"captures {cap} + {synth.captures - cap} timed, speculation hits {synth.spec_hits} misses {synth.spec_misses}")
 
 
 if __name__ == "__main__":
