@@ -106,8 +106,9 @@ constexpr int kLgkm0 = 0xC07F;
 // s_waitcnt immediate waiting for vmcnt <= n only (gfx9 encoding: vmcnt [3:0] + [15:14])
 constexpr int vm_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
 
-// MB = 16-row activation blocks per tile: 7 (112 rows: the full-chip decoder launches) or 4 (64 rows:
-// the split-hidden form of small launches, whose 4 splits x 64-row tiles fill the chip)
+// MB = 16-row activation blocks per tile: 7 (112 rows: the full-chip decoder launches), 6 (96 rows x 2
+// hidden splits: a free-running decoder's ~8-12k rows, 232 workgroups that stream half the weights
+// each) or 4 (64 rows: the split-hidden form of small launches, whose 4 splits x 64-row tiles fill the chip)
 template <int KS, int NCH, int MB, bool PRE = false>
 __global__ __launch_bounds__(256, 1) void ffn_fused_kernel(FfnArgs p) {
   constexpr int BM = 16 * MB;
@@ -1074,9 +1075,10 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
     if (d->pre_w == nullptr || d->pre_b == nullptr || d->pre_gamma == nullptr || d->pre_beta == nullptr ||
         d->pre_att_row_stride < kD || (d->pre_att_row_stride & 7) || d->pre_att == d->out)
       return FS2_EINVAL;
-    // packed unsplit launches on 112- or 64-row tiles (the decoder; 64 rows when free-running) or
-    // padded [B, T] rows with lengths, 64-row tiles in the split-hidden form (the encoder)
-    const bool dec_form = d->rows_dev != nullptr && S == 1;
+    // packed launches (the decoder: unsplit 112- or 64-row tiles, or 96-row tiles x 2 splits when
+    // free-running -- every split of a tile computes the prologue) or padded [B, T] rows with
+    // lengths, 64-row tiles in the split-hidden form (the encoder)
+    const bool dec_form = d->rows_dev != nullptr;
     const bool enc_form = d->rows_dev == nullptr && d->tile_rows == 64;
     if (!(dec_form || enc_form) || d->KS != 9 || d->F != 1024) return FS2_EUNSUPPORTED;
     const int64_t ab = M64 * d->pre_att_row_stride * 2;
@@ -1090,8 +1092,10 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
     p.be1 = d->pre_beta;
     p.eps1 = d->pre_eps;
   }
-  if (d->rows_max < 0 || !(d->tile_rows == 0 || d->tile_rows == 112 || d->tile_rows == 64)) return FS2_EINVAL;
-  const int MB = d->tile_rows == 64 ? 4 : 7, BM = 16 * MB;
+  if (d->rows_max < 0 || !(d->tile_rows == 0 || d->tile_rows == 112 || d->tile_rows == 96 || d->tile_rows == 64))
+    return FS2_EINVAL;
+  const int MB = d->tile_rows == 64 ? 4 : d->tile_rows == 96 ? 6 : 7, BM = 16 * MB;
+  if (MB == 6 && (d->KS != 9 || d->F != 1024)) return FS2_EUNSUPPORTED;  // instantiated for the model's FFN only
   const int64_t kPartBytes = part_bytes(MB);
   const int64_t Mg = (d->rows_dev != nullptr && d->rows_max > 0 && d->rows_max < M64) ? d->rows_max : M64;
   a.M = (int)Mg;
@@ -1131,7 +1135,12 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
     constexpr int ks = decltype(KSC)::value, nc = decltype(NCHC)::value;
     if (MB == 4)
       hipLaunchKernelGGL((ffn_fused_kernel<ks, nc, 4>), dim3(nwg), dim3(256), 0, s, p);
-    else
+    else if constexpr (ks == 9 && nc == 4) {
+      if (MB == 6)
+        hipLaunchKernelGGL((ffn_fused_kernel<9, 4, 6>), dim3(nwg), dim3(256), 0, s, p);
+      else
+        hipLaunchKernelGGL((ffn_fused_kernel<ks, nc, 7>), dim3(nwg), dim3(256), 0, s, p);
+    } else
       hipLaunchKernelGGL((ffn_fused_kernel<ks, nc, 7>), dim3(nwg), dim3(256), 0, s, p);
   };
   using I9 = std::integral_constant<int, 9>;
@@ -1140,6 +1149,8 @@ extern "C" int fs2_ffn(const fs2_ffn_desc *d, fs2_stream_t stream) {
   using C2 = std::integral_constant<int, 2>;
   if (pre && MB == 4)
     hipLaunchKernelGGL((ffn_fused_kernel<9, 4, 4, true>), dim3(nwg), dim3(256), 0, s, p);
+  else if (pre && MB == 6)
+    hipLaunchKernelGGL((ffn_fused_kernel<9, 4, 6, true>), dim3(nwg), dim3(256), 0, s, p);
   else if (pre)
     hipLaunchKernelGGL((ffn_fused_kernel<9, 4, 7, true>), dim3(nwg), dim3(256), 0, s, p);
   else if (d->KS == 9 && nch == 4)

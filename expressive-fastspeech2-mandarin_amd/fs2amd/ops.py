@@ -543,7 +543,11 @@ def rows_bucket(rows, capacity, step=1024):
 # shape, tools/kernel_probe.py enc_ffn): per 256-column hidden chunk, fixed cost (x tile, LN
 # epilogue), and the split hand-off (partial stores, arrival counter, partial loads) per nsplit.
 # Measured: 112-row tiles 90 / 59.6 / 45.8 us at nsplit 1 / 2 / 4; 64-row tiles 57.3 / 40.2 / 38.8.
-FFN_COST = {112: (20.0, 10.0, {1: 0.0, 2: 10.0, 4: 16.0}), 64: (13.0, 5.0, {1: 0.0, 2: 9.0, 4: 21.0})}
+# 96-row tiles only as 2 splits (round 6: a free-running decoder's 8-12k rows -> ~230 workgroups that
+# each stream half the weights; the per-CU weight stream, ~5.2 MB at ~70 GB/s, bounds the 64-row form
+# there), interpolated between the two measured tile heights.
+FFN_COST = {112: (20.0, 10.0, {1: 0.0, 2: 10.0, 4: 16.0}), 96: (17.5, 8.5, {2: 10.0}),
+            64: (13.0, 5.0, {1: 0.0, 2: 9.0, 4: 21.0})}
 
 
 def ffn_form(rows, F):
@@ -558,7 +562,7 @@ def ffn_form(rows, F):
     for tr, (chunk, base, over) in FFN_COST.items():
         tiles = -(-rows // tr)
         for s in (1, 2, 4):
-            if s > nch:
+            if s > nch or s not in over:
                 continue
             if s > 1 and (tiles > 1024 or 4096 + tiles * s * ffn_part_bytes(tr) > SPLITK_WS_BYTES):
                 continue
@@ -599,9 +603,11 @@ def ffn_pre_ok(x, layout, F, ks):
         return False
     form = ffn_form(ffn_launch_rows(x, layout), F)
     if layout is not None:
-        # packed unsplit launches: 112-row tiles (teacher-forced cfg2) or 64-row tiles (a
-        # free-running decoder of ~11k rows); FS2_FFN_PRE64=0 keeps the fc launch for the latter
-        return form == (112, 1) or (form == (64, 1) and os.environ.get("FS2_FFN_PRE64", "1") != "0")
+        # packed launches: unsplit 112-row tiles (teacher-forced cfg2), 96-row tiles x 2 splits (a
+        # free-running decoder of ~8-12k rows; every split computes the prologue) or unsplit 64-row
+        # tiles; FS2_FFN_PRE64=0 keeps the fc launch for the smaller forms
+        small = os.environ.get("FS2_FFN_PRE64", "1") != "0"
+        return form == (112, 1) or (form in ((64, 1), (96, 2)) and small)
     return form[0] == 64 and os.environ.get("FS2_FFN_PRE_ENC", "0") == "1"
 
 
@@ -609,7 +615,7 @@ def ffn(x, w_packed, b1, b2, *, ks, pad, ln, lens=None, addvec1=None, addvec2=No
         nsplit=None, tile_rows=None, next_qkv=None, pre=None):
     """PositionwiseFeedForward + residual + LayerNorm + mask in one launch (fs2_ffn): bf16 rows of
     256 (padded [B, T, 256] or packed [B*T, 256] in ``layout``); ``w_packed`` from
-    :func:`pack_ffn_weights`. The hidden [rows, F] never reaches HBM. ``tile_rows`` (112 / 64) and
+    :func:`pack_ffn_weights`. The hidden [rows, F] never reaches HBM. ``tile_rows`` (112 / 96 / 64) and
     ``nsplit`` (workgroups per row tile): None = :func:`ffn_form` of the row count the host knows
     (``layout.rows_hint`` or the capacity). ``next_qkv`` = (wqkv in :func:`pack_frag_rows` order,
     bqkv f32): the epilogue also projects the output rows to the next block's Q|K|V; returns

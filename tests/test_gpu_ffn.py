@@ -111,7 +111,7 @@ def test_ffn_matches_two_launch_path(gpu):
     assert float(d.max()) <= 3e-2 and float(d.mean()) <= 1e-3, (float(d.max()), float(d.mean()))
 
 
-@pytest.mark.parametrize("tile_rows,nsplit", [(112, 1), (112, 2), (112, 4), (64, 1), (64, 4)])
+@pytest.mark.parametrize("tile_rows,nsplit", [(112, 1), (112, 2), (112, 4), (96, 2), (64, 1), (64, 4)])
 @pytest.mark.parametrize("lens_l,T", [([37, 0, 130, 1, 64, 129, 130, 5], 130),
                                       ([430] * 3 + [2, 3, 4, 111, 112, 113, 224, 225], 430)])
 def test_ffn_packed_equals_padded(gpu, lens_l, T, tile_rows, nsplit):
@@ -163,7 +163,8 @@ def test_ffn_rejects_bad_shapes(gpu):
 
 
 @pytest.mark.parametrize("F,ks,nsplit,tile_rows", [(1024, 9, 2, 112), (1024, 9, 4, 112), (512, 3, 2, 112),
-                                                   (1024, 9, 4, 64), (1024, 9, 2, 64), (1024, 9, 1, 64)])
+                                                   (1024, 9, 4, 64), (1024, 9, 2, 64), (1024, 9, 1, 64),
+                                                   (1024, 9, 2, 96)])
 @pytest.mark.parametrize("packed", [False, True])
 def test_ffn_split_hidden(gpu, F, ks, nsplit, tile_rows, packed):
     """Split-hidden fs2_ffn: encoder-like padded rows with lens + speaker / emotion vectors, or
@@ -222,10 +223,54 @@ def test_ffn_form_rule(gpu):
     assert ns > 1 and -(-4096 // tr) * ns <= ops.FFN_SLOTS
     for rows in (1, 500, 4096, 11141, 24883, 200000):
         tr, ns = ops.ffn_form(rows, 1024)
-        assert tr in (112, 64) and ns in (1, 2, 4)
+        assert tr in (112, 96, 64) and ns in (1, 2, 4) and (tr != 96 or ns == 2)
         assert ns == 1 or 4096 + -(-rows // tr) * ns * ops.ffn_part_bytes(tr) <= ops.SPLITK_WS_BYTES
     with ops.splitk_enabled(False):
         assert ops.ffn_form(4096, 1024) == (112, 1)
+    # a free-running cfg2 decoder (~9-12k rows): 96-row tiles x 2 hidden splits (~230 workgroups)
+    assert ops.ffn_form(10240, 1024) == (96, 2) and ops.ffn_form(11264, 1024) == (96, 2)
+
+
+@pytest.mark.parametrize("B,T,seed", [(64, 180, 71), (8, 130, 72), (3, 37, 73)])
+def test_ffn_pre_packed_split_96(gpu, B, T, seed):
+    """The free-running decoder's form: packed rows, 96-row tiles x 2 hidden splits, the fc + residual
+    + LN prologue computed by both splits of a tile (round 6). Against the unsplit 112-row PRE launch
+    (the same h up to the prologue's per-tile halo rounding; the split partials summed in split
+    order: within 2 bf16 ulps) and a float64 statement within the FFN's bf16 tolerance; repeated
+    launches identical (counters reset themselves)."""
+    ops, L = gpu
+    W = _weights(ops, L, seed=seed)
+    g = torch.Generator(device=DEV).manual_seed(seed + 7)
+    lens = torch.randint(T // 2, T + 1, (B,), device=DEV, generator=g)
+    lens[0] = T
+    if B > 2:
+        lens[1], lens[2] = 0, 1
+    x = _x(B, T, lens, seed + 1)
+    att = _x(B, T, lens, seed + 2)
+    wfc = torch.randn(256, 256, device=DEV, generator=g) / 16
+    bfc = 0.1 * torch.randn(256, device=DEV, generator=g)
+    ln1 = (1 + 0.1 * torch.randn(256, device=DEV, generator=g), 0.1 * torch.randn(256, device=DEV, generator=g), 1e-5)
+    lay = ops.SeqLayout(lens, T)
+    pk = lambda t: _pack(lay, t)
+    pre = (pk(att), ops.pack_frag_rows(wfc), bfc, ln1)
+    kw = dict(ks=9, pad=4, ln=W["ln"], layout=lay, pre=pre)
+    outs = [ops.ffn(pk(x), W["w12"], W["b1"], W["b2"], tile_rows=96, nsplit=2, **kw) for _ in range(3)]
+    ref112 = ops.ffn(pk(x), W["w12"], W["b1"], W["b2"], tile_rows=112, nsplit=1, **kw)
+    torch.cuda.synchronize()
+    R = int(lay.cu[-1])
+    got = outs[0][:R]
+    for o in outs[1:]:
+        assert torch.equal(o[:R], got)
+    d = (got.float() - ref112[:R].float()).abs()
+    ulp = ref112[:R].float().abs().clamp(min=2 ** -8) * 2 ** -7
+    assert float((d / ulp).max()) <= 2.0, float((d / ulp).max())
+    h = torch.nn.functional.layer_norm(att.double() @ wfc.to(torch.bfloat16).double().t() + bfc.double() + x.double(),
+                                       (256,), ln1[0].double(), ln1[1].double(), ln1[2])
+    valid = (torch.arange(T, device=DEV)[None, :] < lens[:, None])
+    h = (h * valid[..., None]).to(torch.bfloat16)
+    refp = _ref(h, lens, W).reshape(-1, 256)[valid.reshape(-1)]
+    err = (got.double() - refp).abs()
+    assert float(err.max()) <= 0.1 and float(err.mean()) <= 6e-3, (float(err.max()), float(err.mean()))
 
 
 @pytest.mark.parametrize("tile_rows,nsplit,packed", [(112, 1, True), (64, 4, False), (112, 2, True), (64, 1, False)])
