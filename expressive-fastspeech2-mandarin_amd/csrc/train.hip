@@ -178,18 +178,25 @@ __global__ __launch_bounds__(256) void res_ln_bwd_kernel(const float *__restrict
 }
 
 // VariancePredictor layer (model/modules.py:218-235, train mode): y = dropout(LN(relu(a))).
-// Saves xhat / rstd; the backward reads a again for the relu mask.
+// Saves xhat / rstd; the backward reads a again for the relu mask. HEAD (the predictor's second
+// layer): also the predictor's output, out[r] = masked ? 0 : y[r] . hw + hb (linear_layer + squeeze
+// + masked_fill, modules.py:245-250) from the row still in registers; y itself is then not stored
+// (nothing else reads it).
+template <bool HEAD>
 __global__ __launch_bounds__(256) void relu_ln_fwd_kernel(const float *__restrict__ a, const float *__restrict__ gamma,
                                                           const float *__restrict__ beta, int64_t R, float eps,
                                                           uint32_t thr, float scale, const int64_t *seed, uint32_t salt,
                                                           float *__restrict__ y, bf16 *__restrict__ y_bf,
-                                                          float *__restrict__ xhat, float *__restrict__ rstd_out) {
+                                                          float *__restrict__ xhat, float *__restrict__ rstd_out,
+                                                          const float *__restrict__ hw, const float *__restrict__ hb,
+                                                          const bool *__restrict__ hmask, float *__restrict__ hout) {
   const int lane = threadIdx.x & 63;
   const int c = lane * 4;
   const uint32_t key = drop_key(seed, salt);
-  float g[4], bt[4];
+  float g[4], bt[4], w4[4] = {0.f, 0.f, 0.f, 0.f};
   load4(gamma + c, g);
   load4(beta + c, bt);
+  if constexpr (HEAD) load4(hw + c, w4);
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < R; row += nw) {
     float v[4];
@@ -216,36 +223,65 @@ __global__ __launch_bounds__(256) void relu_ln_fwd_kernel(const float *__restric
       for (int q = 0; q < 4; ++q) o[q] = ((k >> q) & 1) ? o[q] * scale : 0.0f;
     }
     store4(xhat + row * kD + c, v);
-    store4(y + row * kD + c, o);
+    if (y != nullptr) store4(y + row * kD + c, o);
     if (y_bf != nullptr) store4(y_bf + row * kD + c, o);
+    if constexpr (HEAD) {
+      const float hs = wave_sum((o[0] * w4[0] + o[1] * w4[1]) + (o[2] * w4[2] + o[3] * w4[3]));
+      if (lane == 0) hout[row] = (hmask != nullptr && hmask[row]) ? 0.0f : hs + hb[0];
+    }
     if (lane == 0) rstd_out[row] = rs;
   }
 }
 
 // dz = dy * keep * scale; dr = rstd * (g*dz - mean(g*dz) - xhat * mean(g*dz*xhat)); da = dr * (a > 0)
 // (bf16). part[blk][0..3][kD]: sum dz*xhat (gamma), sum dz (beta), sum da (the conv's bias).
+// HEAD: dy is not read but formed from the predictor output's gradient, dy[r][c] = dm[r] * hw[c]
+// (dm = masked ? 0 : dout[r]), and hpart[blk][kD + 4] gets the head's gradients: sum dm * y (its
+// weight; y recomputed from xhat, gamma, beta and the dropout mask) and sum dm (its bias, col kD).
+template <bool HEAD>
 __global__ __launch_bounds__(256) void relu_ln_bwd_kernel(const float *__restrict__ dy, const float *__restrict__ a,
                                                           const float *__restrict__ xhat, const float *__restrict__ rstd,
                                                           const float *__restrict__ gamma, int64_t R, uint32_t thr,
                                                           float scale, const int64_t *seed, uint32_t salt,
-                                                          bf16 *__restrict__ da, float *__restrict__ part) {
+                                                          bf16 *__restrict__ da, float *__restrict__ part,
+                                                          const float *__restrict__ dout, const bool *__restrict__ hmask,
+                                                          const float *__restrict__ hw, const float *__restrict__ beta,
+                                                          float *__restrict__ hpart) {
   __shared__ float red[3][4][kD];
+  __shared__ float hred[HEAD ? 4 : 1][HEAD ? kD + 4 : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c = lane * 4;
   const uint32_t key = drop_key(seed, salt);
-  float g[4];
+  float g[4], w4[4] = {0.f, 0.f, 0.f, 0.f}, bt[4] = {0.f, 0.f, 0.f, 0.f};
   load4(gamma + c, g);
+  if constexpr (HEAD) {
+    load4(hw + c, w4);
+    load4(beta + c, bt);
+  }
   float pg[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f}, pa[4] = {0.f, 0.f, 0.f, 0.f};
+  float ph[4] = {0.f, 0.f, 0.f, 0.f}, phb = 0.f;
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t row = (int64_t)blockIdx.x * 4 + wv; row < R; row += nw) {
     float d[4], xh[4], av[4], gd[4];
-    load4(dy + row * kD + c, d);
     load4(xhat + row * kD + c, xh);
     load4(a + row * kD + c, av);
-    if (thr != 0) {
-      const unsigned k = keep4(key, (uint32_t)(row * kD + c), thr);
+    unsigned keep = 0xf;
+    if (thr != 0) keep = keep4(key, (uint32_t)(row * kD + c), thr);
+    if constexpr (HEAD) {
+      const float dm = (hmask != nullptr && hmask[row]) ? 0.0f : dout[row];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) d[q] = ((k >> q) & 1) ? d[q] * scale : 0.0f;
+      for (int q = 0; q < 4; ++q) {
+        d[q] = dm * w4[q];
+        const float yq = ((keep >> q) & 1) ? (xh[q] * g[q] + bt[q]) * (thr != 0 ? scale : 1.0f) : 0.0f;
+        ph[q] += dm * yq;
+      }
+      phb += dm;
+    } else {
+      load4(dy + row * kD + c, d);
+    }
+    if (thr != 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = ((keep >> q) & 1) ? d[q] * scale : 0.0f;
     }
     const float rs = rstd[row];
     float s1 = 0.f, s2 = 0.f;
@@ -271,11 +307,19 @@ __global__ __launch_bounds__(256) void relu_ln_bwd_kernel(const float *__restric
     red[0][wv][c + q] = pg[q];
     red[1][wv][c + q] = pb[q];
     red[2][wv][c + q] = pa[q];
+    if constexpr (HEAD) hred[wv][c + q] = ph[q];
+  }
+  if constexpr (HEAD) {
+    if (lane < 4) hred[wv][kD + lane] = lane == 0 ? phb : 0.0f;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 3 * kD; i += 256) {
     const int k = i / kD, col = i - k * kD;
     part[(int64_t)blockIdx.x * 3 * kD + i] = (red[k][0][col] + red[k][1][col]) + (red[k][2][col] + red[k][3][col]);
+  }
+  if constexpr (HEAD) {
+    for (int i = threadIdx.x; i < kD + 4; i += 256)
+      hpart[(int64_t)blockIdx.x * (kD + 4) + i] = (hred[0][i] + hred[1][i]) + (hred[2][i] + hred[3][i]);
   }
 }
 
@@ -446,9 +490,9 @@ extern "C" int fs2_relu_ln_fwd(const float *a, const float *gamma, const float *
   if (R < 0 || !(p_drop >= 0.0f && p_drop < 1.0f) || (p_drop > 0.0f && seed == nullptr)) return FS2_EINVAL;
   if (R == 0) return FS2_OK;
   const int64_t b64 = (R + 3) / 4;
-  hipLaunchKernelGGL(relu_ln_fwd_kernel, dim3((unsigned)(b64 < 2048 ? b64 : 2048)), dim3(256), 0, as_stream(stream), a,
-                     gamma, beta, R, eps, drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt, y,
-                     reinterpret_cast<bf16 *>(y_bf), xhat, rstd);
+  hipLaunchKernelGGL(relu_ln_fwd_kernel<false>, dim3((unsigned)(b64 < 2048 ? b64 : 2048)), dim3(256), 0,
+                     as_stream(stream), a, gamma, beta, R, eps, drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed,
+                     (uint32_t)salt, y, reinterpret_cast<bf16 *>(y_bf), xhat, rstd, nullptr, nullptr, nullptr, nullptr);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }
@@ -478,9 +522,9 @@ extern "C" int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xha
   }
   const int64_t b64 = (R + 3) / 4;
   const int grid = (int)(b64 < kLnBlocks ? b64 : kLnBlocks);
-  hipLaunchKernelGGL(relu_ln_bwd_kernel, dim3(grid), dim3(256), 0, s, dy, a, xhat, rstd, gamma, R,
+  hipLaunchKernelGGL(relu_ln_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, dy, a, xhat, rstd, gamma, R,
                      drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt,
-                     reinterpret_cast<bf16 *>(da), ws);
+                     reinterpret_cast<bf16 *>(da), ws, nullptr, nullptr, nullptr, nullptr, nullptr);
   if (defer) {
     FS2_CHECK_LAUNCH();
     return FS2_OK;
@@ -488,6 +532,71 @@ extern "C" int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xha
   hipLaunchKernelGGL(ln_finish_kernel, dim3(3 * kD / 64), dim3(256), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
+}
+
+// The VariancePredictor's second layer with its head (model/modules.py:230-250 in train mode): the
+// relu + LN + dropout of fs2_relu_ln_fwd and out = masked_fill(y . hw + hb, mask, 0) in one launch
+// (no y tensor); the backward takes dout (the predictor output's gradient) instead of dy. The head's
+// gradients (dhw [kD], dhb [1]) are per-block partials in the workspace after the LN ones, finished
+// here or (defer) by fs2_reduce_batch_launch kind 2.
+extern "C" int64_t fs2_relu_ln_head_bwd_ws_bytes(int D) {
+  return fs2_res_ln_bwd_ws_bytes(D) + (int64_t)kLnBlocks * (D + 4) * (int64_t)sizeof(float);
+}
+
+extern "C" int fs2_relu_ln_head_fwd(const float *a, const float *gamma, const float *beta, int64_t R, int D, float eps,
+                                    float p_drop, const int64_t *seed, int salt, void *y_bf, float *xhat, float *rstd,
+                                    const float *hw, const float *hb, const bool *hmask, float *hout,
+                                    fs2_stream_t stream) {
+  if (a == nullptr || gamma == nullptr || beta == nullptr || xhat == nullptr || rstd == nullptr || hw == nullptr ||
+      hb == nullptr || hout == nullptr)
+    return FS2_EINVAL;
+  if (D != kD) return FS2_EUNSUPPORTED;
+  if (R < 0 || !(p_drop >= 0.0f && p_drop < 1.0f) || (p_drop > 0.0f && seed == nullptr)) return FS2_EINVAL;
+  if (R == 0) return FS2_OK;
+  const int64_t b64 = (R + 3) / 4;
+  hipLaunchKernelGGL(relu_ln_fwd_kernel<true>, dim3((unsigned)(b64 < 2048 ? b64 : 2048)), dim3(256), 0,
+                     as_stream(stream), a, gamma, beta, R, eps, drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed,
+                     (uint32_t)salt, nullptr, reinterpret_cast<bf16 *>(y_bf), xhat, rstd, hw, hb, hmask, hout);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+extern "C" int fs2_relu_ln_head_bwd(const float *dout, const bool *hmask, const float *hw, const float *beta,
+                                    const float *a, const float *xhat, const float *rstd, const float *gamma,
+                                    int64_t R, int D, float p_drop, const int64_t *seed, int salt, void *da,
+                                    float *dgamma, float *dbeta, float *dbias, float *dhw, float *dhb, int accumulate,
+                                    int defer, float *ws, int64_t ws_bytes, fs2_stream_t stream) {
+  if (dout == nullptr || hw == nullptr || beta == nullptr || a == nullptr || xhat == nullptr || rstd == nullptr ||
+      gamma == nullptr || da == nullptr || ws == nullptr ||
+      ((dgamma == nullptr || dbeta == nullptr || dhw == nullptr || dhb == nullptr) && !defer))
+    return FS2_EINVAL;
+  if (D != kD) return FS2_EUNSUPPORTED;
+  if (R <= 0 || !(p_drop >= 0.0f && p_drop < 1.0f) || (p_drop > 0.0f && seed == nullptr)) return FS2_EINVAL;
+  if (ws_bytes < fs2_relu_ln_head_bwd_ws_bytes(D)) return FS2_EINVAL;
+  hipStream_t s = as_stream(stream);
+  const int64_t b64 = (R + 3) / 4;
+  const int grid = (int)(b64 < kLnBlocks ? b64 : kLnBlocks);
+  float *hpart = ws + (int64_t)kLnBlocks * 3 * kD;
+  hipLaunchKernelGGL(relu_ln_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, nullptr, a, xhat, rstd, gamma, R,
+                     drop_threshold(p_drop), 1.0f / (1.0f - p_drop), seed, (uint32_t)salt,
+                     reinterpret_cast<bf16 *>(da), ws, dout, hmask, hw, beta, hpart);
+  if (defer) {
+    FS2_CHECK_LAUNCH();
+    return FS2_OK;
+  }
+  hipLaunchKernelGGL(ln_finish_kernel, dim3(3 * kD / 64), dim3(256), 0, s, ws, grid, dgamma, dbeta, dbias, accumulate);
+  FS2_CHECK_LAUNCH();
+  fs2_reduce_batch rb{};
+  rb.n = 1;
+  rb.d[0].part = hpart;
+  rb.d[0].M = kD + 4;
+  rb.d[0].S = grid;
+  rb.d[0].kind = 2;
+  rb.d[0].split = kD;
+  rb.d[0].accumulate = accumulate;
+  rb.d[0].out0 = dhw;
+  rb.d[0].out1 = dhb;
+  return fs2_reduce_batch_launch(&rb, stream);
 }
 
 extern "C" int fs2_embedding_bwd(const int64_t *tokens, int64_t n, const float *dy, int64_t dy_row_stride, int V,
@@ -1631,16 +1740,71 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
   for (int j = 1; j < a.n; ++j)
     if (a.d[j].blk0 <= (int64_t)blockIdx.x) i = j;
   const fs2_reduce_desc &d = a.d[i];
+  if (d.kind == 1 && d.KS > 1) {
+    // a wide-tap weight gradient: partials [S][KS][N][C] -> out[n][c][k]. The plain mapping below
+    // scatters every store KS floats apart (36 B at KS = 9: a partial line per 4 bytes, read-modify-
+    // write when accumulating); here a block owns (n, 256 channels): each thread sums its channel's
+    // KS taps over the S splits (coalesced loads per tap, the same fixed split order), the block
+    // transposes them through LDS and stores its 256 x KS contiguous outputs coalesced.
+    __shared__ float tr[256 * 9];
+    const int KS = d.KS, C = d.C, N = d.N;
+    const int cb = (C + 255) / 256;
+    const int64_t bl = (int64_t)blockIdx.x - d.blk0;
+    const int n = (int)(bl / cb), c0 = (int)(bl - (int64_t)n * cb) * 256;
+    const int cn = min(256, C - c0), t = threadIdx.x;
+    if (t < cn) {
+      // every (tap, split) load issued before the first add (a dependent loop paid one memory
+      // latency per load: ~100 us per batched launch); S <= 8 for wide taps (wgrad_splits)
+      const float *pp = d.part + (int64_t)n * C + c0 + t;
+      const int64_t NC = (int64_t)N * C;
+      float v[9][8];
+#pragma unroll
+      for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2)
+          v[k][s2] = (k < KS && s2 < d.S) ? pp[(int64_t)s2 * d.M + k * NC] : 0.0f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        if (k < KS) {
+          float acc = v[k][0];
+#pragma unroll
+          for (int s2 = 1; s2 < 8; ++s2)
+            if (s2 < d.S) acc += v[k][s2];
+          tr[t * KS + k] = acc;
+        }
+      }
+    }
+    __syncthreads();
+    const int which = n / d.split;
+    float *base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
+    if (base == nullptr) return;
+    float *dst = base + ((int64_t)(n - which * d.split) * C + c0) * KS;
+    for (int e = t; e < cn * KS; e += 256) dst[e] = d.accumulate ? dst[e] + tr[e] : tr[e];
+    return;
+  }
   const int64_t col0 = (((int64_t)blockIdx.x - d.blk0) * 256 + threadIdx.x) * 4;
   if (col0 >= d.M) return;
-  float4 acc = *reinterpret_cast<const float4 *>(d.part + col0);
-#pragma unroll 4
-  for (int k = 1; k < d.S; ++k) {
-    const float4 v = *reinterpret_cast<const float4 *>(d.part + (int64_t)k * d.M + col0);
-    acc.x += v.x;
-    acc.y += v.y;
-    acc.z += v.z;
-    acc.w += v.w;
+  // the splits in groups of 8: all 8 loads of a group issued before its adds (one memory latency per
+  // group, not per split), summed in split order
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k0 = 0; k0 < d.S; k0 += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = k0 + j < d.S ? *reinterpret_cast<const float4 *>(d.part + (int64_t)(k0 + j) * d.M + col0)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (k0 + j >= d.S) break;
+      if (k0 + j == 0) {
+        acc = v[0];
+      } else {
+        acc.x += v[j].x;
+        acc.y += v[j].y;
+        acc.z += v[j].z;
+        acc.w += v[j].w;
+      }
+    }
   }
   const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
 #pragma unroll
@@ -1652,6 +1816,10 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
       const int64_t which = col / d.split;
       base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
       off = col - which * d.split;
+    } else if (d.kind == 2) {  // a vector and one scalar: m < split -> out0[m], m == split -> out1[0]
+      if (col > d.split) continue;
+      base = col < d.split ? d.out0 : d.out1;
+      off = col < d.split ? col : 0;
     } else {  // weight gradient partials [S][KS][N][C] -> out[n][c][k] (rows split into parameters)
       const int64_t NC = (int64_t)d.N * d.C;
       const int k = (int)(col / NC);
@@ -1673,12 +1841,14 @@ extern "C" int fs2_reduce_batch_launch(fs2_reduce_batch *a, fs2_stream_t stream)
   int64_t blk = 0;
   for (int i = 0; i < a->n; ++i) {
     fs2_reduce_desc &d = a->d[i];
-    if (d.part == nullptr || d.S <= 0 || d.M <= 0 || (d.M & 3) || d.split <= 0 || (d.kind != 0 && d.kind != 1) ||
+    if (d.part == nullptr || d.S <= 0 || d.M <= 0 || (d.M & 3) || d.split <= 0 || (d.kind < 0 || d.kind > 2) ||
         (reinterpret_cast<uintptr_t>(d.part) & 15))
       return FS2_EINVAL;
-    if (d.kind == 1 && (d.KS <= 0 || d.N <= 0 || d.C <= 0 || (int64_t)d.KS * d.N * d.C != d.M)) return FS2_EINVAL;
+    if (d.kind == 1 && (d.KS <= 0 || d.KS > 9 || d.N <= 0 || d.C <= 0 || (int64_t)d.KS * d.N * d.C != d.M))
+      return FS2_EINVAL;
+    if (d.kind == 1 && d.KS > 1 && d.S > 8) return FS2_EINVAL;  // the wide-tap path sums <= 8 splits
     d.blk0 = blk;
-    blk += (d.M + 1023) / 1024;
+    blk += d.kind == 1 && d.KS > 1 ? (int64_t)d.N * ((d.C + 255) / 256) : (d.M + 1023) / 1024;
   }
   if (blk >= (1LL << 31)) return FS2_EUNSUPPORTED;
   hipLaunchKernelGGL(reduce_batch_kernel, dim3((unsigned)blk), dim3(256), 0, as_stream(stream), *a);

@@ -205,6 +205,10 @@ SIGNATURES = {
     "fs2_res_ln_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p, _i, _p, _p, _p, _p, _p, _i, _i, _p, _i64, _p]),
     "fs2_relu_ln_fwd": (_i, [_p, _p, _p, _i64, _i, _f, _f, _p, _i, _p, _p, _p, _p, _p]),
     "fs2_relu_ln_bwd": (_i, [_p, _p, _p, _p, _p, _i64, _i, _f, _p, _i, _p, _p, _p, _p, _i, _i, _p, _i64, _p]),
+    "fs2_relu_ln_head_fwd": (_i, [_p, _p, _p, _i64, _i, _f, _f, _p, _i, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "fs2_relu_ln_head_bwd_ws_bytes": (_i64, [_i]),
+    "fs2_relu_ln_head_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _p, _i, _p, _p, _p, _p, _p, _p, _i, _i,
+                                  _p, _i64, _p]),
     "fs2_embedding_bwd": (_i, [_p, _i64, _p, _i64, _i, _i, _i, _p, _i, _p]),
     "fs2_loss_ws_bytes": (_i64, []),
     "fs2_loss_fwd": (_i, [_p, _p, _p, _p, _i64, _p]),

@@ -9,9 +9,16 @@ import torch
 import torch.nn as nn
 
 
+_G6 = {}
+
+
 class _LossFn(torch.autograd.Function):
     """The five masked means + total on fs2_loss_fwd (one reduction, deterministic) and all five
-    prediction gradients on fs2_loss_bwd (one pass): 3 launches instead of ~80 small torch ones."""
+    prediction gradients on fs2_loss_bwd (one pass): 3 launches instead of ~80 small torch ones.
+    The six losses are separate outputs whose gradients are not materialised: a step that
+    back-propagates the total alone (train.py:85-86) hands fs2_loss_bwd [g, 0, 0, 0, 0, 0] through ONE
+    copy into a persistent zero vector (unbind's backward zero-filled five scalars and stacked them:
+    seven launches)."""
 
     @staticmethod
     def forward(ctx, mel, post, p, e, logd, mel_tgt, p_tgt, e_tgt, d_tgt, mv, pm, em, dm):
@@ -19,11 +26,22 @@ class _LossFn(torch.autograd.Function):
         out, stats, args, keep = ops.loss_fwd(mel, post, p, e, logd, mel_tgt, p_tgt, e_tgt, d_tgt, mv, pm, em, dm)
         ctx.args, ctx.keep, ctx.stats = args, keep, stats
         ctx.shapes = (mel.shape, post.shape, p.shape, e.shape, logd.shape)
-        return out
+        ctx.set_materialize_grads(False)
+        return tuple(out.unbind())
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, *gs):
         from . import ops
+        dev = ctx.keep[0].device
+        if all(x is None for x in gs):
+            return (None,) * 13
+        if gs[0] is not None and all(x is None for x in gs[1:]):
+            g = _G6.get(dev)
+            if g is None:
+                g = _G6[dev] = torch.zeros(6, device=dev, dtype=torch.float32)
+            g[:1].copy_(gs[0].reshape(1))
+        else:
+            g = torch.stack([torch.zeros((), device=dev) if x is None else x.float().reshape(()) for x in gs])
         grads = ops.loss_bwd(ctx.args, ctx.keep, g, ctx.stats, ctx.shapes)
         return (*grads, None, None, None, None, None, None, None, None)
 
@@ -43,7 +61,6 @@ class FastSpeech2Loss(nn.Module):
         (mel_pred, postnet_pred, pitch_pred, energy_pred, log_d_pred, _, src_masks, mel_masks, _, _) = predictions
         src_valid = ~src_masks
         mel_valid = ~mel_masks
-        log_d_targets = torch.log(duration_targets.float() + 1).detach()
         mel_targets = mel_targets[:, : mel_valid.shape[1], :].detach()
         pitch_targets, energy_targets = pitch_targets.detach(), energy_targets.detach()
 
@@ -60,7 +77,8 @@ class FastSpeech2Loss(nn.Module):
             out = _LossFn.apply(mel_pred, postnet_pred, pitch_pred, energy_pred, log_d_pred, mel_targets,
                                 pitch_targets, energy_targets, duration_targets, mel_valid,
                                 sel(self.pitch_feature_level), sel(self.energy_feature_level), src_valid)
-            return tuple(out.unbind())
+            return out
+        log_d_targets = torch.log(duration_targets.float() + 1).detach()
         mv = mel_valid.unsqueeze(-1)
         mel_loss = mmean((mel_pred - mel_targets).abs(), mv)
         postnet_mel_loss = mmean((postnet_pred - mel_targets).abs(), mv)

@@ -1330,6 +1330,56 @@ def relu_ln_bwd(dy, a, xhat, rstd, gamma, p_drop=0.0, seed=None, salt=0, dgamma=
     return da, dgamma, dbeta, dbias
 
 
+def relu_ln_head_fwd(a, gamma, beta, eps, hw, hb, mask, p_drop=0.0, seed=None, salt=0):
+    """The VariancePredictor's second layer and its head in one launch (fs2_relu_ln_head_fwd):
+    out = masked_fill(dropout(LayerNorm(relu(a))) . hw + hb, mask, 0) over rows of 256 (a f32
+    [..., 256], hw f32 [256], hb f32 [1], mask bool [...]). Returns (out f32 [...], xhat, rstd)."""
+    _gpu(a, gamma, beta, hw, hb, mask, seed)
+    assert a.dtype == torch.float32 and a.is_contiguous() and a.shape[-1] == 256
+    assert hw.numel() == 256 and hb.numel() == 1 and hw.is_contiguous()
+    R = a.numel() // 256
+    if mask is not None:
+        assert mask.dtype == torch.bool and mask.numel() == R
+        mask = mask.contiguous()
+    out = torch.empty(a.shape[:-1], device=a.device, dtype=torch.float32)
+    xhat = torch.empty_like(a)
+    rstd = torch.empty(R, device=a.device, dtype=torch.float32)
+    L.check(_lib.fs2_relu_ln_head_fwd(_ptr(a), _ptr(gamma), _ptr(beta), R, 256, float(eps), float(p_drop), _ptr(seed),
+                                      int(salt), None, _ptr(xhat), _ptr(rstd), _ptr(hw), _ptr(hb), _ptr(mask),
+                                      _ptr(out), _stream(a)), "fs2_relu_ln_head_fwd")
+    return out, xhat, rstd
+
+
+def relu_ln_head_bwd(dout, mask, hw, beta, a, xhat, rstd, gamma, p_drop=0.0, seed=None, salt=0, dgamma=None,
+                     dbeta=None, dbias=None, dhw=None, dhb=None, accumulate=False, defer=None):
+    """Backward of :func:`relu_ln_head_fwd` (fs2_relu_ln_head_bwd): from dout (the predictor output's
+    gradient) -> (da bf16, dgamma, dbeta, dbias, dhw, dhb)."""
+    _gpu(dout, mask, hw, beta, a, xhat, rstd, gamma, seed)
+    dout = dout.contiguous()
+    R = a.numel() // 256
+    assert dout.dtype == torch.float32 and dout.numel() == R
+    da = torch.empty(a.shape, device=a.device, dtype=torch.bfloat16)
+    new = lambda n: torch.empty(n, device=a.device, dtype=torch.float32)
+    dgamma = new(256) if dgamma is None else dgamma
+    dbeta = new(256) if dbeta is None else dbeta
+    dbias = new(256) if dbias is None else dbias
+    dhw = new(256) if dhw is None else dhw
+    dhb = new(1) if dhb is None else dhb
+    ws = torch.empty(_lib.fs2_relu_ln_head_bwd_ws_bytes(256) // 4, device=a.device, dtype=torch.float32)
+    L.check(_lib.fs2_relu_ln_head_bwd(_ptr(dout), _ptr(mask.contiguous() if mask is not None else None), _ptr(hw),
+                                      _ptr(beta), _ptr(a), _ptr(xhat), _ptr(rstd), _ptr(gamma), R, 256, float(p_drop),
+                                      _ptr(seed), int(salt), _ptr(da), _ptr(dgamma), _ptr(dbeta), _ptr(dbias),
+                                      _ptr(dhw), _ptr(dhb), 1 if accumulate else 0, 1 if defer is not None else 0,
+                                      _ptr(ws), ws.numel() * 4, _stream(a)), "fs2_relu_ln_head_bwd")
+    if defer is not None:
+        S = _lib.fs2_ln_bwd_parts(R)
+        acc = 1 if accumulate else 0
+        _defer_add(defer, ws, M=3 * 256, S=S, kind=0, split=256, accumulate=acc, outs=(dgamma, dbeta, dbias))
+        head = ws[(_lib.fs2_res_ln_bwd_ws_bytes(256) // 4):]
+        _defer_add(defer, head, M=256 + 4, S=S, kind=2, split=256, accumulate=acc, outs=(dhw, dhb))
+    return da, dgamma, dbeta, dbias, dhw, dhb
+
+
 def embedding_bwd(tokens, dy, V, padding_idx=None, out=None, accumulate=False):
     """nn.Embedding weight gradient (fs2_embedding_bwd): tokens int64 [...], dy f32 [..., D] ->
     out f32 [V, D], deterministic; padding_idx row zero (or untouched when accumulating)."""

@@ -242,6 +242,22 @@ class TrainStep:
         cur.wait_stream(self._stream)
         return out
 
+    @staticmethod
+    def _static_inputs(batch):
+        """The captured step's static inputs as views of ONE byte slab (widest element type first, so
+        every view is aligned): a later batch is copied in by one concatenating launch instead of one
+        copy per tensor (~5 us each inside the step). Returns (static dict, (key order, slab))."""
+        order = sorted((k for k, v in batch.items() if torch.is_tensor(v)), key=lambda k: -batch[k].element_size())
+        flat = [batch[k].contiguous().view(-1).view(torch.uint8) for k in order]
+        slab = torch.cat(flat)
+        static = dict(batch)
+        off = 0
+        for k, f in zip(order, flat):
+            n = f.numel()
+            static[k] = slab[off:off + n].view(batch[k].dtype).view(batch[k].shape)
+            off += n
+        return static, (order, slab)
+
     def _graphed(self, batch):
         # warm-up by the calls of THIS TrainStep (at least one eager step, whatever `warmup` says): a
         # step resumed from a checkpoint (current_step > warmup) still runs the lazy one-time setup
@@ -261,7 +277,7 @@ class TrainStep:
                 # all-reduces) is capturing, and the watchdog aborts the process on that error
                 torch.cuda.synchronize(self.device)
                 time.sleep(0.5)
-            static = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in batch.items()}
+            static, self._slab = self._static_inputs(batch)
             self.optimizer._update_learning_rate()
             g = torch.cuda.CUDAGraph()
             cur = torch.cuda.current_stream(self.device)
@@ -279,9 +295,13 @@ class TrainStep:
             self.step_no += 1
             return list(torch.stack(losses).unbind())
         _, g, static, losses = self._graph
-        for k, v in batch.items():
-            if torch.is_tensor(v):
-                static[k].copy_(v, non_blocking=True)
+        order, slab = self._slab
+        if all(batch[k].device == slab.device for k in order):
+            # one launch: the batch's bytes into the slab the static inputs are views of
+            torch.cat([batch[k].contiguous().view(-1).view(torch.uint8) for k in order], out=slab)
+        else:
+            for k in order:
+                static[k].copy_(batch[k], non_blocking=True)
         self.optimizer._update_learning_rate()
         g.replay()
         self.step_no += 1

@@ -471,10 +471,12 @@ class PostNetFn(torch.autograd.Function):
                                                   bn.running_var, use_tanh=not last, p_drop=p_drop, seed=seed,
                                                   salt=salt + i, residual=mel.detach() if last else None,
                                                   want_bf16=not last, want_f32=last)
-            if bn.num_batches_tracked is not None:
-                bn.num_batches_tracked.add_(1)
             saved.append((x_bf, z, mean, rstd, wT, pad, KS))
             x_bf, out = yb, yf
+        # BatchNorm's step counters, all layers in one multi-tensor launch (one add kernel each before)
+        nbt = [seq[1].num_batches_tracked for seq in convs if seq[1].num_batches_tracked is not None]
+        if nbt:
+            torch._foreach_add_(nbt, 1)
         ctx.saved = saved
         ctx.meta = (p_drop, seed, salt)
         ctx.save_for_backward(*params)
@@ -590,6 +592,51 @@ class VPLayerFn(torch.autograd.Function):
         return dx, None, None, dw, db, dg, dbe
 
 
+class VPHeadLayerFn(torch.autograd.Function):
+    """The VariancePredictor's second layer WITH its head (model/modules.py:225-250, train mode):
+    Conv (fs2_conv1d, f32 out) -> fs2_relu_ln_head_fwd (relu + LayerNorm + dropout + Linear(256->1) +
+    masked_fill in one launch: no y tensor, no hipBLASLt GEMV and elementwise launches); backward
+    fs2_relu_ln_head_bwd (the LayerNorm and head gradients straight from the predictor output's
+    gradient) -> input gradient conv -> fs2_conv_wgrad. FS2_VP_HEAD_FUSED=0: VPLayerFn + F.linear."""
+
+    @staticmethod
+    def forward(ctx, x, x_bf, mask, meta, w, b, g, be, hw, hb):
+        pad, p_drop, seed, salt, eps = meta[:5]
+        N, Cin, KS = w.shape
+        BF = L.FS2_BF16
+        xb = x_bf if x_bf is not None else x.to(torch.bfloat16)
+        wf, wT = meta[5] if len(meta) > 5 and meta[5] is not None else (ops.pack_conv_weight(w, BF), _packT_any(w))
+        a = ops.conv1d(xb, wf, b.detach(), cin=Cin, ks=KS, pad=pad, compute=BF, epilogue=L.EPI_BIAS,
+                       out_dtype=L.FS2_F32)
+        out, xh, rs = ops.relu_ln_head_fwd(a, g.detach(), be.detach(), eps, hw.detach().reshape(-1), hb.detach(), mask,
+                                           p_drop, seed, salt)
+        ctx.save_for_backward(xb, a, xh, rs, w, b, g, be, hw, hb, mask)
+        ctx.meta = meta
+        ctx.wT = wT
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        xb, a, xh, rs, w, b, g, be, hw, hb, mask = ctx.saved_tensors
+        pad, p_drop, seed, salt, eps = ctx.meta[:5]
+        N, Cin, KS = w.shape
+        sink = _SINK[0] and all(t.grad is not None for t in (w, b, g, be, hw, hb))
+        G = (lambda t: t.grad) if sink else (lambda t: None)
+        q = _DEFER[0] if sink else None
+        da, dg, dbe, db, dhw, dhb = ops.relu_ln_head_bwd(
+            dout.float(), mask, hw.detach().reshape(-1), be.detach(), a, xh, rs, g.detach(), p_drop, seed, salt,
+            dgamma=G(g), dbeta=G(be), dbias=G(b), dhw=None if G(hw) is None else G(hw).view(-1), dhb=G(hb),
+            accumulate=sink, defer=q)
+        dw, _ = ops.conv_wgrad(da, xb, KS, pad, dw=G(w), accumulate=sink, defer=q)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.conv1d(da, ctx.wT, None, cin=N, ks=KS, pad=KS - 1 - pad, compute=L.FS2_BF16,
+                            epilogue=L.EPI_BIAS, out_dtype=L.FS2_F32)
+        if sink:
+            return dx, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, dw, db, dg, dbe, dhw.view_as(hw), dhb.view_as(hb)
+
+
 def _vp_fused(vp, x, mask, training, seed, salt):
     cl = vp.conv_layer
     c1, c2 = cl.conv1d_1.conv, cl.conv1d_2.conv
@@ -599,9 +646,14 @@ def _vp_fused(vp, x, mask, training, seed, salt):
     pk = _PACKED[0]
     h, hb = VPLayerFn.apply(x.contiguous(), None, ((k - 1) // 2, p1, seed, salt, cl.layer_norm_1.eps, pk.get(c1)),
                             c1.weight, c1.bias, cl.layer_norm_1.weight, cl.layer_norm_1.bias)
+    lin = vp.linear_layer
+    if os.environ.get("FS2_VP_HEAD_FUSED", "1") != "0" and lin.in_features == 256 and lin.out_features == 1 \
+            and lin.bias is not None and mask is not None and mask.shape == x.shape[:-1]:
+        return VPHeadLayerFn.apply(h, hb, mask, (1, p2, seed, salt + 1, cl.layer_norm_2.eps, pk.get(c2)), c2.weight,
+                                   c2.bias, cl.layer_norm_2.weight, cl.layer_norm_2.bias, lin.weight, lin.bias)
     h, _ = VPLayerFn.apply(h, hb, (1, p2, seed, salt + 1, cl.layer_norm_2.eps, pk.get(c2)), c2.weight, c2.bias,
                            cl.layer_norm_2.weight, cl.layer_norm_2.bias)
-    out = F.linear(h, vp.linear_layer.weight, vp.linear_layer.bias).squeeze(-1)
+    out = F.linear(h, lin.weight, lin.bias).squeeze(-1)
     return out.masked_fill(mask, 0.0)
 
 

@@ -693,6 +693,24 @@ int fs2_relu_ln_bwd(const float *dy, const float *a, const float *xhat, const fl
                     int64_t R, int D, float p_drop, const int64_t *seed, int salt, void *da, float *dgamma,
                     float *dbeta, float *dbias, int accumulate, int defer, float *ws, int64_t ws_bytes,
                     fs2_stream_t stream);
+/* fs2_relu_ln_head_fwd / fs2_relu_ln_head_bwd — the VariancePredictor's second layer WITH its head
+ *   (model/modules.py:230-250, train mode): fs2_relu_ln_fwd's relu + LayerNorm + dropout and
+ *   hout[r] = hmask[r] ? 0 : y[r] . hw + hb[0] (linear_layer + squeeze + masked_fill) in one launch; y
+ *   itself is not written (optional bf16 copy). The backward takes dout (the predictor output's
+ *   gradient) in place of dy (dy[r][c] = masked ? 0 : dout[r] * hw[c]) and also gives the head's
+ *   dhw [D] / dhb [1]; defer != 0: the LN partials (first fs2_res_ln_bwd_ws_bytes(D) bytes of ws, S =
+ *   fs2_ln_bwd_parts(R)) and the head's [S][D + 4] partials after them go to fs2_reduce_batch_launch
+ *   (kinds 0 and 2). ws: fs2_relu_ln_head_bwd_ws_bytes(D). Replaces the reference's F.linear +
+ *   masked_fill pair (and their backward) for the bf16 training path. */
+int fs2_relu_ln_head_fwd(const float *a, const float *gamma, const float *beta, int64_t R, int D, float eps,
+                         float p_drop, const int64_t *seed, int salt, void *y_bf, float *xhat, float *rstd,
+                         const float *hw, const float *hb, const bool *hmask, float *hout, fs2_stream_t stream);
+int64_t fs2_relu_ln_head_bwd_ws_bytes(int D);
+int fs2_relu_ln_head_bwd(const float *dout, const bool *hmask, const float *hw, const float *beta, const float *a,
+                         const float *xhat, const float *rstd, const float *gamma, int64_t R, int D, float p_drop,
+                         const int64_t *seed, int salt, void *da, float *dgamma, float *dbeta, float *dbias,
+                         float *dhw, float *dhb, int accumulate, int defer, float *ws, int64_t ws_bytes,
+                         fs2_stream_t stream);
 /* fs2_embedding_bwd — nn.Embedding's weight gradient (transformer/Models.py:82 src_word_emb with
  *   padding_idx, model/modules.py:80-100 pitch / energy tables, fastspeech2.py:101-110 speaker /
  *   emotion tables): out[v][:] (+)= sum over i with tokens[i] == v, in increasing i, of dy[i][:]
@@ -804,7 +822,9 @@ int fs2_adam_flat(float *grads, int64_t n, const fs2_adam_param *params_dev, int
  * launch (the fused training nodes' gradient finishes, batched after the backward): per descriptor
  * out[m] (+)= sum over s < S of part[s * M + m] (fixed order), scattered by kind:
  *   0: m -> (out0 | out1 | out2)[m / split][m % split] (LayerNorm gamma / beta / bias, Q|K|V biases);
- *   1: weight-gradient partials m = (k*N + n)*C + c -> out_{n / split}[((n % split)*C + c)*KS + k].
+ *   1: weight-gradient partials m = (k*N + n)*C + c -> out_{n / split}[((n % split)*C + c)*KS + k];
+ *   2: m < split -> out0[m], m == split -> out1[0], m > split ignored (a vector + one scalar: the
+ *      VariancePredictor head's weight and bias, fs2_relu_ln_head_bwd).
  * blk0 is filled in. Partials come from fs2_conv_wgrad / fs2_res_ln_bwd / fs2_relu_ln_bwd with
  * defer != 0 (fs2_conv_wgrad_splits / fs2_ln_bwd_parts give their S).
  */

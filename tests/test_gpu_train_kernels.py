@@ -244,6 +244,55 @@ def test_relu_ln_fwd_bwd(ops, p):
     assert torch.allclose(db.cpu().double(), dsum, rtol=1e-3, atol=1e-3 * float(dsum.abs().max()))
 
 
+@pytest.mark.parametrize("p", [0.0, 0.5])
+@pytest.mark.parametrize("defer", [False, True])
+def test_relu_ln_head_fwd_bwd(ops, p, defer):
+    """fs2_relu_ln_head_fwd / _bwd: the VariancePredictor's second layer and head,
+    out = masked_fill(dropout(LayerNorm(relu(a))) . w + b, mask, 0) (model/modules.py:225-250), and
+    the gradients of a, gamma, beta, the conv bias, w and b from the output's gradient, against
+    float64 autograd with the kernel's keep mask; the head's gradients finished in place or deferred
+    (fs2_reduce_batch_launch kind 2), accumulating into existing gradients in the deferred case."""
+    torch.manual_seed(7)
+    B, Lx, D = 9, 37, 256
+    R = B * Lx
+    a = torch.randn(R, D)
+    gam, bet = 1 + 0.1 * torch.randn(D), 0.1 * torch.randn(D)
+    hw, hb = torch.randn(D) / 16, 0.3 * torch.randn(1)
+    mask = torch.rand(B, Lx) < 0.2
+    seed = torch.tensor([77], dtype=torch.int64, device=DEV)
+    salt = 5
+    out, xh, rs = ops.relu_ln_head_fwd(a.to(DEV).view(B, Lx, D), gam.to(DEV), bet.to(DEV), 1e-5, hw.to(DEV), hb.to(DEV),
+                                       mask.to(DEV), p, seed, salt)
+    keep = _keep_mask(ops, 1, R, p, seed, salt).view(R, D) if p > 0 else torch.ones(R, D, dtype=torch.bool)
+    ad = a.double().requires_grad_()
+    gd, bd = gam.double().requires_grad_(), bet.double().requires_grad_()
+    wd, hbd = hw.double().requires_grad_(), hb.double().requires_grad_()
+    y = F.layer_norm(torch.relu(ad), (D,), gd, bd, 1e-5) * keep / (1 - p)
+    ref = (y @ wd + hbd).view(B, Lx).masked_fill(mask, 0.0)
+    torch.cuda.synchronize()
+    assert out.shape == (B, Lx)
+    assert float((out.cpu().double() - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
+    dout = torch.randn(B, Lx)
+    ref.backward(dout.double())
+    q = [] if defer else None
+    base = [torch.randn(n, device=DEV) if defer else None for n in (D, D, D, D, 1)]
+    prev = [None if t is None else t.clone() for t in base]
+    da, dg, dbe, db, dhw, dhb = ops.relu_ln_head_bwd(dout.to(DEV), mask.to(DEV), hw.to(DEV), bet.to(DEV),
+                                                     a.to(DEV).view(B, Lx, D), xh, rs, gam.to(DEV), p, seed, salt,
+                                                     dgamma=base[0], dbeta=base[1], dbias=base[2], dhw=base[3],
+                                                     dhb=base[4], accumulate=defer, defer=q)
+    if defer:
+        ops.reduce_flush(q, da)
+    torch.cuda.synchronize()
+    off = [torch.zeros(1, dtype=torch.float64) if t is None else t.cpu().double() for t in prev]
+    assert float((da.cpu().double().view(R, D) - ad.grad).abs().max()) <= 1e-2 * float(ad.grad.abs().max())
+    for got, want, o in ((dg, gd.grad, off[0]), (dbe, bd.grad, off[1]), (db, ad.grad.sum(0), off[2]),
+                         (dhw, wd.grad, off[3]), (dhb, hbd.grad, off[4])):
+        want = want + o
+        assert torch.allclose(got.cpu().double(), want, rtol=1e-3, atol=1e-3 * float(want.abs().max())), \
+            float((got.cpu().double() - want).abs().max())
+
+
 @pytest.mark.parametrize("V,D,n,pad", [(300, 256, 1024, 0), (256, 256, 7000, None), (5, 64, 16, None)])
 def test_embedding_bwd(ops, V, D, n, pad):
     """fs2_embedding_bwd against a float64 index_add (the nn.Embedding weight gradient), padding
