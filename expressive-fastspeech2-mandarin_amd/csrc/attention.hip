@@ -18,6 +18,20 @@
 
 #include "fs2_common.h"
 
+#ifndef ATTN_ABL
+#define ATTN_ABL 0  // analysis builds only (tools/attn_abl.py): bit 0 no exp / max, 1 no QK MFMAs,
+#endif              // 2 no PV MFMAs, 3 no K / V DMA wait, 4 no K / V DMA
+#ifndef ATTN_TRACE
+#define ATTN_TRACE 0  // analysis builds only: per-workgroup shader-clock stamps of attn32_kernel
+#endif
+
+#if ATTN_TRACE
+__device__ unsigned long long g_attn_stamps[4096 * 8];
+extern "C" int fs2_attn_trace_read(void *dst) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 namespace {
 
 constexpr int DK = 128;
@@ -561,6 +575,10 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
   }
   if (q0 >= T) return;
   const bool active = q0 + 32 * w < T;  // wave-uniform
+#if ATTN_TRACE
+  unsigned long long tst[4];
+  tst[0] = __builtin_readcyclecounter();
+#endif
 
   const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16 *>(qkv), (short)0, (int)qkv_bytes, 0x00020000);
   const uint32_t row_bytes = (uint32_t)qs * 2u;
@@ -592,6 +610,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
     char *Vb = Kb + KTT * 256;
     const int lim = T - k0;
     const uint32_t so = (uint32_t)k0 * row_bytes;
+    if (ATTN_ABL & 16) return;
 #pragma unroll
     for (int it = 0; it < PPW; ++it) {
       const int p = w + NWV * it;
@@ -643,7 +662,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
     constexpr bool MASKED = decltype(masked_tag)::value;
     const int k0 = kt * KTT;
     const int ahead = ntiles - 1 - kt;
-    if (NST >= 3 && ahead >= NST - 2)
+    if (ATTN_ABL & 8)
+      ;
+    else if (NST >= 3 && ahead >= NST - 2)
       attn_vm_wait<LPS * (NST - 2)>();
     else
       attn_vm_wait<0>();
@@ -673,8 +694,13 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
       }
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
-        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s & 1][kb], qf[s], sacc[kb], 0, 0, 0);
+        if (!(ATTN_ABL & 2)) sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s & 1][kb], qf[s], sacc[kb], 0, 0, 0);
     }
+    if (ATTN_ABL & 2)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[kb][r] += (float)kf[1][kb][r & 7];
     if constexpr (MASKED) {  // keys >= len -> -inf
       const int lim = len - k0 - 4 * hh;
 #pragma unroll
@@ -682,6 +708,29 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           if (kb * 32 + (r & 3) + 8 * (r >> 2) >= lim) sacc[kb][r] = -INFINITY;
+    }
+    if (ATTN_ABL & 1) {  // ablation: P = bf16(S), no max / exp
+      bf16x8 pf[KTT / 16];
+#pragma unroll
+      for (int s = 0; s < KTT / 16; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[s][j] = (bf16)sacc[s >> 1][8 * (s & 1) + j];
+#pragma unroll
+      for (int s = 0; s < KTT / 16; ++s) {
+        bf16x8 vf[DK / 32];
+#pragma unroll
+        for (int db = 0; db < DK / 32; ++db) {
+          auto lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)(Vb + s * 16 * 256 + voff[db][0]));
+          auto hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4 *)(Vb + s * 16 * 256 + voff[db][1]));
+          __builtin_memcpy(&vf[db], &lo, 8);
+          __builtin_memcpy(reinterpret_cast<char *>(&vf[db]) + 8, &hi, 8);
+        }
+#pragma unroll
+        for (int db = 0; db < DK / 32; ++db)
+          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[db], pf[s], oacc[db], 0, 0, 0);
+      }
+      l_run = 1.f;
+      return;
     }
     float mx = m_run;
 #pragma unroll
@@ -733,7 +782,10 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
       }
 #pragma unroll
       for (int db = 0; db < DK / 32; ++db)
-        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[db], pf[s], oacc[db], 0, 0, 0);
+        if (ATTN_ABL & 4)
+          oacc[db][s] += (float)vf[db][s & 7] + (float)pf[s][db];
+        else
+          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[db], pf[s], oacc[db], 0, 0, 0);
     }
   };
   // the ring slot of tile kt is kt % NST: the loop walks NST tiles per iteration with constant
@@ -742,6 +794,14 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
   using F = std::false_type;
   using Tr = std::true_type;
   int kt = 0;
+#if ATTN_TRACE
+  if (NST == 2 && ntiles > 2) {  // the first two tiles apart: prologue latency
+    tile(0, std::integral_constant<int, 0>{}, F{});
+    tile(1, std::integral_constant<int, 1>{}, F{});
+    kt = 2;
+  }
+  tst[1] = __builtin_readcyclecounter();
+#endif
   for (; kt + NST < ntiles; kt += NST) {
     tile(kt, std::integral_constant<int, 0>{}, F{});
     tile(kt + 1, std::integral_constant<int, 1>{}, F{});
@@ -766,6 +826,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
       tile(kt, std::integral_constant<int, 2 % NST>{}, Tr{});
   }
 
+#if ATTN_TRACE
+  tst[2] = __builtin_readcyclecounter();
+#endif
   // the two halves' sums (same m); O^T[d][query r32], d = 32 db + (r & 3) + 8 (r >> 2) + 4 hh
   {
     auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
@@ -825,6 +888,17 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
           *reinterpret_cast<bf16x4 *>(orow + 32 * db + 8 * r4) = o;
       }
   }
+#if ATTN_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tst[3] = __builtin_readcyclecounter();
+  if (tid == 0 && blockIdx.x < 4096) {
+    unsigned long long *d = g_attn_stamps + blockIdx.x * 8;
+    for (int i = 0; i < 4; ++i) d[i] = tst[i];
+    d[4] = (unsigned long long)ntiles;
+    d[5] = (unsigned long long)(T - q0 < QTW ? T - q0 : QTW);
+    d[6] = 1;
+  }
+#endif
 }
 
 }  // namespace

@@ -1733,6 +1733,8 @@ extern "C" int fs2_ln_bwd_parts(int64_t R) {
 // ---------------------------------------------------------------------------------------------
 namespace {
 
+constexpr int kReduceLongS = 16;  // more partials than this: the 64-column, 4-wave path
+
 // one thread = 4 consecutive columns (16-byte partial loads, the S splits summed in order): the
 // partial buffers are large (up to 8 x 9.4 MB for the FFN w_1 gradient) and S small
 __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
@@ -1782,6 +1784,54 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
     for (int e = t; e < cn * KS; e += 256) dst[e] = d.accumulate ? dst[e] + tr[e] : tr[e];
     return;
   }
+  // output column -> destination (kind 0: row split into up to 3 vectors; kind 2: a vector and one
+  // scalar; kind 1: weight gradient partials [S][KS][N][C] -> out[n][c][k], rows split into parameters)
+  auto put = [&](int64_t col, float val) {
+    float *base;
+    int64_t off;
+    if (d.kind == 0) {
+      const int64_t which = col / d.split;
+      base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
+      off = col - which * d.split;
+    } else if (d.kind == 2) {  // m < split -> out0[m], m == split -> out1[0]
+      if (col > d.split) return;
+      base = col < d.split ? d.out0 : d.out1;
+      off = col < d.split ? col : 0;
+    } else {
+      const int64_t NC = (int64_t)d.N * d.C;
+      const int k = (int)(col / NC);
+      const int64_t nc = col - (int64_t)k * NC;
+      const int n = (int)(nc / d.C), which = n / d.split;
+      base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
+      off = (nc - (int64_t)which * d.split * d.C) * d.KS + k;
+    }
+    if (base == nullptr) return;  // an output not wanted (e.g. no conv bias behind a LayerNorm)
+    float *dst = base + off;
+    *dst = d.accumulate ? *dst + val : val;
+  };
+  if (d.S > kReduceLongS) {
+    // many partials of a short vector (LayerNorm parameters: 256 partial blocks x 768): a block owns
+    // 64 columns, wave g sums partials g, g + 4, ... in order with every load of a 32-group issued
+    // before its adds, the 4 wave sums added in a fixed order through LDS (the per-column loop of the
+    // path below paid S / 8 memory latencies in ONE block: the tail of every batched launch)
+    __shared__ float red[4][64];
+    const int rg = threadIdx.x >> 6, cl = threadIdx.x & 63;
+    const int64_t col = ((int64_t)blockIdx.x - d.blk0) * 64 + cl;
+    float acc = 0.f;
+    if (col < d.M) {
+      for (int k0 = rg; k0 < d.S; k0 += 4 * 32) {
+        float v[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) v[j] = k0 + 4 * j < d.S ? d.part[(int64_t)(k0 + 4 * j) * d.M + col] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) acc += v[j];
+      }
+    }
+    red[rg][cl] = acc;
+    __syncthreads();
+    if (rg == 0 && col < d.M) put(col, (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]));
+    return;
+  }
   const int64_t col0 = (((int64_t)blockIdx.x - d.blk0) * 256 + threadIdx.x) * 4;
   if (col0 >= d.M) return;
   // the splits in groups of 8: all 8 loads of a group issued before its adds (one memory latency per
@@ -1806,32 +1856,10 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
       }
     }
   }
-  const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t col = col0 + q;
-    float *base;
-    int64_t off;
-    if (d.kind == 0) {
-      const int64_t which = col / d.split;
-      base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
-      off = col - which * d.split;
-    } else if (d.kind == 2) {  // a vector and one scalar: m < split -> out0[m], m == split -> out1[0]
-      if (col > d.split) continue;
-      base = col < d.split ? d.out0 : d.out1;
-      off = col < d.split ? col : 0;
-    } else {  // weight gradient partials [S][KS][N][C] -> out[n][c][k] (rows split into parameters)
-      const int64_t NC = (int64_t)d.N * d.C;
-      const int k = (int)(col / NC);
-      const int64_t nc = col - (int64_t)k * NC;
-      const int n = (int)(nc / d.C), which = n / d.split;
-      base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
-      off = (nc - (int64_t)which * d.split * d.C) * d.KS + k;
-    }
-    if (base == nullptr) continue;  // an output not wanted (e.g. no conv bias behind a LayerNorm)
-    float *dst = base + off;
-    *dst = d.accumulate ? *dst + vals[q] : vals[q];
-  }
+  put(col0, acc.x);
+  put(col0 + 1, acc.y);
+  put(col0 + 2, acc.z);
+  put(col0 + 3, acc.w);
 }
 
 }  // namespace
@@ -1848,7 +1876,9 @@ extern "C" int fs2_reduce_batch_launch(fs2_reduce_batch *a, fs2_stream_t stream)
       return FS2_EINVAL;
     if (d.kind == 1 && d.KS > 1 && d.S > 8) return FS2_EINVAL;  // the wide-tap path sums <= 8 splits
     d.blk0 = blk;
-    blk += d.kind == 1 && d.KS > 1 ? (int64_t)d.N * ((d.C + 255) / 256) : (d.M + 1023) / 1024;
+    blk += d.kind == 1 && d.KS > 1 ? (int64_t)d.N * ((d.C + 255) / 256)
+           : d.S > kReduceLongS     ? (d.M + 63) / 64
+                                    : (d.M + 1023) / 1024;
   }
   if (blk >= (1LL << 31)) return FS2_EUNSUPPORTED;
   hipLaunchKernelGGL(reduce_batch_kernel, dim3((unsigned)blk), dim3(256), 0, as_stream(stream), *a);

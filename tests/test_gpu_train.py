@@ -205,7 +205,8 @@ def test_graphed_train_step_bf16_resumed(gpu):
     on the sink-filled flat buffer) through TrainStep, captured, against the same step body run
     eagerly (flat_grads=True), dropout off. Both resume at step 100 (> warmup): the graph must still
     be captured after this TrainStep's own warm-up calls, not on its first call. Tolerances (bf16,
-    same kernels, non-deterministic f32 atomics only in the torch LR gather backward): losses rtol
+    same kernels, no atomics on the gradient path — the margins are headroom, not a measured
+    spread): losses rtol
     1e-3; parameters as _assert_params_close with rtol 1e-3 and at most 0.05 % of the elements
     differing by up to 2x the summed learning rates."""
     from fs2amd import config as C

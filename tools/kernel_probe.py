@@ -224,6 +224,30 @@ def main():
                 _, x = ops.vp_fused(x, V.dp, le, embed=emb_p)
             if a.kernel != "vpf_dp":
                 ops.vp_fused(x, V.energy, le, embed=emb_e)
+    elif a.kernel == "reduce_ln":  # 8 LayerNorm-parameter partial sets (256 partial blocks x 768) in one launch
+        parts = [torch.randn(256 * 768, generator=g).to(dev) for _ in range(8)]
+        outs = [[torch.empty(256, device=dev) for _ in range(3)] for _ in range(8)]
+
+        def fn():
+            q = []
+            for p, o in zip(parts, outs):
+                ops._defer_add(q, p, M=768, S=256, kind=0, split=256, accumulate=0, outs=o)
+            ops.reduce_flush(q, parts[0])
+    elif a.kernel in ("reduce_w1", "reduce_w2", "reduce_qkv"):
+        # deferred split-partial reductions (fs2_reduce_batch_launch) as the training backward queues
+        # them: 8 layers' weight gradients in one launch (partials past the 256 MB MALL, as in a step)
+        KS, N, C, S = {"reduce_w1": (9, 1024, 256, 4), "reduce_w2": (1, 256, 1024, 16),
+                       "reduce_qkv": (1, 768, 256, 16)}[a.kernel]
+        M = KS * N * C
+        parts = [torch.randn(S * M, generator=g).to(dev) for _ in range(8)]
+        outs = [torch.empty(N, C, KS, device=dev) for _ in range(8)]
+        print(f"bytes per launch {8 * (S + 1) * M * 4 / 1e6:.1f} MB")
+
+        def fn():
+            q = []
+            for p, o in zip(parts, outs):
+                ops._defer_add(q, p, M=M, S=S, kind=1, KS=KS, N=N, C=C, split=N, accumulate=0, outs=(o,))
+            ops.reduce_flush(q, parts[0])
     else:
         raise SystemExit(f"unknown kernel {a.kernel}")
     flush_buf = torch.empty(a.flush << 18, device=dev, dtype=torch.float32) if a.flush else None

@@ -14,6 +14,7 @@
 #   free_trace              rocprofv3 kernel trace of the free-running loop -> free_kernels.txt
 #   voc                     rocprofv3 kernel trace of the vocoder probe -> voc_kernels.txt
 #   pmc                     PMC passes over eager forwards (tools/pmc_fwd.sh)
+#   attn_abl                tools/attn_abl.py run (build the tracelib/ variants first)
 #   probe:ARGS              python tools/kernel_probe.py ARGS (colons in ARGS become spaces)
 # Environment variables set on the call (FS2_*) apply to every step.
 TAG=${1:?tag}; shift
@@ -51,6 +52,9 @@ for st in "$@"; do
       python3 tools/prof_summary.py $(ls $O/voc/trace/*kernel_trace.csv | head -1) > $O/voc_kernels.txt
       head -8 $O/voc_kernels.txt ;;
     pmc) bash tools/pmc_fwd.sh $TAG > $O/pmc.log 2>&1 || fail $O/pmc.log 20 ;;
+    attn_abl)
+      timeout -k 10 600 python tools/attn_abl.py run > $O/attn_abl.log 2>&1 || fail $O/attn_abl.log
+      cat $O/attn_abl.log ;;
     probe:*)
       A=${st#probe:}; A=${A//:/ }
       N=$(echo $A | tr ' ' '_')
