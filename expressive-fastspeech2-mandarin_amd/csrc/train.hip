@@ -1754,6 +1754,15 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
     const int64_t bl = (int64_t)blockIdx.x - d.blk0;
     const int n = (int)(bl / cb), c0 = (int)(bl - (int64_t)n * cb) * 256;
     const int cn = min(256, C - c0), t = threadIdx.x;
+    const int which = n / d.split;
+    float *base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
+    float *dst = base == nullptr ? nullptr : base + ((int64_t)(n - which * d.split) * C + c0) * KS;
+    // accumulating: the outputs' old values are loaded first, beside the partials (a load-add-store
+    // per output after the sums paid one more memory latency per store)
+    float old[9];
+    const int ne = cn * KS;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) old[i] = (dst != nullptr && d.accumulate && t + 256 * i < ne) ? dst[t + 256 * i] : 0.f;
     if (t < cn) {
       // every (tap, split) load issued before the first add (a dependent loop paid one memory
       // latency per load: ~100 us per batched launch); S <= 8 for wide taps (wgrad_splits)
@@ -1777,16 +1786,15 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
       }
     }
     __syncthreads();
-    const int which = n / d.split;
-    float *base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
-    if (base == nullptr) return;
-    float *dst = base + ((int64_t)(n - which * d.split) * C + c0) * KS;
-    for (int e = t; e < cn * KS; e += 256) dst[e] = d.accumulate ? dst[e] + tr[e] : tr[e];
+    if (dst == nullptr) return;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+      if (t + 256 * i < ne) dst[t + 256 * i] = old[i] + tr[t + 256 * i];
     return;
   }
   // output column -> destination (kind 0: row split into up to 3 vectors; kind 2: a vector and one
   // scalar; kind 1: weight gradient partials [S][KS][N][C] -> out[n][c][k], rows split into parameters)
-  auto put = [&](int64_t col, float val) {
+  auto where = [&](int64_t col) -> float * {
     float *base;
     int64_t off;
     if (d.kind == 0) {
@@ -1794,7 +1802,7 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
       base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
       off = col - which * d.split;
     } else if (d.kind == 2) {  // m < split -> out0[m], m == split -> out1[0]
-      if (col > d.split) return;
+      if (col > d.split) return nullptr;
       base = col < d.split ? d.out0 : d.out1;
       off = col < d.split ? col : 0;
     } else {
@@ -1805,10 +1813,10 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
       base = which == 0 ? d.out0 : which == 1 ? d.out1 : d.out2;
       off = (nc - (int64_t)which * d.split * d.C) * d.KS + k;
     }
-    if (base == nullptr) return;  // an output not wanted (e.g. no conv bias behind a LayerNorm)
-    float *dst = base + off;
-    *dst = d.accumulate ? *dst + val : val;
+    return base == nullptr ? nullptr : base + off;  // null: an output not wanted (no conv bias behind a LN)
   };
+  // accumulating outputs: their old values are loaded before the partial sums (one latency, overlapped)
+  auto old_of = [&](float *p) { return (p != nullptr && d.accumulate) ? *p : 0.f; };
   if (d.S > kReduceLongS) {
     // many partials of a short vector (LayerNorm parameters: 256 partial blocks x 768): a block owns
     // 64 columns, wave g sums partials g, g + 4, ... in order with every load of a 32-group issued
@@ -1817,6 +1825,8 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
     __shared__ float red[4][64];
     const int rg = threadIdx.x >> 6, cl = threadIdx.x & 63;
     const int64_t col = ((int64_t)blockIdx.x - d.blk0) * 64 + cl;
+    float *dst = (rg == 0 && col < d.M) ? where(col) : nullptr;
+    const float o = old_of(dst);
     float acc = 0.f;
     if (col < d.M) {
       for (int k0 = rg; k0 < d.S; k0 += 4 * 32) {
@@ -1829,11 +1839,18 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
     }
     red[rg][cl] = acc;
     __syncthreads();
-    if (rg == 0 && col < d.M) put(col, (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]));
+    if (dst != nullptr) *dst = o + ((red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]));
     return;
   }
   const int64_t col0 = (((int64_t)blockIdx.x - d.blk0) * 256 + threadIdx.x) * 4;
   if (col0 >= d.M) return;
+  float *dst[4];
+  float o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    dst[q] = where(col0 + q);
+    o[q] = old_of(dst[q]);
+  }
   // the splits in groups of 8: all 8 loads of a group issued before its adds (one memory latency per
   // group, not per split), summed in split order
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1856,10 +1873,10 @@ __global__ __launch_bounds__(256) void reduce_batch_kernel(fs2_reduce_batch a) {
       }
     }
   }
-  put(col0, acc.x);
-  put(col0 + 1, acc.y);
-  put(col0 + 2, acc.z);
-  put(col0 + 3, acc.w);
+  const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (dst[q] != nullptr) *dst[q] = o[q] + vals[q];
 }
 
 }  // namespace

@@ -231,7 +231,7 @@ def main():
         def fn():
             q = []
             for p, o in zip(parts, outs):
-                ops._defer_add(q, p, M=768, S=256, kind=0, split=256, accumulate=0, outs=o)
+                ops._defer_add(q, p, M=768, S=256, kind=0, split=256, accumulate=1, outs=o)
             ops.reduce_flush(q, parts[0])
     elif a.kernel in ("reduce_w1", "reduce_w2", "reduce_qkv"):
         # deferred split-partial reductions (fs2_reduce_batch_launch) as the training backward queues
@@ -246,7 +246,7 @@ def main():
         def fn():
             q = []
             for p, o in zip(parts, outs):
-                ops._defer_add(q, p, M=M, S=S, kind=1, KS=KS, N=N, C=C, split=N, accumulate=0, outs=(o,))
+                ops._defer_add(q, p, M=M, S=S, kind=1, KS=KS, N=N, C=C, split=N, accumulate=1, outs=(o,))
             ops.reduce_flush(q, parts[0])
     else:
         raise SystemExit(f"unknown kernel {a.kernel}")

@@ -12,6 +12,7 @@
 #   free / free_eager       tools/free_probe.py (SynthGraphs / eager), 8 distinct batches
 #   fwd_trace               rocprofv3 kernel trace of the bench -> forward_kernels.txt
 #   free_trace              rocprofv3 kernel trace of the free-running loop -> free_kernels.txt
+#   train_trace             rocprofv3 kernel trace of the graphed cfg3 step -> train_steps.txt
 #   voc                     rocprofv3 kernel trace of the vocoder probe -> voc_kernels.txt
 #   pmc                     PMC passes over eager forwards (tools/pmc_fwd.sh)
 #   attn_abl                tools/attn_abl.py run (build the tracelib/ variants first)
@@ -47,6 +48,10 @@ for st in "$@"; do
       grep -v amdgpu.ids $O/free_eager.log | tail -1 ;;
     fwd_trace) bash tools/fwd_trace.sh $TAG/fwd || exit 1 ;;
     free_trace) bash tools/free_trace.sh $TAG/free || exit 1 ;;
+    train_trace)
+      GRAPH=1 bash tools/prof_train.sh $TAG/ttr || exit 1
+      python3 tools/train_steps.py $O/ttr/trace/train_kernel_trace.csv > $O/train_steps.txt
+      head -12 $O/train_steps.txt ;;
     voc)
       bash tools/prof_voc.sh $TAG/voc || exit 1
       python3 tools/prof_summary.py $(ls $O/voc/trace/*kernel_trace.csv | head -1) > $O/voc_kernels.txt
