@@ -347,8 +347,19 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t *__restric
       const int total = (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
       if (hit) list[off + __popcll(m & ((1ull << lane) - 1ull))] = tid;
       __syncthreads();
-      if (tid < D)
-        for (int j = 0; j < total; ++j) acc += dy[(base + list[j]) * dys + tid];
+      if (tid < D) {
+        // 8 hit rows' loads in flight before their adds (same order: bit-identical; a row with
+        // hundreds of hits -- a common pitch / energy bucket -- paid one memory latency per hit)
+        int j = 0;
+        for (; j + 8 <= total; j += 8) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = dy[(base + list[j + u]) * dys + tid];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc += v[u];
+        }
+        for (; j < total; ++j) acc += dy[(base + list[j]) * dys + tid];
+      }
       __syncthreads();
     }
   if (tid < D) {
@@ -1899,6 +1910,285 @@ extern "C" int fs2_reduce_batch_launch(fs2_reduce_batch *a, fs2_stream_t stream)
   }
   if (blk >= (1LL << 31)) return FS2_EUNSUPPORTED;
   hipLaunchKernelGGL(reduce_batch_kernel, dim3((unsigned)blk), dim3(256), 0, as_stream(stream), *a);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Backward of the conditioning add (model/fastspeech2.py:101-110 in training):
+//   x + speaker_emb(s)[b] + relu(W cat(emo_emb(e), aro_emb(a), val_emb(v))[b] + bias)
+// dc[b] = sum_l dy[b, l] (the broadcast's gradient), dh = dc * (relu output > 0); then the
+// speaker / emotion / arousal / valence table rows, W and bias. Two launches, every sum in a fixed
+// order (the batch entries that share an id are added to its row in batch order): deterministic.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+// launch 1: (64 channels, one utterance) per workgroup: wave g sums positions g, g + 4, ... in order,
+// the 4 wave sums added in a fixed order; writes dc and dh ([B][D] each) into the workspace
+__global__ __launch_bounds__(256) void cond_colsum_kernel(const float *__restrict__ dy, int L, int D,
+                                                          const float *__restrict__ emo_out, float *__restrict__ dc,
+                                                          float *__restrict__ dh) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6, b = blockIdx.y, n = blockIdx.x * 64 + c;
+  float acc = 0.f;
+  if (n < D) {
+    const float *p = dy + (int64_t)b * L * D + n;
+    for (int l = g; l < L; l += 4) acc += p[(int64_t)l * D];
+  }
+  red[g][c] = acc;
+  __syncthreads();
+  if (g == 0 && n < D) {
+    const float s = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    dc[(int64_t)b * D + n] = s;
+    if (emo_out != nullptr) dh[(int64_t)b * D + n] = emo_out[(int64_t)b * D + n] > 0.f ? s : 0.f;
+  }
+}
+
+// launch 2: three kinds of workgroups, by block index (none waits on another):
+//  A  [0, nA): 16 Linear input columns k each: de[b][k] = sum_n dh[b][n] W[n][k] for every utterance
+//     (dh and the W columns staged in LDS), then those columns of the emotion / arousal / valence
+//     tables: each row = old + its utterances' de in batch order;
+//  B  [nA, nA + nB): 4 rows n of dW each: dW[n][k] (+)= sum_b dh[b][n] cat[b][k];
+//  C  the rest: 64 output channels each: the bias (sum over the batch) and the speaker rows.
+// (One workgroup per 64 columns doing all of it ran ~30k dependent instructions per wave on 16
+// waves: 90-150 us. Every global load here is unconditional at a clamped address, issued in
+// batches before its use.)
+constexpr int kCondKA = 16;  // Linear input columns per A workgroup
+constexpr int kCondNB = 4;   // dW rows per B workgroup
+
+__global__ __launch_bounds__(256) void cond_param_kernel(fs2_cond_desc f, fs2_cond_grads gr, int B, int D, int nA,
+                                                         int nB, const float *__restrict__ dcw,
+                                                         const float *__restrict__ dhw) {
+  extern __shared__ float sm[];
+  const int dcat = dhw != nullptr ? f.d_emo + f.d_aro + f.d_val : 0;
+  const int tid = threadIdx.x, blk = blockIdx.x;
+  auto clampi = [](int64_t v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : (int)v); };
+  // table column k -> (table, source, gradient, row width, column in the row)
+  auto col = [&](int k, int &t, const float *&src, float *&dst, const int64_t *&ids, int &nrow, int &dd, int &kk) {
+    if (k >= f.d_emo + f.d_aro)
+      t = 2, src = f.val_table, dst = gr.d_val_table, ids = f.valences, nrow = f.n_val, dd = f.d_val, kk = k - f.d_emo - f.d_aro;
+    else if (k >= f.d_emo)
+      t = 1, src = f.aro_table, dst = gr.d_aro_table, ids = f.arousals, nrow = f.n_aro, dd = f.d_aro, kk = k - f.d_emo;
+    else
+      t = 0, src = f.emo_table, dst = gr.d_emo_table, ids = f.emotions, nrow = f.n_emo, dd = f.d_emo, kk = k;
+  };
+  if (blk < nA) {
+    // ---- A: de and the three tables' columns [k0, k0 + 16)
+    float *dh = sm;                 // [B][D]
+    float *ws = dh + B * D;         // [D][16] W columns
+    float *de = ws + D * kCondKA;   // [B][16]
+    float *ov = de + B * kCondKA;   // [B][16] old row values / running row sums
+    int *idl = reinterpret_cast<int *>(ov + B * kCondKA);  // [3][B] rows, [3][B] reps
+    const int k0 = blk * kCondKA;
+    for (int i0 = tid; i0 < B * D; i0 += 256 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = dhw[i0 + 256 * u < B * D ? i0 + 256 * u : B * D - 1];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + 256 * u < B * D) dh[i0 + 256 * u] = v[u];
+    }
+    for (int i0 = tid; i0 < D * kCondKA; i0 += 256 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 256 * u < D * kCondKA ? i0 + 256 * u : D * kCondKA - 1;
+        const int n = i / kCondKA, kc = k0 + (i - n * kCondKA);
+        v[u] = f.lin_w[(int64_t)n * dcat + (kc < dcat ? kc : dcat - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + 256 * u < D * kCondKA) ws[i0 + 256 * u] = v[u];
+    }
+    for (int i = tid; i < 3 * B; i += 256) {
+      const int t = i / B, b = i - t * B;
+      idl[i] = t == 0 ? clampi(f.emotions[b], f.n_emo) : t == 1 ? clampi(f.arousals[b], f.n_aro)
+                                                                 : clampi(f.valences[b], f.n_val);
+    }
+    __syncthreads();
+    for (int i = tid; i < 3 * B; i += 256) {  // rep: the first utterance sharing the row
+      const int t = i / B, b = i - t * B, r = idl[i];
+      int f0 = b;
+      for (int b2 = 0; b2 < b; ++b2)
+        if (idl[t * B + b2] == r) {
+          f0 = b2;
+          break;
+        }
+      idl[3 * B + i] = f0;
+    }
+    // de: thread (column kc, utterance b = bb, bb + 16, ...), n in order
+    const int kc = tid & (kCondKA - 1), bb = tid / kCondKA;
+    for (int b = bb; b < B; b += 256 / kCondKA) {
+      float a0 = 0.f, a1 = 0.f;  // two chains (even / odd n), added at the end
+      const float *dr = dh + b * D;
+      int n = 0;
+      for (; n + 1 < D; n += 2) {
+        a0 = fmaf(dr[n], ws[n * kCondKA + kc], a0);
+        a1 = fmaf(dr[n + 1], ws[(n + 1) * kCondKA + kc], a1);
+      }
+      if (n < D) a0 = fmaf(dr[n], ws[n * kCondKA + kc], a0);
+      de[b * kCondKA + kc] = a0 + a1;
+    }
+    // old values of every (utterance, column) row entry (only the reps' are used)
+    for (int i = tid; i < B * kCondKA; i += 256) {
+      const int b = i / kCondKA, k = k0 + (i - b * kCondKA);
+      int t, nrow, dd, kk;
+      const float *src;
+      float *dst;
+      const int64_t *ids;
+      col(k < dcat ? k : dcat - 1, t, src, dst, ids, nrow, dd, kk);
+      ov[i] = dst != nullptr ? dst[(int64_t)idl[t * B + b] * dd + kk] : 0.f;
+    }
+    __syncthreads();
+    if (tid < kCondKA && k0 + tid < dcat) {
+      const int k = k0 + tid;
+      int t, nrow, dd, kk;
+      const float *src;
+      float *dst;
+      const int64_t *ids;
+      col(k, t, src, dst, ids, nrow, dd, kk);
+      if (dst != nullptr) {
+        for (int b = 0; b < B; ++b) ov[idl[3 * B + t * B + b] * kCondKA + tid] += de[b * kCondKA + tid];
+        for (int b = 0; b < B; ++b)
+          if (idl[3 * B + t * B + b] == b) dst[(int64_t)idl[t * B + b] * dd + kk] = ov[b * kCondKA + tid];
+      }
+    }
+    return;
+  }
+  if (blk < nA + nB) {
+    // ---- B: dW rows [n0, n0 + 4), every column k (the batch's cat column gathered per thread)
+    if (gr.d_lin_w == nullptr) return;
+    const int n0 = (blk - nA) * kCondNB;
+    float *dhr = sm;  // [B][4] this workgroup's dh rows
+    for (int i = tid; i < B * kCondNB; i += 256) {
+      const int b = i / kCondNB, r = i - b * kCondNB;
+      dhr[i] = dhw[(int64_t)b * D + (n0 + r < D ? n0 + r : D - 1)];
+    }
+    __syncthreads();
+    for (int k = tid; k < dcat; k += 256) {
+      int t, nrow, dd, kk;
+      const float *src;
+      float *dst;
+      const int64_t *ids;
+      col(k, t, src, dst, ids, nrow, dd, kk);
+      float od[kCondNB], acc[kCondNB];
+#pragma unroll
+      for (int r = 0; r < kCondNB; ++r) {
+        od[r] = gr.d_lin_w[(int64_t)(n0 + r < D ? n0 + r : D - 1) * dcat + k];
+        acc[r] = 0.f;
+      }
+      for (int b0 = 0; b0 < B; b0 += 8) {
+        float cv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int b = b0 + u < B ? b0 + u : B - 1;
+          cv[u] = src[(int64_t)clampi(ids[b], nrow) * dd + kk];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (b0 + u >= B) break;
+#pragma unroll
+          for (int r = 0; r < kCondNB; ++r) acc[r] = fmaf(dhr[(b0 + u) * kCondNB + r], cv[u], acc[r]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kCondNB; ++r)
+        if (n0 + r < D) gr.d_lin_w[(int64_t)(n0 + r) * dcat + k] = od[r] + acc[r];
+    }
+    return;
+  }
+  // ---- C: output channels [n0, n0 + 64): bias and speaker rows
+  const int n0 = (blk - nA - nB) * 64, c = tid & 63, g = tid >> 6;
+  const int n = n0 + c, nc = n < D ? n : D - 1;
+  float *dcb = sm;              // [B][64]
+  float *ov = dcb + B * 64;     // [B][64]
+  int *idl = reinterpret_cast<int *>(ov + B * 64);  // [B] rows, [B] reps
+  const bool spk = f.speaker_table != nullptr && gr.d_speaker_table != nullptr;
+  for (int b = tid; b < B; b += 256) idl[b] = spk ? clampi(f.speakers[b], f.n_speaker) : 0;
+  __syncthreads();
+  for (int b = tid; b < B; b += 256) {
+    int f0 = b;
+    for (int b2 = 0; b2 < b; ++b2)
+      if (idl[b2] == idl[b]) {
+        f0 = b2;
+        break;
+      }
+    idl[B + b] = f0;
+  }
+  for (int b0 = g; b0 < B; b0 += 4 * 8) {
+    float v[8], o[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = b0 + 4 * u < B ? b0 + 4 * u : B - 1;
+      v[u] = dcw[(int64_t)b * D + nc];
+      o[u] = spk ? gr.d_speaker_table[(int64_t)idl[b] * D + nc] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (b0 + 4 * u < B) dcb[(b0 + 4 * u) * 64 + c] = v[u], ov[(b0 + 4 * u) * 64 + c] = o[u];
+  }
+  float bs = 0.f;
+  if (g == 0 && dcat && gr.d_lin_b != nullptr) {
+    const float old = gr.d_lin_b[nc];
+    for (int b0 = 0; b0 < B; b0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = dhw[(int64_t)(b0 + j < B ? b0 + j : B - 1) * D + nc];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (b0 + j < B) bs += v[j];
+    }
+    bs += old;
+  }
+  __syncthreads();
+  if (g == 0 && n < D) {
+    if (dcat && gr.d_lin_b != nullptr) gr.d_lin_b[n] = bs;
+    if (spk) {
+      for (int b = 0; b < B; ++b) ov[idl[B + b] * 64 + c] += dcb[b * 64 + c];
+      for (int b = 0; b < B; ++b)
+        if (idl[B + b] == b) gr.d_speaker_table[(int64_t)idl[b] * D + n] = ov[b * 64 + c];
+    }
+  }
+}
+
+}  // namespace
+
+static size_t fs2_cond_bwd_smem(int B, int D, bool emo) {  // cond_param_kernel's LDS (the largest role)
+  const size_t a = emo ? ((size_t)B * D + (size_t)D * kCondKA + 2 * (size_t)B * kCondKA) * sizeof(float) +
+                             6 * (size_t)B * sizeof(int)
+                       : 0;
+  const size_t c = 2 * (size_t)B * 64 * sizeof(float) + 2 * (size_t)B * sizeof(int);
+  return a > c ? a : c;
+}
+
+extern "C" int64_t fs2_cond_bwd_ws_bytes(int B, int D) {
+  return B <= 0 || D <= 0 ? 0 : 2 * (int64_t)B * D * (int64_t)sizeof(float);
+}
+
+extern "C" int fs2_cond_bwd(const float *dy, int B, int L, int D, const fs2_cond_desc *fwd, const fs2_cond_grads *grads,
+                            void *ws, int64_t ws_bytes, fs2_stream_t stream) {
+  if (dy == nullptr || fwd == nullptr || grads == nullptr || ws == nullptr || B < 0 || L < 0 || D <= 0)
+    return FS2_EINVAL;
+  const fs2_cond_desc &f = *fwd;
+  if (f.speaker_table != nullptr && (f.speakers == nullptr || f.n_speaker <= 0)) return FS2_EINVAL;
+  if (f.emo_table != nullptr &&
+      (f.emotions == nullptr || f.arousals == nullptr || f.valences == nullptr || f.aro_table == nullptr ||
+       f.val_table == nullptr || f.lin_w == nullptr || f.emo_out == nullptr || f.n_emo <= 0 || f.n_aro <= 0 ||
+       f.n_val <= 0 || f.d_emo <= 0 || f.d_aro <= 0 || f.d_val <= 0))
+    return FS2_EINVAL;
+  if (ws_bytes < fs2_cond_bwd_ws_bytes(B, D)) return FS2_EINVAL;
+  if (B == 0 || L == 0 || (f.speaker_table == nullptr && f.emo_table == nullptr)) return FS2_OK;
+  const size_t smem = fs2_cond_bwd_smem(B, D, f.emo_table != nullptr);
+  if (B > 64 || smem > 65536) return FS2_EUNSUPPORTED;
+  hipStream_t s = as_stream(stream);
+  float *dc = static_cast<float *>(ws), *dh = dc + (int64_t)B * D;
+  hipLaunchKernelGGL(cond_colsum_kernel, dim3((unsigned)((D + 63) / 64), (unsigned)B), dim3(256), 0, s, dy, L, D,
+                     f.emo_table != nullptr ? f.emo_out : nullptr, dc, dh);
+  const int dcat = f.emo_table != nullptr ? f.d_emo + f.d_aro + f.d_val : 0;
+  const int nA = (dcat + kCondKA - 1) / kCondKA, nB = dcat > 0 ? (D + kCondNB - 1) / kCondNB : 0;
+  const int nC = (D + 63) / 64;
+  hipLaunchKernelGGL(cond_param_kernel, dim3((unsigned)(nA + nB + nC)), dim3(256), smem, s, f, *grads, B, D, nA, nB,
+                     dc, f.emo_table != nullptr ? dh : nullptr);
   FS2_CHECK_LAUNCH();
   return FS2_OK;
 }

@@ -123,6 +123,13 @@ class CondDesc(ctypes.Structure):
     ]
 
 
+class CondGrads(ctypes.Structure):
+    """Mirror of ``fs2_cond_grads`` (include/fs2hip.h)."""
+
+    _fields_ = [("d_speaker_table", _p), ("d_emo_table", _p), ("d_aro_table", _p), ("d_val_table", _p),
+                ("d_lin_w", _p), ("d_lin_b", _p)]
+
+
 class FfnDesc(ctypes.Structure):
     """Mirror of ``fs2_ffn_desc`` (include/fs2hip.h)."""
 
@@ -226,6 +233,8 @@ SIGNATURES = {
     "fs2_conv_wgrad_splits": (_i, [_i, _i, _i, _i, _i]),
     "fs2_ln_bwd_parts": (_i, [_i64]),
     "fs2_reduce_batch_launch": (_i, [_p, _p]),
+    "fs2_cond_bwd_ws_bytes": (_i64, [_i, _i]),
+    "fs2_cond_bwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _i64, _p]),
     "fs2_length_masks": (_i, [_p, _i, _i, _p, _p]),
     "fs2_length_regulate": (_i, [_p, _i, _p, _i, _f, _i, _i, _i, _i, _p, _p, _i, _p, _p, _p, _p, _p]),
 }

@@ -927,6 +927,34 @@ def cond_vectors(speakers, spk_table, emotions, arousals, valences, emo_table, a
     return spk_out, emo_out
 
 
+def cond_bwd(dy, speakers, spk_table, emotions, arousals, valences, emo_table, aro_table, val_table, lin_w, emo_out,
+             d_spk=None, d_emo=None, d_aro=None, d_val=None, d_w=None, d_b=None):
+    """Backward of y = x + spk_out[b] + emo_out[b] (fs2_cond_bwd): ACCUMULATES the speaker /
+    emotion / arousal / valence table gradients and the emotion Linear's weight / bias gradients
+    into the given tensors (None: skipped). dy [B, L, D] f32. The gradient of x is dy itself."""
+    _gpu(dy, speakers, spk_table, emotions, emo_table, lin_w, emo_out)
+    dy = dy.contiguous()
+    assert dy.dtype == torch.float32 and dy.dim() == 3
+    B, Lx, D = dy.shape
+    cd = L.CondDesc()
+    if spk_table is not None:
+        cd.speakers, cd.speaker_table, cd.n_speaker = _ptr(speakers), _ptr(spk_table), spk_table.shape[0]
+    if emo_table is not None:
+        cd.emotions, cd.emo_table, cd.n_emo, cd.d_emo = _ptr(emotions), _ptr(emo_table), emo_table.shape[0], \
+            emo_table.shape[1]
+        cd.arousals, cd.aro_table, cd.n_aro, cd.d_aro = _ptr(arousals), _ptr(aro_table), aro_table.shape[0], \
+            aro_table.shape[1]
+        cd.valences, cd.val_table, cd.n_val, cd.d_val = _ptr(valences), _ptr(val_table), val_table.shape[0], \
+            val_table.shape[1]
+        cd.lin_w, cd.emo_out = _ptr(lin_w), _ptr(emo_out)
+    gr = L.CondGrads()
+    gr.d_speaker_table, gr.d_emo_table, gr.d_aro_table, gr.d_val_table, gr.d_lin_w, gr.d_lin_b = (
+        _ptr(d_spk), _ptr(d_emo), _ptr(d_aro), _ptr(d_val), _ptr(d_w), _ptr(d_b))
+    ws = torch.empty(max(1, _lib.fs2_cond_bwd_ws_bytes(B, D) // 4), device=dy.device, dtype=torch.float32)
+    L.check(_lib.fs2_cond_bwd(_ptr(dy), B, Lx, D, ctypes.byref(cd), ctypes.byref(gr), _ptr(ws), ws.numel() * 4,
+                              _stream(dy)), "fs2_cond_bwd")
+
+
 def variance_embed(x, pred, target, control, bins, table):
     """In place: pred *= control (no target); x += table[bucketize(target or pred, bins)]."""
     _gpu(x, pred, target, bins, table)

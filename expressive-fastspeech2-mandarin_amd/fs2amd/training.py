@@ -432,6 +432,53 @@ def _embed(emb, idx, fused):
     return EmbeddingFn.apply(idx, emb.weight, emb.padding_idx)
 
 
+class CondFn(torch.autograd.Function):
+    """The conditioning of fastspeech2.py:101-110 in training: x + speaker_emb(speakers) +
+    emotion_linear(cat(emotion_emb, arousal_emb, valence_emb)) broadcast over the positions.
+    Forward: fs2_cond_vectors (one launch) and the two adds in the reference's order; backward:
+    fs2_cond_bwd (two launches, deterministic) instead of the autograd of four lookups, a cat, the
+    Linear + ReLU and the broadcast adds (~20 launches); gradient sink as FFTBlockFn."""
+
+    @staticmethod
+    def forward(ctx, x, speakers, emotions, arousals, valences, spk_w, emo_w, aro_w, val_w, lin_w, lin_b):
+        D = x.shape[-1]
+        spk, emo = ops.cond_vectors(speakers, spk_w, emotions, arousals, valences, emo_w, aro_w, val_w, lin_w, lin_b,
+                                    D)
+        y = x + spk.unsqueeze(1) if spk is not None else x.clone()
+        if emo is not None:
+            y.add_(emo.unsqueeze(1))
+        ctx.save_for_backward(speakers, emotions, arousals, valences, spk_w, emo_w, aro_w, val_w, lin_w, lin_b, emo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        speakers, emotions, arousals, valences, spk_w, emo_w, aro_w, val_w, lin_w, lin_b, emo = ctx.saved_tensors
+        params = (spk_w, emo_w, aro_w, val_w, lin_w, lin_b)  # None where the model has no such table
+        present = [p for p in params if p is not None]
+        sink = _SINK[0] and all(p.grad is not None for p in present)
+        if sink:
+            grads = [None if p is None else p.grad for p in params]
+        else:
+            grads = [None if p is None else torch.zeros_like(p) for p in params]
+        ops.cond_bwd(dy.float(), speakers, spk_w, emotions, arousals, valences, emo_w, aro_w, val_w, lin_w, emo,
+                     *grads)
+        if sink:
+            grads = [None] * 6
+        return (dy, None, None, None, None, *grads)
+
+
+def cond_fused_on(model, x):
+    """CondFn applies: f32 positions, fs2_cond_bwd's limits (B <= 64 and its LDS bound), at least one
+    conditioning table; FS2_TRAIN_COND=0 keeps the per-op autograd form."""
+    if os.environ.get("FS2_TRAIN_COND", "1") == "0" or x.dtype != torch.float32:
+        return False
+    if model.speaker_emb is None and model.emotion_emb is None:
+        return False
+    B, D = x.shape[0], x.shape[-1]
+    emo = model.emotion_emb is not None
+    return B <= 64 and (not emo or (B * D + 16 * D + 32 * B) * 4 + 24 * B <= 65536)
+
+
 def _packT_any(w):
     """Input-gradient weight of a conv whose output width may need channel padding as the
     transposed conv's input (PostNet's 80 mel channels)."""
@@ -794,12 +841,20 @@ def train_forward(model, speakers, emotions, arousals, valences, texts, src_lens
                                     packs[i])
         else:
             x = fft_block(blk, x, src_masks, lens_src, tr["encoder_dropout"], training, compute)
-    if model.speaker_emb is not None:
-        x = x + _embed(model.speaker_emb, speakers, fused).unsqueeze(1)
-    if model.emotion_emb is not None:
-        emb = torch.cat([_embed(model.emotion_emb, emotions, fused), _embed(model.arousal_emb, arousals, fused),
-                         _embed(model.valence_emb, valences, fused)], -1)
-        x = x + model.emotion_linear(emb).unsqueeze(1)
+    if fused and cond_fused_on(model, x):
+        emo_on = model.emotion_emb is not None
+        spk_w = model.speaker_emb.weight if model.speaker_emb is not None else None
+        x = CondFn.apply(x, speakers if spk_w is not None else None, emotions if emo_on else None,
+                         arousals if emo_on else None, valences if emo_on else None, spk_w,
+                         *((model.emotion_emb.weight, model.arousal_emb.weight, model.valence_emb.weight,
+                            model.emotion_linear[0].weight, model.emotion_linear[0].bias) if emo_on else (None,) * 5))
+    else:
+        if model.speaker_emb is not None:
+            x = x + _embed(model.speaker_emb, speakers, fused).unsqueeze(1)
+        if model.emotion_emb is not None:
+            emb = torch.cat([_embed(model.emotion_emb, emotions, fused), _embed(model.arousal_emb, arousals, fused),
+                             _embed(model.valence_emb, valences, fused)], -1)
+            x = x + model.emotion_linear(emb).unsqueeze(1)
 
     # variance adaptor (model/modules.py:102-158)
     vseed = seed if fused else None

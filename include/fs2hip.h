@@ -425,6 +425,31 @@ int fs2_attention_bwd(const void *qkv, int dtype, int64_t qkv_row_stride, const 
                       float *ws, int64_t ws_bytes, const float *lse, fs2_stream_t stream);
 
 /*
+ * fs2_cond_bwd — backward of the training forward's conditioning add (fastspeech2.py:101-110):
+ * y[b, l] = x[b, l] + spk_out[b] + emo_out[b] with fwd the forward's fs2_cond_vectors arguments
+ * (ids, tables, lin_w; emo_out = its relu output, read for the relu mask; spk_out unused).
+ * dy [B, L, D] f32. Every gradient ACCUMULATES into its output (zero it for a fresh gradient); a
+ * NULL output is skipped; a table row gets the batch entries with its id in batch order (fixed
+ * order, deterministic). ids are clamped into their table as fs2_cond_vectors does. The gradient
+ * of x is dy itself (the caller passes it on). ws: fs2_cond_bwd_ws_bytes(B, D) bytes. Needs
+ * B <= 64 and, with the emotion path, (B * D + 16 * D + 32 * B) * 4 + 24 * B <= 64 KiB
+ * (FS2_EUNSUPPORTED otherwise). Two launches.
+ * Replaces the autograd of the three adds, the four nn.Embedding lookups, the cat and
+ * emotion_linear (nn.Linear + ReLU) in training.
+ */
+typedef struct fs2_cond_grads {
+  float *d_speaker_table; /* [n_speaker, D] */
+  float *d_emo_table;     /* [n_emo, d_emo] */
+  float *d_aro_table;     /* [n_aro, d_aro] */
+  float *d_val_table;     /* [n_val, d_val] */
+  float *d_lin_w;         /* [D, d_emo + d_aro + d_val] */
+  float *d_lin_b;         /* [D] */
+} fs2_cond_grads;
+int64_t fs2_cond_bwd_ws_bytes(int B, int D);
+int fs2_cond_bwd(const float *dy, int B, int L, int D, const fs2_cond_desc *fwd, const fs2_cond_grads *grads,
+                 void *ws, int64_t ws_bytes, fs2_stream_t stream);
+
+/*
  * fs2_embed_pe — out[b,l,:] = table[tokens[b,l], :] + pe[l, :]   (f32 math)
  * Replaces Encoder src_word_emb + position_enc (transformer/Models.py:82-91).
  * A token outside [0, vocab) — the reference's nn.Embedding raises IndexError (CPU) or a

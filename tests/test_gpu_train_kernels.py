@@ -537,3 +537,65 @@ def test_deferred_reductions_bit_identical(ops):
         assert close(t1, t2)
     assert close(w9a, w9b) and close(b9a, b9b) and torch.equal(w9b, w9c)
     assert close(ga, gb) and close(ba, bb) and close(bia, bib)
+
+
+@pytest.mark.parametrize("B,Lx,spk,emo", [(16, 64, True, True), (5, 37, True, True), (7, 20, False, True),
+                                          (3, 11, True, False)])
+def test_cond_fn_fwd_bwd(ops, B, Lx, spk, emo):
+    """training.CondFn (fs2_cond_vectors + the two adds; backward fs2_cond_bwd): y = x + spk[s] +
+    relu(W cat(emo[e], aro[a], val[v]) + b) (model/fastspeech2.py:101-110) and the gradients of x,
+    the four tables, W and b against float64 autograd; repeated ids (their rows summed), relu-dead
+    channels (bias shifted negative), accumulation into existing gradients through the sink path's
+    fs2_cond_bwd call; two backward calls bit-identical."""
+    from fs2amd.training import CondFn
+
+    torch.manual_seed(B * 100 + Lx)
+    D = 256
+    x = torch.randn(B, Lx, D)
+    ts = torch.randn(5, D)
+    te, ta, tv = torch.randn(7, 128), torch.randn(3, 64), torch.randn(4, 64)
+    W, bl = torch.randn(D, 256) / 16, torch.randn(D) - 0.5
+    s_id = torch.randint(0, 5, (B,))
+    e_id, a_id, v_id = torch.randint(0, 7, (B,)), torch.randint(0, 3, (B,)), torch.randint(0, 4, (B,))
+    dev = lambda t: t.to(DEV).contiguous()
+    params = [dev(t).requires_grad_() if on else None
+              for t, on in ((ts, spk), (te, emo), (ta, emo), (tv, emo), (W, emo), (bl, emo))]
+    xg = dev(x).requires_grad_()
+    y = CondFn.apply(xg, dev(s_id) if spk else None, dev(e_id) if emo else None, dev(a_id) if emo else None,
+                     dev(v_id) if emo else None, *params)
+    dy = torch.randn(B, Lx, D)
+    y.backward(dev(dy))
+    torch.cuda.synchronize()
+    # float64 reference
+    ref_p = [t.double().requires_grad_() if on else None
+             for t, on in ((ts, spk), (te, emo), (ta, emo), (tv, emo), (W, emo), (bl, emo))]
+    xd = x.double().requires_grad_()
+    r = xd
+    if spk:
+        r = r + ref_p[0][s_id].unsqueeze(1)
+    if emo:
+        cat = torch.cat([ref_p[1][e_id], ref_p[2][a_id], ref_p[3][v_id]], -1)
+        r = r + torch.relu(cat @ ref_p[4].t() + ref_p[5]).unsqueeze(1)
+    r.backward(dy.double())
+    assert float((y.detach().cpu().double() - r.detach()).abs().max()) <= 1e-5 * float(r.detach().abs().max())
+    assert torch.equal(xg.grad.cpu(), dy)
+    for got, want in zip(params, ref_p):
+        if got is None:
+            continue
+        g = got.grad.cpu().double()
+        assert float((g - want.grad).abs().max()) <= 2e-5 * max(1.0, float(want.grad.abs().max())), \
+            (tuple(got.shape), float((g - want.grad).abs().max()))
+    # accumulation (the sink path): into existing gradients, deterministic
+    if emo:
+        dt = torch.zeros(ta.shape, device=DEV)
+        dw = [torch.full_like(W, 0.5, device=DEV) for _ in range(2)]
+        for k in range(2):
+            ops.cond_bwd(dev(dy), dev(s_id) if spk else None, params[0], dev(e_id), dev(a_id), dev(v_id),
+                         params[1], params[2], params[3], params[4],
+                         ops.cond_vectors(dev(s_id) if spk else None, params[0], dev(e_id), dev(a_id), dev(v_id),
+                                          params[1], params[2], params[3], params[4], params[5], D)[1].detach(),
+                         d_aro=dt if k == 0 else None, d_w=dw[k])
+        torch.cuda.synchronize()
+        assert torch.equal(dw[0], dw[1])
+        assert torch.allclose(dw[0].cpu().double(), ref_p[4].grad + 0.5, rtol=1e-5, atol=2e-5 * float(ref_p[4].grad.abs().max()))
+        assert torch.allclose(dt.cpu().double(), ref_p[2].grad, rtol=1e-5, atol=2e-5 * float(ref_p[2].grad.abs().max()))

@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
     lib = _lib.load()
     declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
-    assert len(declared) == len(_lib.SIGNATURES) == 66
+    assert len(declared) == len(_lib.SIGNATURES) == 68
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
@@ -64,7 +64,8 @@ int main(void){ P(x) P(x_row_stride) P(w) P(B) P(compute) P(residual) P(res_row_
                                           ("fs2_vp_fused_desc", "VpFusedDesc"), ("fs2_ffn8_desc", "Ffn8Desc"),
                                           ("fs2_pack_desc", "PackDesc"), ("fs2_loss_args", "LossArgs"),
                                           ("fs2_adam_param", "AdamParam"), ("fs2_reduce_desc", "ReduceDesc"),
-                                          ("fs2_reduce_batch", "ReduceBatch"), ("fs2_cond_desc", "CondDesc")])
+                                          ("fs2_reduce_batch", "ReduceBatch"), ("fs2_cond_desc", "CondDesc"),
+                                          ("fs2_cond_grads", "CondGrads")])
 def test_ffn_desc_layout_matches_header(cname, pyname):
     """ctypes mirrors of fs2_ffn_desc / fs2_wconv_desc have the C layout (every field's offset, and
     the size)."""

@@ -224,6 +224,19 @@ def main():
                 _, x = ops.vp_fused(x, V.dp, le, embed=emb_p)
             if a.kernel != "vpf_dp":
                 ops.vp_fused(x, V.energy, le, embed=emb_e)
+    elif a.kernel == "cond_bwd":  # the training conditioning backward (fs2_cond_bwd) at cfg3's B = 16, L = 64
+        m = model
+        Bq, Lq = 16, 64
+        ids = [torch.randint(0, n, (Bq,), generator=g).to(dev) for n in
+               (m.speaker_emb.num_embeddings, m.emotion_emb.num_embeddings, m.arousal_emb.num_embeddings,
+                m.valence_emb.num_embeddings)]
+        tabs = [m.speaker_emb.weight, m.emotion_emb.weight, m.arousal_emb.weight, m.valence_emb.weight]
+        lw, lb = m.emotion_linear[0].weight, m.emotion_linear[0].bias
+        _, emo_o = ops.cond_vectors(ids[0], tabs[0], ids[1], ids[2], ids[3], tabs[1], tabs[2], tabs[3], lw, lb, 256)
+        dyq = torch.randn(Bq, Lq, 256, generator=g).to(dev)
+        grads = [torch.zeros_like(t) for t in tabs] + [torch.zeros_like(lw), torch.zeros_like(lb)]
+        fn = lambda: ops.cond_bwd(dyq, ids[0], tabs[0], ids[1], ids[2], ids[3], tabs[1], tabs[2], tabs[3], lw, emo_o,
+                                  *grads)
     elif a.kernel == "reduce_ln":  # 8 LayerNorm-parameter partial sets (256 partial blocks x 768) in one launch
         parts = [torch.randn(256 * 768, generator=g).to(dev) for _ in range(8)]
         outs = [[torch.empty(256, device=dev) for _ in range(3)] for _ in range(8)]
