@@ -903,9 +903,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
 
 }  // namespace
 
-extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
-                             int H, int dk, float temperature, void *out, int64_t out_row_stride,
-                             const int32_t *seq_cu, float *lse, fs2_stream_t stream) {
+static int attention_launch(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
+                            int H, int dk, float temperature, void *out, int64_t out_row_stride,
+                            const int32_t *seq_cu, float *lse, int waves, fs2_stream_t stream) {
   if (qkv == nullptr || (key_lens == nullptr && seq_cu == nullptr) || out == nullptr) return FS2_EINVAL;
   if (dk != DK || H <= 0 || B < 0 || T < 0 || !(temperature > 0.f)) return FS2_EINVAL;
   if (qkv_row_stride < 3LL * H * dk || out_row_stride < (int64_t)H * dk) return FS2_EINVAL;
@@ -935,14 +935,18 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
       const char *e = getenv("FS2_OUT_SC1"), *f = getenv("FS2_ATTN_OSTAGE");
       return ((e != nullptr && e[0] == '0') ? 0 : 1) | ((f != nullptr && f[0] == '0') ? 0 : 2);
     }();
-    // waves x K/V ring stages: 4x2. 8x2 (FS2_ATTN32_FORM=8x2) is 1.2 us faster at the cfg2 decoder
-    // shape (24.1 vs 25.3 us) but with a long max length over short sequences (free-running cfg2:
-    // T 960, mean 174 frames) its 256-query tiles leave most (utterance, head) pairs ONE workgroup
-    // and the forward ~0.1 ms slower; the host knows only T here. 8x3: 25.4-26.2 us.
-    static const int form32 = [] {
+    // waves x K/V ring stages: 4x2, or 8x2 when the caller says the sequences are long and dense
+    // (fs2_attention_ex waves = 8: the cfg2 decoder, ~390 of T = 430 frames each: 145.2 vs
+    // 148.4-149.3 us of decoder attention per forward, same box). With a long max length over short
+    // sequences (free-running cfg2: T 960, mean 174 frames) the 256-query tiles leave most
+    // (utterance, head) pairs ONE workgroup (forced 8x2: 1.2845 vs 1.2253 ms per call), and cfg4
+    // (8.58 vs 8.49 ms); the kernel sees only T, so the caller decides. FS2_ATTN32_FORM=4x2 / 8x2 /
+    // 8x3 overrides (8x3: 25.4-26.2 us at cfg2).
+    static const int form_env = [] {
       const char *e = getenv("FS2_ATTN32_FORM");
-      return e == nullptr ? 0 : (e[0] == '8' && e[2] == '3') ? 2 : (e[0] == '8') ? 1 : 0;
+      return e == nullptr ? -1 : (e[0] == '8' && e[2] == '3') ? 2 : (e[0] == '8') ? 1 : 0;
     }();
+    const int form32 = form_env >= 0 ? form_env : (waves == 8 ? 1 : 0);
     if (T > 64 && use32 && form32 == 0) {
       // 4 waves x 32 queries, two workgroups per CU (2 x 64 KiB of K / V ring)
       const int nqt = (T + 127) / 128;
@@ -979,4 +983,19 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
     return FS2_EUNSUPPORTED;
   FS2_CHECK_LAUNCH();
   return FS2_OK;
+}
+
+extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
+                             int H, int dk, float temperature, void *out, int64_t out_row_stride,
+                             const int32_t *seq_cu, float *lse, fs2_stream_t stream) {
+  return attention_launch(qkv, dtype, qkv_row_stride, key_lens, B, T, H, dk, temperature, out, out_row_stride, seq_cu,
+                          lse, 0, stream);
+}
+
+extern "C" int fs2_attention_ex(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B,
+                                int T, int H, int dk, float temperature, void *out, int64_t out_row_stride,
+                                const int32_t *seq_cu, float *lse, int waves, fs2_stream_t stream) {
+  if (waves != 0 && waves != 4 && waves != 8) return FS2_EINVAL;
+  return attention_launch(qkv, dtype, qkv_row_stride, key_lens, B, T, H, dk, temperature, out, out_row_stride, seq_cu,
+                          lse, waves, stream);
 }

@@ -765,11 +765,23 @@ def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None, lse=No
     _check_attention_args(qkv, lens, B, n_head, d_k, layout)
     if out is None:
         out = torch.empty(*shape, device=qkv.device, dtype=qkv.dtype)
-    L.check(_lib.fs2_attention(_ptr(qkv), _dt(qkv), _rows(qkv, "qkv"), _ptr(lens), B, T, n_head, d_k,
-                               float(temperature), _ptr(out), _rows(out, "out"),
-                               _ptr(layout.cu) if layout is not None else None, _ptr(lse), _stream(qkv)),
-            "fs2_attention")
+    L.check(_lib.fs2_attention_ex(_ptr(qkv), _dt(qkv), _rows(qkv, "qkv"), _ptr(lens), B, T, n_head, d_k,
+                                  float(temperature), _ptr(out), _rows(out, "out"),
+                                  _ptr(layout.cu) if layout is not None else None, _ptr(lse),
+                                  attention_waves(B, T, layout), _stream(qkv)),
+            "fs2_attention_ex")
     return out
+
+
+def attention_waves(B, T, layout=None):
+    """fs2_attention_ex's work-shape hint: 8 waves (256-query tiles) for long, dense sequences —
+    64 < T <= 512 and, when the host knows the packed row count (free-running synthesis sets
+    layout.rows_hint), at least 70 % of B * T valid; else 4. (Teacher-forced batches, whose row
+    count the host does not see, are taken as dense.) Results do not depend on it."""
+    if not 64 < T <= 512:
+        return 4
+    rows = getattr(layout, "rows_hint", None) if layout is not None else None
+    return 8 if rows is None or rows >= 0.7 * B * T else 4
 
 
 def enc_attn_block(x, lens, wqkv_frag, bqkv, wfc_frag, bfc, ln, n_head, d_k, temperature, out=None, embed=None,

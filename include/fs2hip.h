@@ -354,6 +354,12 @@ int64_t fs2_wconv_weight_elems(int KS, int Cin, int N); /* N*KS*Cin */
 int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
                   int H, int dk, float temperature, void *out, int64_t out_row_stride, const int32_t *seq_cu,
                   float *lse, fs2_stream_t stream);
+/* fs2_attention with the caller's work-shape hint: waves = 8 (256 queries per workgroup: long,
+   dense sequences — most of [B, T] valid, T <= 512), 4 (128 queries) or 0 (fs2_attention's
+   default, 4). Same results either way (each query's arithmetic does not depend on the grouping). */
+int fs2_attention_ex(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
+                     int H, int dk, float temperature, void *out, int64_t out_row_stride, const int32_t *seq_cu,
+                     float *lse, int waves, fs2_stream_t stream);
 
 /*
  * fs2_enc_attn_block — the encoder FFT block's attention sub-layer as ONE launch (bf16): Q|K|V

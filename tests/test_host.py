@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
     lib = _lib.load()
     declared = _lib.header_symbols(os.path.join(REPO, "include", "fs2hip.h"))
-    assert len(declared) == len(_lib.SIGNATURES) == 68
+    assert len(declared) == len(_lib.SIGNATURES) == 69
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} not bound in fs2amd/_lib.py"
@@ -323,7 +323,7 @@ def test_forward_launch_sequence_dry_run(monkeypatch, packed, teacher, streams):
     # per group: 10 FFT blocks x 4 GEMMs + 3 VPs x 2 + mel_linear + 5 PostNet convs (these batches
     # are not mostly padding: the padded PostNet form)
     assert n_conv == k * (10 * 4 + 6 + 1 + 5), rec.calls
-    assert rec.calls.count("fs2_attention") == k * 10
+    assert rec.calls.count("fs2_attention_ex") == k * 10
     # the packed decoder's layout: built by the one-launch LengthRegulator (fs2_lr_fused)
     assert any(c.startswith("fs2_lr_fused") for c in rec.calls) == (packed == "1")
     assert ("fs2_lr_expand" in rec.calls) == (packed == "0")
@@ -350,7 +350,7 @@ def test_training_step_dry_run(monkeypatch):
     got = {k for k, p in m.named_parameters() if p.grad is not None}
     ref = {str(k) for k in np.load(f"{GOLDEN}/train_grads.npz")["grad_keys"]}
     assert got == ref, got ^ ref
-    assert "fs2_conv1d" in lib.calls and "fs2_attention" in lib.calls
+    assert "fs2_conv1d" in lib.calls and "fs2_attention_ex" in lib.calls
 
 
 def test_loss_matches_oracle_masked_select_form():
