@@ -539,12 +539,32 @@ __device__ __forceinline__ rsrc_t make_rsrc_any(const void *p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int NWV, int NST>
+// Key-split form (SPL; packed rows with their work list, no lse). A sequence longer than
+// kSplitKeys keys is cut into kSplitKeys-key ranges, one workgroup per (query tile, head, range):
+// each stores its unnormalised O, running max and sum (write-through) in a workspace slot and the
+// last range of the (query tile, head) to arrive (an arrival counter) merges them in range order
+// and stores the output; a sequence of <= kSplitKeys keys runs exactly the unsplit arithmetic. The
+// workgroups take the items of a compact list (attn_items_kernel, once per packed layout: a dense
+// (query tile, head, sequence, range) grid over a free-running batch is ~90 % empty workgroups,
+// each paying a memory round trip to find out), so the grid is one workgroup per item. A
+// sequence's split depends on its own length only: the result does not depend on T.
+constexpr int kSplitKeys = 256;
+constexpr int kSplitMax = 8;   // ranges per sequence (T <= 2048)
+constexpr int kPartLane = 68;  // floats per lane: O^T 64, m, l, 2 pad (17 pieces of 16 bytes)
+
+struct SplitArgs {
+  const int *items;  // (b << 16) | (qt << 8) | (s << 4) | h
+  const int *count;  // number of items
+  float *part;       // partials: slot (tile, head) x kSplitMax ranges x 17 pieces x 256 lanes x 16 B
+  int *cnt;          // arrival counters per slot (zero between launches)
+};
+
+template <int NWV, int NST, bool SPL = false>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *__restrict__ qkv, int64_t qs, uint32_t qkv_bytes,
                                                              const int64_t *__restrict__ lens, int B, int T, int H, int nqt,
                                                              float scale_log2, bf16 *__restrict__ out, int64_t os,
                                                              const int32_t *__restrict__ cu, float *__restrict__ lse,
-                                                             int oflags) {
+                                                             int oflags, SplitArgs sa = SplitArgs{}) {
   constexpr int KTT = 64;
   constexpr int QTW = 32 * NWV;       // queries per workgroup
   constexpr int PPW = KTT / 4 / NWV;  // K (and V) 1 KiB pieces per wave per tile
@@ -558,10 +578,23 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
 
   // XCD-contiguous work order, as attn_bf16_kernel
   const int nwg = gridDim.x, id = blockIdx.x;
-  const int q8 = nwg >> 3, rem = nwg & 7, xcd = id & 7;
-  const int t = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (id >> 3);
-  const int qt = t % nqt, bh = t / nqt, h = bh % H, b = bh / H;
+  int qt, h, b, s = 0;
+  if constexpr (SPL) {
+    // item groups of 4 (consecutive ranges / query tiles of one sequence and head: shared K / V in
+    // one L2) dealt round-robin over the XCDs, so a list shorter than the grid still covers all 8
+    const int k = id >> 3, t = ((k >> 2) << 5) + ((id & 7) << 2) + (k & 3);
+    if (t >= *sa.count) return;
+    const int it = sa.items[t];
+    b = it >> 16, qt = (it >> 8) & 0xff, s = (it >> 4) & 0xf, h = it & 0xf;
+  } else {
+    const int q8 = nwg >> 3, rem = nwg & 7, xcd = id & 7;
+    const int t = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + (id >> 3);
+    qt = t % nqt;
+    const int bh = t / nqt;
+    h = bh % H, b = bh / H;
+  }
   const int q0 = qt * QTW;
+  const int T_all = T;
   int len;
   uint32_t seq_base;
   if (cu != nullptr) {
@@ -574,6 +607,12 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
     seq_base = (uint32_t)b * (uint32_t)T;
   }
   if (q0 >= T) return;
+  int k_lo = 0, k_hi = len, nsp = 1;
+  if constexpr (SPL) {
+    nsp = (len + kSplitKeys - 1) / kSplitKeys;
+    k_lo = s * kSplitKeys;
+    k_hi = k_lo + kSplitKeys < len ? k_lo + kSplitKeys : len;
+  }
   const bool active = q0 + 32 * w < T;  // wave-uniform
 #if ATTN_TRACE
   unsigned long long tst[4];
@@ -629,10 +668,10 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
     for (int r = 0; r < 16; ++r) oacc[i][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;  // m: raw score units, both lane halves equal; l: this half's keys
 
-  const int ntiles = (len + KTT - 1) / KTT;
+  const int ntiles = (k_hi - k_lo + KTT - 1) / KTT;
 #pragma unroll
   for (int st = 0; st < NST - 1; ++st)
-    if (st < ntiles) dma(st * KTT, st);
+    if (st < ntiles) dma(k_lo + st * KTT, st);
   // transposed V reads: 16-lane group gq = lane >> 4 takes dims 16 (gq & 1) .. +15 of a 32-dim
   // block and key rows 4 (gq >> 1) + q (+ 8 for the second read); lane 4q + p of the group
   // addresses row q, dims 4p .. 4p + 3 (chunk 2 (gq & 1) + (p >> 1), byte 8 (p & 1))
@@ -660,7 +699,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
   auto tile = [&](int kt, auto slot_tag, auto masked_tag) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_tag)::value;
     constexpr bool MASKED = decltype(masked_tag)::value;
-    const int k0 = kt * KTT;
+    const int k0 = k_lo + kt * KTT;
     const int ahead = ntiles - 1 - kt;
     if (ATTN_ABL & 8)
       ;
@@ -834,6 +873,92 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
     auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
     l_run = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
   }
+  if constexpr (SPL) {
+    if (nsp > 1) {
+      // the range's partial -> slot (query tile of the sequence, head): piece q4 of every lane
+      // contiguous (each store / load of a wave one 1 KiB run; a lane-major image made every
+      // instruction 64 partial-line writes)
+      const int64_t slot = (int64_t)((cu[b] >> 7) + b + qt) * H + h;  // distinct: see split_layout
+      const int S = (T_all + kSplitKeys - 1) / kSplitKeys;             // ranges per slot
+      const rsrc_t prs = make_rsrc_any(sa.part, 0x7fffffffu);
+      auto pofs = [&](int sr, int q4) {
+        return (uint32_t)(((((slot * S + sr) * (kPartLane / 4) + q4) * (64 * NWV) + (64 * w + lane)) * 4) * 4);
+      };
+#pragma unroll
+      for (int db = 0; db < DK / 32; ++db)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
+                                 f32x4{oacc[db][4 * r4], oacc[db][4 * r4 + 1], oacc[db][4 * r4 + 2], oacc[db][4 * r4 + 3]}),
+              prs, pofs(s, 4 * db + r4), 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, f32x4{m_run, l_run, 0.f, 0.f}), prs,
+          pofs(s, 16), 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      __shared__ int last_s;
+      if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(sa.cnt + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int lst = old == nsp - 1;
+        if (lst) {
+          __hip_atomic_store(sa.cnt + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        last_s = lst;
+      }
+      __syncthreads();
+      if (!last_s) return;
+      // merge in range order: M = max_r m_r; O = sum_r O_r 2^((m_r - M) scale); l likewise. The
+      // m / l pieces of all ranges, then the O pieces two ranges at a time, loaded ahead of use.
+      float M = -INFINITY, mls[kSplitMax][2];
+#pragma unroll
+      for (int sr = 0; sr < kSplitMax; ++sr) {
+        if (sr < nsp) {
+          const f32x4 ml = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, pofs(sr, 16), 0, 16));
+          mls[sr][0] = ml[0];
+          mls[sr][1] = ml[1];
+        } else {
+          mls[sr][0] = -INFINITY;
+          mls[sr][1] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int sr = 0; sr < kSplitMax; ++sr) M = max_nn(M, mls[sr][0]);
+      float lt = 0.f;
+#pragma unroll
+      for (int db = 0; db < DK / 32; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[db][r] = 0.f;
+#pragma unroll
+      for (int sr = 0; sr < kSplitMax; sr += 2) {
+        if (sr >= nsp) break;
+        f32x4 v[2][16];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int q4 = 0; q4 < 16; ++q4)
+            v[u][q4] = sr + u < nsp
+                           ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, pofs(sr + u, q4), 0, 16))
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const float mu = mls[sr + u][0];
+          const float a = mu == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((mu - M) * scale_log2);
+          lt = __builtin_fmaf(mls[sr + u][1], a, lt);
+#pragma unroll
+          for (int db = 0; db < DK / 32; ++db)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4)
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                oacc[db][4 * r4 + j] = __builtin_fmaf(v[u][4 * db + r4][j], a, oacc[db][4 * r4 + j]);
+        }
+      }
+      l_run = lt;
+      m_run = M;
+    }
+  }
   const float inv = l_run > 0.f ? 1.0f / l_run : 0.f;
   if (active && qrow < T && lse != nullptr && hh == 0)
     lse[((int64_t)seq_base + qrow) * H + h] = l_run > 0.f ? m_run * scale_log2 + __log2f(l_run) : INFINITY;
@@ -901,11 +1026,67 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void attn32_kernel(const bf16 *_
 #endif
 }
 
+// The key-split work list of a packed layout: for every sequence b (len = cu[b+1] - cu[b] > 0),
+// heads h, query tiles qt < ceil(len / 128) and ranges s < ceil(len / kSplitKeys) (1 when len <=
+// kSplitKeys): one item, in (b, h, qt, s) order; *count = their number. ONE wave: a shuffle scan
+// over 64 sequences at a time (a 1024-thread block scan with its barriers took ~10 us in the graph).
+__global__ __launch_bounds__(64) void attn_items_kernel(const int32_t *__restrict__ cu, int B, int H,
+                                                        int *__restrict__ items, int *__restrict__ count, int cap,
+                                                        int *__restrict__ cnt, int slots) {
+  const int lane = threadIdx.x;
+  for (int i = lane; i < slots; i += 64) cnt[i] = 0;  // the arrival counters start at zero
+  int carry = 0;
+  for (int b0 = 0; b0 < B; b0 += 64) {
+    const int b = b0 + lane;
+    int nq = 0, ns = 1;
+    if (b < B) {
+      const int len = cu[b + 1] - cu[b];
+      nq = len > 0 ? (len + 127) / 128 : 0;
+      ns = len > kSplitKeys ? (len + kSplitKeys - 1) / kSplitKeys : 1;
+    }
+    const int n = nq * ns * H;
+    int inc = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += v;
+    }
+    const int off = carry + inc - n;
+    for (int h = 0; h < H; ++h)
+      for (int qt = 0; qt < nq; ++qt)
+        for (int s = 0; s < ns; ++s) {
+          const int i = off + (h * nq + qt) * ns + s;
+          if (i < cap) items[i] = (b << 16) | (qt << 8) | (s << 4) | h;
+        }
+    carry += __shfl(inc, 63, 64);
+  }
+  if (lane == 0) *count = carry < cap ? carry : cap;
+}
+
 }  // namespace
+
+// the key-split workspace: [count, pad][items: cap][arrival counters: slots][partials: slots x S
+// ranges]. A slot is (cu[b] >> 7) + b + qt per sequence query tile and head: distinct, and below
+// (rows_max / 128 + B + ceil(T / 128)) * H when cu[B] <= rows_max; items <= that many x S.
+struct SplitLayout {
+  int64_t slots, cap, items_off, cnt_off, part_off, bytes;
+};
+static SplitLayout split_layout(int B, int T, int H, int64_t rows_max) {
+  SplitLayout l;
+  const int S = (T + kSplitKeys - 1) / kSplitKeys;
+  l.slots = (rows_max / 128 + B + (T + 127) / 128) * (int64_t)H;
+  l.cap = l.slots * S;
+  l.items_off = 256;
+  l.cnt_off = (l.items_off + l.cap * 4 + 255) / 256 * 256;
+  l.part_off = (l.cnt_off + l.slots * 4 + 255) / 256 * 256;
+  l.bytes = l.part_off + l.slots * S * 256 * kPartLane * 4;
+  return l;
+}
 
 static int attention_launch(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
                             int H, int dk, float temperature, void *out, int64_t out_row_stride,
-                            const int32_t *seq_cu, float *lse, int waves, fs2_stream_t stream) {
+                            const int32_t *seq_cu, float *lse, int waves, void *split_ws, int64_t split_ws_bytes,
+                            int64_t rows_max, fs2_stream_t stream) {
   if (qkv == nullptr || (key_lens == nullptr && seq_cu == nullptr) || out == nullptr) return FS2_EINVAL;
   if (dk != DK || H <= 0 || B < 0 || T < 0 || !(temperature > 0.f)) return FS2_EINVAL;
   if (qkv_row_stride < 3LL * H * dk || out_row_stride < (int64_t)H * dk) return FS2_EINVAL;
@@ -947,7 +1128,23 @@ static int attention_launch(const void *qkv, int dtype, int64_t qkv_row_stride, 
       return e == nullptr ? -1 : (e[0] == '8' && e[2] == '3') ? 2 : (e[0] == '8') ? 1 : 0;
     }();
     const int form32 = form_env >= 0 ? form_env : (waves == 8 ? 1 : 0);
-    if (T > 64 && use32 && form32 == 0) {
+    if (split_ws != nullptr && use32) {
+      // the key-split form over the layout's work list (fs2_attention_items)
+      if (seq_cu == nullptr || lse != nullptr || T <= kSplitKeys || (T + kSplitKeys - 1) / kSplitKeys > kSplitMax ||
+          H > 16 || rows_max <= 0 || rows_max > (int64_t)B * T)
+        return FS2_EINVAL;
+      const SplitLayout l = split_layout(B, T, H, rows_max);
+      if (split_ws_bytes < l.bytes) return FS2_EINVAL;
+      if (l.bytes - l.part_off >= (1LL << 31) || l.cap >= (1LL << 31) - 64) return FS2_EUNSUPPORTED;
+      char *w0 = static_cast<char *>(split_ws);
+      SplitArgs sa{reinterpret_cast<const int *>(w0 + l.items_off), reinterpret_cast<const int *>(w0),
+                   reinterpret_cast<float *>(w0 + l.part_off), reinterpret_cast<int *>(w0 + l.cnt_off)};
+      const int64_t nwg = (l.cap + 31) / 32 * 32;  // whole groups of 4 items per XCD
+      hipLaunchKernelGGL((attn32_kernel<4, 2, true>), dim3((unsigned)nwg), dim3(256), 0, s,
+                         reinterpret_cast<const bf16 *>(qkv), qkv_row_stride, (uint32_t)bytes, key_lens, B, T, H,
+                         (T + 127) / 128, scale_log2, reinterpret_cast<bf16 *>(out), out_row_stride, seq_cu, lse,
+                         oflags, sa);
+    } else if (T > 64 && use32 && form32 == 0) {
       // 4 waves x 32 queries, two workgroups per CU (2 x 64 KiB of K / V ring)
       const int nqt = (T + 127) / 128;
       hipLaunchKernelGGL((attn32_kernel<4, 2>), dim3(nqt * H * B), dim3(256), 0, s,
@@ -989,13 +1186,35 @@ extern "C" int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride,
                              int H, int dk, float temperature, void *out, int64_t out_row_stride,
                              const int32_t *seq_cu, float *lse, fs2_stream_t stream) {
   return attention_launch(qkv, dtype, qkv_row_stride, key_lens, B, T, H, dk, temperature, out, out_row_stride, seq_cu,
-                          lse, 0, stream);
+                          lse, 0, nullptr, 0, 0, stream);
 }
 
 extern "C" int fs2_attention_ex(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B,
                                 int T, int H, int dk, float temperature, void *out, int64_t out_row_stride,
-                                const int32_t *seq_cu, float *lse, int waves, fs2_stream_t stream) {
+                                const int32_t *seq_cu, float *lse, int waves, void *split_ws, int64_t split_ws_bytes,
+                                int64_t rows_max, fs2_stream_t stream) {
   if (waves != 0 && waves != 4 && waves != 8) return FS2_EINVAL;
   return attention_launch(qkv, dtype, qkv_row_stride, key_lens, B, T, H, dk, temperature, out, out_row_stride, seq_cu,
-                          lse, waves, stream);
+                          lse, waves, split_ws, split_ws_bytes, rows_max, stream);
+}
+
+extern "C" int64_t fs2_attention_split_ws_bytes(int B, int T, int H, int64_t rows_max) {
+  if (B <= 0 || T <= kSplitKeys || (T + kSplitKeys - 1) / kSplitKeys > kSplitMax || H <= 0 || H > 16 || rows_max <= 0)
+    return 0;
+  return split_layout(B, T, H, rows_max).bytes;
+}
+
+extern "C" int fs2_attention_items(const int32_t *seq_cu, int B, int T, int H, void *split_ws, int64_t split_ws_bytes,
+                                   int64_t rows_max, fs2_stream_t stream) {
+  if (seq_cu == nullptr || split_ws == nullptr || B <= 0 || B >= 32768 || T <= kSplitKeys || T > 256 * 128 ||
+      H <= 0 || H > 16 || rows_max <= 0 || rows_max > (int64_t)B * T)
+    return FS2_EINVAL;
+  const SplitLayout l = split_layout(B, T, H, rows_max);
+  if (split_ws_bytes < l.bytes) return FS2_EINVAL;
+  char *w0 = static_cast<char *>(split_ws);
+  hipLaunchKernelGGL(attn_items_kernel, dim3(1), dim3(64), 0, as_stream(stream), seq_cu, B, H,
+                     reinterpret_cast<int *>(w0 + l.items_off), reinterpret_cast<int *>(w0), (int)l.cap,
+                     reinterpret_cast<int *>(w0 + l.cnt_off), (int)l.slots);
+  FS2_CHECK_LAUNCH();
+  return FS2_OK;
 }

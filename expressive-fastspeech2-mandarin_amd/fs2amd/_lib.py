@@ -175,7 +175,9 @@ SIGNATURES = {
     "fs2_wconv": (_i, [ctypes.POINTER(WconvDesc), _p]),
     "fs2_wconv_weight_elems": (ctypes.c_int64, [_i, _i, _i]),
     "fs2_attention": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p, _p]),
-    "fs2_attention_ex": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p, _i, _p]),
+    "fs2_attention_ex": (_i, [_p, _i, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p, _i, _p, _i64, _i64, _p]),
+    "fs2_attention_split_ws_bytes": (_i64, [_i, _i, _i, _i64]),
+    "fs2_attention_items": (_i, [_p, _i, _i, _i, _p, _i64, _i64, _p]),
     "fs2_embed_pe": (_i, [_p, _p, _i, _p, _i, _i, _i, _p, _i, _p, _p]),
     "fs2_attention_bwd": (_i, [_p, _i, _i64, _p, _i64, _p, _i64, _p, _i, _i, _i, _i, _f, _p, _i64, _p, _p, _i64, _p,
                                _p]),

@@ -765,12 +765,42 @@ def attention(qkv, lens, n_head, d_k, temperature, out=None, layout=None, lse=No
     _check_attention_args(qkv, lens, B, n_head, d_k, layout)
     if out is None:
         out = torch.empty(*shape, device=qkv.device, dtype=qkv.dtype)
+    ws, ws_bytes, rows_max = None, 0, 0
+    if attention_split_on(B, T, n_head, layout, lse, qkv.dtype):
+        ws, ws_bytes, rows_max = _attn_split_items(layout, B, T, n_head, qkv)
     L.check(_lib.fs2_attention_ex(_ptr(qkv), _dt(qkv), _rows(qkv, "qkv"), _ptr(lens), B, T, n_head, d_k,
                                   float(temperature), _ptr(out), _rows(out, "out"),
                                   _ptr(layout.cu) if layout is not None else None, _ptr(lse),
-                                  attention_waves(B, T, layout), _stream(qkv)),
+                                  attention_waves(B, T, layout), _ptr(ws), ws_bytes, rows_max, _stream(qkv)),
             "fs2_attention_ex")
     return out
+
+
+def attention_split_on(B, T, H, layout, lse, dtype):
+    """Key-split attention (fs2_attention_ex split_ws): packed rows whose active row count the host
+    knows (free-running synthesis sets layout.rows_hint), 256 < T <= 2048, bf16, inference (no lse).
+    The split arithmetic depends on each sequence's length only, so every T bucket of a batch gives
+    the same result. FS2_ATTN_SPLIT=0 turns it off."""
+    if os.environ.get("FS2_ATTN_SPLIT", "1") == "0" or lse is not None or dtype != torch.bfloat16:
+        return False
+    if layout is None or getattr(layout, "rows_hint", None) is None:
+        return False
+    return _lib.fs2_attention_split_ws_bytes(B, T, H, int(layout.rows_hint)) > 0
+
+
+def _attn_split_items(layout, B, T, H, like):
+    """The layout's key-split workspace with its work list (fs2_attention_items: one launch per
+    layout, reused by every layer; it also zeroes the arrival counters). The workspace is owned by
+    the layout, so a captured graph keeps its own."""
+    rows_max = int(layout.rows_hint)
+    nbytes = _lib.fs2_attention_split_ws_bytes(B, T, H, rows_max)
+    st = getattr(layout, "_attn_split", None)
+    if st is None or st[1] != nbytes:
+        ws = torch.empty(nbytes, device=like.device, dtype=torch.uint8)
+        L.check(_lib.fs2_attention_items(_ptr(layout.cu), B, T, H, _ptr(ws), nbytes, rows_max, _stream(like)),
+                "fs2_attention_items")
+        st = layout._attn_split = (ws, nbytes)
+    return st[0], nbytes, rows_max
 
 
 def attention_waves(B, T, layout=None):

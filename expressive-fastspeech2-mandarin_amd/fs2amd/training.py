@@ -470,7 +470,7 @@ class CondFn(torch.autograd.Function):
 def cond_fused_on(model, x):
     """CondFn applies: f32 positions, fs2_cond_bwd's limits (B <= 64 and its LDS bound), at least one
     conditioning table; FS2_TRAIN_COND=0 keeps the per-op autograd form."""
-    if os.environ.get("FS2_TRAIN_COND", "1") == "0" or x.dtype != torch.float32:
+    if os.environ.get("FS2_TRAIN_COND", "1") == "0" or x.dtype != torch.float32 or not x.is_cuda:
         return False
     if model.speaker_emb is None and model.emotion_emb is None:
         return False

@@ -356,10 +356,24 @@ int fs2_attention(const void *qkv, int dtype, int64_t qkv_row_stride, const int6
                   float *lse, fs2_stream_t stream);
 /* fs2_attention with the caller's work-shape hint: waves = 8 (256 queries per workgroup: long,
    dense sequences — most of [B, T] valid, T <= 512), 4 (128 queries) or 0 (fs2_attention's
-   default, 4). Same results either way (each query's arithmetic does not depend on the grouping). */
+   default, 4). Same results either way (each query's arithmetic does not depend on the grouping).
+   split_ws != NULL: the key-split form (packed rows, lse == NULL, 256 < T <= 2048, H <= 16) over
+   the work list fs2_attention_items wrote into split_ws for the same seq_cu: a sequence longer
+   than 256 keys is cut into 256-key ranges, one workgroup each, merged by the last range of each
+   (query tile, head) to finish — a batch of many short and a few long sequences (free-running
+   synthesis) is no longer bound by the longest one's single workgroup. Those sequences' outputs
+   then differ from the unsplit form by f32 rounding and depend on their own length only (not on
+   T); shorter ones are bit-identical. rows_max >= seq_cu[B]; split_ws:
+   fs2_attention_split_ws_bytes(B, T, H, rows_max) bytes (fs2_attention_items zeroes its arrival
+   counters; each call leaves them zero). */
 int fs2_attention_ex(const void *qkv, int dtype, int64_t qkv_row_stride, const int64_t *key_lens, int B, int T,
                      int H, int dk, float temperature, void *out, int64_t out_row_stride, const int32_t *seq_cu,
-                     float *lse, int waves, fs2_stream_t stream);
+                     float *lse, int waves, void *split_ws, int64_t split_ws_bytes, int64_t rows_max,
+                     fs2_stream_t stream);
+int64_t fs2_attention_split_ws_bytes(int B, int T, int H, int64_t rows_max); /* 0: no split form */
+/* the key-split work list of a packed layout (one launch; every layer of a stack reuses it) */
+int fs2_attention_items(const int32_t *seq_cu, int B, int T, int H, void *split_ws, int64_t split_ws_bytes,
+                        int64_t rows_max, fs2_stream_t stream);
 
 /*
  * fs2_enc_attn_block — the encoder FFT block's attention sub-layer as ONE launch (bf16): Q|K|V

@@ -39,7 +39,7 @@ class ZeroingLib(RecordingLib):
                 d = args[0]._obj
                 es = 2 if d.out_dtype == 1 else 4
                 ctypes.memset(d.out, 0, d.B * d.T * (d.out_row_stride if d.epilogue != 6 else 1) * es)
-            elif name == "fs2_attention":
+            elif name in ("fs2_attention", "fs2_attention_ex"):
                 B, T, out, os_ = args[4], args[5], args[9], args[10]
                 ctypes.memset(out, 0, B * T * os_ * (2 if args[1] == 1 else 4))
             elif name == "fs2_attention_bwd":  # dqkv f32 [B*T, >= 3*H*dk] (else uninitialised memory)

@@ -618,3 +618,48 @@ def test_weight_resident_projection(ops, K, N, relu, packed):
     torch.cuda.synchronize()
     err = (got - ref).abs().max().item()
     assert err <= 1e-2 * ref.abs().max().item(), err
+
+
+def test_attention_key_split(ops, monkeypatch):
+    """fs2_attention_ex's key-split form over its work list (free-running synthesis: packed rows
+    with a known row count, T > 256): sequences of up to 959 keys in 256-key ranges merged by the
+    last range, against the float reference (2e-2 of the output scale, bf16 operands); sequences
+    of <= 256 keys bit-identical to the unsplit kernel; the result bit-identical for two T buckets
+    of the same batch (the split depends on each sequence's length only) and over repeated calls."""
+    g = torch.Generator().manual_seed(11)
+    H, dk = 2, 128
+    lens = torch.tensor([959, 12, 256, 257, 300, 520, 64, 700, 1, 180, 511, 768], dtype=torch.int64)
+    B, T = lens.numel(), 960
+    C = 3 * H * dk
+    qkv = torch.randn(B, T, C, generator=g).to(torch.bfloat16)
+
+    def run(Tb, split):
+        monkeypatch.setenv("FS2_ATTN_SPLIT", "1" if split else "0")
+        lay = ops.SeqLayout(lens.to(DEV), Tb)
+        lay.rows_hint = int(lens.sum())
+        rm = lay.rowmap.long().cpu()
+        ok = rm >= 0
+        src = torch.zeros(B, Tb, C, dtype=torch.bfloat16)
+        src[:, :min(T, Tb)] = qkv[:, :min(T, Tb)]
+        xp = torch.zeros(lay.capacity, C, dtype=torch.bfloat16)
+        xp[rm[ok]] = src.reshape(-1, C)[ok]
+        out = ops.attention(xp.to(DEV), None, H, dk, float(np.power(dk, 0.5)), layout=lay)
+        torch.cuda.synchronize()
+        cu = lay.cu.long().cpu()
+        return [out[int(cu[b]):int(cu[b + 1])].float().cpu() for b in range(B)]
+
+    split = run(T, True)
+    plain = run(T, False)
+    ref = _ref_attention(qkv.float(), lens, H, dk)
+    for b in range(B):
+        n = int(lens[b])
+        r = ref[b, :n]
+        err = float((split[b] - r).abs().max() / r.abs().max())
+        assert err < 2e-2, (b, n, err)
+        if n <= 256:
+            assert torch.equal(split[b], plain[b]), (b, n)
+    again = run(T, True)
+    other = run(1024, True)
+    for b in range(B):
+        assert torch.equal(again[b], split[b]), ("nondeterministic", b)
+        assert torch.equal(other[b], split[b]), ("T-dependent", b)

@@ -239,9 +239,11 @@ torch.save(outs, sys.argv[1])
         path = f"/tmp/fs2_packed_{tag}_{os.getpid()}.pt"
         # FS2_LR_PROJ=0: the packed decoder's first Q|K|V by linearity (fs2_lr_fused_proj) rounds
         # once instead of twice, so it is not bit-identical to the padded GEMM; test_lr_fused_proj
-        # and the oracle-level model tests cover it
+        # and the oracle-level model tests cover it. FS2_ATTN_SPLIT=0: the key-split attention of
+        # free-running packed rows merges its ranges in f32 (not bit-identical to one pass;
+        # test_gpu_ops.py::test_attention_key_split covers it)
         env = dict(os.environ, FS2_PACKED_DECODER=packed, FS2_STREAMS=streams, REPO=repo, FS2_CONV_SPLITK="0",
-                   FS2_CONV_PHASED="0", FS2_LR_PROJ="0")
+                   FS2_CONV_PHASED="0", FS2_LR_PROJ="0", FS2_ATTN_SPLIT="0")
         r = subprocess.run([sys.executable, "-c", code, path], env=env, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-3000:]
         res[tag] = torch.load(path, weights_only=True)

@@ -116,6 +116,13 @@ def main():
     elif a.kernel == "attn":
         qkv = rnd(B * T, 768)
         fn = lambda: ops.attention(qkv, None, 2, 128, 128 ** 0.5, layout=lay)
+    elif a.kernel == "attn_free":  # free-running-like packed attention: 63 short sequences + one of 959 frames
+        lf = torch.randint(60, 300, (64,), generator=g)
+        lf[7] = 959
+        layf = ops.SeqLayout(lf.to(dev), 960)
+        layf.rows_hint = ops.rows_bucket(int(lf.sum()), 64 * 960)
+        qkvf = rnd(layf.capacity, 768)
+        fn = lambda: ops.attention(qkvf, None, 2, 128, 128 ** 0.5, layout=layf)
     elif a.kernel == "lr":
         x = rnd(B, 64, 256)
         cum, ml, _ = ops.lr_durations(b["d_targets"])
