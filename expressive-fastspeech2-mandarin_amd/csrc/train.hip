@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256) void relu_ln_bwd_kernel(const float *__restric
 
 // Embedding backward (nn.Embedding autograd; src_word_emb with padding_idx, pitch / energy
 // bucket embeddings, speaker / emotion tables): workgroup v sums the dy rows of every position i
-// with tokens[i] == v in increasing i (chunks of 256 positions compacted in order through LDS),
+// with tokens[i] == v (chunks of 256 positions compacted in order through LDS) in a fixed order,
 // so the result is deterministic (no atomics). Row padding_idx gets no gradient.
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t *__restrict__ tokens, int64_t n,
                                                         const float *__restrict__ dy, int64_t dys, int D,
@@ -334,6 +334,8 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t *__restric
   __shared__ int wcnt[4];
   const int v = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   float acc = 0.f;
+  float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool vec = (D & 3) == 0 && (dys & 3) == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
   const bool skip = v == padding_idx;
   if (!skip)
     for (int64_t base = 0; base < n; base += 256) {
@@ -347,9 +349,28 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t *__restric
       const int total = (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
       if (hit) list[off + __popcll(m & ((1ull << lane) - 1ull))] = tid;
       __syncthreads();
-      if (tid < D) {
-        // 8 hit rows' loads in flight before their adds (same order: bit-identical; a row with
-        // hundreds of hits -- a common pitch / energy bucket -- paid one memory latency per hit)
+      if (vec) {
+        // D % 4 == 0: wave wv sums the chunk's hits [wv q, wv q + q) in order, a lane 4 columns
+        // (16-byte loads), 8 hit rows' loads in flight before their adds; the 4 wave sums are
+        // added in wave order at the end (a common pitch / energy bucket has hundreds of hits: one
+        // wave's serial adds were the launch's critical path)
+        const int q = (total + 3) >> 2, j0 = wv * q, j1 = j0 + q < total ? j0 + q : total;
+        if (4 * lane < D) {
+          int j = j0;
+          for (; j + 8 <= j1; j += 8) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4 *>(dy + (base + list[j + u]) * dys + 4 * lane);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc4.x += v[u].x, acc4.y += v[u].y, acc4.z += v[u].z, acc4.w += v[u].w;
+          }
+          for (; j < j1; ++j) {
+            const float4 v = *reinterpret_cast<const float4 *>(dy + (base + list[j]) * dys + 4 * lane);
+            acc4.x += v.x, acc4.y += v.y, acc4.z += v.z, acc4.w += v.w;
+          }
+        }
+      } else if (tid < D) {
+        // 8 hit rows' loads in flight before their adds (in order)
         int j = 0;
         for (; j + 8 <= total; j += 8) {
           float v[8];
@@ -362,6 +383,15 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t *__restric
       }
       __syncthreads();
     }
+  if (vec) {
+    __shared__ float4 red[4][64];
+    red[wv][lane] = acc4;
+    __syncthreads();
+    if (tid < D) {
+      const float *r = reinterpret_cast<const float *>(&red[0][0]);
+      acc = ((r[tid] + r[256 + tid]) + r[512 + tid]) + r[768 + tid];
+    }
+  }
   if (tid < D) {
     float *o = out + (int64_t)v * D + tid;
     *o = accumulate ? *o + acc : acc;
